@@ -1,0 +1,192 @@
+/*
+ * grape.h -- C ABI of the MI355X GRAPE propagator-and-gradient engine.
+ *
+ * Drop-in boundary for RobustGRAPE.jl's hot path.  Every entry point takes
+ * plain pointers and sizes (no torch, no C++ types) so that a Julia `ccall`
+ * shim, Python `ctypes` or C/C++ can bind it.  The reference interfaces each
+ * entry point replaces are cited per function (paths are into the reference
+ * tree, srtweezer/RobustGRAPE).
+ *
+ * Layout conventions (match the reference / Julia):
+ *   - complex numbers are interleaved (re, im) float64 pairs (Julia ComplexF64);
+ *   - matrices are COLUMN-MAJOR d x d (element (i,j) at [i + j*d]);
+ *   - a control vector x has n_x = nparam*ntimes + nadd entries with
+ *     x[p + k*nparam] = control p at time step k (0-based) and x_add in the
+ *     last nadd slots (src/UnitaryCalculations.jl:21-26);
+ *   - batched inputs are n_x-major: eval b's vector starts at x + b*n_x;
+ *   - F_dx has n_x entries per eval (src/FidelityCalculations.jl:116),
+ *     F_d2err_dx is (n_x, nerr) column-major per eval (:117).
+ *
+ * Ownership: all host buffers are caller-owned; the library never keeps a
+ * pointer to them after a call returns.  Calls are synchronous unless their
+ * name ends in _async.  A plan is bound to one device and one HIP stream;
+ * distinct plans may be used from different threads concurrently.
+ *
+ * Errors: every int-returning function returns GRAPE_OK (0) or a negative
+ * grape_status; grape_last_error() returns a thread-local message.
+ */
+#ifndef GRAPE_H
+#define GRAPE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GRAPE_ABI_VERSION 1
+
+typedef enum grape_status {
+    GRAPE_OK = 0,
+    GRAPE_ERR_INVALID = -1,     /* bad descriptor / shape (reference: AssertionError, UnitaryCalculations.jl:22) */
+    GRAPE_ERR_UNSUPPORTED = -2, /* valid but outside this engine (e.g. ndim > GRAPE_MAX_SMALL_DIM) */
+    GRAPE_ERR_ALLOC = -3,       /* device or host allocation failed */
+    GRAPE_ERR_HIP = -4,         /* a HIP runtime call failed */
+    GRAPE_ERR_SINGULAR = -5,    /* singular Pade denominator (Julia: SingularException from gesv!) */
+    GRAPE_ERR_NO_DEVICE = -6    /* no usable GPU */
+} grape_status;
+
+/* Largest Hilbert-space dimension served by the small-d (VALU) engine. */
+#define GRAPE_MAX_SMALL_DIM 16
+
+/*
+ * Operator-basis description of the reference's Hamiltonian closures.
+ *
+ * The reference takes arbitrary Julia closures H0(nt, x, x_add) and
+ * Herror(nt, x, x_add, err) (src/Types.jl:10,25) and target_unitary(x_add)
+ * (src/Types.jl:50).  Closures cannot run on the GPU, so the device path
+ * takes them as a sum of fixed operators with scalar coefficients:
+ *
+ *     H0(nt, x, x_add)        = sum_t  c_t(nt, x, x_add)        * OPS[op_t]
+ *     Herror_e(nt,x,x_add,err) = err * sum_t c_t(nt, x, x_add)  * OPS[op_t]
+ *     U0(x_add)               = sum_t  c_t(x_add)               * OPS[op_t]
+ *
+ * with c_t = scale_t * f_t(a_t * v_t + b_t), f in {one, identity, cos, sin,
+ * cis = exp(i .)} and v the variable named by var/index.  This covers every
+ * Hamiltonian, error source and target in the reference's tests, examples and
+ * RydbergTools.jl (phase control: cos/sin terms; amplitude/detuning errors:
+ * linear in err).
+ */
+typedef enum grape_var {
+    GRAPE_VAR_ONE = 0,   /* v = 1 */
+    GRAPE_VAR_X = 1,     /* v = x_main[index] at the current time step */
+    GRAPE_VAR_XADD = 2,  /* v = x_add[index] */
+    GRAPE_VAR_TSTEP = 3  /* v = nt, the 1-based time step (Types.jl:25) */
+} grape_var;
+
+typedef enum grape_func {
+    GRAPE_FN_ONE = 0,    /* f(t) = 1 */
+    GRAPE_FN_LINEAR = 1, /* f(t) = t */
+    GRAPE_FN_COS = 2,    /* f(t) = cos t */
+    GRAPE_FN_SIN = 3,    /* f(t) = sin t */
+    GRAPE_FN_CIS = 4     /* f(t) = cos t + i sin t  (target terms only) */
+} grape_func;
+
+typedef struct grape_term {
+    int32_t op;        /* index into grape_desc.ops */
+    int32_t var;       /* grape_var */
+    int32_t index;     /* parameter index for GRAPE_VAR_X / GRAPE_VAR_XADD */
+    int32_t func;      /* grape_func */
+    double a, b;       /* argument t = a*v + b */
+    double scale_re;   /* complex scale */
+    double scale_im;
+} grape_term;
+
+typedef struct grape_desc {
+    int32_t ndim;       /* UnitaryRobustGRAPEProblem.ndim   (Types.jl:34) */
+    int32_t ntimes;     /* UnitaryRobustGRAPEProblem.ntimes (Types.jl:33) */
+    int32_t nparam;     /* controls per step: (n_x - nadd)/ntimes (UnitaryCalculations.jl:24) */
+    int32_t nadd;       /* nb_additional_param (Types.jl:36) */
+    int32_t nerr;       /* length(error_sources) (Types.jl:37) */
+    int32_t n_ops;
+    double t0;          /* total time (Types.jl:32) */
+    double eps;         /* first-order FD step, default 1e-8 (Types.jl:38) */
+    double eps2;        /* second-order FD step, default 1e-4 (Types.jl:39) */
+    const double *projector_diag; /* ndim reals: diagonal of FidelityRobustGRAPEProblem.projector (Types.jl:54) */
+    const double *ops;            /* n_ops * ndim * ndim complex, column-major, interleaved */
+    int32_t n_h0_terms;
+    const grape_term *h0_terms;
+    const int32_t *err_term_offsets; /* nerr+1 offsets into err_terms (NULL when nerr == 0) */
+    const grape_term *err_terms;
+    int32_t n_target_terms;
+    const grape_term *target_terms;  /* may only use GRAPE_VAR_ONE / GRAPE_VAR_XADD */
+    int32_t max_batch;  /* largest nbatch a single call will use (workspace sizing); <=0 -> 256 */
+    int32_t reserved[7];
+} grape_desc;
+
+typedef struct grape_plan grape_plan;
+
+/* Library / ABI identification. */
+int grape_abi_version(void);
+const char *grape_last_error(void);
+
+/* Number of visible HIP devices (0 when none); does not create a context. */
+int grape_device_count(void);
+
+/*
+ * Build a plan: validates the descriptor, uploads the operator basis to
+ * `device`, allocates the workspace for desc->max_batch evaluations and
+ * creates the plan's stream.  Replaces the problem structs
+ * UnitaryRobustGRAPEProblem / FidelityRobustGRAPEProblem (src/Types.jl:31-56).
+ */
+int grape_plan_create(const grape_desc *desc, int device, grape_plan **out);
+void grape_plan_destroy(grape_plan *plan);
+
+/* Device stream of the plan (a hipStream_t), for callers that enqueue around it. */
+void *grape_plan_stream(grape_plan *plan);
+
+/*
+ * Fidelity + gradient (+ error sensitivity and its gradient) for a batch of
+ * control vectors.  One evaluation b equals one reference call
+ *   (F, F_dx_tot, F_d2err, F_d2err_dx_tot) =
+ *       calculate_fidelity_and_derivatives(fidelity_problem, x_b)
+ * (src/FidelityCalculations.jl:19-119, which calls
+ *  calculate_unitary_and_derivatives, src/UnitaryCalculations.jl:20-155).
+ *
+ *   x          [nbatch][n_x]             host, read-only
+ *   F          [nbatch]                  host, written
+ *   F_dx       [nbatch][n_x]             host, written
+ *   F_d2err    [nbatch][nerr]            host, written (may be NULL if nerr == 0)
+ *   F_d2err_dx [nbatch][nerr][n_x]       host, written (may be NULL if nerr == 0)
+ *              (per eval: column-major (n_x, nerr) like the reference's matrix)
+ */
+int grape_fidelity_grad(grape_plan *plan, int nbatch, const double *x,
+                        double *F, double *F_dx, double *F_d2err, double *F_d2err_dx);
+
+/*
+ * Same as grape_fidelity_grad with DEVICE pointers, enqueued on the plan's
+ * stream without synchronising (inputs resident in HBM; used by the
+ * throughput benchmark and by callers that keep x on the GPU).
+ */
+int grape_fidelity_grad_device_async(grape_plan *plan, int nbatch, const double *d_x,
+                                     double *d_F, double *d_F_dx,
+                                     double *d_F_d2err, double *d_F_d2err_dx);
+
+/* Block until all work enqueued on the plan's stream finished; reports device-side errors. */
+int grape_plan_synchronize(grape_plan *plan);
+
+/*
+ * Materialised unitary derivatives for ONE control vector, replacing
+ * calculate_unitary_and_derivatives (src/UnitaryCalculations.jl:20-155).
+ * Output shapes are the reference's (complex, column-major):
+ *   U (d,d); U_dx (d,d,nparam,ntimes); U_dx_add (d,d,nadd); U_derr (d,d,nerr);
+ *   U_derr_dx (d,d,nparam,ntimes,nerr); U_derr_dx_add (d,d,nadd,nerr).
+ * Any output pointer may be NULL to skip it.
+ */
+int grape_unitary_derivs(grape_plan *plan, const double *x,
+                         double *U, double *U_dx, double *U_dx_add,
+                         double *U_derr, double *U_derr_dx, double *U_derr_dx_add);
+
+/*
+ * Batched matrix exponential exp(A) of n column-major ndim x ndim complex
+ * matrices on `device`, with the reference's algorithm (Julia
+ * LinearAlgebra.exp!: Pade degree by 1-norm, gesv, squaring).  Host buffers.
+ * stats (optional, 5 ints) receives how many matrices used Pade m=3,5,7,9,13.
+ */
+int grape_expm_batch(int device, int ndim, int n, const double *A, double *E, int *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRAPE_H */

@@ -1,0 +1,206 @@
+"""Operator-basis descriptors: the device-side stand-in for the reference's closures.
+
+The reference passes Julia closures ``H0(nt, x, x_add)``,
+``Herror(nt, x, x_add, err)`` and ``target_unitary(x_add)`` (src/Types.jl:10,25,50).
+A closure cannot run on the GPU, so the device path takes each of them as a
+sum of fixed operators times scalar coefficients (see ``include/grape.h``):
+
+    H(nt, x, x_add) = sum_t scale_t * f_t(a_t * v_t + b_t) * OP_t
+
+Each descriptor is ALSO a callable with the reference signature, so it can be
+handed to anything that expects the closure (including the CPU oracle).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+# grape_var / grape_func (include/grape.h)
+VAR_ONE, VAR_X, VAR_XADD, VAR_TSTEP = 0, 1, 2, 3
+FN_ONE, FN_LINEAR, FN_COS, FN_SIN, FN_CIS = 0, 1, 2, 3, 4
+
+
+@dataclass(frozen=True)
+class Term:
+    """One coefficient * operator term (grape_term)."""
+    op: np.ndarray          # (d, d) complex
+    var: int = VAR_ONE
+    index: int = 0
+    func: int = FN_ONE
+    a: float = 1.0
+    b: float = 0.0
+    scale: complex = 1.0
+
+    def coefficient(self, nt, x, x_add):
+        if self.var == VAR_ONE:
+            v = 1.0
+        elif self.var == VAR_X:
+            v = float(x[self.index])
+        elif self.var == VAR_XADD:
+            v = float(x_add[self.index])
+        elif self.var == VAR_TSTEP:
+            v = float(nt)
+        else:
+            raise ValueError(f"bad var {self.var}")
+        t = self.a * v + self.b
+        if self.func == FN_ONE:
+            f = 1.0
+        elif self.func == FN_LINEAR:
+            f = t
+        elif self.func == FN_COS:
+            f = np.cos(t)
+        elif self.func == FN_SIN:
+            f = np.sin(t)
+        elif self.func == FN_CIS:
+            f = complex(np.cos(t), np.sin(t))
+        else:
+            raise ValueError(f"bad func {self.func}")
+        s = complex(self.scale)
+        if isinstance(f, complex) or s.imag != 0.0:
+            return s * f
+        return s.real * f  # real coefficient times complex operator, like the closures
+
+
+def _accumulate(terms: Sequence[Term], nt, x, x_add, ndim):
+    H = np.zeros((ndim, ndim), np.complex128)
+    for t in terms:
+        H = H + t.coefficient(nt, x, x_add) * t.op
+    return H
+
+
+class OperatorBasisHamiltonian:
+    """H0(nt, x, x_add) = sum_t c_t * OP_t  (a device-buildable H0 closure)."""
+
+    def __init__(self, terms: Sequence[Term]):
+        self.terms: Tuple[Term, ...] = tuple(terms)
+        if not self.terms:
+            raise ValueError("need at least one term")
+        self.ndim = self.terms[0].op.shape[0]
+        for t in self.terms:
+            if t.op.shape != (self.ndim, self.ndim):
+                raise ValueError("all operators must share one shape")
+            if t.func == FN_CIS:
+                raise ValueError("cis coefficients are only allowed in target terms")
+
+    def __call__(self, nt, x, x_add):
+        return _accumulate(self.terms, nt, x, x_add, self.ndim)
+
+    def depends_on_xadd(self) -> bool:
+        return any(t.var == VAR_XADD for t in self.terms)
+
+
+class OperatorBasisError:
+    """Herror(nt, x, x_add, err) = err * sum_t c_t * OP_t (linear in err)."""
+
+    def __init__(self, terms: Sequence[Term]):
+        self.terms: Tuple[Term, ...] = tuple(terms)
+        if not self.terms:
+            raise ValueError("need at least one term")
+        self.ndim = self.terms[0].op.shape[0]
+        for t in self.terms:
+            if t.func == FN_CIS:
+                raise ValueError("cis coefficients are only allowed in target terms")
+
+    def __call__(self, nt, x, x_add, err):
+        return err * _accumulate(self.terms, nt, x, x_add, self.ndim)
+
+
+class OperatorBasisTarget:
+    """target_unitary(x_add) = sum_t c_t(x_add) * OP_t."""
+
+    def __init__(self, terms: Sequence[Term]):
+        self.terms: Tuple[Term, ...] = tuple(terms)
+        self.ndim = self.terms[0].op.shape[0]
+        for t in self.terms:
+            if t.var in (VAR_X, VAR_TSTEP):
+                raise ValueError("target terms may only depend on x_add")
+
+    def __call__(self, x_add):
+        return _accumulate(self.terms, 1, (), x_add, self.ndim)
+
+
+# ---------------------------------------------------------------------------
+# ctypes mirror of grape_term / grape_desc (include/grape.h)
+# ---------------------------------------------------------------------------
+class CTerm(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("var", ctypes.c_int32), ("index", ctypes.c_int32),
+                ("func", ctypes.c_int32), ("a", ctypes.c_double), ("b", ctypes.c_double),
+                ("scale_re", ctypes.c_double), ("scale_im", ctypes.c_double)]
+
+
+class CDesc(ctypes.Structure):
+    _fields_ = [("ndim", ctypes.c_int32), ("ntimes", ctypes.c_int32), ("nparam", ctypes.c_int32),
+                ("nadd", ctypes.c_int32), ("nerr", ctypes.c_int32), ("n_ops", ctypes.c_int32),
+                ("t0", ctypes.c_double), ("eps", ctypes.c_double), ("eps2", ctypes.c_double),
+                ("projector_diag", ctypes.POINTER(ctypes.c_double)),
+                ("ops", ctypes.POINTER(ctypes.c_double)),
+                ("n_h0_terms", ctypes.c_int32), ("h0_terms", ctypes.POINTER(CTerm)),
+                ("err_term_offsets", ctypes.POINTER(ctypes.c_int32)),
+                ("err_terms", ctypes.POINTER(CTerm)),
+                ("n_target_terms", ctypes.c_int32), ("target_terms", ctypes.POINTER(CTerm)),
+                ("max_batch", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+
+
+class DescriptorBuffers:
+    """Owns the host arrays a CDesc points into (keep alive while the C call runs)."""
+
+    def __init__(self, fp, nparam: int, max_batch: int = 256):
+        up = fp.unitary_problem
+        if not isinstance(up.H0, OperatorBasisHamiltonian):
+            raise TypeError("device path needs an OperatorBasisHamiltonian H0")
+        if not isinstance(fp.target_unitary, OperatorBasisTarget):
+            raise TypeError("device path needs an OperatorBasisTarget target_unitary")
+        for es in up.error_sources:
+            if not isinstance(es.Herror, OperatorBasisError):
+                raise TypeError("device path needs OperatorBasisError error sources")
+        P = np.asarray(fp.projector, np.float64)
+        if np.count_nonzero(P - np.diag(np.diag(P))):
+            raise ValueError("device path supports diagonal projectors only")
+        ops: List[np.ndarray] = []
+        index = {}
+
+        def op_id(m):
+            key = id(m)
+            if key not in index:
+                index[key] = len(ops)
+                ops.append(np.asarray(m, np.complex128))
+            return index[key]
+
+        def cterms(terms):
+            arr = (CTerm * max(1, len(terms)))()
+            for i, t in enumerate(terms):
+                s = complex(t.scale)
+                arr[i] = CTerm(op_id(t.op), t.var, t.index, t.func, t.a, t.b, s.real, s.imag)
+            return arr
+
+        self.h0 = cterms(up.H0.terms)
+        err_terms: List[Term] = []
+        offs = [0]
+        for es in up.error_sources:
+            err_terms.extend(es.Herror.terms)
+            offs.append(len(err_terms))
+        self.err = cterms(err_terms)
+        self.offs = (ctypes.c_int32 * len(offs))(*offs)
+        self.target = cterms(fp.target_unitary.terms)
+        d = up.ndim
+        stack = np.stack([np.asfortranarray(o) for o in ops])  # (n_ops, d, d)
+        inter = np.empty((len(ops), d * d * 2), np.float64)
+        for k, o in enumerate(ops):
+            flat = o.reshape(-1, order="F")
+            inter[k, 0::2] = flat.real
+            inter[k, 1::2] = flat.imag
+        self.ops = np.ascontiguousarray(inter.reshape(-1))
+        self.pdiag = np.ascontiguousarray(np.diag(P).astype(np.float64))
+        dp = ctypes.POINTER(ctypes.c_double)
+        self.desc = CDesc(
+            ndim=d, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param,
+            nerr=len(up.error_sources), n_ops=len(ops), t0=float(up.t0), eps=float(up.eps),
+            eps2=float(up.eps2), projector_diag=self.pdiag.ctypes.data_as(dp),
+            ops=self.ops.ctypes.data_as(dp), n_h0_terms=len(up.H0.terms), h0_terms=self.h0,
+            err_term_offsets=self.offs, err_terms=self.err,
+            n_target_terms=len(fp.target_unitary.terms), target_terms=self.target,
+            max_batch=int(max_batch))
+        del stack

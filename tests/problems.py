@@ -1,0 +1,101 @@
+"""Problem builders shared by the tests: the reference's test/example problems
+(test/runtests.jl, examples/*.jl) and the SURVEY.md section 8d configs, each in
+closure form (reference idiom, host-evaluated) and operator-basis form (device)."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from robustgrape_amd import rydberg as R
+from robustgrape_amd.types import ErrorSource, FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+
+T0_TEST = 2 * math.pi * 1.22     # runtests.jl:53
+T0_TO = 7.613                    # examples/time_optimal_cz.jl:14
+W_SYM = np.diag([1.0, 2.0, 1.0, 0.0, 0.0])   # runtests.jl:73
+W_FULLBLK = np.diag([1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0])  # runtests.jl:492
+W_FULL9 = np.diag([1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0])
+
+
+def sym_problem(ntimes, t0=T0_TEST, errors=(), device=True):
+    """d=5 symmetric blockaded CZ (runtests.jl:57-75); errors subset of {'amp','freq'}."""
+    if device:
+        H0 = R.rydberg_symmetric_blockaded_operator_basis()
+        errs = [ErrorSource(R.symmetric_amplitude_error() if e == "amp" else R.symmetric_frequency_error())
+                for e in errors]
+        target = R.cz_symmetric_target()
+    else:
+        H0 = lambda t, p, xa: R.rydberg_hamiltonian_symmetric_blockaded(p[0], 0, 0)
+        amp = lambda t, p, xa, e: (R.rydberg_hamiltonian_symmetric_blockaded(p[0], e, 0)
+                                   - R.rydberg_hamiltonian_symmetric_blockaded(p[0], 0, 0))
+        frq = lambda t, p, xa, e: (R.rydberg_hamiltonian_symmetric_blockaded(p[0], 0, e)
+                                   - R.rydberg_hamiltonian_symmetric_blockaded(p[0], 0, 0))
+        errs = [ErrorSource(amp if e == "amp" else frq) for e in errors]
+        target = lambda xa: R.cz_with_1q_phase_symmetric(xa[0])
+    up = UnitaryRobustGRAPEProblem(t0=t0, ntimes=ntimes, ndim=5, H0=H0, nb_additional_param=1,
+                                   error_sources=errs)
+    return FidelityRobustGRAPEProblem(up, W_SYM, target)
+
+
+def fullblk_problem(ntimes, t0=T0_TO, errors=(), device=True):
+    """d=7 full blockaded CZ (runtests.jl:474-494)."""
+    if device:
+        H0 = R.rydberg_full_blockaded_operator_basis()
+        errs = [ErrorSource(R.full_blockaded_amplitude_error() if e == "amp"
+                            else R.full_blockaded_frequency_error()) for e in errors]
+        target = R.cz_full_target(rydberg_dimension=3)
+    else:
+        H0 = lambda t, p, xa: R.rydberg_hamiltonian_full_blockaded(p[0], 0, 0)
+        amp = lambda t, p, xa, e: (R.rydberg_hamiltonian_full_blockaded(p[0], e, 0)
+                                   - R.rydberg_hamiltonian_full_blockaded(p[0], 0, 0))
+        frq = lambda t, p, xa, e: (R.rydberg_hamiltonian_full_blockaded(p[0], 0, e)
+                                   - R.rydberg_hamiltonian_full_blockaded(p[0], 0, 0))
+        errs = [ErrorSource(amp if e == "amp" else frq) for e in errors]
+        target = lambda xa: R.cz_with_1q_phase_full(xa[0], rydberg_dimension=3)
+    up = UnitaryRobustGRAPEProblem(t0=t0, ntimes=ntimes, ndim=7, H0=H0, nb_additional_param=1,
+                                   error_sources=errs)
+    return FidelityRobustGRAPEProblem(up, W_FULLBLK, target)
+
+
+def full9_problem(ntimes=512, t0=T0_TO, nerr=0, device=True, B=10.0):
+    """SURVEY.md 8d C2 (nerr=0) / C3 (nerr=4): d=9 rydberg_hamiltonian_full, Omega=1, B=10."""
+    kinds = [("rabi", 1), ("rabi", 2), ("det", 1), ("det", 2)][:nerr]
+    if device:
+        H0 = R.rydberg_full_operator_basis(1.0, 1.0, 0.0, 0.0, B)
+        errs = [ErrorSource(R.full_rabi_error(w) if k == "rabi" else R.full_detuning_error(w))
+                for k, w in kinds]
+        target = R.cz_full_target()
+    else:
+        H0 = lambda t, p, xa: R.rydberg_hamiltonian_full(p[0], 1, 1, 0, 0, B)
+
+        def mk(k, w):
+            def herr(t, p, xa, e):
+                args = [1.0, 1.0, 0.0, 0.0]
+                if k == "rabi":
+                    args[w - 1] = 1.0 + e
+                else:
+                    args[1 + w] = e
+                return R.rydberg_hamiltonian_full(p[0], *args, B) - R.rydberg_hamiltonian_full(p[0], 1, 1, 0, 0, B)
+            return herr
+        errs = [ErrorSource(mk(k, w)) for k, w in kinds]
+        target = lambda xa: R.cz_with_1q_phase_full(xa[0])
+    up = UnitaryRobustGRAPEProblem(t0=t0, ntimes=ntimes, ndim=9, H0=H0, nb_additional_param=1,
+                                   error_sources=errs)
+    return FidelityRobustGRAPEProblem(up, W_FULL9, target)
+
+
+def evered_pulse(ntimes=1000):
+    """runtests.jl:127-138: the Evered et al. time-optimal CZ pulse."""
+    t0 = 2 * math.pi * 1.22
+    A, w0, p0, d0 = 0.7701624, 0.97525275, -0.97449603, -0.04319765
+    theta = 2.0802725844516097
+    ts = np.linspace(0, t0, ntimes)
+    phis = A * np.cos(w0 * ts - p0) + d0 * ts
+    return np.concatenate([phis, [theta]])
+
+
+def random_x(ntimes, seed, nparam=1, small=False):
+    """x_main = 2pi*U (runtests.jl:335) or 2pi*0.001*U (examples/time_optimal_cz.jl:32); theta = 2pi*U."""
+    rng = np.random.default_rng(seed)
+    scale = 2 * math.pi * (0.001 if small else 1.0)
+    return np.concatenate([scale * rng.uniform(size=ntimes * nparam), [2 * math.pi * rng.uniform()]])
