@@ -1,0 +1,185 @@
+"""Throughput benchmark: GRAPE gradient-evals/sec, Rydberg CZ d=9, N_t=512 (BASELINE.json).
+
+One step = one fidelity+gradient evaluation of every restart this rank owns
+(SURVEY.md 8d C2 problem; restarts r with x_main = 2pi*0.001*U, theta = 2pi*U,
+seed 1000+r as config C4), inputs resident in HBM, followed by the restart
+sweep's exchange: one all_gather of (best F, restart id) over RCCL when N > 1.
+Weak scaling: every rank owns --batch restarts.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+``roofline`` for the dominant kernel (k_expm, per-launch HIP-event time on the
+plan's stream) and ``cpu_baseline`` (the oracle's CPU restatement timed on a
+bounded sample on this host, rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == matrix rate on gfx950)
+D, NT, T0 = 9, 512, 7.613
+
+
+def problem():
+    from robustgrape_amd import rydberg as R
+    from robustgrape_amd.types import FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    up = UnitaryRobustGRAPEProblem(t0=T0, ntimes=NT, ndim=D, H0=R.rydberg_full_operator_basis(1.0, 1.0, 0.0, 0.0, 10.0),
+                                   nb_additional_param=1)
+    return FidelityRobustGRAPEProblem(up, np.diag([1.0] * 4 + [0.0] * 5), R.cz_full_target())
+
+
+def restart_inputs(first, count):
+    xs = []
+    for r in range(first, first + count):
+        rng = np.random.default_rng(1000 + r)
+        xs.append(np.concatenate([2 * math.pi * 0.001 * rng.uniform(size=NT), [2 * math.pi * rng.uniform()]]))
+    return np.stack(xs)
+
+
+def flops_expm(d, m=5, s=0):
+    """Algorithmic FP64 flops of one d x d complex Pade-m exp ((pi_m + s + 5/3) * 8 d^3)."""
+    pi = {3: 2, 5: 3, 7: 4, 9: 5, 13: 6}[m]
+    return (pi + s + 5.0 / 3.0) * 8 * d ** 3
+
+
+def cpu_baseline(seconds=15.0):
+    """Time the CPU restatement on a bounded sample of the same workload (rank 0, N = 1)."""
+    try:
+        from oracle.cref import cref
+        have_c = cref.available()
+    except Exception:
+        have_c = False
+    x = restart_inputs(0, 1)[0]
+    if have_c:
+        fp = problem()
+        t = time.perf_counter()
+        n = 0
+        while True:
+            cref.fidelity_grad(fp, x)
+            n += 1
+            if time.perf_counter() - t > seconds:
+                break
+        dt = time.perf_counter() - t
+        return {"value": n / dt, "unit": "gradient-evals/s", "cores": 1, "kind": "port",
+                "sample": f"{n} sequential C2 evaluations (d=9, N_t=512) by the reference-faithful C++ "
+                          f"restatement oracle/cref (same exp/inv/product counts as the Julia code), 1 thread"}
+    from oracle import grape_oracle as O
+    from tests import problems as P
+    fp = P.full9_problem(NT, device=False)
+    t = time.perf_counter()
+    n = 0
+    while True:
+        O.calculate_fidelity_and_derivatives(fp, x)
+        n += 1
+        if time.perf_counter() - t > seconds:
+            break
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "gradient-evals/s", "cores": 1, "kind": "port",
+            "sample": f"{n} sequential C2 evaluations by the numpy restatement oracle/grape_oracle.py, 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="restarts per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from robustgrape_amd.engine import GrapePlan
+    fp = problem()
+    B = args.batch
+    plan = GrapePlan(fp, nparam=1, device=local, max_batch=B)
+    X = torch.from_numpy(restart_inputs(rank * B, B)).to(dev)
+    F = torch.empty(B, dtype=torch.float64, device=dev)
+    Fdx = torch.empty(B, X.shape[1], dtype=torch.float64, device=dev)
+    ids = torch.arange(rank * B, rank * B + B, device=dev, dtype=torch.float64)
+    gathered = torch.empty(world * 2, dtype=torch.float64, device=dev)
+
+    def step():
+        plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), B)
+        plan.synchronize()
+        if world > 1:  # restart sweep exchange: best (F, id) of every rank
+            best = torch.argmax(F)
+            mine = torch.stack([F[best], ids[best]])
+            dist.all_gather_into_tensor(gathered, mine)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    plan.kernel_times(reset=True)
+    plan.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    plan.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    evals = args.steps * B * world
+    value = evals / elapsed
+    ktimes = plan.kernel_times()
+    if rank == 0:
+        ms_expm, n_expm = ktimes["k_expm"]
+        per_launch_ms = ms_expm / max(1, n_expm)
+        nv = 2  # nominal + the control's eps variant (H0 does not read x_add)
+        flop_launch = B * NT * nv * flops_expm(D)
+        achieved = flop_launch / (per_launch_ms * 1e-3) / 1e12
+        out = {
+            "metric": "GRAPE gradient-evals/sec (fidelity+∇), Rydberg CZ d=9 N_t=512, 1→8 GPU",
+            "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
+                                   "np=1, na=1, ne=0; restart sweep",
+                       "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
+            "roofline": {"bound": "mfma", "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)",
+                         "kernel": "k_expm", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch},
+            "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

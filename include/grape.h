@@ -48,7 +48,7 @@ typedef enum grape_status {
 } grape_status;
 
 /* Largest Hilbert-space dimension served by the small-d (VALU) engine. */
-#define GRAPE_MAX_SMALL_DIM 16
+#define GRAPE_MAX_SMALL_DIM 12
 
 /*
  * Operator-basis description of the reference's Hamiltonian closures.
@@ -177,6 +177,25 @@ int grape_plan_synchronize(grape_plan *plan);
 int grape_unitary_derivs(grape_plan *plan, const double *x,
                          double *U, double *U_dx, double *U_dx_add,
                          double *U_derr, double *U_derr_dx, double *U_derr_dx_add);
+
+/*
+ * Per-kernel timing for measurement (bench.py's roofline): when enabled, every
+ * launch of the plan's pipeline is bracketed by HIP events recorded ON THE
+ * PLAN'S STREAM; grape_plan_synchronize accumulates the elapsed times.
+ * grape_plan_kernel_times copies GRAPE_NUM_KERNELS totals (ms) and launch
+ * counts, indexed by grape_kernel, and optionally resets them.
+ */
+typedef enum grape_kernel {
+    GRAPE_KERNEL_EXPM = 0,      /* propagators of every FD variant (Pade m <= 5) */
+    GRAPE_KERNEL_EXPM_HIGH = 1, /* Pade m = 7/9/13 items parked by the above */
+    GRAPE_KERNEL_SCAN = 2,      /* chunked prefix products, fidelity, gradient kernels */
+    GRAPE_KERNEL_GRAD = 3,      /* per-step gradient contractions */
+    GRAPE_KERNEL_REDUCE = 4,    /* x_add reductions */
+    GRAPE_NUM_KERNELS = 5
+} grape_kernel;
+
+int grape_plan_set_profiling(grape_plan *plan, int enable);
+int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launches, int reset);
 
 /*
  * Batched matrix exponential exp(A) of n column-major ndim x ndim complex

@@ -1,0 +1,84 @@
+"""ctypes binding of libgrape.so (include/grape.h).
+
+Loading fails loudly: there is no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from .operators import CDesc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgrape.so")
+
+GRAPE_OK = 0
+STATUS_NAMES = {-1: "GRAPE_ERR_INVALID", -2: "GRAPE_ERR_UNSUPPORTED", -3: "GRAPE_ERR_ALLOC",
+                -4: "GRAPE_ERR_HIP", -5: "GRAPE_ERR_SINGULAR", -6: "GRAPE_ERR_NO_DEVICE"}
+
+# every symbol include/grape.h declares
+EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grape_plan_create",
+            "grape_plan_destroy", "grape_plan_stream", "grape_fidelity_grad",
+            "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
+            "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times"]
+KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add"]
+
+
+class GrapeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run `python -m robustgrape_amd.build` "
+                              "(the GPU path has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        dp = ctypes.POINTER(ctypes.c_double)
+        vp = ctypes.c_void_p
+        L.grape_abi_version.restype = ctypes.c_int
+        L.grape_last_error.restype = ctypes.c_char_p
+        L.grape_device_count.restype = ctypes.c_int
+        L.grape_plan_create.argtypes = [ctypes.POINTER(CDesc), ctypes.c_int, ctypes.POINTER(vp)]
+        L.grape_plan_create.restype = ctypes.c_int
+        L.grape_plan_destroy.argtypes = [vp]
+        L.grape_plan_destroy.restype = None
+        L.grape_plan_stream.argtypes = [vp]
+        L.grape_plan_stream.restype = vp
+        L.grape_fidelity_grad.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp]
+        L.grape_fidelity_grad.restype = ctypes.c_int
+        L.grape_fidelity_grad_device_async.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]
+        L.grape_fidelity_grad_device_async.restype = ctypes.c_int
+        L.grape_plan_synchronize.argtypes = [vp]
+        L.grape_plan_synchronize.restype = ctypes.c_int
+        L.grape_unitary_derivs.argtypes = [vp, dp, dp, dp, dp, dp, dp, dp]
+        L.grape_unitary_derivs.restype = ctypes.c_int
+        L.grape_expm_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp,
+                                       ctypes.POINTER(ctypes.c_int)]
+        L.grape_expm_batch.restype = ctypes.c_int
+        L.grape_plan_set_profiling.argtypes = [vp, ctypes.c_int]
+        L.grape_plan_set_profiling.restype = ctypes.c_int
+        L.grape_plan_kernel_times.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+        L.grape_plan_kernel_times.restype = ctypes.c_int
+        if L.grape_abi_version() != 1:
+            raise ImportError("libgrape.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(code):
+    if code != GRAPE_OK:
+        raise GrapeError(code, lib().grape_last_error().decode())
+
+
+def dptr(a):
+    """double* of a C-contiguous float64 (or complex128) numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))

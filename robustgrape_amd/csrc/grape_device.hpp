@@ -1,0 +1,448 @@
+// grape_device.hpp -- CDNA4 (gfx950) device building blocks of the GRAPE engine.
+//
+// Execution model ("row groups"): a 64-lane wave is split into GPW = 64/D
+// groups of D lanes; each group owns ONE d x d complex FP64 matrix at a time,
+// lane i of the group holding row i in VGPRs (D complex = 4*D VGPRs per
+// matrix).  A product C = A.B keeps the left operand's row in registers and
+// broadcasts the right operand from the group's LDS tile (all D lanes of a
+// group read the same 16-B element -> one ds_read_b128 per complex MAC, groups
+// land on disjoint banks because a tile is D*D*16 B = 4 (mod 64) dwords apart).
+// FP64 throughout: eps = 1e-8 finite differences forbid lower precision.
+//
+// Numerics follow the reference's third-party kernels (Julia LinearAlgebra
+// exp!, LAPACK zgetrf/zgetrs as called by gesv!):
+//   * Pade degree by 1-norm thresholds 0.015/0.25/0.95/2.1 (m = 3/5/7/9),
+//     else m = 13 with s = ceil(log2(|A|_1/5.4)) squarings;
+//   * Julia's accumulation order for U and V;
+//   * gesv: partial pivoting with izamax's |re|+|im| (first max wins), the
+//     multiplier formed as a_ij * (1/pivot) (zgetf2's zscal by the reciprocal),
+//     forward substitution in pivot order, back substitution dividing by the
+//     diagonal (ztrsm), complex division by Smith's method (gfortran).
+// Balancing (zgebal 'B') is not applied on the device: for the skew-Hermitian
+// generators A = -i dt H of a Hermitian H it is a permutation only (scaling is
+// the identity because row and column norms coincide), which changes nothing
+// but the summation order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace grape {
+
+struct cd {
+    double re, im;
+};
+
+__device__ __forceinline__ cd cmake(double r, double i) { cd z; z.re = r; z.im = i; return z; }
+__device__ __forceinline__ cd czero() { return cmake(0.0, 0.0); }
+__device__ __forceinline__ cd cadd(cd a, cd b) { return cmake(a.re + b.re, a.im + b.im); }
+__device__ __forceinline__ cd csub(cd a, cd b) { return cmake(a.re - b.re, a.im - b.im); }
+__device__ __forceinline__ cd cconj(cd a) { return cmake(a.re, -a.im); }
+__device__ __forceinline__ cd cscale(double s, cd a) { return cmake(s * a.re, s * a.im); }
+// plain (unfused) complex product, as Julia's *(::Complex, ::Complex)
+__device__ __forceinline__ cd cmul(cd a, cd b) {
+    return cmake(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re);
+}
+// c += a*b with four FMAs (the BLAS-kernel form)
+__device__ __forceinline__ void cmac(cd &c, cd a, cd b) {
+    c.re = fma(a.re, b.re, c.re);
+    c.re = fma(-a.im, b.im, c.re);
+    c.im = fma(a.re, b.im, c.im);
+    c.im = fma(a.im, b.re, c.im);
+}
+// Smith's complex division a/b (gfortran's complex division, used by LAPACK)
+__device__ __forceinline__ cd cdiv(cd a, cd b) {
+    if (fabs(b.re) >= fabs(b.im)) {
+        const double r = b.im / b.re, den = b.re + b.im * r;
+        return cmake((a.re + a.im * r) / den, (a.im - a.re * r) / den);
+    }
+    const double r = b.re / b.im, den = b.im + b.re * r;
+    return cmake((a.re * r + a.im) / den, (a.im * r - a.re) / den);
+}
+
+// ---------------------------------------------------------------------------
+// Group geometry
+// ---------------------------------------------------------------------------
+template <int D>
+struct Geo {
+    static constexpr int GPW = 64 / D;          // groups per wave
+    static constexpr int TILE = D * D;          // complex elements per matrix tile
+    static constexpr int AUX = 2 * D;           // complex scratch per group (pivot row / reductions)
+    static constexpr int GROUP_CD = TILE + AUX; // LDS complex elements per group
+};
+
+// Per-lane view of its group.
+template <int D>
+struct Group {
+    int i;          // row owned by this lane (0..D-1)
+    int g;          // group index within the wave
+    bool lane_ok;   // lane belongs to a group (lane < GPW*D)
+    cd *tile;       // LDS D*D tile (row-major)
+    cd *aux;        // LDS 2*D scratch
+    __device__ __forceinline__ double *auxd() { return reinterpret_cast<double *>(aux); }
+};
+
+template <int D>
+__device__ __forceinline__ Group<D> make_group(cd *wave_lds, int lane) {
+    Group<D> G;
+    G.lane_ok = lane < Geo<D>::GPW * D;
+    G.g = G.lane_ok ? lane / D : Geo<D>::GPW - 1;
+    G.i = G.lane_ok ? lane % D : 0;
+    G.tile = wave_lds + G.g * Geo<D>::GROUP_CD;
+    G.aux = G.tile + Geo<D>::TILE;
+    return G;
+}
+
+// All group synchronisation goes through the workgroup barrier; kernels that
+// use row groups launch 64-thread (one-wave) workgroups or keep every wave on
+// the same barrier sequence.
+__device__ __forceinline__ void gsync() { __syncthreads(); }
+
+template <int D>
+__device__ __forceinline__ void tile_store_row(Group<D> &G, const cd (&r)[D], bool wr) {
+    if (wr) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) G.tile[G.i * D + j] = r[j];
+    }
+}
+
+// Materialise a register row here: the empty asm "redefines" every element,
+// so the compiler can neither sink the producing FMAs past this point nor keep
+// the operands they consumed alive.  Without it, fully unrolled straight-line
+// code gets its product chains interleaved with later stages (the LU solve)
+// and register use quadruples (measured 412 -> 146 VGPRs at d = 9).
+template <int D>
+__device__ __forceinline__ void pin(cd (&r)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) asm volatile("" : "+v"(r[j].re), "+v"(r[j].im));
+}
+
+// c = a . B  (a: this lane's row, B: tile in LDS, row-major)
+template <int D, bool TRANS = false, bool CONJ = false>
+__device__ __forceinline__ void mm_tile(const cd (&a)[D], const cd *B, cd (&c)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) c[j] = czero();
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const cd ak = a[k];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            cd b = TRANS ? B[j * D + k] : B[k * D + j];
+            if (CONJ) b.im = -b.im;
+            cmac(c[j], ak, b);
+        }
+    }
+    pin<D>(c);
+}
+
+// Group-wide sum / max of one double per lane (all lanes receive the result).
+template <int D>
+__device__ __forceinline__ double group_sum(Group<D> &G, double v, bool wr) {
+    double *s = G.auxd();
+    if (wr) s[G.i] = v;
+    gsync();
+    double t = 0.0;
+#pragma unroll
+    for (int r = 0; r < D; ++r) t += s[r];
+    gsync();
+    return t;
+}
+template <int D>
+__device__ __forceinline__ double group_max(Group<D> &G, double v, bool wr) {
+    double *s = G.auxd();
+    if (wr) s[G.i] = v;
+    gsync();
+    double t = s[0];
+#pragma unroll
+    for (int r = 1; r < D; ++r) t = fmax(t, s[r]);
+    gsync();
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// Pade tables (Julia LinearAlgebra.exp!)
+// ---------------------------------------------------------------------------
+__constant__ const double kPade3[4] = {120.0, 60.0, 12.0, 1.0};
+__constant__ const double kPade5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
+__constant__ const double kPade7[8] = {17297280.0, 8648640.0, 1995840.0, 277200.0,
+                                       25200.0, 1512.0, 56.0, 1.0};
+__constant__ const double kPade9[10] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0,
+                                        30270240.0, 2162160.0, 110880.0, 3960.0, 90.0, 1.0};
+__constant__ const double kPade13[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+                                         1187353796428800.0, 129060195264000.0, 10559470521600.0,
+                                         670442572800.0, 33522128640.0, 1323241920.0,
+                                         40840800.0, 960960.0, 16380.0, 182.0, 1.0};
+
+// Degree choice of exp! for a 1-norm: returns m, writes s (squarings).
+__device__ __forceinline__ int pade_degree(double nA, int &s) {
+    s = 0;
+    if (nA <= 2.1) {
+        if (nA > 0.95) return 9;
+        if (nA > 0.25) return 7;
+        if (nA > 0.015) return 5;
+        return 3;
+    }
+    const double l = log2(nA / 5.4);
+    if (l > 0.0) s = (int)ceil(l);
+    return 13;
+}
+
+// ---------------------------------------------------------------------------
+// gesv(Y, X): solve Y Z = X in place (Z returned in x), LAPACK semantics.
+// On return lane i holds row `pos` of the solution (pos returned).
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ int gesv_rows(Group<D> &G, cd (&y)[D], cd (&x)[D], bool wr, int &singular) {
+    int pos = G.i;  // physical row position of the row this lane holds
+    double *red = G.auxd();
+    cd *prow = G.tile;  // pivot row broadcast: y part [0,D), x part [D,2D)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        __builtin_amdgcn_sched_barrier(0);
+        // izamax over positions j..D-1 with |re|+|im|; first (smallest position) max wins
+        const double v = (pos >= j) ? (fabs(y[j].re) + fabs(y[j].im)) : -1.0;
+        if (wr) {
+            red[2 * G.i] = v;
+            red[2 * G.i + 1] = (double)pos;
+        }
+        gsync();
+        double best = -1.0;
+        int bpos = D;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const double vr = red[2 * r];
+            const int pr = (int)red[2 * r + 1];
+            if (vr > best || (vr == best && pr < bpos)) {
+                best = vr;
+                bpos = pr;
+            }
+        }
+        gsync();
+        if (pos == bpos) pos = j;
+        else if (pos == j) pos = bpos;
+        if (best == 0.0) singular = 1;
+        if (pos == j && wr) {
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) {
+                prow[jj] = y[jj];
+                prow[D + jj] = x[jj];
+            }
+        }
+        gsync();
+        if (pos > j && best != 0.0) {
+            const cd piv = prow[j];
+            const cd rp = cdiv(cmake(1.0, 0.0), piv);
+            const cd l = cmul(y[j], rp);
+            y[j] = l;
+#pragma unroll
+            for (int jj = j + 1; jj < D; ++jj) {
+                const cd u = prow[jj];
+                y[jj] = cadd(y[jj], cmul(l, cmake(-u.re, -u.im)));
+            }
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) x[jj] = csub(x[jj], cmul(prow[D + jj], l));
+        }
+        gsync();
+    }
+    // back substitution (ztrsm, upper, non-unit)
+#pragma unroll
+    for (int k = D - 1; k >= 0; --k) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (pos == k) {
+            const cd piv = y[k];
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) x[jj] = cdiv(x[jj], piv);
+            if (wr) {
+#pragma unroll
+                for (int jj = 0; jj < D; ++jj) prow[jj] = x[jj];
+            }
+        }
+        gsync();
+        if (pos < k) {
+            const cd u = y[k];
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) x[jj] = csub(x[jj], cmul(prow[jj], u));
+        }
+        gsync();
+    }
+    return pos;
+}
+
+// Put row `pos` of a distributed matrix back on lane `pos` (via the tile).
+template <int D>
+__device__ __forceinline__ void regather_rows(Group<D> &G, cd (&x)[D], int pos, bool wr) {
+    if (wr) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) G.tile[pos * D + j] = x[j];
+    }
+    gsync();
+#pragma unroll
+    for (int j = 0; j < D; ++j) x[j] = G.tile[G.i * D + j];
+    gsync();
+}
+
+// ---------------------------------------------------------------------------
+// expm of the group's matrix (a = this lane's row of A).
+//
+// expm_prologue: Julia's isdiag fast path and the 1-norm -> (m, s) choice.
+// expm_low:      m in {3, 5} with at most three row-matrices live in VGPRs
+//                (A2, A4 and an accumulator); the row of A is REBUILT by the
+//                caller-supplied `reload` for the final U = A*U' product
+//                instead of being kept alive -- A is cheap to rebuild from
+//                the operator basis, registers are not.
+// expm_high:     m in {7, 9, 13} (+ squarings), generous registers; runs in a
+//                separate kernel so its pressure does not cap the main one.
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ int expm_prologue(Group<D> &G, const cd (&a)[D], cd (&x)[D], bool wr, int &s_out) {
+    const int i = G.i;
+    bool off = false;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        if (j != i && (a[j].re != 0.0 || a[j].im != 0.0)) off = true;
+    const double anyoff = group_max(G, off ? 1.0 : 0.0, wr);
+    s_out = 0;
+    if (anyoff == 0.0) {  // isdiag(A): exp of the diagonal
+        cd aii = czero();
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+            if (j == i) aii = a[j];
+        const double e = exp(aii.re);
+        const double sn = sin(aii.im), cs = cos(aii.im);
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = (j == i) ? cmake(e * cs, e * sn) : czero();
+        return 0;
+    }
+    double *t = reinterpret_cast<double *>(G.tile);
+    if (wr) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) t[i * D + j] = hypot(a[j].re, a[j].im);
+    }
+    gsync();
+    double cs = 0.0;
+#pragma unroll
+    for (int r = 0; r < D; ++r) cs += t[r * D + i];
+    gsync();
+    const double nA = group_max(G, cs, wr);  // opnorm(A, 1)
+    return pade_degree(nA, s_out);
+}
+
+// Final stage shared by every degree: X = V + U, Y = V - U, gesv(Y, X).
+template <int D>
+__device__ __forceinline__ void pade_finish(Group<D> &G, const cd (&v)[D], const cd (&u)[D], cd (&x)[D],
+                                            bool wr, int &singular) {
+    cd y[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        x[j] = cadd(v[j], u[j]);
+        y[j] = csub(v[j], u[j]);
+    }
+    const int pos = gesv_rows<D>(G, y, x, wr, singular);
+    regather_rows<D>(G, x, pos, wr);
+}
+
+template <int D, class Reload>
+__device__ __forceinline__ void expm_low(Group<D> &G, int m, cd (&a)[D], cd (&x)[D], bool wr, int &singular,
+                                         Reload reload) {
+    const int i = G.i;
+    const double *C = (m == 3) ? kPade3 : kPade5;
+    cd p[D], q[D];
+    // A2 = A*A
+    tile_store_row(G, a, wr);
+    gsync();
+    mm_tile<D>(a, G.tile, p);
+    gsync();
+    if (m == 5) {
+        // A4 = P*A2 with P = I*A2 = A2 (Julia's first loop product is exact)
+        tile_store_row(G, p, wr);
+        gsync();
+        mm_tile<D>(p, G.tile, q);
+        gsync();
+    }
+    // U' = (C1 I + C3 A2) [+ C5 A4],  V = (C0 I + C2 A2) [+ C4 A4]   (Julia's order)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double du = (j == i) ? C[1] : 0.0, dv = (j == i) ? C[0] : 0.0;
+        cd u = cmake(du + C[3] * p[j].re, 0.0 + C[3] * p[j].im);
+        cd v = cmake(dv + C[2] * p[j].re, 0.0 + C[2] * p[j].im);
+        if (m == 5) {
+            u = cadd(u, cscale(C[5], q[j]));
+            v = cadd(v, cscale(C[4], q[j]));
+        }
+        p[j] = u;
+        q[j] = v;
+    }
+    // U = A*U'
+    tile_store_row(G, p, wr);
+    gsync();
+    reload(a);
+    mm_tile<D>(a, G.tile, p);
+    gsync();
+    pade_finish<D>(G, q, p, x, wr, singular);
+}
+
+template <int D>
+__device__ __forceinline__ void expm_high(Group<D> &G, int m, int s, cd (&a)[D], cd (&x)[D], bool wr, int &singular) {
+    const int i = G.i;
+    if (m <= 9) {
+        const double *C = m == 3 ? kPade3 : m == 5 ? kPade5 : m == 7 ? kPade7 : kPade9;
+        const int half = (m + 1) / 2;
+        cd p[D], u[D], v[D], t[D];
+        tile_store_row(G, a, wr); gsync(); mm_tile<D>(a, G.tile, p); gsync();
+        tile_store_row(G, p, wr); gsync();  // A2 stays in the tile for P *= A2
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const double du = (j == i) ? C[1] : 0.0, dv = (j == i) ? C[0] : 0.0;
+            u[j] = cmake(du + C[3] * p[j].re, 0.0 + C[3] * p[j].im);
+            v[j] = cmake(dv + C[2] * p[j].re, 0.0 + C[2] * p[j].im);
+        }
+        for (int kk = 2; kk < half; ++kk) {
+            mm_tile<D>(p, G.tile, t);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                p[j] = t[j];
+                u[j] = cadd(u[j], cscale(C[2 * kk + 1], p[j]));
+                v[j] = cadd(v[j], cscale(C[2 * kk], p[j]));
+            }
+        }
+        gsync();
+        tile_store_row(G, u, wr); gsync(); mm_tile<D>(a, G.tile, t); gsync();
+        pade_finish<D>(G, v, t, x, wr, singular);
+        return;
+    }
+    // m = 13: A /= 2^s, Pade 13, s squarings
+    if (s > 0) {
+        const double f = ldexp(1.0, s);
+#pragma unroll
+        for (int j = 0; j < D; ++j) a[j] = cmake(a[j].re / f, a[j].im / f);
+    }
+    const double *C = kPade13;
+    cd a2[D], a4[D], a6[D], w[D], u[D], v[D];
+    tile_store_row(G, a, wr); gsync(); mm_tile<D>(a, G.tile, a2); gsync();
+    tile_store_row(G, a2, wr); gsync(); mm_tile<D>(a2, G.tile, a4); gsync();
+    tile_store_row(G, a4, wr); gsync(); mm_tile<D>(a2, G.tile, a6); gsync();
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        w[j] = cadd(cadd(cscale(C[12], a6[j]), cscale(C[10], a4[j])), cscale(C[8], a2[j]));
+    tile_store_row(G, w, wr); gsync(); mm_tile<D>(a6, G.tile, v); gsync();
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        v[j] = cadd(cadd(cadd(v[j], cscale(C[6], a6[j])), cscale(C[4], a4[j])), cscale(C[2], a2[j]));
+        if (j == i) v[j] = cadd(v[j], cmake(C[0], 0.0));
+        w[j] = cadd(cadd(cscale(C[13], a6[j]), cscale(C[11], a4[j])), cscale(C[9], a2[j]));
+    }
+    tile_store_row(G, w, wr); gsync(); mm_tile<D>(a6, G.tile, u); gsync();
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        u[j] = cadd(cadd(cadd(u[j], cscale(C[7], a6[j])), cscale(C[5], a4[j])), cscale(C[3], a2[j]));
+        if (j == i) u[j] = cadd(u[j], cmake(C[1], 0.0));
+    }
+    tile_store_row(G, u, wr); gsync(); mm_tile<D>(a, G.tile, w); gsync();
+    pade_finish<D>(G, v, w, x, wr, singular);
+    for (int r = 0; r < s; ++r) {
+        tile_store_row(G, x, wr); gsync(); mm_tile<D>(x, G.tile, w); gsync();
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = w[j];
+    }
+}
+
+}  // namespace grape

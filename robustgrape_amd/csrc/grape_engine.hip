@@ -1,0 +1,490 @@
+// grape_engine.hip -- C ABI (include/grape.h) over the gfx950 GRAPE kernels.
+//
+// A plan owns: the device copy of the operator basis (row-major tiles), the
+// term tables, and a workspace for `max_batch` evaluations laid out in HBM as
+//   E  [b][k][v][D][D]   propagators of every FD variant   (c128)
+//   Q  [b][k][D][D]      chunk-local prefix products
+//   Mc [b][c][D][D]      per-chunk gradient kernels
+// (288 GB per MI355X; at d=9, N_t=512 one evaluation needs 2.0 MB).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "grape.h"
+#include "grape_kernels.hpp"
+
+using grape::cd;
+using grape::DevBatch;
+using grape::DevProblem;
+using grape::Term;
+
+static_assert(sizeof(Term) == sizeof(grape_term), "grape_term layout");
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHECK(expr)                                                                  \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(GRAPE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kScanWaves = 8;
+
+template <int D>
+size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
+template <int D>
+size_t scan_lds() {
+    return ((size_t)kScanWaves * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 3 * grape::Geo<D>::TILE) *
+           sizeof(cd);
+}
+
+// ---------------------------------------------------------------------------
+// dispatch helpers over the compile-time dimension
+// ---------------------------------------------------------------------------
+// Optional per-kernel event marks (profiling mode): fn(ctx, kernel, 0|1) around each launch.
+struct KMark {
+    void *ctx = nullptr;
+    void (*fn)(void *, int, int) = nullptr;
+    void operator()(int k, int phase) const {
+        if (fn) fn(ctx, k, phase);
+    }
+};
+
+template <int D>
+hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mark) {
+    constexpr int GPW = grape::Geo<D>::GPW;
+    const long nexp = (long)B.nb * P.Nt * P.nv;
+    mark(GRAPE_KERNEL_EXPM, 0);
+    hipLaunchKernelGGL(grape::k_expm<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
+                       P, B);
+    mark(GRAPE_KERNEL_EXPM, 1);
+    mark(GRAPE_KERNEL_EXPM_HIGH, 0);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
+                       B.overflow_count, B.status);
+    mark(GRAPE_KERNEL_EXPM_HIGH, 1);
+    mark(GRAPE_KERNEL_SCAN, 0);
+    hipLaunchKernelGGL((grape::k_scan<D, kScanWaves>), dim3(B.nb), dim3(64 * kScanWaves), scan_lds<D>(), st, P,
+                       B);
+    mark(GRAPE_KERNEL_SCAN, 1);
+    const long ng = (long)B.nb * P.Nt;
+    mark(GRAPE_KERNEL_GRAD, 0);
+    hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st, P,
+                       B);
+    mark(GRAPE_KERNEL_GRAD, 1);
+    if (P.xadd_dep && P.na > 0) {
+        mark(GRAPE_KERNEL_REDUCE, 0);
+        hipLaunchKernelGGL(grape::k_reduce_add, dim3((B.nb * P.na + 255) / 256), dim3(256), 0, st, P, B);
+        mark(GRAPE_KERNEL_REDUCE, 1);
+    }
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_expm_raw(const cd *A, cd *Erm, cd *Ecm, int n, int *ovf, int *ovf_count, int *status,
+                           int *mstats, hipStream_t st) {
+    constexpr int GPW = grape::Geo<D>::GPW;
+    hipLaunchKernelGGL(grape::k_expm_raw<D>, dim3((n + GPW - 1) / GPW), dim3(64), expm_lds<D>(), st, A, Erm, n,
+                       ovf, ovf_count, status, mstats);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, Erm, ovf, ovf_count, status);
+    const long tot = (long)n * D * D;
+    hipLaunchKernelGGL(grape::k_transpose_tiles<D>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, Erm, Ecm,
+                       n);
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t set_lds_limits() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, kScanWaves>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>());
+    return e;
+}
+
+#define GRAPE_DIMS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+
+hipError_t dispatch_pipeline(int D, const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mk) {
+    switch (D) {
+#define CASE(d) \
+    case d: return launch_pipeline<d>(P, B, st, mk);
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
+hipError_t dispatch_expm_raw(int D, const cd *A, cd *Erm, cd *Ecm, int n, int *ovf, int *ovfc, int *status,
+                             int *mstats, hipStream_t st) {
+    switch (D) {
+#define CASE(d) \
+    case d: return launch_expm_raw<d>(A, Erm, Ecm, n, ovf, ovfc, status, mstats, st);
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
+hipError_t dispatch_lds_limits(int D) {
+    switch (D) {
+#define CASE(d) \
+    case d: return set_lds_limits<d>();
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t dalloc(T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T));
+}
+
+}  // namespace
+
+struct grape_plan {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevProblem P{};
+    int max_batch = 0;
+    // device buffers
+    cd *d_ops = nullptr;
+    Term *d_h0 = nullptr, *d_tgt = nullptr, *d_err = nullptr;
+    int *d_err_off = nullptr;
+    double *d_W = nullptr;
+    cd *d_E = nullptr, *d_Q = nullptr, *d_Mc = nullptr;
+    double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
+    int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0] overflow count, [1] status
+    // optional per-kernel timing with HIP events on the plan's stream
+    bool profiling = false;
+    struct Pending {
+        int kernel;
+        hipEvent_t a, b;
+    };
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<Pending> pending;
+    double kernel_ms[GRAPE_NUM_KERNELS] = {0};
+    long long kernel_launches[GRAPE_NUM_KERNELS] = {0};
+    hipEvent_t get_event() {
+        hipEvent_t e = nullptr;
+        if (!ev_pool.empty()) {
+            e = ev_pool.back();
+            ev_pool.pop_back();
+        } else if (hipEventCreate(&e) != hipSuccess) {
+            e = nullptr;
+        }
+        return e;
+    }
+};
+
+static void free_plan(grape_plan *p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    void *bufs[] = {p->d_ops, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
+                    p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
+    for (auto &pe : p->pending) {
+        (void)hipEventDestroy(pe.a);
+        (void)hipEventDestroy(pe.b);
+    }
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+static int validate_terms(const grape_term *t, int n, int n_ops, int np, int na, bool target, const char *what) {
+    for (int k = 0; k < n; ++k) {
+        if (t[k].op < 0 || t[k].op >= n_ops) return fail(GRAPE_ERR_INVALID, std::string(what) + ": op out of range");
+        if (t[k].var < 0 || t[k].var > 3) return fail(GRAPE_ERR_INVALID, std::string(what) + ": bad var");
+        if (t[k].func < 0 || t[k].func > 4) return fail(GRAPE_ERR_INVALID, std::string(what) + ": bad func");
+        if (t[k].var == 1 && (t[k].index < 0 || t[k].index >= np))
+            return fail(GRAPE_ERR_INVALID, std::string(what) + ": control index out of range");
+        if (t[k].var == 2 && (t[k].index < 0 || t[k].index >= na))
+            return fail(GRAPE_ERR_INVALID, std::string(what) + ": x_add index out of range");
+        if (target && (t[k].var == 1 || t[k].var == 3))
+            return fail(GRAPE_ERR_INVALID, std::string(what) + ": target terms may only use x_add");
+        if (!target && t[k].func == 4)
+            return fail(GRAPE_ERR_INVALID, std::string(what) + ": cis coefficients only in target terms");
+    }
+    return GRAPE_OK;
+}
+
+extern "C" {
+
+int grape_abi_version(void) { return GRAPE_ABI_VERSION; }
+
+const char *grape_last_error(void) { return g_err.c_str(); }
+
+int grape_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
+    if (!desc || !out) return fail(GRAPE_ERR_INVALID, "null argument");
+    *out = nullptr;
+    const int D = desc->ndim;
+    if (D < 2 || desc->ntimes < 1 || desc->nparam < 1 || desc->nadd < 0 || desc->nerr < 0 || desc->n_ops < 1)
+        return fail(GRAPE_ERR_INVALID, "bad dimensions in descriptor");
+    if (D > GRAPE_MAX_SMALL_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim > GRAPE_MAX_SMALL_DIM");
+    if (desc->nerr > 0) return fail(GRAPE_ERR_UNSUPPORTED, "error sources are not served by this build yet");
+    if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || !desc->projector_diag || !desc->target_terms ||
+        desc->n_target_terms < 1)
+        return fail(GRAPE_ERR_INVALID, "missing operator basis / terms / projector");
+    if (!(desc->t0 > 0) || !(desc->eps > 0)) return fail(GRAPE_ERR_INVALID, "t0 and eps must be positive");
+    int rc;
+    if ((rc = validate_terms(desc->h0_terms, desc->n_h0_terms, desc->n_ops, desc->nparam, desc->nadd, false, "H0")))
+        return rc;
+    if ((rc = validate_terms(desc->target_terms, desc->n_target_terms, desc->n_ops, desc->nparam, desc->nadd, true,
+                             "target")))
+        return rc;
+    double trP = 0.0;
+    for (int i = 0; i < D; ++i) trP += desc->projector_diag[i];
+    if (!(trP > 0)) return fail(GRAPE_ERR_INVALID, "projector trace must be positive");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GRAPE_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(GRAPE_ERR_NO_DEVICE, "device index out of range");
+
+    grape_plan *p = new grape_plan();
+    p->device = device;
+    p->max_batch = desc->max_batch > 0 ? desc->max_batch : 256;
+    auto bail = [&](int code) {
+        free_plan(p);
+        return code;
+    };
+    if (hipSetDevice(device) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(GRAPE_ERR_HIP, "hipStreamCreate failed"));
+    if (dispatch_lds_limits(D) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
+
+    DevProblem &P = p->P;
+    P.D = D;
+    P.Nt = desc->ntimes;
+    P.np = desc->nparam;
+    P.na = desc->nadd;
+    P.ne = desc->nerr;
+    P.nx = desc->nparam * desc->ntimes + desc->nadd;
+    P.n_h0 = desc->n_h0_terms;
+    P.n_tgt = desc->n_target_terms;
+    P.xadd_dep = 0;
+    for (int k = 0; k < desc->n_h0_terms; ++k)
+        if (desc->h0_terms[k].var == 2) P.xadd_dep = 1;
+    // nominal + one FD variant per control; x_add variants only when H0 reads x_add
+    // (otherwise exp(A(x_add+eps)) == exp(A) bit for bit and the difference is 0).
+    P.nv = 1 + P.np + (P.xadd_dep ? P.na : 0);
+    P.dt = desc->t0 / desc->ntimes;
+    P.eps = desc->eps;
+    P.eps2 = desc->eps2;
+    P.inv_eps = 1.0 / desc->eps;
+    P.DD = trP * (trP + 1.0);
+    const int NG = kScanWaves * (64 / D);
+    const int nc0 = std::min(NG, P.Nt);
+    P.L = (P.Nt + nc0 - 1) / nc0;
+    P.nchunks = (P.Nt + P.L - 1) / P.L;
+
+    // operator basis: column-major interleaved -> row-major cd tiles
+    std::vector<cd> ops((size_t)desc->n_ops * D * D);
+    for (int o = 0; o < desc->n_ops; ++o)
+        for (int r = 0; r < D; ++r)
+            for (int c = 0; c < D; ++c) {
+                const double *src = desc->ops + 2 * ((size_t)o * D * D + r + (size_t)c * D);
+                ops[(size_t)o * D * D + r * D + c] = cd{src[0], src[1]};
+            }
+    const size_t MB = p->max_batch, T = (size_t)D * D;
+    bool ok = dalloc(&p->d_ops, ops.size()) == hipSuccess && dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
+              dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess && dalloc(&p->d_W, (size_t)D) == hipSuccess &&
+              dalloc(&p->d_E, MB * P.Nt * P.nv * T) == hipSuccess && dalloc(&p->d_Q, MB * P.Nt * T) == hipSuccess &&
+              dalloc(&p->d_Mc, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
+              dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
+              dalloc(&p->d_part, MB * P.Nt * std::max(P.na, 1)) == hipSuccess &&
+              dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
+              dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, 4) == hipSuccess;
+    if (!ok) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed"));
+    if (hipMemcpy(p->d_ops, ops.data(), ops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMemcpy(p->d_W, desc->projector_diag, D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(GRAPE_ERR_HIP, "upload failed"));
+    P.ops = p->d_ops;
+    P.h0 = p->d_h0;
+    P.tgt = p->d_tgt;
+    P.W = p->d_W;
+    *out = p;
+    return GRAPE_OK;
+}
+
+void grape_plan_destroy(grape_plan *plan) { free_plan(plan); }
+
+void *grape_plan_stream(grape_plan *plan) { return plan ? (void *)plan->stream : nullptr; }
+
+static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx) {
+    DevBatch B{};
+    B.nb = nb;
+    B.x = d_x;
+    B.E = p->d_E;
+    B.Q = p->d_Q;
+    B.Mc = p->d_Mc;
+    B.F = d_F;
+    B.Fdx = d_Fdx;
+    B.part_add = p->d_part;
+    B.tgt_part = p->d_tgt_part;
+    B.overflow = p->d_ovf;
+    B.overflow_count = p->d_ctrl;
+    B.status = p->d_ctrl + 1;
+    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, sizeof(int), p->stream));  // overflow count (status is sticky)
+    KMark mk;
+    if (p->profiling) {
+        mk.ctx = p;
+        mk.fn = [](void *ctx, int k, int phase) {
+            grape_plan *pl = static_cast<grape_plan *>(ctx);
+            hipEvent_t e = pl->get_event();
+            if (!e) return;
+            (void)hipEventRecord(e, pl->stream);
+            if (phase == 0) {
+                pl->pending.push_back({k, e, nullptr});
+            } else {
+                pl->pending.back().b = e;
+            }
+        };
+    }
+    HIPCHECK(dispatch_pipeline(p->P.D, p->P, B, p->stream, mk));
+    return GRAPE_OK;
+}
+
+static void resolve_events(grape_plan *p) {
+    for (auto &pe : p->pending) {
+        float ms = 0.f;
+        if (pe.a && pe.b && hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            p->kernel_ms[pe.kernel] += ms;
+            p->kernel_launches[pe.kernel] += 1;
+        }
+        if (pe.a) p->ev_pool.push_back(pe.a);
+        if (pe.b) p->ev_pool.push_back(pe.b);
+    }
+    p->pending.clear();
+}
+
+int grape_fidelity_grad_device_async(grape_plan *p, int nbatch, const double *d_x, double *d_F, double *d_F_dx,
+                                     double *d_F_d2err, double *d_F_d2err_dx) {
+    (void)d_F_d2err;
+    (void)d_F_d2err_dx;
+    if (!p || nbatch < 0 || (nbatch > 0 && (!d_x || !d_F || !d_F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    HIPCHECK(hipSetDevice(p->device));
+    for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
+        const int nb = std::min(p->max_batch, nbatch - b0);
+        int rc = enqueue(p, nb, d_x + (size_t)b0 * p->P.nx, d_F + b0, d_F_dx + (size_t)b0 * p->P.nx);
+        if (rc) return rc;
+    }
+    return GRAPE_OK;
+}
+
+int grape_plan_synchronize(grape_plan *p) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    HIPCHECK(hipSetDevice(p->device));
+    HIPCHECK(hipStreamSynchronize(p->stream));
+    resolve_events(p);
+    int st = 0;
+    HIPCHECK(hipMemcpy(&st, p->d_ctrl + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (st & 1) {
+        HIPCHECK(hipMemset(p->d_ctrl + 1, 0, sizeof(int)));
+        return fail(GRAPE_ERR_SINGULAR, "singular Pade denominator (Julia gesv! would throw SingularException)");
+    }
+    return GRAPE_OK;
+}
+
+int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, double *F_dx, double *F_d2err,
+                        double *F_d2err_dx) {
+    (void)F_d2err;
+    (void)F_d2err_dx;
+    if (!p || nbatch < 0 || (nbatch > 0 && (!x || !F || !F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    HIPCHECK(hipSetDevice(p->device));
+    const int nx = p->P.nx;
+    for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
+        const int nb = std::min(p->max_batch, nbatch - b0);
+        HIPCHECK(hipMemcpyAsync(p->d_x, x + (size_t)b0 * nx, (size_t)nb * nx * sizeof(double),
+                                hipMemcpyHostToDevice, p->stream));
+        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx);
+        if (rc) return rc;
+        HIPCHECK(hipMemcpyAsync(F + b0, p->d_F, nb * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        HIPCHECK(hipMemcpyAsync(F_dx + (size_t)b0 * nx, p->d_Fdx, (size_t)nb * nx * sizeof(double),
+                                hipMemcpyDeviceToHost, p->stream));
+        rc = grape_plan_synchronize(p);
+        if (rc) return rc;
+    }
+    return GRAPE_OK;
+}
+
+int grape_plan_set_profiling(grape_plan *p, int enable) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    p->profiling = enable != 0;
+    return GRAPE_OK;
+}
+
+int grape_plan_kernel_times(grape_plan *p, double *total_ms, long long *launches, int reset) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    for (int k = 0; k < GRAPE_NUM_KERNELS; ++k) {
+        if (total_ms) total_ms[k] = p->kernel_ms[k];
+        if (launches) launches[k] = p->kernel_launches[k];
+        if (reset) {
+            p->kernel_ms[k] = 0.0;
+            p->kernel_launches[k] = 0;
+        }
+    }
+    return GRAPE_OK;
+}
+
+int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
+                         double *U_derr_dx, double *U_derr_dx_add) {
+    (void)p; (void)x; (void)U; (void)U_dx; (void)U_dx_add; (void)U_derr; (void)U_derr_dx; (void)U_derr_dx_add;
+    return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs is not implemented in this build");
+}
+
+int grape_expm_batch(int device, int ndim, int n, const double *A, double *E, int *stats) {
+    if (ndim < 2 || ndim > GRAPE_MAX_SMALL_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim outside [2, GRAPE_MAX_SMALL_DIM]");
+    if (n < 0 || (n > 0 && (!A || !E))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (n == 0) return GRAPE_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GRAPE_ERR_NO_DEVICE, "no HIP device");
+    HIPCHECK(hipSetDevice(device));
+    const size_t T = (size_t)ndim * ndim;
+    cd *dA = nullptr, *dErm = nullptr, *dEcm = nullptr;
+    int *dovf = nullptr, *dctrl = nullptr;
+    auto cleanup = [&]() {
+        (void)hipFree(dA); (void)hipFree(dErm); (void)hipFree(dEcm); (void)hipFree(dovf); (void)hipFree(dctrl);
+    };
+    if (dalloc(&dA, n * T) || dalloc(&dErm, n * T) || dalloc(&dEcm, n * T) || dalloc(&dovf, (size_t)n) ||
+        dalloc(&dctrl, 8)) {
+        cleanup();
+        return fail(GRAPE_ERR_ALLOC, "device allocation failed");
+    }
+    int rc = GRAPE_OK;
+    int ctrl[8] = {0};
+    if (hipMemcpy(dA, A, n * T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(dctrl, 0, 8 * sizeof(int)) != hipSuccess ||
+        dispatch_expm_raw(ndim, dA, dErm, dEcm, n, dovf, dctrl, dctrl + 1, dctrl + 2, nullptr) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(E, dEcm, n * T * sizeof(cd), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ctrl, dctrl, 8 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(GRAPE_ERR_HIP, std::string("expm batch failed: ") + hipGetErrorString(hipGetLastError()));
+    cleanup();
+    if (rc) return rc;
+    if (stats)
+        for (int k = 0; k < 5; ++k) stats[k] = ctrl[2 + k];
+    if (ctrl[1] & 1) return fail(GRAPE_ERR_SINGULAR, "singular Pade denominator");
+    return GRAPE_OK;
+}
+
+}  // extern "C"

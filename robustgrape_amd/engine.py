@@ -1,0 +1,138 @@
+"""Host side of the GPU path: plans over libgrape.so and the reference's functions.
+
+``calculate_fidelity_and_derivatives`` mirrors src/FidelityCalculations.jl:19-119
+(same arguments, same return tuple, AssertionError on a bad x shape as
+src/UnitaryCalculations.jl:22) and additionally accepts a 2-D ``x`` of shape
+(nbatch, n_x) to evaluate a batch of control vectors in one device pass.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _capi
+from .operators import DescriptorBuffers
+from .types import FidelityRobustGRAPEProblem, split_x
+
+
+class GrapePlan:
+    """One device plan for one problem (grape_plan_create / grape_plan_destroy)."""
+
+    def __init__(self, fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 256):
+        L = _capi.lib()
+        self.fp = fp
+        self.up = fp.unitary_problem
+        self.nparam = int(nparam)
+        self.device = int(device)
+        self.nx = self.nparam * self.up.ntimes + self.up.nb_additional_param
+        self.nerr = len(self.up.error_sources)
+        self.max_batch = int(max_batch)
+        self._bufs = DescriptorBuffers(fp, self.nparam, self.max_batch)
+        h = ctypes.c_void_p()
+        _capi.check(L.grape_plan_create(ctypes.byref(self._bufs.desc), self.device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _capi.lib().grape_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return _capi.lib().grape_plan_stream(self.handle)
+
+    def fidelity_grad(self, X):
+        """Host arrays in/out. X: (nbatch, n_x). Returns F (nb,), F_dx (nb, n_x),
+        F_d2err (nb, nerr), F_d2err_dx (nb, n_x, nerr)."""
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        if X.ndim != 2 or X.shape[1] != self.nx:
+            raise AssertionError("Control parameter size must be a multiple of time steps")
+        nb = X.shape[0]
+        F = np.empty(nb)
+        Fdx = np.empty((nb, self.nx))
+        Fd2 = np.empty((nb, self.nerr)) if self.nerr else None
+        Fd2dx = np.empty((nb, self.nerr, self.nx)) if self.nerr else None
+        _capi.check(_capi.lib().grape_fidelity_grad(self.handle, nb, _capi.dptr(X), _capi.dptr(F),
+                                                     _capi.dptr(Fdx), _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
+        if not self.nerr:
+            Fd2 = np.zeros((nb, 0))
+            Fd2dx = np.zeros((nb, self.nx, 0))
+        else:
+            Fd2dx = Fd2dx.transpose(0, 2, 1)
+        return F, Fdx, Fd2, Fd2dx
+
+    def fidelity_grad_device_async(self, x_ptr: int, F_ptr: int, Fdx_ptr: int, nbatch: int,
+                                   Fd2_ptr: int = 0, Fd2dx_ptr: int = 0):
+        """Device pointers (e.g. torch CUDA tensors' data_ptr()), enqueued on the plan stream."""
+        _capi.check(_capi.lib().grape_fidelity_grad_device_async(
+            self.handle, int(nbatch), ctypes.c_void_p(x_ptr), ctypes.c_void_p(F_ptr),
+            ctypes.c_void_p(Fdx_ptr), ctypes.c_void_p(Fd2_ptr or None), ctypes.c_void_p(Fd2dx_ptr or None)))
+
+    def set_profiling(self, enable: bool):
+        _capi.check(_capi.lib().grape_plan_set_profiling(self.handle, int(bool(enable))))
+
+    def kernel_times(self, reset: bool = False):
+        """{kernel name: (total ms, launches)} accumulated while profiling was on."""
+        ms = (ctypes.c_double * 5)()
+        n = (ctypes.c_longlong * 5)()
+        _capi.check(_capi.lib().grape_plan_kernel_times(self.handle, ms, n, int(reset)))
+        return {name: (ms[k], n[k]) for k, name in enumerate(_capi.KERNEL_NAMES)}
+
+    def synchronize(self):
+        _capi.check(_capi.lib().grape_plan_synchronize(self.handle))
+
+
+_cache_lock = threading.Lock()
+_plan_cache: dict = {}
+
+
+def get_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 256) -> GrapePlan:
+    """Plans are cached per (problem object, nparam, device, max_batch)."""
+    key = (id(fp), nparam, device, max_batch)
+    with _cache_lock:
+        ent = _plan_cache.get(key)
+        if ent is not None and ent.fp is fp:
+            return ent
+        plan = GrapePlan(fp, nparam, device, max_batch)
+        _plan_cache[key] = plan
+        return plan
+
+
+def clear_plans():
+    with _cache_lock:
+        for p in _plan_cache.values():
+            p.close()
+        _plan_cache.clear()
+
+
+def calculate_fidelity_and_derivatives(fidelity_problem: FidelityRobustGRAPEProblem, x, device: int = 0):
+    """GPU restatement of src/FidelityCalculations.jl:19-119.
+
+    Returns (F, F_dx_tot, F_d2err, F_d2err_dx_tot) with the reference's shapes:
+    F scalar, F_dx_tot (n_x,), F_d2err (nerr,), F_d2err_dx_tot (n_x, nerr).
+    A 2-D x of shape (nbatch, n_x) returns the same quantities with a leading
+    batch axis.
+    """
+    x = np.asarray(x, dtype=np.float64)
+    batched = x.ndim == 2
+    X = x if batched else x[None, :]
+    _, _, nparam = split_x(fidelity_problem.unitary_problem, X[0])
+    plan = get_plan(fidelity_problem, nparam, device, max_batch=min(256, max(1, X.shape[0])))
+    F, Fdx, Fd2, Fd2dx = plan.fidelity_grad(X)
+    if batched:
+        return F, Fdx, Fd2, Fd2dx
+    return float(F[0]), Fdx[0], Fd2[0], Fd2dx[0]
+
+
+def calculate_unitary_and_derivatives(unitary_problem, x, device: int = 0):
+    """src/UnitaryCalculations.jl:20-155 through grape_unitary_derivs (C ABI)."""
+    raise NotImplementedError("grape_unitary_derivs (materialised U_dx tensors, SURVEY.md 8f row f4) "
+                              "is not in this build; use calculate_fidelity_and_derivatives")

@@ -78,7 +78,7 @@ def main():
     # expm parity set: skew-Hermitian generators across every Pade degree
     rng = np.random.default_rng(123)
     As, Es, ms = [], [], []
-    for d in (5, 7, 9, 16):
+    for d in (5, 7, 9, 12):
         for norm in (0.01, 0.2, 0.6, 1.5, 4.0, 30.0):
             for _ in range(3):
                 H = rng.normal(size=(d, d)) + 1j * rng.normal(size=(d, d))

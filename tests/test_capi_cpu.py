@@ -1,0 +1,64 @@
+"""CPU-side checks of the boundary: the library builds, loads, exports every
+symbol include/grape.h declares, and the host-side descriptor packing is right.
+No compute call is made (no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests import problems as P
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "grape.h")).read()
+    return sorted(set(re.findall(r"\b(grape_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from robustgrape_amd import _capi
+    from robustgrape_amd.build import build_library
+    build_library(verbose=False)
+    L = _capi.lib()
+    declared = _header_symbols()
+    assert set(declared) == set(_capi.EXPORTED)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.grape_abi_version() == 1
+
+
+def test_descriptor_packing_roundtrip():
+    """The ctypes descriptor reproduces the operator basis (column-major, interleaved)."""
+    from robustgrape_amd.operators import DescriptorBuffers
+    fp = P.full9_problem(16)
+    buf = DescriptorBuffers(fp, nparam=1, max_batch=8)
+    d = buf.desc
+    assert (d.ndim, d.ntimes, d.nparam, d.nadd, d.nerr) == (9, 16, 1, 1, 0)
+    ops = buf.ops.reshape(d.n_ops, 9 * 9 * 2)
+    x = np.array([0.37])
+    H = np.zeros((9, 9), complex)
+    for k in range(d.n_h0_terms):
+        t = d.h0_terms[k]
+        op = (ops[t.op, 0::2] + 1j * ops[t.op, 1::2]).reshape(9, 9, order="F")
+        coef = {2: np.cos, 3: np.sin}.get(t.func, lambda v: 1.0)(t.a * x[0] + t.b)
+        H += complex(t.scale_re, t.scale_im) * coef * op
+    np.testing.assert_allclose(H, fp.unitary_problem.H0(1, x, [0.0]), atol=1e-15)
+    np.testing.assert_array_equal(buf.pdiag, np.diag(P.W_FULL9))
+
+
+def test_closure_problems_are_rejected_by_the_device_path():
+    from robustgrape_amd.operators import DescriptorBuffers
+    with pytest.raises(TypeError):
+        DescriptorBuffers(P.sym_problem(8, device=False), nparam=1)
+
+
+def test_non_diagonal_projector_rejected():
+    from robustgrape_amd.operators import DescriptorBuffers
+    fp = P.sym_problem(8)
+    W = np.array(P.W_SYM)
+    W[0, 1] = 0.5
+    with pytest.raises(ValueError):
+        DescriptorBuffers(fp.replace(projector=W), nparam=1)

@@ -1,0 +1,132 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Tolerance tiers (FD noise analysis there):
+  T0  propagators E_k              <= 1e-13 relative (max-abs / max|E|, x max(1, |A|_1) for m = 13)
+  T1  U, F                         <= 1e-12 absolute
+  T2  eps-FD quantities (F_dx)     <= 1e-6 * max|ref|
+"""
+import os
+
+import numpy as np
+import pytest
+
+from tests import problems as P
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T1 = 1e-12
+T2 = 1e-6
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from robustgrape_amd import _capi
+    assert _capi.lib().grape_device_count() > 0
+
+
+def _golden(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+
+
+def _assert_fid(F, Fdx, ref_F, ref_Fdx):
+    assert abs(F - ref_F) <= T1, (F, ref_F)
+    err = np.max(np.abs(Fdx - ref_Fdx))
+    assert err <= T2 * np.max(np.abs(ref_Fdx)), (err, np.max(np.abs(ref_Fdx)))
+
+
+def test_expm_batch_matches_oracle_every_pade_degree():
+    from robustgrape_amd import _capi
+    g = _golden("expm")
+    n = len(g["m"])
+    groups = {}
+    for i in range(n):
+        groups.setdefault(g[f"A{i}"].shape[0], []).append(i)
+    for d, idx in groups.items():
+        A = np.stack([np.asfortranarray(g[f"A{i}"]) for i in idx])
+        Acm = np.ascontiguousarray(A.transpose(0, 2, 1))  # column-major storage per matrix
+        E = np.empty_like(Acm)
+        stats = (_capi.ctypes.c_int * 5)()
+        _capi.check(_capi.lib().grape_expm_batch(0, d, len(idx), _capi.dptr(Acm), _capi.dptr(E), stats))
+        E = E.transpose(0, 2, 1)
+        for j, i in enumerate(idx):
+            ref = g[f"E{i}"]
+            norm = np.abs(g[f"A{i}"]).sum(axis=0).max()
+            rel = np.max(np.abs(E[j] - ref)) / np.max(np.abs(ref))
+            assert rel <= 1e-13 * max(1.0, norm), (d, i, g["m"][i], rel)
+        hist = {3: 0, 5: 1, 7: 2, 9: 3, 13: 4}
+        expect = [0] * 5
+        for i in idx:
+            expect[hist[int(g["m"][i])]] += 1
+        assert list(stats) == expect
+
+
+@pytest.mark.parametrize("name,builder", [
+    ("c1", lambda: P.sym_problem(500, t0=P.T0_TO)),
+    ("c2", lambda: P.full9_problem(512)),
+])
+def test_fidelity_gradient_matches_golden(name, builder):
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    g = _golden(name)
+    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(builder(), g["x"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    assert d2.shape == (0,) and d2dx.shape == (len(g["x"]), 0)
+
+
+def test_restart_batch_matches_golden():
+    """C4 sample: four restarts evaluated in one batched device pass."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    g = _golden("c4")
+    F, Fdx, _, _ = calculate_fidelity_and_derivatives(P.full9_problem(512), g["x"])
+    for b in range(len(F)):
+        _assert_fid(F[b], Fdx[b], g["F"][b], g["F_dx"][b])
+
+
+@pytest.mark.parametrize("d,ntimes", [(5, 1), (5, 2), (5, 7), (7, 3), (9, 1), (9, 13), (9, 57), (5, 130)])
+def test_small_problems_match_live_oracle(d, ntimes):
+    """Edge sizes (single step, chunk remainders, d = 5/7/9) against the oracle computed here."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    mk = {5: lambda dev: P.sym_problem(ntimes, device=dev), 7: lambda dev: P.fullblk_problem(ntimes, device=dev),
+          9: lambda dev: P.full9_problem(ntimes, device=dev)}[d]
+    x = P.random_x(ntimes, 100 + ntimes)
+    F0, g0, _, _ = O.calculate_fidelity_and_derivatives(mk(False), x)
+    F, g, _, _ = calculate_fidelity_and_derivatives(mk(True), x)
+    _assert_fid(F, g, F0, g0)
+
+
+def test_batch_equals_single_and_ragged_batches():
+    """Deterministic kernels: a batch element is bitwise the single evaluation; odd batch sizes."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = P.full9_problem(64)
+    X = np.stack([P.random_x(64, s) for s in range(11)])
+    F, Fdx, _, _ = calculate_fidelity_and_derivatives(fp, X)
+    for b in (0, 5, 10):
+        Fs, gs, _, _ = calculate_fidelity_and_derivatives(fp, X[b])
+        assert Fs == F[b] and np.array_equal(gs, Fdx[b])
+
+
+def test_known_answer_and_fd_identity_on_gpu():
+    """runtests.jl:115-165 (F > 0.9999) and :292-354 (FD of F vs F_dx) on the device path."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = P.sym_problem(1000)
+    F = calculate_fidelity_and_derivatives(fp, P.evered_pulse(1000))[0]
+    assert F > 0.9999 and abs(F - 0.999996184760959) < 1e-12
+    fp = P.sym_problem(50)
+    rng = np.random.default_rng(7)
+    for idx in (3, 17, 49, 50):
+        xs = 2 * np.pi * rng.uniform(size=51)
+        F0, g0, _, _ = calculate_fidelity_and_derivatives(fp, xs)
+        xs[idx] += fp.unitary_problem.eps
+        F1 = calculate_fidelity_and_derivatives(fp, xs)[0]
+        np.testing.assert_allclose((F1 - F0) / fp.unitary_problem.eps, g0[idx], rtol=1e-3, atol=1e-3)
+
+
+def test_errors_are_loud():
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    with pytest.raises(AssertionError):
+        calculate_fidelity_and_derivatives(P.full9_problem(64), np.zeros(64 + 2))
+    with pytest.raises(TypeError):
+        calculate_fidelity_and_derivatives(P.sym_problem(8, device=False), np.zeros(9))
