@@ -187,11 +187,12 @@ __device__ __forceinline__ int pade_degree(double nA, int &s) {
 }
 
 // ---------------------------------------------------------------------------
-// gesv(Y, X): solve Y Z = X in place (Z returned in x), LAPACK semantics.
+// gesv(Y, X): solve Y Z = X in place (Z returned in x), LAPACK semantics
+// (zgetrf partial pivoting + zgetrs).  General path with row interchanges.
 // On return lane i holds row `pos` of the solution (pos returned).
 // ---------------------------------------------------------------------------
 template <int D>
-__device__ __forceinline__ int gesv_rows(Group<D> &G, cd (&y)[D], cd (&x)[D], bool wr, int &singular) {
+__device__ __forceinline__ int gesv_rows_pivot(Group<D> &G, cd (&y)[D], cd (&x)[D], bool wr, int &singular) {
     int pos = G.i;  // physical row position of the row this lane holds
     double *red = G.auxd();
     cd *prow = G.tile;  // pivot row broadcast: y part [0,D), x part [D,2D)
@@ -267,6 +268,75 @@ __device__ __forceinline__ int gesv_rows(Group<D> &G, cd (&y)[D], cd (&x)[D], bo
     return pos;
 }
 
+// Interchange-free elimination, used when partial pivoting provably never
+// swaps rows.  Sufficient condition (checked by gesv_solve): every column of
+// Y is diagonally dominant with margin r = 3/2 > sqrt(2),
+//     |y_jj| >= r * sum_{i != j} |y_ij|.
+// Margin-r column dominance is inherited by every Schur complement (the
+// excess |a_jj| - r*sum|a_ij| cannot decrease under one elimination step when
+// the pivot column is itself margin-r dominant), so at every step the
+// diagonal modulus exceeds sqrt(2) times any sub-diagonal modulus, and since
+// |z| <= |re z| + |im z| <= sqrt(2)|z|, izamax's |re|+|im| metric picks the
+// diagonal too.  The arithmetic is then exactly that of the pivoted path.
+// Pade denominators for |A|_1 <= 0.25 (m <= 5) have margin ~7.
+// One barrier per step: the broadcast row alternates between two LDS buffers.
+template <int D>
+__device__ __forceinline__ void gesv_rows_nopivot(Group<D> &G, cd (&y)[D], cd (&x)[D], bool wr) {
+    const int i = G.i;
+    cd *buf[2] = {G.aux, G.tile};
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        cd *pr = buf[j & 1];
+        if (i == j && wr) {
+#pragma unroll
+            for (int jj = j; jj < D; ++jj) pr[jj] = y[jj];
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) pr[D + jj] = x[jj];
+        }
+        gsync();
+        if (i > j) {
+            const cd rp = cdiv(cmake(1.0, 0.0), pr[j]);  // zgetf2: scale the column by 1/pivot
+            const cd l = cmul(y[j], rp);
+            y[j] = l;
+#pragma unroll
+            for (int jj = j + 1; jj < D; ++jj) {
+                const cd u = pr[jj];
+                y[jj] = cadd(y[jj], cmul(l, cmake(-u.re, -u.im)));
+            }
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) x[jj] = csub(x[jj], cmul(pr[D + jj], l));
+        }
+    }
+    // back substitution; each lane inverts its own diagonal in parallel
+    cd ydiag = czero();
+#pragma unroll
+    for (int jj = 0; jj < D; ++jj)
+        if (jj == i) ydiag = y[jj];
+    const cd rd = cdiv(cmake(1.0, 0.0), ydiag);
+#pragma unroll
+    for (int k = D - 1; k >= 0; --k) {
+        cd *pr = buf[(k + D) & 1];
+        if (i == k) {
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) x[jj] = cmul(x[jj], rd);
+            if (wr) {
+#pragma unroll
+                for (int jj = 0; jj < D; ++jj) pr[jj] = x[jj];
+            }
+        }
+        gsync();
+        if (i < k) {
+            cd u = czero();
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj)
+                if (jj == k) u = y[jj];
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) x[jj] = csub(x[jj], cmul(pr[jj], u));
+        }
+    }
+    gsync();
+}
+
 // Put row `pos` of a distributed matrix back on lane `pos` (via the tile).
 template <int D>
 __device__ __forceinline__ void regather_rows(Group<D> &G, cd (&x)[D], int pos, bool wr) {
@@ -278,6 +348,32 @@ __device__ __forceinline__ void regather_rows(Group<D> &G, cd (&x)[D], int pos, 
 #pragma unroll
     for (int j = 0; j < D; ++j) x[j] = G.tile[G.i * D + j];
     gsync();
+}
+
+// Solve Y Z = X; lane i returns row i of Z in x.
+template <int D>
+__device__ __forceinline__ void gesv_solve(Group<D> &G, cd (&y)[D], cd (&x)[D], bool wr, int &singular) {
+    const int i = G.i;
+    double *t = reinterpret_cast<double *>(G.tile);
+    if (wr) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) t[i * D + j] = sqrt(y[j].re * y[j].re + y[j].im * y[j].im);
+    }
+    gsync();
+    double off = 0.0;
+#pragma unroll
+    for (int r = 0; r < D; ++r)
+        if (r != i) off += t[r * D + i];
+    const double dg = t[i * D + i];
+    const bool dominant = dg >= 1.5 * off && dg > 0.0;  // false on NaN
+    gsync();
+    const double bad = group_max(G, dominant ? 0.0 : 1.0, wr);
+    if (bad == 0.0) {
+        gesv_rows_nopivot<D>(G, y, x, wr);
+    } else {
+        const int pos = gesv_rows_pivot<D>(G, y, x, wr, singular);
+        regather_rows<D>(G, x, pos, wr);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -315,7 +411,7 @@ __device__ __forceinline__ int expm_prologue(Group<D> &G, const cd (&a)[D], cd (
     double *t = reinterpret_cast<double *>(G.tile);
     if (wr) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) t[i * D + j] = hypot(a[j].re, a[j].im);
+        for (int j = 0; j < D; ++j) t[i * D + j] = sqrt(a[j].re * a[j].re + a[j].im * a[j].im);
     }
     gsync();
     double cs = 0.0;
@@ -336,8 +432,7 @@ __device__ __forceinline__ void pade_finish(Group<D> &G, const cd (&v)[D], const
         x[j] = cadd(v[j], u[j]);
         y[j] = csub(v[j], u[j]);
     }
-    const int pos = gesv_rows<D>(G, y, x, wr, singular);
-    regather_rows<D>(G, x, pos, wr);
+    gesv_solve<D>(G, y, x, wr, singular);
 }
 
 template <int D, class Reload>

@@ -146,7 +146,7 @@ __device__ __forceinline__ void park(Group<D> &G, cd *slot_row, const cd (&a)[D]
 }
 
 template <int D>
-__global__ __launch_bounds__(64) void k_expm(DevProblem P, DevBatch B) {
+__global__ __launch_bounds__(64, (D <= 9 ? 3 : 2)) void k_expm(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     Group<D> G = make_group<D>(lds, threadIdx.x);
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 // k_grad: one row group per (b, k)
 // ---------------------------------------------------------------------------
 template <int D>
-__global__ __launch_bounds__(64) void k_grad(DevProblem P, DevBatch B) {
+__global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     constexpr int TILE = Geo<D>::TILE;
