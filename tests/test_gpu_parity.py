@@ -3,7 +3,7 @@
 Tolerance tiers (FD noise analysis there):
   T0  propagators E_k              <= 1e-13 relative (max-abs / max|E|, x max(1, |A|_1) for m = 13)
   T1  U, F                         <= 1e-12 absolute
-  T2  eps-FD quantities (F_dx)     <= 1e-6 * max|ref|
+  T2  eps-FD quantities (F_dx)     <= 1e-6 * max|ref| + 1e-8
 """
 import os
 
@@ -15,7 +15,7 @@ from tests import problems as P
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 T1 = 1e-12
-T2 = 1e-6
+T2, T2_ABS = 1e-6, 1e-8      # + absolute floor u/eps for gradients near an optimum
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -34,7 +34,7 @@ def _golden(name):
 def _assert_fid(F, Fdx, ref_F, ref_Fdx):
     assert abs(F - ref_F) <= T1, (F, ref_F)
     err = np.max(np.abs(Fdx - ref_Fdx))
-    assert err <= T2 * np.max(np.abs(ref_Fdx)), (err, np.max(np.abs(ref_Fdx)))
+    assert err <= T2 * np.max(np.abs(ref_Fdx)) + T2_ABS, (err, np.max(np.abs(ref_Fdx)))
 
 
 def test_expm_batch_matches_oracle_every_pade_degree():
