@@ -1,0 +1,128 @@
+# RobustGRAPEMI355X.jl -- ccall shim that routes RobustGRAPE.jl's hot path to libgrape.so.
+#
+# Keeps the reference's names (src/RobustGRAPE.jl:6-13): a FidelityRobustGRAPEProblem
+# whose H0 / error sources / target are `OperatorBasis` objects evaluates on the MI355X
+# through include/grape.h.  Julia is not installed in the build image, so this file is
+# not executed there; the same C entry points are exercised from Python by tests/.
+module RobustGRAPEMI355X
+
+using LinearAlgebra
+
+export OperatorTerm, OperatorBasis, calculate_fidelity_and_derivatives, grape_expm_batch
+
+const libgrape = normpath(joinpath(@__DIR__, "..", "robustgrape_amd", "libgrape.so"))
+
+# grape_var / grape_func (include/grape.h)
+const VAR_ONE, VAR_X, VAR_XADD, VAR_TSTEP = Int32(0), Int32(1), Int32(2), Int32(3)
+const FN_ONE, FN_LINEAR, FN_COS, FN_SIN, FN_CIS = Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
+
+struct GrapeTerm
+    op::Int32; var::Int32; index::Int32; func::Int32
+    a::Float64; b::Float64; scale_re::Float64; scale_im::Float64
+end
+
+struct GrapeDesc
+    ndim::Int32; ntimes::Int32; nparam::Int32; nadd::Int32; nerr::Int32; n_ops::Int32
+    t0::Float64; eps::Float64; eps2::Float64
+    projector_diag::Ptr{Float64}; ops::Ptr{ComplexF64}
+    n_h0_terms::Int32; h0_terms::Ptr{GrapeTerm}
+    err_term_offsets::Ptr{Int32}; err_terms::Ptr{GrapeTerm}
+    n_target_terms::Int32; target_terms::Ptr{GrapeTerm}
+    max_batch::Int32; reserved::NTuple{7,Int32}
+end
+
+"One coefficient * operator term: scale * f(a*v + b) * op (v = 1, x[index], x_add[index] or nt)."
+struct OperatorTerm
+    op::Matrix{ComplexF64}
+    var::Int32; index::Int32; func::Int32
+    a::Float64; b::Float64; scale::ComplexF64
+end
+OperatorTerm(op; var=VAR_ONE, index=1, func=FN_ONE, a=1.0, b=0.0, scale=1.0) =
+    OperatorTerm(ComplexF64.(op), var, Int32(index - 1), func, a, b, ComplexF64(scale))
+
+"Callable like the reference's closures: H0(nt, x, x_add) / Herror(nt, x, x_add, err) / target(x_add)."
+struct OperatorBasis
+    terms::Vector{OperatorTerm}
+    scaled_by_err::Bool
+end
+function _coef(t::OperatorTerm, nt, x, x_add)
+    v = t.var == VAR_ONE ? 1.0 : t.var == VAR_X ? x[t.index+1] : t.var == VAR_XADD ? x_add[t.index+1] : Float64(nt)
+    arg = t.a * v + t.b
+    f = t.func == FN_ONE ? 1.0 : t.func == FN_LINEAR ? arg : t.func == FN_COS ? cos(arg) :
+        t.func == FN_SIN ? sin(arg) : cis(arg)
+    return t.scale * f
+end
+(B::OperatorBasis)(nt, x, x_add) = sum(_coef(t, nt, x, x_add) * t.op for t in B.terms)
+(B::OperatorBasis)(nt, x, x_add, err) = err * sum(_coef(t, nt, x, x_add) * t.op for t in B.terms)
+(B::OperatorBasis)(x_add) = sum(_coef(t, 1, Float64[], x_add) * t.op for t in B.terms)
+
+function _check(rc)
+    rc == 0 || error("libgrape: " * unsafe_string(ccall((:grape_last_error, libgrape), Cstring, ())))
+end
+
+mutable struct DevicePlan
+    handle::Ptr{Cvoid}
+    keep::Vector{Any}      # arrays the descriptor points into
+    nx::Int; nerr::Int
+end
+
+const _plans = IdDict{Any,DevicePlan}()
+
+function device_plan(fp, nparam::Int; device::Integer=0, max_batch::Integer=256)
+    get!(_plans, fp) do
+        up = fp.unitary_problem
+        ops = Matrix{ComplexF64}[]
+        tr(terms) = [GrapeTerm((push!(ops, t.op); Int32(length(ops) - 1)), t.var, t.index, t.func,
+                               t.a, t.b, real(t.scale), imag(t.scale)) for t in terms]
+        h0 = tr(up.H0.terms)
+        errs = GrapeTerm[]; offs = Int32[0]
+        for es in up.error_sources
+            append!(errs, tr(es.Herror.terms)); push!(offs, length(errs))
+        end
+        tgt = tr(fp.target_unitary.terms)
+        opsflat = reduce(vcat, [vec(o) for o in ops])            # column-major, like the C side
+        pdiag = Float64.(diag(fp.projector))
+        keep = Any[opsflat, h0, errs, offs, tgt, pdiag]
+        desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, length(up.error_sources),
+                             length(ops), up.t0, up.ϵ, up.ϵ2, pointer(pdiag), pointer(opsflat),
+                             length(h0), pointer(h0), pointer(offs), isempty(errs) ? C_NULL : pointer(errs),
+                             length(tgt), pointer(tgt), max_batch, ntuple(_ -> Int32(0), 7)))
+        out = Ref{Ptr{Cvoid}}(C_NULL)
+        GC.@preserve keep begin
+            _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
+                         desc, device, out))
+        end
+        p = DevicePlan(out[], keep, nparam * up.ntimes + up.nb_additional_param, length(up.error_sources))
+        finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
+        p
+    end
+end
+
+"Drop-in for src/FidelityCalculations.jl:19-119: (F, F_dx_tot, F_d2err, F_d2err_dx_tot)."
+function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
+    up = fp.unitary_problem
+    xm = length(x) - up.nb_additional_param
+    @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
+    p = device_plan(fp, xm ÷ up.ntimes)
+    xv = Vector{Float64}(x)
+    F = Ref{Float64}(0.0); F_dx = zeros(p.nx); F_d2err = zeros(p.nerr); F_d2err_dx = zeros(p.nx, p.nerr)
+    GC.@preserve xv F_dx F_d2err F_d2err_dx begin
+        _check(ccall((:grape_fidelity_grad, libgrape), Cint,
+                     (Ptr{Cvoid}, Cint, Ptr{Float64}, Ref{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                     p.handle, 1, xv, F, F_dx, F_d2err, F_d2err_dx))
+    end
+    return (F[], F_dx, F_d2err, F_d2err_dx)
+end
+
+"Batched exp of n column-major d x d ComplexF64 matrices (LinearAlgebra.exp!'s algorithm)."
+function grape_expm_batch(As::Vector{Matrix{ComplexF64}}; device::Integer=0)
+    d = size(As[1], 1); n = length(As)
+    A = reduce(vcat, vec.(As)); E = similar(A); stats = zeros(Int32, 5)
+    GC.@preserve A E stats begin
+        _check(ccall((:grape_expm_batch, libgrape), Cint,
+                     (Cint, Cint, Cint, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{Int32}), device, d, n, A, E, stats))
+    end
+    return [reshape(E[(k-1)*d*d+1:k*d*d], d, d) for k in 1:n], stats
+end
+
+end # module
