@@ -191,7 +191,9 @@ typedef enum grape_kernel {
     GRAPE_KERNEL_SCAN = 2,      /* chunked prefix products, fidelity, gradient kernels */
     GRAPE_KERNEL_GRAD = 3,      /* per-step gradient contractions */
     GRAPE_KERNEL_REDUCE = 4,    /* x_add reductions */
-    GRAPE_NUM_KERNELS = 5
+    GRAPE_KERNEL_ERR_SCAN = 5,  /* error sources: U_derr, F_d2err, per-chunk kernels */
+    GRAPE_KERNEL_ERR_GRAD = 6,  /* error sources: F_d2err_dx contractions */
+    GRAPE_NUM_KERNELS = 7
 } grape_kernel;
 
 int grape_plan_set_profiling(grape_plan *plan, int enable);

@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "grape.h"
-#include "grape_kernels.hpp"
+#include "grape_errpath.hpp"
 
 using grape::cd;
 using grape::DevBatch;
@@ -46,6 +46,11 @@ constexpr int kScanWaves = 8;
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
 template <int D>
+size_t errscan_lds() {
+    return ((size_t)kScanWaves * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 4 * grape::Geo<D>::TILE) *
+           sizeof(cd);
+}
+template <int D>
 size_t scan_lds() {
     return ((size_t)kScanWaves * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 3 * grape::Geo<D>::TILE) *
            sizeof(cd);
@@ -68,8 +73,12 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     constexpr int GPW = grape::Geo<D>::GPW;
     const long nexp = (long)B.nb * P.Nt * P.nv;
     mark(GRAPE_KERNEL_EXPM, 0);
-    hipLaunchKernelGGL(grape::k_expm<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
-                       P, B);
+    if (P.ne > 0)
+        hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
     mark(GRAPE_KERNEL_EXPM, 1);
     mark(GRAPE_KERNEL_EXPM_HIGH, 0);
     hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
@@ -84,6 +93,17 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st, P,
                        B);
     mark(GRAPE_KERNEL_GRAD, 1);
+    if (P.ne > 0) {
+        mark(GRAPE_KERNEL_ERR_SCAN, 0);
+        hipLaunchKernelGGL((grape::k_err_scan<D, kScanWaves>), dim3(B.nb * P.ne), dim3(64 * kScanWaves),
+                           errscan_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_ERR_SCAN, 1);
+        const long ne_items = (long)B.nb * P.nchunks * P.ne;
+        mark(GRAPE_KERNEL_ERR_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_err_grad<D>, dim3((unsigned)((ne_items + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_ERR_GRAD, 1);
+    }
     if (P.xadd_dep && P.na > 0) {
         mark(GRAPE_KERNEL_REDUCE, 0);
         hipLaunchKernelGGL(grape::k_reduce_add, dim3((B.nb * P.na + 255) / 256), dim3(256), 0, st, P, B);
@@ -109,7 +129,9 @@ template <int D>
 hipError_t set_lds_limits() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, kScanWaves>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>());
-    return e;
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_err_scan<D, kScanWaves>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)errscan_lds<D>());
 }
 
 #define GRAPE_DIMS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
@@ -162,7 +184,9 @@ struct grape_plan {
     Term *d_h0 = nullptr, *d_tgt = nullptr, *d_err = nullptr;
     int *d_err_off = nullptr;
     double *d_W = nullptr;
-    cd *d_E = nullptr, *d_Q = nullptr, *d_Mc = nullptr;
+    cd *d_E = nullptr, *d_Q = nullptr, *d_Mc = nullptr, *d_Carry = nullptr, *d_Ub = nullptr, *d_Me = nullptr;
+    grape::VSpec *d_vs = nullptr;
+    double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0] overflow count, [1] status
     // optional per-kernel timing with HIP events on the plan's stream
@@ -191,7 +215,8 @@ static void free_plan(grape_plan *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_ops, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
-                    p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl};
+                    p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl,
+                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -239,7 +264,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (D < 2 || desc->ntimes < 1 || desc->nparam < 1 || desc->nadd < 0 || desc->nerr < 0 || desc->n_ops < 1)
         return fail(GRAPE_ERR_INVALID, "bad dimensions in descriptor");
     if (D > GRAPE_MAX_SMALL_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim > GRAPE_MAX_SMALL_DIM");
-    if (desc->nerr > 0) return fail(GRAPE_ERR_UNSUPPORTED, "error sources are not served by this build yet");
+    if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
     if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || !desc->projector_diag || !desc->target_terms ||
         desc->n_target_terms < 1)
         return fail(GRAPE_ERR_INVALID, "missing operator basis / terms / projector");
@@ -250,6 +275,24 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if ((rc = validate_terms(desc->target_terms, desc->n_target_terms, desc->n_ops, desc->nparam, desc->nadd, true,
                              "target")))
         return rc;
+    int n_err_terms = 0;
+    if (desc->nerr > 0) {
+        for (int e = 0; e < desc->nerr; ++e)
+            if (desc->err_term_offsets[e + 1] <= desc->err_term_offsets[e])
+                return fail(GRAPE_ERR_INVALID, "each error source needs at least one term");
+        if (desc->err_term_offsets[0] != 0) return fail(GRAPE_ERR_INVALID, "err_term_offsets[0] must be 0");
+        n_err_terms = desc->err_term_offsets[desc->nerr];
+        if ((rc = validate_terms(desc->err_terms, n_err_terms, desc->n_ops, desc->nparam, desc->nadd, false,
+                                 "error source")))
+            return rc;
+    }
+    bool xadd_dep = false;
+    for (int k = 0; k < desc->n_h0_terms; ++k)
+        if (desc->h0_terms[k].var == 2) xadd_dep = true;
+    for (int k = 0; k < n_err_terms; ++k)
+        if (desc->err_terms[k].var == 2) xadd_dep = true;
+    if (xadd_dep && desc->nerr > 0)
+        return fail(GRAPE_ERR_UNSUPPORTED, "error sources together with an x_add-dependent Hamiltonian");
     double trP = 0.0;
     for (int i = 0; i < D; ++i) trP += desc->projector_diag[i];
     if (!(trP > 0)) return fail(GRAPE_ERR_INVALID, "projector trace must be positive");
@@ -278,17 +321,46 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.nx = desc->nparam * desc->ntimes + desc->nadd;
     P.n_h0 = desc->n_h0_terms;
     P.n_tgt = desc->n_target_terms;
-    P.xadd_dep = 0;
-    for (int k = 0; k < desc->n_h0_terms; ++k)
-        if (desc->h0_terms[k].var == 2) P.xadd_dep = 1;
-    // nominal + one FD variant per control; x_add variants only when H0 reads x_add
-    // (otherwise exp(A(x_add+eps)) == exp(A) bit for bit and the difference is 0).
-    P.nv = 1 + P.np + (P.xadd_dep ? P.na : 0);
+    P.xadd_dep = xadd_dep ? 1 : 0;
+    // Propagator variants of one step (the closure call sites of UnitaryCalculations.jl:45-90):
+    //   0 nominal | dx: x_p + eps | dxa: x_add_q + eps (only if H0 reads x_add, otherwise
+    //   exp(A(x_add + eps)) == exp(A) bit for bit and the reference's difference is 0)
+    //   | ne > 0: dx2: x_p + eps2 | per error e: err(eps), err2(eps2), mix_p (x_p + eps2, err eps2)
+    // The eps2 variants only feed the mixed stencils: skipped when ne == 0 (dead work).
+    std::vector<grape::VSpec> vs;
+    auto addv = [&](int var, int idx, double delta, int err, double errval) {
+        grape::VSpec v;
+        v.pert.var = var;
+        v.pert.index = idx;
+        v.pert.delta = delta;
+        v.err = err;
+        v.errval = errval;
+        vs.push_back(v);
+    };
+    addv(-1, 0, 0.0, -1, 0.0);
+    P.off_dx = (int)vs.size();
+    for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps, -1, 0.0);
+    P.off_dxa = (int)vs.size();
+    if (xadd_dep)
+        for (int q = 0; q < desc->nadd; ++q) addv(2, q, desc->eps, -1, 0.0);
+    P.off_dx2 = (int)vs.size();
+    if (desc->nerr > 0)
+        for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps2, -1, 0.0);
+    P.off_err = (int)vs.size();
+    P.err_stride = 2 + desc->nparam;
+    for (int e = 0; e < desc->nerr; ++e) {
+        addv(-1, 0, 0.0, e, desc->eps);
+        addv(-1, 0, 0.0, e, desc->eps2);
+        for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps2, e, desc->eps2);
+    }
+    P.nv = (int)vs.size();
     P.dt = desc->t0 / desc->ntimes;
     P.eps = desc->eps;
     P.eps2 = desc->eps2;
     P.inv_eps = 1.0 / desc->eps;
+    P.inv_eps2sq = 1.0 / (desc->eps2 * desc->eps2);
     P.DD = trP * (trP + 1.0);
+    P.Dtr = trP;
     const int NG = kScanWaves * (64 / D);
     const int nc0 = std::min(NG, P.Nt);
     P.L = (P.Nt + nc0 - 1) / nc0;
@@ -310,8 +382,21 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_part, MB * P.Nt * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
-              dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, 4) == hipSuccess;
+              dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, 4) == hipSuccess &&
+              dalloc(&p->d_vs, vs.size()) == hipSuccess;
+    if (ok && P.ne > 0)
+        ok = dalloc(&p->d_Carry, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, MB * T) == hipSuccess &&
+             dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
+             dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
+             dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
     if (!ok) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed"));
+    if (hipMemcpy(p->d_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(GRAPE_ERR_HIP, "upload failed"));
+    if (P.ne > 0 &&
+        (hipMemcpy(p->d_err, desc->err_terms, n_err_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(p->d_err_off, desc->err_term_offsets, (P.ne + 1) * sizeof(int), hipMemcpyHostToDevice) !=
+             hipSuccess))
+        return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     if (hipMemcpy(p->d_ops, ops.data(), ops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
@@ -321,6 +406,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.ops = p->d_ops;
     P.h0 = p->d_h0;
     P.tgt = p->d_tgt;
+    P.err = p->d_err;
+    P.err_off = p->d_err_off;
+    P.vs = p->d_vs;
     P.W = p->d_W;
     *out = p;
     return GRAPE_OK;
@@ -330,8 +418,14 @@ void grape_plan_destroy(grape_plan *plan) { free_plan(plan); }
 
 void *grape_plan_stream(grape_plan *plan) { return plan ? (void *)plan->stream : nullptr; }
 
-static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx) {
+static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
+                   double *d_Fd2dx) {
     DevBatch B{};
+    B.Carry = p->d_Carry;
+    B.Ub = p->d_Ub;
+    B.Me = p->d_Me;
+    B.Fd2 = d_Fd2;
+    B.Fd2dx = d_Fd2dx;
     B.nb = nb;
     B.x = d_x;
     B.E = p->d_E;
@@ -379,13 +473,15 @@ static void resolve_events(grape_plan *p) {
 
 int grape_fidelity_grad_device_async(grape_plan *p, int nbatch, const double *d_x, double *d_F, double *d_F_dx,
                                      double *d_F_d2err, double *d_F_d2err_dx) {
-    (void)d_F_d2err;
-    (void)d_F_d2err_dx;
     if (!p || nbatch < 0 || (nbatch > 0 && (!d_x || !d_F || !d_F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (p->P.ne > 0 && nbatch > 0 && (!d_F_d2err || !d_F_d2err_dx))
+        return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     HIPCHECK(hipSetDevice(p->device));
     for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
         const int nb = std::min(p->max_batch, nbatch - b0);
-        int rc = enqueue(p, nb, d_x + (size_t)b0 * p->P.nx, d_F + b0, d_F_dx + (size_t)b0 * p->P.nx);
+        int rc = enqueue(p, nb, d_x + (size_t)b0 * p->P.nx, d_F + b0, d_F_dx + (size_t)b0 * p->P.nx,
+                         p->P.ne ? d_F_d2err + (size_t)b0 * p->P.ne : nullptr,
+                         p->P.ne ? d_F_d2err_dx + (size_t)b0 * p->P.ne * p->P.nx : nullptr);
         if (rc) return rc;
     }
     return GRAPE_OK;
@@ -407,18 +503,25 @@ int grape_plan_synchronize(grape_plan *p) {
 
 int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, double *F_dx, double *F_d2err,
                         double *F_d2err_dx) {
-    (void)F_d2err;
-    (void)F_d2err_dx;
     if (!p || nbatch < 0 || (nbatch > 0 && (!x || !F || !F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (p->P.ne > 0 && nbatch > 0 && (!F_d2err || !F_d2err_dx))
+        return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     HIPCHECK(hipSetDevice(p->device));
     const int nx = p->P.nx;
     for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
         const int nb = std::min(p->max_batch, nbatch - b0);
         HIPCHECK(hipMemcpyAsync(p->d_x, x + (size_t)b0 * nx, (size_t)nb * nx * sizeof(double),
                                 hipMemcpyHostToDevice, p->stream));
-        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx);
+        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx, p->d_Fd2, p->d_Fd2dx);
         if (rc) return rc;
         HIPCHECK(hipMemcpyAsync(F + b0, p->d_F, nb * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        if (p->P.ne > 0) {
+            const int ne = p->P.ne;
+            HIPCHECK(hipMemcpyAsync(F_d2err + (size_t)b0 * ne, p->d_Fd2, (size_t)nb * ne * sizeof(double),
+                                    hipMemcpyDeviceToHost, p->stream));
+            HIPCHECK(hipMemcpyAsync(F_d2err_dx + (size_t)b0 * ne * nx, p->d_Fd2dx,
+                                    (size_t)nb * ne * nx * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        }
         HIPCHECK(hipMemcpyAsync(F_dx + (size_t)b0 * nx, p->d_Fdx, (size_t)nb * nx * sizeof(double),
                                 hipMemcpyDeviceToHost, p->stream));
         rc = grape_plan_synchronize(p);

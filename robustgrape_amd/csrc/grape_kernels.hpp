@@ -38,6 +38,15 @@ struct Pert {
     double delta;
 };
 
+// One propagator variant of a time step: the closure call sites of
+// UnitaryCalculations.jl:45-90 (perturb one variable by delta; optionally add
+// the error Hamiltonian e with strength errval).
+struct VSpec {
+    Pert pert;
+    int err;        // -1: none
+    double errval;
+};
+
 // Everything a kernel needs to know about the problem (passed by value).
 struct DevProblem {
     int D, Nt, np, na, ne, nx;
@@ -45,10 +54,15 @@ struct DevProblem {
     int n_h0, n_tgt;
     int xadd_dep;        // H0 depends on x_add -> x_add FD variants exist
     int L, nchunks;      // scan chunking
-    double dt, eps, eps2, inv_eps, DD;
+    // variant layout (see grape_engine.hip: build_variants)
+    int off_dx, off_dxa, off_dx2, off_err, err_stride;
+    double dt, eps, eps2, inv_eps, inv_eps2sq, DD, Dtr;
     const cd *ops;       // [n_ops][D][D] row-major
     const Term *h0;
     const Term *tgt;
+    const Term *err;     // error-source terms
+    const int *err_off;  // [ne+1]
+    const VSpec *vs;     // [nv]
     const double *W;     // projector diagonal (weights)
 };
 
@@ -62,6 +76,11 @@ struct DevBatch {
     double *Fdx;            // [nb][nx]
     double *part_add;       // [nb][Nt][na]   (xadd_dep only)
     double *tgt_part;       // [nb][na]
+    cd *Carry;              // [nb][nchunks][D][D]  C_{cL-1} (identity for c = 0)
+    cd *Ub;                 // [nb][D][D]           U = C_Nt
+    cd *Me;                 // [nb][ne][nchunks][3][D][D]  M'_{c,e}, T_c, Ttot_c (error path)
+    double *Fd2;            // [nb][ne]
+    double *Fd2dx;          // [nb][ne][nx]
     int *overflow;          // parked m=13 item ids
     int *overflow_count;
     int *status;            // bit 0: singular Pade denominator
@@ -100,38 +119,26 @@ __device__ __forceinline__ void build_row(const cd *ops, const Term *terms, int 
     }
 }
 
-// Variant v of the ne = 0 path: 0 nominal, 1..np control p = v-1 (+eps),
-// then (xadd_dep) x_add q (+eps).
-__device__ __forceinline__ Pert variant_pert(const DevProblem &P, int v) {
-    Pert p;
-    p.var = -1;
-    p.index = 0;
-    p.delta = 0.0;
-    if (v >= 1 && v <= P.np) {
-        p.var = VAR_X;
-        p.index = v - 1;
-        p.delta = P.eps;
-    } else if (v > P.np) {
-        p.var = VAR_XADD;
-        p.index = v - 1 - P.np;
-        p.delta = P.eps;
-    }
-    return p;
-}
-
 // ---------------------------------------------------------------------------
 // k_expm: all propagator variants of the batch
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, bool ERR>
 struct ItemBuilder {  // rebuilds this lane's row of A = -i dt H for one (b, k, v) item
     const DevProblem *P;
     const double *xk, *xadd;
     int i, nt1;
-    Pert pp;
+    VSpec vs;
     bool valid;
     __device__ __forceinline__ void operator()(cd (&a)[D]) const {
         cd h[D];
-        build_row<D>(P->ops, P->h0, P->n_h0, i, nt1, xk, xadd, pp, h);
+        build_row<D>(P->ops, P->h0, P->n_h0, i, nt1, xk, xadd, vs.pert, h);
+        if (ERR && vs.err >= 0) {  // exp(-i dt (Herror(.., err) + H0(..)))   UnitaryCalculations.jl:67-68
+            cd he[D];
+            const int o0 = P->err_off[vs.err], o1 = P->err_off[vs.err + 1];
+            build_row<D>(P->ops, P->err + o0, o1 - o0, i, nt1, xk, xadd, vs.pert, he);
+#pragma unroll
+            for (int j = 0; j < D; ++j) h[j] = cadd(cscale(vs.errval, he[j]), h[j]);
+        }
 #pragma unroll
         for (int j = 0; j < D; ++j) a[j] = valid ? cmake(P->dt * h[j].im, -P->dt * h[j].re) : czero();
     }
@@ -145,7 +152,9 @@ __device__ __forceinline__ void park(Group<D> &G, cd *slot_row, const cd (&a)[D]
     if (G.i == 0) list[atomicAdd(count, 1)] = (int)gid;
 }
 
-template <int D>
+// ERR = false for problems without error sources (keeps the error-term
+// builder, and its registers, out of the common kernel).
+template <int D, bool ERR>
 __global__ __launch_bounds__(64, (D <= 9 ? 3 : 2)) void k_expm(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
@@ -158,8 +167,7 @@ __global__ __launch_bounds__(64, (D <= 9 ? 3 : 2)) void k_expm(DevProblem P, Dev
     const int k = (int)((gidc / P.nv) % P.Nt);
     const int b = (int)(gidc / ((long)P.nv * P.Nt));
     const double *xb = B.x + (size_t)b * P.nx;
-    ItemBuilder<D> rebuild{&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1,
-                           variant_pert(P, v), valid};
+    ItemBuilder<D, ERR> rebuild{&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1, P.vs[v], valid};
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
@@ -394,7 +402,18 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         }
     }
     if (f0 && i == 0) B.F[b] = Fv;
+    if (f0 && B.Ub) {  // U for the error path
+        cd *du = B.Ub + (size_t)b * TILE + i * D;
+#pragma unroll
+        for (int jj = 0; jj < D; ++jj) du[jj] = Ut[i * D + jj];
+    }
     // Phase D: M'_c = Carry_c M Carry_c^dag, Carry_c = P_{c-1} (identity for c = 0)
+    if (gvalid && B.Carry) {  // carries for the error path (identity for chunk 0)
+        cd *dc = B.Carry + ((size_t)b * P.nchunks + c) * TILE + i * D;
+        const cd *Cr = c > 0 ? tile_of(c - 1) : nullptr;
+#pragma unroll
+        for (int jj = 0; jj < D; ++jj) dc[jj] = Cr ? Cr[i * D + jj] : cmake(jj == i ? 1.0 : 0.0, 0.0);
+    }
     if (gvalid) {
         cd mc[D];
         if (c == 0) {
@@ -457,7 +476,9 @@ __global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, Dev
     cd e0[D];
 #pragma unroll
     for (int jj = 0; jj < D; ++jj) e0[jj] = E0[jj];
-    for (int v = 1; v < P.nv; ++v) {
+    const int nvg = P.np + (P.xadd_dep ? P.na : 0);  // dx then dxa variants are contiguous
+    for (int vi = 0; vi < nvg; ++vi) {
+        const int v = P.off_dx + vi;
         const cd *Ev = E0 + (size_t)v * TILE;
         double s = 0.0;
 #pragma unroll
@@ -467,8 +488,8 @@ __global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, Dev
         }
         s = group_sum(G, s, valid);
         if (valid && i == 0) {
-            if (v <= P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + (v - 1)] = s;
-            else B.part_add[((size_t)b * P.Nt + k) * P.na + (v - 1 - P.np)] = s;
+            if (vi < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + vi] = s;
+            else B.part_add[((size_t)b * P.Nt + k) * P.na + (vi - P.np)] = s;
         }
     }
 }

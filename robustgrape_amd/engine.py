@@ -81,8 +81,9 @@ class GrapePlan:
 
     def kernel_times(self, reset: bool = False):
         """{kernel name: (total ms, launches)} accumulated while profiling was on."""
-        ms = (ctypes.c_double * 5)()
-        n = (ctypes.c_longlong * 5)()
+        nk = len(_capi.KERNEL_NAMES)
+        ms = (ctypes.c_double * nk)()
+        n = (ctypes.c_longlong * nk)()
         _capi.check(_capi.lib().grape_plan_kernel_times(self.handle, ms, n, int(reset)))
         return {name: (ms[k], n[k]) for k, name in enumerate(_capi.KERNEL_NAMES)}
 

@@ -130,3 +130,73 @@ def test_errors_are_loud():
         calculate_fidelity_and_derivatives(P.full9_problem(64), np.zeros(64 + 2))
     with pytest.raises(TypeError):
         calculate_fidelity_and_derivatives(P.sym_problem(8, device=False), np.zeros(9))
+
+
+# ---------------------------------------------------------------- error sources (C3)
+T3, T3_ABS, T3_XADD_ABS = 1e-5, 1e-7, 1e-5
+
+
+def _assert_err(fp, d2, d2dx, ref_d2, ref_d2dx):
+    nmain = d2dx.shape[0] - fp.unitary_problem.nb_additional_param
+    assert np.max(np.abs(d2 - ref_d2)) <= T3 * np.max(np.abs(ref_d2)) + T3_ABS, (d2, ref_d2)
+    err = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain]))
+    assert err <= T3 * np.max(np.abs(ref_d2dx[:nmain])) + T3_ABS, err
+    assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
+
+
+@pytest.mark.parametrize("name,builder", [
+    ("c1err", lambda: P.sym_problem(500, t0=P.T0_TO, errors=("amp", "freq"))),
+    ("d7err", lambda: P.fullblk_problem(500, errors=("amp", "freq"))),
+    ("c3n64", lambda: P.full9_problem(64, nerr=4)),
+    ("c3", lambda: P.full9_problem(512, nerr=4)),
+])
+def test_error_sensitivities_match_golden(name, builder):
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    g = _golden(name)
+    fp = builder()
+    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(fp, g["x"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    _assert_err(fp, d2, d2dx, g["F_d2err"], g["F_d2err_dx"])
+
+
+@pytest.mark.parametrize("d,ntimes,errors", [(5, 1, ("amp",)), (5, 9, ("amp", "freq")), (7, 20, ("freq",)),
+                                            (9, 3, 2), (9, 61, 4)])
+def test_error_path_small_problems_match_live_oracle(d, ntimes, errors):
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    if d == 5:
+        mk = lambda dev: P.sym_problem(ntimes, errors=errors, device=dev)
+    elif d == 7:
+        mk = lambda dev: P.fullblk_problem(ntimes, errors=errors, device=dev)
+    else:
+        mk = lambda dev: P.full9_problem(ntimes, nerr=errors, device=dev)
+    x = P.random_x(ntimes, 200 + ntimes)
+    F0, g0, d20, d2dx0 = O.calculate_fidelity_and_derivatives(mk(False), x)
+    fp = mk(True)
+    F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0)
+    _assert_err(fp, d2, d2dx, d20, d2dx0)
+
+
+def test_error_sensitivity_gradient_identity_on_gpu():
+    """runtests.jl:48-113 on the device path: (F_d2err(x + 1e-4 e_i) - F_d2err(x))/1e-4 vs F_d2err_dx[i]."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = P.sym_problem(200, errors=("amp",))
+    rng = np.random.default_rng(42)
+    for idx in (int(rng.integers(200)), 200):
+        xs = 2 * np.pi * rng.uniform(size=201)
+        _, _, d0, d0dx = calculate_fidelity_and_derivatives(fp, xs)
+        xs[idx] += 1e-4
+        _, _, d1, _ = calculate_fidelity_and_derivatives(fp, xs)
+        np.testing.assert_allclose((d1[0] - d0[0]) / 1e-4, d0dx[idx, 0], rtol=1e-3, atol=1e-5)
+
+
+def test_error_batch_matches_single():
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = P.full9_problem(40, nerr=4)
+    X = np.stack([P.random_x(40, s) for s in range(5)])
+    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(fp, X)
+    for b in (0, 4):
+        Fs, gs, d2s, d2dxs = calculate_fidelity_and_derivatives(fp, X[b])
+        assert Fs == F[b] and np.array_equal(gs, Fdx[b])
+        assert np.array_equal(d2s, d2[b]) and np.array_equal(d2dxs, d2dx[b])
