@@ -189,11 +189,13 @@ typedef enum grape_kernel {
     GRAPE_KERNEL_EXPM = 0,      /* propagators of every FD variant (Pade m <= 5) */
     GRAPE_KERNEL_EXPM_HIGH = 1, /* Pade m = 7/9/13 items parked by the above */
     GRAPE_KERNEL_SCAN = 2,      /* chunked prefix products, fidelity, gradient kernels */
-    GRAPE_KERNEL_GRAD = 3,      /* per-step gradient contractions */
+    GRAPE_KERNEL_GRAD = 3,      /* per-step gradient contractions (error-source pipeline) */
     GRAPE_KERNEL_REDUCE = 4,    /* x_add reductions */
     GRAPE_KERNEL_ERR_SCAN = 5,  /* error sources: U_derr, F_d2err, per-chunk kernels */
     GRAPE_KERNEL_ERR_GRAD = 6,  /* error sources: F_d2err_dx contractions */
-    GRAPE_NUM_KERNELS = 7
+    GRAPE_KERNEL_EXPM_GRAD = 7, /* no error sources: eps-variant propagators contracted in place */
+    GRAPE_KERNEL_GRAD_HIGH = 8, /* Pade m > 5 items parked by the above */
+    GRAPE_NUM_KERNELS = 9
 } grape_kernel;
 
 int grape_plan_set_profiling(grape_plan *plan, int enable);

@@ -10,7 +10,7 @@ import os
 from .operators import CDesc
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgrape.so")
+LIB_PATH = os.environ.get("GRAPE_LIB") or os.path.join(HERE, "libgrape.so")
 
 GRAPE_OK = 0
 STATUS_NAMES = {-1: "GRAPE_ERR_INVALID", -2: "GRAPE_ERR_UNSUPPORTED", -3: "GRAPE_ERR_ALLOC",
@@ -21,7 +21,8 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_plan_destroy", "grape_plan_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times"]
-KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad"]
+KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
+                "k_expm_grad", "k_grad_high"]
 
 
 class GrapeError(RuntimeError):

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrape.so")
 SOURCES = [os.path.join(CSRC, "grape_engine.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("grape_device.hpp", "grape_kernels.hpp")] + \
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -35,16 +35,17 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
 
 
-def build_library(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
+def build_library(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
+    """Build libgrape.so (or a variant with extra -D defines into `out`, for tuning runs)."""
+    if out == LIB and not defines and not force and not needs_build():
         return LIB
-    tmp = LIB + ".tmp"
-    cmd = [HIPCC] + FLAGS + SOURCES + ["-o", tmp]
+    tmp = out + ".tmp"
+    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + SOURCES + ["-o", tmp]
     if verbose:
-        print("[robustgrape_amd] building", os.path.relpath(LIB, ROOT), flush=True)
+        print("[robustgrape_amd] building", os.path.relpath(out, ROOT), *defines, flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

@@ -41,7 +41,10 @@ int fail(int code, const std::string &msg) {
             return fail(GRAPE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kScanWaves = 8;
+#ifndef GRAPE_SCAN_WAVES
+#define GRAPE_SCAN_WAVES 8
+#endif
+constexpr int kScanWaves = GRAPE_SCAN_WAVES;
 
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
@@ -72,8 +75,9 @@ template <int D>
 hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mark) {
     constexpr int GPW = grape::Geo<D>::GPW;
     const long nexp = (long)B.nb * P.Nt * P.nv;
+    const bool fused = P.ne == 0;  // eps-variants exp'd and contracted in k_expm_grad
     mark(GRAPE_KERNEL_EXPM, 0);
-    if (P.ne > 0)
+    if (!fused)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lds<D>(), st, P, B);
     else
@@ -82,17 +86,29 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     mark(GRAPE_KERNEL_EXPM, 1);
     mark(GRAPE_KERNEL_EXPM_HIGH, 0);
     hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
-                       B.overflow_count, B.status);
+                       B.overflow_count, B.status, 1);
     mark(GRAPE_KERNEL_EXPM_HIGH, 1);
     mark(GRAPE_KERNEL_SCAN, 0);
     hipLaunchKernelGGL((grape::k_scan<D, kScanWaves>), dim3(B.nb), dim3(64 * kScanWaves), scan_lds<D>(), st, P,
                        B);
     mark(GRAPE_KERNEL_SCAN, 1);
-    const long ng = (long)B.nb * P.Nt;
-    mark(GRAPE_KERNEL_GRAD, 0);
-    hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st, P,
-                       B);
-    mark(GRAPE_KERNEL_GRAD, 1);
+    if (fused) {
+        const int nvg = P.np + (P.xadd_dep ? P.na : 0);
+        const long ng = (long)B.nb * P.Nt * nvg;
+        mark(GRAPE_KERNEL_EXPM_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(),
+                           st, P, B);
+        mark(GRAPE_KERNEL_EXPM_GRAD, 1);
+        mark(GRAPE_KERNEL_GRAD_HIGH, 0);
+        hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_GRAD_HIGH, 1);
+    } else {
+        const long ng = (long)B.nb * P.Nt;
+        mark(GRAPE_KERNEL_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
+                           P, B);
+        mark(GRAPE_KERNEL_GRAD, 1);
+    }
     if (P.ne > 0) {
         mark(GRAPE_KERNEL_ERR_SCAN, 0);
         hipLaunchKernelGGL((grape::k_err_scan<D, kScanWaves>), dim3(B.nb * P.ne), dim3(64 * kScanWaves),
@@ -113,15 +129,12 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
 }
 
 template <int D>
-hipError_t launch_expm_raw(const cd *A, cd *Erm, cd *Ecm, int n, int *ovf, int *ovf_count, int *status,
-                           int *mstats, hipStream_t st) {
+hipError_t launch_expm_raw(const cd *A, cd *E, int n, int *ovf, int *ovf_count, int *status, int *mstats,
+                           hipStream_t st) {
     constexpr int GPW = grape::Geo<D>::GPW;
-    hipLaunchKernelGGL(grape::k_expm_raw<D>, dim3((n + GPW - 1) / GPW), dim3(64), expm_lds<D>(), st, A, Erm, n,
-                       ovf, ovf_count, status, mstats);
-    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, Erm, ovf, ovf_count, status);
-    const long tot = (long)n * D * D;
-    hipLaunchKernelGGL(grape::k_transpose_tiles<D>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, Erm, Ecm,
-                       n);
+    hipLaunchKernelGGL(grape::k_expm_raw<D>, dim3((n + GPW - 1) / GPW), dim3(64), expm_lds<D>(), st, A, E, n, ovf,
+                       ovf_count, status, mstats);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, E, ovf, ovf_count, status, 0);
     return hipGetLastError();
 }
 
@@ -145,11 +158,11 @@ hipError_t dispatch_pipeline(int D, const DevProblem &P, const DevBatch &B, hipS
     }
     return hipErrorInvalidValue;
 }
-hipError_t dispatch_expm_raw(int D, const cd *A, cd *Erm, cd *Ecm, int n, int *ovf, int *ovfc, int *status,
+hipError_t dispatch_expm_raw(int D, const cd *A, cd *E, int n, int *ovf, int *ovfc, int *status,
                              int *mstats, hipStream_t st) {
     switch (D) {
 #define CASE(d) \
-    case d: return launch_expm_raw<d>(A, Erm, Ecm, n, ovf, ovfc, status, mstats, st);
+    case d: return launch_expm_raw<d>(A, E, n, ovf, ovfc, status, mstats, st);
         GRAPE_DIMS(CASE)
 #undef CASE
     }
@@ -181,11 +194,14 @@ struct grape_plan {
     int max_batch = 0;
     // device buffers
     cd *d_ops = nullptr;
+    cd *d_opsT = nullptr;
     Term *d_h0 = nullptr, *d_tgt = nullptr, *d_err = nullptr;
     int *d_err_off = nullptr;
     double *d_W = nullptr;
     cd *d_E = nullptr, *d_Q = nullptr, *d_Mc = nullptr, *d_Carry = nullptr, *d_Ub = nullptr, *d_Me = nullptr;
     grape::VSpec *d_vs = nullptr;
+    int *d_ovf2 = nullptr;
+    cd *d_ovf2_slots = nullptr;
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0] overflow count, [1] status
@@ -214,9 +230,9 @@ struct grape_plan {
 static void free_plan(grape_plan *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
-    void *bufs[] = {p->d_ops, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
+    void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl,
-                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx};
+                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -353,7 +369,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         addv(-1, 0, 0.0, e, desc->eps2);
         for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps2, e, desc->eps2);
     }
-    P.nv = (int)vs.size();
+    // E stores every variant for the error-source pipeline; without error sources
+    // only the nominal propagators are stored (k_expm_grad consumes the rest in place)
+    P.nv = desc->nerr > 0 ? (int)vs.size() : 1;
     P.dt = desc->t0 / desc->ntimes;
     P.eps = desc->eps;
     P.eps2 = desc->eps2;
@@ -366,16 +384,19 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.L = (P.Nt + nc0 - 1) / nc0;
     P.nchunks = (P.Nt + P.L - 1) / P.L;
 
-    // operator basis: column-major interleaved -> row-major cd tiles
-    std::vector<cd> ops((size_t)desc->n_ops * D * D);
+    // operator basis: column-major interleaved -> row-major cd tiles (row builds)
+    // and column-major ones (the exp kernels build columns)
+    std::vector<cd> ops((size_t)desc->n_ops * D * D), opsT(ops.size());
     for (int o = 0; o < desc->n_ops; ++o)
         for (int r = 0; r < D; ++r)
             for (int c = 0; c < D; ++c) {
                 const double *src = desc->ops + 2 * ((size_t)o * D * D + r + (size_t)c * D);
                 ops[(size_t)o * D * D + r * D + c] = cd{src[0], src[1]};
+                opsT[(size_t)o * D * D + c * D + r] = cd{src[0], src[1]};
             }
     const size_t MB = p->max_batch, T = (size_t)D * D;
-    bool ok = dalloc(&p->d_ops, ops.size()) == hipSuccess && dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
+    bool ok = dalloc(&p->d_ops, ops.size()) == hipSuccess && dalloc(&p->d_opsT, opsT.size()) == hipSuccess &&
+              dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
               dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess && dalloc(&p->d_W, (size_t)D) == hipSuccess &&
               dalloc(&p->d_E, MB * P.Nt * P.nv * T) == hipSuccess && dalloc(&p->d_Q, MB * P.Nt * T) == hipSuccess &&
               dalloc(&p->d_Mc, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
@@ -384,6 +405,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
               dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, 4) == hipSuccess &&
               dalloc(&p->d_vs, vs.size()) == hipSuccess;
+    const int nvg = P.np + (P.xadd_dep ? P.na : 0);
+    if (ok && P.ne == 0)
+        ok = dalloc(&p->d_ovf2, MB * P.Nt * nvg) == hipSuccess &&
+             dalloc(&p->d_ovf2_slots, MB * P.Nt * nvg * T) == hipSuccess;
     if (ok && P.ne > 0)
         ok = dalloc(&p->d_Carry, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, MB * T) == hipSuccess &&
              dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
@@ -398,12 +423,14 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
              hipSuccess))
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     if (hipMemcpy(p->d_ops, ops.data(), ops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_opsT, opsT.data(), opsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
             hipSuccess ||
         hipMemcpy(p->d_W, desc->projector_diag, D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     P.ops = p->d_ops;
+    P.opsT = p->d_opsT;
     P.h0 = p->d_h0;
     P.tgt = p->d_tgt;
     P.err = p->d_err;
@@ -438,7 +465,12 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     B.overflow = p->d_ovf;
     B.overflow_count = p->d_ctrl;
     B.status = p->d_ctrl + 1;
-    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, sizeof(int), p->stream));  // overflow count (status is sticky)
+    B.ovf2 = p->d_ovf2;
+    B.ovf2_count = p->d_ctrl + 2;
+    B.ovf2_slots = p->d_ovf2_slots;
+    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, sizeof(int), p->stream));      // k_expm overflow count
+    HIPCHECK(hipMemsetAsync(p->d_ctrl + 2, 0, sizeof(int), p->stream));  // k_expm_grad overflow count
+    // (ctrl[1], the status word, is sticky until grape_plan_synchronize reports it)
     KMark mk;
     if (p->profiling) {
         mk.ctx = p;
@@ -563,12 +595,12 @@ int grape_expm_batch(int device, int ndim, int n, const double *A, double *E, in
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GRAPE_ERR_NO_DEVICE, "no HIP device");
     HIPCHECK(hipSetDevice(device));
     const size_t T = (size_t)ndim * ndim;
-    cd *dA = nullptr, *dErm = nullptr, *dEcm = nullptr;
+    cd *dA = nullptr, *dE = nullptr;
     int *dovf = nullptr, *dctrl = nullptr;
     auto cleanup = [&]() {
-        (void)hipFree(dA); (void)hipFree(dErm); (void)hipFree(dEcm); (void)hipFree(dovf); (void)hipFree(dctrl);
+        (void)hipFree(dA); (void)hipFree(dE); (void)hipFree(dovf); (void)hipFree(dctrl);
     };
-    if (dalloc(&dA, n * T) || dalloc(&dErm, n * T) || dalloc(&dEcm, n * T) || dalloc(&dovf, (size_t)n) ||
+    if (dalloc(&dA, n * T) || dalloc(&dE, n * T) || dalloc(&dovf, (size_t)n) ||
         dalloc(&dctrl, 8)) {
         cleanup();
         return fail(GRAPE_ERR_ALLOC, "device allocation failed");
@@ -577,9 +609,9 @@ int grape_expm_batch(int device, int ndim, int n, const double *A, double *E, in
     int ctrl[8] = {0};
     if (hipMemcpy(dA, A, n * T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(dctrl, 0, 8 * sizeof(int)) != hipSuccess ||
-        dispatch_expm_raw(ndim, dA, dErm, dEcm, n, dovf, dctrl, dctrl + 1, dctrl + 2, nullptr) != hipSuccess ||
+        dispatch_expm_raw(ndim, dA, dE, n, dovf, dctrl, dctrl + 1, dctrl + 2, nullptr) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(E, dEcm, n * T * sizeof(cd), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(E, dE, n * T * sizeof(cd), hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(ctrl, dctrl, 8 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
         rc = fail(GRAPE_ERR_HIP, std::string("expm batch failed: ") + hipGetErrorString(hipGetLastError()));
     cleanup();

@@ -58,6 +58,7 @@ struct DevProblem {
     int off_dx, off_dxa, off_dx2, off_err, err_stride;
     double dt, eps, eps2, inv_eps, inv_eps2sq, DD, Dtr;
     const cd *ops;       // [n_ops][D][D] row-major
+    const cd *opsT;      // [n_ops][D][D] column-major (column builds for the exp kernels)
     const Term *h0;
     const Term *tgt;
     const Term *err;     // error-source terms
@@ -81,8 +82,11 @@ struct DevBatch {
     cd *Me;                 // [nb][ne][nchunks][3][D][D]  M'_{c,e}, T_c, Ttot_c (error path)
     double *Fd2;            // [nb][ne]
     double *Fd2dx;          // [nb][ne][nx]
-    int *overflow;          // parked m=13 item ids
+    int *overflow;          // parked (Pade m > 5) item ids of k_expm
     int *overflow_count;
+    int *ovf2;              // parked item ids of k_expm_grad
+    int *ovf2_count;
+    cd *ovf2_slots;         // [nb][Nt][nvg][D][D]  A of parked k_expm_grad items
     int *status;            // bit 0: singular Pade denominator
 };
 
@@ -122,20 +126,64 @@ __device__ __forceinline__ void build_row(const cd *ops, const Term *terms, int 
 // ---------------------------------------------------------------------------
 // k_expm: all propagator variants of the batch
 // ---------------------------------------------------------------------------
+// Rebuilds this lane's COLUMN of A = -i dt H for one (b, k, v) item.  The scalar
+// coefficients (the trig of the controls) are evaluated once and cached in
+// registers (up to kCachedTerms per operator set); the row is then a short
+// sum of cached coefficient x operator-row products, cheap enough to redo
+// instead of keeping A live through the Pade evaluation.
+constexpr int kCachedTerms = 6;
+
 template <int D, bool ERR>
-struct ItemBuilder {  // rebuilds this lane's row of A = -i dt H for one (b, k, v) item
+struct ItemBuilder {
     const DevProblem *P;
     const double *xk, *xadd;
     int i, nt1;
     VSpec vs;
     bool valid;
+    cd c0[kCachedTerms], ce[kCachedTerms];
+    int o0, ne_t;
+
+    __device__ __forceinline__ ItemBuilder(const DevProblem *P_, const double *xk_, const double *xadd_, int i_,
+                                           int nt1_, const VSpec &vs_, bool valid_)
+        : P(P_), xk(xk_), xadd(xadd_), i(i_), nt1(nt1_), vs(vs_), valid(valid_), o0(0), ne_t(0) {
+#pragma unroll
+        for (int t = 0; t < kCachedTerms; ++t)
+            c0[t] = (t < P->n_h0) ? term_coef(P->h0[t], nt1, xk, xadd, vs.pert) : czero();
+        if (ERR && vs.err >= 0) {
+            o0 = P->err_off[vs.err];
+            ne_t = P->err_off[vs.err + 1] - o0;
+#pragma unroll
+            for (int t = 0; t < kCachedTerms; ++t)
+                ce[t] = (t < ne_t) ? term_coef(P->err[o0 + t], nt1, xk, xadd, vs.pert) : czero();
+        }
+    }
+
+    __device__ __forceinline__ void accumulate(const Term *terms, int n, const cd (&cache)[kCachedTerms],
+                                               cd (&h)[D]) const {
+#pragma unroll
+        for (int j = 0; j < D; ++j) h[j] = czero();
+#pragma unroll
+        for (int t = 0; t < kCachedTerms; ++t) {
+            if (t < n) {
+                const cd *op = P->opsT + (size_t)terms[t].op * D * D + i * D;
+#pragma unroll
+                for (int j = 0; j < D; ++j) h[j] = cadd(h[j], cmul(cache[t], op[j]));
+            }
+        }
+        for (int t = kCachedTerms; t < n; ++t) {  // rare: more terms than cached
+            const cd c = term_coef(terms[t], nt1, xk, xadd, vs.pert);
+            const cd *op = P->opsT + (size_t)terms[t].op * D * D + i * D;
+#pragma unroll
+            for (int j = 0; j < D; ++j) h[j] = cadd(h[j], cmul(c, op[j]));
+        }
+    }
+
     __device__ __forceinline__ void operator()(cd (&a)[D]) const {
         cd h[D];
-        build_row<D>(P->ops, P->h0, P->n_h0, i, nt1, xk, xadd, vs.pert, h);
+        accumulate(P->h0, P->n_h0, c0, h);
         if (ERR && vs.err >= 0) {  // exp(-i dt (Herror(.., err) + H0(..)))   UnitaryCalculations.jl:67-68
             cd he[D];
-            const int o0 = P->err_off[vs.err], o1 = P->err_off[vs.err + 1];
-            build_row<D>(P->ops, P->err + o0, o1 - o0, i, nt1, xk, xadd, vs.pert, he);
+            accumulate(P->err + o0, ne_t, ce, he);
 #pragma unroll
             for (int j = 0; j < D; ++j) h[j] = cadd(cscale(vs.errval, he[j]), h[j]);
         }
@@ -144,7 +192,8 @@ struct ItemBuilder {  // rebuilds this lane's row of A = -i dt H for one (b, k, 
     }
 };
 
-// Parks an item whose Pade degree is > 5: A goes to its output slot, the id to the list.
+// Parks an item whose Pade degree is > 5: A (column i at slot + i*D) goes to
+// its output slot, the id to the list.
 template <int D>
 __device__ __forceinline__ void park(Group<D> &G, cd *slot_row, const cd (&a)[D], long gid, int *list, int *count) {
 #pragma unroll
@@ -154,8 +203,11 @@ __device__ __forceinline__ void park(Group<D> &G, cd *slot_row, const cd (&a)[D]
 
 // ERR = false for problems without error sources (keeps the error-term
 // builder, and its registers, out of the common kernel).
+#ifndef GRAPE_EXPM_WAVES_D9
+#define GRAPE_EXPM_WAVES_D9 3   // waves per SIMD requested for d <= 9 (register budget 512/w)
+#endif
 template <int D, bool ERR>
-__global__ __launch_bounds__(64, (D <= 9 ? 3 : 2)) void k_expm(DevProblem P, DevBatch B) {
+__global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     Group<D> G = make_group<D>(lds, threadIdx.x);
@@ -167,27 +219,31 @@ __global__ __launch_bounds__(64, (D <= 9 ? 3 : 2)) void k_expm(DevProblem P, Dev
     const int k = (int)((gidc / P.nv) % P.Nt);
     const int b = (int)(gidc / ((long)P.nv * P.Nt));
     const double *xb = B.x + (size_t)b * P.nx;
-    ItemBuilder<D, ERR> rebuild{&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1, P.vs[v], valid};
+    const ItemBuilder<D, ERR> rebuild(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1, P.vs[v],
+                                      valid);
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
     const int m = expm_prologue<D>(G, a, x, valid, s);
     cd *out = B.E + (size_t)gidc * D * D + G.i * D;
+    if (m > 5) {  // group-uniform: A (columns) to the slot, exp'd by k_expm_high
+        if (valid) park<D>(G, out, a, gid, B.overflow, B.overflow_count);
+        return;
+    }
     if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
+    transpose_group<D>(G, x, valid);  // E is stored row-major
     if (valid) {
-        if (m > 5) {
-            park<D>(G, out, a, gid, B.overflow, B.overflow_count);
-        } else {
 #pragma unroll
-            for (int j = 0; j < D; ++j) out[j] = x[j];
-        }
+        for (int j = 0; j < D; ++j) out[j] = x[j];
         if (singular) atomicOr(B.status, 1);
     }
 }
 
-// Items parked by k_expm / k_expm_raw (slots hold A, overwritten with exp(A)).
+// Items parked by k_expm / k_expm_raw (slots hold A column-major, overwritten
+// with exp(A): row-major for the pipeline, column-major for grape_expm_batch).
 template <int D>
-__global__ __launch_bounds__(64) void k_expm_high(cd *slots, const int *list, const int *count, int *status) {
+__global__ __launch_bounds__(64) void k_expm_high(cd *slots, const int *list, const int *count, int *status,
+                                                  int rows_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     Group<D> G = make_group<D>(lds, threadIdx.x);
@@ -203,6 +259,7 @@ __global__ __launch_bounds__(64) void k_expm_high(cd *slots, const int *list, co
         const int m = expm_prologue<D>(G, a, x, valid, s);
         if (m > 0) expm_high<D>(G, m, s, a, x, valid, singular);
         gsync();
+        if (rows_out) transpose_group<D>(G, x, valid);
         if (valid) {
 #pragma unroll
             for (int j = 0; j < D; ++j) slot[j] = x[j];
@@ -211,8 +268,8 @@ __global__ __launch_bounds__(64) void k_expm_high(cd *slots, const int *list, co
     }
 }
 
-// Standalone batched expm of column-major matrices (grape_expm_batch); writes
-// row-major tiles that k_transpose_tiles turns back into column-major.
+// Standalone batched expm of column-major matrices (grape_expm_batch): lane i
+// loads column i and stores column i of the result (column-major in and out).
 template <int D>
 __global__ __launch_bounds__(64) void k_expm_raw(const cd *A, cd *E, int n, int *overflow, int *overflow_count,
                                                  int *status, int *mstats) {
@@ -221,10 +278,10 @@ __global__ __launch_bounds__(64) void k_expm_raw(const cd *A, cd *E, int n, int 
     Group<D> G = make_group<D>(lds, threadIdx.x);
     const int gid = blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < n;
-    const cd *src = A + (size_t)(valid ? gid : 0) * D * D;
+    const cd *src = A + (size_t)(valid ? gid : 0) * D * D + G.i * D;
     auto reload = [&](cd (&a)[D]) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) a[j] = valid ? src[G.i + j * D] : czero();
+        for (int j = 0; j < D; ++j) a[j] = valid ? src[j] : czero();
     };
     cd a[D], x[D];
     reload(a);
@@ -245,15 +302,6 @@ __global__ __launch_bounds__(64) void k_expm_raw(const cd *A, cd *E, int n, int 
         }
         if (singular) atomicOr(status, 1);
     }
-}
-
-template <int D>
-__global__ void k_transpose_tiles(const cd *in, cd *out, int n) {  // row-major -> column-major
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long)n * D * D) return;
-    const long m = t / (D * D);
-    const int r = (int)(t % (D * D)) / D, c = (int)(t % (D * D)) % D;
-    out[m * D * D + r + c * D] = in[m * D * D + r * D + c];
 }
 
 // ---------------------------------------------------------------------------
@@ -280,32 +328,51 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     // Phase A: local inclusive chain Q_k = E_k ... E_{cL}
     cd q[D], e[D], t[D];
     const int k0 = c * P.L;
+    auto load_e = [&](int k, cd (&dst)[D]) {
+        const bool ok = gvalid && k < P.Nt;
+        const cd *src = Eb + ((size_t)(ok ? k : 0) * P.nv) * TILE + i * D;
+#pragma unroll
+        for (int jj = 0; jj < D; ++jj) dst[jj] = ok ? src[jj] : czero();
+    };
+    load_e(k0, e);
+#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 0
+    return;
+#endif
     for (int j = 0; j < P.L; ++j) {
         const int k = k0 + j;
         const bool act = gvalid && k < P.Nt;
-        if (act) {
-            const cd *src = Eb + ((size_t)k * P.nv) * TILE + i * D;
-#pragma unroll
-            for (int jj = 0; jj < D; ++jj) e[jj] = src[jj];
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < D; ++jj) e[jj] = czero();
-        }
+        cd en[D];
+#ifndef GRAPE_DIAG_NOLOAD
+        load_e(k + 1, en);  // prefetch the next step's propagator row behind this product
+#else
+        for (int jj = 0; jj < D; ++jj) en[jj] = cscale(1.0000001, e[jj]);
+#endif
         if (j == 0) {
 #pragma unroll
             for (int jj = 0; jj < D; ++jj) q[jj] = e[jj];
         } else {
+#ifndef GRAPE_DIAG_NOMM
             mm_tile<D>(e, G.tile, q);
+#else
+            for (int jj = 0; jj < D; ++jj) q[jj] = cadd(e[jj], G.tile[i * D + jj]);
+#endif
         }
         gsync();
         if (act) {
             tile_store_row(G, q, true);
+#ifndef GRAPE_DIAG_NOSTORE
             cd *dst = Qb + (size_t)k * TILE + i * D;
 #pragma unroll
             for (int jj = 0; jj < D; ++jj) dst[jj] = q[jj];
+#endif
         }
         gsync();
+#pragma unroll
+        for (int jj = 0; jj < D; ++jj) e[jj] = en[jj];
     }
+#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 1
+    return;
+#endif
     // Phase B: inclusive scan of the chunk totals, P_c = T_c ... T_0 (Hillis-Steele)
     for (int o = 1; o < P.nchunks; o <<= 1) {
         const bool doit = gvalid && c >= o;
@@ -318,6 +385,9 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         if (doit) tile_store_row(G, t, true);
         gsync();
     }
+#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 2
+    return;
+#endif
     // Phase C: fidelity and M = G U on group 0 (everyone keeps the barrier sequence)
     const bool f0 = (c == 0) && G.lane_ok;
     const cd *Ut = tile_of(P.nchunks - 1);
@@ -407,6 +477,9 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) du[jj] = Ut[i * D + jj];
     }
+#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 3
+    return;
+#endif
     // Phase D: M'_c = Carry_c M Carry_c^dag, Carry_c = P_{c-1} (identity for c = 0)
     if (gvalid && B.Carry) {  // carries for the error path (identity for chunk 0)
         cd *dc = B.Carry + ((size_t)b * P.nchunks + c) * TILE + i * D;
@@ -433,24 +506,19 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 }
 
 // ---------------------------------------------------------------------------
-// k_grad: one row group per (b, k)
+// Gradient contraction.  Row i of Z_k = Y_k^T with Y_k = C_{k-1} M C_k^dag
+// = Q_{k-1} M'_c Q_k^dag:  Z_k = conj(Q_k) M'^T Q_{k-1}^T  (Q_{k-1} = I at a
+// chunk start), so that F_dx[p,k] = Re tr(Y_k dE) = Re sum_ij Z_ij dE_ij.
 // ---------------------------------------------------------------------------
 template <int D>
-__global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, DevBatch B) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    cd *lds = reinterpret_cast<cd *>(smem_raw);
+__device__ __forceinline__ void grad_kernel_row(Group<D> &G, const DevProblem &P, const DevBatch &B, int b, int k,
+                                                bool valid, cd (&z)[D]) {
     constexpr int TILE = Geo<D>::TILE;
-    Group<D> G = make_group<D>(lds, threadIdx.x);
-    const long nitems = (long)B.nb * P.Nt;
-    const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
-    const bool valid = G.lane_ok && gid < nitems;
-    const long gidc = valid ? gid : 0;
-    const int k = (int)(gidc % P.Nt), b = (int)(gidc / P.Nt);
     const int c = k / P.L, j0 = k - c * P.L;
     const int i = G.i;
     const cd *Qk = B.Q + ((size_t)b * P.Nt + k) * TILE;
     const cd *Mc = B.Mc + ((size_t)b * P.nchunks + c) * TILE;
-    cd ql[D], t[D], z[D];
+    cd ql[D], t[D];
 #pragma unroll
     for (int jj = 0; jj < D; ++jj) ql[jj] = cconj(Qk[i * D + jj]);
     if (valid) {
@@ -472,25 +540,119 @@ __global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, Dev
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) z[jj] = t[jj];
     }
-    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + i * D;
-    cd e0[D];
+}
+
+// Group-summed Re sum_j z_j * (ev_j - e0_j) * inv_eps, written to F_dx (control
+// variant u < np) or to the per-step x_add partial (u >= np).
+template <int D>
+__device__ __forceinline__ void grad_store(Group<D> &G, const DevProblem &P, const DevBatch &B, int b, int k, int u,
+                                           const cd (&z)[D], const cd (&ev)[D], const cd *e0, bool valid) {
+    double s = 0.0;
 #pragma unroll
-    for (int jj = 0; jj < D; ++jj) e0[jj] = E0[jj];
+    for (int jj = 0; jj < D; ++jj) {
+        const cd de = cscale(P.inv_eps, csub(ev[jj], e0[jj]));  // (1/eps) * (E' - E)
+        s += z[jj].re * de.re - z[jj].im * de.im;
+    }
+    s = group_sum(G, s, valid);
+    if (valid && G.i == 0) {
+        if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+        else B.part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
+    }
+}
+
+// k_grad: one row group per (b, k), variants read back from E (error-source pipeline)
+template <int D>
+__global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, DevBatch B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    cd *lds = reinterpret_cast<cd *>(smem_raw);
+    constexpr int TILE = Geo<D>::TILE;
+    Group<D> G = make_group<D>(lds, threadIdx.x);
+    const long nitems = (long)B.nb * P.Nt;
+    const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
+    const bool valid = G.lane_ok && gid < nitems;
+    const long gidc = valid ? gid : 0;
+    const int k = (int)(gidc % P.Nt), b = (int)(gidc / P.Nt);
+    cd z[D];
+    grad_kernel_row<D>(G, P, B, b, k, valid, z);
+    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i * D;
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);  // dx then dxa variants are contiguous
-    for (int vi = 0; vi < nvg; ++vi) {
-        const int v = P.off_dx + vi;
-        const cd *Ev = E0 + (size_t)v * TILE;
-        double s = 0.0;
+    for (int u = 0; u < nvg; ++u) {
+        const cd *Ev = E0 + (size_t)(P.off_dx + u) * TILE;
+        cd ev[D];
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) {
-            const cd de = cscale(P.inv_eps, csub(Ev[jj], e0[jj]));
-            s += z[jj].re * de.re - z[jj].im * de.im;
-        }
-        s = group_sum(G, s, valid);
-        if (valid && i == 0) {
-            if (vi < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + vi] = s;
-            else B.part_add[((size_t)b * P.Nt + k) * P.na + (vi - P.np)] = s;
-        }
+        for (int jj = 0; jj < D; ++jj) ev[jj] = Ev[jj];
+        grad_store<D>(G, P, B, b, k, u, z, ev, E0, valid);
+    }
+}
+
+// k_expm_grad (no error sources): one row group per (b, k, eps-variant u):
+// the variant's propagator E' = exp(-i dt H(x + eps e_u)) is computed and
+// contracted on the spot -- it never goes to memory.  Pade m > 5 items are
+// parked (A to a slot) for k_grad_high.
+template <int D>
+__global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm_grad(DevProblem P, DevBatch B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    cd *lds = reinterpret_cast<cd *>(smem_raw);
+    constexpr int TILE = Geo<D>::TILE;
+    Group<D> G = make_group<D>(lds, threadIdx.x);
+    const int nvg = P.np + (P.xadd_dep ? P.na : 0);
+    const long nitems = (long)B.nb * P.Nt * nvg;
+    const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
+    const bool valid = G.lane_ok && gid < nitems;
+    const long gidc = valid ? gid : 0;
+    const int u = (int)(gidc % nvg);
+    const int k = (int)((gidc / nvg) % P.Nt);
+    const int b = (int)(gidc / ((long)nvg * P.Nt));
+    const double *xb = B.x + (size_t)b * P.nx;
+    const ItemBuilder<D, false> rebuild(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1,
+                                        P.vs[P.off_dx + u], valid);
+    cd a[D], x[D];
+    rebuild(a);
+    int singular = 0, s = 0;
+    const int m = expm_prologue<D>(G, a, x, valid, s);
+    if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
+    if (m > 5) {
+        if (valid) park<D>(G, B.ovf2_slots + (size_t)gidc * TILE + G.i * D, a, gid, B.ovf2, B.ovf2_count);
+        return;  // group-uniform: the whole group parks
+    }
+    if (valid && singular) atomicOr(B.status, 1);
+    transpose_group<D>(G, x, valid);  // row i of E'
+    cd z[D];
+    grad_kernel_row<D>(G, P, B, b, k, valid, z);
+    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i * D;
+    grad_store<D>(G, P, B, b, k, u, z, x, E0, valid);
+}
+
+// Parked k_expm_grad items: Pade m = 7/9/13, then the same contraction.
+template <int D>
+__global__ __launch_bounds__(64) void k_grad_high(DevProblem P, DevBatch B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    cd *lds = reinterpret_cast<cd *>(smem_raw);
+    constexpr int TILE = Geo<D>::TILE;
+    Group<D> G = make_group<D>(lds, threadIdx.x);
+    const int nvg = P.np + (P.xadd_dep ? P.na : 0);
+    const int n = *B.ovf2_count;
+    for (int base = blockIdx.x * Geo<D>::GPW; base < n; base += gridDim.x * Geo<D>::GPW) {
+        const int idx = base + G.g;
+        const bool valid = G.lane_ok && idx < n;
+        const long gid = valid ? B.ovf2[idx] : 0;
+        const int u = (int)(gid % nvg);
+        const int k = (int)((gid / nvg) % P.Nt);
+        const int b = (int)(gid / ((long)nvg * P.Nt));
+        const cd *slot = B.ovf2_slots + (size_t)gid * TILE + G.i * D;
+        cd a[D], x[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) a[j] = valid ? slot[j] : czero();
+        int singular = 0, s = 0;
+        const int m = expm_prologue<D>(G, a, x, valid, s);
+        if (m > 0) expm_high<D>(G, m, s, a, x, valid, singular);
+        gsync();
+        if (valid && singular) atomicOr(B.status, 1);
+        transpose_group<D>(G, x, valid);  // row i of E'
+        cd z[D];
+        grad_kernel_row<D>(G, P, B, b, k, valid, z);
+        const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i * D;
+        grad_store<D>(G, P, B, b, k, u, z, x, E0, valid);
     }
 }
 

@@ -3,7 +3,7 @@
 Tolerance tiers (FD noise analysis there):
   T0  propagators E_k              <= 1e-13 relative (max-abs / max|E|, x max(1, |A|_1) for m = 13)
   T1  U, F                         <= 1e-12 absolute
-  T2  eps-FD quantities (F_dx)     <= 1e-6 * max|ref| + 1e-8
+  T2  eps-FD quantities (F_dx)     <= 1e-6 * max|ref| + 1e-7
 """
 import os
 
@@ -15,7 +15,7 @@ from tests import problems as P
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 T1 = 1e-12
-T2, T2_ABS = 1e-6, 1e-8      # + absolute floor u/eps for gradients near an optimum
+T2, T2_ABS = 1e-6, 1e-7      # + absolute floor ~10 u/eps: FD noise of a gradient entry near an optimum
 
 
 @pytest.fixture(scope="module", autouse=True)
