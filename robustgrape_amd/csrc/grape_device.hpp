@@ -50,6 +50,11 @@ __device__ __forceinline__ cd cscale(double s, cd a) { return cmake(s * a.re, s 
 __device__ __forceinline__ cd cmul(cd a, cd b) {
     return cmake(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re);
 }
+// fused forms: s*x + y (2 FMAs) and a*b with 2 MULs + 2 FMAs
+__device__ __forceinline__ cd caxpy(double s, cd x, cd y) { return cmake(fma(s, x.re, y.re), fma(s, x.im, y.im)); }
+__device__ __forceinline__ cd cmulf(cd a, cd b) {
+    return cmake(fma(a.re, b.re, -(a.im * b.im)), fma(a.re, b.im, a.im * b.re));
+}
 // c += a*b with four FMAs (the BLAS-kernel form)
 __device__ __forceinline__ void cmac(cd &c, cd a, cd b) {
     c.re = fma(a.re, b.re, c.re);
@@ -345,7 +350,7 @@ __device__ __forceinline__ void gesv_cols_nopivot(Group<D> &G, cd (&y)[D], cd (&
             const cd r = crecip(y[p]);
 #pragma unroll
             for (int q = 0; q < D; ++q)
-                if (q > p) l[q] = cmul(y[q], r);
+                if (q > p) l[q] = cmulf(y[q], r);
         }
         gsync();
 #pragma unroll
@@ -374,7 +379,7 @@ __device__ __forceinline__ void gesv_cols_nopivot(Group<D> &G, cd (&y)[D], cd (&
     gsync();
 #pragma unroll
     for (int k = D - 1; k >= 0; --k) {
-        x[k] = cmul(x[k], G.tile[k * D + k]);
+        x[k] = cmulf(x[k], G.tile[k * D + k]);
 #pragma unroll
         for (int q = 0; q < D; ++q)
             if (q < k) cmsub(x[q], G.tile[k * D + q], x[k]);
@@ -500,13 +505,13 @@ __device__ __forceinline__ void expm_low(Group<D> &G, int m, cd (&a)[D], cd (&x)
     }
     // U' = (C1 I + C3 A2) [+ C5 A4],  V = (C0 I + C2 A2) [+ C4 A4]   (Julia's order)
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
+    for (int j = 0; j < D; ++j) {  // (fused: rounding-level differences from Julia's order)
         const double du = (j == i) ? C[1] : 0.0, dv = (j == i) ? C[0] : 0.0;
-        cd u = cmake(du + C[3] * p[j].re, 0.0 + C[3] * p[j].im);
-        cd v = cmake(dv + C[2] * p[j].re, 0.0 + C[2] * p[j].im);
+        cd u = cmake(fma(C[3], p[j].re, du), C[3] * p[j].im);
+        cd v = cmake(fma(C[2], p[j].re, dv), C[2] * p[j].im);
         if (m == 5) {
-            u = cadd(u, cscale(C[5], q[j]));
-            v = cadd(v, cscale(C[4], q[j]));
+            u = caxpy(C[5], q[j], u);
+            v = caxpy(C[4], q[j], v);
         }
         p[j] = u;
         q[j] = v;

@@ -140,55 +140,57 @@ struct ItemBuilder {
     int i, nt1;
     VSpec vs;
     bool valid;
-    cd c0[kCachedTerms], ce[kCachedTerms];
+    cd c0[kCachedTerms], ce[kCachedTerms];  // coefficients pre-scaled by -i dt (and errval)
     int o0, ne_t;
+
+    // -i dt c
+    __device__ __forceinline__ cd gen(cd c) const { return cmake(P->dt * c.im, -(P->dt * c.re)); }
 
     __device__ __forceinline__ ItemBuilder(const DevProblem *P_, const double *xk_, const double *xadd_, int i_,
                                            int nt1_, const VSpec &vs_, bool valid_)
         : P(P_), xk(xk_), xadd(xadd_), i(i_), nt1(nt1_), vs(vs_), valid(valid_), o0(0), ne_t(0) {
 #pragma unroll
         for (int t = 0; t < kCachedTerms; ++t)
-            c0[t] = (t < P->n_h0) ? term_coef(P->h0[t], nt1, xk, xadd, vs.pert) : czero();
+            c0[t] = (t < P->n_h0) ? gen(term_coef(P->h0[t], nt1, xk, xadd, vs.pert)) : czero();
         if (ERR && vs.err >= 0) {
             o0 = P->err_off[vs.err];
             ne_t = P->err_off[vs.err + 1] - o0;
 #pragma unroll
             for (int t = 0; t < kCachedTerms; ++t)
-                ce[t] = (t < ne_t) ? term_coef(P->err[o0 + t], nt1, xk, xadd, vs.pert) : czero();
+                ce[t] = (t < ne_t) ? gen(cscale(vs.errval, term_coef(P->err[o0 + t], nt1, xk, xadd, vs.pert)))
+                                   : czero();
         }
     }
 
-    __device__ __forceinline__ void accumulate(const Term *terms, int n, const cd (&cache)[kCachedTerms],
+    __device__ __forceinline__ void accumulate(const Term *terms, int n, const cd (&cache)[kCachedTerms], double sc,
                                                cd (&h)[D]) const {
-#pragma unroll
-        for (int j = 0; j < D; ++j) h[j] = czero();
 #pragma unroll
         for (int t = 0; t < kCachedTerms; ++t) {
             if (t < n) {
                 const cd *op = P->opsT + (size_t)terms[t].op * D * D + i * D;
 #pragma unroll
-                for (int j = 0; j < D; ++j) h[j] = cadd(h[j], cmul(cache[t], op[j]));
+                for (int j = 0; j < D; ++j) cmac(h[j], cache[t], op[j]);
             }
         }
         for (int t = kCachedTerms; t < n; ++t) {  // rare: more terms than cached
-            const cd c = term_coef(terms[t], nt1, xk, xadd, vs.pert);
+            const cd c = gen(cscale(sc, term_coef(terms[t], nt1, xk, xadd, vs.pert)));
             const cd *op = P->opsT + (size_t)terms[t].op * D * D + i * D;
 #pragma unroll
-            for (int j = 0; j < D; ++j) h[j] = cadd(h[j], cmul(c, op[j]));
+            for (int j = 0; j < D; ++j) cmac(h[j], c, op[j]);
         }
     }
 
+    // column i of A = -i dt (H0 [+ errval Herror]): sum of cached coefficient x operator-column
+    // MACs (fused: rounding-level differences from Julia's -1im*dt*H, within T0)
     __device__ __forceinline__ void operator()(cd (&a)[D]) const {
-        cd h[D];
-        accumulate(P->h0, P->n_h0, c0, h);
-        if (ERR && vs.err >= 0) {  // exp(-i dt (Herror(.., err) + H0(..)))   UnitaryCalculations.jl:67-68
-            cd he[D];
-            accumulate(P->err + o0, ne_t, ce, he);
 #pragma unroll
-            for (int j = 0; j < D; ++j) h[j] = cadd(cscale(vs.errval, he[j]), h[j]);
+        for (int j = 0; j < D; ++j) a[j] = czero();
+        accumulate(P->h0, P->n_h0, c0, 1.0, a);
+        if (ERR && vs.err >= 0) accumulate(P->err + o0, ne_t, ce, vs.errval, a);  // UnitaryCalculations.jl:67-68
+        if (!valid) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) a[j] = czero();
         }
-#pragma unroll
-        for (int j = 0; j < D; ++j) a[j] = valid ? cmake(P->dt * h[j].im, -P->dt * h[j].re) : czero();
     }
 };
 
@@ -231,10 +233,10 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
         return;
     }
     if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
-    transpose_group<D>(G, x, valid);  // E is stored row-major
-    if (valid) {
+    if (valid) {  // E row-major: column i at stride D (coalesced across the group)
+        cd *col = B.E + (size_t)gidc * D * D + G.i;
 #pragma unroll
-        for (int j = 0; j < D; ++j) out[j] = x[j];
+        for (int j = 0; j < D; ++j) col[j * D] = x[j];
         if (singular) atomicOr(B.status, 1);
     }
 }
@@ -258,11 +260,12 @@ __global__ __launch_bounds__(64) void k_expm_high(cd *slots, const int *list, co
         int singular = 0, s = 0;
         const int m = expm_prologue<D>(G, a, x, valid, s);
         if (m > 0) expm_high<D>(G, m, s, a, x, valid, singular);
-        gsync();
-        if (rows_out) transpose_group<D>(G, x, valid);
+        gsync();  // every lane has read its A column before any result lands in the slot
         if (valid) {
+            cd *dst = rows_out ? slot - G.i * D + G.i : slot;  // row-major / column-major result
+            const int stride = rows_out ? D : 1;
 #pragma unroll
-            for (int j = 0; j < D; ++j) slot[j] = x[j];
+            for (int j = 0; j < D; ++j) dst[j * stride] = x[j];
             if (singular) atomicOr(status, 1);
         }
     }
@@ -306,6 +309,13 @@ __global__ __launch_bounds__(64) void k_expm_raw(const cd *A, cd *E, int n, int 
 
 // ---------------------------------------------------------------------------
 // k_scan: one workgroup (W waves) per evaluation
+//
+// Column form: lane j of a group holds column j of its chunk's running
+// product, so that every global access is coalesced (lane j touches the
+// pieces m*D + j of a row-major tile: D lanes cover 16*D contiguous bytes per
+// instruction) -- the local chain is a dependent load -> product -> store
+// sequence, and its per-step latency is what bounds this kernel.  Chunk
+// totals live in the groups' LDS tiles COLUMN-major (tile[j*D + i] = S[i][j]).
 // ---------------------------------------------------------------------------
 template <int D, int W>
 __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
@@ -325,14 +335,14 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     const cd *Eb = B.E + (size_t)b * P.Nt * P.nv * TILE;
     cd *Qb = B.Q + (size_t)b * P.Nt * TILE;
 
-    // Phase A: local inclusive chain Q_k = E_k ... E_{cL}
+    // Phase A: local inclusive chain Q_k = E_k ... E_{cL}; lane i owns column i
     cd q[D], e[D], t[D];
     const int k0 = c * P.L;
-    auto load_e = [&](int k, cd (&dst)[D]) {
+    auto load_e = [&](int k, cd (&dst)[D]) {  // column i of E_k (coalesced)
         const bool ok = gvalid && k < P.Nt;
-        const cd *src = Eb + ((size_t)(ok ? k : 0) * P.nv) * TILE + i * D;
+        const cd *src = Eb + ((size_t)(ok ? k : 0) * P.nv) * TILE + i;
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) dst[jj] = ok ? src[jj] : czero();
+        for (int m = 0; m < D; ++m) dst[m] = ok ? src[m * D] : czero();
     };
     load_e(k0, e);
 #if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 0
@@ -342,44 +352,42 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         const int k = k0 + j;
         const bool act = gvalid && k < P.Nt;
         cd en[D];
-#ifndef GRAPE_DIAG_NOLOAD
-        load_e(k + 1, en);  // prefetch the next step's propagator row behind this product
-#else
-        for (int jj = 0; jj < D; ++jj) en[jj] = cscale(1.0000001, e[jj]);
-#endif
+        load_e(k + 1, en);  // prefetch the next step's propagator column behind this product
         if (j == 0) {
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) q[jj] = e[jj];
+            for (int m = 0; m < D; ++m) q[m] = e[m];
         } else {
-#ifndef GRAPE_DIAG_NOMM
-            mm_tile<D>(e, G.tile, q);
-#else
-            for (int jj = 0; jj < D; ++jj) q[jj] = cadd(e[jj], G.tile[i * D + jj]);
-#endif
+            tile_store_row(G, e, gvalid);  // E_k column-major in the tile (lanes outside a group must not write)
+            gsync();
+            mm_tile<D>(q, G.tile, t);  // E_k . q
+            gsync();
+            if (act) {  // past N_t (last chunk's tail) the total stays put
+#pragma unroll
+                for (int m = 0; m < D; ++m) q[m] = t[m];
+            }
         }
-        gsync();
         if (act) {
-            tile_store_row(G, q, true);
-#ifndef GRAPE_DIAG_NOSTORE
-            cd *dst = Qb + (size_t)k * TILE + i * D;
+            cd *dst = Qb + (size_t)k * TILE + i;  // Q row-major: column i at stride D (coalesced)
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) dst[jj] = q[jj];
-#endif
+            for (int m = 0; m < D; ++m) dst[m * D] = q[m];
         }
-        gsync();
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) e[jj] = en[jj];
+        for (int m = 0; m < D; ++m) e[m] = en[m];
     }
+    tile_store_row(G, q, gvalid);  // chunk total T_c, column-major
+    gsync();
 #if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 1
     return;
 #endif
-    // Phase B: inclusive scan of the chunk totals, P_c = T_c ... T_0 (Hillis-Steele)
+    // Phase B: inclusive scan of the chunk totals, P_c = T_c ... T_0 (Hillis-Steele):
+    // column i of S_c . S_{c-o} = S_c . (column i of S_{c-o})
     for (int o = 1; o < P.nchunks; o <<= 1) {
         const bool doit = gvalid && c >= o;
         if (doit) {
+            const cd *src = tile_of(c - o) + i * D;
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) q[jj] = G.tile[i * D + jj];
-            mm_tile<D>(q, tile_of(c - o), t);
+            for (int m = 0; m < D; ++m) q[m] = src[m];
+            mm_tile<D>(q, G.tile, t);
         }
         gsync();
         if (doit) tile_store_row(G, t, true);
@@ -390,7 +398,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 #endif
     // Phase C: fidelity and M = G U on group 0 (everyone keeps the barrier sequence)
     const bool f0 = (c == 0) && G.lane_ok;
-    const cd *Ut = tile_of(P.nchunks - 1);
+    const cd *Ut = tile_of(P.nchunks - 1);  // U column-major
     const double *xb = B.x + (size_t)b * P.nx;
     const double *xadd = xb + (size_t)P.np * P.Nt;
     Pert none;
@@ -404,7 +412,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     gsync();
 #pragma unroll
     for (int r = 0; r < D; ++r) l[r] = cconj(S1[r * D + i]);
-    mm_tile<D>(l, Ut, kk);  // K = U0^dag U, row i
+    mm_tile<D, true>(l, Ut, kk);  // K = U0^dag U, row i
     const double wi = P.W[i];
     double part = 0.0;
     cd kii = czero();
@@ -417,7 +425,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     const double sum_part = group_sum(G, wi * part, f0);
     const double tau_re = group_sum(G, wi * kii.re, f0);
     const double tau_im = group_sum(G, wi * kii.im, f0);
-    // F = [Re tr(W K P K^dag) + |tau|^2] / (D(D+1))          (FidelityCalculations.jl:54)
+// F = [Re tr(W K P K^dag) + |tau|^2] / (D(D+1))          (FidelityCalculations.jl:54)
     const double Fv = (sum_part + tau_re * tau_re + tau_im * tau_im) / P.DD;
     // M = G U = 2 (P K^dag W K + conj(tau) W K) / (D(D+1))
     if (f0) {
@@ -453,7 +461,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         gsync();
 #pragma unroll
         for (int r = 0; r < D; ++r) l[r] = cconj(S1[r * D + i]);
-        mm_tile<D>(l, Ut, t);  // Kd = U0d^dag U
+        mm_tile<D, true>(l, Ut, t);  // Kd = U0d^dag U
         double pr = 0.0;
         cd kdii = czero();
 #pragma unroll
@@ -475,7 +483,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     if (f0 && B.Ub) {  // U for the error path
         cd *du = B.Ub + (size_t)b * TILE + i * D;
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) du[jj] = Ut[i * D + jj];
+        for (int jj = 0; jj < D; ++jj) du[jj] = Ut[jj * D + i];
     }
 #if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 3
     return;
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         cd *dc = B.Carry + ((size_t)b * P.nchunks + c) * TILE + i * D;
         const cd *Cr = c > 0 ? tile_of(c - 1) : nullptr;
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) dc[jj] = Cr ? Cr[i * D + jj] : cmake(jj == i ? 1.0 : 0.0, 0.0);
+        for (int jj = 0; jj < D; ++jj) dc[jj] = Cr ? Cr[jj * D + i] : cmake(jj == i ? 1.0 : 0.0, 0.0);
     }
     if (gvalid) {
         cd mc[D];
@@ -493,11 +501,11 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 #pragma unroll
             for (int jj = 0; jj < D; ++jj) mc[jj] = S3[i * D + jj];
         } else {
-            const cd *Cr = tile_of(c - 1);
+            const cd *Cr = tile_of(c - 1);  // column-major
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) q[jj] = Cr[i * D + jj];
+            for (int jj = 0; jj < D; ++jj) q[jj] = Cr[jj * D + i];
             mm_tile<D>(q, S3, t);
-            mm_tile<D, true, true>(t, Cr, mc);
+            mm_tile<D, false, true>(t, Cr, mc);
         }
         cd *dst = B.Mc + ((size_t)b * P.nchunks + c) * TILE + i * D;
 #pragma unroll
@@ -542,11 +550,49 @@ __device__ __forceinline__ void grad_kernel_row(Group<D> &G, const DevProblem &P
     }
 }
 
+// Column j of Z_k for lane j (the fused kernels keep E' in columns):
+//   column j of Z = conj(Q_k) M'^T (row j of Q_{k-1})^T,
+// with M' and Q_k staged through the group tile by coalesced cooperative loads.
+template <int D>
+__device__ __forceinline__ void tile_load(Group<D> &G, const cd *src, bool valid) {  // row-major copy
+    if (valid) {
+#pragma unroll
+        for (int m = 0; m < D; ++m) G.tile[m * D + G.i] = src[m * D + G.i];
+    }
+}
+template <int D>
+__device__ __forceinline__ void grad_kernel_col(Group<D> &G, const DevProblem &P, const DevBatch &B, int b, int k,
+                                                bool valid, cd (&z)[D]) {
+    constexpr int TILE = Geo<D>::TILE;
+    const int c = k / P.L, j0 = k - c * P.L;
+    const int i = G.i;
+    const cd *Qk = B.Q + ((size_t)b * P.Nt + k) * TILE;
+    const cd *Mc = B.Mc + ((size_t)b * P.nchunks + c) * TILE;
+    cd r[D], t[D];
+    if (j0 > 0) {
+#pragma unroll
+        for (int m = 0; m < D; ++m) r[m] = Qk[i * D + m - TILE];  // row i of Q_{k-1}
+    }
+    tile_load<D>(G, Mc, valid);
+    gsync();
+    if (j0 > 0) {
+        mm_tile<D>(r, G.tile, t);  // M'^T r
+    } else {
+#pragma unroll
+        for (int m = 0; m < D; ++m) t[m] = G.tile[i * D + m];  // row i of M'
+    }
+    gsync();
+    tile_load<D>(G, Qk, valid);
+    gsync();
+    mm_tile<D, true, true>(t, G.tile, z);  // conj(Q_k) t
+    gsync();
+}
+
 // Group-summed Re sum_j z_j * (ev_j - e0_j) * inv_eps, written to F_dx (control
 // variant u < np) or to the per-step x_add partial (u >= np).
 template <int D>
 __device__ __forceinline__ void grad_store(Group<D> &G, const DevProblem &P, const DevBatch &B, int b, int k, int u,
-                                           const cd (&z)[D], const cd (&ev)[D], const cd *e0, bool valid) {
+                                           const cd (&z)[D], const cd (&ev)[D], const cd (&e0)[D], bool valid) {
     double s = 0.0;
 #pragma unroll
     for (int jj = 0; jj < D; ++jj) {
@@ -575,13 +621,16 @@ __global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, Dev
     cd z[D];
     grad_kernel_row<D>(G, P, B, b, k, valid, z);
     const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i * D;
+    cd e0[D];
+#pragma unroll
+    for (int jj = 0; jj < D; ++jj) e0[jj] = E0[jj];
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);  // dx then dxa variants are contiguous
     for (int u = 0; u < nvg; ++u) {
         const cd *Ev = E0 + (size_t)(P.off_dx + u) * TILE;
         cd ev[D];
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) ev[jj] = Ev[jj];
-        grad_store<D>(G, P, B, b, k, u, z, ev, E0, valid);
+        grad_store<D>(G, P, B, b, k, u, z, ev, e0, valid);
     }
 }
 
@@ -616,11 +665,12 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
         return;  // group-uniform: the whole group parks
     }
     if (valid && singular) atomicOr(B.status, 1);
-    transpose_group<D>(G, x, valid);  // row i of E'
-    cd z[D];
-    grad_kernel_row<D>(G, P, B, b, k, valid, z);
-    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i * D;
-    grad_store<D>(G, P, B, b, k, u, z, x, E0, valid);
+    cd z[D], e0[D];
+    grad_kernel_col<D>(G, P, B, b, k, valid, z);
+    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i;  // column i of E
+#pragma unroll
+    for (int m = 0; m < D; ++m) e0[m] = E0[m * D];
+    grad_store<D>(G, P, B, b, k, u, z, x, e0, valid);
 }
 
 // Parked k_expm_grad items: Pade m = 7/9/13, then the same contraction.
@@ -648,11 +698,12 @@ __global__ __launch_bounds__(64) void k_grad_high(DevProblem P, DevBatch B) {
         if (m > 0) expm_high<D>(G, m, s, a, x, valid, singular);
         gsync();
         if (valid && singular) atomicOr(B.status, 1);
-        transpose_group<D>(G, x, valid);  // row i of E'
-        cd z[D];
-        grad_kernel_row<D>(G, P, B, b, k, valid, z);
-        const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i * D;
-        grad_store<D>(G, P, B, b, k, u, z, x, E0, valid);
+        cd z[D], e0[D];
+        grad_kernel_col<D>(G, P, B, b, k, valid, z);
+        const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i;
+#pragma unroll
+        for (int m = 0; m < D; ++m) e0[m] = E0[m * D];
+        grad_store<D>(G, P, B, b, k, u, z, x, e0, valid);
     }
 }
 
