@@ -136,6 +136,11 @@ void grape_plan_destroy(grape_plan *plan);
 /* Device stream of the plan (a hipStream_t), for callers that enqueue around it. */
 void *grape_plan_stream(grape_plan *plan);
 
+/* Enqueue the plan's work on the caller's hipStream_t from now on (NULL: the
+ * plan's own stream).  Lets a caller keep the evaluation stream-ordered with
+ * its own kernels and collectives instead of synchronising between them. */
+int grape_plan_set_stream(grape_plan *plan, void *stream);
+
 /*
  * Fidelity + gradient (+ error sensitivity and its gradient) for a batch of
  * control vectors.  One evaluation b equals one reference call

@@ -18,7 +18,7 @@ STATUS_NAMES = {-1: "GRAPE_ERR_INVALID", -2: "GRAPE_ERR_UNSUPPORTED", -3: "GRAPE
 
 # every symbol include/grape.h declares
 EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grape_plan_create",
-            "grape_plan_destroy", "grape_plan_stream", "grape_fidelity_grad",
+            "grape_plan_destroy", "grape_plan_stream", "grape_plan_set_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
@@ -52,6 +52,8 @@ def lib():
         L.grape_plan_destroy.restype = None
         L.grape_plan_stream.argtypes = [vp]
         L.grape_plan_stream.restype = vp
+        L.grape_plan_set_stream.argtypes = [vp, vp]
+        L.grape_plan_set_stream.restype = ctypes.c_int
         L.grape_fidelity_grad.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp]
         L.grape_fidelity_grad.restype = ctypes.c_int
         L.grape_fidelity_grad_device_async.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]

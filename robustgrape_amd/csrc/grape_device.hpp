@@ -147,6 +147,41 @@ __device__ __forceinline__ void mm_tile(const cd (&a)[D], const cd *B, cd (&c)[D
     pin<D>(c);
 }
 
+// The same product with row k+1 of B read while row k is consumed: D LDS
+// reads in flight behind D complex MACs instead of one or two.  For the
+// latency-bound scan kernels (two waves per SIMD, registers to spare); the
+// exp kernels keep mm_tile, whose registers are spoken for.
+template <int D, bool TRANS = false, bool CONJ = false>
+__device__ __forceinline__ void mm_tile_pf(const cd (&a)[D], const cd *B, cd (&c)[D]) {
+    auto ld = [&](int k, int j) {
+        cd b = TRANS ? B[j * D + k] : B[k * D + j];
+        if (CONJ) b.im = -b.im;
+        return b;
+    };
+    cd cur[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        c[j] = czero();
+        cur[j] = ld(0, j);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        cd nxt[D];
+        if (k + 1 < D) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) nxt[j] = ld(k + 1, j);
+        }
+        const cd ak = a[k];
+#pragma unroll
+        for (int j = 0; j < D; ++j) cmac(c[j], ak, cur[j]);
+        if (k + 1 < D) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) cur[j] = nxt[j];
+        }
+    }
+    pin<D>(c);
+}
+
 // Group-wide sum / max of one double per lane (all lanes receive the result).
 template <int D>
 __device__ __forceinline__ double group_sum(Group<D> &G, double v, bool wr) {

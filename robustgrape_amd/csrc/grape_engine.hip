@@ -189,7 +189,9 @@ hipError_t dalloc(T **p, size_t n) {
 
 struct grape_plan {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // where work is enqueued (own_stream or the caller's)
+    hipStream_t own_stream = nullptr;
+    int *h_status = nullptr;           // pinned copy of the device status word
     DevProblem P{};
     int max_batch = 0;
     // device buffers
@@ -204,7 +206,7 @@ struct grape_plan {
     cd *d_ovf2_slots = nullptr;
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
-    int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0] overflow count, [1] status
+    int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -240,7 +242,8 @@ static void free_plan(grape_plan *p) {
         (void)hipEventDestroy(pe.a);
         (void)hipEventDestroy(pe.b);
     }
-    if (p->stream) (void)hipStreamDestroy(p->stream);
+    if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+    if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
 }
 
@@ -324,8 +327,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         return code;
     };
     if (hipSetDevice(device) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "hipSetDevice failed"));
-    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "hipStreamCreate failed"));
+    p->stream = p->own_stream;
+    if (hipHostMalloc(reinterpret_cast<void **>(&p->h_status), sizeof(int), hipHostMallocDefault) != hipSuccess)
+        return bail(fail(GRAPE_ERR_ALLOC, "pinned allocation failed"));
+    *p->h_status = 0;
     if (dispatch_lds_limits(D) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
 
     DevProblem &P = p->P;
@@ -415,6 +422,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
     if (!ok) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed"));
+    if (hipMemset(p->d_ctrl, 0, 4 * sizeof(int)) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "memset failed"));
     if (hipMemcpy(p->d_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     if (P.ne > 0 &&
@@ -445,6 +453,12 @@ void grape_plan_destroy(grape_plan *plan) { free_plan(plan); }
 
 void *grape_plan_stream(grape_plan *plan) { return plan ? (void *)plan->stream : nullptr; }
 
+int grape_plan_set_stream(grape_plan *plan, void *stream) {
+    if (!plan) return fail(GRAPE_ERR_INVALID, "null plan");
+    plan->stream = stream ? static_cast<hipStream_t>(stream) : plan->own_stream;
+    return GRAPE_OK;
+}
+
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
                    double *d_Fd2dx) {
     DevBatch B{};
@@ -464,13 +478,13 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     B.tgt_part = p->d_tgt_part;
     B.overflow = p->d_ovf;
     B.overflow_count = p->d_ctrl;
-    B.status = p->d_ctrl + 1;
     B.ovf2 = p->d_ovf2;
-    B.ovf2_count = p->d_ctrl + 2;
+    B.ovf2_count = p->d_ctrl + 1;
+    B.status = p->d_ctrl + 2;
     B.ovf2_slots = p->d_ovf2_slots;
-    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, sizeof(int), p->stream));      // k_expm overflow count
-    HIPCHECK(hipMemsetAsync(p->d_ctrl + 2, 0, sizeof(int), p->stream));  // k_expm_grad overflow count
-    // (ctrl[1], the status word, is sticky until grape_plan_synchronize reports it)
+    // ctrl: [0] k_expm overflow count, [1] k_expm_grad overflow count, [2] status
+    // (sticky until grape_plan_synchronize reports it; copied to pinned memory below)
+    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), p->stream));
     KMark mk;
     if (p->profiling) {
         mk.ctx = p;
@@ -487,6 +501,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         };
     }
     HIPCHECK(dispatch_pipeline(p->P.D, p->P, B, p->stream, mk));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return GRAPE_OK;
 }
 
@@ -524,10 +539,10 @@ int grape_plan_synchronize(grape_plan *p) {
     HIPCHECK(hipSetDevice(p->device));
     HIPCHECK(hipStreamSynchronize(p->stream));
     resolve_events(p);
-    int st = 0;
-    HIPCHECK(hipMemcpy(&st, p->d_ctrl + 1, sizeof(int), hipMemcpyDeviceToHost));
+    const int st = *p->h_status;
     if (st & 1) {
-        HIPCHECK(hipMemset(p->d_ctrl + 1, 0, sizeof(int)));
+        *p->h_status = 0;
+        HIPCHECK(hipMemset(p->d_ctrl + 2, 0, sizeof(int)));
         return fail(GRAPE_ERR_SINGULAR, "singular Pade denominator (Julia gesv! would throw SingularException)");
     }
     return GRAPE_OK;

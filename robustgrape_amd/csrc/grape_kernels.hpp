@@ -359,7 +359,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         } else {
             tile_store_row(G, e, gvalid);  // E_k column-major in the tile (lanes outside a group must not write)
             gsync();
-            mm_tile<D>(q, G.tile, t);  // E_k . q
+            mm_tile_pf<D>(q, G.tile, t);  // E_k . q
             gsync();
             if (act) {  // past N_t (last chunk's tail) the total stays put
 #pragma unroll
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
             const cd *src = tile_of(c - o) + i * D;
 #pragma unroll
             for (int m = 0; m < D; ++m) q[m] = src[m];
-            mm_tile<D>(q, G.tile, t);
+            mm_tile_pf<D>(q, G.tile, t);
         }
         gsync();
         if (doit) tile_store_row(G, t, true);
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     gsync();
 #pragma unroll
     for (int r = 0; r < D; ++r) l[r] = cconj(S1[r * D + i]);
-    mm_tile<D, true>(l, Ut, kk);  // K = U0^dag U, row i
+    mm_tile_pf<D, true>(l, Ut, kk);  // K = U0^dag U, row i
     const double wi = P.W[i];
     double part = 0.0;
     cd kii = czero();
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     gsync();
 #pragma unroll
     for (int r = 0; r < D; ++r) l[r] = cscale(P.W[r], cconj(S2[r * D + i]));
-    mm_tile<D>(l, S2, t);
+    mm_tile_pf<D>(l, S2, t);
     {
         const double pi_ = wi != 0.0 ? 1.0 : 0.0;
         const double sc = 2.0 / P.DD;
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         gsync();
 #pragma unroll
         for (int r = 0; r < D; ++r) l[r] = cconj(S1[r * D + i]);
-        mm_tile<D, true>(l, Ut, t);  // Kd = U0d^dag U
+        mm_tile_pf<D, true>(l, Ut, t);  // Kd = U0d^dag U
         double pr = 0.0;
         cd kdii = czero();
 #pragma unroll
@@ -504,8 +504,8 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
             const cd *Cr = tile_of(c - 1);  // column-major
 #pragma unroll
             for (int jj = 0; jj < D; ++jj) q[jj] = Cr[jj * D + i];
-            mm_tile<D>(q, S3, t);
-            mm_tile<D, false, true>(t, Cr, mc);
+            mm_tile_pf<D>(q, S3, t);
+            mm_tile_pf<D, false, true>(t, Cr, mc);
         }
         cd *dst = B.Mc + ((size_t)b * P.nchunks + c) * TILE + i * D;
 #pragma unroll

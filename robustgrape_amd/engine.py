@@ -49,6 +49,11 @@ class GrapePlan:
     def stream(self) -> int:
         return _capi.lib().grape_plan_stream(self.handle)
 
+    def set_stream(self, stream_ptr: int | None):
+        """Enqueue on the caller's hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+        None restores the plan's own stream."""
+        _capi.check(_capi.lib().grape_plan_set_stream(self.handle, ctypes.c_void_p(stream_ptr or None)))
+
     def fidelity_grad(self, X):
         """Host arrays in/out. X: (nbatch, n_x). Returns F (nb,), F_dx (nb, n_x),
         F_d2err (nb, nerr), F_d2err_dx (nb, n_x, nerr)."""
