@@ -54,6 +54,26 @@ def flops_expm(d, m=5, s=0):
     return (pi + s + 5.0 / 3.0) * 8 * d ** 3
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+
+
+def pmc_traffic(kernel, batch):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_profile.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), if it was
+    recorded at this batch size; else None."""
+    try:
+        with open(PMC_SUMMARY) as fh:
+            js = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if js.get("batch") != batch:
+        return None
+    for name, row in js.get("kernels", {}).items():
+        if name.split("<")[0] == kernel and "hbm_bytes_per_launch" in row:
+            return row["hbm_bytes_per_launch"]
+    return None
+
+
 def cpu_baseline(seconds=15.0):
     """Time the CPU restatement on a bounded sample of the same workload (rank 0, N = 1)."""
     try:
@@ -95,7 +115,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="restarts per GPU")
+    ap.add_argument("--batch", type=int, default=1024, help="restarts per GPU (one device pass each step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -184,7 +204,8 @@ def main():
                        "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
             "roofline": {"bound": "mfma", "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)",
                          "kernel": kname, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+                         "traffic": pmc_traffic(kname, B), "traffic_unit": "HBM bytes per launch (PMC)",
                          "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch},
             "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items()},
         }

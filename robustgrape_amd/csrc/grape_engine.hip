@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "grape.h"
@@ -41,22 +42,21 @@ int fail(int code, const std::string &msg) {
             return fail(GRAPE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-#ifndef GRAPE_SCAN_WAVES
-#define GRAPE_SCAN_WAVES 8
-#endif
-constexpr int kScanWaves = GRAPE_SCAN_WAVES;
+// Scan workgroups: one per evaluation, W waves of row groups.  W = 8 (52 chunks
+// of L = 10 steps at d = 9, N_t = 512) has the shortest chains; W = 4 halves
+// the LDS and registers per block so two evaluations share a CU, which wins
+// once there are more evaluations than CUs (plan-time choice, see kScanWide).
+constexpr int kScanWide = 8, kScanNarrow = 4;
 
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
 template <int D>
-size_t errscan_lds() {
-    return ((size_t)kScanWaves * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 4 * grape::Geo<D>::TILE) *
-           sizeof(cd);
+size_t errscan_lds(int W) {
+    return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 4 * grape::Geo<D>::TILE) * sizeof(cd);
 }
 template <int D>
-size_t scan_lds() {
-    return ((size_t)kScanWaves * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 3 * grape::Geo<D>::TILE) *
-           sizeof(cd);
+size_t scan_lds(int W) {
+    return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 3 * grape::Geo<D>::TILE) * sizeof(cd);
 }
 
 // ---------------------------------------------------------------------------
@@ -89,8 +89,12 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
                        B.overflow_count, B.status, 1);
     mark(GRAPE_KERNEL_EXPM_HIGH, 1);
     mark(GRAPE_KERNEL_SCAN, 0);
-    hipLaunchKernelGGL((grape::k_scan<D, kScanWaves>), dim3(B.nb), dim3(64 * kScanWaves), scan_lds<D>(), st, P,
-                       B);
+    if (P.scan_waves == kScanNarrow)
+        hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
+                           scan_lds<D>(kScanNarrow), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide),
+                           st, P, B);
     mark(GRAPE_KERNEL_SCAN, 1);
     if (fused) {
         const int nvg = P.np + (P.xadd_dep ? P.na : 0);
@@ -111,8 +115,12 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     }
     if (P.ne > 0) {
         mark(GRAPE_KERNEL_ERR_SCAN, 0);
-        hipLaunchKernelGGL((grape::k_err_scan<D, kScanWaves>), dim3(B.nb * P.ne), dim3(64 * kScanWaves),
-                           errscan_lds<D>(), st, P, B);
+        if (P.scan_waves == kScanNarrow)
+            hipLaunchKernelGGL((grape::k_err_scan<D, kScanNarrow>), dim3(B.nb * P.ne), dim3(64 * kScanNarrow),
+                               errscan_lds<D>(kScanNarrow), st, P, B);
+        else
+            hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
+                               errscan_lds<D>(kScanWide), st, P, B);
         mark(GRAPE_KERNEL_ERR_SCAN, 1);
         const long ne_items = (long)B.nb * P.nchunks * P.ne;
         mark(GRAPE_KERNEL_ERR_GRAD, 0);
@@ -138,13 +146,18 @@ hipError_t launch_expm_raw(const cd *A, cd *E, int n, int *ovf, int *ovf_count, 
     return hipGetLastError();
 }
 
+template <int D, int W>
+hipError_t set_lds_limits_w() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, W>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>(W));
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_err_scan<D, W>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)errscan_lds<D>(W));
+}
 template <int D>
 hipError_t set_lds_limits() {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, kScanWaves>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>());
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_err_scan<D, kScanWaves>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)errscan_lds<D>());
+    hipError_t e = set_lds_limits_w<D, kScanWide>();
+    return e != hipSuccess ? e : set_lds_limits_w<D, kScanNarrow>();
 }
 
 #define GRAPE_DIMS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
@@ -386,7 +399,19 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.inv_eps2sq = 1.0 / (desc->eps2 * desc->eps2);
     P.DD = trP * (trP + 1.0);
     P.Dtr = trP;
-    const int NG = kScanWaves * (64 / D);
+    // scan width: narrow once a launch can hold two evaluations per CU
+    int ncu = 256;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            ncu = prop.multiProcessorCount;
+    }
+    P.scan_waves = p->max_batch >= 2 * ncu ? kScanNarrow : kScanWide;
+    if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {  // tuning override: 4 or 8
+        const int wv = std::atoi(w);
+        if (wv == kScanNarrow || wv == kScanWide) P.scan_waves = wv;
+    }
+    const int NG = P.scan_waves * (64 / D);
     const int nc0 = std::min(NG, P.Nt);
     P.L = (P.Nt + nc0 - 1) / nc0;
     P.nchunks = (P.Nt + P.L - 1) / P.L;

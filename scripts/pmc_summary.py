@@ -45,7 +45,10 @@ def load(dirs):
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--batch" in sys.argv:
+        args.remove(sys.argv[sys.argv.index("--batch") + 1])
     js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else None
     if js in args:
         args.remove(js)
     data = load(args)
@@ -68,7 +71,7 @@ def main():
             print(f"    {c:36s} {v:16.1f}")
     if js:
         with open(js, "w") as fh:
-            json.dump(summary, fh, indent=1)
+            json.dump({"batch": batch, "kernels": summary}, fh, indent=1)
 
 
 if __name__ == "__main__":

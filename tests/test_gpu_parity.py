@@ -200,3 +200,38 @@ def test_error_batch_matches_single():
         Fs, gs, d2s, d2dxs = calculate_fidelity_and_derivatives(fp, X[b])
         assert Fs == F[b] and np.array_equal(gs, Fdx[b])
         assert np.array_equal(d2s, d2[b]) and np.array_equal(d2dxs, d2dx[b])
+
+
+@pytest.mark.parametrize("waves", ["4", "8"])
+def test_scan_widths_match_golden(waves, monkeypatch):
+    """Both k_scan / k_err_scan widths (the plan picks 4 waves for large batches): C2 golden and
+    the C3 (4 error sources) golden through a plan forced to each width."""
+    from robustgrape_amd.engine import GrapePlan
+    monkeypatch.setenv("GRAPE_SCAN_WAVES", waves)
+    g = _golden("c2")
+    plan = GrapePlan(P.full9_problem(512), nparam=1, max_batch=8)
+    F, Fdx, _, _ = plan.fidelity_grad(g["x"][None, :])
+    plan.close()
+    _assert_fid(F[0], Fdx[0], float(g["F"]), g["F_dx"])
+    g = _golden("c3n64")
+    fp = P.full9_problem(64, nerr=4)
+    plan = GrapePlan(fp, nparam=1, max_batch=8)
+    F, Fdx, d2, d2dx = plan.fidelity_grad(g["x"][None, :])
+    plan.close()
+    _assert_fid(F[0], Fdx[0], float(g["F"]), g["F_dx"])
+    _assert_err(fp, d2[0], d2dx[0], g["F_d2err"], g["F_d2err_dx"])
+
+
+def test_large_batch_plan_matches_single():
+    """A 600-restart launch (narrow scan, several waves of workgroups per CU) against single evaluations."""
+    from robustgrape_amd.engine import GrapePlan
+    fp = P.full9_problem(512)
+    X = np.stack([P.random_x(512, s) for s in range(600)])
+    big = GrapePlan(fp, nparam=1, max_batch=600)
+    F, Fdx, _, _ = big.fidelity_grad(X)
+    big.close()
+    one = GrapePlan(fp, nparam=1, max_batch=1)
+    for b in (0, 299, 599):
+        Fs, gs, _, _ = one.fidelity_grad(X[b][None, :])
+        assert abs(Fs[0] - F[b]) <= T1 and np.max(np.abs(gs[0] - Fdx[b])) <= T2 * np.max(np.abs(gs[0])) + T2_ABS
+    one.close()
