@@ -1,18 +1,23 @@
 // grape_kernels.hpp -- the hot-path kernels (small-d row-group engine).
 //
-//   k_expm    one row group per (eval b, step k, variant v): builds
-//             A = -i dt H(x_b,k perturbed by v) from the operator basis and
-//             computes E = exp(A) (Pade m <= 9 in registers); m = 13 items are
-//             parked for k_expm13.                      UnitaryCalculations.jl:45,51,59
-//   k_expm13  m = 13 scaling-and-squaring for parked items.
-//   k_scan    one workgroup per eval: chunked prefix product of the nominal
-//             propagators (local chains + Hillis-Steele over chunk totals),
-//             fidelity F, the gradient kernel M = G U and the per-chunk
-//             M'_c = Carry_c M Carry_c^dagger.         UnitaryCalculations.jl:46-47,99
-//                                                        FidelityCalculations.jl:32-54
-//   k_grad    one row group per (b, k): Z_k = (C_{k-1} M C_k^dagger)^T and
-//             F_dx[p,k] = Re sum(Z_k o dE_{k,p}).     FidelityCalculations.jl:56-76
-//   k_reduce_add  sum over k of the x_add contributions (only when H0 depends on x_add).
+//   k_expm       one row group per (eval b, step k, variant v): builds column i
+//                of A = -i dt H(x_b,k perturbed by v) from the operator basis and
+//                computes E = exp(A) in column form (Pade m <= 5 here; m > 5 items
+//                are parked for k_expm_high).   UnitaryCalculations.jl:45,51,59-90
+//                Without error sources only the nominal v = 0 is launched.
+//   k_expm_high  Pade 7/9/13 (+ squarings) for parked items.
+//   k_scan       one workgroup per eval: chunked prefix product of the nominal
+//                propagators (local chains + Hillis-Steele over chunk totals),
+//                fidelity F, the gradient kernel M = G U and the per-chunk
+//                M'_c = Carry_c M Carry_c^dagger.   UnitaryCalculations.jl:46-47,99
+//                                                   FidelityCalculations.jl:32-54
+//   k_expm_grad  (no error sources) one row group per (b, k, eps-variant u): exp of
+//                the variant and, in place, F_dx[u,k] = Re sum(Z_k o dE) with
+//                Z_k = (C_{k-1} M C_k^dagger)^T.   FidelityCalculations.jl:56-76
+//   k_grad_high  the same for its parked (Pade m > 5) items.
+//   k_grad       (error-source pipeline) one row group per (b, k): Z_k and the
+//                traces against every stored variant.
+//   k_reduce_add sum over k of the x_add contributions (only when H0 depends on x_add).
 //
 // Gradient algebra (verified against the reference formulas at rounding level):
 //   F_dx[p,k] = Re tr(G U_dx[p,k]),  G = 2(P K^dag + conj(tau) I) W U0^dag / (D(D+1)),
