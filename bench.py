@@ -2,9 +2,10 @@
 
 One step = one fidelity+gradient evaluation of every restart this rank owns
 (SURVEY.md 8d C2 problem; restarts r with x_main = 2pi*0.001*U, theta = 2pi*U,
-seed 1000+r as config C4), inputs resident in HBM, followed by the restart
-sweep's exchange: one all_gather of (best F, restart id) over RCCL when N > 1.
-Weak scaling: every rank owns --batch restarts.
+seed 1000+r as config C4), inputs resident in HBM. After the K timed steps, still
+inside the timed region, the sweep's exchange (robustgrape_amd/sweep.py): one
+all_gather of (best F, restart id) over RCCL and a broadcast of the winning x,
+when N > 1.  Weak scaling: every rank owns --batch restarts.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -132,28 +133,24 @@ def main():
     dev = torch.device("cuda", local)
 
     from robustgrape_amd.engine import GrapePlan
+    from robustgrape_amd.sweep import gather_best, shard
     fp = problem()
     B = args.batch
-    plan = GrapePlan(fp, nparam=1, device=local, max_batch=B)
-    X = torch.from_numpy(restart_inputs(rank * B, B)).to(dev)
-    F = torch.empty(B, dtype=torch.float64, device=dev)
-    Fdx = torch.empty(B, X.shape[1], dtype=torch.float64, device=dev)
-    ids = torch.arange(rank * B, rank * B + B, device=dev, dtype=torch.float64)
-    gathered = torch.empty(world * 2, dtype=torch.float64, device=dev)
+    first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
+    plan = GrapePlan(fp, nparam=1, device=local, max_batch=count)
+    X = torch.from_numpy(restart_inputs(first, count)).to(dev)
+    F = torch.empty(count, dtype=torch.float64, device=dev)
+    Fdx = torch.empty(count, X.shape[1], dtype=torch.float64, device=dev)
+    ids = torch.arange(first, first + count, device=dev)
 
-    # The evaluation is enqueued on torch's current stream, so the sweep exchange
-    # below is stream-ordered behind it and steps queue back to back without a
-    # host round trip; the timed region still ends with a full synchronize.
+    # The evaluation is enqueued on one torch stream, so steps queue back to back without
+    # a host round trip; the timed region still ends with a full synchronize.
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     plan.set_stream(stream.cuda_stream)
 
     def step():
-        plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), B)
-        if world > 1:  # restart sweep exchange: best (F, id) of every rank
-            best = torch.argmax(F)
-            mine = torch.stack([F[best], ids[best]])
-            dist.all_gather_into_tensor(gathered, mine)
+        plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), count)
 
     for _ in range(args.warmup):
         step()
@@ -167,7 +164,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if world > 1:
+    best = None
+    if world > 1:  # the sweep's exchange: all_gather of (best F, id), winner broadcasts its x
+        best = gather_best(F, ids, X)
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -209,6 +208,18 @@ def main():
                          "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch},
             "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items()},
         }
+        # whole-evaluation view: FLOP of the work executed per evaluation
+        # (nominal + one eps-variant exp per step, chain + contraction products), and the
+        # survey's canonical C2 figure, which also counts the x_add-variant exps this engine
+        # skips because H0 does not read x_add (their differences are exactly zero)
+        exe = NT * ((1 + nvg) * flops_expm(D) + 3 * 8 * D ** 3 + nvg * 8 * D ** 2)
+        canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
+        out["roofline"]["whole_eval"] = {
+            "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
+            "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
+            "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+        if best is not None:
+            out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -1,0 +1,61 @@
+"""Random-restart sweep across GPUs: one process per GPU, restarts sharded in contiguous
+blocks, no communication inside the evaluation loop, one exchange per sweep step
+(SURVEY.md 8(e)):
+
+  1. all_gather of (best F, restart id) from every rank (world x 16 B over RCCL/xGMI);
+  2. broadcast of the winning control vector from the rank that owns it.
+
+The evaluation itself is `GrapePlan.fidelity_grad_device_async` on each rank's block
+of restarts; nothing here touches the kernels.  Works with the "nccl" (RCCL) backend on
+device tensors and with "gloo" on host tensors (the CPU tests use gloo, world_size 2).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous block of restarts owned by `rank`: (first, count). Blocks differ in
+    size by at most one; every restart is owned by exactly one rank."""
+    if n_total < 0 or world < 1 or not 0 <= rank < world:
+        raise ValueError("bad shard arguments")
+    base, extra = divmod(n_total, world)
+    first = rank * base + min(rank, extra)
+    return first, base + (1 if rank < extra else 0)
+
+
+def local_best(F: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """(F_best, id) of this rank as a 2-vector (float64); an empty shard reports (-inf, -1).
+    Ties go to the smallest restart id."""
+    if F.numel() == 0:
+        return torch.tensor([float("-inf"), -1.0], dtype=torch.float64, device=F.device)
+    fmax = torch.max(F)
+    cand = torch.where(F == fmax, ids.to(torch.float64), torch.full_like(F, float("inf")))
+    return torch.stack([fmax.to(torch.float64), torch.min(cand)])
+
+
+def gather_best(F: torch.Tensor, ids: torch.Tensor, X: torch.Tensor | None = None, group=None):
+    """Global best over all ranks. Returns (F_best, restart_id, owner_rank, x_best or None).
+
+    One all_gather of every rank's (F_best, id); ties go to the smallest restart id (so the
+    answer does not depend on the world size). When X (this rank's (count, n_x) block, rows
+    in `ids` order) is given, the owner broadcasts the winning row to every rank."""
+    world = dist.get_world_size(group)
+    mine = local_best(F, ids)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    allp = torch.stack(parts)                                  # (world, 2)
+    fbest = torch.max(allp[:, 0])
+    cand = torch.where(allp[:, 0] == fbest, allp[:, 1], torch.full_like(allp[:, 1], float("inf")))
+    rid = torch.min(cand)
+    owner = int(torch.nonzero(allp[:, 1] == rid)[0, 0].item())
+    xb = None
+    if X is not None:
+        if dist.get_rank(group) == owner:
+            row = int(torch.nonzero(ids.to(torch.float64) == rid)[0, 0].item())
+            xb = X[row].clone()
+        else:
+            xb = torch.empty(X.shape[1], dtype=X.dtype, device=X.device)
+        dist.broadcast(xb, src=dist.get_global_rank(group, owner) if group is not None else owner, group=group)
+    return float(fbest.item()), int(rid.item()), owner, xb
