@@ -15,13 +15,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrape.so")
-SOURCES = [os.path.join(CSRC, "grape_engine.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp")] + \
+OBJ = os.path.join(HERE, "_obj")
+ENGINE = os.path.join(CSRC, "grape_engine.hip")
+INST = os.path.join(CSRC, "grape_inst.hip")
+DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
+SOURCES = [ENGINE, INST]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in
+                  ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GRAPE_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
          # no implicit FMA contraction: the reference (Julia) never fuses; the
          # kernels use explicit fma() where fusion is intended (complex MACs)
          "-ffp-contract=off",
@@ -35,15 +40,45 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
 
 
+def _units(defines):
+    """(source, extra -D flags, object path): the C ABI + one object per dimension."""
+    tag = "_".join(d.replace("=", "") for d in defines)
+    sub = os.path.join(OBJ, tag or "default")
+    units = [(ENGINE, [], os.path.join(sub, "grape_engine.o"))]
+    units += [(INST, [f"-DGRAPE_INST_DIM={d}"], os.path.join(sub, f"grape_inst_d{d}.o")) for d in DIMS]
+    return sub, units
+
+
 def build_library(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
-    """Build libgrape.so (or a variant with extra -D defines into `out`, for tuning runs)."""
+    """Build libgrape.so (or a variant with extra -D defines into `out`, for tuning runs).
+
+    Every translation unit is compiled in parallel (one per dimension D: the
+    kernels are templates on D), then linked into one shared library."""
     if out == LIB and not defines and not force and not needs_build():
         return LIB
-    tmp = out + ".tmp"
-    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + SOURCES + ["-o", tmp]
+    sub, units = _units(defines)
+    os.makedirs(sub, exist_ok=True)
     if verbose:
-        print("[robustgrape_amd] building", os.path.relpath(out, ROOT), *defines, flush=True)
-    subprocess.run(cmd, check=True)
+        print("[robustgrape_amd] building", os.path.relpath(out, ROOT), *defines,
+              f"({len(units)} translation units)", flush=True)
+    dflags = [f"-D{d}" for d in defines]
+    jobs = max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+    pending = list(units)
+    running = []
+    failed = []
+    while pending or running:
+        while pending and len(running) < jobs:
+            src, extra, obj = pending.pop(0)
+            cmd = [HIPCC] + FLAGS + dflags + extra + ["-c", src, "-o", obj]
+            running.append((subprocess.Popen(cmd), obj))
+        proc, obj = running.pop(0)
+        if proc.wait() != 0:
+            failed.append(obj)
+    if failed:
+        raise RuntimeError("hipcc failed for " + ", ".join(os.path.basename(f) for f in failed))
+    tmp = out + ".tmp"
+    subprocess.run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + [u[2] for u in units] + ["-o", tmp],
+                   check=True)
     os.replace(tmp, out)
     return out
 

@@ -714,6 +714,7 @@ __global__ __launch_bounds__(64) void k_grad_high(DevProblem P, DevBatch B) {
 }
 
 // F_dx_add = target part + sum_k per-step contributions (xadd_dep only)
+template <int D>
 __global__ void k_reduce_add(DevProblem P, DevBatch B) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= B.nb * P.na) return;

@@ -1,0 +1,143 @@
+// grape_launch.hpp -- host-side launch sequences of the small-d engine, one
+// instantiation per compile-time dimension D.  Each D is compiled in its own
+// translation unit (grape_inst.hip with -DGRAPE_INST_DIM=D) so the build runs
+// in parallel; grape_engine.hip only sees the declarations (extern template).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "grape.h"
+#include "grape_errpath.hpp"
+
+namespace grape_host {
+
+using grape::cd;
+using grape::DevBatch;
+using grape::DevProblem;
+
+// Scan workgroups: one per evaluation, W waves of row groups.  W = 8 (52 chunks
+// of L = 10 steps at d = 9, N_t = 512) has the shortest chains; W = 4 halves
+// the LDS and registers per block so two evaluations share a CU, which wins
+// once there are more evaluations than CUs (plan-time choice, see kScanWide).
+constexpr int kScanWide = 8, kScanNarrow = 4;
+
+template <int D>
+size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
+template <int D>
+size_t errscan_lds(int W) {
+    return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 4 * grape::Geo<D>::TILE) * sizeof(cd);
+}
+template <int D>
+size_t scan_lds(int W) {
+    return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 3 * grape::Geo<D>::TILE) * sizeof(cd);
+}
+
+// ---------------------------------------------------------------------------
+// dispatch helpers over the compile-time dimension
+// ---------------------------------------------------------------------------
+// Optional per-kernel event marks (profiling mode): fn(ctx, kernel, 0|1) around each launch.
+struct KMark {
+    void *ctx = nullptr;
+    void (*fn)(void *, int, int) = nullptr;
+    void operator()(int k, int phase) const {
+        if (fn) fn(ctx, k, phase);
+    }
+};
+
+template <int D>
+hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mark) {
+    constexpr int GPW = grape::Geo<D>::GPW;
+    const long nexp = (long)B.nb * P.Nt * P.nv;
+    const bool fused = P.ne == 0;  // eps-variants exp'd and contracted in k_expm_grad
+    mark(GRAPE_KERNEL_EXPM, 0);
+    if (!fused)
+        hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+    mark(GRAPE_KERNEL_EXPM, 1);
+    mark(GRAPE_KERNEL_EXPM_HIGH, 0);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
+                       B.overflow_count, B.status, 1);
+    mark(GRAPE_KERNEL_EXPM_HIGH, 1);
+    mark(GRAPE_KERNEL_SCAN, 0);
+    if (P.scan_waves == kScanNarrow)
+        hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
+                           scan_lds<D>(kScanNarrow), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide),
+                           st, P, B);
+    mark(GRAPE_KERNEL_SCAN, 1);
+    if (fused) {
+        const int nvg = P.np + (P.xadd_dep ? P.na : 0);
+        const long ng = (long)B.nb * P.Nt * nvg;
+        mark(GRAPE_KERNEL_EXPM_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(),
+                           st, P, B);
+        mark(GRAPE_KERNEL_EXPM_GRAD, 1);
+        mark(GRAPE_KERNEL_GRAD_HIGH, 0);
+        hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_GRAD_HIGH, 1);
+    } else {
+        const long ng = (long)B.nb * P.Nt;
+        mark(GRAPE_KERNEL_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
+                           P, B);
+        mark(GRAPE_KERNEL_GRAD, 1);
+    }
+    if (P.ne > 0) {
+        mark(GRAPE_KERNEL_ERR_SCAN, 0);
+        if (P.scan_waves == kScanNarrow)
+            hipLaunchKernelGGL((grape::k_err_scan<D, kScanNarrow>), dim3(B.nb * P.ne), dim3(64 * kScanNarrow),
+                               errscan_lds<D>(kScanNarrow), st, P, B);
+        else
+            hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
+                               errscan_lds<D>(kScanWide), st, P, B);
+        mark(GRAPE_KERNEL_ERR_SCAN, 1);
+        const long ne_items = (long)B.nb * P.nchunks * P.ne;
+        mark(GRAPE_KERNEL_ERR_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_err_grad<D>, dim3((unsigned)((ne_items + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_ERR_GRAD, 1);
+    }
+    if (P.xadd_dep && P.na > 0) {
+        mark(GRAPE_KERNEL_REDUCE, 0);
+        hipLaunchKernelGGL(grape::k_reduce_add<D>, dim3((B.nb * P.na + 255) / 256), dim3(256), 0, st, P, B);
+        mark(GRAPE_KERNEL_REDUCE, 1);
+    }
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_expm_raw(const cd *A, cd *E, int n, int *ovf, int *ovf_count, int *status, int *mstats,
+                           hipStream_t st) {
+    constexpr int GPW = grape::Geo<D>::GPW;
+    hipLaunchKernelGGL(grape::k_expm_raw<D>, dim3((n + GPW - 1) / GPW), dim3(64), expm_lds<D>(), st, A, E, n, ovf,
+                       ovf_count, status, mstats);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, E, ovf, ovf_count, status, 0);
+    return hipGetLastError();
+}
+
+template <int D, int W>
+hipError_t set_lds_limits_w() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, W>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>(W));
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_err_scan<D, W>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)errscan_lds<D>(W));
+}
+template <int D>
+hipError_t set_lds_limits() {
+    hipError_t e = set_lds_limits_w<D, kScanWide>();
+    return e != hipSuccess ? e : set_lds_limits_w<D, kScanNarrow>();
+}
+
+
+#define GRAPE_DIMS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+
+#define GRAPE_DECLARE_DIM(d, EXT)                                                                          \
+    EXT template hipError_t launch_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &); \
+    EXT template hipError_t launch_expm_raw<d>(const cd *, cd *, int, int *, int *, int *, int *, hipStream_t);  \
+    EXT template hipError_t set_lds_limits<d>();
+
+}  // namespace grape_host
