@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 1
+#define GRAPE_ABI_VERSION 2
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -47,8 +47,13 @@ typedef enum grape_status {
     GRAPE_ERR_NO_DEVICE = -6    /* no usable GPU */
 } grape_status;
 
-/* Largest Hilbert-space dimension served by the small-d (VALU) engine. */
+/* Largest Hilbert-space dimension served by the small-d (VALU row-group) engine. */
 #define GRAPE_MAX_SMALL_DIM 12
+/* Largest dimension served by the dense (MFMA) engine, used for
+ * GRAPE_MAX_SMALL_DIM < ndim <= GRAPE_MAX_DENSE_DIM (zero-padded to 64).  It
+ * requires a Hermitian H0 operator basis (Hermitian operators, real
+ * coefficients), no error sources and an H0 independent of x_add. */
+#define GRAPE_MAX_DENSE_DIM 64
 
 /*
  * Operator-basis description of the reference's Hamiltonian closures.
@@ -200,7 +205,12 @@ typedef enum grape_kernel {
     GRAPE_KERNEL_ERR_GRAD = 6,  /* error sources: F_d2err_dx contractions */
     GRAPE_KERNEL_EXPM_GRAD = 7, /* no error sources: eps-variant propagators contracted in place */
     GRAPE_KERNEL_GRAD_HIGH = 8, /* Pade m > 5 items parked by the above */
-    GRAPE_NUM_KERNELS = 9
+    GRAPE_KERNEL_DEXP = 9,      /* dense engine: nominal propagators (MFMA) */
+    GRAPE_KERNEL_DSCAN = 10,    /* dense engine: chunk-local prefix products */
+    GRAPE_KERNEL_DCARRY = 11,   /* dense engine: carries, U, F, M = G U */
+    GRAPE_KERNEL_DMC = 12,      /* dense engine: per-chunk M'_c */
+    GRAPE_KERNEL_DGRAD = 13,    /* dense engine: eps-variant propagators contracted in place */
+    GRAPE_NUM_KERNELS = 14
 } grape_kernel;
 
 int grape_plan_set_profiling(grape_plan *plan, int enable);
@@ -208,7 +218,8 @@ int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launc
 
 /*
  * Batched matrix exponential exp(A) of n column-major ndim x ndim complex
- * matrices on `device`, with the reference's algorithm (Julia
+ * matrices (2 <= ndim <= GRAPE_MAX_DENSE_DIM; above GRAPE_MAX_SMALL_DIM the
+ * dense engine's solve needs a skew-Hermitian A, see grape_dense.hpp) on `device`, with the reference's algorithm (Julia
  * LinearAlgebra.exp!: Pade degree by 1-norm, gesv, squaring).  Host buffers.
  * stats (optional, 5 ints) receives how many matrices used Pade m=3,5,7,9,13.
  */

@@ -22,7 +22,8 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
-                "k_expm_grad", "k_grad_high"]
+                "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
+ABI_VERSION = 2  # GRAPE_ABI_VERSION in include/grape.h
 
 
 class GrapeError(RuntimeError):
@@ -69,7 +70,7 @@ def lib():
         L.grape_plan_set_profiling.restype = ctypes.c_int
         L.grape_plan_kernel_times.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.grape_plan_kernel_times.restype = ctypes.c_int
-        if L.grape_abi_version() != 1:
+        if L.grape_abi_version() != ABI_VERSION:
             raise ImportError("libgrape.so ABI version mismatch")
         _lib = L
     return _lib

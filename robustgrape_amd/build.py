@@ -18,10 +18,12 @@ LIB = os.path.join(HERE, "libgrape.so")
 OBJ = os.path.join(HERE, "_obj")
 ENGINE = os.path.join(CSRC, "grape_engine.hip")
 INST = os.path.join(CSRC, "grape_inst.hip")
+DENSE = os.path.join(CSRC, "grape_dense.hip")
 DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
-SOURCES = [ENGINE, INST]
+SOURCES = [ENGINE, INST, DENSE]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
-                  ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp")] + \
+                  ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp",
+                   "grape_dense.hpp", "grape_dense_api.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -44,7 +46,7 @@ def _units(defines):
     """(source, extra -D flags, object path): the C ABI + one object per dimension."""
     tag = "_".join(d.replace("=", "") for d in defines)
     sub = os.path.join(OBJ, tag or "default")
-    units = [(ENGINE, [], os.path.join(sub, "grape_engine.o"))]
+    units = [(DENSE, [], os.path.join(sub, "grape_dense.o")), (ENGINE, [], os.path.join(sub, "grape_engine.o"))]
     units += [(INST, [f"-DGRAPE_INST_DIM={d}"], os.path.join(sub, f"grape_inst_d{d}.o")) for d in DIMS]
     return sub, units
 

@@ -1,0 +1,612 @@
+// grape_dense.hpp -- CDNA4 (gfx950) building blocks of the DENSE engine
+// (13 <= d <= 64; SURVEY.md 8d config C5, the dense-GEMM regime).
+//
+// One workgroup of 8 waves (two per SIMD) owns one 64 x 64 complex FP64 matrix problem at a
+// time (smaller d is zero-padded to 64: exp, products and the fidelity are
+// unchanged by a zero block with zero weight).  Every d x d complex product is
+// four real GEMMs on v_mfma_f64_16x16x4_f64 (16 x 16 output, K = 4, one f64 per
+// lane for A and B, 4 f64 accumulators per lane):
+//
+//   A fragment (16 x 4):  lane l holds A[l & 15][l >> 4]
+//   B fragment (4 x 16):  lane l holds B[l >> 4][l & 15]
+//   C tile (16 x 16):     lane l, element r holds C[(l >> 4) + 4r][l & 15]
+//
+// (checked on the hardware with exact integer data, scripts/probes/mfma_probe.hip).
+// Element r of a C tile is therefore the B fragment of k-rows 4r..4r+3: a
+// matrix kept in registers in C-tile layout IS the right operand of the next
+// product, with no data movement.  Register matrices (HM) are distributed by
+// tile: wave (w, h) holds columns 16w..16w+15 of row tiles 2h and 2h+1 (2 C
+// tiles, re and im: 32 VGPRs per complex matrix, so an exponential keeps its
+// five live matrices in registers at two waves per SIMD).  A product
+// P = L . R reads both operands from LDS (A and B fragments); each wave
+// computes its own two tiles of P.
+//
+// LDS matrices (SM) are two row-major 64 x 64 double planes with the column
+// swizzle  col ^ (((row & 15) << 1) ^ ((row & 1) << 4)):  C-tile stores
+// (16 contiguous columns of one row per 16 lanes), A-fragment reads of L and
+// of L^T, and B-fragment reads of R and R^T are all bank-conflict free
+// (gfx950 ds_read_b64: two 32-lane groups over 64 banks; ds_write_b64: four
+// 16-lane groups over 32 banks).
+//
+// HBM images: a complex matrix is stored as its register file, plane by plane
+// (re then im), index ((w*4 + t)*4 + r)*64 + lane: a wave loads or stores its
+// 16 KB as 32 fully coalesced 512-B rows.
+//
+// The matrix exponential follows Julia's LinearAlgebra.exp! (Pade degree by
+// 1-norm thresholds 0.015/0.25/0.95/2.1, else Pade 13 with squarings; U and
+// V as in exp!; X = (V-U) \ (V+U)).  The solve is a blocked Gauss-Jordan
+// elimination WITHOUT row interchanges, all on MFMA (4 block steps of 16
+// columns; the 16 x 16 diagonal block is inverted by one wave).  That is safe
+// here: for a Hermitian H (checked at plan creation) A = -i dt H is
+// skew-Hermitian, the Pade denominator q(A) = V - U has Hermitian part V with
+// eigenvalues Re q(i theta) = |q(i theta)| cos(theta/2) > 0 for
+// |theta| <= |A|_2 <= |A|_1 < pi, so every leading block and Schur complement
+// is nonsingular with bounded growth (no pivoting needed).  For Pade 13 the
+// scaling is raised, if necessary, until |A/2^s|_1 <= 1.6 (Julia: 5.4) to keep
+// that margin; the result differs from exp! by rounding only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "grape_kernels.hpp"
+
+namespace grape_dense {
+
+using grape::cd;
+using grape::Term;
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+constexpr int N = 64;          // padded dimension
+constexpr int NT = 4;          // 16-row tiles per dimension
+constexpr int NW = 8;          // waves per workgroup: (column block w, row half h)
+constexpr int NTHREADS = 64 * NW;
+constexpr int PLANE = N * N;   // doubles per plane
+constexpr int IMG = 2 * PLANE; // doubles per complex matrix image (64 KB)
+constexpr int SMALL = 16 * 16; // doubles per plane of a 16 x 16 block
+
+// LDS (doubles): matrix region 0 | matrix region 1 | reduction scratch
+constexpr int LDS_R0 = 0;
+constexpr int LDS_R1 = 2 * PLANE;
+constexpr int LDS_RED = 4 * PLANE;
+constexpr int LDS_TOTAL = LDS_RED + 2 * N + 16;
+// Gauss-Jordan buffers overlay region 0 (even block steps) and region 1 (odd)
+constexpr int GJ_DINV = 0;                        // D^-1: 2 planes x 16 x 16
+constexpr int GJ_PCOL = GJ_DINV + 2 * SMALL;      // -Q[:, block kb]: 2 planes x 64 x 16
+constexpr int GJ_NR = GJ_PCOL + 2 * 4 * SMALL;    // new row block: [w][q|p][plane][16 x 16]
+constexpr int GJ_SET = GJ_NR + 4 * 2 * 2 * SMALL; // 6 656 doubles <= 2 * PLANE
+static_assert(GJ_SET <= 2 * PLANE, "GJ buffers must fit one matrix region");
+
+struct HM {
+    v4d re[2];  // tiles 2h, 2h+1 of column block w
+    v4d im[2];
+};
+
+struct SM {
+    double *re, *im;
+};
+
+__device__ __forceinline__ SM sm_at(double *lds, int off) {
+    SM s;
+    s.re = lds + off;
+    s.im = lds + off + PLANE;
+    return s;
+}
+
+__device__ __forceinline__ int sidx(int row, int col) {
+    return row * N + (col ^ (((row & 15) << 1) ^ ((row & 1) << 4)));
+}
+// 64 x 16 / 16 x 16 buffers read as A fragments: conflict-free with this swizzle
+__device__ __forceinline__ int sidx16(int row, int col) { return row * 16 + (col ^ (row & 14)); }
+
+__device__ __forceinline__ v4d mfma(double a, double b, v4d c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+struct Lane {
+    int l;    // lane in the wave
+    int w;    // column block (wave-uniform)
+    int h;    // row half: tiles 2h, 2h+1 (wave-uniform)
+    int wid;  // wave in the workgroup
+    __device__ __forceinline__ int tile(int i) const { return 2 * h + i; }
+    __device__ __forceinline__ int row(int i, int r) const { return 16 * (2 * h + i) + (l >> 4) + 4 * r; }
+    __device__ __forceinline__ int col() const { return 16 * w + (l & 15); }
+    __device__ __forceinline__ int img(int i, int r) const { return ((w * NT + 2 * h + i) * 4 + r) * 64 + l; }
+};
+
+__device__ __forceinline__ Lane make_lane() {
+    Lane L;
+    L.l = threadIdx.x & 63;
+    L.wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    L.w = L.wid & 3;
+    L.h = L.wid >> 2;
+    return L;
+}
+
+__device__ __forceinline__ void hm_zero(HM &M) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        M.re[i] = v4d{0.0, 0.0, 0.0, 0.0};
+        M.im[i] = v4d{0.0, 0.0, 0.0, 0.0};
+    }
+}
+
+__device__ __forceinline__ void hm_identity(HM &M, const Lane &ln, double s) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            M.re[i][r] = ln.row(i, r) == ln.col() ? s : 0.0;
+            M.im[i][r] = 0.0;
+        }
+}
+
+// M += c X
+__device__ __forceinline__ void hm_axpy(HM &M, double c, const HM &X) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            M.re[i][r] = fma(c, X.re[i][r], M.re[i][r]);
+            M.im[i][r] = fma(c, X.im[i][r], M.im[i][r]);
+        }
+}
+
+__device__ __forceinline__ void hm_scale(HM &M, double c) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        M.re[i] *= c;
+        M.im[i] *= c;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// HBM images and LDS stores
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void img_load(const double *img, HM &M, const Lane &ln) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            M.re[i][r] = img[ln.img(i, r)];
+            M.im[i][r] = img[PLANE + ln.img(i, r)];
+        }
+}
+
+__device__ __forceinline__ void img_store(double *img, const HM &M, const Lane &ln) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            img[ln.img(i, r)] = M.re[i][r];
+            img[PLANE + ln.img(i, r)] = M.im[i][r];
+        }
+}
+
+__device__ __forceinline__ void sm_store(SM S, const HM &M, const Lane &ln) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = sidx(ln.row(i, r), ln.col());
+            S.re[o] = M.re[i][r];
+            S.im[o] = M.im[i][r];
+        }
+}
+
+// ---------------------------------------------------------------------------
+// P += op(L) . op(R), both operands in LDS (LT/RT: transpose, LC/RC: conjugate).
+// Wave (w, h) computes tiles (2h, w), (2h+1, w): 16 k-steps x 8 MFMAs.
+// ---------------------------------------------------------------------------
+template <bool LC>
+__device__ __forceinline__ void cmfma2(HM &P, const double (&aR)[2], const double (&aI)[2], double bR, double bI) {
+    // (aR + i aI)(bR + i bI), with aI -> -aI for conj(L)
+    const double xR = LC ? bI : -bI;  // coefficient of aI in the real part
+    const double xI = LC ? -bR : bR;  // coefficient of aI in the imaginary part
+#pragma unroll
+    for (int i = 0; i < 2; ++i) P.re[i] = mfma(aR[i], bR, P.re[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) P.im[i] = mfma(aR[i], bI, P.im[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) P.re[i] = mfma(aI[i], xR, P.re[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) P.im[i] = mfma(aI[i], xI, P.im[i]);
+}
+
+template <bool LT, bool LC, bool RT, bool RC>
+__device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        double aR[2], aI[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ir = 16 * ln.tile(i) + (ln.l & 15), kc = 4 * s + (ln.l >> 4);
+            const int o = LT ? sidx(kc, ir) : sidx(ir, kc);
+            aR[i] = L.re[o];
+            aI[i] = L.im[o];
+        }
+        const int kr = 4 * s + (ln.l >> 4), jc = ln.col();
+        const int o = RT ? sidx(jc, kr) : sidx(kr, jc);
+        const double bR = R.re[o];
+        const double bI = RC ? -R.im[o] : R.im[o];
+        cmfma2<LC>(P, aR, aI, bR, bI);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup reductions (fixed order: deterministic)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wg_sum(double v, double *lds, const Lane &ln) {
+    double *red = lds + LDS_RED + 2 * N;
+    v = wave_sum(v);
+    __syncthreads();  // slots free
+    if (ln.l == 0) red[ln.wid] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
+}
+
+// |A|_1 = max_j sum_i |a_ij| (Julia opnorm(A, 1)), identical in every wave
+__device__ __forceinline__ double wg_norm1(const HM &A, double *lds, const Lane &ln) {
+    double *red = lds + LDS_RED;
+    double cs = 0.0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs += hypot(A.re[i][r], A.im[i][r]);
+    cs += __shfl_xor(cs, 16, 64);
+    cs += __shfl_xor(cs, 32, 64);
+    __syncthreads();  // slots free
+    if (ln.l < 16) red[ln.h * N + ln.col()] = cs;
+    __syncthreads();
+    return wave_max(red[ln.l] + red[N + ln.l]);
+}
+
+// ---------------------------------------------------------------------------
+// Operator-basis builder: M += c OP (OP image in HBM)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void hm_cmac_img(HM &M, cd c, const double *img, const Lane &ln) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double orr = img[ln.img(i, r)], oi = img[PLANE + ln.img(i, r)];
+            double re = M.re[i][r], im = M.im[i][r];
+            re = fma(c.re, orr, re);
+            re = fma(-c.im, oi, re);
+            im = fma(c.re, oi, im);
+            im = fma(c.im, orr, im);
+            M.re[i][r] = re;
+            M.im[i][r] = im;
+        }
+}
+
+// ---------------------------------------------------------------------------
+// 16 x 16 complex inverse by one wave (Gauss-Jordan without interchanges; the
+// block has a positive definite Hermitian part, see the header).  In and out
+// in C-tile layout: lane l holds column l & 15, rows (l >> 4) + 4r.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ cd crecip_smith(cd z) {
+    if (fabs(z.re) >= fabs(z.im)) {
+        const double q = z.im / z.re, den = z.re + z.im * q;
+        return grape::cmake(1.0 / den, -q / den);
+    }
+    const double q = z.re / z.im, den = z.im + z.re * q;
+    return grape::cmake(q / den, -1.0 / den);
+}
+
+__device__ __forceinline__ void wave_inv16(v4d &Dr, v4d &Di, v4d &Xr, v4d &Xi, int l, bool &singular) {
+    const int c = l & 15, g = l >> 4;
+    double dr[4], di[4], xr[4], xi[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        dr[r] = Dr[r];
+        di[r] = Di[r];
+        xr[r] = (g + 4 * r) == c ? 1.0 : 0.0;
+        xi[r] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int kr = k >> 2, kg = k & 3;
+        // pivot D[k][k] (lane k + 16 kg, element kr) and the pivot-row entries of my column
+        const double pr = __shfl(dr[kr], k + 16 * kg, 64), pi = __shfl(di[kr], k + 16 * kg, 64);
+        const int src = c + 16 * kg;
+        const double rr = __shfl(dr[kr], src, 64), ri = __shfl(di[kr], src, 64);
+        const double er = __shfl(xr[kr], src, 64), ei = __shfl(xi[kr], src, 64);
+        double mr[4], mi[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            mr[r] = __shfl(dr[r], k + 16 * g, 64);
+            mi[r] = __shfl(di[r], k + 16 * g, 64);
+        }
+        if (pr == 0.0 && pi == 0.0) singular = true;
+        const cd inv = crecip_smith(grape::cmake(pr, pi));
+        const cd rs = grape::cmulf(grape::cmake(rr, ri), inv);
+        const cd es = grape::cmulf(grape::cmake(er, ei), inv);
+        const bool prow = g == kg;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // a -= m * (scaled pivot row); the pivot row becomes it
+            const bool piv = prow && (r == kr);
+            const double nr = fma(-mr[r], rs.re, fma(mi[r], rs.im, dr[r]));
+            const double ni = fma(-mr[r], rs.im, fma(-mi[r], rs.re, di[r]));
+            const double nxr = fma(-mr[r], es.re, fma(mi[r], es.im, xr[r]));
+            const double nxi = fma(-mr[r], es.im, fma(-mi[r], es.re, xi[r]));
+            dr[r] = piv ? rs.re : nr;
+            di[r] = piv ? rs.im : ni;
+            xr[r] = piv ? es.re : nxr;
+            xi[r] = piv ? es.im : nxi;
+        }
+        // one step at a time: keeps the compiler from overlapping steps (register blow-up)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(dr[r]), "+v"(di[r]), "+v"(xr[r]), "+v"(xi[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        Dr[r] = dr[r];
+        Di[r] = di[r];
+        Xr[r] = xr[r];
+        Xi[r] = xi[r];
+    }
+}
+
+// (aR + i aI)(bR + i bI) accumulated into (cr, ci)
+__device__ __forceinline__ void cmfma1(v4d &cr, v4d &ci, double aR, double aI, double bR, double bI) {
+    cr = mfma(aR, bR, cr);
+    ci = mfma(aR, bI, ci);
+    cr = mfma(aI, -bI, cr);
+    ci = mfma(aI, bR, ci);
+}
+
+// ---------------------------------------------------------------------------
+// Solve Q X = Pm in place (X returned in Pm): blocked Gauss-Jordan on MFMA.
+// Block step kb:
+//   1. wave (kb, kb/2) inverts the diagonal block D; waves (kb, *) publish
+//      -Q[:, block kb] (the multipliers);
+//   2. waves holding row block kb replace it by D^-1 (row block) and publish it;
+//   3. every wave subtracts Q[t-block, kb-block] (new row block) from its tiles.
+// Q's column blocks left of or at kb are never read again: skipped (w <= kb).
+// Buffers alternate between the two LDS matrix regions (no trailing barrier).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void gj_solve(HM &Q, HM &Pm, double *lds, const Lane &ln, bool &singular) {
+    __syncthreads();  // the matrix regions are free
+#pragma unroll
+    for (int kb = 0; kb < NT; ++kb) {
+        double *set = lds + ((kb & 1) ? LDS_R1 : LDS_R0);
+        double *dvr = set + GJ_DINV, *dvi = dvr + SMALL;
+        double *pcr = set + GJ_PCOL, *pci = pcr + 4 * SMALL;
+        double *nr = set + GJ_NR;
+        const int hk = kb >> 1, ik = kb & 1;
+        const bool owner_row = ln.h == hk;  // holds row block kb of column block w (tile ik)
+        if (ln.w == kb) {
+            if (owner_row) {
+                v4d dr = Q.re[ik], di = Q.im[ik], xr, xi;
+                wave_inv16(dr, di, xr, xi, ln.l, singular);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int o = sidx16((ln.l >> 4) + 4 * r, ln.l & 15);
+                    dvr[o] = xr[r];
+                    dvi[o] = xi[r];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (ln.tile(i) == kb) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int o = sidx16(ln.row(i, r), ln.l & 15);
+                    pcr[o] = -Q.re[i][r];
+                    pci[o] = -Q.im[i][r];
+                }
+            }
+        }
+        __syncthreads();
+        const bool doq = ln.w > kb;
+        double *nq = nr + (ln.w * 2 + 0) * 2 * SMALL, *np = nr + (ln.w * 2 + 1) * 2 * SMALL;
+        if (owner_row) {
+            v4d nqr = {0, 0, 0, 0}, nqi = {0, 0, 0, 0}, npr = {0, 0, 0, 0}, npi = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int o = sidx16(ln.l & 15, 4 * s + (ln.l >> 4));
+                const double aR = dvr[o], aI = dvi[o];
+                cmfma1(npr, npi, aR, aI, Pm.re[ik][s], Pm.im[ik][s]);
+                if (doq) cmfma1(nqr, nqi, aR, aI, Q.re[ik][s], Q.im[ik][s]);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = ((ln.l >> 4) + 4 * r) * 16 + (ln.l & 15);
+                np[o] = npr[r];
+                np[SMALL + o] = npi[r];
+                if (doq) {
+                    nq[o] = nqr[r];
+                    nq[SMALL + o] = nqi[r];
+                }
+            }
+            Pm.re[ik] = npr;
+            Pm.im[ik] = npi;
+            if (doq) {
+                Q.re[ik] = nqr;
+                Q.im[ik] = nqi;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int t = ln.tile(i);
+            if (t == kb) continue;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int oa = sidx16(16 * t + (ln.l & 15), 4 * s + (ln.l >> 4));
+                const int ob = (4 * s + (ln.l >> 4)) * 16 + (ln.l & 15);
+                const double aR = pcr[oa], aI = pci[oa];
+                cmfma1(Pm.re[i], Pm.im[i], aR, aI, np[ob], np[SMALL + ob]);
+                if (doq) cmfma1(Q.re[i], Q.im[i], aR, aI, nq[ob], nq[SMALL + ob]);
+            }
+        }
+    }
+    __syncthreads();  // regions free for the caller
+}
+
+// ---------------------------------------------------------------------------
+// Pade tables (Julia LinearAlgebra.exp!) and the degree choice
+// ---------------------------------------------------------------------------
+__constant__ const double kDPade[5][14] = {
+    {120.0, 60.0, 12.0, 1.0},
+    {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0},
+    {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0},
+    {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0, 2162160.0, 110880.0, 3960.0, 90.0, 1.0},
+    {64764752532480000.0, 32382376266240000.0, 7771770303897600.0, 1187353796428800.0, 129060195264000.0,
+     10559470521600.0, 670442572800.0, 33522128640.0, 1323241920.0, 40840800.0, 960960.0, 16380.0, 182.0, 1.0}};
+
+// Julia's (m, s) for |A|_1, with the Pade-13 scaling raised until |A/2^s|_1 <= 1.6
+// (keeps Re q(i theta) > 0 with margin: no-interchange solve, see the header)
+__device__ __forceinline__ int dense_pade_degree(double nA, int &s) {
+    s = 0;
+    if (nA <= 2.1) {
+        if (nA > 0.95) return 9;
+        if (nA > 0.25) return 7;
+        if (nA > 0.015) return 5;
+        return 3;
+    }
+    const double l = log2(nA / 5.4);
+    if (l > 0.0) s = (int)ceil(l);
+    const double l2 = log2(nA / 1.6);
+    const int s2 = l2 > 0.0 ? (int)ceil(l2) : 0;
+    if (s2 > s) s = s2;
+    return 13;
+}
+
+__device__ __forceinline__ int m_index(int m) { return m == 3 ? 0 : m == 5 ? 1 : m == 7 ? 2 : m == 9 ? 3 : 4; }
+
+// ---------------------------------------------------------------------------
+// X = exp(A) for the workgroup's matrix A (registers; consumed).  Uses all of
+// LDS [0, LDS_TOTAL).  Returns the Pade degree m.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wg_expm(HM &A, HM &X, double *lds, const Lane &ln, bool &singular) {
+    SM S0 = sm_at(lds, LDS_R0), S1 = sm_at(lds, LDS_R1);
+    const double nA = wg_norm1(A, lds, ln);
+    int s = 0;
+    const int m = dense_pade_degree(nA, s);
+    const double *C = kDPade[m_index(m)];
+    if (s > 0) hm_scale(A, ldexp(1.0, -s));
+    HM U, V;
+    if (m <= 9) {
+        // exp!: A2 = A*A; P = I; U = c1 P; V = c0 P; repeat P *= A2; U += c_{2k+1} P;
+        // V += c_{2k} P; U = A*U
+        __syncthreads();
+        sm_store(S0, A, ln);
+        __syncthreads();
+        HM A2;
+        hm_zero(A2);
+        mm<false, false, false, false>(S0, S0, A2, ln);
+        hm_identity(U, ln, C[1]);
+        hm_identity(V, ln, C[0]);
+        hm_axpy(U, C[3], A2);
+        hm_axpy(V, C[2], A2);
+        const int nk = (m + 1) / 2;
+        if (nk > 2) {
+            __syncthreads();
+            sm_store(S0, A2, ln);  // L = A2 for every further power
+            __syncthreads();
+            HM P;
+            hm_zero(P);
+            mm<false, false, false, false>(S0, S0, P, ln);  // A4
+            hm_axpy(U, C[5], P);
+            hm_axpy(V, C[4], P);
+            for (int kk = 3; kk < nk; ++kk) {
+                __syncthreads();
+                sm_store(S1, P, ln);
+                __syncthreads();
+                HM Pn;
+                hm_zero(Pn);
+                mm<false, false, false, false>(S0, S1, Pn, ln);  // A2 . P
+                P = Pn;
+                hm_axpy(U, C[2 * kk + 1], P);
+                hm_axpy(V, C[2 * kk], P);
+            }
+        }
+    } else {
+        // exp! Pade 13: U = A (A6 (c13 A6 + c11 A4 + c9 A2) + c7 A6 + c5 A4 + c3 A2 + c1 I),
+        //               V = A6 (c12 A6 + c10 A4 + c8 A2) + c6 A6 + c4 A4 + c2 A2 + c0 I
+        HM A2, A4, W1, Z1;
+        __syncthreads();
+        sm_store(S0, A, ln);
+        __syncthreads();
+        hm_zero(A2);
+        mm<false, false, false, false>(S0, S0, A2, ln);
+        __syncthreads();
+        sm_store(S0, A2, ln);
+        __syncthreads();
+        hm_zero(A4);
+        mm<false, false, false, false>(S0, S0, A4, ln);
+        sm_store(S1, A4, ln);  // region 1 unused so far
+        hm_zero(W1);
+        hm_zero(Z1);
+        hm_identity(U, ln, C[1]);
+        hm_identity(V, ln, C[0]);
+        hm_axpy(W1, C[11], A4);
+        hm_axpy(W1, C[9], A2);
+        hm_axpy(Z1, C[10], A4);
+        hm_axpy(Z1, C[8], A2);
+        hm_axpy(U, C[5], A4);
+        hm_axpy(U, C[3], A2);
+        hm_axpy(V, C[4], A4);
+        hm_axpy(V, C[2], A2);
+        __syncthreads();
+        HM A6;
+        hm_zero(A6);
+        mm<false, false, false, false>(S0, S1, A6, ln);  // A2 . A4
+        hm_axpy(W1, C[13], A6);
+        hm_axpy(Z1, C[12], A6);
+        hm_axpy(U, C[7], A6);
+        hm_axpy(V, C[6], A6);
+        __syncthreads();
+        sm_store(S0, A6, ln);
+        sm_store(S1, W1, ln);
+        __syncthreads();
+        mm<false, false, false, false>(S0, S1, U, ln);  // U += A6 W1
+        __syncthreads();
+        sm_store(S1, Z1, ln);
+        __syncthreads();
+        mm<false, false, false, false>(S0, S1, V, ln);  // V += A6 Z1
+    }
+    __syncthreads();
+    sm_store(S0, A, ln);
+    sm_store(S1, U, ln);
+    __syncthreads();
+    {
+        HM Uf;
+        hm_zero(Uf);
+        mm<false, false, false, false>(S0, S1, Uf, ln);  // U = A U
+        U = Uf;
+    }
+    // Q = V - U, X = V + U: solve Q X' = X
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const v4d ur = U.re[i], ui = U.im[i], vr = V.re[i], vi = V.im[i];
+        U.re[i] = vr - ur;
+        U.im[i] = vi - ui;
+        V.re[i] = vr + ur;
+        V.im[i] = vi + ui;
+    }
+    gj_solve(U, V, lds, ln, singular);
+    for (int q = 0; q < s; ++q) {
+        sm_store(S0, V, ln);
+        __syncthreads();
+        HM Sq;
+        hm_zero(Sq);
+        mm<false, false, false, false>(S0, S0, Sq, ln);
+        V = Sq;
+        __syncthreads();
+    }
+    X = V;
+    return m;
+}
+
+}  // namespace grape_dense

@@ -1,0 +1,43 @@
+// grape_dense_api.hpp -- what the C ABI (grape_engine.hip) sees of the dense
+// engine (grape_dense.hip): the problem / batch descriptors and the launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "grape_launch.hpp"
+
+namespace grape_dense {
+
+// Scalars and term tables are shared with the small-d engine (DevProblem:
+// ops/opsT/vs unused here); the operator basis is stored as padded 64 x 64
+// register-file images (grape_dense.hpp).
+struct DenseProblem {
+    grape::DevProblem P;
+    const double *opimg;  // [n_ops][IMG]
+    const double *W;      // [64] projector diagonal, zero-padded
+    int Lc, Nc;           // chunk length / count of the prefix-product scan
+};
+
+struct DenseBatch {
+    int nb;
+    const double *x;  // [nb][nx]
+    double *E;        // [nb][Nt][IMG]   nominal propagators
+    double *Q;        // [nb][Nt][IMG]   chunk-local prefix products
+    double *Carry;    // [nb][Nc][IMG]   C_{cL-1} (identity for c = 0)
+    double *M;        // [nb][IMG]       gradient kernel M = G U
+    double *Mc;       // [nb][Nc][IMG]   Carry_c M Carry_c^dagger
+    double *F;        // [nb]
+    double *Fdx;      // [nb][nx]
+    int *status;      // bit 0: singular Pade denominator
+    int *mstats;      // optional [5]: Pade degree histogram (m = 3, 5, 7, 9, 13)
+};
+
+constexpr int kImgDoubles = 2 * 64 * 64;
+
+// Pipeline of one batch (k_dexp, k_dscan, k_dcarry, k_dmc, k_dgrad) on `st`.
+hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream_t st,
+                           const grape_host::KMark &mark);
+// n exponentials of padded images (grape_expm_batch for 12 < d <= 64).
+hipError_t launch_expm_raw(const double *A, double *E, int n, int *status, int *mstats, hipStream_t st);
+hipError_t set_lds_limits();
+
+}  // namespace grape_dense

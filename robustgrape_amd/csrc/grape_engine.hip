@@ -18,6 +18,7 @@
 
 #include "grape.h"
 #include "grape_launch.hpp"
+#include "grape_dense_api.hpp"
 
 // instantiated in grape_inst.hip (one translation unit per dimension)
 namespace grape_host {
@@ -114,6 +115,11 @@ struct grape_plan {
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
+    // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
+    bool dense = false;
+    grape_dense::DenseProblem DP{};
+    double *dn_opimg = nullptr, *dn_W = nullptr, *dn_E = nullptr, *dn_Q = nullptr, *dn_Carry = nullptr,
+           *dn_M = nullptr, *dn_Mc = nullptr;
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -141,7 +147,8 @@ static void free_plan(grape_plan *p) {
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl,
-                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots};
+                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots,
+                    p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -171,6 +178,109 @@ static int validate_terms(const grape_term *t, int n, int n_ops, int np, int na,
     return GRAPE_OK;
 }
 
+// ---------------------------------------------------------------------------
+// dense engine plan (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
+// ---------------------------------------------------------------------------
+// column-major interleaved d x d complex -> zero-padded 64 x 64 register-file image
+static void to_dense_image(const double *src, int d, double *img) {
+    const int P = 64 * 64;
+    for (int w = 0; w < 4; ++w)
+        for (int t = 0; t < 4; ++t)
+            for (int r = 0; r < 4; ++r)
+                for (int l = 0; l < 64; ++l) {
+                    const int row = 16 * t + (l >> 4) + 4 * r, col = 16 * w + (l & 15);
+                    const int o = ((w * 4 + t) * 4 + r) * 64 + l;
+                    const bool in = row < d && col < d;
+                    img[o] = in ? src[2 * ((size_t)row + (size_t)col * d)] : 0.0;
+                    img[P + o] = in ? src[2 * ((size_t)row + (size_t)col * d) + 1] : 0.0;
+                }
+}
+static void from_dense_image(const double *img, int d, double *dst) {
+    const int P = 64 * 64;
+    for (int w = 0; w < 4; ++w)
+        for (int t = 0; t < 4; ++t)
+            for (int r = 0; r < 4; ++r)
+                for (int l = 0; l < 64; ++l) {
+                    const int row = 16 * t + (l >> 4) + 4 * r, col = 16 * w + (l & 15);
+                    if (row >= d || col >= d) continue;
+                    const int o = ((w * 4 + t) * 4 + r) * 64 + l;
+                    dst[2 * ((size_t)row + (size_t)col * d)] = img[o];
+                    dst[2 * ((size_t)row + (size_t)col * d) + 1] = img[P + o];
+                }
+}
+
+static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, double trP) {
+    const int D = desc->ndim;
+    if (desc->nerr > 0)
+        return fail(GRAPE_ERR_UNSUPPORTED, "dense engine (ndim > GRAPE_MAX_SMALL_DIM): error sources not supported");
+    if (xadd_dep) return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 must not depend on x_add");
+    // Hermitian H0 (see grape_dense.hpp: the no-interchange solve relies on it)
+    for (int k = 0; k < desc->n_h0_terms; ++k) {
+        const grape_term &t = desc->h0_terms[k];
+        if (t.scale_im != 0.0 || t.func == GRAPE_FN_CIS)
+            return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 coefficients must be real");
+        const double *op = desc->ops + 2 * (size_t)t.op * D * D;
+        double mx = 0.0, dev = 0.0;
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j) {
+                const double *a = op + 2 * ((size_t)i + (size_t)j * D), *b = op + 2 * ((size_t)j + (size_t)i * D);
+                mx = std::max(mx, std::hypot(a[0], a[1]));
+                dev = std::max(dev, std::hypot(a[0] - b[0], a[1] + b[1]));
+            }
+        if (dev > 1e-12 * std::max(mx, 1e-300))
+            return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 operators must be Hermitian");
+    }
+    if (grape_dense::set_lds_limits() != hipSuccess) return fail(GRAPE_ERR_HIP, "cannot raise LDS limit (dense)");
+    p->dense = true;
+    grape_dense::DenseProblem &DP = p->DP;
+    DevProblem &P = DP.P;
+    P.D = D;
+    P.Nt = desc->ntimes;
+    P.np = desc->nparam;
+    P.na = desc->nadd;
+    P.ne = 0;
+    P.nx = desc->nparam * desc->ntimes + desc->nadd;
+    P.nv = 1;
+    P.n_h0 = desc->n_h0_terms;
+    P.n_tgt = desc->n_target_terms;
+    P.dt = desc->t0 / desc->ntimes;
+    P.eps = desc->eps;
+    P.eps2 = desc->eps2;
+    P.inv_eps = 1.0 / desc->eps;
+    P.DD = trP * (trP + 1.0);
+    P.Dtr = trP;
+    // scan chunking: ~sqrt(N_t) chunks balances the chunk chains against the carry chain
+    int nc = (int)std::ceil(std::sqrt((double)P.Nt));
+    DP.Lc = (P.Nt + nc - 1) / nc;
+    DP.Nc = (P.Nt + DP.Lc - 1) / DP.Lc;
+    const size_t IMG = grape_dense::kImgDoubles, MB = p->max_batch;
+    std::vector<double> img((size_t)desc->n_ops * IMG), W(64, 0.0);
+    for (int o = 0; o < desc->n_ops; ++o) to_dense_image(desc->ops + 2 * (size_t)o * D * D, D, img.data() + o * IMG);
+    for (int i = 0; i < D; ++i) W[i] = desc->projector_diag[i];
+    bool ok = dalloc(&p->dn_opimg, img.size()) == hipSuccess && dalloc(&p->dn_W, (size_t)64) == hipSuccess &&
+              dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
+              dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess &&
+              dalloc(&p->dn_E, MB * P.Nt * IMG) == hipSuccess && dalloc(&p->dn_Q, MB * P.Nt * IMG) == hipSuccess &&
+              dalloc(&p->dn_Carry, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_M, MB * IMG) == hipSuccess &&
+              dalloc(&p->dn_Mc, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
+              dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
+              dalloc(&p->d_ctrl, 4) == hipSuccess;
+    if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense)");
+    if (hipMemset(p->d_ctrl, 0, 4 * sizeof(int)) != hipSuccess ||
+        hipMemcpy(p->dn_opimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->dn_W, W.data(), 64 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
+            hipSuccess)
+        return fail(GRAPE_ERR_HIP, "upload failed (dense)");
+    P.h0 = p->d_h0;
+    P.tgt = p->d_tgt;
+    DP.opimg = p->dn_opimg;
+    DP.W = p->dn_W;
+    p->P = P;  // the C ABI reads nx / np / ne from the plan's problem for every engine
+    return GRAPE_OK;
+}
+
 extern "C" {
 
 int grape_abi_version(void) { return GRAPE_ABI_VERSION; }
@@ -189,7 +299,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     const int D = desc->ndim;
     if (D < 2 || desc->ntimes < 1 || desc->nparam < 1 || desc->nadd < 0 || desc->nerr < 0 || desc->n_ops < 1)
         return fail(GRAPE_ERR_INVALID, "bad dimensions in descriptor");
-    if (D > GRAPE_MAX_SMALL_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim > GRAPE_MAX_SMALL_DIM");
+    if (D > GRAPE_MAX_DENSE_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim > GRAPE_MAX_DENSE_DIM");
     if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
     if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || !desc->projector_diag || !desc->target_terms ||
         desc->n_target_terms < 1)
@@ -240,6 +350,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (hipHostMalloc(reinterpret_cast<void **>(&p->h_status), sizeof(int), hipHostMallocDefault) != hipSuccess)
         return bail(fail(GRAPE_ERR_ALLOC, "pinned allocation failed"));
     *p->h_status = 0;
+    if (D > GRAPE_MAX_SMALL_DIM) {
+        const int rcd = create_dense(desc, p, xadd_dep, trP);
+        if (rcd) return bail(rcd);
+        *out = p;
+        return GRAPE_OK;
+    }
     if (dispatch_lds_limits(D) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
 
     DevProblem &P = p->P;
@@ -380,6 +496,38 @@ int grape_plan_set_stream(grape_plan *plan, void *stream) {
 
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
                    double *d_Fd2dx) {
+    KMark mk;
+    if (p->profiling) {
+        mk.ctx = p;
+        mk.fn = [](void *ctx, int k, int phase) {
+            grape_plan *pl = static_cast<grape_plan *>(ctx);
+            hipEvent_t e = pl->get_event();
+            if (!e) return;
+            (void)hipEventRecord(e, pl->stream);
+            if (phase == 0) {
+                pl->pending.push_back({k, e, nullptr});
+            } else {
+                pl->pending.back().b = e;
+            }
+        };
+    }
+    if (p->dense) {
+        grape_dense::DenseBatch DB{};
+        DB.nb = nb;
+        DB.x = d_x;
+        DB.E = p->dn_E;
+        DB.Q = p->dn_Q;
+        DB.Carry = p->dn_Carry;
+        DB.M = p->dn_M;
+        DB.Mc = p->dn_Mc;
+        DB.F = d_F;
+        DB.Fdx = d_Fdx;
+        DB.status = p->d_ctrl + 2;
+        DB.mstats = nullptr;
+        HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, p->stream, mk));
+        HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+        return GRAPE_OK;
+    }
     DevBatch B{};
     B.Carry = p->d_Carry;
     B.Ub = p->d_Ub;
@@ -404,21 +552,6 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     // ctrl: [0] k_expm overflow count, [1] k_expm_grad overflow count, [2] status
     // (sticky until grape_plan_synchronize reports it; copied to pinned memory below)
     HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), p->stream));
-    KMark mk;
-    if (p->profiling) {
-        mk.ctx = p;
-        mk.fn = [](void *ctx, int k, int phase) {
-            grape_plan *pl = static_cast<grape_plan *>(ctx);
-            hipEvent_t e = pl->get_event();
-            if (!e) return;
-            (void)hipEventRecord(e, pl->stream);
-            if (phase == 0) {
-                pl->pending.push_back({k, e, nullptr});
-            } else {
-                pl->pending.back().b = e;
-            }
-        };
-    }
     HIPCHECK(dispatch_pipeline(p->P.D, p->P, B, p->stream, mk));
     HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return GRAPE_OK;
@@ -521,8 +654,48 @@ int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx
     return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs is not implemented in this build");
 }
 
+static int dense_expm_batch(int device, int ndim, int n, const double *A, double *E, int *stats) {
+    const size_t IMG = grape_dense::kImgDoubles;
+    std::vector<double> h((size_t)n * IMG);
+    for (int i = 0; i < n; ++i) to_dense_image(A + 2 * (size_t)i * ndim * ndim, ndim, h.data() + i * IMG);
+    double *dA = nullptr, *dE = nullptr;
+    int *dctrl = nullptr;
+    auto cleanup = [&]() {
+        (void)hipFree(dA); (void)hipFree(dE); (void)hipFree(dctrl);
+    };
+    if (dalloc(&dA, n * IMG) || dalloc(&dE, n * IMG) || dalloc(&dctrl, 8)) {
+        cleanup();
+        return fail(GRAPE_ERR_ALLOC, "device allocation failed");
+    }
+    int rc = GRAPE_OK;
+    int ctrl[8] = {0};
+    if (grape_dense::set_lds_limits() != hipSuccess ||
+        hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(dctrl, 0, 8 * sizeof(int)) != hipSuccess ||
+        grape_dense::launch_expm_raw(dA, dE, n, dctrl + 1, dctrl + 2, nullptr) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h.data(), dE, h.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ctrl, dctrl, 8 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(GRAPE_ERR_HIP, std::string("dense expm batch failed: ") + hipGetErrorString(hipGetLastError()));
+    cleanup();
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i) from_dense_image(h.data() + i * IMG, ndim, E + 2 * (size_t)i * ndim * ndim);
+    if (stats)
+        for (int k = 0; k < 5; ++k) stats[k] = ctrl[2 + k];
+    if (ctrl[1] & 1) return fail(GRAPE_ERR_SINGULAR, "singular Pade denominator");
+    return GRAPE_OK;
+}
+
 int grape_expm_batch(int device, int ndim, int n, const double *A, double *E, int *stats) {
-    if (ndim < 2 || ndim > GRAPE_MAX_SMALL_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim outside [2, GRAPE_MAX_SMALL_DIM]");
+    if (ndim < 2 || ndim > GRAPE_MAX_DENSE_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim outside [2, GRAPE_MAX_DENSE_DIM]");
+    if (ndim > GRAPE_MAX_SMALL_DIM) {
+        if (n < 0 || (n > 0 && (!A || !E))) return fail(GRAPE_ERR_INVALID, "bad argument");
+        if (n == 0) return GRAPE_OK;
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GRAPE_ERR_NO_DEVICE, "no HIP device");
+        HIPCHECK(hipSetDevice(device));
+        return dense_expm_batch(device, ndim, n, A, E, stats);
+    }
     if (n < 0 || (n > 0 && (!A || !E))) return fail(GRAPE_ERR_INVALID, "bad argument");
     if (n == 0) return GRAPE_OK;
     int ndev = 0;

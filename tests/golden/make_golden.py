@@ -103,5 +103,20 @@ def main():
         print("wrote", name)
 
 
+def make_c5():
+    """SURVEY.md 8d C5 (d = 64, N_t = 1024, np = 2; robustgrape_amd/synthetic.py), with the
+    oracle's (m, s) Pade histogram.  Separate entry point: ~1 min of oracle time."""
+    from robustgrape_amd import synthetic as S
+    st = {}
+    x = S.dense_x()
+    F, Fdx, _, _ = O.calculate_fidelity_and_derivatives(S.dense_problem(), x, st)
+    hist = np.array([[m, s, n] for (m, s), n in sorted(st.items())], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "c5.npz"), x=x, F=np.float64(F), F_dx=Fdx, pade_hist=hist)
+    print("wrote c5", F, hist.tolist())
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["c5"]:
+        make_c5()
+    else:
+        main()

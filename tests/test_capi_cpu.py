@@ -27,7 +27,8 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) == set(_capi.EXPORTED)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.grape_abi_version() == 1
+    assert L.grape_abi_version() == _capi.ABI_VERSION == 2
+    assert len(_capi.KERNEL_NAMES) == 14  # GRAPE_NUM_KERNELS
 
 
 def test_descriptor_packing_roundtrip():

@@ -1,0 +1,135 @@
+"""GPU parity of the dense (MFMA) engine, 12 < d <= 64,
+through the C ABI, against the CPU oracle (live, small sizes) and the committed
+C5 golden fixture (d = 64, N_t = 1024).
+
+Tolerances (SURVEY.md 8c tiers):
+  T0  exp(A)          <= 1e-13 relative x max(1, |A|_1); Pade 13 (where this engine
+                       takes extra squarings to keep its pivot-free solve safe) 1e-12
+  T1  F               <= 1e-12 absolute
+  T2  F_dx            <= 1e-6 max|ref| + 1e-7
+"""
+import os
+
+import numpy as np
+import pytest
+
+from robustgrape_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T1 = 1e-12
+T2, T2_ABS = 1e-6, 1e-7
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _assert_fid(F, Fdx, ref_F, ref_Fdx):
+    assert abs(F - ref_F) <= T1, (F, ref_F)
+    err = np.max(np.abs(Fdx - ref_Fdx))
+    assert err <= T2 * np.max(np.abs(ref_Fdx)) + T2_ABS, (err, np.max(np.abs(ref_Fdx)))
+
+
+def _skew_hermitian(d, norm, rng):
+    H = rng.normal(size=(d, d)) + 1j * rng.normal(size=(d, d))
+    H = (H + H.conj().T) / 2
+    return -1j * H / np.abs(H).sum(axis=0).max() * norm
+
+
+@pytest.mark.parametrize("d", [13, 24, 64])
+def test_dense_expm_matches_oracle_every_pade_degree(d):
+    from oracle import grape_oracle as O
+    from robustgrape_amd import _capi
+    rng = np.random.default_rng(1000 + d)
+    norms = (0.01, 0.2, 0.6, 1.5, 4.0, 30.0)
+    A = np.stack([_skew_hermitian(d, nm, rng) for nm in norms])
+    refs, ms = [], []
+    for a in A:
+        st = {}
+        refs.append(O.julia_exp(a, st))
+        ms.append(list(st)[0][0])
+    Acm = np.ascontiguousarray(A.transpose(0, 2, 1))  # column-major per matrix
+    E = np.empty_like(Acm)
+    stats = (_capi.ctypes.c_int * 5)()
+    _capi.check(_capi.lib().grape_expm_batch(0, d, len(A), _capi.dptr(Acm), _capi.dptr(E), stats))
+    E = E.transpose(0, 2, 1)
+    for j, nm in enumerate(norms):
+        rel = np.max(np.abs(E[j] - refs[j])) / np.max(np.abs(refs[j]))
+        tol = (1e-12 if ms[j] == 13 else 1e-13) * max(1.0, nm)
+        assert rel <= tol, (d, nm, ms[j], rel)
+        # unitary to rounding
+        assert np.max(np.abs(E[j].conj().T @ E[j] - np.eye(d))) < 1e-12 * max(1.0, nm)
+    hist = {3: 0, 5: 1, 7: 2, 9: 3, 13: 4}
+    expect = [0] * 5
+    for m in ms:
+        expect[hist[m]] += 1
+    assert list(stats) == expect
+
+
+@pytest.mark.parametrize("d,ntimes,scale", [(13, 1, 1.0), (16, 5, 1.0), (24, 17, 0.3), (40, 9, 2.0),
+                                            (64, 3, 1.0), (64, 37, 1.0), (64, 20, 0.05)])
+def test_dense_fidelity_gradient_matches_live_oracle(d, ntimes, scale):
+    """Edge sizes: one step, chunk remainders, padded d, Pade 3..9 (scale moves |A|_1)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = S.dense_problem(d, ntimes, rank=min(16, d - 3), scale=scale)
+    x = S.dense_x(ntimes, seed=300 + ntimes)
+    F0, g0, _, _ = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0)
+    assert d2.shape == (0,) and d2dx.shape == (len(x), 0)
+
+
+def test_c5_matches_golden():
+    """d = 64, N_t = 1024, np = 2 (oracle fixture from tests/golden/make_golden.py)."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    g = dict(np.load(os.path.join(GOLDEN, "c5.npz"), allow_pickle=False))
+    F, Fdx, _, _ = calculate_fidelity_and_derivatives(S.dense_problem(), g["x"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+
+
+def test_dense_batch_equals_single():
+    """Deterministic kernels: a batch element is bitwise the single evaluation."""
+    from robustgrape_amd.engine import GrapePlan
+    fp = S.dense_problem(64, 48)
+    X = np.stack([S.dense_x(48, seed=s) for s in range(5)])
+    plan = GrapePlan(fp, nparam=2, max_batch=5)
+    F, Fdx, _, _ = plan.fidelity_grad(X)
+    plan.close()
+    one = GrapePlan(fp, nparam=2, max_batch=2)  # ragged: 2 + 2 + 1 through one plan
+    F1, Fdx1, _, _ = one.fidelity_grad(X)
+    one.close()
+    assert np.array_equal(F, F1) and np.array_equal(Fdx, Fdx1)
+
+
+def test_dense_fd_identity():
+    """runtests.jl:292-354 on the dense path: forward difference of F vs F_dx."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = S.dense_problem(32, 24)
+    x = S.dense_x(24, seed=5)
+    F0, g0, _, _ = calculate_fidelity_and_derivatives(fp, x)
+    for idx in (0, 17, 47):
+        xs = x.copy()
+        xs[idx] += 1e-6
+        F1 = calculate_fidelity_and_derivatives(fp, xs)[0]
+        np.testing.assert_allclose((F1 - F0) / 1e-6, g0[idx], rtol=1e-3, atol=1e-6)
+
+
+def test_dense_rejects_what_it_does_not_serve():
+    from robustgrape_amd import _capi
+    from robustgrape_amd.engine import GrapePlan
+    from robustgrape_amd.operators import OperatorBasisError, OperatorBasisHamiltonian, Term
+    from robustgrape_amd.types import ErrorSource
+    fp = S.dense_problem(20, 4)
+    up = fp.unitary_problem
+    errs = (ErrorSource(OperatorBasisError([Term(np.eye(20, dtype=complex))])),)
+    with pytest.raises(_capi.GrapeError, match="UNSUPPORTED"):
+        GrapePlan(fp.replace(unitary_problem=up.replace(error_sources=errs)), nparam=2)
+    H = np.triu(np.ones((20, 20), complex))  # not Hermitian
+    bad = up.replace(H0=OperatorBasisHamiltonian([Term(H)]))
+    with pytest.raises(_capi.GrapeError, match="UNSUPPORTED"):
+        GrapePlan(fp.replace(unitary_problem=bad), nparam=2)
