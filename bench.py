@@ -49,6 +49,12 @@ def restart_inputs(first, count):
     return np.stack(xs)
 
 
+def c5_inputs(first, count):
+    """C5 restarts: x ~ U[-1, 1) with seed 67 + r (r = 0 is the golden fixture's x)."""
+    from robustgrape_amd import synthetic as S
+    return np.stack([S.dense_x(seed=67 + r) for r in range(first, first + count)])
+
+
 def flops_expm(d, m=5, s=0):
     """Algorithmic FP64 flops of one d x d complex Pade-m exp ((pi_m + s + 5/3) * 8 d^3)."""
     pi = {3: 2, 5: 3, 7: 4, 9: 5, 13: 6}[m]
@@ -56,21 +62,22 @@ def flops_expm(d, m=5, s=0):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
 
 
-def pmc_traffic(kernel, batch):
+def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
     """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_profile.sh:
     separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), if it was
     recorded at this batch size; else None."""
     try:
-        with open(PMC_SUMMARY) as fh:
+        with open(path) as fh:
             js = json.load(fh)
     except (OSError, ValueError):
         return None
     if js.get("batch") != batch:
         return None
     for name, row in js.get("kernels", {}).items():
-        if name.split("<")[0] == kernel and "hbm_bytes_per_launch" in row:
+        if name.split("<")[0].split("::")[-1] == kernel and "hbm_bytes_per_launch" in row:
             return row["hbm_bytes_per_launch"]
     return None
 
@@ -111,12 +118,88 @@ def cpu_baseline(seconds=15.0):
             "sample": f"{n} sequential C2 evaluations by the numpy restatement oracle/grape_oracle.py, 1 thread"}
 
 
+def _roofline(kname, flop_launch, ktimes, batch, pmc_path=PMC_SUMMARY):
+    ms_k, n_k = ktimes[kname]
+    per_launch_ms = ms_k / max(1, n_k)
+    achieved = flop_launch / (per_launch_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": kname, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+            "traffic": pmc_traffic(kname, batch, pmc_path), "traffic_unit": "HBM bytes per launch (PMC)",
+            "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch}
+
+
+def c2_report(args, B, world, value, elapsed, ktimes):
+    # algorithmic flops per launch of the two exp-carrying kernels:
+    # k_expm exps the nominal step propagators (B*NT items); k_expm_grad exps each
+    # eps-variant (np=1 control; H0 does not read x_add, so no x_add variants) and
+    # contracts it: Z_k = conj(Q_k) M'^T Q_{k-1}^T (2 complex products) + Re<Z, dE>.
+    nvg = 1
+    flop_model = {"k_expm": B * NT * flops_expm(D),
+                  "k_expm_grad": B * NT * nvg * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)}
+    kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
+    out = {
+        "metric": "GRAPE gradient-evals/sec (fidelity+∇), Rydberg CZ d=9 N_t=512, 1→8 GPU",
+        "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
+                               "np=1, na=1, ne=0; restart sweep",
+                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, B),
+                         pipe="fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"),
+        "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
+    }
+    # whole-evaluation view: FLOP of the work executed per evaluation
+    # (nominal + one eps-variant exp per step, chain + contraction products), and the
+    # survey's canonical C2 figure, which also counts the x_add-variant exps this engine
+    # skips because H0 does not read x_add (their differences are exactly zero)
+    exe = NT * ((1 + nvg) * flops_expm(D) + 3 * 8 * D ** 3 + nvg * 8 * D ** 2)
+    canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
+    out["roofline"]["whole_eval"] = {
+        "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
+        "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
+        "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    return out
+
+
+def c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam):
+    # C5 draws Pade m = 7 for every exponential (tests/golden/c5.npz pade_hist); per launch:
+    # k_dexp: B*nt nominal exps; k_dgrad: per step 2 products (Q_{k-1} M'_c, Z_k) and, per
+    # control, one eps-variant exp + the contraction; k_dscan: one product per step.
+    fe = flops_expm(d, 7)
+    flop_model = {"k_dexp": B * nt * fe,
+                  "k_dgrad": B * nt * (2 * 8 * d ** 3 + nparam * (fe + 8 * d ** 2)),
+                  "k_dscan": B * nt * 8 * d ** 3}
+    kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
+    out = {
+        "metric": "GRAPE gradient-evals/sec (fidelity+∇), synthetic d=64 N_t=1024 (SURVEY C5)",
+        "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C5: d=64 Hermitian Ginibre basis, N_t=1024, dt=0.5, np=2, na=0, ne=0",
+                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, B, PMC_SUMMARY_C5),
+                         pipe="fp64 MFMA v_mfma_f64_16x16x4_f64"),
+        "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
+    }
+    # SURVEY.md 8d canonical FLOP per C5 evaluation (na = 0, ne = 0: the survey's exp count
+    # N_t (1 + np) is exactly what this engine executes)
+    canon = nt * ((1 + nparam) * fe + 3 * 8 * d ** 3 + nparam * 8 * d ** 2)
+    out["roofline"]["whole_eval"] = {"flop_per_eval": canon, "achieved": canon * value / 1e12,
+                                     "frac": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="restarts per GPU (one device pass each step)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="restarts per GPU (one device pass each step); default 1024 (c2), 4 (c5)")
+    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
+                    help="c2: the BASELINE metric (d=9 Rydberg CZ); c5: synthetic d=64, N_t=1024 "
+                         "(dense MFMA engine, SURVEY.md 8d C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -134,11 +217,16 @@ def main():
 
     from robustgrape_amd.engine import GrapePlan
     from robustgrape_amd.sweep import gather_best, shard
-    fp = problem()
-    B = args.batch
+    c5 = args.workload == "c5"
+    if c5:
+        from robustgrape_amd import synthetic as S
+        fp, nparam, d, nt, inputs = S.dense_problem(), 2, S.C5_DIM, S.C5_NTIMES, c5_inputs
+    else:
+        fp, nparam, d, nt, inputs = problem(), 1, D, NT, restart_inputs
+    B = args.batch or (4 if c5 else 1024)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
-    plan = GrapePlan(fp, nparam=1, device=local, max_batch=count)
-    X = torch.from_numpy(restart_inputs(first, count)).to(dev)
+    plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=count)
+    X = torch.from_numpy(inputs(first, count)).to(dev)
     F = torch.empty(count, dtype=torch.float64, device=dev)
     Fdx = torch.empty(count, X.shape[1], dtype=torch.float64, device=dev)
     ids = torch.arange(first, first + count, device=dev)
@@ -181,46 +269,13 @@ def main():
     value = evals / elapsed
     ktimes = plan.kernel_times()
     if rank == 0:
-        # algorithmic flops per launch of the two exp-carrying kernels:
-        # k_expm exps the nominal step propagators (B*NT items); k_expm_grad exps each
-        # eps-variant (np=1 control; H0 does not read x_add, so no x_add variants) and
-        # contracts it: Z_k = conj(Q_k) M'^T Q_{k-1}^T (2 complex products) + Re<Z, dE>.
-        nvg = 1
-        flop_model = {"k_expm": B * NT * flops_expm(D),
-                      "k_expm_grad": B * NT * nvg * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)}
-        kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
-        ms_k, n_k = ktimes[kname]
-        per_launch_ms = ms_k / max(1, n_k)
-        flop_launch = flop_model[kname]
-        achieved = flop_launch / (per_launch_ms * 1e-3) / 1e12
-        out = {
-            "metric": "GRAPE gradient-evals/sec (fidelity+∇), Rydberg CZ d=9 N_t=512, 1→8 GPU",
-            "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
-                                   "np=1, na=1, ne=0; restart sweep",
-                       "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
-            "roofline": {"bound": "mfma", "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)",
-                         "kernel": kname, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(kname, B), "traffic_unit": "HBM bytes per launch (PMC)",
-                         "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch},
-            "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items()},
-        }
-        # whole-evaluation view: FLOP of the work executed per evaluation
-        # (nominal + one eps-variant exp per step, chain + contraction products), and the
-        # survey's canonical C2 figure, which also counts the x_add-variant exps this engine
-        # skips because H0 does not read x_add (their differences are exactly zero)
-        exe = NT * ((1 + nvg) * flops_expm(D) + 3 * 8 * D ** 3 + nvg * 8 * D ** 2)
-        canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
-        out["roofline"]["whole_eval"] = {
-            "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
-            "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
-            "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+        if c5:
+            out = c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam)
+        else:
+            out = c2_report(args, B, world, value, elapsed, ktimes)
         if best is not None:
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not c5:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)
     plan.close()

@@ -60,10 +60,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dexp(DenseProblem DP, DenseBatc
     const grape::DevProblem &P = DP.P;
     const long item = blockIdx.x;
     const int b = (int)(item / P.Nt), k = (int)(item % P.Nt);
-    HM A, X;
-    build_generator(DP, B.x + (size_t)b * P.nx, k, kNoPert, A, ln);
+    HM X;
+    const double *xb = B.x + (size_t)b * P.nx;
     bool singular = false;
-    const int m = wg_expm(A, X, lds, ln, singular);
+    const int m = wg_expm([&](HM &A) { build_generator(DP, xb, k, kNoPert, A, ln); }, X, lds, ln, singular);
     img_store(B.E + (size_t)item * IMG, X, ln);
     if (singular) atomicOr(B.status, 1);
     note_m(B.mstats, m);
@@ -72,10 +72,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dexp(DenseProblem DP, DenseBatc
 __global__ __launch_bounds__(NTHREADS, 1) void k_dexp_raw(const double *Ain, double *Eout, int *status, int *mstats) {
     extern __shared__ double lds[];
     const Lane ln = make_lane();
-    HM A, X;
-    img_load(Ain + (size_t)blockIdx.x * IMG, A, ln);
+    HM X;
+    const double *src = Ain + (size_t)blockIdx.x * IMG;
     bool singular = false;
-    const int m = wg_expm(A, X, lds, ln, singular);
+    const int m = wg_expm([&](HM &A) { img_load(src, A, ln); }, X, lds, ln, singular);
     img_store(Eout + (size_t)blockIdx.x * IMG, X, ln);
     if (singular) atomicOr(status, 1);
     note_m(mstats, m);
@@ -286,9 +286,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dgrad(DenseProblem DP, DenseBat
         pp.index = p;
         pp.delta = P.eps;
         HM A, X;
-        build_generator(DP, xb, k, pp, A, ln);
         bool singular = false;
-        wg_expm(A, X, lds, ln, singular);
+        wg_expm([&](HM &G) { build_generator(DP, xb, k, pp, G, ln); }, X, lds, ln, singular);
         if (singular) atomicOr(B.status, 1);
         img_load(B.E + (qbase + k) * IMG, A, ln);
         double acc = 0.0;

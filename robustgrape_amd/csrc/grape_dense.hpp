@@ -181,7 +181,17 @@ __device__ __forceinline__ void img_store(double *img, const HM &M, const Lane &
         }
 }
 
-__device__ __forceinline__ void sm_store(SM S, const HM &M, const Lane &ln) {
+// a copy of the lane descriptor whose lane id the compiler cannot see through:
+// index math derived from it is recomputed where used instead of being hoisted
+// out of every enclosing loop and kept live
+__device__ __forceinline__ Lane pinned(const Lane &ln) {
+    Lane p = ln;
+    asm volatile("" : "+v"(p.l));
+    return p;
+}
+
+__device__ __forceinline__ void sm_store(SM S, const HM &M, const Lane &ln_in) {
+    const Lane ln = pinned(ln_in);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -211,23 +221,46 @@ __device__ __forceinline__ void cmfma2(HM &P, const double (&aR)[2], const doubl
     for (int i = 0; i < 2; ++i) P.im[i] = mfma(aI[i], xI, P.im[i]);
 }
 
+struct Frag {
+    double aR[2], aI[2], bR, bI;
+};
+
+template <bool LT, bool RT, bool RC>
+__device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &ln) {
+    // Indices are recomputed from a freshly pinned lane id every step: otherwise
+    // the compiler hoists all 16 steps' swizzled addresses of every product
+    // out of the enclosing loops and keeps them live (~100 VGPRs -> spills).
+    int l = ln.l;
+    asm volatile("" : "+v"(l));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ir = 16 * ln.tile(i) + (l & 15), kc = 4 * s + (l >> 4);
+        const int o = LT ? sidx(kc, ir) : sidx(ir, kc);
+        f.aR[i] = L.re[o];
+        f.aI[i] = L.im[o];
+    }
+    const int kr = 4 * s + (l >> 4), jc = 16 * ln.w + (l & 15);
+    const int o = RT ? sidx(jc, kr) : sidx(kr, jc);
+    f.bR = R.re[o];
+    f.bI = RC ? -R.im[o] : R.im[o];
+}
+
+// Software-pipelined over the 16 k-steps: the fragments of step s+1 are loaded
+// while step s's 8 MFMAs issue; the "memory" pin stops the compiler from hoisting
+// every step's loads to the top (that costs ~100 VGPRs and forces spills).
 template <bool LT, bool LC, bool RT, bool RC>
 __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
+    Frag cur, nxt;
+    mm_load<LT, RT, RC>(L, R, 0, cur, ln);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-        double aR[2], aI[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ir = 16 * ln.tile(i) + (ln.l & 15), kc = 4 * s + (ln.l >> 4);
-            const int o = LT ? sidx(kc, ir) : sidx(ir, kc);
-            aR[i] = L.re[o];
-            aI[i] = L.im[o];
+        if (s < 15) mm_load<LT, RT, RC>(L, R, s + 1, nxt, ln);
+        cmfma2<LC>(P, cur.aR, cur.aI, cur.bR, cur.bI);
+        if (s < 15) {
+            cur = nxt;
+            asm volatile("" : "+v"(cur.aR[0]), "+v"(cur.aR[1]), "+v"(cur.aI[0]), "+v"(cur.aI[1]), "+v"(cur.bR),
+                         "+v"(cur.bI)::"memory");
         }
-        const int kr = 4 * s + (ln.l >> 4), jc = ln.col();
-        const int o = RT ? sidx(jc, kr) : sidx(kr, jc);
-        const double bR = R.re[o];
-        const double bI = RC ? -R.im[o] : R.im[o];
-        cmfma2<LC>(P, aR, aI, bR, bI);
     }
 }
 
@@ -374,10 +407,11 @@ __device__ __forceinline__ void cmfma1(v4d &cr, v4d &ci, double aR, double aI, d
 // Q's column blocks left of or at kb are never read again: skipped (w <= kb).
 // Buffers alternate between the two LDS matrix regions (no trailing barrier).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void gj_solve(HM &Q, HM &Pm, double *lds, const Lane &ln, bool &singular) {
+__device__ __forceinline__ void gj_solve(HM &Q, HM &Pm, double *lds, const Lane &ln_in, bool &singular) {
     __syncthreads();  // the matrix regions are free
 #pragma unroll
     for (int kb = 0; kb < NT; ++kb) {
+        const Lane ln = pinned(ln_in);
         double *set = lds + ((kb & 1) ? LDS_R1 : LDS_R0);
         double *dvr = set + GJ_DINV, *dvi = dvr + SMALL;
         double *pcr = set + GJ_PCOL, *pci = pcr + 4 * SMALL;
@@ -484,36 +518,51 @@ __device__ __forceinline__ int dense_pade_degree(double nA, int &s) {
 
 __device__ __forceinline__ int m_index(int m) { return m == 3 ? 0 : m == 5 ? 1 : m == 7 ? 2 : m == 9 ? 3 : 4; }
 
+// keeps the compiler from hoisting work across a phase boundary (register pressure)
+__device__ __forceinline__ void hm_pin(HM &M) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) asm volatile("" : "+v"(M.re[i]), "+v"(M.im[i]));
+}
+
 // ---------------------------------------------------------------------------
-// X = exp(A) for the workgroup's matrix A (registers; consumed).  Uses all of
-// LDS [0, LDS_TOTAL).  Returns the Pade degree m.
+// X = exp(A) for the workgroup's matrix A.  `build(HM&)` (re)constructs A: it is
+// called twice (at the start and for the final U = A U), so A is never live
+// through the Pade polynomial (register budget: 256 VGPRs at 2 waves/SIMD).
+// Uses all of LDS [0, LDS_TOTAL).  Returns the Pade degree m.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wg_expm(HM &A, HM &X, double *lds, const Lane &ln, bool &singular) {
+template <class Build>
+__device__ __forceinline__ int wg_expm(const Build &build, HM &X, double *lds, const Lane &ln, bool &singular) {
     SM S0 = sm_at(lds, LDS_R0), S1 = sm_at(lds, LDS_R1);
-    const double nA = wg_norm1(A, lds, ln);
-    int s = 0;
-    const int m = dense_pade_degree(nA, s);
-    const double *C = kDPade[m_index(m)];
-    if (s > 0) hm_scale(A, ldexp(1.0, -s));
+    int s = 0, m;
     HM U, V;
-    if (m <= 9) {
-        // exp!: A2 = A*A; P = I; U = c1 P; V = c0 P; repeat P *= A2; U += c_{2k+1} P;
-        // V += c_{2k} P; U = A*U
+    {
+        HM A;
+        build(A);
+        const double nA = wg_norm1(A, lds, ln);
+        m = dense_pade_degree(nA, s);
+        if (s > 0) hm_scale(A, ldexp(1.0, -s));
         __syncthreads();
         sm_store(S0, A, ln);
         __syncthreads();
-        HM A2;
-        hm_zero(A2);
-        mm<false, false, false, false>(S0, S0, A2, ln);
-        hm_identity(U, ln, C[1]);
-        hm_identity(V, ln, C[0]);
-        hm_axpy(U, C[3], A2);
-        hm_axpy(V, C[2], A2);
-        const int nk = (m + 1) / 2;
-        if (nk > 2) {
+    }
+    const double *C = kDPade[m_index(m)];
+    if (m <= 9) {
+        // exp!: A2 = A*A; P = I; U = c1 P; V = c0 P; repeat P *= A2; U += c_{2k+1} P;
+        // V += c_{2k} P; U = A*U
+        {
+            HM A2;
+            hm_zero(A2);
+            mm<false, false, false, false>(S0, S0, A2, ln);
+            hm_identity(U, ln, C[1]);
+            hm_identity(V, ln, C[0]);
+            hm_axpy(U, C[3], A2);
+            hm_axpy(V, C[2], A2);
             __syncthreads();
             sm_store(S0, A2, ln);  // L = A2 for every further power
             __syncthreads();
+        }
+        const int nk = (m + 1) / 2;
+        if (nk > 2) {
             HM P;
             hm_zero(P);
             mm<false, false, false, false>(S0, S0, P, ln);  // A4
@@ -523,69 +572,78 @@ __device__ __forceinline__ int wg_expm(HM &A, HM &X, double *lds, const Lane &ln
                 __syncthreads();
                 sm_store(S1, P, ln);
                 __syncthreads();
-                HM Pn;
-                hm_zero(Pn);
-                mm<false, false, false, false>(S0, S1, Pn, ln);  // A2 . P
-                P = Pn;
+                hm_zero(P);
+                mm<false, false, false, false>(S0, S1, P, ln);  // A2 . P
                 hm_axpy(U, C[2 * kk + 1], P);
                 hm_axpy(V, C[2 * kk], P);
+                hm_pin(U);
+                hm_pin(V);
             }
         }
     } else {
         // exp! Pade 13: U = A (A6 (c13 A6 + c11 A4 + c9 A2) + c7 A6 + c5 A4 + c3 A2 + c1 I),
         //               V = A6 (c12 A6 + c10 A4 + c8 A2) + c6 A6 + c4 A4 + c2 A2 + c0 I
-        HM A2, A4, W1, Z1;
-        __syncthreads();
-        sm_store(S0, A, ln);
-        __syncthreads();
-        hm_zero(A2);
-        mm<false, false, false, false>(S0, S0, A2, ln);
-        __syncthreads();
-        sm_store(S0, A2, ln);
-        __syncthreads();
-        hm_zero(A4);
-        mm<false, false, false, false>(S0, S0, A4, ln);
-        sm_store(S1, A4, ln);  // region 1 unused so far
-        hm_zero(W1);
-        hm_zero(Z1);
-        hm_identity(U, ln, C[1]);
-        hm_identity(V, ln, C[0]);
-        hm_axpy(W1, C[11], A4);
-        hm_axpy(W1, C[9], A2);
-        hm_axpy(Z1, C[10], A4);
-        hm_axpy(Z1, C[8], A2);
-        hm_axpy(U, C[5], A4);
-        hm_axpy(U, C[3], A2);
-        hm_axpy(V, C[4], A4);
-        hm_axpy(V, C[2], A2);
-        __syncthreads();
-        HM A6;
-        hm_zero(A6);
-        mm<false, false, false, false>(S0, S1, A6, ln);  // A2 . A4
-        hm_axpy(W1, C[13], A6);
-        hm_axpy(Z1, C[12], A6);
-        hm_axpy(U, C[7], A6);
-        hm_axpy(V, C[6], A6);
-        __syncthreads();
-        sm_store(S0, A6, ln);
-        sm_store(S1, W1, ln);
-        __syncthreads();
+        // A2 and A4 live in LDS once consumed: registers hold W1, Z1, U, V (+ one power)
+        HM W1, Z1;
+        {
+            HM A2;
+            hm_zero(A2);
+            mm<false, false, false, false>(S0, S0, A2, ln);
+            hm_zero(W1);
+            hm_zero(Z1);
+            hm_identity(U, ln, C[1]);
+            hm_identity(V, ln, C[0]);
+            hm_axpy(W1, C[9], A2);
+            hm_axpy(Z1, C[8], A2);
+            hm_axpy(U, C[3], A2);
+            hm_axpy(V, C[2], A2);
+            __syncthreads();
+            sm_store(S0, A2, ln);
+            __syncthreads();
+        }
+        {
+            HM A4;
+            hm_zero(A4);
+            mm<false, false, false, false>(S0, S0, A4, ln);
+            hm_axpy(W1, C[11], A4);
+            hm_axpy(Z1, C[10], A4);
+            hm_axpy(U, C[5], A4);
+            hm_axpy(V, C[4], A4);
+            sm_store(S1, A4, ln);  // region 1 unused so far
+            __syncthreads();
+        }
+        {
+            HM A6;
+            hm_zero(A6);
+            mm<false, false, false, false>(S0, S1, A6, ln);  // A2 . A4
+            hm_axpy(W1, C[13], A6);
+            hm_axpy(Z1, C[12], A6);
+            hm_axpy(U, C[7], A6);
+            hm_axpy(V, C[6], A6);
+            __syncthreads();
+            sm_store(S0, A6, ln);
+            sm_store(S1, W1, ln);
+            __syncthreads();
+        }
         mm<false, false, false, false>(S0, S1, U, ln);  // U += A6 W1
         __syncthreads();
         sm_store(S1, Z1, ln);
         __syncthreads();
         mm<false, false, false, false>(S0, S1, V, ln);  // V += A6 Z1
     }
+    hm_pin(U);
+    hm_pin(V);
     __syncthreads();
-    sm_store(S0, A, ln);
     sm_store(S1, U, ln);
-    __syncthreads();
     {
-        HM Uf;
-        hm_zero(Uf);
-        mm<false, false, false, false>(S0, S1, Uf, ln);  // U = A U
-        U = Uf;
+        HM A;
+        build(A);
+        if (s > 0) hm_scale(A, ldexp(1.0, -s));
+        sm_store(S0, A, ln);
     }
+    __syncthreads();
+    hm_zero(U);
+    mm<false, false, false, false>(S0, S1, U, ln);  // U = A U
     // Q = V - U, X = V + U: solve Q X' = X
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -599,10 +657,8 @@ __device__ __forceinline__ int wg_expm(HM &A, HM &X, double *lds, const Lane &ln
     for (int q = 0; q < s; ++q) {
         sm_store(S0, V, ln);
         __syncthreads();
-        HM Sq;
-        hm_zero(Sq);
-        mm<false, false, false, false>(S0, S0, Sq, ln);
-        V = Sq;
+        hm_zero(V);
+        mm<false, false, false, false>(S0, S0, V, ln);
         __syncthreads();
     }
     X = V;

@@ -18,7 +18,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     for pre in ("void ", "grape::"):
         n = n.replace(pre, "")
     return n
