@@ -17,6 +17,8 @@ What it restates (citations are into the read-only reference tree):
   ``calculate_expectation_values`` -- src/FidelityCalculations.jl:368-390,
   ``calculate_fidelity_response`` -- :246-280, ``calculate_fidelity_response_fft``
   -- :306-343 (used by the "next" rows of SURVEY.md section 8f).
+* ``regularization_cost`` / ``regularization_cost_phase`` -- src/Regularization.jl:26-115,
+  and the optimiser's cost assembly ``calculate_common!`` -- src/FidelityCalculations.jl:172-196.
 * Julia's ``LinearAlgebra.exp!`` (third-party: Julia stdlib, the only Julia
   the reference pins is 1.9 in .github/workflows/docs.yml:17; not present in
   /root/reference).  Restated from its published algorithm: ``isdiag`` early
@@ -581,6 +583,74 @@ def calculate_fidelity_response_fft(fp, x, oversampling=1):
                 - 1 / (D * (D + 1)) * np.real(tr_mod(fi[:, :, it] @ P) * tr_mod(f[:, :, it] @ P)))
     freqs = (2 * np.pi / (nfft * dt)) * np.arange(nfft)
     return out, freqs
+
+
+# ---------------------------------------------------------------------------
+# src/Regularization.jl and the optimiser's cost (FidelityCalculations.jl:161-218)
+# ---------------------------------------------------------------------------
+
+def regularization_cost(x, f=None, df=None):
+    """Regularization.jl:26-48 (and :76-81 with a transform f, derivative df):
+    (reg1, jac1, reg2, jac2) for one control's time series, written loop by
+    loop like the reference (jac2 has explicit end stencils, n >= 4)."""
+    x = np.asarray(x, dtype=np.float64)
+    if f is not None:
+        fx = np.array([f(v) for v in x])
+        r1, j1, r2, j2 = regularization_cost(fx)
+        dfx = np.array([df(v) for v in x])
+        return r1, dfx * j1, r2, dfx * j2
+    n = x.shape[0]
+    diff_x = np.diff(x)
+    diff_diff_x = np.diff(diff_x)
+    reg1 = float(np.sum(diff_x ** 2))
+    reg2 = float(np.sum(diff_diff_x ** 2))
+    jac1 = np.zeros(n)
+    jac2 = np.zeros(n)
+    jac1[1:n - 1] = -2.0 * diff_diff_x
+    jac1[0] += -2.0 * diff_x[0]
+    jac1[n - 1] += 2.0 * diff_x[n - 2]
+    jac2[0] = 2 * (x[2] - 2 * x[1] + x[0])
+    jac2[1] = 2 * (x[3] - 4 * x[2] + 5 * x[1] - 2 * x[0])
+    for i in range(2, n - 2):
+        jac2[i] = 2 * (x[i + 2] - 4 * x[i + 1] + 6 * x[i] - 4 * x[i - 1] + x[i - 2])
+    jac2[n - 2] = 2 * (x[n - 4] - 4 * x[n - 3] + 5 * x[n - 2] - 2 * x[n - 1])
+    jac2[n - 1] = 2 * (x[n - 3] - 2 * x[n - 2] + x[n - 1])
+    return reg1, jac1, reg2, jac2
+
+
+def regularization_cost_phase(phis):
+    """Regularization.jl:111-115: cos and sin transforms, summed."""
+    a = regularization_cost(phis, math.cos, lambda v: -math.sin(v))
+    b = regularization_cost(phis, math.sin, math.cos)
+    return a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]
+
+
+def optimization_cost(fp, x, regularization_functions, coeff1, coeff2, error_source_coeff):
+    """calculate_common! (FidelityCalculations.jl:172-196): returns the buffer
+    [cost, grad...] the optimiser's f / g! read.  nparam > 1 follows the intent
+    (each control's regularisation gradient on its own entries); the reference's
+    `buffer[2:end-na] += sum(reg_costs_grad, dims=1)[1,:]` (:195) only has matching
+    shapes for nparam == 1."""
+    up = fp.unitary_problem
+    na = up.nb_additional_param
+    F, F_dx, F_d2err, F_d2err_dx = calculate_fidelity_and_derivatives(fp, x)
+    x_main, _, nparam = _unpack(up, x)
+    buf = np.zeros(len(x) + 1)
+    buf[0] = 1.0 - F
+    buf[1:] = -F_dx
+    if len(F_d2err) > 0:
+        c = np.asarray(error_source_coeff, dtype=np.float64)
+        buf[0] += float(np.sum(c * F_d2err ** 2))
+        buf[1:] += 2.0 * np.sum((c * F_d2err)[None, :] * F_d2err_dx, axis=1)
+    reg_tot = np.zeros(nparam)
+    reg_grad = np.zeros((nparam, up.ntimes))
+    for p in range(nparam):
+        r1, j1, r2, j2 = regularization_functions[p](x_main[p, :])
+        reg_tot[p] = coeff1[p] * r1 + coeff2[p] * r2
+        reg_grad[p, :] = coeff1[p] * np.asarray(j1) + coeff2[p] * np.asarray(j2)
+    buf[0] += float(np.sum(reg_tot))
+    buf[1:len(buf) - na] += reg_grad.T.reshape(-1)
+    return buf
 
 
 # ---------------------------------------------------------------------------

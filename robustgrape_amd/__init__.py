@@ -14,6 +14,9 @@ from .operators import (OperatorBasisError, OperatorBasisHamiltonian, OperatorBa
 from .engine import (GrapePlan, calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
                      clear_plans, get_plan)
 from . import rydberg as RydbergTools
+from .regularization import regularization_cost, regularization_cost_phase
+from .optimize import (OptimizationResult, minimizer, minimum, optimize_fidelity_and_error_sources,
+                       optimize_restarts)
 
 # north-star aliases (BASELINE.json)
 FidelityOptimProblem = FidelityRobustGRAPEProblem
@@ -24,5 +27,6 @@ __all__ = [
     "ErrorSource", "UnitaryRobustGRAPEProblem", "FidelityRobustGRAPEProblem", "FidelityRobustGRAPEParameters",
     "calculate_fidelity_and_derivatives", "calculate_unitary_and_derivatives", "GrapePlan", "get_plan",
     "clear_plans", "OperatorBasisHamiltonian", "OperatorBasisError", "OperatorBasisTarget", "Term",
-    "RydbergTools", "FidelityOptimProblem", "compute_fidelity_and_gradient", "compute_unitary_and_derivatives",
+    "RydbergTools", "regularization_cost", "regularization_cost_phase", "optimize_fidelity_and_error_sources",
+    "optimize_restarts", "OptimizationResult", "minimizer", "minimum", "FidelityOptimProblem", "compute_fidelity_and_gradient", "compute_unitary_and_derivatives",
 ]

@@ -1,0 +1,436 @@
+"""The optimiser around the hot path: src/FidelityCalculations.jl:161-218
+(``optimize_fidelity_and_error_sources``), run as a BATCHED L-BFGS over
+random restarts with every evaluation on the GPU.
+
+Reference behaviour kept:
+  * the cost and gradient of ``calculate_common!`` (:172-196):
+      cost = 1 - F + sum_e c_e F_d2err_e^2 + sum_p (c1_p r1_p + c2_p r2_p)
+      grad = -F_dx + 2 sum_e c_e F_d2err_e F_d2err_dx[:, e] + regulariser gradients
+    (nparam > 1: each control's regulariser gradient lands on its own entries;
+    the reference's ``sum(reg_costs_grad, dims=1)`` at :195 only has matching
+    shapes for nparam == 1 and throws DimensionMismatch otherwise);
+  * the shape assertions (:162-170) -> AssertionError;
+  * Optim.jl's stopping rules for ``iterations``, ``time_limit`` and the
+    ``additional_parameters`` g_tol (|g|_inf), f_abstol, f_reltol, x_abstol.
+Optim.jl (the reference's solver, a third-party dependency absent here) is
+replaced by an L-BFGS (memory 10, initial inverse-Hessian scaling s.y/y.y, as
+Optim's LBFGS) with a strong-Wolfe line search (Nocedal & Wright alg. 3.5/3.6,
+c1 = 1e-4, c2 = 0.9) in place of Optim's default Hager-Zhang: iterates are
+not bit-identical to Optim's, the minimisation problem is.
+
+MI355X design: all restarts of a sweep advance together.  Their control
+vectors, gradients and L-BFGS histories live in HBM as (restarts, n_x)
+tensors; each line-search round evaluates the still-active restarts in ONE
+batched device pass (``GrapePlan.fidelity_grad_device_async``) and the
+two-loop recursion is a handful of batched reductions.  Nothing leaves the
+GPU inside the loop except the per-round active count.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+
+from .types import FidelityRobustGRAPEParameters, FidelityRobustGRAPEProblem
+
+C1, C2 = 1e-4, 0.9
+MAX_LS_ROUNDS = 30
+
+
+@dataclass
+class OptimizationResult:
+    """What callers read from Optim's result (Optim.minimizer / minimum / iterations ...)."""
+    minimizer: np.ndarray
+    minimum: float
+    iterations: int
+    f_calls: int
+    converged: bool
+    g_converged: bool
+    f_converged: bool
+    x_converged: bool
+    time_run: float
+    stop_reason: str = ""
+
+
+@dataclass
+class BatchResult:
+    """Per-restart results of a batched run (rows follow the input order)."""
+    minimizer: torch.Tensor          # (R, n)
+    minimum: torch.Tensor            # (R,)
+    gradient: torch.Tensor           # (R, n)
+    iterations: torch.Tensor         # (R,) int64
+    f_calls: torch.Tensor            # (R,) int64
+    g_converged: torch.Tensor        # (R,) bool
+    f_converged: torch.Tensor
+    x_converged: torch.Tensor
+    ls_failed: torch.Tensor
+    time_run: float
+    extra: dict = field(default_factory=dict)
+
+    def result(self, r: int) -> OptimizationResult:
+        conv = bool(self.g_converged[r] or self.f_converged[r] or self.x_converged[r])
+        reason = "converged" if conv else ("line search failed" if bool(self.ls_failed[r]) else "iterations/time")
+        return OptimizationResult(self.minimizer[r].detach().cpu().numpy(), float(self.minimum[r]),
+                                  int(self.iterations[r]), int(self.f_calls[r]), conv,
+                                  bool(self.g_converged[r]), bool(self.f_converged[r]),
+                                  bool(self.x_converged[r]), self.time_run, reason)
+
+
+def minimizer(res):
+    """Optim.minimizer"""
+    return res.minimizer
+
+
+def minimum(res):
+    """Optim.minimum"""
+    return res.minimum
+
+
+# ---------------------------------------------------------------------------
+# batched L-BFGS with a strong-Wolfe line search (device agnostic)
+# ---------------------------------------------------------------------------
+def _rowdot(a, b):
+    return torch.sum(a * b, dim=1)
+
+
+def _cubic_min(a0, f0, g0, a1, f1, g1):
+    """Minimiser of the cubic interpolating (a0, f0, g0), (a1, f1, g1), safeguarded into
+    the middle 80 % of the interval; bisection where the cubic is not usable."""
+    d1 = g0 + g1 - 3 * (f0 - f1) / (a0 - a1)
+    disc = d1 * d1 - g0 * g1
+    d2 = torch.sign(a1 - a0) * torch.sqrt(torch.clamp(disc, min=0.0))
+    den = g1 - g0 + 2 * d2
+    a = a1 - (a1 - a0) * (g1 + d2 - d1) / den
+    lo = torch.minimum(a0, a1)
+    hi = torch.maximum(a0, a1)
+    w = hi - lo
+    ok = (disc >= 0) & torch.isfinite(a) & (den != 0)
+    a = torch.where(ok, a, 0.5 * (a0 + a1))
+    return torch.clamp(a, lo + 0.1 * w, hi - 0.1 * w)
+
+
+def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.Tensor, *, m: int = 10,
+                  iterations: int = 1000, g_tol: float = 1e-8, f_abstol: float = 0.0, f_reltol: float = 0.0,
+                  x_abstol: float = 0.0, time_limit: float = float("nan"),
+                  callback: Optional[Callable] = None) -> BatchResult:
+    """Minimise fun row-wise from every row of X0.
+
+    fun(X, rows) -> (f (r,), g (r, n)) evaluates the rows `rows` (int64 indices into the
+    batch) at control vectors X (r, n).  Rows stop independently (Optim's rules)."""
+    t_start = time.perf_counter()
+    X = X0.clone()
+    R, n = X.shape
+    dev, dt = X.device, X.dtype
+    all_rows = torch.arange(R, device=dev)
+    f, g = fun(X, all_rows)
+    f_calls = torch.ones(R, dtype=torch.int64, device=dev)
+    iters = torch.zeros(R, dtype=torch.int64, device=dev)
+    S = torch.zeros(m, R, n, dtype=dt, device=dev)
+    Y = torch.zeros(m, R, n, dtype=dt, device=dev)
+    rho = torch.zeros(m, R, dtype=dt, device=dev)
+    hist = torch.zeros(R, dtype=torch.int64, device=dev)     # stored pairs (<= m)
+    head = torch.zeros(R, dtype=torch.int64, device=dev)     # next slot (ring buffer)
+    gconv = torch.amax(torch.abs(g), dim=1) <= g_tol
+    fconv = torch.zeros(R, dtype=torch.bool, device=dev)
+    xconv = torch.zeros(R, dtype=torch.bool, device=dev)
+    lsfail = torch.zeros(R, dtype=torch.bool, device=dev)
+    gamma = torch.ones(R, dtype=dt, device=dev)
+    timed_out = False
+    while True:
+        active = ~(gconv | fconv | xconv | lsfail) & (iters < iterations)
+        if not math.isnan(time_limit) and time.perf_counter() - t_start > time_limit:
+            timed_out = True
+            break
+        if not bool(active.any()):
+            break
+        # ---- two-loop recursion (ring buffer, newest first), batched over rows
+        q = -g.clone()
+        alpha = torch.zeros(m, R, dtype=dt, device=dev)
+        for j in range(m):
+            slot = (head - 1 - j) % m
+            use = (j < hist)
+            s_j = S[slot, all_rows]
+            y_j = Y[slot, all_rows]
+            r_j = rho[slot, all_rows]
+            a_j = torch.where(use, r_j * _rowdot(s_j, q), torch.zeros_like(r_j))
+            alpha[j] = a_j
+            q = q - a_j[:, None] * y_j
+        q = q * gamma[:, None]
+        for j in reversed(range(m)):
+            slot = (head - 1 - j) % m
+            use = (j < hist)
+            s_j = S[slot, all_rows]
+            y_j = Y[slot, all_rows]
+            r_j = rho[slot, all_rows]
+            b_j = r_j * _rowdot(y_j, q)
+            q = q + torch.where(use, alpha[j] - b_j, torch.zeros_like(b_j))[:, None] * s_j
+        D = q
+        dphi0 = _rowdot(g, D)
+        bad = ~(dphi0 < 0) & active           # not a descent direction: restart from -g
+        if bool(bad.any()):
+            D[bad] = -g[bad]
+            dphi0 = torch.where(bad, _rowdot(g, D), dphi0)
+            hist = torch.where(bad, torch.zeros_like(hist), hist)
+            gamma = torch.where(bad, torch.ones_like(gamma), gamma)
+        # ---- strong-Wolfe line search, all active rows in lock step
+        f0 = f.clone()
+        phase = torch.where(active, torch.zeros_like(iters), torch.full_like(iters, 2))  # 0 bracket 1 zoom 2 done
+        a_cur = torch.ones(R, dtype=dt, device=dev)
+        a_prev = torch.zeros(R, dtype=dt, device=dev)
+        f_prev, dp_prev = f0.clone(), dphi0.clone()
+        a_lo, f_lo, dp_lo = a_prev.clone(), f0.clone(), dphi0.clone()
+        a_hi, f_hi, dp_hi = a_prev.clone(), f0.clone(), dphi0.clone()
+        Xn, fn, gn = X.clone(), f.clone(), g.clone()
+        accepted = torch.zeros(R, dtype=torch.bool, device=dev)
+        first = torch.ones(R, dtype=torch.bool, device=dev)
+        for _ in range(MAX_LS_ROUNDS):
+            todo = phase < 2
+            if not bool(todo.any()):
+                break
+            rows = torch.nonzero(todo).flatten()
+            a = a_cur[rows]
+            Xt = X[rows] + a[:, None] * D[rows]
+            ft, gt = fun(Xt, rows)
+            f_calls[rows] += 1
+            dpt = _rowdot(gt, D[rows])
+            f0r, d0r = f0[rows], dphi0[rows]
+            armijo = ft <= f0r + C1 * a * d0r
+            curv = torch.abs(dpt) <= -C2 * d0r
+            ph = phase[rows]
+            newph = ph.clone()
+            # bracketing phase (alg. 3.5)
+            br = ph == 0
+            to_zoom_a = br & (~armijo | (~first[rows] & (ft >= f_prev[rows])))
+            acc_b = br & ~to_zoom_a & curv
+            to_zoom_b = br & ~to_zoom_a & ~acc_b & (dpt >= 0)
+            expand = br & ~to_zoom_a & ~acc_b & ~to_zoom_b
+            # zoom phase (alg. 3.6)
+            zm = ph == 1
+            z_hi = zm & (~armijo | (ft >= f_lo[rows]))
+            z_acc = zm & ~z_hi & curv
+            z_flip = zm & ~z_hi & ~z_acc & (dpt * (a_hi[rows] - a_lo[rows]) >= 0)
+            z_lo = zm & ~z_hi & ~z_acc
+            acc = acc_b | z_acc
+            # bookkeeping on the row subset
+            A_lo, F_lo, P_lo = a_lo[rows], f_lo[rows], dp_lo[rows]
+            A_hi, F_hi, P_hi = a_hi[rows], f_hi[rows], dp_hi[rows]
+            Ap, Fp, Pp = a_prev[rows], f_prev[rows], dp_prev[rows]
+            # bracket (a): zoom(a_prev, a)
+            A_lo = torch.where(to_zoom_a, Ap, A_lo)
+            F_lo = torch.where(to_zoom_a, Fp, F_lo)
+            P_lo = torch.where(to_zoom_a, Pp, P_lo)
+            A_hi = torch.where(to_zoom_a, a, A_hi)
+            F_hi = torch.where(to_zoom_a, ft, F_hi)
+            P_hi = torch.where(to_zoom_a, dpt, P_hi)
+            # bracket (b): zoom(a, a_prev)
+            A_lo = torch.where(to_zoom_b, a, A_lo)
+            F_lo = torch.where(to_zoom_b, ft, F_lo)
+            P_lo = torch.where(to_zoom_b, dpt, P_lo)
+            A_hi = torch.where(to_zoom_b, Ap, A_hi)
+            F_hi = torch.where(to_zoom_b, Fp, F_hi)
+            P_hi = torch.where(to_zoom_b, Pp, P_hi)
+            # zoom: new hi
+            A_hi = torch.where(z_hi, a, A_hi)
+            F_hi = torch.where(z_hi, ft, F_hi)
+            P_hi = torch.where(z_hi, dpt, P_hi)
+            # zoom: flip (hi <- lo) then lo <- a
+            A_hi = torch.where(z_flip, a_lo[rows], A_hi)
+            F_hi = torch.where(z_flip, f_lo[rows], F_hi)
+            P_hi = torch.where(z_flip, dp_lo[rows], P_hi)
+            A_lo = torch.where(z_lo, a, A_lo)
+            F_lo = torch.where(z_lo, ft, F_lo)
+            P_lo = torch.where(z_lo, dpt, P_lo)
+            newph = torch.where(to_zoom_a | to_zoom_b, torch.ones_like(newph), newph)
+            newph = torch.where(acc, torch.full_like(newph, 2), newph)
+            # the best Armijo point so far is kept as a fallback
+            better = armijo & (ft < fn[rows])
+            keep = acc | better
+            if bool(keep.any()):
+                kr = rows[keep]
+                Xn[kr] = Xt[keep]
+                fn[kr] = ft[keep]
+                gn[kr] = gt[keep]
+            accepted[rows[acc]] = True
+            # next trial step
+            zoom_now = newph == 1
+            a_zoom = _cubic_min(A_lo, F_lo, P_lo, A_hi, F_hi, P_hi)
+            a_next = torch.where(expand, 4.0 * a, a)
+            a_next = torch.where(zoom_now, a_zoom, a_next)
+            # a collapsed bracket ends the search (keep the best Armijo point if any)
+            tiny = zoom_now & (torch.abs(A_hi - A_lo) <= 1e-12 * torch.maximum(torch.abs(A_lo), torch.ones_like(A_lo)))
+            newph = torch.where(tiny, torch.full_like(newph, 2), newph)
+            a_prev[rows] = torch.where(expand, a, Ap)
+            f_prev[rows] = torch.where(expand, ft, Fp)
+            dp_prev[rows] = torch.where(expand, dpt, Pp)
+            a_lo[rows], f_lo[rows], dp_lo[rows] = A_lo, F_lo, P_lo
+            a_hi[rows], f_hi[rows], dp_hi[rows] = A_hi, F_hi, P_hi
+            a_cur[rows] = a_next
+            phase[rows] = newph
+            first[rows] = False
+        moved = active & (fn < f0)
+        lsfail = lsfail | (active & ~moved & ~accepted)
+        step = active & (accepted | moved)
+        # ---- L-BFGS update and convergence (Optim's rules)
+        s = Xn - X
+        y = gn - g
+        sy = _rowdot(s, y)
+        upd = step & (sy > 0)
+        if bool(upd.any()):
+            ur = torch.nonzero(upd).flatten()
+            slot = head[ur]
+            S[slot, ur] = s[ur]
+            Y[slot, ur] = y[ur]
+            rho[slot, ur] = 1.0 / sy[ur]
+            head[ur] = (head[ur] + 1) % m
+            hist[ur] = torch.clamp(hist[ur] + 1, max=m)
+            gamma[ur] = sy[ur] / _rowdot(y[ur], y[ur])
+        fold = f.clone()
+        X = torch.where(step[:, None], Xn, X)
+        f = torch.where(step, fn, f)
+        g = torch.where(step[:, None], gn, g)
+        iters = iters + step.to(iters.dtype)
+        gconv = gconv | (step & (torch.amax(torch.abs(g), dim=1) <= g_tol))
+        df = torch.abs(f - fold)
+        fconv = fconv | (step & ((df <= f_abstol) | (df <= f_reltol * torch.abs(f))))
+        xconv = xconv | (step & (torch.amax(torch.abs(s), dim=1) <= x_abstol))
+        if callback is not None:
+            callback(X, f, iters)
+    return BatchResult(X, f, g, iters, f_calls, gconv, fconv, xconv, lsfail,
+                       time.perf_counter() - t_start, {"timed_out": timed_out})
+
+
+# ---------------------------------------------------------------------------
+# the reference's cost (calculate_common!) on the GPU
+# ---------------------------------------------------------------------------
+class RobustCost:
+    """cost(X) and its gradient for a batch of control vectors, FidelityCalculations.jl:172-196.
+
+    The fidelity terms come from the GPU engine in one batched pass; the error-source and
+    regulariser terms are assembled with torch on the same device."""
+
+    def __init__(self, fp: FidelityRobustGRAPEProblem, params: FidelityRobustGRAPEParameters, nparam: int,
+                 max_batch: int, device: int = 0, evaluate: Optional[Callable] = None):
+        up = fp.unitary_problem
+        self.fp, self.up, self.nparam = fp, up, nparam
+        self.ntimes, self.na = up.ntimes, up.nb_additional_param
+        self.nx = nparam * up.ntimes + up.nb_additional_param
+        self.nerr = len(up.error_sources)
+        self.params = params
+        self.c1 = [float(c) for c in params.regularization_coeff1]
+        self.c2 = [float(c) for c in params.regularization_coeff2]
+        self.ce = [float(c) for c in params.error_source_coeff]
+        self.regs = list(params.regularization_functions)
+        self._evaluate = evaluate
+        self.plan = None
+        if evaluate is None:
+            from .engine import GrapePlan
+            self.plan = GrapePlan(fp, nparam, device=device, max_batch=max_batch)
+            self.device = torch.device("cuda", device)
+        else:
+            self.device = torch.device("cpu")
+
+    def close(self):
+        if self.plan is not None:
+            self.plan.close()
+            self.plan = None
+
+    def fidelity_terms(self, X: torch.Tensor):
+        """(F (r,), F_dx (r,nx), F_d2err (r,ne), F_d2err_dx (r,nx,ne)) for the rows of X."""
+        if self._evaluate is not None:
+            return self._evaluate(X)
+        X = X.contiguous()
+        r = X.shape[0]
+        F = torch.empty(r, dtype=torch.float64, device=X.device)
+        Fdx = torch.empty(r, self.nx, dtype=torch.float64, device=X.device)
+        Fd2 = torch.empty(r, max(1, self.nerr), dtype=torch.float64, device=X.device)
+        Fd2dx = torch.empty(r, max(1, self.nerr), self.nx, dtype=torch.float64, device=X.device)
+        stream = torch.cuda.current_stream(X.device)
+        self.plan.set_stream(stream.cuda_stream)
+        self.plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), r,
+                                             Fd2.data_ptr() if self.nerr else 0,
+                                             Fd2dx.data_ptr() if self.nerr else 0)
+        self.plan.synchronize()  # raises on a singular Pade denominator
+        if not self.nerr:
+            return F, Fdx, Fd2[:, :0], Fd2dx[:, :0, :].transpose(1, 2)
+        return F, Fdx, Fd2, Fd2dx.transpose(1, 2)
+
+    def __call__(self, X: torch.Tensor, rows=None):
+        F, Fdx, Fd2, Fd2dx = self.fidelity_terms(X)
+        cost = 1.0 - F
+        grad = -Fdx
+        if self.nerr:
+            ce = torch.tensor(self.ce, dtype=X.dtype, device=X.device)
+            cost = cost + torch.sum(ce[None, :] * Fd2 ** 2, dim=1)
+            grad = grad + 2.0 * torch.sum((ce[None, :] * Fd2)[:, None, :] * Fd2dx, dim=2)
+        nm = self.nparam * self.ntimes
+        xm = X[:, :nm].reshape(X.shape[0], self.ntimes, self.nparam)
+        reg_cost = torch.zeros_like(cost)
+        reg_grad = torch.zeros(X.shape[0], self.ntimes, self.nparam, dtype=X.dtype, device=X.device)
+        for p, fn in enumerate(self.regs):
+            r1, j1, r2, j2 = _call_reg(fn, xm[:, :, p])
+            reg_cost = reg_cost + (self.c1[p] * r1 + self.c2[p] * r2)
+            reg_grad[:, :, p] = self.c1[p] * j1 + self.c2[p] * j2
+        cost = cost + reg_cost
+        grad = grad.clone()
+        grad[:, :nm] += reg_grad.reshape(X.shape[0], nm)
+        return cost, grad
+
+
+def _call_reg(fn, xp: torch.Tensor):
+    """Batched call when the function supports it, else the reference's 1-D signature per row."""
+    if getattr(fn, "batched", False):
+        return fn(xp)
+    outs = [fn(row.detach().cpu().numpy()) for row in xp]
+    t = lambda v: torch.as_tensor(np.asarray(v, dtype=np.float64), device=xp.device)
+    return (t([o[0] for o in outs]), torch.stack([t(o[1]) for o in outs]),
+            t([o[2] for o in outs]), torch.stack([t(o[3]) for o in outs]))
+
+
+def _checks(fp, params, nx):
+    up = fp.unitary_problem
+    nerr = len(up.error_sources)
+    if len(params.error_source_coeff) != nerr:
+        raise AssertionError("error_source_coeff must have one entry per error source")
+    nparam = (nx - up.nb_additional_param) // up.ntimes
+    if not (len(params.regularization_coeff1) == len(params.regularization_coeff2)
+            == len(params.regularization_functions) == nparam):
+        raise AssertionError("regularization functions / coefficients must have one entry per control")
+    return nparam
+
+
+def _solver_options(params):
+    ap = dict(params.additional_parameters)
+    return dict(iterations=int(params.iterations), time_limit=float(params.time_limit),
+                g_tol=float(ap.get("g_tol", ap.get("g_abstol", 1e-8))), f_abstol=float(ap.get("f_abstol", 0.0)),
+                f_reltol=float(ap.get("f_reltol", 0.0)), x_abstol=float(ap.get("x_abstol", 0.0)))
+
+
+def optimize_restarts(fidelity_problem: FidelityRobustGRAPEProblem, fidelity_parameters: FidelityRobustGRAPEParameters,
+                      X0, device: int = 0, evaluate: Optional[Callable] = None, m: int = 10) -> BatchResult:
+    """Batched restarts: every row of X0 (R, n_x) is one optimisation of the reference's
+    problem; all of them advance together on the GPU (see the module docstring)."""
+    X0 = torch.as_tensor(np.asarray(X0, dtype=np.float64) if not isinstance(X0, torch.Tensor) else X0,
+                         dtype=torch.float64)
+    if X0.dim() != 2:
+        raise AssertionError("X0 must be (restarts, n_x)")
+    nparam = _checks(fidelity_problem, fidelity_parameters, X0.shape[1])
+    cost = RobustCost(fidelity_problem, fidelity_parameters, nparam, max_batch=X0.shape[0], device=device,
+                      evaluate=evaluate)
+    try:
+        res = lbfgs_batched(cost, X0.to(cost.device), m=m, **_solver_options(fidelity_parameters))
+    finally:
+        cost.close()
+    return res
+
+
+def optimize_fidelity_and_error_sources(fidelity_problem: FidelityRobustGRAPEProblem,
+                                        fidelity_parameters: FidelityRobustGRAPEParameters,
+                                        device: int = 0, evaluate: Optional[Callable] = None) -> OptimizationResult:
+    """FidelityCalculations.jl:161-218: one optimisation from fidelity_parameters.x_initial."""
+    x0 = np.asarray(fidelity_parameters.x_initial, dtype=np.float64)
+    res = optimize_restarts(fidelity_problem, fidelity_parameters, x0[None, :], device=device, evaluate=evaluate)
+    return res.result(0)

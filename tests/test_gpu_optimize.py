@@ -1,0 +1,85 @@
+"""The optimiser (FidelityCalculations.jl:161-218) with its
+evaluations on the GPU: the cost assembly against the oracle's calculate_common!
+restatement, the reference's optimisation testset (runtests.jl:356-416), and
+batched restarts equal to independent runs."""
+import numpy as np
+import pytest
+import torch
+
+from robustgrape_amd import optimize as OPT
+from robustgrape_amd import regularization as REG
+from robustgrape_amd.types import FidelityRobustGRAPEParameters
+from tests import problems as P
+
+pytestmark = pytest.mark.gpu
+T2, T2_ABS, T3 = 1e-6, 1e-7, 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _params(x0, nerr=0, iterations=40, **extra):
+    return FidelityRobustGRAPEParameters(
+        x_initial=x0, regularization_functions=[REG.regularization_cost_phase], regularization_coeff1=[1e-6],
+        regularization_coeff2=[1e-6], error_source_coeff=[0.5] * nerr, iterations=iterations,
+        additional_parameters=dict(f_abstol=1e-11, g_tol=3e-10, **extra))
+
+
+def test_device_cost_matches_oracle_cost():
+    from oracle import grape_oracle as O
+    fpd = P.sym_problem(50, errors=("amp", "freq"))
+    fph = P.sym_problem(50, errors=("amp", "freq"), device=False)
+    X = np.stack([P.random_x(50, s) for s in (11, 12, 13)])
+    params = _params(X[0], nerr=2)
+    cost = OPT.RobustCost(fpd, params, nparam=1, max_batch=3)
+    c, g = cost(torch.as_tensor(X, device="cuda"))
+    cost.close()
+    for b in range(3):
+        ref = O.optimization_cost(fph, X[b], [O.regularization_cost_phase], [1e-6], [1e-6], [0.5, 0.5])
+        assert abs(float(c[b]) - ref[0]) <= T3 * abs(ref[0]) + 1e-9
+        gb = g[b].cpu().numpy()
+        assert np.max(np.abs(gb - ref[1:])) <= T3 * np.max(np.abs(ref[1:])) + T2_ABS
+
+
+def test_reference_optimisation_testset_on_gpu():
+    """runtests.jl:356-416: N = 200, 40 L-BFGS iterations from 2pi*0.001*U reach 1 - F < 1e-6."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = P.sym_problem(200)
+    rng = np.random.default_rng(42)
+    x0 = np.concatenate([2 * np.pi * 0.001 * rng.uniform(size=200), [2 * np.pi * rng.uniform()]])
+    res = OPT.optimize_fidelity_and_error_sources(fp, _params(x0))
+    F = calculate_fidelity_and_derivatives(fp, OPT.minimizer(res))[0]
+    assert 1 - F < 1e-6 and res.iterations <= 40
+
+
+def test_batched_restarts_equal_independent_runs():
+    """Rows advance independently: a restart's trajectory in a batch of 6 equals its own run
+    (deterministic kernels: a batch element is bitwise the single evaluation)."""
+    fp = P.sym_problem(100, t0=P.T0_TO)
+    X0 = np.stack([P.random_x(100, 1000 + r, small=True) for r in range(6)])
+    res = OPT.optimize_restarts(fp, _params(X0[0], iterations=25), X0)
+    for r in (0, 4):
+        one = OPT.optimize_restarts(fp, _params(X0[r], iterations=25), X0[r:r + 1])
+        assert int(one.iterations[0]) == int(res.iterations[r])
+        assert torch.equal(one.minimizer[0], res.minimizer[r])
+    assert float(torch.min(res.minimum)) < 1e-3
+
+
+def test_optimise_with_error_sources():
+    """examples/time_optimal_cz.jl:60-71 pattern: the error sensitivity joins the cost
+    (error_source_coeff); the optimiser lowers that cost and reports it consistently."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = P.sym_problem(100, t0=P.T0_TO, errors=("amp",))
+    x0 = P.random_x(100, 77, small=True)
+    params = _params(x0, nerr=1, iterations=30)
+    cost = OPT.RobustCost(fp, params, nparam=1, max_batch=1)
+    c0 = float(cost(torch.as_tensor(x0[None, :], device="cuda"))[0][0])
+    cost.close()
+    res = OPT.optimize_fidelity_and_error_sources(fp, params)
+    F, _, d2, _ = calculate_fidelity_and_derivatives(fp, res.minimizer)
+    reg = REG.regularization_cost_phase(res.minimizer[:100])
+    assert res.minimum < c0
+    assert abs(res.minimum - (1 - F + 0.5 * d2[0] ** 2 + 1e-6 * (reg[0] + reg[2]))) < 1e-12
