@@ -19,6 +19,7 @@
 #include "grape.h"
 #include "grape_launch.hpp"
 #include "grape_dense_api.hpp"
+#include "grape_unitary_api.hpp"
 
 // instantiated in grape_inst.hip (one translation unit per dimension)
 namespace grape_host {
@@ -76,6 +77,15 @@ hipError_t dispatch_expm_raw(int D, const cd *A, cd *E, int n, int *ovf, int *ov
     }
     return hipErrorInvalidValue;
 }
+hipError_t dispatch_expm_variants(int D, const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    switch (D) {
+#define CASE(d) \
+    case d: return grape_host::launch_expm_variants<d>(P, B, st);
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
 hipError_t dispatch_lds_limits(int D) {
     switch (D) {
 #define CASE(d) \
@@ -120,6 +130,10 @@ struct grape_plan {
     grape_dense::DenseProblem DP{};
     double *dn_opimg = nullptr, *dn_W = nullptr, *dn_E = nullptr, *dn_Q = nullptr, *dn_Carry = nullptr,
            *dn_M = nullptr, *dn_Mc = nullptr;
+    // grape_unitary_derivs workspace (allocated on first use)
+    grape::VSpec *ud_vs = nullptr;
+    cd *ud_E = nullptr, *ud_C = nullptr, *ud_V = nullptr, *ud_S = nullptr, *ud_out = nullptr;
+    int *ud_ovf = nullptr;
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -148,7 +162,8 @@ static void free_plan(grape_plan *p) {
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots,
-                    p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc};
+                    p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc,
+                    p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -650,8 +665,108 @@ int grape_plan_kernel_times(grape_plan *p, double *total_ms, long long *launches
 
 int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
                          double *U_derr_dx, double *U_derr_dx_add) {
-    (void)p; (void)x; (void)U; (void)U_dx; (void)U_dx_add; (void)U_derr; (void)U_derr_dx; (void)U_derr_dx_add;
-    return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs is not implemented in this build");
+    if (!p || !x) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (p->dense)
+        return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: ndim > GRAPE_MAX_SMALL_DIM (dense engine) "
+                                           "is not supported; use grape_fidelity_grad");
+    HIPCHECK(hipSetDevice(p->device));
+    const DevProblem &P0 = p->P;
+    const int D = P0.D, Nt = P0.Nt, np = P0.np, na = P0.na, ne = P0.ne;
+    const size_t T = (size_t)D * D;
+    // every closure call site of UnitaryCalculations.jl:45-90 as a propagator variant
+    std::vector<grape::VSpec> vs;
+    auto addv = [&](int var, int idx, double delta, int err, double errval) {
+        grape::VSpec v;
+        v.pert.var = var;
+        v.pert.index = idx;
+        v.pert.delta = delta;
+        v.err = err;
+        v.errval = errval;
+        vs.push_back(v);
+    };
+    addv(-1, 0, 0.0, -1, 0.0);
+    for (int q = 0; q < np; ++q) addv(1, q, P0.eps, -1, 0.0);
+    for (int q = 0; q < na; ++q) addv(2, q, P0.eps, -1, 0.0);
+    grape_unitary::UProblem UP{};
+    UP.off_x2 = (int)vs.size();
+    if (ne > 0) {
+        for (int q = 0; q < np; ++q) addv(1, q, P0.eps2, -1, 0.0);
+        for (int q = 0; q < na; ++q) addv(2, q, P0.eps2, -1, 0.0);
+    }
+    UP.off_err = (int)vs.size();
+    for (int e = 0; e < ne; ++e) {
+        addv(-1, 0, 0.0, e, P0.eps);
+        addv(-1, 0, 0.0, e, P0.eps2);
+        for (int q = 0; q < np; ++q) addv(1, q, P0.eps2, e, P0.eps2);
+        for (int q = 0; q < na; ++q) addv(2, q, P0.eps2, e, P0.eps2);
+    }
+    const int nv = (int)vs.size();
+    UP.D = D;
+    UP.Nt = Nt;
+    UP.np = np;
+    UP.na = na;
+    UP.ne = ne;
+    UP.nv = nv;
+    UP.nslots = np + na + ne + ne * (np + na);
+    UP.inv_eps = P0.inv_eps;
+    UP.inv_eps2sq = 1.0 / (P0.eps2 * P0.eps2);
+    // outputs, packed: U_dx | U_dx_add | U_derr | U_derr_dx | U_derr_dx_add
+    const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
+    if (!p->ud_vs) {
+        bool ok = dalloc(&p->ud_vs, (size_t)nv) == hipSuccess && dalloc(&p->ud_E, (size_t)Nt * nv * T) == hipSuccess &&
+                  dalloc(&p->ud_ovf, (size_t)Nt * nv) == hipSuccess && dalloc(&p->ud_C, (size_t)Nt * T) == hipSuccess &&
+                  dalloc(&p->ud_V, (size_t)Nt * UP.nslots * T) == hipSuccess &&
+                  dalloc(&p->ud_S, (size_t)Nt * std::max(ne, 1) * T) == hipSuccess &&
+                  dalloc(&p->ud_out, n_dx + n_dxa + n_e + n_edx + n_edxa) == hipSuccess;
+        if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (unitary derivatives)");
+    }
+    hipStream_t st = p->stream;
+    HIPCHECK(hipMemcpyAsync(p->ud_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), st));
+    DevProblem Pu = P0;
+    Pu.nv = nv;
+    Pu.vs = p->ud_vs;
+    DevBatch Bu{};
+    Bu.nb = 1;
+    Bu.x = p->d_x;
+    Bu.E = p->ud_E;
+    Bu.overflow = p->ud_ovf;
+    Bu.overflow_count = p->d_ctrl;
+    Bu.status = p->d_ctrl + 2;
+    HIPCHECK(dispatch_expm_variants(D, Pu, Bu, st));
+    grape_unitary::UBuffers UB{};
+    UB.E = p->ud_E;
+    UB.C = p->ud_C;
+    UB.V = p->ud_V;
+    UB.S = p->ud_S;
+    UB.Udx = p->ud_out;
+    UB.Udxa = UB.Udx + n_dx;
+    UB.Ue = UB.Udxa + n_dxa;
+    UB.Uedx = UB.Ue + n_e;
+    UB.Uedxa = UB.Uedx + n_edx;
+    HIPCHECK(grape_unitary::launch_assembly(UP, UB, st));
+    std::vector<cd> Ulast(T);
+    HIPCHECK(hipMemcpyAsync(Ulast.data(), p->ud_C + (size_t)(Nt - 1) * T, T * sizeof(cd), hipMemcpyDeviceToHost, st));
+    auto out = [&](double *dst, const cd *src, size_t n) -> hipError_t {
+        if (!dst || n == 0) return hipSuccess;
+        return hipMemcpyAsync(dst, src, n * sizeof(cd), hipMemcpyDeviceToHost, st);
+    };
+    HIPCHECK(out(U_dx, UB.Udx, n_dx));
+    HIPCHECK(out(U_dx_add, UB.Udxa, n_dxa));
+    HIPCHECK(out(U_derr, UB.Ue, n_e));
+    HIPCHECK(out(U_derr_dx, UB.Uedx, n_edx));
+    HIPCHECK(out(U_derr_dx_add, UB.Uedxa, n_edxa));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, st));
+    const int rc = grape_plan_synchronize(p);
+    if (rc) return rc;
+    if (U)  // C_N is stored row-major; the reference's layout is column-major
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j) {
+                U[2 * ((size_t)i + (size_t)j * D)] = Ulast[(size_t)i * D + j].re;
+                U[2 * ((size_t)i + (size_t)j * D) + 1] = Ulast[(size_t)i * D + j].im;
+            }
+    return GRAPE_OK;
 }
 
 static int dense_expm_batch(int device, int ndim, int n, const double *A, double *E, int *stats) {

@@ -118,6 +118,24 @@ hipError_t launch_expm_raw(const cd *A, cd *E, int n, int *ovf, int *ovf_count, 
     return hipGetLastError();
 }
 
+// Every variant of every step of ONE launch's evaluations stored in B.E (P.nv, P.vs
+// as given): grape_unitary_derivs' propagator table.  ERR selects the builder with
+// error terms.
+template <int D>
+hipError_t launch_expm_variants(const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    constexpr int GPW = grape::Geo<D>::GPW;
+    const long nexp = (long)B.nb * P.Nt * P.nv;
+    if (P.ne > 0)
+        hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
+                       B.overflow_count, B.status, 1);
+    return hipGetLastError();
+}
+
 template <int D, int W>
 hipError_t set_lds_limits_w() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, W>),
@@ -138,6 +156,7 @@ hipError_t set_lds_limits() {
 #define GRAPE_DECLARE_DIM(d, EXT)                                                                          \
     EXT template hipError_t launch_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &); \
     EXT template hipError_t launch_expm_raw<d>(const cd *, cd *, int, int *, int *, int *, int *, hipStream_t);  \
-    EXT template hipError_t set_lds_limits<d>();
+    EXT template hipError_t set_lds_limits<d>();                                                          \
+    EXT template hipError_t launch_expm_variants<d>(const DevProblem &, const DevBatch &, hipStream_t);
 
 }  // namespace grape_host

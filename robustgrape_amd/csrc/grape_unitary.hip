@@ -1,0 +1,228 @@
+// grape_unitary.hip -- materialised unitary derivatives for ONE control vector,
+// the output of calculate_unitary_and_derivatives (src/UnitaryCalculations.jl:20-155)
+// through the C ABI (grape_unitary_derivs).
+//
+// The propagator table E[k][v] (every finite-difference variant of every step,
+// the closure call sites :45-90) comes from the engine's k_expm.  Then:
+//   k_u_chain     C_k = E_k C_{k-1}                                    (:46)
+//   k_u_vmats     V_{k,s} = C_k^dagger (stencil_s of E[k][.]) C_{k-1}   (:51-52,59-60,67-68,77-83,89-95)
+//                 (C_k^{-1} = C_k^dagger: C_k is unitary; the reference's LU inverse
+//                  differs at the 1e-15 level)
+//   k_u_cumsum    S_{k,e} = sum_{j<=k} V^err_{j,e}                      (:112)
+//   k_u_assemble  U_dx[p,k] = U V^dx_{k,p};  U_derr_dx[p,k,e] =
+//                 U (V^dx_{k,p} S_{k-1,e} + R_{k+1,e} V^dx_{k,p} + V^mix_{k,p,e}),
+//                 R_{k+1,e} = S_{N-1,e} - S_{k,e}                       (:114-118, :124-139)
+//   k_u_reduce    U_dx_add, U_derr, U_derr_dx_add (sums over k)         (:119-123, :140-151)
+// Outputs are written straight into the reference's column-major layouts.
+//
+// This path is write-bound (U_dx is d^2 np N_t complex numbers) and runs once per
+// call, not inside an optimiser loop, so its kernels are plain thread-per-element
+// ones over LDS-staged d x d tiles (d <= GRAPE_MAX_SMALL_DIM).
+#include "grape_unitary_api.hpp"
+
+namespace grape_unitary {
+
+namespace {
+
+constexpr int BLOCK = 256;  // >= d^2 for d <= 12 (kMaxD)
+
+__device__ __forceinline__ cd u_add(cd a, cd b) { return cd{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cd u_sub(cd a, cd b) { return cd{a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cd u_scale(double s, cd a) { return cd{s * a.re, s * a.im}; }
+__device__ __forceinline__ cd u_mul(cd a, cd b) { return cd{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+__device__ __forceinline__ cd u_mulc(cd a, cd b) {  // conj(a) b
+    return cd{a.re * b.re + a.im * b.im, a.re * b.im - a.im * b.re};
+}
+
+// element (i, j) of A B, A and B row-major D x D in LDS
+__device__ __forceinline__ cd mm_el(const cd *A, const cd *B, int D, int i, int j) {
+    cd s{0.0, 0.0};
+    for (int l = 0; l < D; ++l) s = u_add(s, u_mul(A[i * D + l], B[l * D + j]));
+    return s;
+}
+// element (i, j) of A^dagger B
+__device__ __forceinline__ cd mmh_el(const cd *A, const cd *B, int D, int i, int j) {
+    cd s{0.0, 0.0};
+    for (int l = 0; l < D; ++l) s = u_add(s, u_mulc(A[l * D + i], B[l * D + j]));
+    return s;
+}
+
+__device__ __forceinline__ void load_tile(cd *dst, const cd *src, int D) {
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) dst[t] = src[t];
+}
+__device__ __forceinline__ void identity_tile(cd *dst, int D) {
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) dst[t] = cd{(t / D == t % D) ? 1.0 : 0.0, 0.0};
+}
+
+// C_k = E_k C_{k-1}: one workgroup walks the chain (the only serial dependency, :46)
+__global__ __launch_bounds__(BLOCK) void k_u_chain(UProblem P, const cd *E, cd *C) {
+    __shared__ cd sE[kMaxD * kMaxD], sC[kMaxD * kMaxD];
+    const int D = P.D, DD = D * D, t = threadIdx.x;
+    identity_tile(sC, D);
+    for (int k = 0; k < P.Nt; ++k) {
+        load_tile(sE, E + ((size_t)k * P.nv) * DD, D);
+        __syncthreads();
+        cd v{0.0, 0.0};
+        if (t < DD) v = mm_el(sE, sC, D, t / D, t % D);
+        __syncthreads();
+        if (t < DD) {
+            sC[t] = v;
+            C[(size_t)k * DD + t] = v;
+        }
+    }
+}
+
+// the stencil of slot s at step k (difference of stored variants, reference order)
+__device__ __forceinline__ cd stencil(const UProblem &P, const cd *Ek, int s, int t) {
+    const int DD = P.D * P.D;
+    const cd e0 = Ek[t];
+    if (s < P.np + P.na)  // dx_p / dxa_q: inv_eps * (E' - E)
+        return u_scale(P.inv_eps, u_sub(Ek[(size_t)(1 + s) * DD + t], e0));
+    s -= P.np + P.na;
+    if (s < P.ne)  // err_e
+        return u_scale(P.inv_eps, u_sub(Ek[(size_t)P.v_err(s) * DD + t], e0));
+    s -= P.ne;
+    // mixed: (E(x + eps2, err eps2) + E - E(err eps2) - E(x + eps2)) / eps2^2
+    const int nq = P.np + P.na, e = s / nq, q = s % nq;
+    const cd a = Ek[(size_t)P.v_mix(e, q) * DD + t];
+    const cd b = Ek[(size_t)P.v_err2(e) * DD + t];
+    const cd c = Ek[(size_t)P.v_x2(q) * DD + t];
+    return u_scale(P.inv_eps2sq, u_sub(u_sub(u_add(a, e0), b), c));
+}
+
+// V_{k,s} = C_k^dagger stencil C_{k-1}
+__global__ __launch_bounds__(BLOCK) void k_u_vmats(UProblem P, const cd *E, const cd *C, cd *V) {
+    __shared__ cd sCk[kMaxD * kMaxD], sCp[kMaxD * kMaxD], sX[kMaxD * kMaxD], sT[kMaxD * kMaxD];
+    const int D = P.D, DD = D * D, t = threadIdx.x;
+    const int k = blockIdx.x / P.nslots, s = blockIdx.x % P.nslots;
+    load_tile(sCk, C + (size_t)k * DD, D);
+    if (k > 0) load_tile(sCp, C + (size_t)(k - 1) * DD, D);
+    else identity_tile(sCp, D);
+    const cd *Ek = E + (size_t)k * P.nv * DD;
+    if (t < DD) sX[t] = stencil(P, Ek, s, t);
+    __syncthreads();
+    if (t < DD) sT[t] = mm_el(sX, sCp, D, t / D, t % D);
+    __syncthreads();
+    if (t < DD) V[((size_t)k * P.nslots + s) * DD + t] = mmh_el(sCk, sT, D, t / D, t % D);
+}
+
+// S_{k,e} = sum_{j <= k} V^err_{j,e}  (one thread per (e, element), sequential in k)
+__global__ void k_u_cumsum(UProblem P, const cd *V, cd *S) {
+    const int DD = P.D * P.D;
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= P.ne * DD) return;
+    const int e = id / DD, t = id % DD;
+    const int s = P.np + P.na + e;
+    cd acc{0.0, 0.0};
+    for (int k = 0; k < P.Nt; ++k) {
+        acc = u_add(acc, V[((size_t)k * P.nslots + s) * DD + t]);
+        S[((size_t)k * P.ne + e) * DD + t] = acc;
+    }
+}
+
+// column-major (reference) offset of element (i, j) of matrix number `m` (complex units)
+__device__ __forceinline__ size_t cm(int D, size_t m, int i, int j) { return m * D * D + (size_t)i + (size_t)j * D; }
+
+// U_dx (d,d,np,Nt) and U_derr_dx (d,d,np,Nt,ne): one workgroup per (k, p, e|-1)
+__global__ __launch_bounds__(BLOCK) void k_u_assemble(UProblem P, const cd *C, const cd *V, const cd *S, cd *Udx,
+                                                      cd *Uedx) {
+    __shared__ cd sU[kMaxD * kMaxD], sA[kMaxD * kMaxD], sB[kMaxD * kMaxD], sX[kMaxD * kMaxD];
+    const int D = P.D, DD = D * D, t = threadIdx.x, i = t / D, j = t % D;
+    const int per_k = P.np * (1 + P.ne);
+    const int k = blockIdx.x / per_k, r = blockIdx.x % per_k, p = r % P.np, e = r / P.np - 1;
+    load_tile(sU, C + (size_t)(P.Nt - 1) * DD, D);
+    load_tile(sA, V + ((size_t)k * P.nslots + p) * DD, D);  // V^dx_{k,p}
+    if (e < 0) {
+        __syncthreads();
+        if (t < DD) Udx[cm(D, (size_t)k * P.np + p, i, j)] = mm_el(sU, sA, D, i, j);
+        return;
+    }
+    // X = V^dx S_{k-1,e} + R_{k+1,e} V^dx + V^mix_{k,p,e}
+    if (k > 0) load_tile(sB, S + ((size_t)(k - 1) * P.ne + e) * DD, D);
+    else for (int q = t; q < DD; q += blockDim.x) sB[q] = cd{0.0, 0.0};
+    __syncthreads();
+    cd x{0.0, 0.0};
+    if (t < DD && k > 0) x = mm_el(sA, sB, D, i, j);
+    __syncthreads();
+    if (k < P.Nt - 1) {  // R_{k+1,e} = S_{N-1,e} - S_{k,e}
+        const cd *Stot = S + ((size_t)(P.Nt - 1) * P.ne + e) * DD, *Sk = S + ((size_t)k * P.ne + e) * DD;
+        for (int q = t; q < DD; q += blockDim.x) sB[q] = u_sub(Stot[q], Sk[q]);
+    }
+    __syncthreads();
+    if (t < DD) {
+        if (k < P.Nt - 1) x = u_add(x, mm_el(sB, sA, D, i, j));
+        const int smix = P.np + P.na + P.ne + e * (P.np + P.na) + p;
+        x = u_add(x, V[((size_t)k * P.nslots + smix) * DD + t]);
+        sX[t] = x;
+    }
+    __syncthreads();
+    if (t < DD) Uedx[cm(D, ((size_t)e * P.Nt + k) * P.np + p, i, j)] = mm_el(sU, sX, D, i, j);
+}
+
+// U_dx_add (d,d,na), U_derr (d,d,ne), U_derr_dx_add (d,d,na,ne): one workgroup per output matrix
+__global__ __launch_bounds__(BLOCK) void k_u_reduce(UProblem P, const cd *C, const cd *V, const cd *S, cd *Udxa,
+                                                    cd *Ue, cd *Uedxa) {
+    __shared__ cd sU[kMaxD * kMaxD], sA[kMaxD * kMaxD], sB[kMaxD * kMaxD], sX[kMaxD * kMaxD];
+    const int D = P.D, DD = D * D, t = threadIdx.x, i = t / D, j = t % D;
+    load_tile(sU, C + (size_t)(P.Nt - 1) * DD, D);
+    int m = blockIdx.x;
+    cd acc{0.0, 0.0};
+    cd *out;
+    size_t oidx;
+    if (m < P.na) {  // U_dx_add[q] = U sum_k V^dxa_{k,q}
+        const int s = P.np + m;
+        for (int k = 0; k < P.Nt; ++k)
+            if (t < DD) acc = u_add(acc, V[((size_t)k * P.nslots + s) * DD + t]);
+        out = Udxa;
+        oidx = m;
+    } else if ((m -= P.na) < P.ne) {  // U_derr[e] = U S_{N-1,e}
+        if (t < DD) acc = S[((size_t)(P.Nt - 1) * P.ne + m) * DD + t];
+        out = Ue;
+        oidx = m;
+    } else {  // U_derr_dx_add[q, e]
+        m -= P.ne;
+        const int q = m % P.na, e = m / P.na, sq = P.np + q;
+        const int smix = P.np + P.na + P.ne + e * (P.np + P.na) + P.np + q;
+        const cd *Stot = S + ((size_t)(P.Nt - 1) * P.ne + e) * DD;
+        for (int k = 0; k < P.Nt; ++k) {
+            __syncthreads();
+            load_tile(sA, V + ((size_t)k * P.nslots + sq) * DD, D);
+            if (k > 0) load_tile(sB, S + ((size_t)(k - 1) * P.ne + e) * DD, D);
+            __syncthreads();
+            if (t < DD && k > 0) acc = u_add(acc, mm_el(sA, sB, D, i, j));
+            __syncthreads();
+            if (k < P.Nt - 1) {
+                const cd *Sk = S + ((size_t)k * P.ne + e) * DD;
+                for (int w = t; w < DD; w += blockDim.x) sB[w] = u_sub(Stot[w], Sk[w]);
+            }
+            __syncthreads();
+            if (t < DD && k < P.Nt - 1) acc = u_add(acc, mm_el(sB, sA, D, i, j));
+        }
+        for (int k = 0; k < P.Nt; ++k)
+            if (t < DD) acc = u_add(acc, V[((size_t)k * P.nslots + smix) * DD + t]);
+        out = Uedxa;
+        oidx = (size_t)e * P.na + q;
+    }
+    __syncthreads();
+    if (t < DD) sX[t] = acc;
+    __syncthreads();
+    if (t < DD) out[cm(D, oidx, i, j)] = mm_el(sU, sX, D, i, j);
+}
+
+}  // namespace
+
+hipError_t launch_assembly(const UProblem &P, const UBuffers &B, hipStream_t st) {
+    const int DD = P.D * P.D;
+    hipLaunchKernelGGL(k_u_chain, dim3(1), dim3(BLOCK), 0, st, P, B.E, B.C);
+    hipLaunchKernelGGL(k_u_vmats, dim3((unsigned)(P.Nt * P.nslots)), dim3(BLOCK), 0, st, P, B.E, B.C, B.V);
+    if (P.ne > 0)
+        hipLaunchKernelGGL(k_u_cumsum, dim3((P.ne * DD + 63) / 64), dim3(64), 0, st, P, B.V, B.S);
+    hipLaunchKernelGGL(k_u_assemble, dim3((unsigned)(P.Nt * P.np * (1 + P.ne))), dim3(BLOCK), 0, st, P, B.C, B.V,
+                       B.S, B.Udx, B.Uedx);
+    const int nred = P.na + P.ne + P.na * P.ne;
+    if (nred > 0)
+        hipLaunchKernelGGL(k_u_reduce, dim3(nred), dim3(BLOCK), 0, st, P, B.C, B.V, B.S, B.Udxa, B.Ue, B.Uedxa);
+    return hipGetLastError();
+}
+
+}  // namespace grape_unitary

@@ -1,0 +1,39 @@
+// grape_unitary_api.hpp -- what the C ABI sees of grape_unitary.hip (materialised
+// unitary derivatives, grape_unitary_derivs).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "grape_kernels.hpp"
+
+namespace grape_unitary {
+
+using grape::cd;
+
+constexpr int kMaxD = 12;  // GRAPE_MAX_SMALL_DIM
+
+// Propagator variants of one step, E[k][v] (built by the engine's k_expm):
+//   0 nominal | 1 + q, q < np + na: x_q + eps (controls, then x_add)
+//   ne > 0:  off_x2 + q: x_q + eps2 | per error e (stride 2 + np + na), from off_err:
+//            err eps, err eps2, then x_q + eps2 with err eps2
+// Slots of V (per step): dx_p (np) | dxa_q (na) | err_e (ne) | mix_{e,q} (ne x (np + na)).
+struct UProblem {
+    int D, Nt, np, na, ne, nv, nslots;
+    int off_x2, off_err;
+    double inv_eps, inv_eps2sq;
+    __host__ __device__ int v_x2(int q) const { return off_x2 + q; }
+    __host__ __device__ int v_err(int e) const { return off_err + e * (2 + np + na); }
+    __host__ __device__ int v_err2(int e) const { return v_err(e) + 1; }
+    __host__ __device__ int v_mix(int e, int q) const { return v_err(e) + 2 + q; }
+};
+
+struct UBuffers {
+    const cd *E;  // [Nt][nv][D][D] row-major
+    cd *C;        // [Nt][D][D]     C_k
+    cd *V;        // [Nt][nslots][D][D]
+    cd *S;        // [Nt][ne][D][D] cumulative sums of V^err
+    cd *Udx, *Uedx, *Udxa, *Ue, *Uedxa;  // outputs, reference column-major layouts
+};
+
+hipError_t launch_assembly(const UProblem &P, const UBuffers &B, hipStream_t st);
+
+}  // namespace grape_unitary

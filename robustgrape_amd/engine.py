@@ -81,6 +81,20 @@ class GrapePlan:
             self.handle, int(nbatch), ctypes.c_void_p(x_ptr), ctypes.c_void_p(F_ptr),
             ctypes.c_void_p(Fdx_ptr), ctypes.c_void_p(Fd2_ptr or None), ctypes.c_void_p(Fd2dx_ptr or None)))
 
+    def unitary_derivs(self, x):
+        """grape_unitary_derivs: the 6-tuple of src/UnitaryCalculations.jl:154 for ONE x, as
+        complex arrays in the reference's shapes (column-major, like Julia)."""
+        up = self.up
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.ndim != 1 or x.shape[0] != self.nx:
+            raise AssertionError("Control parameter size must be a multiple of time steps")
+        d, nt, npar, na, ne = up.ndim, up.ntimes, self.nparam, up.nb_additional_param, self.nerr
+        shapes = [(d, d), (d, d, npar, nt), (d, d, na), (d, d, ne), (d, d, npar, nt, ne), (d, d, na, ne)]
+        outs = [np.zeros(sh, dtype=np.complex128, order="F") for sh in shapes]
+        ptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if a.size else None
+        _capi.check(_capi.lib().grape_unitary_derivs(self.handle, _capi.dptr(x), *[ptr(a) for a in outs]))
+        return tuple(outs)
+
     def set_profiling(self, enable: bool):
         _capi.check(_capi.lib().grape_plan_set_profiling(self.handle, int(bool(enable))))
 
@@ -138,7 +152,23 @@ def calculate_fidelity_and_derivatives(fidelity_problem: FidelityRobustGRAPEProb
     return float(F[0]), Fdx[0], Fd2[0], Fd2dx[0]
 
 
+_unitary_fp: dict = {}
+
+
 def calculate_unitary_and_derivatives(unitary_problem, x, device: int = 0):
-    """src/UnitaryCalculations.jl:20-155 through grape_unitary_derivs (C ABI)."""
-    raise NotImplementedError("grape_unitary_derivs (materialised U_dx tensors, SURVEY.md 8f row f4) "
-                              "is not in this build; use calculate_fidelity_and_derivatives")
+    """GPU restatement of src/UnitaryCalculations.jl:20-155 (through grape_unitary_derivs).
+
+    Returns (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add) with the reference's shapes
+    (d,d), (d,d,np,N_t), (d,d,na), (d,d,ne), (d,d,np,N_t,ne), (d,d,na,ne)."""
+    from .operators import OperatorBasisTarget, Term
+    x = np.asarray(x, dtype=np.float64)
+    _, _, nparam = split_x(unitary_problem, x)
+    with _cache_lock:
+        fp = _unitary_fp.get(id(unitary_problem))
+        if fp is None or fp.unitary_problem is not unitary_problem:
+            # the descriptor needs a projector and a target; neither enters these outputs
+            eye = np.eye(unitary_problem.ndim, dtype=np.complex128)
+            fp = FidelityRobustGRAPEProblem(unitary_problem, np.eye(unitary_problem.ndim),
+                                            OperatorBasisTarget([Term(eye)]))
+            _unitary_fp[id(unitary_problem)] = fp
+    return get_plan(fp, nparam, device, max_batch=1).unitary_derivs(x)

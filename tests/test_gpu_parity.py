@@ -235,3 +235,75 @@ def test_large_batch_plan_matches_single():
         Fs, gs, _, _ = one.fidelity_grad(X[b][None, :])
         assert abs(Fs[0] - F[b]) <= T1 and np.max(np.abs(gs[0] - Fdx[b])) <= T2 * np.max(np.abs(gs[0])) + T2_ABS
     one.close()
+
+
+# ---------------------------------------------------------------- materialised derivatives
+def _assert_unitary(got, ref, fac=1.0):
+    """T1 for U; T2 for eps quantities (U_dx, U_dx_add, U_derr); T3 for the eps2 mixed ones.
+    fac = max(1, max_k |dt H_k|_1) scales the FD tiers: an uncontracted (E' - E)/eps carries
+    the exponential's rounding (T0: 1e-13 x max(1, |A|_1), squarings for Pade 13) over eps."""
+    names = ("U", "U_dx", "U_dx_add", "U_derr", "U_derr_dx", "U_derr_dx_add")
+    for name, g, r in zip(names, got, ref):
+        assert g.shape == r.shape, (name, g.shape, r.shape)
+        if r.size == 0:
+            continue
+        err = np.max(np.abs(g - r))
+        scale = np.max(np.abs(r))
+        if name == "U":
+            tol = T1 * fac
+        elif name in ("U_derr_dx", "U_derr_dx_add"):
+            tol = T3 * fac * scale + (T3_XADD_ABS if name == "U_derr_dx_add" else T3_ABS)
+        else:
+            tol = T2 * fac * scale + T2_ABS
+        assert err <= tol, (name, err, scale)
+
+
+def test_unitary_derivatives_match_golden():
+    """grape_unitary_derivs vs the committed fixture (d = 5, N_t = 8, two error sources)."""
+    from robustgrape_amd import calculate_unitary_and_derivatives
+    g = _golden("unitary_small")
+    up = P.sym_problem(8, errors=("amp", "freq")).unitary_problem
+    got = calculate_unitary_and_derivatives(up, g["x"])
+    _assert_unitary(got, [g[k] for k in ("U", "U_dx", "U_dx_add", "U_derr", "U_derr_dx", "U_derr_dx_add")])
+
+
+@pytest.mark.parametrize("d,ntimes,nerr", [(9, 1, 0), (9, 40, 0), (9, 23, 4), (7, 30, 2), (5, 3, 1)])
+def test_unitary_derivatives_match_live_oracle(d, ntimes, nerr):
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_unitary_and_derivatives
+    errs = {0: (), 1: ("amp",), 2: ("amp", "freq")}
+    if d == 9:
+        mk = lambda dev: P.full9_problem(ntimes, nerr=nerr, device=dev)
+    elif d == 7:
+        mk = lambda dev: P.fullblk_problem(ntimes, errors=errs[nerr], device=dev)
+    else:
+        mk = lambda dev: P.sym_problem(ntimes, errors=errs[nerr], device=dev)
+    x = P.random_x(ntimes, 500 + ntimes)
+    up = mk(False).unitary_problem
+    ref = O.calculate_unitary_and_derivatives(up, x)
+    got = calculate_unitary_and_derivatives(mk(True).unitary_problem, x)
+    dt = up.t0 / ntimes
+    fac = max(1.0, max(np.abs(dt * up.H0(k + 1, x[k:k + 1], x[-1:])).sum(axis=0).max() for k in range(ntimes)))
+    _assert_unitary(got, ref, fac)
+
+
+def test_unitary_derivatives_consistent_with_fidelity_gradient():
+    """F_dx from the fused kernels equals the reference's trace formula applied to the
+    materialised U_dx (FidelityCalculations.jl:56-65)."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives
+    fp = P.full9_problem(32)
+    x = P.random_x(32, 9)
+    F, Fdx, _, _ = calculate_fidelity_and_derivatives(fp, x)
+    U, Udx = calculate_unitary_and_derivatives(fp.unitary_problem, x)[:2]
+    U0 = fp.target_unitary(x[-1:])
+    W = np.diag(P.W_FULL9).astype(complex)
+    Pm = (W != 0).astype(float)
+    D = W.sum().real
+    trm = lambda A: np.sum(W * np.diag(A))
+    tau_c = np.conj(trm((Pm[:, None] * U0.conj().T) @ U))
+    for k in (0, 13, 31):
+        Ud = Udx[:, :, 0, k]
+        A1 = (Pm[:, None] * U0.conj().T) @ Ud @ (Pm[:, None] * U.conj().T) @ U0
+        A2 = (Pm[:, None] * U0.conj().T) @ U @ (Pm[:, None] * Ud.conj().T) @ U0
+        ref = (np.real(trm(A1 + A2)) + 2 * np.real(tau_c * trm((Pm[:, None] * U0.conj().T) @ Ud))) / (D * (D + 1))
+        assert abs(ref - Fdx[k]) <= T2 * np.max(np.abs(Fdx)) + T2_ABS
