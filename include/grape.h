@@ -189,6 +189,22 @@ int grape_unitary_derivs(grape_plan *plan, const double *x,
                          double *U_derr, double *U_derr_dx, double *U_derr_dx_add);
 
 /*
+ * Interaction-picture error operators for ONE control vector, replacing
+ * calculate_interaction_error_operators (src/UnitaryCalculations.jl:180-204):
+ *   O (d, d, ntimes, nerr) complex column-major,
+ *   O[:, :, k, e] = C_{k-1}^{-1} (Herror_e(k, x, x_add, eps) / eps) C_{k-1}, C_0 = I.
+ * Nothing is written when the problem has no error sources.
+ */
+int grape_interaction_error_operators(grape_plan *plan, const double *x, double *O);
+
+/*
+ * Time-resolved expectation values of the error generators for ONE control
+ * vector, replacing calculate_expectation_values (src/FidelityCalculations.jl:368-390):
+ *   ev (ntimes, nerr) real column-major, ev[k, e] = Re(dt tr(P0 sum_{j<=k} O_j,e)) / tr(P0).
+ */
+int grape_expectation_values(grape_plan *plan, const double *x, double *ev);
+
+/*
  * Per-kernel timing for measurement (bench.py's roofline): when enabled, every
  * launch of the plan's pipeline is bracketed by HIP events recorded ON THE
  * PLAN'S STREAM; grape_plan_synchronize accumulates the elapsed times.

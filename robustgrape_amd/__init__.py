@@ -14,6 +14,8 @@ from .operators import (OperatorBasisError, OperatorBasisHamiltonian, OperatorBa
 from .engine import (GrapePlan, calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
                      clear_plans, get_plan)
 from . import rydberg as RydbergTools
+from .analysis import (calculate_expectation_values, calculate_fidelity_response, calculate_fidelity_response_fft,
+                       calculate_interaction_error_operators)
 from .regularization import regularization_cost, regularization_cost_phase
 from .optimize import (OptimizationResult, minimizer, minimum, optimize_fidelity_and_error_sources,
                        optimize_restarts)
@@ -28,5 +30,6 @@ __all__ = [
     "calculate_fidelity_and_derivatives", "calculate_unitary_and_derivatives", "GrapePlan", "get_plan",
     "clear_plans", "OperatorBasisHamiltonian", "OperatorBasisError", "OperatorBasisTarget", "Term",
     "RydbergTools", "regularization_cost", "regularization_cost_phase", "optimize_fidelity_and_error_sources",
-    "optimize_restarts", "OptimizationResult", "minimizer", "minimum", "FidelityOptimProblem", "compute_fidelity_and_gradient", "compute_unitary_and_derivatives",
+    "optimize_restarts", "calculate_interaction_error_operators", "calculate_expectation_values",
+    "calculate_fidelity_response", "calculate_fidelity_response_fft", "OptimizationResult", "minimizer", "minimum", "FidelityOptimProblem", "compute_fidelity_and_gradient", "compute_unitary_and_derivatives",
 ]

@@ -20,7 +20,8 @@ STATUS_NAMES = {-1: "GRAPE_ERR_INVALID", -2: "GRAPE_ERR_UNSUPPORTED", -3: "GRAPE
 EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grape_plan_create",
             "grape_plan_destroy", "grape_plan_stream", "grape_plan_set_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
-            "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times"]
+            "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times",
+            "grape_interaction_error_operators", "grape_expectation_values"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
 ABI_VERSION = 2  # GRAPE_ABI_VERSION in include/grape.h
@@ -66,6 +67,10 @@ def lib():
         L.grape_expm_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp,
                                        ctypes.POINTER(ctypes.c_int)]
         L.grape_expm_batch.restype = ctypes.c_int
+        L.grape_interaction_error_operators.argtypes = [vp, dp, dp]
+        L.grape_interaction_error_operators.restype = ctypes.c_int
+        L.grape_expectation_values.argtypes = [vp, dp, dp]
+        L.grape_expectation_values.restype = ctypes.c_int
         L.grape_plan_set_profiling.argtypes = [vp, ctypes.c_int]
         L.grape_plan_set_profiling.restype = ctypes.c_int
         L.grape_plan_kernel_times.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]

@@ -1,0 +1,138 @@
+"""Error-analysis entry points of the reference on the GPU.
+
+* ``calculate_interaction_error_operators`` -- src/UnitaryCalculations.jl:180-204,
+  HIP kernels behind ``grape_interaction_error_operators`` (nominal propagators
+  from the engine's k_expm, the chain C_k, then C_{k-1}^dagger Herror C_{k-1}).
+* ``calculate_expectation_values`` -- src/FidelityCalculations.jl:368-390,
+  ``grape_expectation_values``.
+* ``calculate_fidelity_response`` (:246-280) and ``calculate_fidelity_response_fft``
+  (:306-343): the interaction operators stay on the device and the frequency sums,
+  FFTs (rocFFT through torch.fft) and trace contractions run there as batched
+  tensor ops; only the (nfreq, nerr) result comes back.
+"""
+from __future__ import annotations
+
+import math
+import threading
+
+import numpy as np
+import torch
+
+from . import _capi
+from .engine import get_plan
+from .operators import OperatorBasisTarget, Term
+from .types import FidelityRobustGRAPEProblem, split_x
+
+_lock = threading.Lock()
+_fp_for_up: dict = {}
+
+
+def _plan(fp_or_up, x, device):
+    if isinstance(fp_or_up, FidelityRobustGRAPEProblem):
+        fp = fp_or_up
+    else:  # a UnitaryRobustGRAPEProblem: the descriptor needs a projector and target (unused here)
+        up = fp_or_up
+        with _lock:
+            fp = _fp_for_up.get(id(up))
+            if fp is None or fp.unitary_problem is not up:
+                fp = FidelityRobustGRAPEProblem(up, np.eye(up.ndim),
+                                                OperatorBasisTarget([Term(np.eye(up.ndim, dtype=np.complex128))]))
+                _fp_for_up[id(up)] = fp
+    _, _, nparam = split_x(fp.unitary_problem, x)
+    return fp, get_plan(fp, nparam, device, max_batch=1)
+
+
+def calculate_interaction_error_operators(unitary_problem, x, device: int = 0) -> np.ndarray:
+    """(ndim, ndim, ntimes, nerr) complex, like the reference's permuted tensor."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    fp, plan = _plan(unitary_problem, x, device)
+    up = fp.unitary_problem
+    O = np.zeros((up.ndim, up.ndim, up.ntimes, len(up.error_sources)), dtype=np.complex128, order="F")
+    if O.size:
+        _capi.check(_capi.lib().grape_interaction_error_operators(plan.handle, _capi.dptr(x), _capi.dptr(O)))
+    return O
+
+
+def calculate_expectation_values(fidelity_problem: FidelityRobustGRAPEProblem, x, device: int = 0) -> np.ndarray:
+    """(ntimes, nerr) real."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    fp, plan = _plan(fidelity_problem, x, device)
+    up = fp.unitary_problem
+    ev = np.zeros((up.ntimes, len(up.error_sources)), dtype=np.float64, order="F")
+    if ev.size:
+        _capi.check(_capi.lib().grape_expectation_values(plan.handle, _capi.dptr(x), _capi.dptr(ev)))
+    return ev
+
+
+def _device_operators(fp, x, device):
+    """Interaction operators as a (nerr, ntimes, d, d) complex128 tensor on the device."""
+    O = calculate_interaction_error_operators(fp.unitary_problem, x, device)
+    return torch.from_numpy(np.ascontiguousarray(O.transpose(3, 2, 0, 1))).to(torch.device("cuda", device))
+
+
+def _projector_parts(fp, dev):
+    W = torch.as_tensor(np.diag(np.asarray(fp.projector, dtype=np.float64)).copy(), device=dev).to(torch.complex128)
+    P = (W != 0).to(torch.complex128)
+    D = float(np.trace(np.asarray(fp.projector, dtype=np.float64)))
+    return W, P, D
+
+
+def _response_terms(A, B, W, P, D):
+    """Re of the three trace terms of :268-272 / :333-337 for matching stacks A, B (..., d, d):
+    1/D tr(W A B P) - 1/(D(D+1)) tr(W A P B P) - 1/(D(D+1)) tr(W A P) tr(W B P), before Re."""
+    AB = A @ (B * P[None, :])                        # A B P
+    t1 = torch.einsum("i,...ii->...", W, AB)
+    APBP = (A * P[None, :]) @ (B * P[None, :])       # A P B P
+    t2 = torch.einsum("i,...ii->...", W, APBP)
+    t3 = torch.einsum("i,...ii->...", W, A * P[None, :]) * torch.einsum("i,...ii->...", W, B * P[None, :])
+    return t1 / D - t2 / (D * (D + 1)) - t3 / (D * (D + 1))
+
+
+def calculate_fidelity_response(fidelity_problem: FidelityRobustGRAPEProblem, x, normalized_frequencies,
+                                device: int = 0) -> np.ndarray:
+    """src/FidelityCalculations.jl:246-280 -> (nfreq, nerr)."""
+    up = fidelity_problem.unitary_problem
+    nt, dt = up.ntimes, up.t0 / up.ntimes
+    w = torch.as_tensor(np.asarray(normalized_frequencies, dtype=np.float64))
+    nerr = len(up.error_sources)
+    if nerr == 0 or w.numel() == 0:
+        return np.zeros((w.numel(), nerr))
+    O = _device_operators(fidelity_problem, x, device)                # (ne, nt, d, d)
+    dev = O.device
+    W, P, D = _projector_parts(fidelity_problem, dev)
+    w = w.to(dev)
+    k0 = torch.arange(nt, dtype=torch.float64, device=dev)            # time_indices (0-based, :262)
+    k1 = k0 + 1.0                                                     # k = 1..ntimes (:266)
+    out = torch.empty(w.numel(), nerr, dtype=torch.float64, device=dev)
+    for e in range(nerr):
+        ph0 = torch.exp(-1j * w[:, None] * dt * k0[None, :])            # (nf, nt)
+        S = torch.einsum("ft,tij->fij", ph0, O[e])                    # sum_error_freq per frequency
+        ph1 = torch.exp(1j * w[:, None] * dt * k1[None, :])             # (nf, nt)
+        terms = _response_terms(O[e][None, :, :, :], S[:, None, :, :], W, P, D)  # (nf, nt)
+        out[:, e] = dt ** 2 * torch.sum(torch.real(ph1 * terms), dim=1)
+    return out.cpu().numpy()
+
+
+def calculate_fidelity_response_fft(fidelity_problem: FidelityRobustGRAPEProblem, x, oversampling: int = 1,
+                                    device: int = 0):
+    """src/FidelityCalculations.jl:306-343 -> (response (ntimes*oversampling, nerr), norm_frequencies)."""
+    if oversampling < 1:
+        raise AssertionError("oversampling >= 1")
+    up = fidelity_problem.unitary_problem
+    nt, dt = up.ntimes, up.t0 / up.ntimes
+    N = nt * oversampling
+    nerr = len(up.error_sources)
+    freqs = (2 * math.pi / (N * dt)) * np.arange(N, dtype=np.float64)
+    if nerr == 0:
+        return np.zeros((N, 0)), freqs
+    O = _device_operators(fidelity_problem, x, device)
+    dev = O.device
+    W, P, D = _projector_parts(fidelity_problem, dev)
+    out = torch.empty(N, nerr, dtype=torch.float64, device=dev)
+    for e in range(nerr):
+        Oe = torch.zeros(N, up.ndim, up.ndim, dtype=torch.complex128, device=dev)
+        Oe[:nt] = O[e]
+        Ff = torch.fft.fft(Oe, dim=0)
+        Fi = N * torch.fft.ifft(Oe, dim=0)
+        out[:, e] = dt ** 2 * torch.real(_response_terms(Fi, Ff, W, P, D))
+    return out.cpu().numpy(), freqs

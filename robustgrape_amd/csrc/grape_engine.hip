@@ -52,6 +52,8 @@ int fail(int code, const std::string &msg) {
     } while (0)
 
 constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow;
+constexpr int kMaxSlices = 4;                  // batch slices per call (enqueue_call)
+constexpr int kCtrlInts = 4 + 2 * kMaxSlices;  // [0..1] single-eval counters, [2] status, per-slice counters
 using grape_host::KMark;
 using grape_host::launch_pipeline;
 using grape_host::launch_expm_raw;
@@ -109,6 +111,10 @@ struct grape_plan {
     int device = 0;
     hipStream_t stream = nullptr;      // where work is enqueued (own_stream or the caller's)
     hipStream_t own_stream = nullptr;
+    hipStream_t aux_stream = nullptr;  // second stream for batch slices (enqueue_call)
+    hipStream_t cur_stream = nullptr;  // stream of the launch being enqueued (profiling marks)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int nsplit = 1, split_min = 1 << 30;  // slices per call and the batch size from which to slice
     int *h_status = nullptr;           // pinned copy of the device status word
     DevProblem P{};
     int max_batch = 0;
@@ -172,6 +178,9 @@ static void free_plan(grape_plan *p) {
         (void)hipEventDestroy(pe.b);
     }
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+    if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
 }
@@ -279,9 +288,9 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, do
               dalloc(&p->dn_Carry, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_M, MB * IMG) == hipSuccess &&
               dalloc(&p->dn_Mc, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
-              dalloc(&p->d_ctrl, 4) == hipSuccess;
+              dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess;
     if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense)");
-    if (hipMemset(p->d_ctrl, 0, 4 * sizeof(int)) != hipSuccess ||
+    if (hipMemset(p->d_ctrl, 0, kCtrlInts * sizeof(int)) != hipSuccess ||
         hipMemcpy(p->dn_opimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->dn_W, W.data(), 64 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
@@ -460,7 +469,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_part, MB * P.Nt * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
-              dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, 4) == hipSuccess &&
+              dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess &&
               dalloc(&p->d_vs, vs.size()) == hipSuccess;
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);
     if (ok && P.ne == 0)
@@ -472,7 +481,21 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
     if (!ok) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed"));
-    if (hipMemset(p->d_ctrl, 0, 4 * sizeof(int)) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "memset failed"));
+    if (hipMemset(p->d_ctrl, 0, kCtrlInts * sizeof(int)) != hipSuccess)
+        return bail(fail(GRAPE_ERR_HIP, "memset failed"));
+    // batch slicing over two streams (enqueue_call): large launches only
+    if (hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(GRAPE_ERR_HIP, "stream/event creation failed"));
+    // Measured on C2 (B = 1 024): 1 slice 596k, 2 slices 589k, 4 slices 572k evals/s -- the
+    // exp kernels already fill the CUs the scan leaves idle, so slicing is off by default.
+    p->nsplit = 1;
+    p->split_min = 2 * ncu;
+    if (const char *sp = std::getenv("GRAPE_SPLIT")) {  // tuning override: slices per call (1..kMaxSlices)
+        const int v = std::atoi(sp);
+        if (v >= 1 && v <= kMaxSlices) p->nsplit = v;
+    }
     if (hipMemcpy(p->d_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     if (P.ne > 0 &&
@@ -509,8 +532,14 @@ int grape_plan_set_stream(grape_plan *plan, void *stream) {
     return GRAPE_OK;
 }
 
+// One launch sequence of `nb` evaluations on stream `st`.  `w0` is the first
+// workspace row it uses (slices of one call occupy disjoint rows) and `slot`
+// selects its private overflow counters, so slices may run concurrently on
+// different streams.  The caller copies the status word afterwards.
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
-                   double *d_Fd2dx) {
+                   double *d_Fd2dx, hipStream_t st = nullptr, size_t w0 = 0, int slot = 0) {
+    if (!st) st = p->stream;
+    p->cur_stream = st;
     KMark mk;
     if (p->profiling) {
         mk.ctx = p;
@@ -518,7 +547,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             grape_plan *pl = static_cast<grape_plan *>(ctx);
             hipEvent_t e = pl->get_event();
             if (!e) return;
-            (void)hipEventRecord(e, pl->stream);
+            (void)hipEventRecord(e, pl->cur_stream);
             if (phase == 0) {
                 pl->pending.push_back({k, e, nullptr});
             } else {
@@ -539,35 +568,71 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         DB.Fdx = d_Fdx;
         DB.status = p->d_ctrl + 2;
         DB.mstats = nullptr;
-        HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, p->stream, mk));
-        HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+        HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, st, mk));
         return GRAPE_OK;
     }
+    const DevProblem &P = p->P;
+    const size_t T = (size_t)P.D * P.D, nvg = (size_t)P.np + (P.xadd_dep ? P.na : 0);
     DevBatch B{};
-    B.Carry = p->d_Carry;
-    B.Ub = p->d_Ub;
-    B.Me = p->d_Me;
     B.Fd2 = d_Fd2;
     B.Fd2dx = d_Fd2dx;
     B.nb = nb;
     B.x = d_x;
-    B.E = p->d_E;
-    B.Q = p->d_Q;
-    B.Mc = p->d_Mc;
     B.F = d_F;
     B.Fdx = d_Fdx;
-    B.part_add = p->d_part;
-    B.tgt_part = p->d_tgt_part;
-    B.overflow = p->d_ovf;
-    B.overflow_count = p->d_ctrl;
-    B.ovf2 = p->d_ovf2;
-    B.ovf2_count = p->d_ctrl + 1;
+    // workspace rows [w0, w0 + nb)
+    B.E = p->d_E + w0 * P.Nt * P.nv * T;
+    B.Q = p->d_Q + w0 * P.Nt * T;
+    B.Mc = p->d_Mc + w0 * P.nchunks * T;
+    B.part_add = p->d_part + w0 * P.Nt * std::max(P.na, 1);
+    B.tgt_part = p->d_tgt_part + w0 * std::max(P.na, 1);
+    B.overflow = p->d_ovf + w0 * P.Nt * P.nv;
+    if (P.ne == 0) {
+        B.ovf2 = p->d_ovf2 + w0 * P.Nt * nvg;
+        B.ovf2_slots = p->d_ovf2_slots + w0 * P.Nt * nvg * T;
+    } else {
+        B.Carry = p->d_Carry + w0 * P.nchunks * T;
+        B.Ub = p->d_Ub + w0 * T;
+        B.Me = p->d_Me + w0 * P.ne * P.nchunks * 3 * T;
+    }
+    // ctrl: [2] status (sticky until grape_plan_synchronize reports it), per slot s:
+    // [4 + 2s] k_expm overflow count, [5 + 2s] k_expm_grad overflow count
+    int *cnt = p->d_ctrl + 4 + 2 * slot;
+    B.overflow_count = cnt;
+    B.ovf2_count = cnt + 1;
     B.status = p->d_ctrl + 2;
-    B.ovf2_slots = p->d_ovf2_slots;
-    // ctrl: [0] k_expm overflow count, [1] k_expm_grad overflow count, [2] status
-    // (sticky until grape_plan_synchronize reports it; copied to pinned memory below)
-    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), p->stream));
-    HIPCHECK(dispatch_pipeline(p->P.D, p->P, B, p->stream, mk));
+    HIPCHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+    HIPCHECK(dispatch_pipeline(P.D, P, B, st, mk));
+    return GRAPE_OK;
+}
+
+// Enqueue one call's batch: on the small-d engine a large batch is cut into
+// slices alternating between the plan's stream and its auxiliary stream, so
+// the latency-bound scan of one slice overlaps the exponential kernels of the
+// next ("two streams").  Ends with the status word copied to
+// pinned memory on the plan's stream, after both streams joined.
+static int enqueue_call(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
+                        double *d_Fd2dx) {
+    const int nx = p->P.nx, ne = p->P.ne;
+    int ns = 1;
+    if (!p->dense && p->aux_stream) ns = nb >= p->split_min ? p->nsplit : 1;
+    if (ns <= 1) {
+        if (int rc = enqueue(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx)) return rc;
+    } else {
+        HIPCHECK(hipEventRecord(p->ev_fork, p->stream));
+        HIPCHECK(hipStreamWaitEvent(p->aux_stream, p->ev_fork, 0));
+        const int per = (nb + ns - 1) / ns;
+        for (int s = 0, b0 = 0; b0 < nb; ++s, b0 += per) {
+            const int n = std::min(per, nb - b0);
+            hipStream_t st = (s & 1) ? p->aux_stream : p->stream;
+            int rc = enqueue(p, n, d_x + (size_t)b0 * nx, d_F + b0, d_Fdx + (size_t)b0 * nx,
+                             ne ? d_Fd2 + (size_t)b0 * ne : nullptr, ne ? d_Fd2dx + (size_t)b0 * ne * nx : nullptr, st,
+                             (size_t)b0, s);
+            if (rc) return rc;
+        }
+        HIPCHECK(hipEventRecord(p->ev_join, p->aux_stream));
+        HIPCHECK(hipStreamWaitEvent(p->stream, p->ev_join, 0));
+    }
     HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return GRAPE_OK;
 }
@@ -593,9 +658,9 @@ int grape_fidelity_grad_device_async(grape_plan *p, int nbatch, const double *d_
     HIPCHECK(hipSetDevice(p->device));
     for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
         const int nb = std::min(p->max_batch, nbatch - b0);
-        int rc = enqueue(p, nb, d_x + (size_t)b0 * p->P.nx, d_F + b0, d_F_dx + (size_t)b0 * p->P.nx,
-                         p->P.ne ? d_F_d2err + (size_t)b0 * p->P.ne : nullptr,
-                         p->P.ne ? d_F_d2err_dx + (size_t)b0 * p->P.ne * p->P.nx : nullptr);
+        int rc = enqueue_call(p, nb, d_x + (size_t)b0 * p->P.nx, d_F + b0, d_F_dx + (size_t)b0 * p->P.nx,
+                              p->P.ne ? d_F_d2err + (size_t)b0 * p->P.ne : nullptr,
+                              p->P.ne ? d_F_d2err_dx + (size_t)b0 * p->P.ne * p->P.nx : nullptr);
         if (rc) return rc;
     }
     return GRAPE_OK;
@@ -626,7 +691,7 @@ int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, d
         const int nb = std::min(p->max_batch, nbatch - b0);
         HIPCHECK(hipMemcpyAsync(p->d_x, x + (size_t)b0 * nx, (size_t)nb * nx * sizeof(double),
                                 hipMemcpyHostToDevice, p->stream));
-        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx, p->d_Fd2, p->d_Fd2dx);
+        int rc = enqueue_call(p, nb, p->d_x, p->d_F, p->d_Fdx, p->d_Fd2, p->d_Fd2dx);
         if (rc) return rc;
         HIPCHECK(hipMemcpyAsync(F + b0, p->d_F, nb * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         if (p->P.ne > 0) {
@@ -661,6 +726,80 @@ int grape_plan_kernel_times(grape_plan *p, double *total_ms, long long *launches
         }
     }
     return GRAPE_OK;
+}
+
+// workspace of the single-evaluation analysis entry points (unitary derivatives,
+// interaction-picture error operators, expectation values), allocated on first use
+static int ud_alloc(grape_plan *p) {
+    if (p->ud_vs) return GRAPE_OK;
+    const DevProblem &P = p->P;
+    const size_t T = (size_t)P.D * P.D, Nt = P.Nt, np = P.np, na = P.na, ne = P.ne;
+    const size_t nv = 1 + (np + na) * (ne > 0 ? 2 : 1) + ne * (2 + np + na);
+    const size_t nslots = np + na + ne + ne * (np + na);
+    const size_t nout = T * (np * Nt + na + ne + np * Nt * ne + na * ne + Nt * ne);
+    const bool ok = dalloc(&p->ud_vs, nv) == hipSuccess && dalloc(&p->ud_E, Nt * nv * T) == hipSuccess &&
+                    dalloc(&p->ud_ovf, Nt * nv) == hipSuccess && dalloc(&p->ud_C, Nt * T) == hipSuccess &&
+                    dalloc(&p->ud_V, Nt * nslots * T) == hipSuccess &&
+                    dalloc(&p->ud_S, Nt * std::max<size_t>(ne, 1) * T) == hipSuccess && dalloc(&p->ud_out, nout) == hipSuccess;
+    return ok ? GRAPE_OK : fail(GRAPE_ERR_ALLOC, "device allocation failed (single-evaluation workspace)");
+}
+
+// nominal propagators E_k and the chain C_k of one x into the ud workspace
+static int ud_chain(grape_plan *p, const double *x) {
+    const DevProblem &P0 = p->P;
+    grape::VSpec nominal{};
+    nominal.pert.var = -1;
+    nominal.err = -1;
+    hipStream_t st = p->stream;
+    HIPCHECK(hipMemcpyAsync(p->ud_vs, &nominal, sizeof(nominal), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), st));
+    DevProblem Pu = P0;
+    Pu.nv = 1;
+    Pu.vs = p->ud_vs;
+    DevBatch Bu{};
+    Bu.nb = 1;
+    Bu.x = p->d_x;
+    Bu.E = p->ud_E;
+    Bu.overflow = p->ud_ovf;
+    Bu.overflow_count = p->d_ctrl;
+    Bu.status = p->d_ctrl + 2;
+    HIPCHECK(dispatch_expm_variants(P0.D, Pu, Bu, st));
+    grape_unitary::UProblem UP{};
+    UP.D = P0.D;
+    UP.Nt = P0.Nt;
+    UP.nv = 1;
+    HIPCHECK(grape_unitary::launch_chain(UP, p->ud_E, p->ud_C, st));
+    return GRAPE_OK;
+}
+
+int grape_interaction_error_operators(grape_plan *p, const double *x, double *O) {
+    if (!p || !x || !O) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, "interaction error operators: dense engine not supported");
+    if (p->P.ne == 0) return GRAPE_OK;
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = ud_alloc(p)) return rc;
+    if (int rc = ud_chain(p, x)) return rc;
+    const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
+    HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
+    HIPCHECK(hipMemcpyAsync(O, p->ud_out, n * sizeof(cd), hipMemcpyDeviceToHost, p->stream));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    return grape_plan_synchronize(p);
+}
+
+int grape_expectation_values(grape_plan *p, const double *x, double *ev) {
+    if (!p || !x || !ev) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, "expectation values: dense engine not supported");
+    if (p->P.ne == 0) return GRAPE_OK;
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = ud_alloc(p)) return rc;
+    if (int rc = ud_chain(p, x)) return rc;
+    HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
+    double *dev = reinterpret_cast<double *>(p->ud_V);  // (Nt, ne) column-major
+    HIPCHECK(grape_unitary::launch_expectation(p->P, p->ud_out, dev, p->stream));
+    HIPCHECK(hipMemcpyAsync(ev, dev, (size_t)p->P.Nt * p->P.ne * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    return grape_plan_synchronize(p);
 }
 
 int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
@@ -712,14 +851,7 @@ int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx
     UP.inv_eps2sq = 1.0 / (P0.eps2 * P0.eps2);
     // outputs, packed: U_dx | U_dx_add | U_derr | U_derr_dx | U_derr_dx_add
     const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
-    if (!p->ud_vs) {
-        bool ok = dalloc(&p->ud_vs, (size_t)nv) == hipSuccess && dalloc(&p->ud_E, (size_t)Nt * nv * T) == hipSuccess &&
-                  dalloc(&p->ud_ovf, (size_t)Nt * nv) == hipSuccess && dalloc(&p->ud_C, (size_t)Nt * T) == hipSuccess &&
-                  dalloc(&p->ud_V, (size_t)Nt * UP.nslots * T) == hipSuccess &&
-                  dalloc(&p->ud_S, (size_t)Nt * std::max(ne, 1) * T) == hipSuccess &&
-                  dalloc(&p->ud_out, n_dx + n_dxa + n_e + n_edx + n_edxa) == hipSuccess;
-        if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (unitary derivatives)");
-    }
+    if (int rc = ud_alloc(p)) return rc;
     hipStream_t st = p->stream;
     HIPCHECK(hipMemcpyAsync(p->ud_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));

@@ -209,7 +209,60 @@ __global__ __launch_bounds__(BLOCK) void k_u_reduce(UProblem P, const cd *C, con
     if (t < DD) out[cm(D, oidx, i, j)] = mm_el(sU, sX, D, i, j);
 }
 
+// O_{k,e} = C_{k-1}^dagger (Herror_e / eps) C_{k-1}: one workgroup per (k, e)
+__global__ __launch_bounds__(BLOCK) void k_u_interaction(grape::DevProblem P, const double *x, const cd *C, cd *O) {
+    __shared__ cd sC[kMaxD * kMaxD], sH[kMaxD * kMaxD], sT[kMaxD * kMaxD];
+    const int D = P.D, DD = D * D, t = threadIdx.x, i = t / D, j = t % D;
+    const int k = blockIdx.x % P.Nt, e = blockIdx.x / P.Nt;
+    if (k > 0) load_tile(sC, C + (size_t)(k - 1) * DD, D);
+    else identity_tile(sC, D);
+    if (t < DD) {  // Herror_e(k, x_k, x_add, eps) = eps * sum_t c_t OP_t (operator basis), then / eps
+        const double *xk = x + (size_t)k * P.np, *xadd = x + (size_t)P.np * P.Nt;
+        grape::Pert none;
+        none.var = -1;
+        none.index = 0;
+        none.delta = 0.0;
+        cd h{0.0, 0.0};
+        for (int q = P.err_off[e]; q < P.err_off[e + 1]; ++q) {
+            const grape::Term tm = P.err[q];
+            h = u_add(h, u_mul(grape::term_coef(tm, k + 1, xk, xadd, none), P.ops[(size_t)tm.op * DD + t]));
+        }
+        sH[t] = u_scale(1.0 / P.eps, u_scale(P.eps, h));
+    }
+    __syncthreads();
+    if (t < DD) sT[t] = mm_el(sH, sC, D, i, j);
+    __syncthreads();
+    if (t < DD) O[cm(D, (size_t)e * P.Nt + k, i, j)] = mmh_el(sC, sT, D, i, j);
+}
+
+// expectation values: one thread per error source walks the time steps
+__global__ void k_u_expect(grape::DevProblem P, const cd *O, double *ev) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.ne) return;
+    const int D = P.D;
+    cd acc{0.0, 0.0};
+    for (int k = 0; k < P.Nt; ++k) {
+        for (int i = 0; i < D; ++i) acc = u_add(acc, u_scale(P.W[i], O[cm(D, (size_t)e * P.Nt + k, i, i)]));
+        ev[(size_t)e * P.Nt + k] = P.dt * acc.re / P.Dtr;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st) {
+    hipLaunchKernelGGL(k_u_chain, dim3(1), dim3(BLOCK), 0, st, P, E, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, hipStream_t st) {
+    hipLaunchKernelGGL(k_u_interaction, dim3((unsigned)(P.Nt * P.ne)), dim3(BLOCK), 0, st, P, x, C, O);
+    return hipGetLastError();
+}
+
+hipError_t launch_expectation(const grape::DevProblem &P, const cd *O, double *ev, hipStream_t st) {
+    hipLaunchKernelGGL(k_u_expect, dim3((P.ne + 63) / 64), dim3(64), 0, st, P, O, ev);
+    return hipGetLastError();
+}
 
 hipError_t launch_assembly(const UProblem &P, const UBuffers &B, hipStream_t st) {
     const int DD = P.D * P.D;

@@ -35,5 +35,12 @@ struct UBuffers {
 };
 
 hipError_t launch_assembly(const UProblem &P, const UBuffers &B, hipStream_t st);
+// C_k = E_k C_{k-1} for the nominal table E[k][0] (P.nv variants per step)
+hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st);
+// O[:, :, k, e] = C_{k-1}^dagger (Herror_e(k, eps) / eps) C_{k-1}, column-major (d, d, Nt, ne)
+// (UnitaryCalculations.jl:180-204); x is the plan's device copy of the control vector
+hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, hipStream_t st);
+// ev[k + Nt e] = Re(dt tr(W sum_{j<=k} O_j,e) / D)   (FidelityCalculations.jl:368-390)
+hipError_t launch_expectation(const grape::DevProblem &P, const cd *O, double *ev, hipStream_t st);
 
 }  // namespace grape_unitary
