@@ -8,7 +8,8 @@ module RobustGRAPEMI355X
 
 using LinearAlgebra
 
-export OperatorTerm, OperatorBasis, calculate_fidelity_and_derivatives, grape_expm_batch
+export OperatorTerm, OperatorBasis, calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
+       calculate_interaction_error_operators, calculate_expectation_values, grape_expm_batch
 
 const libgrape = normpath(joinpath(@__DIR__, "..", "robustgrape_amd", "libgrape.so"))
 
@@ -112,6 +113,51 @@ function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
                      p.handle, 1, xv, F, F_dx, F_d2err, F_d2err_dx))
     end
     return (F[], F_dx, F_d2err, F_d2err_dx)
+end
+
+"Drop-in for src/UnitaryCalculations.jl:20-155: (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add)."
+function calculate_unitary_and_derivatives(fp, x::AbstractVector{<:Real})
+    up = fp.unitary_problem
+    d, nt, na, ne = up.ndim, up.ntimes, up.nb_additional_param, length(up.error_sources)
+    xm = length(x) - na
+    @assert mod(xm, nt) == 0 "Control parameter size must be a multiple of time steps"
+    np = xm ÷ nt
+    p = device_plan(fp, np; max_batch=1)
+    xv = Vector{Float64}(x)
+    outs = (zeros(ComplexF64, d, d), zeros(ComplexF64, d, d, np, nt), zeros(ComplexF64, d, d, na),
+            zeros(ComplexF64, d, d, ne), zeros(ComplexF64, d, d, np, nt, ne), zeros(ComplexF64, d, d, na, ne))
+    GC.@preserve xv outs begin
+        _check(ccall((:grape_unitary_derivs, libgrape), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64},
+                      Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64}), p.handle, xv, outs...))
+    end
+    return outs
+end
+
+"Drop-in for src/UnitaryCalculations.jl:180-204: (ndim, ndim, ntimes, nerr)."
+function calculate_interaction_error_operators(fp, x::AbstractVector{<:Real})
+    up = fp.unitary_problem
+    p = device_plan(fp, (length(x) - up.nb_additional_param) ÷ up.ntimes; max_batch=1)
+    xv = Vector{Float64}(x)
+    O = zeros(ComplexF64, up.ndim, up.ndim, up.ntimes, length(up.error_sources))
+    GC.@preserve xv O begin
+        _check(ccall((:grape_interaction_error_operators, libgrape), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}), p.handle, xv, O))
+    end
+    return O
+end
+
+"Drop-in for src/FidelityCalculations.jl:368-390: (ntimes, nerr)."
+function calculate_expectation_values(fp, x::AbstractVector{<:Real})
+    up = fp.unitary_problem
+    p = device_plan(fp, (length(x) - up.nb_additional_param) ÷ up.ntimes; max_batch=1)
+    xv = Vector{Float64}(x)
+    ev = zeros(Float64, up.ntimes, length(up.error_sources))
+    GC.@preserve xv ev begin
+        _check(ccall((:grape_expectation_values, libgrape), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), p.handle, xv, ev))
+    end
+    return ev
 end
 
 "Batched exp of n column-major d x d ComplexF64 matrices (LinearAlgebra.exp!'s algorithm)."
