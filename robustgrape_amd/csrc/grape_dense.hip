@@ -279,6 +279,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dgrad(DenseProblem DP, DenseBat
     __syncthreads();
     hm_zero(Z);
     mm<false, true, true, false>(S0, S1, Z, ln);  // Z = Y^T = conj(Q_k) (Q_{k-1} M'_c)^T
+    // Z is parked in HBM (one coalesced 64-KB image) while the exponentials run:
+    // kept live it costs 32 VGPRs through wg_expm and spills far more than 64 KB
+    double *zimg = B.Z + (size_t)item * IMG;
+    img_store(zimg, Z, ln);
     const double *xb = B.x + (size_t)b * P.nx;
     for (int p = 0; p < P.np; ++p) {
         grape::Pert pp;
@@ -290,6 +294,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dgrad(DenseProblem DP, DenseBat
         wg_expm([&](HM &G) { build_generator(DP, xb, k, pp, G, ln); }, X, lds, ln, singular);
         if (singular) atomicOr(B.status, 1);
         img_load(B.E + (qbase + k) * IMG, A, ln);
+        img_load(zimg, Z, ln);  // written by this same lane above
         double acc = 0.0;
 #pragma unroll
         for (int i = 0; i < 2; ++i)

@@ -161,7 +161,11 @@ __device__ __forceinline__ void hm_scale(HM &M, double c) {
 // ---------------------------------------------------------------------------
 // HBM images and LDS stores
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void img_load(const double *img, HM &M, const Lane &ln) {
+// (pinned lane: a load of a loop-invariant image must not be hoisted out of a
+// loop around an exponential, where it would hold 32 VGPRs through the Pade)
+__device__ __forceinline__ void img_load(const double *img, HM &M, const Lane &ln_in) {
+    Lane ln = ln_in;
+    asm volatile("" : "+v"(ln.l));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -199,6 +203,18 @@ __device__ __forceinline__ void sm_store(SM S, const HM &M, const Lane &ln_in) {
             const int o = sidx(ln.row(i, r), ln.col());
             S.re[o] = M.re[i][r];
             S.im[o] = M.im[i][r];
+        }
+}
+
+__device__ __forceinline__ void sm_load(SM S, HM &M, const Lane &ln_in) {
+    const Lane ln = pinned(ln_in);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = sidx(ln.row(i, r), ln.col());
+            M.re[i][r] = S.re[o];
+            M.im[i][r] = S.im[o];
         }
 }
 
@@ -305,7 +321,11 @@ __device__ __forceinline__ double wg_norm1(const HM &A, double *lds, const Lane 
 // ---------------------------------------------------------------------------
 // Operator-basis builder: M += c OP (OP image in HBM)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void hm_cmac_img(HM &M, cd c, const double *img, const Lane &ln) {
+// (pinned lane: otherwise the loads of the second build of A inside wg_expm are
+// CSE'd with the first and the operator images stay live through the Pade)
+__device__ __forceinline__ void hm_cmac_img(HM &M, cd c, const double *img, const Lane &ln_in) {
+    Lane ln = ln_in;
+    asm volatile("" : "+v"(ln.l));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -399,36 +419,48 @@ __device__ __forceinline__ void cmfma1(v4d &cr, v4d &ci, double aR, double aI, d
 
 // ---------------------------------------------------------------------------
 // Solve Q X = Pm in place (X returned in Pm): blocked Gauss-Jordan on MFMA.
-// Block step kb:
-//   1. wave (kb, kb/2) inverts the diagonal block D; waves (kb, *) publish
-//      -Q[:, block kb] (the multipliers);
+// Block step kb (buffers in LDS set kb & 1):
+//   1. waves (kb, *) publish -Q[:, block kb] (the multipliers); D_kb^-1 is
+//      already in the set (look-ahead, below);
 //   2. waves holding row block kb replace it by D^-1 (row block) and publish it;
 //   3. every wave subtracts Q[t-block, kb-block] (new row block) from its tiles.
+//      Look-ahead: the wave that owns the NEXT diagonal block updates its tiles
+//      first and then inverts that block into the next set while the other
+//      seven waves are still in their rank-16 updates, so the serial 16-step
+//      inversion no longer idles the workgroup (only D_0 is inverted up front).
 // Q's column blocks left of or at kb are never read again: skipped (w <= kb).
-// Buffers alternate between the two LDS matrix regions (no trailing barrier).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void gj_store_dinv(double *set, const v4d &xr, const v4d &xi, int l) {
+    double *dvr = set + GJ_DINV, *dvi = dvr + SMALL;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int o = sidx16((l >> 4) + 4 * r, l & 15);
+        dvr[o] = xr[r];
+        dvi[o] = xi[r];
+    }
+}
+
 __device__ __forceinline__ void gj_solve(HM &Q, HM &Pm, double *lds, const Lane &ln_in, bool &singular) {
     __syncthreads();  // the matrix regions are free
+    {  // D_0^-1 into set 0
+        const Lane ln = pinned(ln_in);
+        if (ln.w == 0 && ln.h == 0) {
+            v4d dr = Q.re[0], di = Q.im[0], xr, xi;
+            wave_inv16(dr, di, xr, xi, ln.l, singular);
+            gj_store_dinv(lds + LDS_R0, xr, xi, ln.l);
+        }
+    }
 #pragma unroll
     for (int kb = 0; kb < NT; ++kb) {
         const Lane ln = pinned(ln_in);
         double *set = lds + ((kb & 1) ? LDS_R1 : LDS_R0);
+        double *nset = lds + ((kb & 1) ? LDS_R0 : LDS_R1);
         double *dvr = set + GJ_DINV, *dvi = dvr + SMALL;
         double *pcr = set + GJ_PCOL, *pci = pcr + 4 * SMALL;
         double *nr = set + GJ_NR;
         const int hk = kb >> 1, ik = kb & 1;
         const bool owner_row = ln.h == hk;  // holds row block kb of column block w (tile ik)
         if (ln.w == kb) {
-            if (owner_row) {
-                v4d dr = Q.re[ik], di = Q.im[ik], xr, xi;
-                wave_inv16(dr, di, xr, xi, ln.l, singular);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int o = sidx16((ln.l >> 4) + 4 * r, ln.l & 15);
-                    dvr[o] = xr[r];
-                    dvi[o] = xi[r];
-                }
-            }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if (ln.tile(i) == kb) continue;
@@ -483,8 +515,15 @@ __device__ __forceinline__ void gj_solve(HM &Q, HM &Pm, double *lds, const Lane 
                 if (doq) cmfma1(Q.re[i], Q.im[i], aR, aI, nq[ob], nq[SMALL + ob]);
             }
         }
+        // look-ahead: the owner of diagonal block kb+1 (updated just above) inverts it
+        if (kb + 1 < NT && ln.w == kb + 1 && ln.h == ((kb + 1) >> 1)) {
+            const int in = (kb + 1) & 1;
+            v4d dr = Q.re[in], di = Q.im[in], xr, xi;
+            wave_inv16(dr, di, xr, xi, ln.l, singular);
+            gj_store_dinv(nset, xr, xi, ln.l);
+        }
+        __syncthreads();  // next set's D^-1 visible; this set's buffers free
     }
-    __syncthreads();  // regions free for the caller
 }
 
 // ---------------------------------------------------------------------------
@@ -583,18 +622,15 @@ __device__ __forceinline__ int wg_expm(const Build &build, HM &X, double *lds, c
     } else {
         // exp! Pade 13: U = A (A6 (c13 A6 + c11 A4 + c9 A2) + c7 A6 + c5 A4 + c3 A2 + c1 I),
         //               V = A6 (c12 A6 + c10 A4 + c8 A2) + c6 A6 + c4 A4 + c2 A2 + c0 I
-        // A2 and A4 live in LDS once consumed: registers hold W1, Z1, U, V (+ one power)
-        HM W1, Z1;
+        // A2 and A4 live in LDS once consumed; W1 and Z1 are formed only after A6
+        // exists (A2, A4 read back from LDS), so no product ever runs with more
+        // than U, V and its accumulator live.
         {
             HM A2;
             hm_zero(A2);
             mm<false, false, false, false>(S0, S0, A2, ln);
-            hm_zero(W1);
-            hm_zero(Z1);
             hm_identity(U, ln, C[1]);
             hm_identity(V, ln, C[0]);
-            hm_axpy(W1, C[9], A2);
-            hm_axpy(Z1, C[8], A2);
             hm_axpy(U, C[3], A2);
             hm_axpy(V, C[2], A2);
             __syncthreads();
@@ -605,26 +641,36 @@ __device__ __forceinline__ int wg_expm(const Build &build, HM &X, double *lds, c
             HM A4;
             hm_zero(A4);
             mm<false, false, false, false>(S0, S0, A4, ln);
-            hm_axpy(W1, C[11], A4);
-            hm_axpy(Z1, C[10], A4);
             hm_axpy(U, C[5], A4);
             hm_axpy(V, C[4], A4);
             sm_store(S1, A4, ln);  // region 1 unused so far
             __syncthreads();
         }
+        hm_pin(U);
+        hm_pin(V);
+        HM A6, W1, Z1;
+        hm_zero(A6);
+        mm<false, false, false, false>(S0, S1, A6, ln);  // A2 . A4
+        hm_axpy(U, C[7], A6);
+        hm_axpy(V, C[6], A6);
         {
-            HM A6;
-            hm_zero(A6);
-            mm<false, false, false, false>(S0, S1, A6, ln);  // A2 . A4
-            hm_axpy(W1, C[13], A6);
+            HM A2, A4;
+            sm_load(S0, A2, ln);
+            sm_load(S1, A4, ln);
+            hm_zero(W1);
+            hm_zero(Z1);
+            hm_axpy(W1, C[13], A6);  // exp!'s order: c13 A6 + c11 A4 + c9 A2
+            hm_axpy(W1, C[11], A4);
+            hm_axpy(W1, C[9], A2);
             hm_axpy(Z1, C[12], A6);
-            hm_axpy(U, C[7], A6);
-            hm_axpy(V, C[6], A6);
-            __syncthreads();
-            sm_store(S0, A6, ln);
-            sm_store(S1, W1, ln);
-            __syncthreads();
+            hm_axpy(Z1, C[10], A4);
+            hm_axpy(Z1, C[8], A2);
         }
+        __syncthreads();
+        sm_store(S0, A6, ln);
+        sm_store(S1, W1, ln);
+        __syncthreads();
+        hm_pin(Z1);
         mm<false, false, false, false>(S0, S1, U, ln);  // U += A6 W1
         __syncthreads();
         sm_store(S1, Z1, ln);

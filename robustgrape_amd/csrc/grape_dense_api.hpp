@@ -25,6 +25,7 @@ struct DenseBatch {
     double *Carry;    // [nb][Nc][IMG]   C_{cL-1} (identity for c = 0)
     double *M;        // [nb][IMG]       gradient kernel M = G U
     double *Mc;       // [nb][Nc][IMG]   Carry_c M Carry_c^dagger
+    double *Z;        // [nb][Nt][IMG]   k_dgrad's Z_k, parked in HBM across the eps-variant exps
     double *F;        // [nb]
     double *Fdx;      // [nb][nx]
     int *status;      // bit 0: singular Pade denominator

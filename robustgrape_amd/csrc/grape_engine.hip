@@ -135,7 +135,7 @@ struct grape_plan {
     bool dense = false;
     grape_dense::DenseProblem DP{};
     double *dn_opimg = nullptr, *dn_W = nullptr, *dn_E = nullptr, *dn_Q = nullptr, *dn_Carry = nullptr,
-           *dn_M = nullptr, *dn_Mc = nullptr;
+           *dn_M = nullptr, *dn_Mc = nullptr, *dn_Z = nullptr;
     // grape_unitary_derivs workspace (allocated on first use)
     grape::VSpec *ud_vs = nullptr;
     cd *ud_E = nullptr, *ud_C = nullptr, *ud_V = nullptr, *ud_S = nullptr, *ud_out = nullptr;
@@ -168,7 +168,7 @@ static void free_plan(grape_plan *p) {
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots,
-                    p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc,
+                    p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -286,7 +286,8 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, do
               dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess &&
               dalloc(&p->dn_E, MB * P.Nt * IMG) == hipSuccess && dalloc(&p->dn_Q, MB * P.Nt * IMG) == hipSuccess &&
               dalloc(&p->dn_Carry, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_M, MB * IMG) == hipSuccess &&
-              dalloc(&p->dn_Mc, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
+              dalloc(&p->dn_Mc, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_Z, MB * P.Nt * IMG) == hipSuccess &&
+              dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess;
     if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense)");
@@ -564,6 +565,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         DB.Carry = p->dn_Carry;
         DB.M = p->dn_M;
         DB.Mc = p->dn_Mc;
+        DB.Z = p->dn_Z;
         DB.F = d_F;
         DB.Fdx = d_Fdx;
         DB.status = p->d_ctrl + 2;
