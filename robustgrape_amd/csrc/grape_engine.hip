@@ -131,6 +131,7 @@ struct grape_plan {
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
+    cd *d_sink = nullptr;                      // DevBatch::sink
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -166,7 +167,7 @@ static void free_plan(grape_plan *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
-                    p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl,
+                    p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf};
@@ -471,6 +472,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
               dalloc(&p->d_part, MB * P.Nt * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess &&
+              dalloc(&p->d_sink, T) == hipSuccess &&
               dalloc(&p->d_vs, vs.size()) == hipSuccess;
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);
     if (ok && P.ne == 0)
@@ -603,6 +605,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     B.overflow_count = cnt;
     B.ovf2_count = cnt + 1;
     B.status = p->d_ctrl + 2;
+    B.sink = p->d_sink;
     HIPCHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
     HIPCHECK(dispatch_pipeline(P.D, P, B, st, mk));
     return GRAPE_OK;

@@ -94,6 +94,7 @@ struct DevBatch {
     int *ovf2_count;
     cd *ovf2_slots;         // [nb][Nt][nvg][D][D]  A of parked k_expm_grad items
     int *status;            // bit 0: singular Pade denominator
+    cd *sink;               // [D][D] write-only target of inactive lanes' unconditional stores
 };
 
 __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,
@@ -344,11 +345,16 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     // Phase A: local inclusive chain Q_k = E_k ... E_{cL}; lane i owns column i
     cd q[D], e[D], t[D];
     const int k0 = c * P.L;
-    auto load_e = [&](int k, cd (&dst)[D]) {  // column i of E_k (coalesced)
-        const bool ok = gvalid && k < P.Nt;
-        const cd *src = Eb + ((size_t)(ok ? k : 0) * P.nv) * TILE + i;
+    // Column i of E_k (coalesced).  The load is unconditional (k clamped into range):
+    // a guarded load compiles to exec-masked branches around the loads, after which
+    // the compiler can no longer count outstanding vector-memory ops and waits with
+    // vmcnt(0) -- i.e. for the prefetch just issued and the previous step's Q stores.
+    // Out-of-range steps only feed products whose results are discarded (act below).
+    auto load_e = [&](int k, cd (&dst)[D]) {
+        const int kk = k < P.Nt ? k : P.Nt - 1;
+        const cd *src = Eb + ((size_t)kk * P.nv) * TILE + i;
 #pragma unroll
-        for (int m = 0; m < D; ++m) dst[m] = ok ? src[m * D] : czero();
+        for (int m = 0; m < D; ++m) dst[m] = src[m * D];
     };
     load_e(k0, e);
 #if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 0
@@ -372,8 +378,11 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
                 for (int m = 0; m < D; ++m) q[m] = t[m];
             }
         }
-        if (act) {
-            cd *dst = Qb + (size_t)k * TILE + i;  // Q row-major: column i at stride D (coalesced)
+        {  // Q row-major: column i at stride D (coalesced).  Unconditional store (inactive
+           // lanes write the sink tile): a store under a branch makes the loop's vmcnt
+           // accounting path-dependent and the compiler then waits for everything
+           // (vmcnt(0)) -- the stores included -- before the next step's prefetch is used.
+            cd *dst = act ? Qb + (size_t)k * TILE + i : B.sink + i;
 #pragma unroll
             for (int m = 0; m < D; ++m) dst[m * D] = q[m];
         }
