@@ -41,6 +41,18 @@ def problem():
     return FidelityRobustGRAPEProblem(up, np.diag([1.0] * 4 + [0.0] * 5), R.cz_full_target())
 
 
+def problem_c3():
+    """SURVEY.md 8d C3: C2 + 4 error sources (Omega1, Omega2 amplitude, delta1, delta2 detuning;
+    the reference idiom Herror = H(perturbed) - H0, runtests.jl:475-476, as operator bases)."""
+    from robustgrape_amd import rydberg as R
+    from robustgrape_amd.types import ErrorSource, FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    errs = [ErrorSource(R.full_rabi_error(1)), ErrorSource(R.full_rabi_error(2)),
+            ErrorSource(R.full_detuning_error(1)), ErrorSource(R.full_detuning_error(2))]
+    up = UnitaryRobustGRAPEProblem(t0=T0, ntimes=NT, ndim=D, H0=R.rydberg_full_operator_basis(1.0, 1.0, 0.0, 0.0, 10.0),
+                                   nb_additional_param=1, error_sources=errs)
+    return FidelityRobustGRAPEProblem(up, np.diag([1.0] * 4 + [0.0] * 5), R.cz_full_target())
+
+
 def restart_inputs(first, count):
     xs = []
     for r in range(first, first + count):
@@ -82,7 +94,7 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
     return None
 
 
-def cpu_baseline(seconds=15.0):
+def cpu_baseline(seconds=15.0, fp=None, label="C2"):
     """Time the CPU restatement on a bounded sample of the same workload (rank 0, N = 1)."""
     try:
         from oracle.cref import cref
@@ -91,7 +103,7 @@ def cpu_baseline(seconds=15.0):
         have_c = False
     x = restart_inputs(0, 1)[0]
     if have_c:
-        fp = problem()
+        fp = fp or problem()
         t = time.perf_counter()
         n = 0
         while True:
@@ -101,7 +113,7 @@ def cpu_baseline(seconds=15.0):
                 break
         dt = time.perf_counter() - t
         return {"value": n / dt, "unit": "gradient-evals/s", "cores": 1, "kind": "port",
-                "sample": f"{n} sequential C2 evaluations (d=9, N_t=512) by the reference-faithful C++ "
+                "sample": f"{n} sequential {label} evaluations (d=9, N_t=512) by the reference-faithful C++ "
                           f"restatement oracle/cref (same exp/inv/product counts as the Julia code), 1 thread"}
     from oracle import grape_oracle as O
     from tests import problems as P
@@ -162,6 +174,35 @@ def c2_report(args, B, world, value, elapsed, ktimes):
     return out
 
 
+def c3_report(args, B, world, value, elapsed, ktimes, ne):
+    # k_expm exponentiates every stored variant of every step: nominal, x + eps, x + eps2,
+    # and per error source err(eps), err(eps2), (x + eps2, err eps2) -> 3 + 3 ne (Pade 5);
+    # the x_add variants are skipped (H0 does not read x_add: their differences are exactly 0)
+    nv = 3 + 3 * ne
+    # k_err_grad: one row group per (eval, chunk, error) walks the chunk, 8 complex d x d
+    # products per (step, error) (grape_errpath.hpp header)
+    flop_model = {"k_expm": B * NT * nv * flops_expm(D), "k_err_grad": B * NT * ne * 8 * 8 * D ** 3}
+    kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
+    out = {
+        "metric": "GRAPE gradient-evals/sec (fidelity+sensitivity+gradients), Rydberg CZ d=9 N_t=512, 4 error sources",
+        "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C3: Rydberg CZ d=9 + 4 error operators (Omega1, Omega2, delta1, delta2), N_t=512, "
+                               "np=1, na=1; F, F_dx, F_d2err, F_d2err_dx",
+                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, B),
+                         pipe="fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"),
+        "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
+    }
+    # SURVEY.md 8d canonical C3 figure: 352.7 MFLOP per evaluation
+    canon = NT * (1 + 2 + 2 + ne * (2 + 1 + 1)) * flops_expm(D) + 3 * NT * 8 * D ** 3 \
+        + 4 * NT * ne * 8 * D ** 3 + 8 * D ** 2 * NT * 2 * (1 + ne)
+    out["roofline"]["whole_eval"] = {"flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
+                                     "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    return out
+
+
 def c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam):
     # C5 draws Pade m = 7 for every exponential (tests/golden/c5.npz pade_hist); per launch:
     # k_dexp: B*nt nominal exps; k_dgrad: per step 2 products (Q_{k-1} M'_c, Z_k) and, per
@@ -197,8 +238,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
                     help="restarts per GPU (one device pass each step); default 1024 (c2), 4 (c5)")
-    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
-                    help="c2: the BASELINE metric (d=9 Rydberg CZ); c5: synthetic d=64, N_t=1024 "
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
+                    help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
+                         "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
                          "(dense MFMA engine, SURVEY.md 8d C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -217,18 +259,23 @@ def main():
 
     from robustgrape_amd.engine import GrapePlan
     from robustgrape_amd.sweep import gather_best, shard
-    c5 = args.workload == "c5"
+    c5, c3 = args.workload == "c5", args.workload == "c3"
     if c5:
         from robustgrape_amd import synthetic as S
         fp, nparam, d, nt, inputs = S.dense_problem(), 2, S.C5_DIM, S.C5_NTIMES, c5_inputs
+    elif c3:
+        fp, nparam, d, nt, inputs = problem_c3(), 1, D, NT, restart_inputs
     else:
         fp, nparam, d, nt, inputs = problem(), 1, D, NT, restart_inputs
-    B = args.batch or (4 if c5 else 1024)
+    ne = len(fp.unitary_problem.error_sources)
+    B = args.batch or (4 if c5 else 256 if c3 else 1024)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
     plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=count)
     X = torch.from_numpy(inputs(first, count)).to(dev)
     F = torch.empty(count, dtype=torch.float64, device=dev)
     Fdx = torch.empty(count, X.shape[1], dtype=torch.float64, device=dev)
+    Fd2 = torch.empty(count, max(ne, 1), dtype=torch.float64, device=dev)
+    Fd2dx = torch.empty(count, max(ne, 1), X.shape[1], dtype=torch.float64, device=dev)
     ids = torch.arange(first, first + count, device=dev)
 
     # The evaluation is enqueued on one torch stream, so steps queue back to back without
@@ -238,7 +285,8 @@ def main():
     plan.set_stream(stream.cuda_stream)
 
     def step():
-        plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), count)
+        plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), count,
+                                        Fd2.data_ptr() if ne else 0, Fd2dx.data_ptr() if ne else 0)
 
     for _ in range(args.warmup):
         step()
@@ -271,12 +319,14 @@ def main():
     if rank == 0:
         if c5:
             out = c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam)
+        elif c3:
+            out = c3_report(args, B, world, value, elapsed, ktimes, ne)
         else:
             out = c2_report(args, B, world, value, elapsed, ktimes)
         if best is not None:
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         if world == 1 and not args.no_cpu_baseline and not c5:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, fp if c3 else None, "C3" if c3 else "C2")
         print(json.dumps(out), flush=True)
     plan.close()
     if world > 1:

@@ -271,8 +271,11 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
     }
 }
 
+#ifndef GRAPE_ERRGRAD_WAVES
+#define GRAPE_ERRGRAD_WAVES 2  // 2 waves/SIMD (308 B/lane of spills) beat 1 (336 registers): 2.51 -> 2.23 ms, C3 B=256
+#endif
 template <int D>
-__global__ __launch_bounds__(64) void k_err_grad(DevProblem P, DevBatch B) {
+__global__ __launch_bounds__(64, GRAPE_ERRGRAD_WAVES) void k_err_grad(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     constexpr int TILE = Geo<D>::TILE;
