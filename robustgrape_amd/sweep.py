@@ -59,3 +59,49 @@ def gather_best(F: torch.Tensor, ids: torch.Tensor, X: torch.Tensor | None = Non
             xb = torch.empty(X.shape[1], dtype=X.dtype, device=X.device)
         dist.broadcast(xb, src=dist.get_global_rank(group, owner) if group is not None else owner, group=group)
     return float(fbest.item()), int(rid.item()), owner, xb
+
+
+def optimize_sweep(fidelity_problem, fidelity_parameters, n_restarts: int, initial_x, device: int = 0,
+                   group=None, evaluate=None):
+    """Random-restart optimisation sweep: the restarts are cut into
+    contiguous shards, one per rank; each rank runs ALL of its restarts as one batched L-BFGS
+    on its own GPU (robustgrape_amd.optimize.optimize_restarts, no communication inside the
+    loop), then one exchange finds the global best and broadcasts its control vector.
+
+    initial_x(r) -> the n_x control vector of restart r (e.g. seeded per restart, as
+    examples/time_optimal_cz.jl:32).  Returns (best_cost, restart_id, owner_rank, x_best,
+    local BatchResult).  Ranking is by the optimiser's cost (1 - F + sensitivities +
+    regularisers), so the exchanged value is -cost through gather_best's max."""
+    import numpy as np
+
+    from .optimize import optimize_restarts
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    first, count = shard(n_restarts, world, rank)
+    X0 = np.stack([np.asarray(initial_x(r), dtype=np.float64) for r in range(first, first + count)]) \
+        if count else None
+    res = optimize_restarts(fidelity_problem, fidelity_parameters, X0, device=device, evaluate=evaluate) \
+        if count else None
+    dev = res.minimizer.device if res is not None else torch.device("cpu")
+    if evaluate is None and res is None:
+        dev = torch.device("cuda", device)
+    ids = torch.arange(first, first + count, device=dev)
+    score = -res.minimum if res is not None else torch.empty(0, dtype=torch.float64, device=dev)
+    X = res.minimizer if res is not None else None
+    if world == 1:
+        if count == 0:
+            return float("inf"), -1, 0, None, res
+        fbest, rid, owner, xb = gather_best_local(score, ids, X)
+    else:
+        if X is None:
+            nx = len(np.asarray(initial_x(0)))
+            X = torch.empty(0, nx, dtype=torch.float64, device=dev)
+        fbest, rid, owner, xb = gather_best(score, ids, X, group=group)
+    return -fbest, rid, owner, xb, res
+
+
+def gather_best_local(F: torch.Tensor, ids: torch.Tensor, X: torch.Tensor):
+    """Single-process form of gather_best (same tie rule)."""
+    fb, rid = local_best(F, ids).tolist()
+    row = int(torch.nonzero(ids.to(torch.float64) == rid)[0, 0].item())
+    return fb, int(rid), 0, X[row].clone()

@@ -83,3 +83,13 @@ def test_optimise_with_error_sources():
     reg = REG.regularization_cost_phase(res.minimizer[:100])
     assert res.minimum < c0
     assert abs(res.minimum - (1 - F + 0.5 * d2[0] ** 2 + 1e-6 * (reg[0] + reg[2]))) < 1e-12
+
+
+def test_optimize_sweep_single_gpu():
+    """C4-style sweep on one GPU: the returned best is the batch minimum and its pulse."""
+    from robustgrape_amd.sweep import optimize_sweep
+    fp = P.sym_problem(100, t0=P.T0_TO)
+    params = _params(np.zeros(101), iterations=15)
+    cost, rid, owner, xb, res = optimize_sweep(fp, params, 8, lambda r: P.random_x(100, 1000 + r, small=True))
+    assert owner == 0 and cost == float(torch.min(res.minimum)) and rid == int(torch.argmin(res.minimum))
+    assert torch.equal(xb, res.minimizer[rid])

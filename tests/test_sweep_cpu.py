@@ -92,3 +92,59 @@ def test_gather_best_matches_single_process(world, n_total):
     for rank, fbest, got_id, got_owner, xb in out:
         assert fbest == best and got_id == rid and got_owner == owner
         assert xb == _xrow(rid).tolist()
+
+
+# ---------------------------------------------------------------- optimiser sweep (C4 + row f1)
+def _opt_worker(rank, world, port, n_total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank,) + _run_sweep(n_total))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _run_sweep(n_total):
+    import numpy as np
+    from oracle import grape_oracle as O
+    from robustgrape_amd.regularization import regularization_cost_phase
+    from robustgrape_amd.sweep import optimize_sweep
+    from robustgrape_amd.types import FidelityRobustGRAPEParameters
+    from tests import problems as P
+    fp = P.sym_problem(24, t0=P.T0_TO, device=False)
+
+    def ev(X):
+        outs = [O.calculate_fidelity_and_derivatives(fp, x.numpy()) for x in X]
+        t = lambda v: torch.as_tensor(np.asarray(v, dtype=np.float64))
+        return (t([o[0] for o in outs]), t(np.stack([o[1] for o in outs])),
+                torch.zeros(len(X), 0, dtype=torch.float64), torch.zeros(len(X), X.shape[1], 0, dtype=torch.float64))
+    params = FidelityRobustGRAPEParameters(
+        x_initial=np.zeros(25), regularization_functions=[regularization_cost_phase],
+        regularization_coeff1=[1e-6], regularization_coeff2=[1e-6], error_source_coeff=[], iterations=6)
+    cost, rid, owner, xb, _ = optimize_sweep(fp, params, n_total, lambda r: P.random_x(24, 1000 + r, small=True),
+                                             evaluate=ev)
+    return cost, rid, owner, xb.tolist()
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 5)])
+def test_optimize_sweep_two_ranks_equals_one(world, n_total):
+    """The sharded sweep (gloo, 2 ranks) finds the same best restart, cost and pulse as one
+    process running every restart: restarts are independent and rows of a batched L-BFGS
+    do not interact."""
+    single = _run_sweep(n_total)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_opt_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, cost, rid, owner, xb in out:
+        assert rid == single[1] and abs(cost - single[0]) < 1e-12
+        assert max(abs(a - b) for a, b in zip(xb, single[3])) < 1e-12
