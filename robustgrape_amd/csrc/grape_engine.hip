@@ -443,6 +443,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             ncu = prop.multiProcessorCount;
     }
     P.scan_waves = p->max_batch >= 2 * ncu ? kScanNarrow : kScanWide;
+    P.pair = 0;
+    if (const char *pe = std::getenv("GRAPE_PAIR")) P.pair = std::atoi(pe) != 0;  // column-pair nominal exps
     if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {  // tuning override: 4 or 8
         const int wv = std::atoi(w);
         if (wv == kScanNarrow || wv == kScanWide) P.scan_waves = wv;
