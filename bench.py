@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == matrix rate on gfx950)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 D, NT, T0 = 9, 512, 7.613
 
 
@@ -171,6 +172,18 @@ def c2_report(args, B, world, value, elapsed, ktimes):
         "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
         "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
         "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    # the scan is the HBM-heavy stage: E in, Q out (algorithmic 2 * 16 d^2 bytes per step)
+    # against the 8 TB/s HBM3E peak, with the PMC bytes where the summary matches this batch
+    ms_s, n_s = ktimes.get("k_scan", (0.0, 0))
+    if n_s:
+        per_ms = ms_s / n_s
+        alg = B * NT * 2 * 16 * D * D
+        pmc = pmc_traffic("k_scan", B)
+        out["roofline_scan"] = {"bound": "hbm", "kernel": "k_scan", "per_launch_ms": per_ms,
+                                "algorithmic_bytes": alg, "achieved": alg / (per_ms * 1e-3) / 1e9,
+                                "traffic": pmc, "achieved_traffic": (pmc / (per_ms * 1e-3) / 1e9) if pmc else None,
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": alg / (per_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     return out
 
 
