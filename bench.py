@@ -244,6 +244,49 @@ def c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam):
     return out
 
 
+def c4opt(args):
+    """SURVEY.md 8d C4 run as the optimiser the reference wraps (FidelityCalculations.jl:161-218):
+    B restarts (x_main = 2pi*0.001*U, theta = 2pi*U, seed 1000 + r) advance together in a
+    batched strong-Wolfe L-BFGS whose every line-search round is one device pass
+    (robustgrape_amd/optimize.py).  Warm-up: W iterations; timed: K more iterations from
+    there.  Reports gradient-evaluations/s including the optimiser's own host/device work,
+    and the best fidelity reached.  One GPU; the multi-GPU form is sweep.optimize_sweep."""
+    import torch
+    from robustgrape_amd import optimize as OPT
+    from robustgrape_amd import regularization as REG
+    from robustgrape_amd.types import FidelityRobustGRAPEParameters
+    B = args.batch or 1024
+    fp = problem()
+    X0 = restart_inputs(0, B)
+    params = FidelityRobustGRAPEParameters(
+        x_initial=X0[0], regularization_functions=[REG.regularization_cost_phase], regularization_coeff1=[1e-7],
+        regularization_coeff2=[1e-7], error_source_coeff=[], iterations=10 ** 9)
+    cost = OPT.RobustCost(fp, params, nparam=1, max_batch=B, device=0)
+    dev = torch.device("cuda", 0)
+    opts = OPT._solver_options(params)
+    opts.update(g_tol=0.0)  # no early stop: every restart iterates through the timed region
+    res = OPT.lbfgs_batched(cost, torch.as_tensor(X0, device=dev), **dict(opts, iterations=args.warmup))
+    torch.cuda.synchronize()
+    calls0 = int(res.f_calls.sum())
+    t0 = time.perf_counter()
+    res2 = OPT.lbfgs_batched(cost, res.minimizer, **dict(opts, iterations=args.steps))
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    calls = int(res2.f_calls.sum())
+    F = 1.0 - cost.fidelity_terms(res2.minimizer)[0]
+    cost.close()
+    out = {"metric": "GRAPE gradient-evals/sec inside batched L-BFGS (C4 sweep), Rydberg CZ d=9 N_t=512",
+           "value": calls / elapsed, "unit": "gradient-evals/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": "C4 as an optimisation: B restarts, strong-Wolfe L-BFGS (m=10), "
+                                  "regularization_cost_phase 1e-7/1e-7", "restarts_per_gpu": B,
+                      "parallelism": "restarts x1"},
+           "optimizer": {"evals_per_iteration": calls / (B * args.steps), "warmup_evals": calls0,
+                         "best_infidelity": float(torch.min(F)), "median_infidelity": float(torch.median(F))}}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -251,10 +294,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
                     help="restarts per GPU (one device pass each step); default 4096 (c2), 256 (c3), 4 (c5)")
-    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c4opt"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
-                         "(dense MFMA engine, SURVEY.md 8d C5)")
+                         "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
+                         "batched L-BFGS (one step = one iteration of every restart)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -262,6 +306,8 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.workload == "c4opt":
+        return c4opt(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
