@@ -117,8 +117,17 @@ typedef struct grape_desc {
     int32_t n_target_terms;
     const grape_term *target_terms;  /* may only use GRAPE_VAR_ONE / GRAPE_VAR_XADD */
     int32_t max_batch;  /* largest nbatch a single call will use (workspace sizing); <=0 -> 256 */
-    int32_t reserved[7];
+    int32_t reserved[7]; /* reserved[0]: flags (GRAPE_DESC_*); the rest must be 0 */
 } grape_desc;
+
+/*
+ * reserved[0] flag: closure fallback (SURVEY.md 8b "host-evaluated H tensors").
+ * H0 and the target stay opaque host closures (the reference's own idiom,
+ * src/Types.jl:10,50); the caller evaluates them at every call site of the
+ * reference and passes the tables to grape_fidelity_grad_tables.  ops / terms
+ * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_SMALL_DIM and nerr == 0 only.
+ */
+#define GRAPE_DESC_HOST_TABLES 1
 
 typedef struct grape_plan grape_plan;
 
@@ -172,6 +181,21 @@ int grape_fidelity_grad(grape_plan *plan, int nbatch, const double *x,
 int grape_fidelity_grad_device_async(grape_plan *plan, int nbatch, const double *d_x,
                                      double *d_F, double *d_F_dx,
                                      double *d_F_d2err, double *d_F_d2err_dx);
+
+/*
+ * Closure fallback (plans created with GRAPE_DESC_HOST_TABLES): the outputs of
+ * grape_fidelity_grad for problems whose H0 / target are host closures.  The
+ * caller evaluates the closures at exactly the reference's call sites
+ * (src/UnitaryCalculations.jl:45,51,59; src/FidelityCalculations.jl:32-40):
+ *   H  [nbatch][ntimes][1 + nparam + nadd][ndim*ndim] complex, column-major, interleaved:
+ *      variant 0: H0(k, x[:,k], x_add); 1 + p: x[p,k] + eps; 1 + nparam + q: x_add[q] + eps
+ *   U0 [nbatch][1 + nadd][ndim*ndim] complex, column-major, interleaved:
+ *      slot 0: target(x_add); 1 + q: target(x_add + eps e_q)
+ * The device runs the exponentials, the scan and the gradient contractions.
+ * Synchronous; host buffers.
+ */
+int grape_fidelity_grad_tables(grape_plan *plan, int nbatch, const double *x, const double *H,
+                               const double *U0, double *F, double *F_dx);
 
 /* Block until all work enqueued on the plan's stream finished; reports device-side errors. */
 int grape_plan_synchronize(grape_plan *plan);

@@ -58,6 +58,7 @@ using grape_host::KMark;
 using grape_host::launch_pipeline;
 using grape_host::launch_expm_raw;
 using grape_host::set_lds_limits;
+using grape_host::launch_table_pipeline;
 
 
 hipError_t dispatch_pipeline(int D, const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mk) {
@@ -83,6 +84,15 @@ hipError_t dispatch_expm_variants(int D, const DevProblem &P, const DevBatch &B,
     switch (D) {
 #define CASE(d) \
     case d: return grape_host::launch_expm_variants<d>(P, B, st);
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
+hipError_t dispatch_table(int D, const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mk) {
+    switch (D) {
+#define CASE(d) \
+    case d: return launch_table_pipeline<d>(P, B, st, mk);
         GRAPE_DIMS(CASE)
 #undef CASE
     }
@@ -131,6 +141,9 @@ struct grape_plan {
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
+    // closure mode (GRAPE_DESC_HOST_TABLES): host-evaluated H and target tables
+    bool tables = false;
+    cd *d_Htab = nullptr, *d_U0tab = nullptr;
     cd *d_sink = nullptr;                      // DevBatch::sink
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
@@ -170,7 +183,8 @@ static void free_plan(grape_plan *p) {
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
-                    p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf};
+                    p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf,
+                    p->d_Htab, p->d_U0tab};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -323,18 +337,27 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (!desc || !out) return fail(GRAPE_ERR_INVALID, "null argument");
     *out = nullptr;
     const int D = desc->ndim;
-    if (D < 2 || desc->ntimes < 1 || desc->nparam < 1 || desc->nadd < 0 || desc->nerr < 0 || desc->n_ops < 1)
+    const bool tables = (desc->reserved[0] & GRAPE_DESC_HOST_TABLES) != 0;
+    if (D < 2 || desc->ntimes < 1 || desc->nparam < 1 || desc->nadd < 0 || desc->nerr < 0 ||
+        (!tables && desc->n_ops < 1))
         return fail(GRAPE_ERR_INVALID, "bad dimensions in descriptor");
     if (D > GRAPE_MAX_DENSE_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim > GRAPE_MAX_DENSE_DIM");
-    if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
-    if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || !desc->projector_diag || !desc->target_terms ||
-        desc->n_target_terms < 1)
-        return fail(GRAPE_ERR_INVALID, "missing operator basis / terms / projector");
+    if (tables) {
+        if (D > GRAPE_MAX_SMALL_DIM)
+            return fail(GRAPE_ERR_UNSUPPORTED, "host tables: ndim > GRAPE_MAX_SMALL_DIM needs an operator basis");
+        if (desc->nerr > 0) return fail(GRAPE_ERR_UNSUPPORTED, "host tables: error sources need an operator basis");
+        if (!desc->projector_diag) return fail(GRAPE_ERR_INVALID, "missing projector");
+    } else {
+        if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
+        if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || !desc->projector_diag || !desc->target_terms ||
+            desc->n_target_terms < 1)
+            return fail(GRAPE_ERR_INVALID, "missing operator basis / terms / projector");
+    }
     if (!(desc->t0 > 0) || !(desc->eps > 0)) return fail(GRAPE_ERR_INVALID, "t0 and eps must be positive");
     int rc;
-    if ((rc = validate_terms(desc->h0_terms, desc->n_h0_terms, desc->n_ops, desc->nparam, desc->nadd, false, "H0")))
+    if (!tables && (rc = validate_terms(desc->h0_terms, desc->n_h0_terms, desc->n_ops, desc->nparam, desc->nadd, false, "H0")))
         return rc;
-    if ((rc = validate_terms(desc->target_terms, desc->n_target_terms, desc->n_ops, desc->nparam, desc->nadd, true,
+    if (!tables && (rc = validate_terms(desc->target_terms, desc->n_target_terms, desc->n_ops, desc->nparam, desc->nadd, true,
                              "target")))
         return rc;
     int n_err_terms = 0;
@@ -348,8 +371,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                                  "error source")))
             return rc;
     }
-    bool xadd_dep = false;
-    for (int k = 0; k < desc->n_h0_terms; ++k)
+    // host tables: H0 is an opaque closure that may read x_add
+    bool xadd_dep = tables && desc->nadd > 0;
+    for (int k = 0; k < (tables ? 0 : desc->n_h0_terms); ++k)
         if (desc->h0_terms[k].var == 2) xadd_dep = true;
     for (int k = 0; k < n_err_terms; ++k)
         if (desc->err_terms[k].var == 2) xadd_dep = true;
@@ -385,6 +409,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (dispatch_lds_limits(D) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
 
     DevProblem &P = p->P;
+    p->tables = tables;
     P.D = D;
     P.Nt = desc->ntimes;
     P.np = desc->nparam;
@@ -427,7 +452,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     }
     // E stores every variant for the error-source pipeline; without error sources
     // only the nominal propagators are stored (k_expm_grad consumes the rest in place)
-    P.nv = desc->nerr > 0 ? (int)vs.size() : 1;
+    // host tables: every variant's propagator is stored (k_grad reads them back)
+    P.nv = (desc->nerr > 0 || tables) ? (int)vs.size() : 1;
     P.dt = desc->t0 / desc->ntimes;
     P.eps = desc->eps;
     P.eps2 = desc->eps2;
@@ -456,8 +482,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
 
     // operator basis: column-major interleaved -> row-major cd tiles (row builds)
     // and column-major ones (the exp kernels build columns)
-    std::vector<cd> ops((size_t)desc->n_ops * D * D), opsT(ops.size());
-    for (int o = 0; o < desc->n_ops; ++o)
+    const int n_ops = tables ? 0 : desc->n_ops;
+    std::vector<cd> ops((size_t)n_ops * D * D), opsT(ops.size());
+    for (int o = 0; o < n_ops; ++o)
         for (int r = 0; r < D; ++r)
             for (int c = 0; c < D; ++c) {
                 const double *src = desc->ops + 2 * ((size_t)o * D * D + r + (size_t)c * D);
@@ -466,8 +493,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             }
     const size_t MB = p->max_batch, T = (size_t)D * D;
     bool ok = dalloc(&p->d_ops, ops.size()) == hipSuccess && dalloc(&p->d_opsT, opsT.size()) == hipSuccess &&
-              dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
-              dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess && dalloc(&p->d_W, (size_t)D) == hipSuccess &&
+              dalloc(&p->d_h0, std::max(desc->n_h0_terms, 0)) == hipSuccess &&
+              dalloc(&p->d_tgt, std::max(desc->n_target_terms, 0)) == hipSuccess &&
+              dalloc(&p->d_W, (size_t)D) == hipSuccess &&
               dalloc(&p->d_E, MB * P.Nt * P.nv * T) == hipSuccess && dalloc(&p->d_Q, MB * P.Nt * T) == hipSuccess &&
               dalloc(&p->d_Mc, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
@@ -485,6 +513,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
              dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
+    if (ok && tables)
+        ok = dalloc(&p->d_Htab, MB * P.Nt * P.nv * T) == hipSuccess &&
+             dalloc(&p->d_U0tab, MB * (1 + P.na) * T) == hipSuccess;
     if (!ok) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed"));
     if (hipMemset(p->d_ctrl, 0, kCtrlInts * sizeof(int)) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "memset failed"));
@@ -508,11 +539,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
          hipMemcpy(p->d_err_off, desc->err_term_offsets, (P.ne + 1) * sizeof(int), hipMemcpyHostToDevice) !=
              hipSuccess))
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
-    if (hipMemcpy(p->d_ops, ops.data(), ops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_opsT, opsT.data(), opsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
-            hipSuccess ||
+    if ((!tables &&
+         (hipMemcpy(p->d_ops, ops.data(), ops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(p->d_opsT, opsT.data(), opsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
+              hipSuccess)) ||
         hipMemcpy(p->d_W, desc->projector_diag, D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     P.ops = p->d_ops;
@@ -609,6 +641,12 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     B.status = p->d_ctrl + 2;
     B.sink = p->d_sink;
     HIPCHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+    if (p->tables) {
+        B.Htab = p->d_Htab + w0 * P.Nt * P.nv * T;
+        B.U0tab = p->d_U0tab + w0 * (1 + P.na) * T;
+        HIPCHECK(dispatch_table(P.D, P, B, st, mk));
+        return GRAPE_OK;
+    }
     HIPCHECK(dispatch_pipeline(P.D, P, B, st, mk));
     return GRAPE_OK;
 }
@@ -660,6 +698,7 @@ static void resolve_events(grape_plan *p) {
 int grape_fidelity_grad_device_async(grape_plan *p, int nbatch, const double *d_x, double *d_F, double *d_F_dx,
                                      double *d_F_d2err, double *d_F_d2err_dx) {
     if (!p || nbatch < 0 || (nbatch > 0 && (!d_x || !d_F || !d_F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (p->tables) return fail(GRAPE_ERR_INVALID, "host-table plan: use grape_fidelity_grad_tables");
     if (p->P.ne > 0 && nbatch > 0 && (!d_F_d2err || !d_F_d2err_dx))
         return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     HIPCHECK(hipSetDevice(p->device));
@@ -690,6 +729,7 @@ int grape_plan_synchronize(grape_plan *p) {
 int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, double *F_dx, double *F_d2err,
                         double *F_d2err_dx) {
     if (!p || nbatch < 0 || (nbatch > 0 && (!x || !F || !F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (p->tables) return fail(GRAPE_ERR_INVALID, "host-table plan: use grape_fidelity_grad_tables");
     if (p->P.ne > 0 && nbatch > 0 && (!F_d2err || !F_d2err_dx))
         return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     HIPCHECK(hipSetDevice(p->device));
@@ -710,6 +750,33 @@ int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, d
         }
         HIPCHECK(hipMemcpyAsync(F_dx + (size_t)b0 * nx, p->d_Fdx, (size_t)nb * nx * sizeof(double),
                                 hipMemcpyDeviceToHost, p->stream));
+        rc = grape_plan_synchronize(p);
+        if (rc) return rc;
+    }
+    return GRAPE_OK;
+}
+
+int grape_fidelity_grad_tables(grape_plan *p, int nbatch, const double *x, const double *H, const double *U0,
+                               double *F, double *F_dx) {
+    if (!p || nbatch < 0 || (nbatch > 0 && (!x || !H || !U0 || !F || !F_dx)))
+        return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (!p->tables) return fail(GRAPE_ERR_INVALID, "plan was not created with GRAPE_DESC_HOST_TABLES");
+    HIPCHECK(hipSetDevice(p->device));
+    const DevProblem &P = p->P;
+    const size_t nx = P.nx, T = (size_t)P.D * P.D, hsz = (size_t)P.Nt * P.nv * T, usz = (1 + (size_t)P.na) * T;
+    for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
+        const int nb = std::min(p->max_batch, nbatch - b0);
+        HIPCHECK(hipMemcpyAsync(p->d_x, x + b0 * nx, nb * nx * sizeof(double), hipMemcpyHostToDevice, p->stream));
+        HIPCHECK(hipMemcpyAsync(p->d_Htab, H + 2 * b0 * hsz, nb * hsz * sizeof(cd), hipMemcpyHostToDevice,
+                                p->stream));
+        HIPCHECK(hipMemcpyAsync(p->d_U0tab, U0 + 2 * b0 * usz, nb * usz * sizeof(cd), hipMemcpyHostToDevice,
+                                p->stream));
+        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx, nullptr, nullptr);
+        if (rc) return rc;
+        HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+        HIPCHECK(hipMemcpyAsync(F + b0, p->d_F, nb * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        HIPCHECK(hipMemcpyAsync(F_dx + b0 * nx, p->d_Fdx, nb * nx * sizeof(double), hipMemcpyDeviceToHost,
+                                p->stream));
         rc = grape_plan_synchronize(p);
         if (rc) return rc;
     }
@@ -812,6 +879,7 @@ int grape_expectation_values(grape_plan *p, const double *x, double *ev) {
 int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
                          double *U_derr_dx, double *U_derr_dx_add) {
     if (!p || !x) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (p->tables) return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: host-table plans are not supported");
     if (p->dense)
         return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: ndim > GRAPE_MAX_SMALL_DIM (dense engine) "
                                            "is not supported; use grape_fidelity_grad");

@@ -96,6 +96,9 @@ struct DevBatch {
     cd *ovf2_slots;         // [nb][Nt][nvg][D][D]  A of parked k_expm_grad items
     int *status;            // bit 0: singular Pade denominator
     cd *sink;               // [D][D] write-only target of inactive lanes' unconditional stores
+    // closure fallback (grape_fidelity_grad_tables): host-evaluated closures, per evaluation
+    const cd *Htab;         // [nb][Nt][nv][D][D] column-major H at every closure call site (else null)
+    const cd *U0tab;        // [nb][1 + na][D][D] column-major target at x_add, x_add + eps e_q (else null)
 };
 
 __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,
@@ -129,6 +132,20 @@ __device__ __forceinline__ void build_row(const cd *ops, const Term *terms, int 
 #pragma unroll
         for (int j = 0; j < D; ++j) h[j] = cadd(h[j], cmul(c, op[j]));
     }
+}
+
+// Row i of the target U0(x_add [+ eps e_q]) of evaluation b: from the operator
+// basis, or from the host-evaluated table in closure mode (slot 0: x_add, 1 + q: x_add + eps e_q)
+template <int D>
+__device__ __forceinline__ void target_row(const DevProblem &P, const DevBatch &B, int b, int slot, int i,
+                                           const double *xb, const double *xadd, const Pert &pp, cd (&h)[D]) {
+    if (B.U0tab) {
+        const cd *U = B.U0tab + ((size_t)b * (1 + P.na) + slot) * D * D + i;
+#pragma unroll
+        for (int j = 0; j < D; ++j) h[j] = U[(size_t)j * D];
+        return;
+    }
+    build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, pp, h);
 }
 
 // ---------------------------------------------------------------------------
@@ -242,6 +259,53 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
     }
     if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
     if (valid) {  // E row-major: column i at stride D (coalesced across the group)
+        cd *col = B.E + (size_t)gidc * D * D + G.i;
+#pragma unroll
+        for (int j = 0; j < D; ++j) col[j * D] = x[j];
+        if (singular) atomicOr(B.status, 1);
+    }
+}
+
+// Closure mode: column i of A = -i dt H for item gid from the host-evaluated table
+// (element-wise (-i dt) * h, exactly the reference's -im*dt*H before exp).
+template <int D>
+struct TableBuilder {
+    const cd *H;  // this item's H, column-major
+    int i;
+    double dt;
+    bool valid;
+    __device__ __forceinline__ void operator()(cd (&a)[D]) const {
+        const cd *col = H + i * D;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd h = col[j];
+            a[j] = valid ? cmake(dt * h.im, -(dt * h.re)) : czero();
+        }
+    }
+};
+
+// k_expm for closure mode: every variant of every step from the H table
+template <int D>
+__global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm_table(DevProblem P, DevBatch B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    cd *lds = reinterpret_cast<cd *>(smem_raw);
+    Group<D> G = make_group<D>(lds, threadIdx.x);
+    const long nitems = (long)B.nb * P.Nt * P.nv;
+    const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
+    const bool valid = G.lane_ok && gid < nitems;
+    const long gidc = valid ? gid : 0;
+    TableBuilder<D> rebuild{B.Htab + (size_t)gidc * D * D, G.i, P.dt, valid};
+    cd a[D], x[D];
+    rebuild(a);
+    int singular = 0, s = 0;
+    const int m = expm_prologue<D>(G, a, x, valid, s);
+    cd *out = B.E + (size_t)gidc * D * D + G.i * D;
+    if (m > 5) {
+        if (valid) park<D>(G, out, a, gid, B.overflow, B.overflow_count);
+        return;
+    }
+    if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
+    if (valid) {
         cd *col = B.E + (size_t)gidc * D * D + G.i;
 #pragma unroll
         for (int j = 0; j < D; ++j) col[j * D] = x[j];
@@ -420,7 +484,7 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     Pert none;
     none.var = -1; none.index = 0; none.delta = 0.0;
     cd l[D], kk[D];
-    build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, none, l);  // U0 row i
+    target_row<D>(P, B, b, 0, i, xb, xadd, none, l);  // U0 row i
     if (f0) {
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) S1[i * D + jj] = l[jj];
@@ -468,8 +532,8 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     for (int qd = 0; qd < P.na; ++qd) {
         Pert pq;
         pq.var = VAR_XADD; pq.index = qd; pq.delta = P.eps;
-        build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, pq, l);
-        build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, none, t);
+        target_row<D>(P, B, b, 1 + qd, i, xb, xadd, pq, l);
+        target_row<D>(P, B, b, 0, i, xb, xadd, none, t);
         if (f0) {
 #pragma unroll
             for (int jj = 0; jj < D; ++jj) S1[i * D + jj] = cscale(P.inv_eps, csub(l[jj], t[jj]));

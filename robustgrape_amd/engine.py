@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 from . import _capi
-from .operators import DescriptorBuffers
+from .operators import DescriptorBuffers, TableDescriptor, has_operator_basis, host_tables
 from .types import FidelityRobustGRAPEProblem, split_x
 
 
@@ -29,7 +29,12 @@ class GrapePlan:
         self.nx = self.nparam * self.up.ntimes + self.up.nb_additional_param
         self.nerr = len(self.up.error_sources)
         self.max_batch = int(max_batch)
-        self._bufs = DescriptorBuffers(fp, self.nparam, self.max_batch)
+        # operator bases -> the fused device path; plain closures -> the host-table fallback
+        self.tables = not has_operator_basis(fp)
+        if self.tables:
+            self._bufs = TableDescriptor(fp, self.nparam, self.max_batch)
+        else:
+            self._bufs = DescriptorBuffers(fp, self.nparam, self.max_batch)
         h = ctypes.c_void_p()
         _capi.check(L.grape_plan_create(ctypes.byref(self._bufs.desc), self.device, ctypes.byref(h)))
         self.handle = h
@@ -63,6 +68,11 @@ class GrapePlan:
         nb = X.shape[0]
         F = np.empty(nb)
         Fdx = np.empty((nb, self.nx))
+        if self.tables:  # closures evaluated here, everything else on the device
+            H, U0 = host_tables(self.fp, X, self.nparam)
+            _capi.check(_capi.lib().grape_fidelity_grad_tables(self.handle, nb, _capi.dptr(X), _capi.dptr(H),
+                                                                _capi.dptr(U0), _capi.dptr(F), _capi.dptr(Fdx)))
+            return F, Fdx, np.zeros((nb, 0)), np.zeros((nb, self.nx, 0))
         Fd2 = np.empty((nb, self.nerr)) if self.nerr else None
         Fd2dx = np.empty((nb, self.nerr, self.nx)) if self.nerr else None
         _capi.check(_capi.lib().grape_fidelity_grad(self.handle, nb, _capi.dptr(X), _capi.dptr(F),

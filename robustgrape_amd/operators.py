@@ -204,3 +204,72 @@ class DescriptorBuffers:
             n_target_terms=len(fp.target_unitary.terms), target_terms=self.target,
             max_batch=int(max_batch))
         del stack
+
+
+# ---------------------------------------------------------------------------
+# closure fallback (GRAPE_DESC_HOST_TABLES, grape_fidelity_grad_tables)
+# ---------------------------------------------------------------------------
+GRAPE_DESC_HOST_TABLES = 1  # include/grape.h
+
+
+def has_operator_basis(fp) -> bool:
+    """True when H0, every error source and the target are operator bases (the fused device path)."""
+    up = fp.unitary_problem
+    return (isinstance(up.H0, OperatorBasisHamiltonian) and isinstance(fp.target_unitary, OperatorBasisTarget)
+            and all(isinstance(es.Herror, OperatorBasisError) for es in up.error_sources))
+
+
+class TableDescriptor:
+    """grape_desc of a closure problem: no operator basis; the host evaluates the closures
+    (host_tables) and the device does the rest (the SURVEY.md 8b fallback)."""
+
+    def __init__(self, fp, nparam: int, max_batch: int = 256):
+        up = fp.unitary_problem
+        if up.error_sources:
+            raise TypeError("device path: error sources need operator-basis H0, Herror and target "
+                            "(the closure fallback covers problems without error sources)")
+        P = np.asarray(fp.projector, np.float64)
+        if np.count_nonzero(P - np.diag(np.diag(P))):
+            raise ValueError("device path supports diagonal projectors only")
+        self.pdiag = np.ascontiguousarray(np.diag(P).astype(np.float64))
+        dp = ctypes.POINTER(ctypes.c_double)
+        self.desc = CDesc(
+            ndim=up.ndim, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param, nerr=0, n_ops=0,
+            t0=float(up.t0), eps=float(up.eps), eps2=float(up.eps2), projector_diag=self.pdiag.ctypes.data_as(dp),
+            n_h0_terms=0, n_target_terms=0, max_batch=int(max_batch),
+            reserved=(ctypes.c_int32 * 7)(GRAPE_DESC_HOST_TABLES))
+
+
+def host_tables(fp, X, nparam: int):
+    """The closure calls of one batch, at exactly the reference's call sites and arguments:
+    H0(nt, x[:,nt], x_add) (UnitaryCalculations.jl:45), with x[p,nt] + eps (:48-51) and
+    x_add[q] + eps (:57-59); target(x_add) and target(x_add + eps e_q)
+    (FidelityCalculations.jl:32-38).  Returns the grape_fidelity_grad_tables layouts:
+    H (nb, N_t, 1 + np + na, d, d) and U0 (nb, 1 + na, d, d), each matrix column-major."""
+    from .types import split_x
+    up = fp.unitary_problem
+    d, nt, na, eps = up.ndim, up.ntimes, up.nb_additional_param, float(up.eps)
+    X = np.asarray(X, np.float64)
+    nb = X.shape[0]
+    H = np.empty((nb, nt, 1 + nparam + na, d, d), np.complex128)
+    U0 = np.empty((nb, 1 + na, d, d), np.complex128)
+    for b in range(nb):
+        x_main, x_add, _ = split_x(up, X[b])
+        for k in range(nt):
+            xk = x_main[:, k].copy()
+            H[b, k, 0] = up.H0(k + 1, xk.copy(), x_add.copy())
+            for p in range(nparam):
+                xp = xk.copy()
+                xp[p] += eps
+                H[b, k, 1 + p] = up.H0(k + 1, xp, x_add.copy())
+            for q in range(na):
+                xa = x_add.copy()
+                xa[q] += eps
+                H[b, k, 1 + nparam + q] = up.H0(k + 1, xk.copy(), xa)
+        U0[b, 0] = fp.target_unitary(x_add.copy())
+        for q in range(na):
+            xa = x_add.copy()
+            xa[q] += eps
+            U0[b, 1 + q] = fp.target_unitary(xa)
+    # a column-major d x d matrix is the C-order layout of its transpose
+    return np.ascontiguousarray(H.swapaxes(-1, -2)), np.ascontiguousarray(U0.swapaxes(-1, -2))

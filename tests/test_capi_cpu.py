@@ -56,6 +56,30 @@ def test_closure_problems_are_rejected_by_the_device_path():
         DescriptorBuffers(P.sym_problem(8, device=False), nparam=1)
 
 
+def test_closure_problems_take_the_table_descriptor():
+    """Closure H0 / target (no error sources): GRAPE_DESC_HOST_TABLES descriptor and host tables
+    laid out as grape_fidelity_grad_tables expects (column-major, variant order 0 | dx | dxa)."""
+    from robustgrape_amd.operators import (GRAPE_DESC_HOST_TABLES, TableDescriptor, has_operator_basis,
+                                           host_tables)
+    fp = P.sym_problem(4, device=False)
+    assert not has_operator_basis(fp) and has_operator_basis(P.sym_problem(4))
+    t = TableDescriptor(fp, nparam=1, max_batch=2)
+    assert t.desc.reserved[0] == GRAPE_DESC_HOST_TABLES and t.desc.n_ops == 0 and t.desc.nerr == 0
+    x = P.random_x(4, 3)
+    H, U0 = host_tables(fp, np.stack([x, x]), 1)
+    assert H.shape == (2, 4, 3, 5, 5) and U0.shape == (2, 2, 5, 5)
+    up = fp.unitary_problem
+    eps = up.eps
+    k = 2
+    Hk = np.asarray(up.H0(k + 1, np.array([x[k]]), x[-1:]))
+    np.testing.assert_array_equal(H[1, k, 0], Hk.T)  # column-major storage
+    np.testing.assert_array_equal(H[1, k, 1], np.asarray(up.H0(k + 1, np.array([x[k] + eps]), x[-1:])).T)
+    np.testing.assert_array_equal(H[1, k, 2], Hk.T)  # H0 ignores x_add: the dxa variant equals the nominal
+    np.testing.assert_array_equal(U0[0, 1], np.asarray(fp.target_unitary(x[-1:] + eps)).T)
+    with pytest.raises(TypeError):
+        TableDescriptor(P.sym_problem(4, errors=("amp",), device=False), nparam=1)
+
+
 def test_non_diagonal_projector_rejected():
     from robustgrape_amd.operators import DescriptorBuffers
     fp = P.sym_problem(8)

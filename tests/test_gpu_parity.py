@@ -128,8 +128,8 @@ def test_errors_are_loud():
     from robustgrape_amd import calculate_fidelity_and_derivatives
     with pytest.raises(AssertionError):
         calculate_fidelity_and_derivatives(P.full9_problem(64), np.zeros(64 + 2))
-    with pytest.raises(TypeError):
-        calculate_fidelity_and_derivatives(P.sym_problem(8, device=False), np.zeros(9))
+    with pytest.raises(TypeError):  # closures + error sources: no device path
+        calculate_fidelity_and_derivatives(P.sym_problem(8, errors=("amp",), device=False), np.zeros(9))
 
 
 # ---------------------------------------------------------------- error sources (C3)
