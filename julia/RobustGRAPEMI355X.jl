@@ -99,11 +99,69 @@ function device_plan(fp, nparam::Int; device::Integer=0, max_batch::Integer=256)
     end
 end
 
+const GRAPE_DESC_HOST_TABLES = Int32(1)
+
+# Closure fallback (grape.h GRAPE_DESC_HOST_TABLES): no operator basis in the descriptor.
+function table_plan(fp, nparam::Int; device::Integer=0)
+    get!(_plans, fp) do
+        up = fp.unitary_problem
+        isempty(up.error_sources) || error("closure problems with error sources need operator bases")
+        pdiag = Float64.(diag(fp.projector))
+        desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, 0, 0, up.t0, up.ϵ, up.ϵ2,
+                             pointer(pdiag), C_NULL, 0, C_NULL, C_NULL, C_NULL, 0, C_NULL, 1,
+                             (GRAPE_DESC_HOST_TABLES, ntuple(_ -> Int32(0), 6)...)))
+        out = Ref{Ptr{Cvoid}}(C_NULL)
+        GC.@preserve pdiag begin
+            _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
+                         desc, device, out))
+        end
+        p = DevicePlan(out[], Any[pdiag], nparam * up.ntimes + up.nb_additional_param, 0)
+        finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
+        p
+    end
+end
+
+# The closure calls of UnitaryCalculations.jl:45,51,59 and FidelityCalculations.jl:32-38, tabulated.
+function closure_tables(fp, x::Vector{Float64}, np::Int)
+    up = fp.unitary_problem; d, nt, na, ϵ = up.ndim, up.ntimes, up.nb_additional_param, up.ϵ
+    x_main = reshape(x[1:end-na], np, nt); x_add = x[end-na+1:end]
+    H = zeros(ComplexF64, d, d, 1 + np + na, nt)
+    for k in 1:nt
+        xk = x_main[:, k]
+        H[:, :, 1, k] = up.H0(k, copy(xk), copy(x_add))
+        for p in 1:np
+            xp = copy(xk); xp[p] += ϵ; H[:, :, 1+p, k] = up.H0(k, xp, copy(x_add))
+        end
+        for q in 1:na
+            xa = copy(x_add); xa[q] += ϵ; H[:, :, 1+np+q, k] = up.H0(k, copy(xk), xa)
+        end
+    end
+    U0 = zeros(ComplexF64, d, d, 1 + na)
+    U0[:, :, 1] = fp.target_unitary(copy(x_add))
+    for q in 1:na
+        xa = copy(x_add); xa[q] += ϵ; U0[:, :, 1+q] = fp.target_unitary(xa)
+    end
+    return H, U0
+end
+
 "Drop-in for src/FidelityCalculations.jl:19-119: (F, F_dx_tot, F_d2err, F_d2err_dx_tot)."
 function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
     up = fp.unitary_problem
     xm = length(x) - up.nb_additional_param
     @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
+    if !(up.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis)   # closure fallback
+        np = xm ÷ up.ntimes
+        p = table_plan(fp, np)
+        xv = Vector{Float64}(x)
+        H, U0 = closure_tables(fp, xv, np)
+        F = Ref{Float64}(0.0); F_dx = zeros(p.nx)
+        GC.@preserve xv H U0 F_dx begin
+            _check(ccall((:grape_fidelity_grad_tables, libgrape), Cint,
+                         (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ref{Float64},
+                          Ptr{Float64}), p.handle, 1, xv, H, U0, F, F_dx))
+        end
+        return (F[], F_dx, Float64[], zeros(p.nx, 0))
+    end
     p = device_plan(fp, xm ÷ up.ntimes)
     xv = Vector{Float64}(x)
     F = Ref{Float64}(0.0); F_dx = zeros(p.nx); F_d2err = zeros(p.nerr); F_d2err_dx = zeros(p.nx, p.nerr)
