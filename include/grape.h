@@ -125,7 +125,9 @@ typedef struct grape_desc {
  * H0 and the target stay opaque host closures (the reference's own idiom,
  * src/Types.jl:10,50); the caller evaluates them at every call site of the
  * reference and passes the tables to grape_fidelity_grad_tables.  ops / terms
- * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_SMALL_DIM and nerr == 0 only.
+ * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_SMALL_DIM.  With nerr > 0 the
+ * caller guarantees that H0 and the error closures do not read x_add (the
+ * operator-basis path has the same restriction).
  */
 #define GRAPE_DESC_HOST_TABLES 1
 
@@ -187,15 +189,23 @@ int grape_fidelity_grad_device_async(grape_plan *plan, int nbatch, const double 
  * grape_fidelity_grad for problems whose H0 / target are host closures.  The
  * caller evaluates the closures at exactly the reference's call sites
  * (src/UnitaryCalculations.jl:45,51,59; src/FidelityCalculations.jl:32-40):
- *   H  [nbatch][ntimes][1 + nparam + nadd][ndim*ndim] complex, column-major, interleaved:
- *      variant 0: H0(k, x[:,k], x_add); 1 + p: x[p,k] + eps; 1 + nparam + q: x_add[q] + eps
+ *   H  [nbatch][ntimes][nv][ndim*ndim] complex, column-major, interleaved, variants v:
+ *      nerr == 0: nv = 1 + nparam + nadd
+ *        0: H0(k, x[:,k], x_add) | 1 + p: x[p,k] + eps | 1 + nparam + q: x_add[q] + eps
+ *      nerr > 0: nv = 1 + 2 nparam + nerr (2 + nparam)     (UnitaryCalculations.jl:45-78)
+ *        0: H0 | 1 + p: x[p,k] + eps | 1 + nparam + p: x[p,k] + eps2 |
+ *        per error e, base 1 + 2 nparam + e (2 + nparam):
+ *          base: H0 + Herror_e(.., eps) | base + 1: H0 + Herror_e(.., eps2) |
+ *          base + 2 + p: H0 + Herror_e(.., eps2), both at x[p,k] + eps2
  *   U0 [nbatch][1 + nadd][ndim*ndim] complex, column-major, interleaved:
  *      slot 0: target(x_add); 1 + q: target(x_add + eps e_q)
  * The device runs the exponentials, the scan and the gradient contractions.
+ * F_d2err / F_d2err_dx as in grape_fidelity_grad (may be NULL when nerr == 0).
  * Synchronous; host buffers.
  */
 int grape_fidelity_grad_tables(grape_plan *plan, int nbatch, const double *x, const double *H,
-                               const double *U0, double *F, double *F_dx);
+                               const double *U0, double *F, double *F_dx, double *F_d2err,
+                               double *F_d2err_dx);
 
 /* Block until all work enqueued on the plan's stream finished; reports device-side errors. */
 int grape_plan_synchronize(grape_plan *plan);

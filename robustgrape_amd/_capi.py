@@ -60,7 +60,7 @@ def lib():
         L.grape_fidelity_grad.restype = ctypes.c_int
         L.grape_fidelity_grad_device_async.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp]
         L.grape_fidelity_grad_device_async.restype = ctypes.c_int
-        L.grape_fidelity_grad_tables.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp]
+        L.grape_fidelity_grad_tables.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp, dp, dp]
         L.grape_fidelity_grad_tables.restype = ctypes.c_int
         L.grape_plan_synchronize.argtypes = [vp]
         L.grape_plan_synchronize.restype = ctypes.c_int

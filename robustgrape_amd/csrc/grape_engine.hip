@@ -58,7 +58,6 @@ using grape_host::KMark;
 using grape_host::launch_pipeline;
 using grape_host::launch_expm_raw;
 using grape_host::set_lds_limits;
-using grape_host::launch_table_pipeline;
 
 
 hipError_t dispatch_pipeline(int D, const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mk) {
@@ -84,15 +83,6 @@ hipError_t dispatch_expm_variants(int D, const DevProblem &P, const DevBatch &B,
     switch (D) {
 #define CASE(d) \
     case d: return grape_host::launch_expm_variants<d>(P, B, st);
-        GRAPE_DIMS(CASE)
-#undef CASE
-    }
-    return hipErrorInvalidValue;
-}
-hipError_t dispatch_table(int D, const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mk) {
-    switch (D) {
-#define CASE(d) \
-    case d: return launch_table_pipeline<d>(P, B, st, mk);
         GRAPE_DIMS(CASE)
 #undef CASE
     }
@@ -345,7 +335,6 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (tables) {
         if (D > GRAPE_MAX_SMALL_DIM)
             return fail(GRAPE_ERR_UNSUPPORTED, "host tables: ndim > GRAPE_MAX_SMALL_DIM needs an operator basis");
-        if (desc->nerr > 0) return fail(GRAPE_ERR_UNSUPPORTED, "host tables: error sources need an operator basis");
         if (!desc->projector_diag) return fail(GRAPE_ERR_INVALID, "missing projector");
     } else {
         if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
@@ -361,7 +350,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                              "target")))
         return rc;
     int n_err_terms = 0;
-    if (desc->nerr > 0) {
+    if (desc->nerr > 0 && !tables) {
         for (int e = 0; e < desc->nerr; ++e)
             if (desc->err_term_offsets[e + 1] <= desc->err_term_offsets[e])
                 return fail(GRAPE_ERR_INVALID, "each error source needs at least one term");
@@ -371,8 +360,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                                  "error source")))
             return rc;
     }
-    // host tables: H0 is an opaque closure that may read x_add
-    bool xadd_dep = tables && desc->nadd > 0;
+    // host tables: H0 is an opaque closure that may read x_add; with error sources the
+    // caller guarantees it does not (like the operator-basis path, which refuses that case)
+    bool xadd_dep = tables && desc->nadd > 0 && desc->nerr == 0;
     for (int k = 0; k < (tables ? 0 : desc->n_h0_terms); ++k)
         if (desc->h0_terms[k].var == 2) xadd_dep = true;
     for (int k = 0; k < n_err_terms; ++k)
@@ -534,7 +524,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     }
     if (hipMemcpy(p->d_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
-    if (P.ne > 0 &&
+    if (P.ne > 0 && !tables &&
         (hipMemcpy(p->d_err, desc->err_terms, n_err_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
          hipMemcpy(p->d_err_off, desc->err_term_offsets, (P.ne + 1) * sizeof(int), hipMemcpyHostToDevice) !=
              hipSuccess))
@@ -644,8 +634,6 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     if (p->tables) {
         B.Htab = p->d_Htab + w0 * P.Nt * P.nv * T;
         B.U0tab = p->d_U0tab + w0 * (1 + P.na) * T;
-        HIPCHECK(dispatch_table(P.D, P, B, st, mk));
-        return GRAPE_OK;
     }
     HIPCHECK(dispatch_pipeline(P.D, P, B, st, mk));
     return GRAPE_OK;
@@ -757,9 +745,11 @@ int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, d
 }
 
 int grape_fidelity_grad_tables(grape_plan *p, int nbatch, const double *x, const double *H, const double *U0,
-                               double *F, double *F_dx) {
+                               double *F, double *F_dx, double *F_d2err, double *F_d2err_dx) {
     if (!p || nbatch < 0 || (nbatch > 0 && (!x || !H || !U0 || !F || !F_dx)))
         return fail(GRAPE_ERR_INVALID, "bad argument");
+    if (p && p->P.ne > 0 && nbatch > 0 && (!F_d2err || !F_d2err_dx))
+        return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     if (!p->tables) return fail(GRAPE_ERR_INVALID, "plan was not created with GRAPE_DESC_HOST_TABLES");
     HIPCHECK(hipSetDevice(p->device));
     const DevProblem &P = p->P;
@@ -771,9 +761,15 @@ int grape_fidelity_grad_tables(grape_plan *p, int nbatch, const double *x, const
                                 p->stream));
         HIPCHECK(hipMemcpyAsync(p->d_U0tab, U0 + 2 * b0 * usz, nb * usz * sizeof(cd), hipMemcpyHostToDevice,
                                 p->stream));
-        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx, nullptr, nullptr);
+        int rc = enqueue(p, nb, p->d_x, p->d_F, p->d_Fdx, p->d_Fd2, p->d_Fd2dx);
         if (rc) return rc;
         HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+        if (P.ne > 0) {
+            HIPCHECK(hipMemcpyAsync(F_d2err + b0 * P.ne, p->d_Fd2, nb * P.ne * sizeof(double), hipMemcpyDeviceToHost,
+                                    p->stream));
+            HIPCHECK(hipMemcpyAsync(F_d2err_dx + b0 * P.ne * nx, p->d_Fd2dx, nb * P.ne * nx * sizeof(double),
+                                    hipMemcpyDeviceToHost, p->stream));
+        }
         HIPCHECK(hipMemcpyAsync(F + b0, p->d_F, nb * sizeof(double), hipMemcpyDeviceToHost, p->stream));
         HIPCHECK(hipMemcpyAsync(F_dx + b0 * nx, p->d_Fdx, nb * nx * sizeof(double), hipMemcpyDeviceToHost,
                                 p->stream));

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
 #pragma unroll
     for (int jj = 0; jj < D; ++jj) x[jj] = Ub[i * D + jj];
     mm_tile<D>(x, Tot, ue);  // Ue row i
-    build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, none, w);  // U0 row i
+    target_row<D>(P, B, b, 0, i, xb, xadd, none, w);  // U0 row i
     if (f0) {
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) {
@@ -208,8 +208,8 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
     for (int qd = 0; qd < P.na; ++qd) {
         Pert pq;
         pq.var = VAR_XADD; pq.index = qd; pq.delta = P.eps;
-        build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, pq, x);
-        build_row<D>(P.ops, P.tgt, P.n_tgt, i, 1, xb, xadd, none, ueu);
+        target_row<D>(P, B, b, 1 + qd, i, xb, xadd, pq, x);
+        target_row<D>(P, B, b, 0, i, xb, xadd, none, ueu);
         if (f0) {
 #pragma unroll
             for (int jj = 0; jj < D; ++jj) S1[i * D + jj] = cscale(P.inv_eps, csub(x[jj], ueu[jj]));

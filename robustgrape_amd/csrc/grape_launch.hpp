@@ -50,9 +50,14 @@ template <int D>
 hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mark) {
     constexpr int GPW = grape::Geo<D>::GPW;
     const long nexp = (long)B.nb * P.Nt * P.nv;
-    const bool fused = P.ne == 0;  // eps-variants exp'd and contracted in k_expm_grad
+    // closure mode (grape_fidelity_grad_tables): every variant comes from the host H table
+    const bool table = B.Htab != nullptr;
+    const bool fused = P.ne == 0 && !table;  // eps-variants exp'd and contracted in k_expm_grad
     mark(GRAPE_KERNEL_EXPM, 0);
-    if (!fused)
+    if (table)
+        hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lds<D>(), st, P, B);
+    else if (!fused)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lds<D>(), st, P, B);
     else if (P.pair) {
@@ -143,43 +148,6 @@ hipError_t launch_expm_variants(const DevProblem &P, const DevBatch &B, hipStrea
     return hipGetLastError();
 }
 
-// Closure mode (grape_fidelity_grad_tables): propagators of every variant from the host
-// H table, then the stored-variant pipeline (scan, contraction, x_add reduction).
-template <int D>
-hipError_t launch_table_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t st, const KMark &mark) {
-    constexpr int GPW = grape::Geo<D>::GPW;
-    const long nexp = (long)B.nb * P.Nt * P.nv;
-    mark(GRAPE_KERNEL_EXPM, 0);
-    hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64), expm_lds<D>(),
-                       st, P, B);
-    mark(GRAPE_KERNEL_EXPM, 1);
-    mark(GRAPE_KERNEL_EXPM_HIGH, 0);
-    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
-                       B.overflow_count, B.status, 1);
-    mark(GRAPE_KERNEL_EXPM_HIGH, 1);
-    mark(GRAPE_KERNEL_SCAN, 0);
-    if (P.scan_waves == kScanNarrow)
-        hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
-                           scan_lds<D>(kScanNarrow), st, P, B);
-    else
-        hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide),
-                           st, P, B);
-    mark(GRAPE_KERNEL_SCAN, 1);
-    mark(GRAPE_KERNEL_GRAD, 0);
-    {
-        const long ng = (long)B.nb * P.Nt;
-        hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st, P,
-                           B);
-    }
-    mark(GRAPE_KERNEL_GRAD, 1);
-    if (P.na > 0) {
-        mark(GRAPE_KERNEL_REDUCE, 0);
-        hipLaunchKernelGGL(grape::k_reduce_add<D>, dim3((B.nb * P.na + 255) / 256), dim3(256), 0, st, P, B);
-        mark(GRAPE_KERNEL_REDUCE, 1);
-    }
-    return hipGetLastError();
-}
-
 template <int D, int W>
 hipError_t set_lds_limits_w() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, W>),
@@ -201,7 +169,6 @@ hipError_t set_lds_limits() {
     EXT template hipError_t launch_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &); \
     EXT template hipError_t launch_expm_raw<d>(const cd *, cd *, int, int *, int *, int *, int *, hipStream_t);  \
     EXT template hipError_t set_lds_limits<d>();                                                          \
-    EXT template hipError_t launch_expm_variants<d>(const DevProblem &, const DevBatch &, hipStream_t);      \
-    EXT template hipError_t launch_table_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &);
+    EXT template hipError_t launch_expm_variants<d>(const DevProblem &, const DevBatch &, hipStream_t);
 
 }  // namespace grape_host

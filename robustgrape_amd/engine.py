@@ -68,15 +68,16 @@ class GrapePlan:
         nb = X.shape[0]
         F = np.empty(nb)
         Fdx = np.empty((nb, self.nx))
-        if self.tables:  # closures evaluated here, everything else on the device
-            H, U0 = host_tables(self.fp, X, self.nparam)
-            _capi.check(_capi.lib().grape_fidelity_grad_tables(self.handle, nb, _capi.dptr(X), _capi.dptr(H),
-                                                                _capi.dptr(U0), _capi.dptr(F), _capi.dptr(Fdx)))
-            return F, Fdx, np.zeros((nb, 0)), np.zeros((nb, self.nx, 0))
         Fd2 = np.empty((nb, self.nerr)) if self.nerr else None
         Fd2dx = np.empty((nb, self.nerr, self.nx)) if self.nerr else None
-        _capi.check(_capi.lib().grape_fidelity_grad(self.handle, nb, _capi.dptr(X), _capi.dptr(F),
-                                                     _capi.dptr(Fdx), _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
+        if self.tables:  # closures evaluated here, everything else on the device
+            H, U0 = host_tables(self.fp, X, self.nparam)
+            _capi.check(_capi.lib().grape_fidelity_grad_tables(
+                self.handle, nb, _capi.dptr(X), _capi.dptr(H), _capi.dptr(U0), _capi.dptr(F), _capi.dptr(Fdx),
+                _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
+        else:
+            _capi.check(_capi.lib().grape_fidelity_grad(self.handle, nb, _capi.dptr(X), _capi.dptr(F),
+                                                         _capi.dptr(Fdx), _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
         if not self.nerr:
             Fd2 = np.zeros((nb, 0))
             Fd2dx = np.zeros((nb, self.nx, 0))

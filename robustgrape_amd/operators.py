@@ -225,47 +225,83 @@ class TableDescriptor:
 
     def __init__(self, fp, nparam: int, max_batch: int = 256):
         up = fp.unitary_problem
-        if up.error_sources:
-            raise TypeError("device path: error sources need operator-basis H0, Herror and target "
-                            "(the closure fallback covers problems without error sources)")
         P = np.asarray(fp.projector, np.float64)
         if np.count_nonzero(P - np.diag(np.diag(P))):
             raise ValueError("device path supports diagonal projectors only")
         self.pdiag = np.ascontiguousarray(np.diag(P).astype(np.float64))
         dp = ctypes.POINTER(ctypes.c_double)
         self.desc = CDesc(
-            ndim=up.ndim, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param, nerr=0, n_ops=0,
-            t0=float(up.t0), eps=float(up.eps), eps2=float(up.eps2), projector_diag=self.pdiag.ctypes.data_as(dp),
-            n_h0_terms=0, n_target_terms=0, max_batch=int(max_batch),
-            reserved=(ctypes.c_int32 * 7)(GRAPE_DESC_HOST_TABLES))
+            ndim=up.ndim, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param,
+            nerr=len(up.error_sources), n_ops=0, t0=float(up.t0), eps=float(up.eps), eps2=float(up.eps2),
+            projector_diag=self.pdiag.ctypes.data_as(dp), n_h0_terms=0, n_target_terms=0,
+            max_batch=int(max_batch), reserved=(ctypes.c_int32 * 7)(GRAPE_DESC_HOST_TABLES))
+
+
+def table_variants(nparam: int, nadd: int, nerr: int) -> int:
+    """Variants per step of the grape_fidelity_grad_tables H table (include/grape.h)."""
+    return 1 + nparam + nadd if nerr == 0 else 1 + 2 * nparam + nerr * (2 + nparam)
 
 
 def host_tables(fp, X, nparam: int):
-    """The closure calls of one batch, at exactly the reference's call sites and arguments:
-    H0(nt, x[:,nt], x_add) (UnitaryCalculations.jl:45), with x[p,nt] + eps (:48-51) and
-    x_add[q] + eps (:57-59); target(x_add) and target(x_add + eps e_q)
-    (FidelityCalculations.jl:32-38).  Returns the grape_fidelity_grad_tables layouts:
-    H (nb, N_t, 1 + np + na, d, d) and U0 (nb, 1 + na, d, d), each matrix column-major."""
+    """The closure calls of one batch, at exactly the reference's call sites and arguments
+    (src/UnitaryCalculations.jl:45-78): H0(nt, x[:,nt], x_add); x[p,nt] + eps (:48-51);
+    without error sources x_add[q] + eps (:57-59); with error sources x[p,nt] + eps2 (:53-54),
+    Herror_e(.., eps) + H0 (:67), Herror_e(.., eps2) + H0 (:71) and the mixed
+    Herror_e(x + eps2 e_p, .., eps2) + H0(x + eps2 e_p) (:77-78); target(x_add) and
+    target(x_add + eps e_q) (FidelityCalculations.jl:32-38).  Returns the
+    grape_fidelity_grad_tables layouts H (nb, N_t, nv, d, d) and U0 (nb, 1 + na, d, d), each
+    matrix column-major.  With error sources H0 / Herror must not read x_add (checked)."""
     from .types import split_x
     up = fp.unitary_problem
-    d, nt, na, eps = up.ndim, up.ntimes, up.nb_additional_param, float(up.eps)
+    d, nt, na = up.ndim, up.ntimes, up.nb_additional_param
+    eps, eps2 = float(up.eps), float(up.eps2)
+    errs = up.error_sources
+    ne = len(errs)
     X = np.asarray(X, np.float64)
     nb = X.shape[0]
-    H = np.empty((nb, nt, 1 + nparam + na, d, d), np.complex128)
+    H = np.empty((nb, nt, table_variants(nparam, na, ne), d, d), np.complex128)
     U0 = np.empty((nb, 1 + na, d, d), np.complex128)
     for b in range(nb):
         x_main, x_add, _ = split_x(up, X[b])
         for k in range(nt):
+            nt1 = k + 1
             xk = x_main[:, k].copy()
-            H[b, k, 0] = up.H0(k + 1, xk.copy(), x_add.copy())
+            H0k = np.asarray(up.H0(nt1, xk.copy(), x_add.copy()), np.complex128)
+            Hb = H[b, k]
+            Hb[0] = H0k
             for p in range(nparam):
                 xp = xk.copy()
                 xp[p] += eps
-                H[b, k, 1 + p] = up.H0(k + 1, xp, x_add.copy())
-            for q in range(na):
+                Hb[1 + p] = up.H0(nt1, xp, x_add.copy())
+            if ne == 0:
+                for q in range(na):
+                    xa = x_add.copy()
+                    xa[q] += eps
+                    Hb[1 + nparam + q] = up.H0(nt1, xk.copy(), xa)
+                continue
+            for q in range(na):  # the device treats H0 / Herror as independent of x_add here
                 xa = x_add.copy()
                 xa[q] += eps
-                H[b, k, 1 + nparam + q] = up.H0(k + 1, xk.copy(), xa)
+                same = np.array_equal(np.asarray(up.H0(nt1, xk.copy(), xa.copy()), np.complex128), H0k) and all(
+                    np.array_equal(np.asarray(es.Herror(nt1, xk.copy(), xa.copy(), eps), np.complex128),
+                                   np.asarray(es.Herror(nt1, xk.copy(), x_add.copy(), eps), np.complex128))
+                    for es in errs)
+                if not same:
+                    raise NotImplementedError("error sources together with an x_add-dependent Hamiltonian "
+                                              "(also unsupported by the operator-basis path)")
+            for p in range(nparam):
+                xp = xk.copy()
+                xp[p] = xk[p] + eps2
+                Hb[1 + nparam + p] = up.H0(nt1, xp, x_add.copy())
+            for e, es in enumerate(errs):
+                base = 1 + 2 * nparam + e * (2 + nparam)
+                Hb[base] = np.asarray(es.Herror(nt1, xk.copy(), x_add.copy(), eps), np.complex128) + H0k
+                Hb[base + 1] = np.asarray(es.Herror(nt1, xk.copy(), x_add.copy(), eps2), np.complex128) + H0k
+                for p in range(nparam):
+                    xp = xk.copy()
+                    xp[p] = xk[p] + eps2
+                    Hb[base + 2 + p] = (np.asarray(es.Herror(nt1, xp.copy(), x_add.copy(), eps2), np.complex128)
+                                        + np.asarray(up.H0(nt1, xp.copy(), x_add.copy()), np.complex128))
         U0[b, 0] = fp.target_unitary(x_add.copy())
         for q in range(na):
             xa = x_add.copy()

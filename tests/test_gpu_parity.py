@@ -128,8 +128,13 @@ def test_errors_are_loud():
     from robustgrape_amd import calculate_fidelity_and_derivatives
     with pytest.raises(AssertionError):
         calculate_fidelity_and_derivatives(P.full9_problem(64), np.zeros(64 + 2))
-    with pytest.raises(TypeError):  # closures + error sources: no device path
-        calculate_fidelity_and_derivatives(P.sym_problem(8, errors=("amp",), device=False), np.zeros(9))
+    from robustgrape_amd._capi import GrapeError
+    from robustgrape_amd.types import FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    up13 = UnitaryRobustGRAPEProblem(t0=1.0, ntimes=4, ndim=13, H0=lambda t, x, xa: np.eye(13) * x[0],
+                                     nb_additional_param=0)
+    with pytest.raises(GrapeError):  # closures above the small-d engine: GRAPE_ERR_UNSUPPORTED
+        calculate_fidelity_and_derivatives(FidelityRobustGRAPEProblem(up13, np.eye(13), lambda xa: np.eye(13)),
+                                           np.zeros(4))
 
 
 # ---------------------------------------------------------------- error sources (C3)

@@ -110,3 +110,53 @@ def test_closure_batch_equals_single_and_equals_operator_basis_path():
         Fs, gs, _, _ = calculate_fidelity_and_derivatives(fp_c, X[b])
         assert Fs == F[b] and np.array_equal(gs, Fdx[b])
         _assert_fid(F[b], Fdx[b], Fo[b], Fdxo[b])
+
+
+# ---------------------------------------------------------------- error sources through the tables
+T3, T3_ABS, T3_XADD_ABS = 1e-5, 1e-7, 1e-5
+
+
+def _assert_err(nx_add, d2, d2dx, ref_d2, ref_d2dx):
+    nmain = d2dx.shape[0] - nx_add
+    assert np.max(np.abs(d2 - ref_d2)) <= T3 * np.max(np.abs(ref_d2)) + T3_ABS, (d2, ref_d2)
+    err = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain]))
+    assert err <= T3 * np.max(np.abs(ref_d2dx[:nmain])) + T3_ABS, err
+    assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
+
+
+@pytest.mark.parametrize("name,builder", [
+    ("c1err", lambda: P.sym_problem(500, t0=P.T0_TO, errors=("amp", "freq"), device=False)),
+    ("d7err", lambda: P.fullblk_problem(500, errors=("amp", "freq"), device=False)),
+    ("c3n64", lambda: P.full9_problem(64, nerr=4, device=False)),
+])
+def test_closure_error_sources_match_golden(name, builder):
+    """The reference's own idiom Herror = H(eps) - H(0) as closures (runtests.jl:57-75, 474-494)."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    g = dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(builder(), g["x"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    _assert_err(1, d2, d2dx, g["F_d2err"], g["F_d2err_dx"])
+
+
+@pytest.mark.parametrize("d,ntimes,errors", [(5, 1, ("amp",)), (5, 11, ("amp", "freq")), (7, 6, ("freq",))])
+def test_closure_error_sources_match_live_oracle(d, ntimes, errors):
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    mk = {5: P.sym_problem, 7: P.fullblk_problem}[d]
+    fp = mk(ntimes, errors=errors, device=False)
+    x = P.random_x(ntimes, 500 + ntimes)
+    F0, g0, e0, ed0 = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, e, ed = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0)
+    _assert_err(1, e, ed, e0, ed0)
+
+
+def test_closure_error_sources_with_xadd_dependent_h0_are_refused():
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    from robustgrape_amd.types import ErrorSource
+    fp = _xadd_problem(4, 5, 1)
+    up = fp.unitary_problem
+    Hz = np.diag(np.arange(4.0))
+    fp = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, x, xa, e: e * Hz)]))
+    with pytest.raises(NotImplementedError):
+        calculate_fidelity_and_derivatives(fp, np.concatenate([np.zeros(5), [0.3, 0.2]]))
