@@ -105,9 +105,9 @@ const GRAPE_DESC_HOST_TABLES = Int32(1)
 function table_plan(fp, nparam::Int; device::Integer=0)
     get!(_plans, fp) do
         up = fp.unitary_problem
-        isempty(up.error_sources) || error("closure problems with error sources need operator bases")
+        ne = length(up.error_sources)
         pdiag = Float64.(diag(fp.projector))
-        desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, 0, 0, up.t0, up.ϵ, up.ϵ2,
+        desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, ne, 0, up.t0, up.ϵ, up.ϵ2,
                              pointer(pdiag), C_NULL, 0, C_NULL, C_NULL, C_NULL, 0, C_NULL, 1,
                              (GRAPE_DESC_HOST_TABLES, ntuple(_ -> Int32(0), 6)...)))
         out = Ref{Ptr{Cvoid}}(C_NULL)
@@ -115,25 +115,45 @@ function table_plan(fp, nparam::Int; device::Integer=0)
             _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
                          desc, device, out))
         end
-        p = DevicePlan(out[], Any[pdiag], nparam * up.ntimes + up.nb_additional_param, 0)
+        p = DevicePlan(out[], Any[pdiag], nparam * up.ntimes + up.nb_additional_param, ne)
         finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
         p
     end
 end
 
-# The closure calls of UnitaryCalculations.jl:45,51,59 and FidelityCalculations.jl:32-38, tabulated.
+# The closure calls of UnitaryCalculations.jl:45-78 and FidelityCalculations.jl:32-38, tabulated
+# in grape_fidelity_grad_tables' variant order (include/grape.h).  With error sources H0 and
+# Herror must not read x_add (the device path's restriction).
 function closure_tables(fp, x::Vector{Float64}, np::Int)
-    up = fp.unitary_problem; d, nt, na, ϵ = up.ndim, up.ntimes, up.nb_additional_param, up.ϵ
+    up = fp.unitary_problem; d, nt, na, ϵ, ϵ2 = up.ndim, up.ntimes, up.nb_additional_param, up.ϵ, up.ϵ2
+    errs = up.error_sources; ne = length(errs)
     x_main = reshape(x[1:end-na], np, nt); x_add = x[end-na+1:end]
-    H = zeros(ComplexF64, d, d, 1 + np + na, nt)
+    nv = ne == 0 ? 1 + np + na : 1 + 2np + ne * (2 + np)
+    H = zeros(ComplexF64, d, d, nv, nt)
     for k in 1:nt
         xk = x_main[:, k]
-        H[:, :, 1, k] = up.H0(k, copy(xk), copy(x_add))
+        H0k = up.H0(k, copy(xk), copy(x_add))
+        H[:, :, 1, k] = H0k
         for p in 1:np
             xp = copy(xk); xp[p] += ϵ; H[:, :, 1+p, k] = up.H0(k, xp, copy(x_add))
         end
-        for q in 1:na
-            xa = copy(x_add); xa[q] += ϵ; H[:, :, 1+np+q, k] = up.H0(k, copy(xk), xa)
+        if ne == 0
+            for q in 1:na
+                xa = copy(x_add); xa[q] += ϵ; H[:, :, 1+np+q, k] = up.H0(k, copy(xk), xa)
+            end
+            continue
+        end
+        for p in 1:np
+            xp = copy(xk); xp[p] += ϵ2; H[:, :, 1+np+p, k] = up.H0(k, xp, copy(x_add))
+        end
+        for (e, es) in enumerate(errs)
+            base = 1 + 2np + (e - 1) * (2 + np)
+            H[:, :, base+1, k] = es.Herror(k, copy(xk), copy(x_add), ϵ) + H0k
+            H[:, :, base+2, k] = es.Herror(k, copy(xk), copy(x_add), ϵ2) + H0k
+            for p in 1:np
+                xp = copy(xk); xp[p] += ϵ2
+                H[:, :, base+2+p, k] = es.Herror(k, copy(xp), copy(x_add), ϵ2) + up.H0(k, copy(xp), copy(x_add))
+            end
         end
     end
     U0 = zeros(ComplexF64, d, d, 1 + na)
@@ -149,18 +169,20 @@ function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
     up = fp.unitary_problem
     xm = length(x) - up.nb_additional_param
     @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
-    if !(up.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis)   # closure fallback
+    if !(up.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis &&
+         all(es.Herror isa OperatorBasis for es in up.error_sources))          # closure fallback
         np = xm ÷ up.ntimes
         p = table_plan(fp, np)
         xv = Vector{Float64}(x)
         H, U0 = closure_tables(fp, xv, np)
-        F = Ref{Float64}(0.0); F_dx = zeros(p.nx)
-        GC.@preserve xv H U0 F_dx begin
+        F = Ref{Float64}(0.0); F_dx = zeros(p.nx); F_d2err = zeros(p.nerr); F_d2err_dx = zeros(p.nx, p.nerr)
+        GC.@preserve xv H U0 F_dx F_d2err F_d2err_dx begin
             _check(ccall((:grape_fidelity_grad_tables, libgrape), Cint,
                          (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ref{Float64},
-                          Ptr{Float64}), p.handle, 1, xv, H, U0, F, F_dx))
+                          Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                         p.handle, 1, xv, H, U0, F, F_dx, F_d2err, F_d2err_dx))
         end
-        return (F[], F_dx, Float64[], zeros(p.nx, 0))
+        return (F[], F_dx, F_d2err, F_d2err_dx)
     end
     p = device_plan(fp, xm ÷ up.ntimes)
     xv = Vector{Float64}(x)
