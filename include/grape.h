@@ -207,6 +207,20 @@ int grape_fidelity_grad_tables(grape_plan *plan, int nbatch, const double *x, co
                                const double *U0, double *F, double *F_dx, double *F_d2err,
                                double *F_d2err_dx);
 
+/*
+ * Optimiser support (robustgrape_amd/optimize.py, the batched replacement of the
+ * Optim.jl LBFGS that drives calculate_fidelity_and_derivatives,
+ * src/FidelityCalculations.jl:199-217): the L-BFGS two-loop recursion for R
+ * restarts at once, DEVICE pointers, enqueued on `stream` (a hipStream_t, NULL =
+ * default stream), asynchronous.
+ *   S, Y [m][R][n], rho [m][R]: ring-buffer history; head [R]: next slot;
+ *   hist [R]: stored pairs (<= m); gamma [R]: initial scaling; g [R][n]: gradients;
+ *   D [R][n] (written): the directions -H g.   m <= 64.
+ */
+int grape_lbfgs_direction(int R, int n, int m, const double *S, const double *Y, const double *rho,
+                          const int64_t *head, const int64_t *hist, const double *gamma,
+                          const double *g, double *D, void *stream);
+
 /* Block until all work enqueued on the plan's stream finished; reports device-side errors. */
 int grape_plan_synchronize(grape_plan *plan);
 

@@ -21,7 +21,8 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_plan_destroy", "grape_plan_stream", "grape_plan_set_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times",
-            "grape_interaction_error_operators", "grape_expectation_values", "grape_fidelity_grad_tables"]
+            "grape_interaction_error_operators", "grape_expectation_values", "grape_fidelity_grad_tables",
+            "grape_lbfgs_direction"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
 ABI_VERSION = 2  # GRAPE_ABI_VERSION in include/grape.h
@@ -62,6 +63,8 @@ def lib():
         L.grape_fidelity_grad_device_async.restype = ctypes.c_int
         L.grape_fidelity_grad_tables.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp, dp, dp]
         L.grape_fidelity_grad_tables.restype = ctypes.c_int
+        L.grape_lbfgs_direction.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int] + [vp] * 9
+        L.grape_lbfgs_direction.restype = ctypes.c_int
         L.grape_plan_synchronize.argtypes = [vp]
         L.grape_plan_synchronize.restype = ctypes.c_int
         L.grape_unitary_derivs.argtypes = [vp, dp, dp, dp, dp, dp, dp, dp]

@@ -20,8 +20,9 @@ ENGINE = os.path.join(CSRC, "grape_engine.hip")
 INST = os.path.join(CSRC, "grape_inst.hip")
 DENSE = os.path.join(CSRC, "grape_dense.hip")
 UNITARY = os.path.join(CSRC, "grape_unitary.hip")
+LBFGS = os.path.join(CSRC, "grape_lbfgs.hip")
 DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
-SOURCES = [ENGINE, INST, DENSE, UNITARY]
+SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
                   ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp",
                    "grape_dense.hpp", "grape_dense_api.hpp", "grape_unitary_api.hpp")] + \
@@ -48,7 +49,7 @@ def _units(defines):
     tag = "_".join(d.replace("=", "") for d in defines)
     sub = os.path.join(OBJ, tag or "default")
     units = [(DENSE, [], os.path.join(sub, "grape_dense.o")), (ENGINE, [], os.path.join(sub, "grape_engine.o")),
-             (UNITARY, [], os.path.join(sub, "grape_unitary.o"))]
+             (UNITARY, [], os.path.join(sub, "grape_unitary.o")), (LBFGS, [], os.path.join(sub, "grape_lbfgs.o"))]
     units += [(INST, [f"-DGRAPE_INST_DIM={d}"], os.path.join(sub, f"grape_inst_d{d}.o")) for d in DIMS]
     return sub, units
 

@@ -28,6 +28,7 @@ GPU inside the loop except the per-round active count.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Optional
@@ -113,6 +114,52 @@ def _cubic_min(a0, f0, g0, a1, f1, g1):
     return torch.clamp(a, lo + 0.1 * w, hi - 0.1 * w)
 
 
+_TORCH_TWO_LOOP = bool(os.environ.get("GRAPE_TORCH_TWO_LOOP"))  # A/B switch for measurements
+
+
+def _torch_direction(S, Y, rho, head, hist, gamma, g):
+    """-H g for every row with batched torch ops (host tensors; the device path's checker)."""
+    m, R, _ = S.shape
+    all_rows = torch.arange(R, device=g.device)
+    q = -g.clone()
+    alpha = torch.zeros(m, R, dtype=g.dtype, device=g.device)
+    for j in range(m):
+        slot = (head - 1 - j) % m
+        use = (j < hist)
+        s_j = S[slot, all_rows]
+        y_j = Y[slot, all_rows]
+        r_j = rho[slot, all_rows]
+        a_j = torch.where(use, r_j * _rowdot(s_j, q), torch.zeros_like(r_j))
+        alpha[j] = a_j
+        q = q - a_j[:, None] * y_j
+    q = q * gamma[:, None]
+    for j in reversed(range(m)):
+        slot = (head - 1 - j) % m
+        use = (j < hist)
+        s_j = S[slot, all_rows]
+        y_j = Y[slot, all_rows]
+        r_j = rho[slot, all_rows]
+        b_j = r_j * _rowdot(y_j, q)
+        q = q + torch.where(use, alpha[j] - b_j, torch.zeros_like(b_j))[:, None] * s_j
+    return q
+
+
+def _device_direction(S, Y, rho, head, hist, gamma, g):
+    """-H g for every row: grape_lbfgs_direction (csrc/grape_lbfgs.hip), enqueued on torch's
+    current stream so it stays ordered with the surrounding torch ops."""
+    import ctypes
+
+    from . import _capi
+    m, R, n = S.shape
+    D = torch.empty_like(g)
+    ptrs = [ctypes.c_void_p(t.data_ptr()) for t in (S, Y, rho, head, hist, gamma, g, D)]
+    assert all(t.is_contiguous() for t in (S, Y, rho, head, hist, gamma, g))
+    assert head.dtype == hist.dtype == torch.int64
+    stream = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+    _capi.check(_capi.lib().grape_lbfgs_direction(R, n, m, *ptrs, stream))
+    return D
+
+
 def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.Tensor, *, m: int = 10,
                   iterations: int = 1000, g_tol: float = 1e-8, f_abstol: float = 0.0, f_reltol: float = 0.0,
                   x_abstol: float = 0.0, time_limit: float = float("nan"),
@@ -148,27 +195,10 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
         if not bool(active.any()):
             break
         # ---- two-loop recursion (ring buffer, newest first), batched over rows
-        q = -g.clone()
-        alpha = torch.zeros(m, R, dtype=dt, device=dev)
-        for j in range(m):
-            slot = (head - 1 - j) % m
-            use = (j < hist)
-            s_j = S[slot, all_rows]
-            y_j = Y[slot, all_rows]
-            r_j = rho[slot, all_rows]
-            a_j = torch.where(use, r_j * _rowdot(s_j, q), torch.zeros_like(r_j))
-            alpha[j] = a_j
-            q = q - a_j[:, None] * y_j
-        q = q * gamma[:, None]
-        for j in reversed(range(m)):
-            slot = (head - 1 - j) % m
-            use = (j < hist)
-            s_j = S[slot, all_rows]
-            y_j = Y[slot, all_rows]
-            r_j = rho[slot, all_rows]
-            b_j = r_j * _rowdot(y_j, q)
-            q = q + torch.where(use, alpha[j] - b_j, torch.zeros_like(b_j))[:, None] * s_j
-        D = q
+        if X.is_cuda and not _TORCH_TWO_LOOP:  # one launch: csrc/grape_lbfgs.hip
+            D = _device_direction(S, Y, rho, head, hist, gamma, g)
+        else:
+            D = _torch_direction(S, Y, rho, head, hist, gamma, g)
         dphi0 = _rowdot(g, D)
         bad = ~(dphi0 < 0) & active           # not a descent direction: restart from -g
         if bool(bad.any()):

@@ -93,3 +93,26 @@ def test_optimize_sweep_single_gpu():
     cost, rid, owner, xb, res = optimize_sweep(fp, params, 8, lambda r: P.random_x(100, 1000 + r, small=True))
     assert owner == 0 and cost == float(torch.min(res.minimum)) and rid == int(torch.argmin(res.minimum))
     assert torch.equal(xb, res.minimizer[rid])
+
+
+def test_device_lbfgs_direction_matches_torch_two_loop():
+    """grape_lbfgs_direction (one launch) against the batched torch two-loop recursion:
+    ragged histories (0..m pairs), wrapped ring-buffer heads, n not a multiple of 256."""
+    import torch
+    from robustgrape_amd.optimize import _device_direction, _torch_direction
+    gen = torch.Generator().manual_seed(3)
+    m, R, n = 10, 37, 513
+    S = torch.randn(m, R, n, generator=gen, dtype=torch.float64)
+    Y = S + 0.3 * torch.randn(m, R, n, generator=gen, dtype=torch.float64)
+    rho = 1.0 / (S * Y).sum(-1)
+    head = torch.randint(0, m, (R,), generator=gen)
+    hist = torch.randint(0, m + 1, (R,), generator=gen)
+    hist[0], hist[1] = 0, m
+    gamma = torch.rand(R, generator=gen, dtype=torch.float64) + 0.5
+    g = torch.randn(R, n, generator=gen, dtype=torch.float64)
+    ref = _torch_direction(S, Y, rho, head, hist, gamma, g)
+    dev = [t.cuda() for t in (S, Y, rho, head, hist, gamma, g)]
+    out = _device_direction(*dev).cpu()
+    assert torch.equal(out[0], -gamma[0] * g[0])  # empty history: steepest descent, scaled
+    err = (out - ref).abs().max() / ref.abs().max()
+    assert err <= 1e-12, float(err)
