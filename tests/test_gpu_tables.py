@@ -160,3 +160,44 @@ def test_closure_error_sources_with_xadd_dependent_h0_are_refused():
     fp = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, x, xa, e: e * Hz)]))
     with pytest.raises(NotImplementedError):
         calculate_fidelity_and_derivatives(fp, np.concatenate([np.zeros(5), [0.3, 0.2]]))
+
+
+@pytest.mark.parametrize("d", list(range(2, 13)))
+def test_every_dimension_with_errors_through_tables(d):
+    """The operator-basis random problems of test_gpu_dims (two controls, cis target, two
+    error sources) handed over as plain closures: the table path against the live oracle."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives, get_plan
+    from tests.test_gpu_dims import random_problem
+    nt = 7
+    fp = random_problem(d, nt, 2, False)
+    rng = np.random.default_rng(d + 77)
+    x = np.concatenate([rng.uniform(-1, 1, size=2 * nt), [rng.uniform(0, 2 * np.pi)]])
+    F0, g0, e0, ed0 = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, e, ed = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0)
+    _assert_err(1, e, ed, e0, ed0)
+    assert get_plan(fp, 2, 0, 1).tables
+
+
+def test_table_plan_chunks_batches_and_refuses_the_operator_entry_points():
+    """nbatch > max_batch runs in chunks (bitwise equal to single calls); a table plan
+    refuses grape_fidelity_grad / grape_unitary_derivs loudly."""
+    from robustgrape_amd import GrapePlan, calculate_fidelity_and_derivatives
+    from robustgrape_amd._capi import GrapeError
+    fp = P.sym_problem(20, errors=("amp",), device=False)
+    X = np.stack([P.random_x(20, s) for s in range(7)])
+    plan = GrapePlan(fp, 1, max_batch=3)
+    F, Fdx, d2, d2dx = plan.fidelity_grad(X)
+    for b in (0, 4, 6):
+        Fs, gs, es, eds = calculate_fidelity_and_derivatives(fp, X[b])
+        assert Fs == F[b] and np.array_equal(gs, Fdx[b]) and np.array_equal(es, d2[b])
+        assert np.array_equal(eds, d2dx[b])
+    with pytest.raises(GrapeError):
+        plan.unitary_derivs(X[0])
+    from robustgrape_amd import _capi
+    F1, G1 = np.empty(1), np.empty((1, 21))
+    with pytest.raises(GrapeError):
+        _capi.check(_capi.lib().grape_fidelity_grad(plan.handle, 1, _capi.dptr(X[:1].copy()), _capi.dptr(F1),
+                                                    _capi.dptr(G1), None, None))
+    plan.close()
