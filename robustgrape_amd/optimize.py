@@ -200,12 +200,12 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
         else:
             D = _torch_direction(S, Y, rho, head, hist, gamma, g)
         dphi0 = _rowdot(g, D)
-        bad = ~(dphi0 < 0) & active           # not a descent direction: restart from -g
-        if bool(bad.any()):
-            D[bad] = -g[bad]
-            dphi0 = torch.where(bad, _rowdot(g, D), dphi0)
-            hist = torch.where(bad, torch.zeros_like(hist), hist)
-            gamma = torch.where(bad, torch.ones_like(gamma), gamma)
+        # not a descent direction: restart from -g (masked, so no host sync)
+        bad = ~(dphi0 < 0) & active
+        D = torch.where(bad[:, None], -g, D)
+        dphi0 = torch.where(bad, _rowdot(g, D), dphi0)
+        hist = torch.where(bad, torch.zeros_like(hist), hist)
+        gamma = torch.where(bad, torch.ones_like(gamma), gamma)
         # ---- strong-Wolfe line search, all active rows in lock step
         f0 = f.clone()
         phase = torch.where(active, torch.zeros_like(iters), torch.full_like(iters, 2))  # 0 bracket 1 zoom 2 done
@@ -218,10 +218,9 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
         accepted = torch.zeros(R, dtype=torch.bool, device=dev)
         first = torch.ones(R, dtype=torch.bool, device=dev)
         for _ in range(MAX_LS_ROUNDS):
-            todo = phase < 2
-            if not bool(todo.any()):
+            rows = torch.nonzero(phase < 2).flatten()  # the round's one host sync
+            if rows.numel() == 0:
                 break
-            rows = torch.nonzero(todo).flatten()
             a = a_cur[rows]
             Xt = X[rows] + a[:, None] * D[rows]
             ft, gt = fun(Xt, rows)
@@ -279,11 +278,9 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
             # the best Armijo point so far is kept as a fallback
             better = armijo & (ft < fn[rows])
             keep = acc | better
-            if bool(keep.any()):
-                kr = rows[keep]
-                Xn[kr] = Xt[keep]
-                fn[kr] = ft[keep]
-                gn[kr] = gt[keep]
+            Xn[rows] = torch.where(keep[:, None], Xt, Xn[rows])
+            fn[rows] = torch.where(keep, ft, fn[rows])
+            gn[rows] = torch.where(keep[:, None], gt, gn[rows])
             accepted[rows[acc]] = True
             # next trial step
             zoom_now = newph == 1
@@ -309,15 +306,14 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
         y = gn - g
         sy = _rowdot(s, y)
         upd = step & (sy > 0)
-        if bool(upd.any()):
-            ur = torch.nonzero(upd).flatten()
-            slot = head[ur]
-            S[slot, ur] = s[ur]
-            Y[slot, ur] = y[ur]
-            rho[slot, ur] = 1.0 / sy[ur]
-            head[ur] = (head[ur] + 1) % m
-            hist[ur] = torch.clamp(hist[ur] + 1, max=m)
-            gamma[ur] = sy[ur] / _rowdot(y[ur], y[ur])
+        # masked ring-buffer update of every row (no host sync; rows without an update keep theirs)
+        slot = head
+        S[slot, all_rows] = torch.where(upd[:, None], s, S[slot, all_rows])
+        Y[slot, all_rows] = torch.where(upd[:, None], y, Y[slot, all_rows])
+        rho[slot, all_rows] = torch.where(upd, 1.0 / sy, rho[slot, all_rows])
+        head = torch.where(upd, (head + 1) % m, head)
+        hist = torch.where(upd, torch.clamp(hist + 1, max=m), hist)
+        gamma = torch.where(upd, sy / _rowdot(y, y), gamma)
         fold = f.clone()
         X = torch.where(step[:, None], Xn, X)
         f = torch.where(step, fn, f)
