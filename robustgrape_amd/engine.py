@@ -55,8 +55,9 @@ class GrapePlan:
         return _capi.lib().grape_plan_stream(self.handle)
 
     def set_stream(self, stream_ptr: int | None):
-        """Enqueue on the caller's hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
-        None restores the plan's own stream."""
+        """Enqueue on the caller's hipStream_t (e.g. a torch.cuda.Stream's cuda_stream);
+        None / 0 selects the plan's own stream -- so torch's default (null) stream cannot be
+        joined this way: use a side stream and wait_stream (optimize.RobustCost does)."""
         _capi.check(_capi.lib().grape_plan_set_stream(self.handle, ctypes.c_void_p(stream_ptr or None)))
 
     def fidelity_grad(self, X):
