@@ -121,7 +121,8 @@ def _assert_err(nx_add, d2, d2dx, ref_d2, ref_d2dx):
     assert np.max(np.abs(d2 - ref_d2)) <= T3 * np.max(np.abs(ref_d2)) + T3_ABS, (d2, ref_d2)
     err = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain]))
     assert err <= T3 * np.max(np.abs(ref_d2dx[:nmain])) + T3_ABS, err
-    assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
+    if nx_add:
+        assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
 
 
 @pytest.mark.parametrize("name,builder", [
@@ -201,3 +202,29 @@ def test_table_plan_chunks_batches_and_refuses_the_operator_entry_points():
         _capi.check(_capi.lib().grape_fidelity_grad(plan.handle, 1, _capi.dptr(X[:1].copy()), _capi.dptr(F1),
                                                     _capi.dptr(G1), None, None))
     plan.close()
+
+
+@pytest.mark.parametrize("nerr", [0, 1])
+def test_closure_without_additional_parameters(nerr):
+    """nb_additional_param = 0 (no x_add, one target slot) with and without an error source."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    from robustgrape_amd.types import ErrorSource, FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    d, nt = 4, 12
+    rng = np.random.default_rng(11)
+
+    def herm():
+        G = rng.normal(size=(d, d)) + 1j * rng.normal(size=(d, d))
+        return (G + G.conj().T) / 4
+    Hd, H1, H2, He = herm(), herm(), herm(), herm()
+    Q, _ = np.linalg.qr(rng.normal(size=(d, d)) + 1j * rng.normal(size=(d, d)))
+    errs = [ErrorSource(lambda t, x, xa, e: e * np.cos(x[0]) * He)] if nerr else []
+    up = UnitaryRobustGRAPEProblem(t0=2.0, ntimes=nt, ndim=d, nb_additional_param=0, error_sources=errs,
+                                   H0=lambda t, x, xa: Hd + x[0] * H1 + np.sin(x[1]) * H2)
+    fp = FidelityRobustGRAPEProblem(up, np.diag([1.0, 1.0, 0.5, 0.0]), lambda xa: Q)
+    x = rng.uniform(-1, 1, size=2 * nt)
+    F0, g0, e0, ed0 = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, e, ed = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0)
+    if nerr:
+        _assert_err(0, e, ed, e0, ed0)
