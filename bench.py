@@ -95,6 +95,20 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
     return None
 
 
+def _host_cpu():
+    """CPU model and logical CPU count of the host (SURVEY.md 8d asks for both)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(seconds=15.0, fp=None, label="C2"):
     """Time the CPU restatement on a bounded sample of the same workload (rank 0, N = 1)."""
     try:
@@ -115,7 +129,8 @@ def cpu_baseline(seconds=15.0, fp=None, label="C2"):
         dt = time.perf_counter() - t
         return {"value": n / dt, "unit": "gradient-evals/s", "cores": 1, "kind": "port",
                 "sample": f"{n} sequential {label} evaluations (d=9, N_t=512) by the reference-faithful C++ "
-                          f"restatement oracle/cref (same exp/inv/product counts as the Julia code), 1 thread"}
+                          f"restatement oracle/cref (same exp/inv/product counts as the Julia code), 1 thread",
+                "host_cpu": _host_cpu()}
     from oracle import grape_oracle as O
     from tests import problems as P
     fp = P.full9_problem(NT, device=False)
