@@ -2,18 +2,21 @@
 
 One step = one fidelity+gradient evaluation of every restart this rank owns
 (SURVEY.md 8d C2 problem; restarts r with x_main = 2pi*0.001*U, theta = 2pi*U,
-seed 1000+r as config C4), inputs resident in HBM. After the K timed steps, still
-inside the timed region, the sweep's exchange (robustgrape_amd/sweep.py): one
-all_gather of (best F, restart id) over RCCL and a broadcast of the winning x,
-when N > 1.  Weak scaling: every rank owns --batch restarts.
+seed 1000+r as config C4), inputs resident in HBM, evaluated in device passes of
+--chunk restarts.  After the K timed steps, still inside the timed region, the
+sweep's exchange (robustgrape_amd/sweep.py): one all_gather of (best F, restart id)
+over RCCL and a broadcast of the winning x, when N > 1.  Weak scaling: every rank
+owns --batch restarts.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--chunk C]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
-``roofline`` for the dominant kernel (k_expm_grad or k_expm, per-launch HIP-event
-time on the plan's stream) and ``cpu_baseline`` (the oracle's CPU restatement timed on a
-bounded sample on this host, rank 0, N = 1 only).
+``roofline`` for the dominant kernel (per-launch HIP-event time on the plan's
+stream), ``host_path`` (the drop-in grape_fidelity_grad with host arrays, PCIe
+included) and ``single_eval`` (nbatch = 1, as Optim's loop calls the reference),
+``cpu_baseline`` (the C++ port, 1 thread) and ``cpu_baseline_allcores`` (the port
+over restarts on the job's CPU share), all on rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -76,12 +79,13 @@ def flops_expm(d, m=5, s=0):
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
+PMC_SUMMARY_C3 = os.path.join(ROOT, "profiles", "pmc_c3_latest.json")
 
 
 def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
     """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_profile.sh:
     separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), if it was
-    recorded at this batch size; else None."""
+    recorded at this launch size (evaluations per device pass); else None."""
     try:
         with open(path) as fh:
             js = json.load(fh)
@@ -146,6 +150,70 @@ def cpu_baseline(seconds=15.0, fp=None, label="C2"):
             "sample": f"{n} sequential C2 evaluations by the numpy restatement oracle/grape_oracle.py, 1 thread"}
 
 
+def cpu_baseline_allcores(seconds=10.0, fp=None, label="C4"):
+    """SURVEY.md 8d C4 CPU baseline: the C++ port over restarts on every host core this job may
+    use (OpenMP; OMP_NUM_THREADS, the GPU box grants 16 CPUs per GPU), timed on a bounded sample."""
+    try:
+        from oracle.cref import cref
+        if not cref.available():
+            return None
+    except Exception:
+        return None
+    fp = fp or problem()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    batch = 4 * threads
+    X = restart_inputs(0, batch)
+    t = time.perf_counter()
+    n = 0
+    while True:
+        cref.fidelity_grad_batch(fp, X, threads)
+        n += batch
+        if time.perf_counter() - t > seconds:
+            break
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "gradient-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{n} {label} restart evaluations (d=9, N_t=512) by oracle/cref, OpenMP over restarts "
+                      f"on {threads} threads (the job's CPU share)", "host_cpu": _host_cpu()}
+
+
+def host_path(fp, nparam, X, reps, label):
+    """The drop-in entry the Julia shim calls: grape_fidelity_grad with HOST arrays in and out
+    (PCIe included), as GrapePlan.fidelity_grad.  Returns evals/s over `reps` calls."""
+    from robustgrape_amd.engine import GrapePlan
+    plan = GrapePlan(fp, nparam=nparam, device=0, max_batch=min(len(X), 4096))
+    plan.fidelity_grad(X)  # warm-up
+    t = time.perf_counter()
+    for _ in range(reps):
+        plan.fidelity_grad(X)
+    dt = time.perf_counter() - t
+    plan.close()
+    return {"value": reps * len(X) / dt, "unit": "gradient-evals/s", "batch": len(X), "calls": reps,
+            "ms_per_call": dt / reps * 1e3,
+            "note": f"{label}: grape_fidelity_grad, host x in / host F, F_dx out (pageable numpy buffers, "
+                    "PCIe-inclusive), synchronous per call"}
+
+
+def single_eval(fp, nparam, x, seconds=3.0):
+    """nbatch = 1 through the host-array path: how Optim's loop calls the reference
+    (FidelityCalculations.jl:177) -- one x per call, latency-bound."""
+    from robustgrape_amd.engine import GrapePlan
+    plan = GrapePlan(fp, nparam=nparam, device=0, max_batch=1)
+    X = x[None, :]
+    for _ in range(5):
+        plan.fidelity_grad(X)
+    lat = []
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        t = time.perf_counter()
+        plan.fidelity_grad(X)
+        lat.append(time.perf_counter() - t)
+    plan.close()
+    lat = np.array(lat)
+    return {"value": len(lat) / lat.sum(), "unit": "gradient-evals/s", "calls": len(lat),
+            "latency_ms_median": float(np.median(lat) * 1e3), "latency_ms_p90": float(np.percentile(lat, 90) * 1e3),
+            "note": "nbatch = 1, host arrays in and out (grape_fidelity_grad), one synchronous call per evaluation"}
+
+
 def _roofline(kname, flop_launch, ktimes, batch, pmc_path=PMC_SUMMARY):
     ms_k, n_k = ktimes[kname]
     per_launch_ms = ms_k / max(1, n_k)
@@ -156,14 +224,14 @@ def _roofline(kname, flop_launch, ktimes, batch, pmc_path=PMC_SUMMARY):
             "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch}
 
 
-def c2_report(args, B, world, value, elapsed, ktimes):
+def c2_report(args, B, L, world, value, elapsed, ktimes):
     # algorithmic flops per launch of the two exp-carrying kernels:
     # k_expm exps the nominal step propagators (B*NT items); k_expm_grad exps each
     # eps-variant (np=1 control; H0 does not read x_add, so no x_add variants) and
     # contracts it: Z_k = conj(Q_k) M'^T Q_{k-1}^T (2 complex products) + Re<Z, dE>.
     nvg = 1
-    flop_model = {"k_expm": B * NT * flops_expm(D),
-                  "k_expm_grad": B * NT * nvg * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)}
+    flop_model = {"k_expm": L * NT * flops_expm(D),
+                  "k_expm_grad": L * NT * nvg * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)}
     kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+∇), Rydberg CZ d=9 N_t=512, 1→8 GPU",
@@ -173,7 +241,7 @@ def c2_report(args, B, world, value, elapsed, ktimes):
         "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
                                "np=1, na=1, ne=0; restart sweep",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
-        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, B),
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, L),
                          pipe="fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"),
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
@@ -192,8 +260,8 @@ def c2_report(args, B, world, value, elapsed, ktimes):
     ms_s, n_s = ktimes.get("k_scan", (0.0, 0))
     if n_s:
         per_ms = ms_s / n_s
-        alg = B * NT * 2 * 16 * D * D
-        pmc = pmc_traffic("k_scan", B)
+        alg = L * NT * 2 * 16 * D * D
+        pmc = pmc_traffic("k_scan", L)
         out["roofline_scan"] = {"bound": "hbm", "kernel": "k_scan", "per_launch_ms": per_ms,
                                 "algorithmic_bytes": alg, "achieved": alg / (per_ms * 1e-3) / 1e9,
                                 "traffic": pmc, "achieved_traffic": (pmc / (per_ms * 1e-3) / 1e9) if pmc else None,
@@ -202,14 +270,14 @@ def c2_report(args, B, world, value, elapsed, ktimes):
     return out
 
 
-def c3_report(args, B, world, value, elapsed, ktimes, ne):
+def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
     # k_expm exponentiates every stored variant of every step: nominal, x + eps, x + eps2,
     # and per error source err(eps), err(eps2), (x + eps2, err eps2) -> 3 + 3 ne (Pade 5);
     # the x_add variants are skipped (H0 does not read x_add: their differences are exactly 0)
     nv = 3 + 3 * ne
     # k_err_grad: one row group per (eval, chunk, error) walks the chunk, 8 complex d x d
     # products per (step, error) (grape_errpath.hpp header)
-    flop_model = {"k_expm": B * NT * nv * flops_expm(D), "k_err_grad": B * NT * ne * 8 * 8 * D ** 3}
+    flop_model = {"k_expm": L * NT * nv * flops_expm(D), "k_err_grad": L * NT * ne * 8 * 8 * D ** 3}
     kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+sensitivity+gradients), Rydberg CZ d=9 N_t=512, 4 error sources",
@@ -219,7 +287,7 @@ def c3_report(args, B, world, value, elapsed, ktimes, ne):
         "config": {"workload": "C3: Rydberg CZ d=9 + 4 error operators (Omega1, Omega2, delta1, delta2), N_t=512, "
                                "np=1, na=1; F, F_dx, F_d2err, F_d2err_dx",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
-        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, B),
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, L, PMC_SUMMARY_C3),
                          pipe="fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"),
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
@@ -231,14 +299,14 @@ def c3_report(args, B, world, value, elapsed, ktimes, ne):
     return out
 
 
-def c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam):
+def c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam):
     # C5 draws Pade m = 7 for every exponential (tests/golden/c5.npz pade_hist); per launch:
     # k_dexp: B*nt nominal exps; k_dgrad: per step 2 products (Q_{k-1} M'_c, Z_k) and, per
     # control, one eps-variant exp + the contraction; k_dscan: one product per step.
     fe = flops_expm(d, 7)
-    flop_model = {"k_dexp": B * nt * fe,
-                  "k_dgrad": B * nt * (2 * 8 * d ** 3 + nparam * (fe + 8 * d ** 2)),
-                  "k_dscan": B * nt * 8 * d ** 3}
+    flop_model = {"k_dexp": L * nt * fe,
+                  "k_dgrad": L * nt * (2 * 8 * d ** 3 + nparam * (fe + 8 * d ** 2)),
+                  "k_dscan": L * nt * 8 * d ** 3}
     kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+∇), synthetic d=64 N_t=1024 (SURVEY C5)",
@@ -247,7 +315,7 @@ def c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam):
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "C5: d=64 Hermitian Ginibre basis, N_t=1024, dt=0.5, np=2, na=0, ne=0",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
-        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, B, PMC_SUMMARY_C5),
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, L, PMC_SUMMARY_C5),
                          pipe="fp64 MFMA v_mfma_f64_16x16x4_f64"),
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
@@ -308,13 +376,18 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
-                    help="restarts per GPU (one device pass each step); default 4096 (c2), 256 (c3), 4 (c5)")
+                    help="restarts per GPU per step; default 65536 (c2), 4096 (c3), 16 (c5)")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="evaluations per device pass (the plan's workspace; larger steps are chunked "
+                         "by the C side); default 16384 (c2), 2048 (c3), 16 (c5)")
     ap.add_argument("--workload", choices=("c2", "c3", "c5", "c4opt"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
                          "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
                          "batched L-BFGS (one step = one iteration of every restart)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-paths", action="store_true",
+                    help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
 
@@ -342,11 +415,13 @@ def main():
     else:
         fp, nparam, d, nt, inputs = problem(), 1, D, NT, restart_inputs
     ne = len(fp.unitary_problem.error_sources)
-    # C2: 4 096 restarts per GPU (measured: 1 024 -> 614k, 2 048 -> 673k, 4 096 -> 707k,
-    # 8 192 -> 729k evals/s on one box)
-    B = args.batch or (4 if c5 else 256 if c3 else 4096)
+    # One step = B restarts per GPU, evaluated in device passes of `chunk` (measured C2 passes:
+    # 1 024 -> 614k, 2 048 -> 673k, 4 096 -> 707k, 8 192 -> 729k evals/s).  B is
+    # sized so that the driver's 20 steps last > 2 s (its GPU-busy sampler must see them).
+    B = args.batch or (16 if c5 else 4096 if c3 else 65536)
+    chunk = args.chunk or (16 if c5 else 2048 if c3 else 16384)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
-    plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=count)
+    plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=min(count, chunk))
     X = torch.from_numpy(inputs(first, count)).to(dev)
     F = torch.empty(count, dtype=torch.float64, device=dev)
     Fdx = torch.empty(count, X.shape[1], dtype=torch.float64, device=dev)
@@ -393,18 +468,37 @@ def main():
     value = evals / elapsed
     ktimes = plan.kernel_times()
     if rank == 0:
+        L = min(count, chunk)
         if c5:
-            out = c5_report(args, B, world, value, elapsed, ktimes, d, nt, nparam)
+            out = c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam)
         elif c3:
-            out = c3_report(args, B, world, value, elapsed, ktimes, ne)
+            out = c3_report(args, B, L, world, value, elapsed, ktimes, ne)
         else:
-            out = c2_report(args, B, world, value, elapsed, ktimes)
+            out = c2_report(args, B, L, world, value, elapsed, ktimes)
         if best is not None:
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
+        out["config"]["evals_per_device_pass"] = min(count, chunk)
+    plan.close()
+    if rank == 0:
+        if world == 1 and not args.no_host_paths:
+            # the drop-in path as the reference's callers use it (host arrays, SURVEY.md 8d's
+            # metric definition): a 4 096-restart batch per call, and single evaluations
+            Xh = inputs(0, min(4096, B))
+            out["host_path"] = host_path(fp, nparam, Xh, reps=3 if c5 else 10, label=args.workload.upper())
+            out["single_eval"] = single_eval(fp, nparam, Xh[0])
         if world == 1 and not args.no_cpu_baseline and not c5:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, fp if c3 else None, "C3" if c3 else "C2")
+            if not c3:
+                allc = cpu_baseline_allcores(args.cpu_seconds * 2 / 3, fp, "C4")
+                if allc is not None:
+                    out["cpu_baseline_allcores"] = allc
+            cb = out["cpu_baseline"]["value"]
+            out["vs_cpu"] = {"device_value": value / cb,
+                             "host_path": out["host_path"]["value"] / cb if "host_path" in out else None,
+                             "single_eval": out["single_eval"]["value"] / cb if "single_eval" in out else None,
+                             "device_value_vs_allcores": (value / out["cpu_baseline_allcores"]["value"]
+                                                          if "cpu_baseline_allcores" in out else None)}
         print(json.dumps(out), flush=True)
-    plan.close()
     if world > 1:
         dist.destroy_process_group()
 

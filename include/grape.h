@@ -246,6 +246,13 @@ int grape_unitary_derivs(grape_plan *plan, const double *x,
 int grape_interaction_error_operators(grape_plan *plan, const double *x, double *O);
 
 /*
+ * The same operators written into DEVICE memory d_O (same layout, d*d*ntimes*nerr
+ * complex), for callers that post-process them on the GPU (the fidelity-response
+ * rows, src/FidelityCalculations.jl:246-343).  x is a host vector.  Synchronous.
+ */
+int grape_interaction_error_operators_device(grape_plan *plan, const double *x, double *d_O);
+
+/*
  * Time-resolved expectation values of the error generators for ONE control
  * vector, replacing calculate_expectation_values (src/FidelityCalculations.jl:368-390):
  *   ev (ntimes, nerr) real column-major, ev[k, e] = Re(dt tr(P0 sum_{j<=k} O_j,e)) / tr(P0).

@@ -18,7 +18,7 @@ def build(force=False):
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) > max(os.path.getmtime(SRC), os.path.getmtime(hdr)):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = ["g++", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared",
+    cmd = ["g++", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared", "-fopenmp",
            "-I" + os.path.join(ROOT, "include"), SRC, "-o", OUT + ".tmp"]
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)

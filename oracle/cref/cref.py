@@ -23,6 +23,8 @@ def lib():
         dp = ctypes.POINTER(ctypes.c_double)
         L.grape_cref_fidelity_grad.argtypes = [ctypes.c_void_p, dp, dp, dp, dp, dp]
         L.grape_cref_fidelity_grad.restype = ctypes.c_int
+        L.grape_cref_fidelity_grad_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp]
+        L.grape_cref_fidelity_grad_batch.restype = ctypes.c_int
         L.grape_cref_unitary_derivs.argtypes = [ctypes.c_void_p, dp, dp, dp, dp, dp, dp, dp]
         L.grape_cref_unitary_derivs.restype = ctypes.c_int
         L.grape_cref_expm.argtypes = [ctypes.c_int, dp, dp]
@@ -55,6 +57,25 @@ def fidelity_grad(fp, x):
     if rc != 0:
         raise RuntimeError(f"grape_cref_fidelity_grad returned {rc}")
     return float(F[0]), Fdx, d2[:ne], d2dx[:ne].T.copy()
+
+
+def fidelity_grad_batch(fp, X, nthreads):
+    """Independent evaluations of the rows of X on `nthreads` OpenMP threads: (F (nb,), F_dx (nb, n_x))."""
+    up = fp.unitary_problem
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    nb, nx = X.shape
+    nparam = (nx - up.nb_additional_param) // up.ntimes
+    buf = _desc(fp, nparam)
+    ne = len(up.error_sources)
+    F = np.zeros(nb)
+    Fdx = np.zeros((nb, nx))
+    d2 = np.zeros((nb, max(ne, 1)))
+    d2dx = np.zeros((nb, max(ne, 1), nx))
+    rc = lib().grape_cref_fidelity_grad_batch(ctypes.addressof(buf.desc), nb, int(nthreads), _p(X), _p(F), _p(Fdx),
+                                             _p(d2), _p(d2dx))
+    if rc != 0:
+        raise RuntimeError(f"grape_cref_fidelity_grad_batch returned {rc}")
+    return F, Fdx
 
 
 def unitary_derivs(fp, x):

@@ -151,7 +151,7 @@ void getrs(const Mat &LU, const std::vector<int> &ipiv, Mat &B) {
         }
     }
 }
-bool g_singular = false;
+thread_local bool g_singular = false;
 Mat gesv(Mat A, Mat B) {
     std::vector<int> ipiv;
     if (!getrf(A, ipiv)) g_singular = true;
@@ -260,7 +260,7 @@ const double P13[] = {64764752532480000.0, 32382376266240000.0, 7771770303897600
                       1187353796428800.0, 129060195264000.0, 10559470521600.0,
                       670442572800.0, 33522128640.0, 1323241920.0,
                       40840800.0, 960960.0, 16380.0, 182.0, 1.0};
-long g_exp_calls = 0;
+thread_local long g_exp_calls = 0;
 
 Mat julia_exp(Mat A) {
     ++g_exp_calls;
@@ -609,6 +609,27 @@ int grape_cref_fidelity_grad(const grape_desc *d, const double *x, double *F_out
         }
     }
     return g_singular ? GRAPE_ERR_SINGULAR : GRAPE_OK;
+}
+
+// SURVEY.md 8d C4 CPU baseline: nb independent evaluations (restarts) spread over
+// nthreads OpenMP threads (the reference itself is single-threaded; this is the
+// "all host cores" form of the port).  Per-eval outputs as grape_cref_fidelity_grad,
+// eval b's arrays at b * (n_x | ne | ne * n_x).  Returns the first nonzero status.
+int grape_cref_fidelity_grad_batch(const grape_desc *d, int nb, int nthreads, const double *x, double *F,
+                                   double *F_dx, double *F_d2err, double *F_d2err_dx) {
+    const int nx = d->nparam * d->ntimes + d->nadd, ne = d->nerr;
+    int status = GRAPE_OK;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int b = 0; b < nb; ++b) {
+        const int rc = grape_cref_fidelity_grad(d, x + (size_t)b * nx, F + b, F_dx + (size_t)b * nx,
+                                                ne ? F_d2err + (size_t)b * ne : nullptr,
+                                                ne ? F_d2err_dx + (size_t)b * ne * nx : nullptr);
+        if (rc) {
+#pragma omp critical
+            if (!status) status = rc;
+        }
+    }
+    return status;
 }
 
 // src/UnitaryCalculations.jl:154 outputs, column-major, reference shapes

@@ -21,7 +21,8 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_plan_destroy", "grape_plan_stream", "grape_plan_set_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times",
-            "grape_interaction_error_operators", "grape_expectation_values", "grape_fidelity_grad_tables",
+            "grape_interaction_error_operators", "grape_interaction_error_operators_device",
+            "grape_expectation_values", "grape_fidelity_grad_tables",
             "grape_lbfgs_direction"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
@@ -74,6 +75,8 @@ def lib():
         L.grape_expm_batch.restype = ctypes.c_int
         L.grape_interaction_error_operators.argtypes = [vp, dp, dp]
         L.grape_interaction_error_operators.restype = ctypes.c_int
+        L.grape_interaction_error_operators_device.argtypes = [vp, dp, vp]
+        L.grape_interaction_error_operators_device.restype = ctypes.c_int
         L.grape_expectation_values.argtypes = [vp, dp, dp]
         L.grape_expectation_values.restype = ctypes.c_int
         L.grape_plan_set_profiling.argtypes = [vp, ctypes.c_int]

@@ -12,32 +12,21 @@
 """
 from __future__ import annotations
 
+import ctypes
 import math
-import threading
 
 import numpy as np
 import torch
 
 from . import _capi
-from .engine import get_plan
-from .operators import OperatorBasisTarget, Term
+from .engine import fidelity_wrapper, get_plan
 from .types import FidelityRobustGRAPEProblem, split_x
-
-_lock = threading.Lock()
-_fp_for_up: dict = {}
-
 
 def _plan(fp_or_up, x, device):
     if isinstance(fp_or_up, FidelityRobustGRAPEProblem):
         fp = fp_or_up
     else:  # a UnitaryRobustGRAPEProblem: the descriptor needs a projector and target (unused here)
-        up = fp_or_up
-        with _lock:
-            fp = _fp_for_up.get(id(up))
-            if fp is None or fp.unitary_problem is not up:
-                fp = FidelityRobustGRAPEProblem(up, np.eye(up.ndim),
-                                                OperatorBasisTarget([Term(np.eye(up.ndim, dtype=np.complex128))]))
-                _fp_for_up[id(up)] = fp
+        fp = fidelity_wrapper(fp_or_up)
     _, _, nparam = split_x(fp.unitary_problem, x)
     return fp, get_plan(fp, nparam, device, max_batch=1)
 
@@ -49,7 +38,8 @@ def calculate_interaction_error_operators(unitary_problem, x, device: int = 0) -
     up = fp.unitary_problem
     O = np.zeros((up.ndim, up.ndim, up.ntimes, len(up.error_sources)), dtype=np.complex128, order="F")
     if O.size:
-        _capi.check(_capi.lib().grape_interaction_error_operators(plan.handle, _capi.dptr(x), _capi.dptr(O)))
+        with plan.lock:
+            _capi.check(_capi.lib().grape_interaction_error_operators(plan.handle, _capi.dptr(x), _capi.dptr(O)))
     return O
 
 
@@ -60,14 +50,26 @@ def calculate_expectation_values(fidelity_problem: FidelityRobustGRAPEProblem, x
     up = fp.unitary_problem
     ev = np.zeros((up.ntimes, len(up.error_sources)), dtype=np.float64, order="F")
     if ev.size:
-        _capi.check(_capi.lib().grape_expectation_values(plan.handle, _capi.dptr(x), _capi.dptr(ev)))
+        with plan.lock:
+            _capi.check(_capi.lib().grape_expectation_values(plan.handle, _capi.dptr(x), _capi.dptr(ev)))
     return ev
 
 
 def _device_operators(fp, x, device):
-    """Interaction operators as a (nerr, ntimes, d, d) complex128 tensor on the device."""
-    O = calculate_interaction_error_operators(fp.unitary_problem, x, device)
-    return torch.from_numpy(np.ascontiguousarray(O.transpose(3, 2, 0, 1))).to(torch.device("cuda", device))
+    """Interaction operators as a (nerr, ntimes, d, d) complex128 tensor, written by the HIP
+    kernels straight into device memory (grape_interaction_error_operators_device): they never
+    visit the host."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    fp, plan = _plan(fp, x, device)
+    up = fp.unitary_problem
+    d, nt, ne = up.ndim, up.ntimes, len(up.error_sources)
+    # the reference's column-major (d, d, nt, ne) tensor is the C-order (ne, nt, d_col, d_row) one
+    O = torch.empty(ne, nt, d, d, dtype=torch.complex128, device=torch.device("cuda", device))
+    torch.cuda.synchronize(O.device)
+    with plan.lock:
+        _capi.check(_capi.lib().grape_interaction_error_operators_device(
+            plan.handle, _capi.dptr(x), ctypes.c_void_p(O.data_ptr())))
+    return O.transpose(-1, -2)
 
 
 def _projector_parts(fp, dev):

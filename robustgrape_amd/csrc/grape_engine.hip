@@ -52,8 +52,7 @@ int fail(int code, const std::string &msg) {
     } while (0)
 
 constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow;
-constexpr int kMaxSlices = 4;                  // batch slices per call (enqueue_call)
-constexpr int kCtrlInts = 4 + 2 * kMaxSlices;  // [0..1] single-eval counters, [2] status, per-slice counters
+constexpr int kCtrlInts = 8;  // [0..1] single-eval counters, [2] status, [4..5] pipeline overflow counters
 using grape_host::KMark;
 using grape_host::launch_pipeline;
 using grape_host::launch_expm_raw;
@@ -111,10 +110,7 @@ struct grape_plan {
     int device = 0;
     hipStream_t stream = nullptr;      // where work is enqueued (own_stream or the caller's)
     hipStream_t own_stream = nullptr;
-    hipStream_t aux_stream = nullptr;  // second stream for batch slices (enqueue_call)
     hipStream_t cur_stream = nullptr;  // stream of the launch being enqueued (profiling marks)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int nsplit = 1, split_min = 1 << 30;  // slices per call and the batch size from which to slice
     int *h_status = nullptr;           // pinned copy of the device status word
     DevProblem P{};
     int max_batch = 0;
@@ -183,9 +179,6 @@ static void free_plan(grape_plan *p) {
         (void)hipEventDestroy(pe.b);
     }
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
-    if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
-    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
-    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
 }
@@ -203,6 +196,34 @@ static int validate_terms(const grape_term *t, int n, int n_ops, int np, int na,
             return fail(GRAPE_ERR_INVALID, std::string(what) + ": target terms may only use x_add");
         if (!target && t[k].func == 4)
             return fail(GRAPE_ERR_INVALID, std::string(what) + ": cis coefficients only in target terms");
+    }
+    return GRAPE_OK;
+}
+
+// The engines take C_k^-1 = C_k^dagger (unitary step propagators) and skip balancing,
+// both valid for Hermitian H only.  A term c(x) * OP keeps H Hermitian for every x when
+// its function is real-valued and scale * OP is Hermitian; anything else (e.g. a
+// -i Gamma/2 decay term) is refused rather than computed wrongly.
+static int check_hermitian_terms(const grape_desc *desc, const grape_term *t, int n, const char *what) {
+    const int D = desc->ndim;
+    for (int k = 0; k < n; ++k) {
+        if (t[k].func == GRAPE_FN_CIS)
+            return fail(GRAPE_ERR_UNSUPPORTED, std::string(what) + ": complex-valued coefficient (H must be Hermitian)");
+        const double *op = desc->ops + 2 * (size_t)t[k].op * D * D;
+        const double sr = t[k].scale_re, si = t[k].scale_im;
+        double mx = 0.0, dev = 0.0;
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j) {
+                const double *a = op + 2 * ((size_t)i + (size_t)j * D), *b = op + 2 * ((size_t)j + (size_t)i * D);
+                // (s a)_ij - conj((s a)_ji)
+                const double re = (sr * a[0] - si * a[1]) - (sr * b[0] - si * b[1]);
+                const double im = (sr * a[1] + si * a[0]) + (sr * b[1] + si * b[0]);
+                mx = std::max(mx, std::hypot(sr * a[0] - si * a[1], sr * a[1] + si * a[0]));
+                dev = std::max(dev, std::hypot(re, im));
+            }
+        if (dev > 1e-12 * std::max(mx, 1e-300))
+            return fail(GRAPE_ERR_UNSUPPORTED,
+                        std::string(what) + ": scale * operator is not Hermitian (non-unitary propagators are not supported)");
     }
     return GRAPE_OK;
 }
@@ -243,22 +264,8 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, do
     if (desc->nerr > 0)
         return fail(GRAPE_ERR_UNSUPPORTED, "dense engine (ndim > GRAPE_MAX_SMALL_DIM): error sources not supported");
     if (xadd_dep) return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 must not depend on x_add");
-    // Hermitian H0 (see grape_dense.hpp: the no-interchange solve relies on it)
-    for (int k = 0; k < desc->n_h0_terms; ++k) {
-        const grape_term &t = desc->h0_terms[k];
-        if (t.scale_im != 0.0 || t.func == GRAPE_FN_CIS)
-            return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 coefficients must be real");
-        const double *op = desc->ops + 2 * (size_t)t.op * D * D;
-        double mx = 0.0, dev = 0.0;
-        for (int i = 0; i < D; ++i)
-            for (int j = 0; j < D; ++j) {
-                const double *a = op + 2 * ((size_t)i + (size_t)j * D), *b = op + 2 * ((size_t)j + (size_t)i * D);
-                mx = std::max(mx, std::hypot(a[0], a[1]));
-                dev = std::max(dev, std::hypot(a[0] - b[0], a[1] + b[1]));
-            }
-        if (dev > 1e-12 * std::max(mx, 1e-300))
-            return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 operators must be Hermitian");
-    }
+    // Hermitian H0: checked for every engine in grape_plan_create (the dense no-interchange
+    // solve relies on it too, grape_dense.hpp)
     if (grape_dense::set_lds_limits() != hipSuccess) return fail(GRAPE_ERR_HIP, "cannot raise LDS limit (dense)");
     p->dense = true;
     grape_dense::DenseProblem &DP = p->DP;
@@ -360,6 +367,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                                  "error source")))
             return rc;
     }
+    if (!tables) {
+        if ((rc = check_hermitian_terms(desc, desc->h0_terms, desc->n_h0_terms, "H0"))) return rc;
+        if ((rc = check_hermitian_terms(desc, desc->err_terms, n_err_terms, "error source"))) return rc;
+    }
     // host tables: H0 is an opaque closure that may read x_add; with error sources the
     // caller guarantees it does not (like the operator-basis path, which refuses that case)
     bool xadd_dep = tables && desc->nadd > 0 && desc->nerr == 0;
@@ -459,8 +470,6 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             ncu = prop.multiProcessorCount;
     }
     P.scan_waves = p->max_batch >= 2 * ncu ? kScanNarrow : kScanWide;
-    P.pair = 0;
-    if (const char *pe = std::getenv("GRAPE_PAIR")) P.pair = std::atoi(pe) != 0;  // column-pair nominal exps
     if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {  // tuning override: 4 or 8
         const int wv = std::atoi(w);
         if (wv == kScanNarrow || wv == kScanWide) P.scan_waves = wv;
@@ -509,19 +518,6 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (!ok) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed"));
     if (hipMemset(p->d_ctrl, 0, kCtrlInts * sizeof(int)) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "memset failed"));
-    // batch slicing over two streams (enqueue_call): large launches only
-    if (hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess)
-        return bail(fail(GRAPE_ERR_HIP, "stream/event creation failed"));
-    // Measured on C2 (B = 1 024): 1 slice 596k, 2 slices 589k, 4 slices 572k evals/s -- the
-    // exp kernels already fill the CUs the scan leaves idle, so slicing is off by default.
-    p->nsplit = 1;
-    p->split_min = 2 * ncu;
-    if (const char *sp = std::getenv("GRAPE_SPLIT")) {  // tuning override: slices per call (1..kMaxSlices)
-        const int v = std::atoi(sp);
-        if (v >= 1 && v <= kMaxSlices) p->nsplit = v;
-    }
     if (hipMemcpy(p->d_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
     if (P.ne > 0 && !tables &&
@@ -559,13 +555,11 @@ int grape_plan_set_stream(grape_plan *plan, void *stream) {
     return GRAPE_OK;
 }
 
-// One launch sequence of `nb` evaluations on stream `st`.  `w0` is the first
-// workspace row it uses (slices of one call occupy disjoint rows) and `slot`
-// selects its private overflow counters, so slices may run concurrently on
-// different streams.  The caller copies the status word afterwards.
+// One launch sequence of `nb` evaluations on the plan's stream over workspace rows
+// [0, nb).  The caller copies the status word afterwards.
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
-                   double *d_Fd2dx, hipStream_t st = nullptr, size_t w0 = 0, int slot = 0) {
-    if (!st) st = p->stream;
+                   double *d_Fd2dx) {
+    hipStream_t st = p->stream;
     p->cur_stream = st;
     KMark mk;
     if (p->profiling) {
@@ -600,7 +594,6 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         return GRAPE_OK;
     }
     const DevProblem &P = p->P;
-    const size_t T = (size_t)P.D * P.D, nvg = (size_t)P.np + (P.xadd_dep ? P.na : 0);
     DevBatch B{};
     B.Fd2 = d_Fd2;
     B.Fd2dx = d_Fd2dx;
@@ -608,64 +601,40 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     B.x = d_x;
     B.F = d_F;
     B.Fdx = d_Fdx;
-    // workspace rows [w0, w0 + nb)
-    B.E = p->d_E + w0 * P.Nt * P.nv * T;
-    B.Q = p->d_Q + w0 * P.Nt * T;
-    B.Mc = p->d_Mc + w0 * P.nchunks * T;
-    B.part_add = p->d_part + w0 * P.Nt * std::max(P.na, 1);
-    B.tgt_part = p->d_tgt_part + w0 * std::max(P.na, 1);
-    B.overflow = p->d_ovf + w0 * P.Nt * P.nv;
+    B.E = p->d_E;
+    B.Q = p->d_Q;
+    B.Mc = p->d_Mc;
+    B.part_add = p->d_part;
+    B.tgt_part = p->d_tgt_part;
+    B.overflow = p->d_ovf;
     if (P.ne == 0) {
-        B.ovf2 = p->d_ovf2 + w0 * P.Nt * nvg;
-        B.ovf2_slots = p->d_ovf2_slots + w0 * P.Nt * nvg * T;
+        B.ovf2 = p->d_ovf2;
+        B.ovf2_slots = p->d_ovf2_slots;
     } else {
-        B.Carry = p->d_Carry + w0 * P.nchunks * T;
-        B.Ub = p->d_Ub + w0 * T;
-        B.Me = p->d_Me + w0 * P.ne * P.nchunks * 3 * T;
+        B.Carry = p->d_Carry;
+        B.Ub = p->d_Ub;
+        B.Me = p->d_Me;
     }
-    // ctrl: [2] status (sticky until grape_plan_synchronize reports it), per slot s:
-    // [4 + 2s] k_expm overflow count, [5 + 2s] k_expm_grad overflow count
-    int *cnt = p->d_ctrl + 4 + 2 * slot;
+    // ctrl: [2] status (sticky until grape_plan_synchronize reports it),
+    // [4] k_expm overflow count, [5] k_expm_grad overflow count
+    int *cnt = p->d_ctrl + 4;
     B.overflow_count = cnt;
     B.ovf2_count = cnt + 1;
     B.status = p->d_ctrl + 2;
     B.sink = p->d_sink;
     HIPCHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
     if (p->tables) {
-        B.Htab = p->d_Htab + w0 * P.Nt * P.nv * T;
-        B.U0tab = p->d_U0tab + w0 * (1 + P.na) * T;
+        B.Htab = p->d_Htab;
+        B.U0tab = p->d_U0tab;
     }
     HIPCHECK(dispatch_pipeline(P.D, P, B, st, mk));
     return GRAPE_OK;
 }
 
-// Enqueue one call's batch: on the small-d engine a large batch is cut into
-// slices alternating between the plan's stream and its auxiliary stream, so
-// the latency-bound scan of one slice overlaps the exponential kernels of the
-// next ("two streams").  Ends with the status word copied to
-// pinned memory on the plan's stream, after both streams joined.
+// Enqueue one call's batch, then copy the status word to pinned memory on the plan's stream.
 static int enqueue_call(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
                         double *d_Fd2dx) {
-    const int nx = p->P.nx, ne = p->P.ne;
-    int ns = 1;
-    if (!p->dense && p->aux_stream) ns = nb >= p->split_min ? p->nsplit : 1;
-    if (ns <= 1) {
-        if (int rc = enqueue(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx)) return rc;
-    } else {
-        HIPCHECK(hipEventRecord(p->ev_fork, p->stream));
-        HIPCHECK(hipStreamWaitEvent(p->aux_stream, p->ev_fork, 0));
-        const int per = (nb + ns - 1) / ns;
-        for (int s = 0, b0 = 0; b0 < nb; ++s, b0 += per) {
-            const int n = std::min(per, nb - b0);
-            hipStream_t st = (s & 1) ? p->aux_stream : p->stream;
-            int rc = enqueue(p, n, d_x + (size_t)b0 * nx, d_F + b0, d_Fdx + (size_t)b0 * nx,
-                             ne ? d_Fd2 + (size_t)b0 * ne : nullptr, ne ? d_Fd2dx + (size_t)b0 * ne * nx : nullptr, st,
-                             (size_t)b0, s);
-            if (rc) return rc;
-        }
-        HIPCHECK(hipEventRecord(p->ev_join, p->aux_stream));
-        HIPCHECK(hipStreamWaitEvent(p->stream, p->ev_join, 0));
-    }
+    if (int rc = enqueue(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx)) return rc;
     HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return GRAPE_OK;
 }
@@ -853,6 +822,20 @@ int grape_interaction_error_operators(grape_plan *p, const double *x, double *O)
     const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
     HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
     HIPCHECK(hipMemcpyAsync(O, p->ud_out, n * sizeof(cd), hipMemcpyDeviceToHost, p->stream));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    return grape_plan_synchronize(p);
+}
+
+int grape_interaction_error_operators_device(grape_plan *p, const double *x, double *d_O) {
+    if (!p || !x || !d_O) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, "interaction error operators: dense engine not supported");
+    if (p->P.ne == 0) return GRAPE_OK;
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = ud_alloc(p)) return rc;
+    if (int rc = ud_chain(p, x)) return rc;
+    const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
+    HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
+    HIPCHECK(hipMemcpyAsync(d_O, p->ud_out, n * sizeof(cd), hipMemcpyDeviceToDevice, p->stream));
     HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return grape_plan_synchronize(p);
 }

@@ -60,7 +60,6 @@ struct DevProblem {
     int xadd_dep;        // H0 depends on x_add -> x_add FD variants exist
     int L, nchunks;      // scan chunking
     int scan_waves;      // waves per k_scan / k_err_scan workgroup (4 or 8)
-    int pair;            // nominal exps in column-pair form (k_expm2, grape_pair.hpp)
     // variant layout (see grape_engine.hip: build_variants)
     int off_dx, off_dxa, off_dx2, off_err, err_stride;
     double dt, eps, eps2, inv_eps, inv_eps2sq, DD, Dtr;

@@ -7,7 +7,6 @@
 
 #include "grape.h"
 #include "grape_errpath.hpp"
-#include "grape_pair.hpp"
 
 namespace grape_host {
 
@@ -23,8 +22,6 @@ constexpr int kScanWide = 8, kScanNarrow = 4;
 
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
-template <int D>
-size_t expm2_lds() { return (size_t)grape::Geo2<D>::GPW * grape::Geo2<D>::GROUP_CD * sizeof(cd); }
 template <int D>
 size_t errscan_lds(int W) {
     return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 4 * grape::Geo<D>::TILE) * sizeof(cd);
@@ -60,11 +57,7 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     else if (!fused)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lds<D>(), st, P, B);
-    else if (P.pair) {
-        constexpr int GPW2 = grape::Geo2<D>::GPW;
-        hipLaunchKernelGGL(grape::k_expm2<D>, dim3((unsigned)((nexp + GPW2 - 1) / GPW2)), dim3(64), expm2_lds<D>(),
-                           st, P, B);
-    } else
+    else
         hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lds<D>(), st, P, B);
     mark(GRAPE_KERNEL_EXPM, 1);

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+from collections import OrderedDict
 
 import numpy as np
 
@@ -29,6 +30,7 @@ class GrapePlan:
         self.nx = self.nparam * self.up.ntimes + self.up.nb_additional_param
         self.nerr = len(self.up.error_sources)
         self.max_batch = int(max_batch)
+        self.lock = threading.Lock()  # one evaluation at a time (the plan's buffers are shared)
         # operator bases -> the fused device path; plain closures -> the host-table fallback
         self.tables = not has_operator_basis(fp)
         if self.tables:
@@ -122,27 +124,77 @@ class GrapePlan:
         _capi.check(_capi.lib().grape_plan_synchronize(self.handle))
 
 
+# Plan cache of the reference-shaped entry points (one plan per problem object, nparam and
+# device).  A plan owns HBM workspace for `max_batch` evaluations; larger batches are
+# chunked by the C side, so one plan serves every batch size: it is recreated larger only
+# up to PLAN_BATCH_CAP.  At most MAX_CACHED_PLANS plans live at once (least recently used
+# evicted and destroyed).  Evaluations on one plan are serialised by its lock, so cached
+# plans may be shared by threads.
+PLAN_BATCH_CAP = 256
+MAX_CACHED_PLANS = 8
 _cache_lock = threading.Lock()
-_plan_cache: dict = {}
+_plan_cache: "OrderedDict" = OrderedDict()
 
 
-def get_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 256) -> GrapePlan:
-    """Plans are cached per (problem object, nparam, device, max_batch)."""
-    key = (id(fp), nparam, device, max_batch)
+def get_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 1) -> GrapePlan:
+    """The cached plan of (problem object, nparam, device) holding at least
+    min(max_batch, PLAN_BATCH_CAP) evaluations of workspace."""
+    want = max(1, min(int(max_batch), PLAN_BATCH_CAP))
+    key = (id(fp), int(nparam), int(device))
     with _cache_lock:
         ent = _plan_cache.get(key)
-        if ent is not None and ent.fp is fp:
+        if ent is not None and ent.fp is fp and ent.max_batch >= want:
+            _plan_cache.move_to_end(key)
             return ent
-        plan = GrapePlan(fp, nparam, device, max_batch)
+        if ent is not None:
+            del _plan_cache[key]
+            with ent.lock:
+                ent.close()
+            if ent.fp is fp:
+                want = max(want, ent.max_batch)
+        plan = GrapePlan(fp, nparam, device, want)
         _plan_cache[key] = plan
+        while len(_plan_cache) > MAX_CACHED_PLANS:
+            _, old = _plan_cache.popitem(last=False)
+            with old.lock:
+                old.close()
         return plan
+
+
+def cached_plan_count() -> int:
+    with _cache_lock:
+        return len(_plan_cache)
 
 
 def clear_plans():
     with _cache_lock:
         for p in _plan_cache.values():
-            p.close()
+            with p.lock:
+                p.close()
         _plan_cache.clear()
+        _wrapped.clear()
+
+
+# UnitaryRobustGRAPEProblem -> a FidelityRobustGRAPEProblem around it (the descriptor needs
+# a projector and a target; neither enters the unitary-level outputs).  Small LRU.
+_wrapped: "OrderedDict" = OrderedDict()
+
+
+def fidelity_wrapper(unitary_problem) -> FidelityRobustGRAPEProblem:
+    from .operators import OperatorBasisTarget, Term, has_operator_basis_h
+    key = id(unitary_problem)
+    with _cache_lock:
+        fp = _wrapped.get(key)
+        if fp is not None and fp.unitary_problem is unitary_problem:
+            _wrapped.move_to_end(key)
+            return fp
+        eye = np.eye(unitary_problem.ndim, dtype=np.complex128)
+        target = OperatorBasisTarget([Term(eye)]) if has_operator_basis_h(unitary_problem) else (lambda xa: eye)
+        fp = FidelityRobustGRAPEProblem(unitary_problem, np.eye(unitary_problem.ndim), target)
+        _wrapped[key] = fp
+        while len(_wrapped) > MAX_CACHED_PLANS:
+            _wrapped.popitem(last=False)
+        return fp
 
 
 def calculate_fidelity_and_derivatives(fidelity_problem: FidelityRobustGRAPEProblem, x, device: int = 0):
@@ -157,14 +209,12 @@ def calculate_fidelity_and_derivatives(fidelity_problem: FidelityRobustGRAPEProb
     batched = x.ndim == 2
     X = x if batched else x[None, :]
     _, _, nparam = split_x(fidelity_problem.unitary_problem, X[0])
-    plan = get_plan(fidelity_problem, nparam, device, max_batch=min(256, max(1, X.shape[0])))
-    F, Fdx, Fd2, Fd2dx = plan.fidelity_grad(X)
+    plan = get_plan(fidelity_problem, nparam, device, max_batch=X.shape[0])
+    with plan.lock:
+        F, Fdx, Fd2, Fd2dx = plan.fidelity_grad(X)
     if batched:
         return F, Fdx, Fd2, Fd2dx
     return float(F[0]), Fdx[0], Fd2[0], Fd2dx[0]
-
-
-_unitary_fp: dict = {}
 
 
 def calculate_unitary_and_derivatives(unitary_problem, x, device: int = 0):
@@ -172,15 +222,8 @@ def calculate_unitary_and_derivatives(unitary_problem, x, device: int = 0):
 
     Returns (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add) with the reference's shapes
     (d,d), (d,d,np,N_t), (d,d,na), (d,d,ne), (d,d,np,N_t,ne), (d,d,na,ne)."""
-    from .operators import OperatorBasisTarget, Term
     x = np.asarray(x, dtype=np.float64)
     _, _, nparam = split_x(unitary_problem, x)
-    with _cache_lock:
-        fp = _unitary_fp.get(id(unitary_problem))
-        if fp is None or fp.unitary_problem is not unitary_problem:
-            # the descriptor needs a projector and a target; neither enters these outputs
-            eye = np.eye(unitary_problem.ndim, dtype=np.complex128)
-            fp = FidelityRobustGRAPEProblem(unitary_problem, np.eye(unitary_problem.ndim),
-                                            OperatorBasisTarget([Term(eye)]))
-            _unitary_fp[id(unitary_problem)] = fp
-    return get_plan(fp, nparam, device, max_batch=1).unitary_derivs(x)
+    plan = get_plan(fidelity_wrapper(unitary_problem), nparam, device, max_batch=1)
+    with plan.lock:
+        return plan.unitary_derivs(x)

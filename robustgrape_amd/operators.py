@@ -212,6 +212,12 @@ class DescriptorBuffers:
 GRAPE_DESC_HOST_TABLES = 1  # include/grape.h
 
 
+def has_operator_basis_h(up) -> bool:
+    """True when H0 and every error source of a UnitaryRobustGRAPEProblem are operator bases."""
+    return isinstance(up.H0, OperatorBasisHamiltonian) and all(
+        isinstance(es.Herror, OperatorBasisError) for es in up.error_sources)
+
+
 def has_operator_basis(fp) -> bool:
     """True when H0, every error source and the target are operator bases (the fused device path)."""
     up = fp.unitary_problem

@@ -40,6 +40,7 @@ from .types import FidelityRobustGRAPEParameters, FidelityRobustGRAPEProblem
 
 C1, C2 = 1e-4, 0.9
 MAX_LS_ROUNDS = 30
+MAX_PLAN_BATCH = 4096
 
 
 @dataclass
@@ -381,6 +382,12 @@ class RobustCost:
             return self._evaluate(X)
         X = X.contiguous()
         r = X.shape[0]
+        if self.plan.tables:
+            # closure problem: the host evaluates the closures into tables, the device does
+            # the rest (grape_fidelity_grad_tables; host arrays in and out)
+            F, Fdx, Fd2, Fd2dx = (torch.as_tensor(a, device=X.device)
+                                  for a in self.plan.fidelity_grad(X.detach().cpu().numpy()))
+            return F, Fdx, Fd2, Fd2dx
         F = torch.empty(r, dtype=torch.float64, device=X.device)
         Fdx = torch.empty(r, self.nx, dtype=torch.float64, device=X.device)
         Fd2 = torch.empty(r, max(1, self.nerr), dtype=torch.float64, device=X.device)
@@ -464,8 +471,10 @@ def optimize_restarts(fidelity_problem: FidelityRobustGRAPEProblem, fidelity_par
     if X0.dim() != 2:
         raise AssertionError("X0 must be (restarts, n_x)")
     nparam = _checks(fidelity_problem, fidelity_parameters, X0.shape[1])
-    cost = RobustCost(fidelity_problem, fidelity_parameters, nparam, max_batch=X0.shape[0], device=device,
-                      evaluate=evaluate)
+    # workspace for at most MAX_PLAN_BATCH restarts per device pass: larger sweeps are
+    # chunked by the C side instead of failing to allocate
+    cost = RobustCost(fidelity_problem, fidelity_parameters, nparam, max_batch=min(X0.shape[0], MAX_PLAN_BATCH),
+                      device=device, evaluate=evaluate)
     try:
         res = lbfgs_batched(cost, X0.to(cost.device), m=m, **_solver_options(fidelity_parameters))
     finally:

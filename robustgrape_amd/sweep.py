@@ -27,9 +27,11 @@ def shard(n_total: int, world: int, rank: int) -> tuple[int, int]:
 
 def local_best(F: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     """(F_best, id) of this rank as a 2-vector (float64); an empty shard reports (-inf, -1).
-    Ties go to the smallest restart id."""
+    Ties go to the smallest restart id; NaN scores count as -inf."""
     if F.numel() == 0:
         return torch.tensor([float("-inf"), -1.0], dtype=torch.float64, device=F.device)
+    # a NaN score (a diverged restart) ranks last instead of poisoning the max
+    F = torch.nan_to_num(F.to(torch.float64), nan=float("-inf"), posinf=float("inf"), neginf=float("-inf"))
     fmax = torch.max(F)
     cand = torch.where(F == fmax, ids.to(torch.float64), torch.full_like(F, float("inf")))
     return torch.stack([fmax.to(torch.float64), torch.min(cand)])

@@ -11,7 +11,7 @@ while read -r group; do
   [ -z "$group" ] && continue
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d $OUT/${TAG}_p$i -o run -- \
-      python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/${TAG}_p$i.log 2>&1
+      python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-paths ${BENCH_ARGS:-} > $OUT/${TAG}_p$i.log 2>&1
   rc=$?; echo "pass $i ($group) rc=$rc"
   if grep -qE "HSA_STATUS_ERROR|illegal memory access|Memory access fault" $OUT/${TAG}_p$i.log; then echo FAULT; exit 99; fi
   [ $rc -ne 0 ] && { tail -5 $OUT/${TAG}_p$i.log; }

@@ -11,7 +11,7 @@ STEPS=${STEPS:-20}
 # a runtime fault can leave the exit code at 0 or 1: treat its message as fatal
 faulted() { grep -qE "HSA_STATUS_ERROR|illegal memory access|Memory access fault|hipErrorLaunchFailure|core dumped" "$1"; }
 
-timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -25 "$OUT/pytest_gpu_$TAG.log"
 if faulted "$OUT/pytest_gpu_$TAG.log"; then echo "GPU FAULT in pytest"; exit 99; fi
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
@@ -29,7 +29,7 @@ if faulted "$OUT/bench_$TAG.log"; then echo "GPU FAULT in bench"; exit 99; fi
 
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/rocprof_$TAG.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-host-paths > "$OUT/rocprof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/rocprof_$TAG.log"
 find "$OUT/prof_$TAG" -name "*stats*" | head
 exit $rc

@@ -14,7 +14,7 @@ fi
 shopt -s nullglob
 for lib in robustgrape_amd/libgrape.so build_variants/*.so; do
   name=$(basename $lib .so)
-  GRAPE_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/bench_${TAG}_$name.log 2>&1
+  GRAPE_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-paths ${BENCH_ARGS:-} > $OUT/bench_${TAG}_$name.log 2>&1
   rc=$?; echo "$name rc=$rc"
   if faulted $OUT/bench_${TAG}_$name.log; then echo FAULT; exit 99; fi
   [ $rc -ne 0 ] && { tail -5 $OUT/bench_${TAG}_$name.log; continue; }

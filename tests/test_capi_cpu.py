@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) == set(_capi.EXPORTED)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.grape_abi_version() == _capi.ABI_VERSION == 2
+    assert L.grape_abi_version() == _capi.ABI_VERSION
     assert len(_capi.KERNEL_NAMES) == 14  # GRAPE_NUM_KERNELS
 
 
@@ -98,3 +98,69 @@ def test_non_diagonal_projector_rejected():
     W[0, 1] = 0.5
     with pytest.raises(ValueError):
         DescriptorBuffers(fp.replace(projector=W), nparam=1)
+
+
+def _create(fp, nparam=1):
+    """grape_plan_create on this host: descriptor validation runs before the device lookup, so
+    a refusal of the descriptor is observable without a GPU."""
+    from robustgrape_amd import _capi
+    from robustgrape_amd.operators import DescriptorBuffers
+    buf = DescriptorBuffers(fp, nparam=nparam, max_batch=1)
+    h = ctypes.c_void_p()
+    rc = _capi.lib().grape_plan_create(ctypes.byref(buf.desc), 0, ctypes.byref(h))
+    return rc, _capi.lib().grape_last_error().decode()
+
+
+def test_non_hermitian_generators_are_refused():
+    """The engines use C_k^-1 = C_k^dagger: a non-Hermitian H (a -i Gamma/2 decay term, a complex
+    scale on a Hermitian operator) must be refused at plan creation, not computed wrongly."""
+    from robustgrape_amd.operators import OperatorBasisHamiltonian, Term
+    fp = P.sym_problem(8)
+    up = fp.unitary_problem
+    decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
+    terms = list(up.H0.terms)
+    bad = [fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(terms + [Term(decay, scale=-0.5j)]))),
+           fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(
+               terms + [Term(np.triu(np.ones((5, 5))).astype(complex))])))]
+    for f in bad:
+        rc, msg = _create(f)
+        assert rc == -2 and "Hermitian" in msg, (rc, msg)
+    # a complex scale that keeps the term Hermitian (i * antisymmetric real) is accepted past validation
+    anti = np.zeros((5, 5), complex)
+    anti[0, 1], anti[1, 0] = 1.0, -1.0
+    ok = fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(terms + [Term(anti, scale=1j)])))
+    rc, msg = _create(ok)
+    assert rc in (0, -6), (rc, msg)  # -6: no device on this host
+
+
+def test_plan_cache_is_bounded_and_keyed_by_problem(monkeypatch):
+    """get_plan keeps one plan per (problem, nparam, device), grows it up to PLAN_BATCH_CAP and
+    evicts the least recently used beyond MAX_CACHED_PLANS."""
+    from robustgrape_amd import engine
+
+    made = []
+
+    class FakePlan:
+        def __init__(self, fp, nparam, device, max_batch):
+            import threading
+            self.fp, self.max_batch, self.closed, self.lock = fp, max_batch, False, threading.Lock()
+            made.append(self)
+
+        def close(self):
+            self.closed = True
+
+    monkeypatch.setattr(engine, "GrapePlan", FakePlan)
+    engine.clear_plans()
+    fp = P.sym_problem(4)
+    a = engine.get_plan(fp, 1, 0, max_batch=1)
+    assert engine.get_plan(fp, 1, 0, max_batch=1) is a and a.max_batch == 1
+    b = engine.get_plan(fp, 1, 0, max_batch=10 ** 6)  # grows once, capped
+    assert a.closed and b.max_batch == engine.PLAN_BATCH_CAP
+    assert engine.get_plan(fp, 1, 0, max_batch=3) is b  # a big plan serves small batches
+    others = [P.sym_problem(4) for _ in range(engine.MAX_CACHED_PLANS + 3)]
+    for o in others:
+        engine.get_plan(o, 1, 0)
+    assert engine.cached_plan_count() == engine.MAX_CACHED_PLANS
+    assert b.closed  # least recently used, evicted
+    engine.clear_plans()
+    assert engine.cached_plan_count() == 0 and all(p.closed for p in made)

@@ -116,3 +116,23 @@ def test_device_lbfgs_direction_matches_torch_two_loop():
     assert torch.equal(out[0], -gamma[0] * g[0])  # empty history: steepest descent, scaled
     err = (out - ref).abs().max() / ref.abs().max()
     assert err <= 1e-12, float(err)
+
+
+def test_optimiser_on_closure_problem():
+    """a closure problem (the reference's native Types.jl form) takes the host-table
+    plan; the optimiser's cost must evaluate through it and equal the operator-basis cost."""
+    fpd = P.sym_problem(40, errors=("amp",))
+    fph = P.sym_problem(40, errors=("amp",), device=False)
+    X = np.stack([P.random_x(40, s) for s in (21, 22)])
+    params = _params(X[0], nerr=1)
+    costs = []
+    for fp in (fpd, fph):
+        cost = OPT.RobustCost(fp, params, nparam=1, max_batch=2)
+        assert cost.plan.tables == (fp is fph)
+        c, g = cost(torch.as_tensor(X, device="cuda"))
+        cost.close()
+        costs.append((c.cpu().numpy(), g.cpu().numpy()))
+    np.testing.assert_allclose(costs[1][0], costs[0][0], rtol=0, atol=1e-10)
+    assert np.max(np.abs(costs[1][1] - costs[0][1])) <= T3 * np.max(np.abs(costs[0][1])) + T2_ABS
+    res = OPT.optimize_fidelity_and_error_sources(fph, _params(X[0], nerr=1, iterations=3))
+    assert np.isfinite(res.minimum)

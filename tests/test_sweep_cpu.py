@@ -51,6 +51,17 @@ def test_local_best_tie_goes_to_smallest_id():
     assert local_best(F[:0], ids[:0]).tolist()[1] == -1.0
 
 
+def test_local_best_nan_ranks_last():
+    """A diverged restart (NaN score) must not poison the exchange (torch.max
+    propagates NaN and the winning id became inf)."""
+    F = torch.tensor([0.3, float("nan"), 0.7, 0.1], dtype=torch.float64)
+    ids = torch.tensor([4, 5, 6, 7])
+    assert local_best(F, ids).tolist() == [0.7, 6.0]
+    allnan = torch.full((3,), float("nan"), dtype=torch.float64)
+    fb, rid = local_best(allnan, torch.tensor([9, 8, 10])).tolist()
+    assert fb == float("-inf") and rid == 8.0
+
+
 def _worker(rank, world, port, n_total, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
