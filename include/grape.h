@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 2
+#define GRAPE_ABI_VERSION 3
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -125,9 +125,8 @@ typedef struct grape_desc {
  * H0 and the target stay opaque host closures (the reference's own idiom,
  * src/Types.jl:10,50); the caller evaluates them at every call site of the
  * reference and passes the tables to grape_fidelity_grad_tables.  ops / terms
- * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_SMALL_DIM.  With nerr > 0 the
- * caller guarantees that H0 and the error closures do not read x_add (the
- * operator-basis path has the same restriction).
+ * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_SMALL_DIM.  The closures may
+ * read x_add: every x_add call site of the reference is tabulated.
  */
 #define GRAPE_DESC_HOST_TABLES 1
 
@@ -190,13 +189,15 @@ int grape_fidelity_grad_device_async(grape_plan *plan, int nbatch, const double 
  * caller evaluates the closures at exactly the reference's call sites
  * (src/UnitaryCalculations.jl:45,51,59; src/FidelityCalculations.jl:32-40):
  *   H  [nbatch][ntimes][nv][ndim*ndim] complex, column-major, interleaved, variants v:
- *      nerr == 0: nv = 1 + nparam + nadd
- *        0: H0(k, x[:,k], x_add) | 1 + p: x[p,k] + eps | 1 + nparam + q: x_add[q] + eps
- *      nerr > 0: nv = 1 + 2 nparam + nerr (2 + nparam)     (UnitaryCalculations.jl:45-78)
- *        0: H0 | 1 + p: x[p,k] + eps | 1 + nparam + p: x[p,k] + eps2 |
- *        per error e, base 1 + 2 nparam + e (2 + nparam):
+ *      with n = nparam + nadd gradient parameters u (u < nparam: control x[u,k];
+ *      u >= nparam: x_add[u - nparam]):
+ *      nerr == 0: nv = 1 + n
+ *        0: H0(k, x[:,k], x_add) | 1 + u: parameter u + eps
+ *      nerr > 0: nv = 1 + 2 n + nerr (2 + n)                (UnitaryCalculations.jl:45-95)
+ *        0: H0 | 1 + u: parameter u + eps | 1 + n + u: parameter u + eps2 |
+ *        per error e, base 1 + 2 n + e (2 + n):
  *          base: H0 + Herror_e(.., eps) | base + 1: H0 + Herror_e(.., eps2) |
- *          base + 2 + p: H0 + Herror_e(.., eps2), both at x[p,k] + eps2
+ *          base + 2 + u: H0 + Herror_e(.., eps2), both at parameter u + eps2
  *   U0 [nbatch][1 + nadd][ndim*ndim] complex, column-major, interleaved:
  *      slot 0: target(x_add); 1 + q: target(x_add + eps e_q)
  * The device runs the exponentials, the scan and the gradient contractions.
@@ -258,6 +259,27 @@ int grape_interaction_error_operators_device(grape_plan *plan, const double *x, 
  *   ev (ntimes, nerr) real column-major, ev[k, e] = Re(dt tr(P0 sum_{j<=k} O_j,e)) / tr(P0).
  */
 int grape_expectation_values(grape_plan *plan, const double *x, double *ev);
+
+/*
+ * Closure fallback of the three analysis entry points above (plans created with
+ * GRAPE_DESC_HOST_TABLES; the reference's closures evaluated by the caller):
+ *   grape_unitary_derivs_tables: H [ntimes][nv][ndim*ndim] complex column-major, the
+ *     variant layout of grape_fidelity_grad_tables for ONE control vector (every x_add
+ *     call site present); outputs as grape_unitary_derivs.
+ *   grape_interaction_error_operators_tables / grape_expectation_values_tables:
+ *     H0   [ntimes][ndim*ndim]        H0(k, x[:,k], x_add)                (UnitaryCalculations.jl:196)
+ *     Oerr [ntimes][nerr][ndim*ndim]  (1/eps) Herror_e(k, x[:,k], x_add, eps) (:193)
+ *     (complex, column-major); O as grape_interaction_error_operators, written to host
+ *     memory or, with O_on_device != 0, to device memory; ev as grape_expectation_values.
+ * Synchronous.
+ */
+int grape_unitary_derivs_tables(grape_plan *plan, const double *x, const double *H,
+                                double *U, double *U_dx, double *U_dx_add,
+                                double *U_derr, double *U_derr_dx, double *U_derr_dx_add);
+int grape_interaction_error_operators_tables(grape_plan *plan, const double *x, const double *H0,
+                                             const double *Oerr, double *O, int O_on_device);
+int grape_expectation_values_tables(grape_plan *plan, const double *x, const double *H0,
+                                    const double *Oerr, double *ev);
 
 /*
  * Per-kernel timing for measurement (bench.py's roofline): when enabled, every

@@ -121,38 +121,35 @@ function table_plan(fp, nparam::Int; device::Integer=0)
     end
 end
 
-# The closure calls of UnitaryCalculations.jl:45-78 and FidelityCalculations.jl:32-38, tabulated
-# in grape_fidelity_grad_tables' variant order (include/grape.h).  With error sources H0 and
-# Herror must not read x_add (the device path's restriction).
+# The closure calls of UnitaryCalculations.jl:45-95 and FidelityCalculations.jl:32-38, tabulated
+# in grape_fidelity_grad_tables' variant order (include/grape.h): gradient parameters u = controls
+# x[:,k] then x_add, each at +ϵ; with error sources also at +ϵ2, then per error the ϵ / ϵ2 error
+# variants and the mixed (u + ϵ2, error ϵ2) ones.
 function closure_tables(fp, x::Vector{Float64}, np::Int)
     up = fp.unitary_problem; d, nt, na, ϵ, ϵ2 = up.ndim, up.ntimes, up.nb_additional_param, up.ϵ, up.ϵ2
-    errs = up.error_sources; ne = length(errs)
+    errs = up.error_sources; ne = length(errs); n = np + na
     x_main = reshape(x[1:end-na], np, nt); x_add = x[end-na+1:end]
-    nv = ne == 0 ? 1 + np + na : 1 + 2np + ne * (2 + np)
+    nv = ne == 0 ? 1 + n : 1 + 2n + ne * (2 + n)
     H = zeros(ComplexF64, d, d, nv, nt)
     for k in 1:nt
         xk = x_main[:, k]
+        at(u, δ) = u <= np ? (setindex!(copy(xk), xk[u] + δ, u), copy(x_add)) :
+                             (copy(xk), setindex!(copy(x_add), x_add[u-np] + δ, u - np))
         H0k = up.H0(k, copy(xk), copy(x_add))
         H[:, :, 1, k] = H0k
-        for p in 1:np
-            xp = copy(xk); xp[p] += ϵ; H[:, :, 1+p, k] = up.H0(k, xp, copy(x_add))
+        for u in 1:n
+            H[:, :, 1+u, k] = up.H0(k, at(u, ϵ)...)
         end
-        if ne == 0
-            for q in 1:na
-                xa = copy(x_add); xa[q] += ϵ; H[:, :, 1+np+q, k] = up.H0(k, copy(xk), xa)
-            end
-            continue
-        end
-        for p in 1:np
-            xp = copy(xk); xp[p] += ϵ2; H[:, :, 1+np+p, k] = up.H0(k, xp, copy(x_add))
+        ne == 0 && continue
+        for u in 1:n
+            H[:, :, 1+n+u, k] = up.H0(k, at(u, ϵ2)...)
         end
         for (e, es) in enumerate(errs)
-            base = 1 + 2np + (e - 1) * (2 + np)
+            base = 1 + 2n + (e - 1) * (2 + n)
             H[:, :, base+1, k] = es.Herror(k, copy(xk), copy(x_add), ϵ) + H0k
             H[:, :, base+2, k] = es.Herror(k, copy(xk), copy(x_add), ϵ2) + H0k
-            for p in 1:np
-                xp = copy(xk); xp[p] += ϵ2
-                H[:, :, base+2+p, k] = es.Herror(k, copy(xp), copy(x_add), ϵ2) + up.H0(k, copy(xp), copy(x_add))
+            for u in 1:n
+                H[:, :, base+2+u, k] = es.Herror(k, at(u, ϵ2)..., ϵ2) + H[:, :, 1+n+u, k]
             end
         end
     end
@@ -164,13 +161,29 @@ function closure_tables(fp, x::Vector{Float64}, np::Int)
     return H, U0
 end
 
+# closure calls of calculate_interaction_error_operators (UnitaryCalculations.jl:193-196)
+function closure_interaction_tables(up, x::Vector{Float64}, np::Int)
+    d, nt, na, ne = up.ndim, up.ntimes, up.nb_additional_param, length(up.error_sources)
+    x_main = reshape(x[1:end-na], np, nt); x_add = x[end-na+1:end]
+    H0 = zeros(ComplexF64, d, d, nt); Oerr = zeros(ComplexF64, d, d, ne, nt)
+    for k in 1:nt
+        H0[:, :, k] = up.H0(k, x_main[:, k], copy(x_add))
+        for (e, es) in enumerate(up.error_sources)
+            Oerr[:, :, e, k] = (1 / up.ϵ) * es.Herror(k, x_main[:, k], copy(x_add), up.ϵ)
+        end
+    end
+    return H0, Oerr
+end
+
+is_operator_basis(fp) = fp.unitary_problem.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis &&
+                        all(es.Herror isa OperatorBasis for es in fp.unitary_problem.error_sources)
+
 "Drop-in for src/FidelityCalculations.jl:19-119: (F, F_dx_tot, F_d2err, F_d2err_dx_tot)."
 function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
     up = fp.unitary_problem
     xm = length(x) - up.nb_additional_param
     @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
-    if !(up.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis &&
-         all(es.Herror isa OperatorBasis for es in up.error_sources))          # closure fallback
+    if !is_operator_basis(fp)          # closure fallback
         np = xm ÷ up.ntimes
         p = table_plan(fp, np)
         xv = Vector{Float64}(x)
@@ -202,10 +215,21 @@ function calculate_unitary_and_derivatives(fp, x::AbstractVector{<:Real})
     xm = length(x) - na
     @assert mod(xm, nt) == 0 "Control parameter size must be a multiple of time steps"
     np = xm ÷ nt
-    p = device_plan(fp, np; max_batch=1)
     xv = Vector{Float64}(x)
     outs = (zeros(ComplexF64, d, d), zeros(ComplexF64, d, d, np, nt), zeros(ComplexF64, d, d, na),
             zeros(ComplexF64, d, d, ne), zeros(ComplexF64, d, d, np, nt, ne), zeros(ComplexF64, d, d, na, ne))
+    if !is_operator_basis(fp)          # closure fallback
+        p = table_plan(fp, np)
+        H, _ = closure_tables(fp, xv, np)
+        GC.@preserve xv H outs begin
+            _check(ccall((:grape_unitary_derivs_tables, libgrape), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64},
+                          Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64}),
+                         p.handle, xv, H, outs...))
+        end
+        return outs
+    end
+    p = device_plan(fp, np; max_batch=1)
     GC.@preserve xv outs begin
         _check(ccall((:grape_unitary_derivs, libgrape), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64},
@@ -217,9 +241,20 @@ end
 "Drop-in for src/UnitaryCalculations.jl:180-204: (ndim, ndim, ntimes, nerr)."
 function calculate_interaction_error_operators(fp, x::AbstractVector{<:Real})
     up = fp.unitary_problem
-    p = device_plan(fp, (length(x) - up.nb_additional_param) ÷ up.ntimes; max_batch=1)
+    np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
     O = zeros(ComplexF64, up.ndim, up.ndim, up.ntimes, length(up.error_sources))
+    if !is_operator_basis(fp)          # closure fallback
+        p = table_plan(fp, np)
+        H0, Oerr = closure_interaction_tables(up, xv, np)
+        GC.@preserve xv H0 Oerr O begin
+            _check(ccall((:grape_interaction_error_operators_tables, libgrape), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Cint),
+                         p.handle, xv, H0, Oerr, O, 0))
+        end
+        return O
+    end
+    p = device_plan(fp, np; max_batch=1)
     GC.@preserve xv O begin
         _check(ccall((:grape_interaction_error_operators, libgrape), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}), p.handle, xv, O))
@@ -230,9 +265,20 @@ end
 "Drop-in for src/FidelityCalculations.jl:368-390: (ntimes, nerr)."
 function calculate_expectation_values(fp, x::AbstractVector{<:Real})
     up = fp.unitary_problem
-    p = device_plan(fp, (length(x) - up.nb_additional_param) ÷ up.ntimes; max_batch=1)
+    np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
     ev = zeros(Float64, up.ntimes, length(up.error_sources))
+    if !is_operator_basis(fp)          # closure fallback
+        p = table_plan(fp, np)
+        H0, Oerr = closure_interaction_tables(up, xv, np)
+        GC.@preserve xv H0 Oerr ev begin
+            _check(ccall((:grape_expectation_values_tables, libgrape), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{Float64}),
+                         p.handle, xv, H0, Oerr, ev))
+        end
+        return ev
+    end
+    p = device_plan(fp, np; max_batch=1)
     GC.@preserve xv ev begin
         _check(ccall((:grape_expectation_values, libgrape), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), p.handle, xv, ev))

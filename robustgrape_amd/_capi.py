@@ -23,10 +23,11 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times",
             "grape_interaction_error_operators", "grape_interaction_error_operators_device",
             "grape_expectation_values", "grape_fidelity_grad_tables",
-            "grape_lbfgs_direction"]
+            "grape_lbfgs_direction", "grape_unitary_derivs_tables", "grape_interaction_error_operators_tables",
+            "grape_expectation_values_tables"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
-ABI_VERSION = 2  # GRAPE_ABI_VERSION in include/grape.h
+ABI_VERSION = 3  # GRAPE_ABI_VERSION in include/grape.h
 
 
 class GrapeError(RuntimeError):
@@ -79,6 +80,12 @@ def lib():
         L.grape_interaction_error_operators_device.restype = ctypes.c_int
         L.grape_expectation_values.argtypes = [vp, dp, dp]
         L.grape_expectation_values.restype = ctypes.c_int
+        L.grape_unitary_derivs_tables.argtypes = [vp, dp, dp, dp, dp, dp, dp, dp, dp]
+        L.grape_unitary_derivs_tables.restype = ctypes.c_int
+        L.grape_interaction_error_operators_tables.argtypes = [vp, dp, dp, dp, vp, ctypes.c_int]
+        L.grape_interaction_error_operators_tables.restype = ctypes.c_int
+        L.grape_expectation_values_tables.argtypes = [vp, dp, dp, dp, dp]
+        L.grape_expectation_values_tables.restype = ctypes.c_int
         L.grape_plan_set_profiling.argtypes = [vp, ctypes.c_int]
         L.grape_plan_set_profiling.restype = ctypes.c_int
         L.grape_plan_kernel_times.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]

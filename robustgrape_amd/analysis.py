@@ -20,6 +20,7 @@ import torch
 
 from . import _capi
 from .engine import fidelity_wrapper, get_plan
+from .operators import host_interaction_tables
 from .types import FidelityRobustGRAPEProblem, split_x
 
 def _plan(fp_or_up, x, device):
@@ -39,7 +40,13 @@ def calculate_interaction_error_operators(unitary_problem, x, device: int = 0) -
     O = np.zeros((up.ndim, up.ndim, up.ntimes, len(up.error_sources)), dtype=np.complex128, order="F")
     if O.size:
         with plan.lock:
-            _capi.check(_capi.lib().grape_interaction_error_operators(plan.handle, _capi.dptr(x), _capi.dptr(O)))
+            if plan.tables:  # closure problem: H0 / Herror evaluated here (the reference's calls)
+                H0, Oerr = host_interaction_tables(up, x, plan.nparam)
+                _capi.check(_capi.lib().grape_interaction_error_operators_tables(
+                    plan.handle, _capi.dptr(x), _capi.dptr(H0), _capi.dptr(Oerr), O.ctypes.data, 0))
+            else:
+                _capi.check(_capi.lib().grape_interaction_error_operators(plan.handle, _capi.dptr(x),
+                                                                           _capi.dptr(O)))
     return O
 
 
@@ -51,7 +58,12 @@ def calculate_expectation_values(fidelity_problem: FidelityRobustGRAPEProblem, x
     ev = np.zeros((up.ntimes, len(up.error_sources)), dtype=np.float64, order="F")
     if ev.size:
         with plan.lock:
-            _capi.check(_capi.lib().grape_expectation_values(plan.handle, _capi.dptr(x), _capi.dptr(ev)))
+            if plan.tables:
+                H0, Oerr = host_interaction_tables(up, x, plan.nparam)
+                _capi.check(_capi.lib().grape_expectation_values_tables(
+                    plan.handle, _capi.dptr(x), _capi.dptr(H0), _capi.dptr(Oerr), _capi.dptr(ev)))
+            else:
+                _capi.check(_capi.lib().grape_expectation_values(plan.handle, _capi.dptr(x), _capi.dptr(ev)))
     return ev
 
 
@@ -67,8 +79,13 @@ def _device_operators(fp, x, device):
     O = torch.empty(ne, nt, d, d, dtype=torch.complex128, device=torch.device("cuda", device))
     torch.cuda.synchronize(O.device)
     with plan.lock:
-        _capi.check(_capi.lib().grape_interaction_error_operators_device(
-            plan.handle, _capi.dptr(x), ctypes.c_void_p(O.data_ptr())))
+        if plan.tables:
+            H0, Oerr = host_interaction_tables(up, x, plan.nparam)
+            _capi.check(_capi.lib().grape_interaction_error_operators_tables(
+                plan.handle, _capi.dptr(x), _capi.dptr(H0), _capi.dptr(Oerr), O.data_ptr(), 1))
+        else:
+            _capi.check(_capi.lib().grape_interaction_error_operators_device(
+                plan.handle, _capi.dptr(x), ctypes.c_void_p(O.data_ptr())))
     return O.transpose(-1, -2)
 
 

@@ -124,7 +124,7 @@ struct grape_plan {
     grape::VSpec *d_vs = nullptr;
     int *d_ovf2 = nullptr;
     cd *d_ovf2_slots = nullptr;
-    double *d_Fd2 = nullptr, *d_Fd2dx = nullptr;
+    double *d_Fd2 = nullptr, *d_Fd2dx = nullptr, *d_part_err = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
     // closure mode (GRAPE_DESC_HOST_TABLES): host-evaluated H and target tables
@@ -167,7 +167,7 @@ static void free_plan(grape_plan *p) {
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
-                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_ovf2, p->d_ovf2_slots,
+                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf,
                     p->d_Htab, p->d_U0tab};
@@ -371,15 +371,13 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         if ((rc = check_hermitian_terms(desc, desc->h0_terms, desc->n_h0_terms, "H0"))) return rc;
         if ((rc = check_hermitian_terms(desc, desc->err_terms, n_err_terms, "error source"))) return rc;
     }
-    // host tables: H0 is an opaque closure that may read x_add; with error sources the
-    // caller guarantees it does not (like the operator-basis path, which refuses that case)
-    bool xadd_dep = tables && desc->nadd > 0 && desc->nerr == 0;
+    // host tables: H0 / Herror are opaque closures that may read x_add, so every x_add call
+    // site of the reference is tabulated (UnitaryCalculations.jl:57-64, 87-95)
+    bool xadd_dep = tables && desc->nadd > 0;
     for (int k = 0; k < (tables ? 0 : desc->n_h0_terms); ++k)
         if (desc->h0_terms[k].var == 2) xadd_dep = true;
     for (int k = 0; k < n_err_terms; ++k)
         if (desc->err_terms[k].var == 2) xadd_dep = true;
-    if (xadd_dep && desc->nerr > 0)
-        return fail(GRAPE_ERR_UNSUPPORTED, "error sources together with an x_add-dependent Hamiltonian");
     double trP = 0.0;
     for (int i = 0; i < D; ++i) trP += desc->projector_diag[i];
     if (!(trP > 0)) return fail(GRAPE_ERR_INVALID, "projector trace must be positive");
@@ -423,8 +421,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     // Propagator variants of one step (the closure call sites of UnitaryCalculations.jl:45-90):
     //   0 nominal | dx: x_p + eps | dxa: x_add_q + eps (only if H0 reads x_add, otherwise
     //   exp(A(x_add + eps)) == exp(A) bit for bit and the reference's difference is 0)
-    //   | ne > 0: dx2: x_p + eps2 | per error e: err(eps), err2(eps2), mix_p (x_p + eps2, err eps2)
+    //   | ne > 0: dx2: x_p + eps2, then x_add_q + eps2 (xadd_dep) | per error e: err(eps),
+    //   err2(eps2), mix_p (x_p + eps2, err eps2), then mix_q (x_add_q + eps2, err eps2) (xadd_dep)
     // The eps2 variants only feed the mixed stencils: skipped when ne == 0 (dead work).
+    // "u" indexes the nvg = np + nad gradient parameters: controls, then (xadd_dep) x_add;
+    // dx + u, dx2 + u and err_base + 2 + u are then the variants of parameter u.
+    const int nad = xadd_dep ? desc->nadd : 0;
     std::vector<grape::VSpec> vs;
     auto addv = [&](int var, int idx, double delta, int err, double errval) {
         grape::VSpec v;
@@ -439,17 +441,19 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.off_dx = (int)vs.size();
     for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps, -1, 0.0);
     P.off_dxa = (int)vs.size();
-    if (xadd_dep)
-        for (int q = 0; q < desc->nadd; ++q) addv(2, q, desc->eps, -1, 0.0);
+    for (int q = 0; q < nad; ++q) addv(2, q, desc->eps, -1, 0.0);
     P.off_dx2 = (int)vs.size();
-    if (desc->nerr > 0)
+    if (desc->nerr > 0) {
         for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps2, -1, 0.0);
+        for (int q = 0; q < nad; ++q) addv(2, q, desc->eps2, -1, 0.0);
+    }
     P.off_err = (int)vs.size();
-    P.err_stride = 2 + desc->nparam;
+    P.err_stride = 2 + desc->nparam + nad;
     for (int e = 0; e < desc->nerr; ++e) {
         addv(-1, 0, 0.0, e, desc->eps);
         addv(-1, 0, 0.0, e, desc->eps2);
         for (int q = 0; q < desc->nparam; ++q) addv(1, q, desc->eps2, e, desc->eps2);
+        for (int q = 0; q < nad; ++q) addv(2, q, desc->eps2, e, desc->eps2);
     }
     // E stores every variant for the error-source pipeline; without error sources
     // only the nominal propagators are stored (k_expm_grad consumes the rest in place)
@@ -512,6 +516,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
              dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
+    if (ok && P.ne > 0 && P.xadd_dep)
+        ok = dalloc(&p->d_part_err, MB * P.ne * P.Nt * P.na) == hipSuccess;
     if (ok && tables)
         ok = dalloc(&p->d_Htab, MB * P.Nt * P.nv * T) == hipSuccess &&
              dalloc(&p->d_U0tab, MB * (1 + P.na) * T) == hipSuccess;
@@ -614,6 +620,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         B.Carry = p->d_Carry;
         B.Ub = p->d_Ub;
         B.Me = p->d_Me;
+        B.part_err_add = p->d_part_err;
     }
     // ctrl: [2] status (sticky until grape_plan_synchronize reports it),
     // [4] k_expm overflow count, [5] k_expm_grad overflow count
@@ -783,130 +790,24 @@ static int ud_alloc(grape_plan *p) {
     return ok ? GRAPE_OK : fail(GRAPE_ERR_ALLOC, "device allocation failed (single-evaluation workspace)");
 }
 
-// nominal propagators E_k and the chain C_k of one x into the ud workspace
-static int ud_chain(grape_plan *p, const double *x) {
-    const DevProblem &P0 = p->P;
-    grape::VSpec nominal{};
-    nominal.pert.var = -1;
-    nominal.err = -1;
-    hipStream_t st = p->stream;
-    HIPCHECK(hipMemcpyAsync(p->ud_vs, &nominal, sizeof(nominal), hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), st));
-    DevProblem Pu = P0;
-    Pu.nv = 1;
-    Pu.vs = p->ud_vs;
-    DevBatch Bu{};
-    Bu.nb = 1;
-    Bu.x = p->d_x;
-    Bu.E = p->ud_E;
-    Bu.overflow = p->ud_ovf;
-    Bu.overflow_count = p->d_ctrl;
-    Bu.status = p->d_ctrl + 2;
-    HIPCHECK(dispatch_expm_variants(P0.D, Pu, Bu, st));
-    grape_unitary::UProblem UP{};
-    UP.D = P0.D;
-    UP.Nt = P0.Nt;
-    UP.nv = 1;
-    HIPCHECK(grape_unitary::launch_chain(UP, p->ud_E, p->ud_C, st));
-    return GRAPE_OK;
-}
-
-int grape_interaction_error_operators(grape_plan *p, const double *x, double *O) {
-    if (!p || !x || !O) return fail(GRAPE_ERR_INVALID, "null argument");
-    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, "interaction error operators: dense engine not supported");
-    if (p->P.ne == 0) return GRAPE_OK;
-    HIPCHECK(hipSetDevice(p->device));
-    if (int rc = ud_alloc(p)) return rc;
-    if (int rc = ud_chain(p, x)) return rc;
-    const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
-    HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
-    HIPCHECK(hipMemcpyAsync(O, p->ud_out, n * sizeof(cd), hipMemcpyDeviceToHost, p->stream));
-    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
-    return grape_plan_synchronize(p);
-}
-
-int grape_interaction_error_operators_device(grape_plan *p, const double *x, double *d_O) {
-    if (!p || !x || !d_O) return fail(GRAPE_ERR_INVALID, "null argument");
-    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, "interaction error operators: dense engine not supported");
-    if (p->P.ne == 0) return GRAPE_OK;
-    HIPCHECK(hipSetDevice(p->device));
-    if (int rc = ud_alloc(p)) return rc;
-    if (int rc = ud_chain(p, x)) return rc;
-    const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
-    HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
-    HIPCHECK(hipMemcpyAsync(d_O, p->ud_out, n * sizeof(cd), hipMemcpyDeviceToDevice, p->stream));
-    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
-    return grape_plan_synchronize(p);
-}
-
-int grape_expectation_values(grape_plan *p, const double *x, double *ev) {
-    if (!p || !x || !ev) return fail(GRAPE_ERR_INVALID, "null argument");
-    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, "expectation values: dense engine not supported");
-    if (p->P.ne == 0) return GRAPE_OK;
-    HIPCHECK(hipSetDevice(p->device));
-    if (int rc = ud_alloc(p)) return rc;
-    if (int rc = ud_chain(p, x)) return rc;
-    HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
-    double *dev = reinterpret_cast<double *>(p->ud_V);  // (Nt, ne) column-major
-    HIPCHECK(grape_unitary::launch_expectation(p->P, p->ud_out, dev, p->stream));
-    HIPCHECK(hipMemcpyAsync(ev, dev, (size_t)p->P.Nt * p->P.ne * sizeof(double), hipMemcpyDeviceToHost, p->stream));
-    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
-    return grape_plan_synchronize(p);
-}
-
-int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
-                         double *U_derr_dx, double *U_derr_dx_add) {
-    if (!p || !x) return fail(GRAPE_ERR_INVALID, "null argument");
-    if (p->tables) return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: host-table plans are not supported");
-    if (p->dense)
-        return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: ndim > GRAPE_MAX_SMALL_DIM (dense engine) "
-                                           "is not supported; use grape_fidelity_grad");
-    HIPCHECK(hipSetDevice(p->device));
-    const DevProblem &P0 = p->P;
-    const int D = P0.D, Nt = P0.Nt, np = P0.np, na = P0.na, ne = P0.ne;
-    const size_t T = (size_t)D * D;
-    // every closure call site of UnitaryCalculations.jl:45-90 as a propagator variant
-    std::vector<grape::VSpec> vs;
-    auto addv = [&](int var, int idx, double delta, int err, double errval) {
-        grape::VSpec v;
-        v.pert.var = var;
-        v.pert.index = idx;
-        v.pert.delta = delta;
-        v.err = err;
-        v.errval = errval;
-        vs.push_back(v);
-    };
-    addv(-1, 0, 0.0, -1, 0.0);
-    for (int q = 0; q < np; ++q) addv(1, q, P0.eps, -1, 0.0);
-    for (int q = 0; q < na; ++q) addv(2, q, P0.eps, -1, 0.0);
-    grape_unitary::UProblem UP{};
-    UP.off_x2 = (int)vs.size();
-    if (ne > 0) {
-        for (int q = 0; q < np; ++q) addv(1, q, P0.eps2, -1, 0.0);
-        for (int q = 0; q < na; ++q) addv(2, q, P0.eps2, -1, 0.0);
+static hipError_t dispatch_expm_table(int D, const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    switch (D) {
+#define CASE(d) \
+    case d: return grape_host::launch_expm_table<d>(P, B, st);
+        GRAPE_DIMS(CASE)
+#undef CASE
     }
-    UP.off_err = (int)vs.size();
-    for (int e = 0; e < ne; ++e) {
-        addv(-1, 0, 0.0, e, P0.eps);
-        addv(-1, 0, 0.0, e, P0.eps2);
-        for (int q = 0; q < np; ++q) addv(1, q, P0.eps2, e, P0.eps2);
-        for (int q = 0; q < na; ++q) addv(2, q, P0.eps2, e, P0.eps2);
-    }
+    return hipErrorInvalidValue;
+}
+
+// Propagator table E[k][v] of ONE x into the ud workspace: from the operator basis for the
+// variant list vs (Htab == nullptr), or -- closure fallback -- from the host-evaluated H table
+// Htab [Nt][nv][D][D] column-major, whose variant layout is vs's.
+static int ud_propagators(grape_plan *p, const double *x, const std::vector<grape::VSpec> &vs, const double *Htab) {
+    const DevProblem &P0 = p->P;
     const int nv = (int)vs.size();
-    UP.D = D;
-    UP.Nt = Nt;
-    UP.np = np;
-    UP.na = na;
-    UP.ne = ne;
-    UP.nv = nv;
-    UP.nslots = np + na + ne + ne * (np + na);
-    UP.inv_eps = P0.inv_eps;
-    UP.inv_eps2sq = 1.0 / (P0.eps2 * P0.eps2);
-    // outputs, packed: U_dx | U_dx_add | U_derr | U_derr_dx | U_derr_dx_add
-    const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
-    if (int rc = ud_alloc(p)) return rc;
     hipStream_t st = p->stream;
+    const size_t T = (size_t)P0.D * P0.D;
     HIPCHECK(hipMemcpyAsync(p->ud_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), st));
@@ -920,7 +821,166 @@ int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx
     Bu.overflow = p->ud_ovf;
     Bu.overflow_count = p->d_ctrl;
     Bu.status = p->d_ctrl + 2;
-    HIPCHECK(dispatch_expm_variants(D, Pu, Bu, st));
+    if (Htab) {
+        HIPCHECK(hipMemcpyAsync(p->d_Htab, Htab, (size_t)P0.Nt * nv * T * sizeof(cd), hipMemcpyHostToDevice, st));
+        Bu.Htab = p->d_Htab;
+        HIPCHECK(dispatch_expm_table(P0.D, Pu, Bu, st));
+    } else {
+        HIPCHECK(dispatch_expm_variants(P0.D, Pu, Bu, st));
+    }
+    return GRAPE_OK;
+}
+
+// nominal propagators E_k and the chain C_k of one x into the ud workspace (H0tab: the
+// closure fallback's host-evaluated H0(k, x_k, x_add), [Nt][D][D] column-major)
+static int ud_chain(grape_plan *p, const double *x, const double *H0tab) {
+    const DevProblem &P0 = p->P;
+    grape::VSpec nominal{};
+    nominal.pert.var = -1;
+    nominal.err = -1;
+    if (int rc = ud_propagators(p, x, std::vector<grape::VSpec>{nominal}, H0tab)) return rc;
+    grape_unitary::UProblem UP{};
+    UP.D = P0.D;
+    UP.Nt = P0.Nt;
+    UP.nv = 1;
+    HIPCHECK(grape_unitary::launch_chain(UP, p->ud_E, p->ud_C, p->stream));
+    return GRAPE_OK;
+}
+
+// interaction-picture error operators of one x into ud_out (d, d, Nt, ne) column-major;
+// closure fallback when H0tab / Oerr are given (host arrays)
+static int ud_interaction(grape_plan *p, const double *x, const double *H0tab, const double *Oerr) {
+    if (int rc = ud_alloc(p)) return rc;
+    if (int rc = ud_chain(p, x, H0tab)) return rc;
+    if (Oerr) {
+        cd *dO = p->ud_V;  // Nt * nslots >= Nt * ne tiles
+        const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
+        HIPCHECK(hipMemcpyAsync(dO, Oerr, n * sizeof(cd), hipMemcpyHostToDevice, p->stream));
+        HIPCHECK(grape_unitary::launch_interaction_table(p->P, dO, p->ud_C, p->ud_out, p->stream));
+    } else {
+        HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
+    }
+    return GRAPE_OK;
+}
+
+static int analysis_check(grape_plan *p, bool tables_call, const char *what) {
+    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, std::string(what) + ": dense engine not supported");
+    if (p->tables && !tables_call)
+        return fail(GRAPE_ERR_INVALID, std::string(what) + ": host-table plan: use the _tables entry point");
+    if (!p->tables && tables_call)
+        return fail(GRAPE_ERR_INVALID, std::string(what) + ": plan was not created with GRAPE_DESC_HOST_TABLES");
+    return GRAPE_OK;
+}
+
+static int interaction_to(grape_plan *p, const double *x, const double *H0tab, const double *Oerr, double *O,
+                          hipMemcpyKind kind) {
+    if (p->P.ne == 0) return GRAPE_OK;
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = ud_interaction(p, x, H0tab, Oerr)) return rc;
+    const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
+    HIPCHECK(hipMemcpyAsync(O, p->ud_out, n * sizeof(cd), kind, p->stream));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    return grape_plan_synchronize(p);
+}
+
+int grape_interaction_error_operators(grape_plan *p, const double *x, double *O) {
+    if (!p || !x || !O) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (int rc = analysis_check(p, false, "interaction error operators")) return rc;
+    return interaction_to(p, x, nullptr, nullptr, O, hipMemcpyDeviceToHost);
+}
+
+int grape_interaction_error_operators_device(grape_plan *p, const double *x, double *d_O) {
+    if (!p || !x || !d_O) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (int rc = analysis_check(p, false, "interaction error operators")) return rc;
+    return interaction_to(p, x, nullptr, nullptr, d_O, hipMemcpyDeviceToDevice);
+}
+
+int grape_interaction_error_operators_tables(grape_plan *p, const double *x, const double *H0, const double *Oerr,
+                                             double *O, int O_on_device) {
+    if (!p || !x || !O || (p->P.ne > 0 && (!H0 || !Oerr))) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (int rc = analysis_check(p, true, "interaction error operators")) return rc;
+    return interaction_to(p, x, H0, Oerr, O, O_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost);
+}
+
+static int expectation_to(grape_plan *p, const double *x, const double *H0tab, const double *Oerr, double *ev) {
+    if (p->P.ne == 0) return GRAPE_OK;
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = ud_interaction(p, x, H0tab, Oerr)) return rc;
+    double *dev = reinterpret_cast<double *>(p->ud_S);  // (Nt, ne) column-major: Nt * ne tiles of room
+    HIPCHECK(grape_unitary::launch_expectation(p->P, p->ud_out, dev, p->stream));
+    HIPCHECK(hipMemcpyAsync(ev, dev, (size_t)p->P.Nt * p->P.ne * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    return grape_plan_synchronize(p);
+}
+
+int grape_expectation_values(grape_plan *p, const double *x, double *ev) {
+    if (!p || !x || !ev) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (int rc = analysis_check(p, false, "expectation values")) return rc;
+    return expectation_to(p, x, nullptr, nullptr, ev);
+}
+
+int grape_expectation_values_tables(grape_plan *p, const double *x, const double *H0, const double *Oerr,
+                                    double *ev) {
+    if (!p || !x || !ev || (p->P.ne > 0 && (!H0 || !Oerr))) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (int rc = analysis_check(p, true, "expectation values")) return rc;
+    return expectation_to(p, x, H0, Oerr, ev);
+}
+
+// every closure call site of UnitaryCalculations.jl:45-95 as a propagator variant, in the
+// layout of grape_unitary::UProblem (= the host-table layout of grape_fidelity_grad_tables
+// with every x_add site present)
+static std::vector<grape::VSpec> ud_variants(const DevProblem &P0, grape_unitary::UProblem &UP) {
+    const int np = P0.np, na = P0.na, ne = P0.ne;
+    std::vector<grape::VSpec> vs;
+    auto addv = [&](int var, int idx, double delta, int err, double errval) {
+        grape::VSpec v;
+        v.pert.var = var;
+        v.pert.index = idx;
+        v.pert.delta = delta;
+        v.err = err;
+        v.errval = errval;
+        vs.push_back(v);
+    };
+    addv(-1, 0, 0.0, -1, 0.0);
+    for (int q = 0; q < np; ++q) addv(1, q, P0.eps, -1, 0.0);
+    for (int q = 0; q < na; ++q) addv(2, q, P0.eps, -1, 0.0);
+    UP.off_x2 = (int)vs.size();
+    if (ne > 0) {
+        for (int q = 0; q < np; ++q) addv(1, q, P0.eps2, -1, 0.0);
+        for (int q = 0; q < na; ++q) addv(2, q, P0.eps2, -1, 0.0);
+    }
+    UP.off_err = (int)vs.size();
+    for (int e = 0; e < ne; ++e) {
+        addv(-1, 0, 0.0, e, P0.eps);
+        addv(-1, 0, 0.0, e, P0.eps2);
+        for (int q = 0; q < np; ++q) addv(1, q, P0.eps2, e, P0.eps2);
+        for (int q = 0; q < na; ++q) addv(2, q, P0.eps2, e, P0.eps2);
+    }
+    return vs;
+}
+
+static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, double *U, double *U_dx,
+                          double *U_dx_add, double *U_derr, double *U_derr_dx, double *U_derr_dx_add) {
+    HIPCHECK(hipSetDevice(p->device));
+    const DevProblem &P0 = p->P;
+    const int D = P0.D, Nt = P0.Nt, np = P0.np, na = P0.na, ne = P0.ne;
+    const size_t T = (size_t)D * D;
+    grape_unitary::UProblem UP{};
+    const std::vector<grape::VSpec> vs = ud_variants(P0, UP);
+    UP.D = D;
+    UP.Nt = Nt;
+    UP.np = np;
+    UP.na = na;
+    UP.ne = ne;
+    UP.nv = (int)vs.size();
+    UP.nslots = np + na + ne + ne * (np + na);
+    UP.inv_eps = P0.inv_eps;
+    UP.inv_eps2sq = 1.0 / (P0.eps2 * P0.eps2);
+    // outputs, packed: U_dx | U_dx_add | U_derr | U_derr_dx | U_derr_dx_add
+    const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
+    if (int rc = ud_alloc(p)) return rc;
+    if (int rc = ud_propagators(p, x, vs, Htab)) return rc;
+    hipStream_t st = p->stream;
     grape_unitary::UBuffers UB{};
     UB.E = p->ud_E;
     UB.C = p->ud_C;
@@ -953,6 +1013,23 @@ int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx
                 U[2 * ((size_t)i + (size_t)j * D) + 1] = Ulast[(size_t)i * D + j].im;
             }
     return GRAPE_OK;
+}
+
+int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
+                         double *U_derr_dx, double *U_derr_dx_add) {
+    if (!p || !x) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (p->dense)
+        return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: ndim > GRAPE_MAX_SMALL_DIM (dense engine) "
+                                           "is not supported; use grape_fidelity_grad");
+    if (p->tables) return fail(GRAPE_ERR_INVALID, "grape_unitary_derivs: host-table plan: use grape_unitary_derivs_tables");
+    return unitary_derivs(p, x, nullptr, U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add);
+}
+
+int grape_unitary_derivs_tables(grape_plan *p, const double *x, const double *H, double *U, double *U_dx,
+                                double *U_dx_add, double *U_derr, double *U_derr_dx, double *U_derr_dx_add) {
+    if (!p || !x || !H) return fail(GRAPE_ERR_INVALID, "null argument");
+    if (!p->tables) return fail(GRAPE_ERR_INVALID, "plan was not created with GRAPE_DESC_HOST_TABLES");
+    return unitary_derivs(p, x, H, U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add);
 }
 
 static int dense_expm_batch(int device, int ndim, int n, const double *A, double *E, int *stats) {

@@ -17,7 +17,9 @@
 //
 // k_err_scan  one workgroup per (b, e): chunk totals of W, carry transform,
 //             additive scan over chunks, U_derr, F_d2err, M_e, per-chunk M', T, Ttot.
-// k_err_grad  one row group per (b, chunk, e): walks the chunk's steps, 8 products/step.
+// k_err_grad  one row group per (b, chunk, e): walks the chunk's steps, 8 products/step
+//             per gradient parameter (controls; x_add too when H0 / Herror read it,
+//             U_derr_dx_add being the sum over k of the same per-step terms, :140-151).
 #pragma once
 #include "grape_kernels.hpp"
 
@@ -203,8 +205,9 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
         for (int jj = 0; jj < D; ++jj) S4[i * D + jj] = w[jj];
     }
     gsync();
-    // target part of F_d2err_dx_add (FidelityCalculations.jl:100-112 with U_derr_dx_add = 0,
-    // H0 not reading x_add): 2[2 Re sum W P Kde conj(Ke) + 2 Re(conj(te) tr(W Kde))]/DD
+    // target part of F_d2err_dx_add (FidelityCalculations.jl:100-112, the U0_dx_add terms):
+    // 2[2 Re sum W P Kde conj(Ke) + 2 Re(conj(te) tr(W Kde))]/DD.  When H0 / Herror read x_add
+    // the U_derr_dx_add terms are per-step sums added by k_err_grad + k_reduce_add.
     for (int qd = 0; qd < P.na; ++qd) {
         Pert pq;
         pq.var = VAR_XADD; pq.index = qd; pq.delta = P.eps;
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(64, GRAPE_ERRGRAD_WAVES) void k_err_grad(DevProblem
     const cd *Mp = Mo, *Tc = Mo + TILE, *Tt = Mo + 2 * TILE;
     const int v_err = P.off_err + e * P.err_stride, v_err2 = v_err + 1;
     double *out = B.Fd2dx + ((size_t)b * P.ne + e) * P.nx;
+    const int nvg = P.np + (P.xadd_dep ? P.na : 0);
     cd A[D], Wk[D], z1[D], x[D], t[D];
 #pragma unroll
     for (int jj = 0; jj < D; ++jj) A[jj] = Tc[i * D + jj];
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(64, GRAPE_ERRGRAD_WAVES) void k_err_grad(DevProblem
         const cd *Qk = Qb + (size_t)kc * TILE;
         delta_row<D>(Ek, v_err, i, P.inv_eps, x);
         local_frame<D>(G, Qk, j == 0, x, Wk, act);  // W_k
-        for (int p = 0; p < P.np; ++p) {
+        for (int p = 0; p < nvg; ++p) {  // controls, then x_add (xadd_dep): variants off_dx + p
             delta_row<D>(Ek, P.off_dx + p, i, P.inv_eps, x);
             local_frame<D>(G, Qk, j == 0, x, z1, act);  // Z1 = Q^dag dE^dx Q
             // S1 = tr(A (M' Z1))
@@ -351,7 +355,10 @@ __global__ __launch_bounds__(64, GRAPE_ERRGRAD_WAVES) void k_err_grad(DevProblem
             s = cadd(s, row_dot_col<D>(x, G.tile, i));
             gsync();
             const double tot = group_sum(G, s.re, act);
-            if (act && i == 0) out[(size_t)k * P.np + p] = tot;
+            if (act && i == 0) {
+                if (p < P.np) out[(size_t)k * P.np + p] = tot;
+                else B.part_err_add[(((size_t)b * P.ne + e) * P.Nt + k) * P.na + (p - P.np)] = tot;
+            }
         }
         if (act) {
 #pragma unroll

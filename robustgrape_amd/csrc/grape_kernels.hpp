@@ -88,6 +88,7 @@ struct DevBatch {
     cd *Me;                 // [nb][ne][nchunks][3][D][D]  M'_{c,e}, T_c, Ttot_c (error path)
     double *Fd2;            // [nb][ne]
     double *Fd2dx;          // [nb][ne][nx]
+    double *part_err_add;   // [nb][ne][Nt][na]  per-step x_add terms of F_d2err_dx (xadd_dep only)
     int *overflow;          // parked (Pade m > 5) item ids of k_expm
     int *overflow_count;
     int *ovf2;              // parked item ids of k_expm_grad
@@ -786,15 +787,28 @@ __global__ __launch_bounds__(64) void k_grad_high(DevProblem P, DevBatch B) {
     }
 }
 
-// F_dx_add = target part + sum_k per-step contributions (xadd_dep only)
+// (xadd_dep only) F_dx_add = target part + sum_k per-step contributions
+// (FidelityCalculations.jl:67-76 over U_dx_add = U sum_k V^dxa_k, UnitaryCalculations.jl:119-121);
+// with error sources also F_d2err_dx_add[q, e] += sum_k per-step terms (k_err_grad) on top of
+// the target part k_err_scan wrote (:99-113 over U_derr_dx_add, UnitaryCalculations.jl:140-151).
+// Threads t < nb*na: F_dx_add; the next nb*ne*na: F_d2err_dx_add.
 template <int D>
 __global__ void k_reduce_add(DevProblem P, DevBatch B) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B.nb * P.na) return;
-    const int b = t / P.na, q = t % P.na;
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < B.nb * P.na) {
+        const int b = t / P.na, q = t % P.na;
+        double s = 0.0;
+        for (int k = 0; k < P.Nt; ++k) s += B.part_add[((size_t)b * P.Nt + k) * P.na + q];
+        B.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = B.tgt_part[(size_t)b * P.na + q] + s;
+        return;
+    }
+    t -= B.nb * P.na;
+    if (P.ne == 0 || t >= B.nb * P.ne * P.na) return;
+    const int q = t % P.na, be = t / P.na;  // be = b * ne + e
+    const double *src = B.part_err_add + (size_t)be * P.Nt * P.na + q;
     double s = 0.0;
-    for (int k = 0; k < P.Nt; ++k) s += B.part_add[((size_t)b * P.Nt + k) * P.na + q];
-    B.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = B.tgt_part[(size_t)b * P.na + q] + s;
+    for (int k = 0; k < P.Nt; ++k) s += src[(size_t)k * P.na];
+    B.Fd2dx[(size_t)be * P.nx + (size_t)P.np * P.Nt + q] += s;
 }
 
 }  // namespace grape

@@ -107,7 +107,8 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     }
     if (P.xadd_dep && P.na > 0) {
         mark(GRAPE_KERNEL_REDUCE, 0);
-        hipLaunchKernelGGL(grape::k_reduce_add<D>, dim3((B.nb * P.na + 255) / 256), dim3(256), 0, st, P, B);
+        const int nred = B.nb * P.na * (1 + P.ne);
+        hipLaunchKernelGGL(grape::k_reduce_add<D>, dim3((nred + 255) / 256), dim3(256), 0, st, P, B);
         mark(GRAPE_KERNEL_REDUCE, 1);
     }
     return hipGetLastError();
@@ -141,6 +142,19 @@ hipError_t launch_expm_variants(const DevProblem &P, const DevBatch &B, hipStrea
     return hipGetLastError();
 }
 
+// Closure mode: every variant of every step of ONE launch's evaluations from the host H
+// table B.Htab ([nb][Nt][P.nv][D][D] column-major) into B.E (row-major).
+template <int D>
+hipError_t launch_expm_table(const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    constexpr int GPW = grape::Geo<D>::GPW;
+    const long nexp = (long)B.nb * P.Nt * P.nv;
+    hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
+                       P, B);
+    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
+                       B.overflow_count, B.status, 1);
+    return hipGetLastError();
+}
+
 template <int D, int W>
 hipError_t set_lds_limits_w() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, W>),
@@ -162,6 +176,7 @@ hipError_t set_lds_limits() {
     EXT template hipError_t launch_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &); \
     EXT template hipError_t launch_expm_raw<d>(const cd *, cd *, int, int *, int *, int *, int *, hipStream_t);  \
     EXT template hipError_t set_lds_limits<d>();                                                          \
-    EXT template hipError_t launch_expm_variants<d>(const DevProblem &, const DevBatch &, hipStream_t);
+    EXT template hipError_t launch_expm_variants<d>(const DevProblem &, const DevBatch &, hipStream_t);     \
+    EXT template hipError_t launch_expm_table<d>(const DevProblem &, const DevBatch &, hipStream_t);
 
 }  // namespace grape_host

@@ -235,6 +235,21 @@ __global__ __launch_bounds__(BLOCK) void k_u_interaction(grape::DevProblem P, co
     if (t < DD) O[cm(D, (size_t)e * P.Nt + k, i, j)] = mmh_el(sC, sT, D, i, j);
 }
 
+// closure fallback: O_{k,e} = C_{k-1}^dagger Oerr_{k,e} C_{k-1}, Oerr host-evaluated (column-major)
+__global__ __launch_bounds__(BLOCK) void k_u_interaction_table(grape::DevProblem P, const cd *Oerr, const cd *C,
+                                                               cd *O) {
+    __shared__ cd sC[kMaxD * kMaxD], sH[kMaxD * kMaxD], sT[kMaxD * kMaxD];
+    const int D = P.D, DD = D * D, t = threadIdx.x, i = t / D, j = t % D;
+    const int k = blockIdx.x % P.Nt, e = blockIdx.x / P.Nt;
+    if (k > 0) load_tile(sC, C + (size_t)(k - 1) * DD, D);
+    else identity_tile(sC, D);
+    if (t < DD) sH[t] = Oerr[cm(D, (size_t)k * P.ne + e, i, j)];
+    __syncthreads();
+    if (t < DD) sT[t] = mm_el(sH, sC, D, i, j);
+    __syncthreads();
+    if (t < DD) O[cm(D, (size_t)e * P.Nt + k, i, j)] = mmh_el(sC, sT, D, i, j);
+}
+
 // expectation values: one thread per error source walks the time steps
 __global__ void k_u_expect(grape::DevProblem P, const cd *O, double *ev) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -256,6 +271,11 @@ hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st) {
 
 hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, hipStream_t st) {
     hipLaunchKernelGGL(k_u_interaction, dim3((unsigned)(P.Nt * P.ne)), dim3(BLOCK), 0, st, P, x, C, O);
+    return hipGetLastError();
+}
+
+hipError_t launch_interaction_table(const grape::DevProblem &P, const cd *Oerr, const cd *C, cd *O, hipStream_t st) {
+    hipLaunchKernelGGL(k_u_interaction_table, dim3((unsigned)(P.Nt * P.ne)), dim3(BLOCK), 0, st, P, Oerr, C, O);
     return hipGetLastError();
 }
 

@@ -40,6 +40,9 @@ hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st);
 // O[:, :, k, e] = C_{k-1}^dagger (Herror_e(k, eps) / eps) C_{k-1}, column-major (d, d, Nt, ne)
 // (UnitaryCalculations.jl:180-204); x is the plan's device copy of the control vector
 hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, hipStream_t st);
+// The same from host-evaluated closures (closure fallback): Oerr [Nt][ne][D][D] column-major
+// holds (1/eps) Herror_e(k, x_k, x_add, eps) as the reference forms it
+hipError_t launch_interaction_table(const grape::DevProblem &P, const cd *Oerr, const cd *C, cd *O, hipStream_t st);
 // ev[k + Nt e] = Re(dt tr(W sum_{j<=k} O_j,e) / D)   (FidelityCalculations.jl:368-390)
 hipError_t launch_expectation(const grape::DevProblem &P, const cd *O, double *ev, hipStream_t st);
 

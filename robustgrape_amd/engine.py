@@ -106,7 +106,12 @@ class GrapePlan:
         shapes = [(d, d), (d, d, npar, nt), (d, d, na), (d, d, ne), (d, d, npar, nt, ne), (d, d, na, ne)]
         outs = [np.zeros(sh, dtype=np.complex128, order="F") for sh in shapes]
         ptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if a.size else None
-        _capi.check(_capi.lib().grape_unitary_derivs(self.handle, _capi.dptr(x), *[ptr(a) for a in outs]))
+        if self.tables:  # closure problem: every closure call site evaluated here
+            H, _ = host_tables(self.fp, x[None, :], self.nparam)
+            _capi.check(_capi.lib().grape_unitary_derivs_tables(self.handle, _capi.dptr(x), _capi.dptr(H),
+                                                                *[ptr(a) for a in outs]))
+        else:
+            _capi.check(_capi.lib().grape_unitary_derivs(self.handle, _capi.dptr(x), *[ptr(a) for a in outs]))
         return tuple(outs)
 
     def set_profiling(self, enable: bool):

@@ -115,8 +115,20 @@ def make_c5():
     print("wrote c5", F, hist.tolist())
 
 
+def make_xadd_err():
+    """Error sources with an H0 and an error generator that read x_add (tests/problems.py
+    xadd_err_problem: d = 5, N_t = 40, na = 2, 2 errors), closures through the oracle."""
+    d, nt = 5, 40
+    x = P.xadd_x(nt, 2024)
+    dct = fid(P.xadd_err_problem(d, nt, device=False), x)
+    np.savez_compressed(os.path.join(HERE, "xadd_err.npz"), d=np.int64(d), ntimes=np.int64(nt), **dct)
+    print("wrote xadd_err", dct["F"], dct["F_d2err"])
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["c5"]:
         make_c5()
+    elif sys.argv[1:] == ["xadd_err"]:
+        make_xadd_err()
     else:
         main()

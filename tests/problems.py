@@ -99,3 +99,39 @@ def random_x(ntimes, seed, nparam=1, small=False):
     rng = np.random.default_rng(seed)
     scale = 2 * math.pi * (0.001 if small else 1.0)
     return np.concatenate([scale * rng.uniform(size=ntimes * nparam), [2 * math.pi * rng.uniform()]])
+
+
+def xadd_err_problem(d, ntimes, nerr=2, device=True):
+    """Error sources together with an H0 that reads x_add (UnitaryCalculations.jl:57-64, 87-95,
+    140-151): the d=5 symmetric (runtests.jl:57-75) or d=9 full Rydberg
+    problem with a second additional parameter x_add[1], a global detuning on a diagonal
+    occupation operator, and an error source whose strength is modulated by cos(x_add[1]).
+    x_add[0] stays the target's single-qubit phase.  device=False: the same physics as plain
+    closures (the reference's idiom), which the table path and the oracle evaluate."""
+    from robustgrape_amd.operators import (FN_COS, FN_LINEAR, VAR_XADD, OperatorBasisError,
+                                           OperatorBasisHamiltonian, Term)
+    base = sym_problem(ntimes, errors=("amp", "freq")[:nerr]) if d == 5 else full9_problem(ntimes, nerr=nerr)
+    up = base.unitary_problem
+    Nr = np.diag(np.linspace(0.0, 1.0, d)).astype(np.complex128)
+    H0 = OperatorBasisHamiltonian(list(up.H0.terms) + [Term(Nr, var=VAR_XADD, index=1, func=FN_LINEAR, scale=0.5)])
+    errs = []
+    for e, es in enumerate(up.error_sources):
+        terms = list(es.Herror.terms)
+        if e == 0:
+            terms.append(Term(Nr, var=VAR_XADD, index=1, func=FN_COS, scale=0.3))
+        errs.append(ErrorSource(OperatorBasisError(terms)))
+    target = base.target_unitary
+    if not device:
+        Hdev, tdev, edev = H0, target, errs
+        H0 = lambda t, x, xa: Hdev(t, x, xa)  # noqa: E731
+        target = lambda xa: tdev(xa)  # noqa: E731
+        errs = [ErrorSource(lambda t, x, xa, e, es=es: es.Herror(t, x, xa, e)) for es in edev]
+    up2 = UnitaryRobustGRAPEProblem(t0=up.t0, ntimes=ntimes, ndim=d, H0=H0, nb_additional_param=2,
+                                    error_sources=errs)
+    return FidelityRobustGRAPEProblem(up2, base.projector, target)
+
+
+def xadd_x(ntimes, seed):
+    """Control vector of xadd_err_problem: x_main = 2pi U, theta = 2pi U, detuning U[-0.5, 0.5)."""
+    rng = np.random.default_rng(seed)
+    return np.concatenate([2 * math.pi * rng.uniform(size=ntimes), [2 * math.pi * rng.uniform(), rng.uniform(-0.5, 0.5)]])

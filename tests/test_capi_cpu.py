@@ -76,19 +76,23 @@ def test_closure_problems_take_the_table_descriptor():
     np.testing.assert_array_equal(H[1, k, 1], np.asarray(up.H0(k + 1, np.array([x[k] + eps]), x[-1:])).T)
     np.testing.assert_array_equal(H[1, k, 2], Hk.T)  # H0 ignores x_add: the dxa variant equals the nominal
     np.testing.assert_array_equal(U0[0, 1], np.asarray(fp.target_unitary(x[-1:] + eps)).T)
-    # with error sources: 1 + 2 np + ne (2 + np) variants in the UnitaryCalculations.jl:45-78 order
+    # with error sources: n = np + na gradient parameters, 1 + 2 n + ne (2 + n) variants in the
+    # UnitaryCalculations.jl:45-95 order (x_add sites included: closures may read x_add)
     fe = P.sym_problem(4, errors=("amp", "freq"), device=False)
     assert TableDescriptor(fe, nparam=1).desc.nerr == 2
     He, _ = host_tables(fe, x[None, :], 1)
-    assert He.shape == (1, 4, 1 + 2 + 2 * 3, 5, 5)
+    assert He.shape == (1, 4, 1 + 2 * 2 + 2 * 4, 5, 5)
     upe = fe.unitary_problem
     xk, xa = np.array([x[k]]), x[-1:]
     H0k = np.asarray(upe.H0(k + 1, xk, xa), complex)
-    np.testing.assert_array_equal(He[0, k, 2], np.asarray(upe.H0(k + 1, xk + upe.eps2, xa)).T)  # dx2
+    np.testing.assert_array_equal(He[0, k, 3], np.asarray(upe.H0(k + 1, xk + upe.eps2, xa)).T)  # dx2
+    np.testing.assert_array_equal(He[0, k, 4], np.asarray(upe.H0(k + 1, xk, xa + upe.eps2)).T)  # dxa2
     herr = upe.error_sources[1].Herror
-    np.testing.assert_array_equal(He[0, k, 6], (np.asarray(herr(k + 1, xk, xa, upe.eps)) + H0k).T)  # freq, eps
+    np.testing.assert_array_equal(He[0, k, 9], (np.asarray(herr(k + 1, xk, xa, upe.eps)) + H0k).T)  # freq, eps
     mix = np.asarray(herr(k + 1, xk + upe.eps2, xa, upe.eps2)) + np.asarray(upe.H0(k + 1, xk + upe.eps2, xa))
-    np.testing.assert_array_equal(He[0, k, 8], mix.T)  # freq, mixed stencil
+    np.testing.assert_array_equal(He[0, k, 11], mix.T)  # freq, mixed stencil (control)
+    mixa = np.asarray(herr(k + 1, xk, xa + upe.eps2, upe.eps2)) + np.asarray(upe.H0(k + 1, xk, xa + upe.eps2))
+    np.testing.assert_array_equal(He[0, k, 12], mixa.T)  # freq, mixed stencil (x_add)
 
 
 def test_non_diagonal_projector_rejected():

@@ -132,7 +132,9 @@ def test_optimiser_on_closure_problem():
         c, g = cost(torch.as_tensor(X, device="cuda"))
         cost.close()
         costs.append((c.cpu().numpy(), g.cpu().numpy()))
-    np.testing.assert_allclose(costs[1][0], costs[0][0], rtol=0, atol=1e-10)
+    # the cost carries c_e F_d2err^2: an eps-FD quantity (tier T2; the two paths round the
+    # sensitivity differently at ~2e-9 relative), not a T1 one
+    np.testing.assert_allclose(costs[1][0], costs[0][0], rtol=1e-8, atol=0)
     assert np.max(np.abs(costs[1][1] - costs[0][1])) <= T3 * np.max(np.abs(costs[0][1])) + T2_ABS
     res = OPT.optimize_fidelity_and_error_sources(fph, _params(X[0], nerr=1, iterations=3))
     assert np.isfinite(res.minimum)

@@ -152,15 +152,22 @@ def test_closure_error_sources_match_live_oracle(d, ntimes, errors):
     _assert_err(1, e, ed, e0, ed0)
 
 
-def test_closure_error_sources_with_xadd_dependent_h0_are_refused():
+def test_closure_error_sources_with_xadd_dependent_h0():
+    """Formerly refused (round 1): an x_add-dependent closure H0 with an error source now takes
+    every x_add call site of the reference (UnitaryCalculations.jl:57-64, 87-95)."""
+    from oracle import grape_oracle as O
     from robustgrape_amd import calculate_fidelity_and_derivatives
     from robustgrape_amd.types import ErrorSource
     fp = _xadd_problem(4, 5, 1)
     up = fp.unitary_problem
     Hz = np.diag(np.arange(4.0))
-    fp = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, x, xa, e: e * Hz)]))
-    with pytest.raises(NotImplementedError):
-        calculate_fidelity_and_derivatives(fp, np.concatenate([np.zeros(5), [0.3, 0.2]]))
+    fp = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, x, xa, e: e * np.cos(xa[1]) * Hz)]))
+    x = np.concatenate([np.linspace(-0.5, 0.5, 5), [0.3, 0.2]])
+    F0, g0, e0, ed0 = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, e, ed = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0)
+    _assert_err(0, e, ed, e0, ed0)
+    assert np.max(np.abs(ed0[-2:])) > 1e-3
 
 
 @pytest.mark.parametrize("d", list(range(2, 13)))
@@ -183,7 +190,7 @@ def test_every_dimension_with_errors_through_tables(d):
 
 def test_table_plan_chunks_batches_and_refuses_the_operator_entry_points():
     """nbatch > max_batch runs in chunks (bitwise equal to single calls); a table plan
-    refuses grape_fidelity_grad / grape_unitary_derivs loudly."""
+    refuses the operator-basis entry point grape_fidelity_grad loudly."""
     from robustgrape_amd import GrapePlan, calculate_fidelity_and_derivatives
     from robustgrape_amd._capi import GrapeError
     fp = P.sym_problem(20, errors=("amp",), device=False)
@@ -194,8 +201,6 @@ def test_table_plan_chunks_batches_and_refuses_the_operator_entry_points():
         Fs, gs, es, eds = calculate_fidelity_and_derivatives(fp, X[b])
         assert Fs == F[b] and np.array_equal(gs, Fdx[b]) and np.array_equal(es, d2[b])
         assert np.array_equal(eds, d2dx[b])
-    with pytest.raises(GrapeError):
-        plan.unitary_derivs(X[0])
     from robustgrape_amd import _capi
     F1, G1 = np.empty(1), np.empty((1, 21))
     with pytest.raises(GrapeError):
