@@ -292,7 +292,7 @@ typedef enum grape_kernel {
     GRAPE_KERNEL_EXPM = 0,      /* propagators of every FD variant (Pade m <= 5) */
     GRAPE_KERNEL_EXPM_HIGH = 1, /* Pade m = 7/9/13 items parked by the above */
     GRAPE_KERNEL_SCAN = 2,      /* chunked prefix products, fidelity, gradient kernels */
-    GRAPE_KERNEL_GRAD = 3,      /* per-step gradient contractions (error-source pipeline) */
+    GRAPE_KERNEL_GRAD = 3,      /* per-step contractions: k_grad (closure tables, no error sources) / k_err_local (error sources) */
     GRAPE_KERNEL_REDUCE = 4,    /* x_add reductions */
     GRAPE_KERNEL_ERR_SCAN = 5,  /* error sources: U_derr, F_d2err, per-chunk kernels */
     GRAPE_KERNEL_ERR_GRAD = 6,  /* error sources: F_d2err_dx contractions */

@@ -125,6 +125,7 @@ struct grape_plan {
     int *d_ovf2 = nullptr;
     cd *d_ovf2_slots = nullptr;
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr, *d_part_err = nullptr;
+    cd *d_Zl = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
     // closure mode (GRAPE_DESC_HOST_TABLES): host-evaluated H and target tables
@@ -167,7 +168,7 @@ static void free_plan(grape_plan *p) {
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
-                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_ovf2, p->d_ovf2_slots,
+                    p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_Zl, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf,
                     p->d_Htab, p->d_U0tab};
@@ -459,6 +460,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     // only the nominal propagators are stored (k_expm_grad consumes the rest in place)
     // host tables: every variant's propagator is stored (k_grad reads them back)
     P.nv = (desc->nerr > 0 || tables) ? (int)vs.size() : 1;
+    P.nvg = desc->nparam + nad;
+    P.nz = P.nvg * (1 + desc->nerr) + desc->nerr;
     P.dt = desc->t0 / desc->ntimes;
     P.eps = desc->eps;
     P.eps2 = desc->eps2;
@@ -516,6 +519,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
              dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
+    if (ok && P.ne > 0) ok = dalloc(&p->d_Zl, MB * P.Nt * P.nz * T) == hipSuccess;
     if (ok && P.ne > 0 && P.xadd_dep)
         ok = dalloc(&p->d_part_err, MB * P.ne * P.Nt * P.na) == hipSuccess;
     if (ok && tables)
@@ -621,6 +625,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         B.Ub = p->d_Ub;
         B.Me = p->d_Me;
         B.part_err_add = p->d_part_err;
+        B.Zl = p->d_Zl;
     }
     // ctrl: [2] status (sticky until grape_plan_synchronize reports it),
     // [4] k_expm overflow count, [5] k_expm_grad overflow count

@@ -5,69 +5,33 @@
 // src/FidelityCalculations.jl:78-113 (F_d2err, F_d2err_dx).
 //
 // Interaction-picture algebra (C_k = Q_k Carry_c for step k of chunk c,
-// C_k^-1 = C_k^dagger):
-//   V^err_k = C_k^dag dE^err_k C_{k-1} = Carry_c^dag W_k Carry_c,  W_k = Q_k^dag dE^err_k Q_{k-1}
-//   U_derr  = U * Tot,  Tot = sum_k V^err_k                        (UnitaryCalculations.jl:122-123)
-//   F_d2err_dx[p,k] = Re tr(G_e U_derr_dx[p,k]),  M_e = G_e U,
+// C_k^-1 = C_k^dagger), for one evaluation and error e:
+//   local frame of step k:  Y(dX) = Q_k^dag dX Q_{k-1}   (Q_{k-1} = I at a chunk start)
+//   W_k = Y(dE^err_k),  Z1_{k,u} = Y(dE^dx_u),  Z2_{k,u} = Y(dE^mix_{u})  (UnitaryCalculations.jl:48-95)
+//   V^err_k = Carry_c^dag W_k Carry_c;  U_derr = U * Tot,  Tot = sum_k V^err_k       (:122-123)
+//   F_d2err_dx[u,k] = Re tr(G_e U_derr_dx[u,k]),  M_e = G_e U,                  (FidelityCalculations.jl:85-113)
 //     G_e = 4[P Ue^dag U0 W U0^dag + conj(tau_e) W U0^dag - (1+D) W Ue^dag]/(D(D+1))
-//   and with Z1 = Q_k^dag dE^dx Q_{k-1}, Z2 = Q_k^dag dE^mix Q_{k-1},
-//     M' = Carry M_e Carry^dag, A_k = Carry S_{k-1} Carry^dag, Ttot = Carry Tot Carry^dag:
-//   F_d2err_dx[p,k,e] = Re[ tr(A_k (M' Z1)) + tr((Ttot - A_k - W_k)(Z1 M')) + tr(M' Z2) ]
-//   (S_{k-1} = cumsum up to k-1 and R_{k+1} = Tot - S_{k-1} - V_k: :112-113, :124-139).
+//   with M' = Carry M_e Carry^dag, A_k = Carry S_{k-1} Carry^dag (S = cumsum, :112; R_{k+1} =
+//   Tot - S_{k-1} - V_k, :113) and Ttot = Carry Tot Carry^dag, the reference's
+//   U (V^dx S_{k-1} + R_{k+1} V^dx + V^mix) contracted with G_e (:124-139) is
+//     Re[ tr(A_k M' Z1) + tr((Ttot - A_k - W_k) Z1 M') + tr(M' Z2) ]
+//   = Re[ tr(Lambda_k Z1) + tr(M' Z2) ],  Lambda_k = [A_k, M'] + M' Ttot - M' W_k.
+//   The running state B_k = [A_k, M'] + M' Ttot obeys B_{k+1} = B_k + W_k M' - M' W_k
+//   (A_{k+1} = A_k + W_k), so a step costs two products per error.  The same Z1 gives the
+//   fidelity gradient F_dx[u,k] = Re tr(M'_c Z1_{k,u}) (FidelityCalculations.jl:56-76).
 //
+// k_err_local one row group per (b, k): every local-frame image Z1_u, W_e, Z2_{e,u} of
+//             step k (2 products each, Q_k / Q_{k-1} staged once), stored to Zl; F_dx.
 // k_err_scan  one workgroup per (b, e): chunk totals of W, carry transform,
 //             additive scan over chunks, U_derr, F_d2err, M_e, per-chunk M', T, Ttot.
-// k_err_grad  one row group per (b, chunk, e): walks the chunk's steps, 8 products/step
-//             per gradient parameter (controls; x_add too when H0 / Herror read it,
-//             U_derr_dx_add being the sum over k of the same per-step terms, :140-151).
+// k_err_grad  one row group per (b, chunk, e): walks the chunk's steps carrying B_k,
+//             two products per step (M' W_k, W_k M') and the traces per gradient
+//             parameter (controls; x_add too when H0 / Herror read it, U_derr_dx_add
+//             being the sum over k of the same per-step terms, :140-151).
 #pragma once
 #include "grape_kernels.hpp"
 
 namespace grape {
-
-// E-variant row (E_v - E_0) * s  (the reference's (1/eps) * (E' - E))
-template <int D>
-__device__ __forceinline__ void delta_row(const cd *Ek, int v, int i, double s, cd (&out)[D]) {
-    const cd *e0 = Ek + i * D;
-    const cd *ev = Ek + (size_t)v * D * D + i * D;
-#pragma unroll
-    for (int j = 0; j < D; ++j) out[j] = cscale(s, csub(ev[j], e0[j]));
-}
-
-// Local-frame transform Z = Q_k^dag X Q_{k-1} (Q_{k-1} = I at a chunk start).
-// x: this lane's row of X (destroyed); z: row of Z.  Uses the group tile.
-template <int D>
-__device__ __forceinline__ void local_frame(Group<D> &G, const cd *Qk, bool first, cd (&x)[D], cd (&z)[D],
-                                            bool wr) {
-    const int i = G.i;
-    tile_store_row(G, x, wr);
-    gsync();
-    cd l[D];
-#pragma unroll
-    for (int r = 0; r < D; ++r) l[r] = cconj(Qk[r * D + i]);  // column i of Q_k, conjugated
-    mm_tile<D>(l, G.tile, z);
-    gsync();
-    if (!first) {
-        if (wr) {
-#pragma unroll
-            for (int j = 0; j < D; ++j) G.tile[i * D + j] = Qk[i * D + j - D * D];  // Q_{k-1}
-        }
-        gsync();
-#pragma unroll
-        for (int j = 0; j < D; ++j) x[j] = z[j];
-        mm_tile<D>(x, G.tile, z);
-        gsync();
-    }
-}
-
-// sum_j a[j] * X[j][i] for the tile X (trace helper: tr(A X) = sum_i row_i(A) . col_i(X))
-template <int D>
-__device__ __forceinline__ cd row_dot_col(const cd (&a)[D], const cd *X, int i) {
-    cd s = czero();
-#pragma unroll
-    for (int j = 0; j < D; ++j) s = cadd(s, cmul(a[j], X[j * D + i]));
-    return s;
-}
 
 template <int D, int W>
 __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
@@ -82,23 +46,17 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
     const int b = blockIdx.x / P.ne, e = blockIdx.x % P.ne;
     const bool gvalid = G.lane_ok && c < P.nchunks;
     auto tile_of = [&](int cc) -> cd * { return lds + (cc / GPW) * GPW * GCD + (cc % GPW) * GCD; };
-    const cd *Eb = B.E + (size_t)b * P.Nt * P.nv * TILE;
-    const cd *Qb = B.Q + (size_t)b * P.Nt * TILE;
-    const int v_err = P.off_err + e * P.err_stride;
-
-    // Phase A: chunk total of W_k = Q_k^dag dE^err_k Q_{k-1}
+    // Phase A: chunk total of the stored W_k = Q_k^dag dE^err_k Q_{k-1} (k_err_local)
     cd acc[D], x[D], w[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) acc[j] = czero();
+    const int w_slot = P.nvg + e;
     for (int j = 0; j < P.L; ++j) {
         const int k = c * P.L + j;
-        const bool act = gvalid && k < P.Nt;
-        const int kc = act ? k : 0;
-        delta_row<D>(Eb + (size_t)kc * P.nv * TILE, v_err, i, P.inv_eps, x);
-        local_frame<D>(G, Qb + (size_t)kc * TILE, j == 0, x, w, act);
-        if (act) {
+        if (gvalid && k < P.Nt) {
+            const cd *Wk = B.Zl + ((size_t)(b * P.Nt + k) * P.nz + w_slot) * TILE + i * D;
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) acc[jj] = cadd(acc[jj], w[jj]);
+            for (int jj = 0; jj < D; ++jj) acc[jj] = cadd(acc[jj], Wk[jj]);
         }
     }
     // Phase A': Vc_c = Carry_c^dag (sum W) Carry_c  -> own tile
@@ -274,15 +232,110 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
     }
 }
 
-#ifndef GRAPE_ERRGRAD_WAVES
-#define GRAPE_ERRGRAD_WAVES 2  // 2 waves/SIMD (308 B/lane of spills) beat 1 (336 registers): 2.51 -> 2.23 ms, C3 B=256
-#endif
+// LDS of the error-path row-group kernels: per group its tile + aux, then one more tile
 template <int D>
-__global__ __launch_bounds__(64, GRAPE_ERRGRAD_WAVES) void k_err_grad(DevProblem P, DevBatch B) {
+__device__ __forceinline__ cd *second_tile(cd *lds, const Group<D> &G) {
+    return lds + Geo<D>::GPW * Geo<D>::GROUP_CD + G.g * Geo<D>::TILE;
+}
+
+// k_err_local: one row group per (b, k).  Lane i holds column i of each difference dX
+// (coalesced loads of the row-major E tiles) and produces row i of Q_k^dag dX Q_{k-1}:
+//   row i of Q_k^dag X = conj(column i of Q_k) . X   (X staged in the group tile)
+//   then . Q_{k-1}                                   (Q_{k-1} staged once in the second tile)
+// (A column-form variant with coalesced Zl stores measured 11 % slower.)
+template <int D>
+__global__ __launch_bounds__(64, 2) void k_err_local(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     constexpr int TILE = Geo<D>::TILE;
     Group<D> G = make_group<D>(lds, threadIdx.x);
+    cd *Qp = second_tile<D>(lds, G);
+    const long nitems = (long)B.nb * P.Nt;
+    const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
+    const bool valid = G.lane_ok && gid < nitems;
+    const long gidc = valid ? gid : 0;
+    const int k = (int)(gidc % P.Nt), b = (int)(gidc / P.Nt);
+    const int c = k / P.L;
+    const bool first = k == c * P.L;  // chunk start: Q_{k-1} = I
+    const int i = G.i;
+    const cd *Qk = B.Q + ((size_t)b * P.Nt + k) * TILE;
+    const cd *Ek = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE;
+    cd *Zk = B.Zl + (((size_t)b * P.Nt + k) * P.nz) * TILE;
+    if (valid && !first) {
+#pragma unroll
+        for (int m = 0; m < D; ++m) Qp[m * D + i] = Qk[m * D + i - TILE];
+    }
+    cd qc[D], e0[D], x[D], y[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        qc[m] = cconj(Qk[m * D + i]);
+        e0[m] = Ek[m * D + i];
+    }
+    // y <- row i of Q_k^dag X Q_{k-1} for the column x of X (x destroyed), stored to slot
+    auto frame = [&](int slot) {
+        if (valid) {
+#pragma unroll
+            for (int m = 0; m < D; ++m) G.tile[m * D + i] = x[m];
+        }
+        gsync();
+        mm_tile<D>(qc, G.tile, y);
+        gsync();
+        if (!first) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) x[j] = y[j];
+            mm_tile<D>(x, Qp, y);
+        }
+        if (valid) {
+            cd *dst = Zk + (size_t)slot * TILE + i * D;
+#pragma unroll
+            for (int j = 0; j < D; ++j) dst[j] = y[j];
+        }
+    };
+    // gradient parameters: Z1_u = Y((E_u - E_0) / eps) and F_dx[u,k] = Re tr(M'_c Z1_u)
+    const cd *Mc = B.Mc + ((size_t)b * P.nchunks + c) * TILE;
+    for (int u = 0; u < P.nvg; ++u) {
+        const cd *Ev = Ek + (size_t)(P.off_dx + u) * TILE;
+#pragma unroll
+        for (int m = 0; m < D; ++m) x[m] = cscale(P.inv_eps, csub(Ev[m * D + i], e0[m]));  // (1/eps)(E' - E)
+        frame(u);
+        double s = 0.0;  // sum_j Z1[i][j] M'[j][i]
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd mm = Mc[j * D + i];
+            s += y[j].re * mm.re - y[j].im * mm.im;
+        }
+        s = group_sum(G, s, valid);
+        if (valid && i == 0) {
+            if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+            else B.part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
+        }
+    }
+    for (int e = 0; e < P.ne; ++e) {
+        const int v_err = P.off_err + e * P.err_stride;
+        const cd *Ee = Ek + (size_t)v_err * TILE;
+#pragma unroll
+        for (int m = 0; m < D; ++m) x[m] = cscale(P.inv_eps, csub(Ee[m * D + i], e0[m]));
+        frame(P.nvg + e);  // W_e
+        for (int u = 0; u < P.nvg; ++u) {
+            // dE^mix = (E(u + eps2, err eps2) + E - E(err eps2) - E(u + eps2)) / eps2^2  (:79-83, :91-94)
+            const cd *em = Ek + (size_t)(v_err + 2 + u) * TILE, *ee2 = Ek + (size_t)(v_err + 1) * TILE;
+            const cd *ed2 = Ek + (size_t)(P.off_dx2 + u) * TILE;
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+                x[m] = cscale(P.inv_eps2sq, csub(csub(cadd(em[m * D + i], e0[m]), ee2[m * D + i]), ed2[m * D + i]));
+            frame(P.nvg + P.ne + e * P.nvg + u);  // Z2_{e,u}
+        }
+    }
+}
+
+// k_err_grad: one row group per (b, chunk, e), lane i holding row i of B_k.
+template <int D>
+__global__ __launch_bounds__(64, 2) void k_err_grad(DevProblem P, DevBatch B) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    cd *lds = reinterpret_cast<cd *>(smem_raw);
+    constexpr int TILE = Geo<D>::TILE;
+    Group<D> G = make_group<D>(lds, threadIdx.x);
+    cd *Mt = second_tile<D>(lds, G);  // M' (constant over the chunk)
     const long nitems = (long)B.nb * P.nchunks * P.ne;
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
@@ -291,79 +344,67 @@ __global__ __launch_bounds__(64, GRAPE_ERRGRAD_WAVES) void k_err_grad(DevProblem
     const int c = (int)((gc / P.ne) % P.nchunks);
     const int b = (int)(gc / ((long)P.ne * P.nchunks));
     const int i = G.i;
-    const cd *Eb = B.E + (size_t)b * P.Nt * P.nv * TILE;
-    const cd *Qb = B.Q + (size_t)b * P.Nt * TILE;
-    const cd *Mo = B.Me + (((size_t)b * P.ne + e) * P.nchunks + c) * 3 * TILE;
-    const cd *Mp = Mo, *Tc = Mo + TILE, *Tt = Mo + 2 * TILE;
-    const int v_err = P.off_err + e * P.err_stride, v_err2 = v_err + 1;
+    const cd *Mo = B.Me + (((size_t)b * P.ne + e) * P.nchunks + c) * 3 * TILE;  // M', Tc, Ttot
     double *out = B.Fd2dx + ((size_t)b * P.ne + e) * P.nx;
-    const int nvg = P.np + (P.xadd_dep ? P.na : 0);
-    cd A[D], Wk[D], z1[D], x[D], t[D];
+    cd mrow[D], bp[D], w[D], t[D];
 #pragma unroll
-    for (int jj = 0; jj < D; ++jj) A[jj] = Tc[i * D + jj];
-    for (int j = 0; j < P.L; ++j) {
-        const int k = c * P.L + j;
+    for (int j = 0; j < D; ++j) {
+        mrow[j] = Mo[i * D + j];
+        w[j] = Mo[TILE + i * D + j];  // Tc = A at the chunk start
+    }
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) Mt[i * D + j] = mrow[j];
+    }
+    tile_store_row(G, w, valid);
+    gsync();
+    // B = Tc M' - M' Tc + M' Ttot
+    mm_tile<D>(w, Mt, bp);
+    mm_tile<D>(mrow, G.tile, t);
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        bp[j] = csub(bp[j], t[j]);
+        w[j] = Mo[2 * TILE + i * D + j];
+    }
+    gsync();
+    tile_store_row(G, w, valid);
+    gsync();
+    mm_tile<D>(mrow, G.tile, t);
+#pragma unroll
+    for (int j = 0; j < D; ++j) bp[j] = cadd(bp[j], t[j]);
+    gsync();
+    const int w_slot = P.nvg + e, z2_slot = P.nvg + P.ne + e * P.nvg;
+    for (int jstep = 0; jstep < P.L; ++jstep) {
+        const int k = c * P.L + jstep;
         const bool act = valid && k < P.Nt;
         const int kc = act ? k : 0;
-        const cd *Ek = Eb + (size_t)kc * P.nv * TILE;
-        const cd *Qk = Qb + (size_t)kc * TILE;
-        delta_row<D>(Ek, v_err, i, P.inv_eps, x);
-        local_frame<D>(G, Qk, j == 0, x, Wk, act);  // W_k
-        for (int p = 0; p < nvg; ++p) {  // controls, then x_add (xadd_dep): variants off_dx + p
-            delta_row<D>(Ek, P.off_dx + p, i, P.inv_eps, x);
-            local_frame<D>(G, Qk, j == 0, x, z1, act);  // Z1 = Q^dag dE^dx Q
-            // S1 = tr(A (M' Z1))
-            tile_store_row(G, z1, act);
-            gsync();
+        const cd *Zk = B.Zl + ((size_t)b * P.Nt + kc) * P.nz * TILE;
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) x[jj] = Mp[i * D + jj];
-            mm_tile<D>(x, G.tile, t);  // (M' Z1) row i
-            gsync();
-            tile_store_row(G, t, act);
-            gsync();
-            cd s = row_dot_col<D>(A, G.tile, i);
-            gsync();
-            // S2 = tr((Ttot - A - W)(Z1 M'))
-            if (act) {
+        for (int j = 0; j < D; ++j) w[j] = Zk[(size_t)w_slot * TILE + i * D + j];  // row i of W_k
+        tile_store_row(G, w, valid);
+        gsync();
+        mm_tile<D>(mrow, G.tile, t);  // M' W
 #pragma unroll
-                for (int jj = 0; jj < D; ++jj) G.tile[i * D + jj] = Mp[i * D + jj];
+        for (int j = 0; j < D; ++j) bp[j] = csub(bp[j], t[j]);  // Lambda_k
+        for (int u = 0; u < P.nvg; ++u) {
+            const cd *z1 = Zk + (size_t)u * TILE + i, *z2 = Zk + (size_t)(z2_slot + u) * TILE + i;
+            double s = 0.0;  // sum_j Lambda[i][j] Z1[j][i] + M'[i][j] Z2[j][i]
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const cd a = z1[j * D], bz = z2[j * D];
+                s += bp[j].re * a.re - bp[j].im * a.im;
+                s += mrow[j].re * bz.re - mrow[j].im * bz.im;
             }
-            gsync();
-            mm_tile<D>(z1, G.tile, t);  // (Z1 M') row i
-            gsync();
-            tile_store_row(G, t, act);
-            gsync();
-#pragma unroll
-            for (int jj = 0; jj < D; ++jj) x[jj] = csub(csub(Tt[i * D + jj], A[jj]), Wk[jj]);
-            s = cadd(s, row_dot_col<D>(x, G.tile, i));
-            gsync();
-            // S3 = tr(M' Z2), dE^mix = (E_mix + E - E_err2 - E_dx2) / eps2^2  (UnitaryCalculations.jl:79-83)
-            {
-                const cd *e0 = Ek + i * D;
-                const cd *em = Ek + (size_t)(v_err + 2 + p) * TILE + i * D;
-                const cd *ee2 = Ek + (size_t)v_err2 * TILE + i * D;
-                const cd *ed2 = Ek + (size_t)(P.off_dx2 + p) * TILE + i * D;
-#pragma unroll
-                for (int jj = 0; jj < D; ++jj)
-                    x[jj] = cscale(P.inv_eps2sq, csub(csub(cadd(em[jj], e0[jj]), ee2[jj]), ed2[jj]));
-            }
-            local_frame<D>(G, Qk, j == 0, x, t, act);  // Z2
-            tile_store_row(G, t, act);
-            gsync();
-#pragma unroll
-            for (int jj = 0; jj < D; ++jj) x[jj] = Mp[i * D + jj];
-            s = cadd(s, row_dot_col<D>(x, G.tile, i));
-            gsync();
-            const double tot = group_sum(G, s.re, act);
+            s = group_sum(G, s, valid);
             if (act && i == 0) {
-                if (p < P.np) out[(size_t)k * P.np + p] = tot;
-                else B.part_err_add[(((size_t)b * P.ne + e) * P.Nt + k) * P.na + (p - P.np)] = tot;
+                if (u < P.np) out[(size_t)k * P.np + u] = s;
+                else B.part_err_add[(((size_t)b * P.ne + e) * P.Nt + k) * P.na + (u - P.np)] = s;
             }
         }
-        if (act) {
+        mm_tile<D>(w, Mt, t);  // W M'
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) A[jj] = cadd(A[jj], Wk[jj]);
-        }
+        for (int j = 0; j < D; ++j) bp[j] = cadd(bp[j], t[j]);  // B_{k+1} = Lambda_k + W_k M'
+        gsync();
     }
 }
 

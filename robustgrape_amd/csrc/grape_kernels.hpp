@@ -62,6 +62,7 @@ struct DevProblem {
     int scan_waves;      // waves per k_scan / k_err_scan workgroup (4 or 8)
     // variant layout (see grape_engine.hip: build_variants)
     int off_dx, off_dxa, off_dx2, off_err, err_stride;
+    int nvg, nz;         // gradient parameters (np + x_add when xadd_dep); local-frame slots per step (error path)
     double dt, eps, eps2, inv_eps, inv_eps2sq, DD, Dtr;
     const cd *ops;       // [n_ops][D][D] row-major
     const cd *opsT;      // [n_ops][D][D] column-major (column builds for the exp kernels)
@@ -86,6 +87,8 @@ struct DevBatch {
     cd *Carry;              // [nb][nchunks][D][D]  C_{cL-1} (identity for c = 0)
     cd *Ub;                 // [nb][D][D]           U = C_Nt
     cd *Me;                 // [nb][ne][nchunks][3][D][D]  M'_{c,e}, T_c, Ttot_c (error path)
+    cd *Zl;                 // [nb][Nt][nz][D][D]  local-frame differences (error path, k_err_local):
+                            //   Z1_u (nvg) | W_e (ne) | Z2_{e,u} (ne x nvg), row-major
     double *Fd2;            // [nb][ne]
     double *Fd2dx;          // [nb][ne][nx]
     double *part_err_add;   // [nb][ne][Nt][na]  per-step x_add terms of F_d2err_dx (xadd_dep only)

@@ -23,6 +23,10 @@ constexpr int kScanWide = 8, kScanNarrow = 4;
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
 template <int D>
+size_t errpath_lds() {  // per group: tile + aux, then a second tile (k_err_local, k_err_grad)
+    return (size_t)grape::Geo<D>::GPW * (grape::Geo<D>::GROUP_CD + grape::Geo<D>::TILE) * sizeof(cd);
+}
+template <int D>
 size_t errscan_lds(int W) {
     return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 4 * grape::Geo<D>::TILE) * sizeof(cd);
 }
@@ -83,11 +87,17 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
         mark(GRAPE_KERNEL_GRAD_HIGH, 0);
         hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
         mark(GRAPE_KERNEL_GRAD_HIGH, 1);
-    } else {
+    } else if (P.ne == 0) {
         const long ng = (long)B.nb * P.Nt;
         mark(GRAPE_KERNEL_GRAD, 0);
         hipLaunchKernelGGL(grape::k_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
                            P, B);
+        mark(GRAPE_KERNEL_GRAD, 1);
+    } else {  // error sources: local-frame images of every difference (and F_dx) per step
+        const long ng = (long)B.nb * P.Nt;
+        mark(GRAPE_KERNEL_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_err_local<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), errpath_lds<D>(),
+                           st, P, B);
         mark(GRAPE_KERNEL_GRAD, 1);
     }
     if (P.ne > 0) {
@@ -102,7 +112,7 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
         const long ne_items = (long)B.nb * P.nchunks * P.ne;
         mark(GRAPE_KERNEL_ERR_GRAD, 0);
         hipLaunchKernelGGL(grape::k_err_grad<D>, dim3((unsigned)((ne_items + GPW - 1) / GPW)), dim3(64),
-                           expm_lds<D>(), st, P, B);
+                           errpath_lds<D>(), st, P, B);
         mark(GRAPE_KERNEL_ERR_GRAD, 1);
     }
     if (P.xadd_dep && P.na > 0) {
