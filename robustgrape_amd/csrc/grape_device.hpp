@@ -81,6 +81,9 @@ struct Geo {
     static constexpr int TILE = D * D;          // complex elements per matrix tile
     static constexpr int AUX = 2 * D + 1;       // complex scratch per group (pivot row + reciprocal / reductions)
     static constexpr int GROUP_CD = TILE + AUX; // LDS complex elements per group
+    // groups that only need the tile and a group reduction (D doubles): the solve-free
+    // exponential kernels -- a smaller LDS footprint lets more one-wave workgroups share a CU
+    static constexpr int LEAN_CD = TILE + (D + 1) / 2;
 };
 
 // Per-lane view of its group.
@@ -95,12 +98,12 @@ struct Group {
 };
 
 template <int D>
-__device__ __forceinline__ Group<D> make_group(cd *wave_lds, int lane) {
+__device__ __forceinline__ Group<D> make_group(cd *wave_lds, int lane, int stride = Geo<D>::GROUP_CD) {
     Group<D> G;
     G.lane_ok = lane < Geo<D>::GPW * D;
     G.g = G.lane_ok ? lane / D : Geo<D>::GPW - 1;
     G.i = G.lane_ok ? lane % D : 0;
-    G.tile = wave_lds + G.g * Geo<D>::GROUP_CD;
+    G.tile = wave_lds + G.g * stride;
     G.aux = G.tile + Geo<D>::TILE;
     return G;
 }
@@ -518,6 +521,99 @@ __device__ __forceinline__ void pade_finish(Group<D> &G, const cd (&v)[D], const
     }
     if (GENERAL) gesv_cols<D>(G, y, x, wr, singular);
     else gesv_cols_nopivot<D>(G, y, x, wr);
+}
+
+// ---------------------------------------------------------------------------
+// Low-norm regime (Julia's Pade 3 / 5, |A|_1 <= 0.25) without a linear solve.
+//
+// Julia's exp! evaluates r_m(A) = q_m(A)^-1 p_m(A), whose backward error is below
+// u = 2^-53 in this regime (Higham's theta_3 = 0.015, theta_5 = 0.25).  The device
+// evaluates the Taylor polynomial of the same accuracy instead: degree 12 for
+// |A|_1 <= 0.25 (remainder |A|^13/13! <= 2.4e-18) and degree 6 for |A|_1 <= 0.015
+// (<= 3.4e-17).  Both approximants agree with exp(A) -- and with each other -- to a
+// few u, inside the T0 tier (1e-13), and both are smooth in A, so the eps-differences
+// of the reference keep their u/eps rounding floor.  What the change buys on gfx950:
+// no elimination (its per-pivot broadcasts are one-lane VALU work and LDS round
+// trips), two tile images in all (A, then A^3) and no rebuild of A.  Products:
+// degree 12: A^2, A^3 + 3 Horner steps = 5 (Pade 5: 3 + the LU solve); degree 6: 3.
+// Measured (C2, 16 384 evaluations per pass): k_expm_grad 41.5 -> 37.7 ms, C2
+// 748k -> 810k evals/s; C3 67.7k -> 76.1k (a Horner-in-A^2 variant with 6 products was
+// slower than Pade in k_expm_grad: 47.5 ms).  -DGRAPE_LOW_PADE=1 restores Pade 3 / 5.
+// ---------------------------------------------------------------------------
+__constant__ const double kInvFact[13] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720,
+                                          1.0 / 5040, 1.0 / 40320, 1.0 / 362880, 1.0 / 3628800,
+                                          1.0 / 39916800, 1.0 / 479001600};
+
+// Degree choice without square roots: the column sums of |re| + |im| bound the 1-norm
+// from above (|z| <= |re| + |im|), so a group whose bound is <= 0.25 is in the low regime
+// for sure; only groups above it take the exact norm (Julia's opnorm(A, 1)) and the
+// Pade degree of exp!.  Returns 0 (isdiag fast path, x = exp(A) done), 3 (Taylor 6),
+// 5 (Taylor 12) or the exact Pade degree > 5 (s_out squarings).
+template <int D>
+__device__ __forceinline__ int expm_prologue_fast(Group<D> &G, const cd (&a)[D], cd (&x)[D], bool wr, int &s_out) {
+    const int i = G.i;
+    bool off = false;
+    double ub = 0.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        if (j != i && (a[j].re != 0.0 || a[j].im != 0.0)) off = true;
+        ub += fabs(a[j].re) + fabs(a[j].im);
+    }
+    s_out = 0;
+    if (!group_any(G, wr && off)) {  // isdiag(A): exp of the diagonal
+        cd aii = czero();
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+            if (j == i) aii = a[j];
+        const double e = exp(aii.re);
+        const double sn = sin(aii.im), cn = cos(aii.im);
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = (j == i) ? cmake(e * cn, e * sn) : czero();
+        return 0;
+    }
+    const double nub = group_max(G, ub, wr);
+    if (nub <= 0.015) return 3;
+    if (nub <= 0.25) return 5;
+    return expm_prologue<D>(G, a, x, wr, s_out);  // exact 1-norm (Julia's degree choice)
+}
+
+// Paterson-Stockmeyer with blocks of three: T = B0 + A^3 (B1 + A^3 (B2 + A^3 B3)),
+// B_j = c_3j I + c_3j+1 A + c_3j+2 A^2 (B3 also + c12 A^3); degree 6: B0 + A^3 (B1 + c6 A^3).
+// Products: A^2, A^3, then 3 (degree 12) or 1 (degree 6) Horner steps with A^3 in the tile.
+template <int D>
+__device__ __forceinline__ void expm_taylor(Group<D> &G, int m, const cd (&a)[D], cd (&x)[D], bool wr) {
+    const int i = G.i;
+    const bool small = m == 3;
+    cd a2[D], p[D];
+    tile_store_row(G, a, wr);
+    gsync();
+    mm_tile<D>(a, G.tile, a2);  // A^2
+    mm_tile<D>(a2, G.tile, p);  // A^3
+    {
+        const int b = small ? 3 : 9;  // top block: c_b I + c_b+1 A + c_b+2 A^2 + c_b+3 A^3
+        const double k0 = kInvFact[b], k1 = kInvFact[b + 1], k2 = kInvFact[b + 2], k3 = kInvFact[b + 3];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            x[j] = caxpy(k1, a[j], caxpy(k2, a2[j], cscale(k3, p[j])));
+            if (j == i) x[j].re += k0;
+        }
+    }
+    gsync();
+    tile_store_row(G, p, wr);  // the tile holds A^3 from here on
+    gsync();
+#pragma unroll
+    for (int st = 2; st >= 0; --st) {
+        if (st == 0 || !small) {  // group-uniform
+            mm_tile<D>(x, G.tile, p);
+            const double k0 = kInvFact[3 * st], k1 = kInvFact[3 * st + 1], k2 = kInvFact[3 * st + 2];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                x[j] = caxpy(k1, a[j], caxpy(k2, a2[j], p[j]));
+                if (j == i) x[j].re += k0;
+            }
+        }
+    }
+    gsync();
 }
 
 template <int D, class Reload>

@@ -161,6 +161,19 @@ __device__ __forceinline__ void target_row(const DevProblem &P, const DevBatch &
 // instead of keeping A live through the Pade evaluation.
 constexpr int kCachedTerms = 6;
 
+// Low-norm regime (m in {3, 5}): the solve-free Taylor evaluation (grape_device.hpp,
+// default) or, built with -DGRAPE_LOW_PADE=1, Julia's Pade 3 / 5 with the LU solve.
+#if defined(GRAPE_LOW_PADE) && GRAPE_LOW_PADE
+#define EXPM_LOW(m_) expm_low<D>(G, (m_), a, x, valid, singular, rebuild)
+#define EXPM_GROUP_CD(D_) ::grape::Geo<D_>::GROUP_CD
+#else
+#define EXPM_LOW(m_) expm_taylor<D>(G, (m_), a, x, valid)
+#define EXPM_GROUP_CD(D_) ::grape::Geo<D_>::LEAN_CD
+#endif
+#ifndef GRAPE_EXPM_GRAD_WAVES
+#define GRAPE_EXPM_GRAD_WAVES 3
+#endif
+
 template <int D, bool ERR>
 struct ItemBuilder {
     const DevProblem *P;
@@ -240,7 +253,7 @@ template <int D, bool ERR>
 __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
-    Group<D> G = make_group<D>(lds, threadIdx.x);
+    Group<D> G = make_group<D>(lds, threadIdx.x, EXPM_GROUP_CD(D));
     const long nitems = (long)B.nb * P.Nt * P.nv;
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
@@ -254,13 +267,13 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
-    const int m = expm_prologue<D>(G, a, x, valid, s);
+    const int m = expm_prologue_fast<D>(G, a, x, valid, s);
     cd *out = B.E + (size_t)gidc * D * D + G.i * D;
     if (m > 5) {  // group-uniform: A (columns) to the slot, exp'd by k_expm_high
         if (valid) park<D>(G, out, a, gid, B.overflow, B.overflow_count);
         return;
     }
-    if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
+    if (m == 3 || m == 5) EXPM_LOW(m);
     if (valid) {  // E row-major: column i at stride D (coalesced across the group)
         cd *col = B.E + (size_t)gidc * D * D + G.i;
 #pragma unroll
@@ -292,7 +305,7 @@ template <int D>
 __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm_table(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
-    Group<D> G = make_group<D>(lds, threadIdx.x);
+    Group<D> G = make_group<D>(lds, threadIdx.x, EXPM_GROUP_CD(D));
     const long nitems = (long)B.nb * P.Nt * P.nv;
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
@@ -301,13 +314,13 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
-    const int m = expm_prologue<D>(G, a, x, valid, s);
+    const int m = expm_prologue_fast<D>(G, a, x, valid, s);
     cd *out = B.E + (size_t)gidc * D * D + G.i * D;
     if (m > 5) {
         if (valid) park<D>(G, out, a, gid, B.overflow, B.overflow_count);
         return;
     }
-    if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
+    if (m == 3 || m == 5) EXPM_LOW(m);
     if (valid) {
         cd *col = B.E + (size_t)gidc * D * D + G.i;
 #pragma unroll
@@ -722,11 +735,11 @@ __global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, Dev
 // contracted on the spot -- it never goes to memory.  Pade m > 5 items are
 // parked (A to a slot) for k_grad_high.
 template <int D>
-__global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm_grad(DevProblem P, DevBatch B) {
+__global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_GRAD_WAVES : 2)) void k_expm_grad(DevProblem P, DevBatch B) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     constexpr int TILE = Geo<D>::TILE;
-    Group<D> G = make_group<D>(lds, threadIdx.x);
+    Group<D> G = make_group<D>(lds, threadIdx.x, EXPM_GROUP_CD(D));
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);
     const long nitems = (long)B.nb * P.Nt * nvg;
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
@@ -741,8 +754,8 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
-    const int m = expm_prologue<D>(G, a, x, valid, s);
-    if (m == 3 || m == 5) expm_low<D>(G, m, a, x, valid, singular, rebuild);
+    const int m = expm_prologue_fast<D>(G, a, x, valid, s);
+    if (m == 3 || m == 5) EXPM_LOW(m);
     if (m > 5) {
         if (valid) park<D>(G, B.ovf2_slots + (size_t)gidc * TILE + G.i * D, a, gid, B.ovf2, B.ovf2_count);
         return;  // group-uniform: the whole group parks

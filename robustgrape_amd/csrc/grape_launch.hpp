@@ -22,6 +22,8 @@ constexpr int kScanWide = 8, kScanNarrow = 4;
 
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
+template <int D>  // k_expm / k_expm_grad / k_expm_table (grape_kernels.hpp EXPM_GROUP_CD)
+size_t expm_lean_lds() { return (size_t)grape::Geo<D>::GPW * EXPM_GROUP_CD(D) * sizeof(cd); }
 template <int D>
 size_t errpath_lds() {  // per group: tile + aux, then a second tile (k_err_local, k_err_grad)
     return (size_t)grape::Geo<D>::GPW * (grape::Geo<D>::GROUP_CD + grape::Geo<D>::TILE) * sizeof(cd);
@@ -57,13 +59,13 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     mark(GRAPE_KERNEL_EXPM, 0);
     if (table)
         hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                           expm_lds<D>(), st, P, B);
+                           expm_lean_lds<D>(), st, P, B);
     else if (!fused)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                           expm_lds<D>(), st, P, B);
+                           expm_lean_lds<D>(), st, P, B);
     else
         hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                           expm_lds<D>(), st, P, B);
+                           expm_lean_lds<D>(), st, P, B);
     mark(GRAPE_KERNEL_EXPM, 1);
     mark(GRAPE_KERNEL_EXPM_HIGH, 0);
     hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
@@ -81,7 +83,7 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
         const int nvg = P.np + (P.xadd_dep ? P.na : 0);
         const long ng = (long)B.nb * P.Nt * nvg;
         mark(GRAPE_KERNEL_EXPM_GRAD, 0);
-        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lds<D>(),
+        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lean_lds<D>(),
                            st, P, B);
         mark(GRAPE_KERNEL_EXPM_GRAD, 1);
         mark(GRAPE_KERNEL_GRAD_HIGH, 0);
@@ -143,10 +145,10 @@ hipError_t launch_expm_variants(const DevProblem &P, const DevBatch &B, hipStrea
     const long nexp = (long)B.nb * P.Nt * P.nv;
     if (P.ne > 0)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                           expm_lds<D>(), st, P, B);
+                           expm_lean_lds<D>(), st, P, B);
     else
         hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                           expm_lds<D>(), st, P, B);
+                           expm_lean_lds<D>(), st, P, B);
     hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
                        B.overflow_count, B.status, 1);
     return hipGetLastError();
@@ -158,7 +160,7 @@ template <int D>
 hipError_t launch_expm_table(const DevProblem &P, const DevBatch &B, hipStream_t st) {
     constexpr int GPW = grape::Geo<D>::GPW;
     const long nexp = (long)B.nb * P.Nt * P.nv;
-    hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64), expm_lds<D>(), st,
+    hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64), expm_lean_lds<D>(), st,
                        P, B);
     hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
                        B.overflow_count, B.status, 1);
