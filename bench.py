@@ -370,6 +370,57 @@ def c4opt(args):
     print(json.dumps(out), flush=True)
 
 
+def c2_closure(args):
+    """SURVEY.md 8b closure fallback on C2: the same physics as plain Python closures (the
+    reference's idiom, src/Types.jl:10,50 -- tests/problems.full9_problem(device=False)), so
+    every evaluation pays the reference's closure calls on the host (robustgrape_amd/tables.py:
+    a worker pool fills shared-memory tables chunk by chunk while the device evaluates the
+    previous chunk) and grape_fidelity_grad_tables does the rest.  Host arrays in and out."""
+    from robustgrape_amd.engine import GrapePlan
+    from robustgrape_amd import tables as TB
+    from tests import problems as P
+    B = args.batch or 1024
+    chunk = args.chunk or 128
+    fp = P.full9_problem(NT, device=False)
+    X = restart_inputs(0, B)
+    plan = GrapePlan(fp, nparam=1, device=0, max_batch=min(B, chunk))
+    for _ in range(max(1, args.warmup)):
+        plan.fidelity_grad(X[:chunk])
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.fidelity_grad(X)
+    elapsed = time.perf_counter() - t0
+    value = args.steps * B / elapsed
+    # the two halves on their own: serial closure tables (one core) and the device part
+    t = time.perf_counter()
+    H, U0 = TB.host_tables(fp, X[:8], 1)
+    serial_ms = (time.perf_counter() - t) / 8 * 1e3
+    from robustgrape_amd import _capi
+    nx = X.shape[1]
+    F, G = np.empty(8), np.empty((8, nx))
+    Xs = np.ascontiguousarray(X[:8])
+    t = time.perf_counter()
+    for _ in range(5):
+        _capi.check(_capi.lib().grape_fidelity_grad_tables(plan.handle, 8, _capi.dptr(Xs), _capi.dptr(H),
+                                                           _capi.dptr(U0), _capi.dptr(F), _capi.dptr(G), None, None))
+    device_ms = (time.perf_counter() - t) / 40 * 1e3
+    workers = TB.default_workers()
+    plan.close()
+    out = {"metric": "GRAPE gradient-evals/sec, closure fallback (host-evaluated Python closures), Rydberg CZ d=9 N_t=512",
+           "value": value, "unit": "gradient-evals/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": "C2 with H0 / target as plain Python closures (grape_fidelity_grad_tables)",
+                      "restarts_per_gpu": B, "evals_per_chunk": min(B, chunk), "table_workers": workers},
+           "closure_tables_serial_ms_per_eval": serial_ms,
+           "device_ms_per_eval_tables_prebuilt": device_ms}
+    if not args.no_cpu_baseline:
+        cb = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        out["vs_cpu"] = value / cb["value"]
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -380,11 +431,12 @@ def main():
     ap.add_argument("--chunk", type=int, default=None,
                     help="evaluations per device pass (the plan's workspace; larger steps are chunked "
                          "by the C side); default 16384 (c2), 2048 (c3), 16 (c5)")
-    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c4opt"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c4opt", "c2-closure"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
                          "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
-                         "batched L-BFGS (one step = one iteration of every restart)")
+                         "batched L-BFGS (one step = one iteration of every restart); c2-closure: C2 as "
+                         "plain Python closures through the host-table fallback")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-paths", action="store_true",
                     help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")
@@ -396,6 +448,8 @@ def main():
 
     if args.workload == "c4opt":
         return c4opt(args)
+    if args.workload == "c2-closure":
+        return c2_closure(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

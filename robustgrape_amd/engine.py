@@ -14,7 +14,8 @@ from collections import OrderedDict
 import numpy as np
 
 from . import _capi
-from .operators import DescriptorBuffers, TableDescriptor, has_operator_basis, host_tables
+from .operators import DescriptorBuffers, TableDescriptor, has_operator_basis
+from .tables import SharedTables, get_workers, host_tables, table_shapes
 from .types import FidelityRobustGRAPEProblem, split_x
 
 
@@ -31,6 +32,7 @@ class GrapePlan:
         self.nerr = len(self.up.error_sources)
         self.max_batch = int(max_batch)
         self.lock = threading.Lock()  # one evaluation at a time (the plan's buffers are shared)
+        self._shared = None  # closure fallback: double-buffered shared-memory tables
         # operator bases -> the fused device path; plain closures -> the host-table fallback
         self.tables = not has_operator_basis(fp)
         if self.tables:
@@ -45,6 +47,13 @@ class GrapePlan:
         if getattr(self, "handle", None) is not None and self.handle.value:
             _capi.lib().grape_plan_destroy(self.handle)
             self.handle = None
+        for tabs in getattr(self, "_shared", None) or ():
+            try:
+                self._workers.release(tabs)
+            except Exception:
+                pass
+            tabs.close()
+        self._shared = None
 
     def __del__(self):
         try:
@@ -74,10 +83,7 @@ class GrapePlan:
         Fd2 = np.empty((nb, self.nerr)) if self.nerr else None
         Fd2dx = np.empty((nb, self.nerr, self.nx)) if self.nerr else None
         if self.tables:  # closures evaluated here, everything else on the device
-            H, U0 = host_tables(self.fp, X, self.nparam)
-            _capi.check(_capi.lib().grape_fidelity_grad_tables(
-                self.handle, nb, _capi.dptr(X), _capi.dptr(H), _capi.dptr(U0), _capi.dptr(F), _capi.dptr(Fdx),
-                _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
+            self._fidelity_grad_tables(X, F, Fdx, Fd2, Fd2dx)
         else:
             _capi.check(_capi.lib().grape_fidelity_grad(self.handle, nb, _capi.dptr(X), _capi.dptr(F),
                                                          _capi.dptr(Fdx), _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
@@ -87,6 +93,41 @@ class GrapePlan:
         else:
             Fd2dx = Fd2dx.transpose(0, 2, 1)
         return F, Fdx, Fd2, Fd2dx
+
+    def _fidelity_grad_tables(self, X, F, Fdx, Fd2, Fd2dx):
+        """Closure fallback: the closure tables are built by the worker pool (tables.py) into
+        shared memory, chunk by chunk of max_batch evaluations, double-buffered: the workers
+        fill chunk j + 1 while the device evaluates chunk j."""
+        L = _capi.lib()
+        nb = X.shape[0]
+        W = get_workers(self.fp)
+        if W is not None and not W.can_ship(self.fp):
+            W = None  # closures cloudpickle cannot serialise: evaluate them here
+        if W is None:  # serial
+            H, U0 = host_tables(self.fp, X, self.nparam)
+            _capi.check(L.grape_fidelity_grad_tables(
+                self.handle, nb, _capi.dptr(X), _capi.dptr(H), _capi.dptr(U0), _capi.dptr(F), _capi.dptr(Fdx),
+                _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
+            return
+        C = self.max_batch
+        if self._shared is None:
+            sh, su = table_shapes(self.fp, C, self.nparam)
+            self._shared = [SharedTables(sh, su) for _ in range(2)]
+            self._workers = W
+        chunks = [(b0, min(C, nb - b0)) for b0 in range(0, nb, C)]
+        pending = {0: W.submit(self.fp, self.nparam, self._shared[0], X, range(chunks[0][0], sum(chunks[0])))}
+        sl = lambda a, b0, n: None if a is None else a[b0:b0 + n]
+        for j, (b0, n) in enumerate(chunks):
+            if j + 1 < len(chunks):  # the other buffer's chunk (j - 1) is done on the device
+                c0, cn = chunks[j + 1]
+                pending[j + 1] = W.submit(self.fp, self.nparam, self._shared[(j + 1) % 2], X, range(c0, c0 + cn))
+            for r in pending.pop(j):
+                r.get()
+            tabs = self._shared[j % 2]
+            _capi.check(L.grape_fidelity_grad_tables(
+                self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(tabs.H), _capi.dptr(tabs.U0),
+                _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
+                _capi.dptr(sl(Fd2dx, b0, n))))
 
     def fidelity_grad_device_async(self, x_ptr: int, F_ptr: int, Fdx_ptr: int, nbatch: int,
                                    Fd2_ptr: int = 0, Fd2dx_ptr: int = 0):

@@ -243,83 +243,8 @@ class TableDescriptor:
             max_batch=int(max_batch), reserved=(ctypes.c_int32 * 7)(GRAPE_DESC_HOST_TABLES))
 
 
-def table_variants(nparam: int, nadd: int, nerr: int) -> int:
-    """Variants per step of the grape_fidelity_grad_tables H table (include/grape.h):
-    n = nparam + nadd gradient parameters; 1 + n without error sources, else
-    1 + 2n + nerr (2 + n)."""
-    n = nparam + nadd
-    return 1 + n if nerr == 0 else 1 + 2 * n + nerr * (2 + n)
-
-
-def _cm(M):
-    """A d x d closure result as the C-order image of its column-major layout (M^T)."""
-    return np.asarray(M, np.complex128).T
-
-
-def host_tables(fp, X, nparam: int, out=None):
-    """The closure calls of one batch, at exactly the reference's call sites and arguments
-    (src/UnitaryCalculations.jl:45-95): H0(nt, x[:,nt], x_add); parameter u + eps for the
-    controls (:48-51) and x_add (:57-59); with error sources parameter u + eps2 (:53-54, :61-62),
-    Herror_e(.., eps) + H0 (:67), Herror_e(.., eps2) + H0 (:71) and the mixed
-    Herror_e(u + eps2, .., eps2) + H0(u + eps2) (:77-78, :89-90); target(x_add) and
-    target(x_add + eps e_q) (FidelityCalculations.jl:32-38).  Returns the
-    grape_fidelity_grad_tables layouts H (nb, N_t, nv, d, d) and U0 (nb, 1 + na, d, d), each
-    matrix column-major (C-order image of its transpose).  `out` = (H, U0) preallocated
-    arrays of those shapes to fill (e.g. pinned / shared buffers)."""
-    from .types import split_x
-    up = fp.unitary_problem
-    d, nt, na = up.ndim, up.ntimes, up.nb_additional_param
-    eps, eps2 = float(up.eps), float(up.eps2)
-    errs = up.error_sources
-    ne = len(errs)
-    X = np.asarray(X, np.float64)
-    nb = X.shape[0]
-    n = nparam + na
-    nv = table_variants(nparam, na, ne)
-    if out is None:
-        H = np.empty((nb, nt, nv, d, d), np.complex128)
-        U0 = np.empty((nb, 1 + na, d, d), np.complex128)
-    else:
-        H, U0 = out
-    H0f, tgt = up.H0, fp.target_unitary
-    for b in range(nb):
-        x_main, x_add, _ = split_x(up, X[b])
-        for k in range(nt):
-            nt1 = k + 1
-            xk = x_main[:, k]
-            Hb = H[b, k]
-            H0k = np.asarray(H0f(nt1, xk.copy(), x_add.copy()), np.complex128)
-            Hb[0] = H0k.T
-
-            def at(u, delta):  # (x_k, x_add) with gradient parameter u moved by delta
-                xp, xa = xk.copy(), x_add.copy()
-                if u < nparam:
-                    xp[u] = xk[u] + delta
-                else:
-                    xa[u - nparam] = x_add[u - nparam] + delta
-                return xp, xa
-
-            for u in range(n):
-                Hb[1 + u] = _cm(H0f(nt1, *at(u, eps)))
-            if ne == 0:
-                continue
-            Hx2 = []
-            for u in range(n):  # H0 at u + eps2 also feeds the mixed stencils below (same call)
-                h = np.asarray(H0f(nt1, *at(u, eps2)), np.complex128)
-                Hx2.append(h)
-                Hb[1 + n + u] = h.T
-            for e, es in enumerate(errs):
-                base = 1 + 2 * n + e * (2 + n)
-                Hb[base] = _cm(np.asarray(es.Herror(nt1, xk.copy(), x_add.copy(), eps), np.complex128) + H0k)
-                Hb[base + 1] = _cm(np.asarray(es.Herror(nt1, xk.copy(), x_add.copy(), eps2), np.complex128) + H0k)
-                for u in range(n):
-                    Hb[base + 2 + u] = _cm(np.asarray(es.Herror(nt1, *at(u, eps2), eps2), np.complex128) + Hx2[u])
-        U0[b, 0] = _cm(tgt(x_add.copy()))
-        for q in range(na):
-            xa = x_add.copy()
-            xa[q] += eps
-            U0[b, 1 + q] = _cm(tgt(xa))
-    return H, U0
+# the closure tables themselves: robustgrape_amd/tables.py
+from .tables import host_tables, table_variants  # noqa: E402,F401
 
 
 def host_interaction_tables(up, x, nparam: int):
@@ -336,7 +261,7 @@ def host_interaction_tables(up, x, nparam: int):
     Oerr = np.empty((nt, len(errs), d, d), np.complex128)
     for k in range(nt):
         xk = x_main[:, k]
-        H0[k] = _cm(up.H0(k + 1, xk.copy(), x_add.copy()))
+        H0[k] = np.asarray(up.H0(k + 1, xk.copy(), x_add.copy()), np.complex128).T
         for e, es in enumerate(errs):
-            Oerr[k, e] = _cm((1 / eps) * np.asarray(es.Herror(k + 1, xk.copy(), x_add.copy(), eps), np.complex128))
+            Oerr[k, e] = ((1 / eps) * np.asarray(es.Herror(k + 1, xk.copy(), x_add.copy(), eps), np.complex128)).T
     return H0, Oerr

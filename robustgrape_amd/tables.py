@@ -1,0 +1,273 @@
+"""Closure fallback, host side: the reference's closure calls tabulated for the device.
+
+A problem whose ``H0`` / ``Herror`` / ``target_unitary`` are plain callables (the
+reference's idiom, src/Types.jl:10,25,50) cannot be evaluated on the GPU.  The host
+calls them at exactly the reference's call sites (src/UnitaryCalculations.jl:45-95,
+src/FidelityCalculations.jl:32-38) and hands the tables to
+``grape_fidelity_grad_tables``; everything else runs on the device.
+
+The closure calls are the reference's own cost (one Python call per call site), so
+this module spreads them over worker processes: ``TableWorkers`` forks a pool once
+(before the tables are needed: the workers never touch the GPU), splits a batch by
+evaluations -- or a single evaluation by time steps -- and the workers write straight
+into shared-memory tables that the device call then copies to HBM.  While the device
+evaluates one chunk of a batch, the workers fill the next (``GrapePlan.fidelity_grad``).
+
+Worker count: ``GRAPE_TABLE_WORKERS`` (0 or 1 = serial in the calling process; default
+min(8, cpu_count)).
+"""
+from __future__ import annotations
+
+import atexit
+import multiprocessing as mp
+import os
+import threading
+import time
+from multiprocessing import shared_memory
+
+import numpy as np
+
+from .types import split_x
+
+
+def table_variants(nparam: int, nadd: int, nerr: int) -> int:
+    """Variants per step of the grape_fidelity_grad_tables H table (include/grape.h):
+    n = nparam + nadd gradient parameters; 1 + n without error sources, else
+    1 + 2n + nerr (2 + n)."""
+    n = nparam + nadd
+    return 1 + n if nerr == 0 else 1 + 2 * n + nerr * (2 + n)
+
+
+def fill_tables(fp, X, nparam: int, H, U0, rows, k0: int, k1: int, target: bool = True):
+    """Fill H[r, k0:k1] (and U0[r] when `target`) for the evaluations r in `rows` with the
+    closure values of X[r], column-major matrices (the C-order image of M^T), in the
+    variant order of include/grape.h:
+      0: H0(nt, x[:,nt], x_add) (:45) | 1 + u: parameter u + eps (:48-51, :57-59) |
+      ne > 0: 1 + n + u: parameter u + eps2 (:53-54, :61-62) | per error e, base 1 + 2n + e(2 + n):
+      base: Herror_e(.., eps) + H0 (:67) | base + 1: Herror_e(.., eps2) + H0 (:71) |
+      base + 2 + u: Herror_e(u + eps2, .., eps2) + H0(u + eps2) (:77-78, :89-90)
+    with u < nparam a control x[u, nt] and u >= nparam the additional parameter
+    x_add[u - nparam]; U0: target(x_add), target(x_add + eps e_q) (FidelityCalculations.jl:32-38).
+    Every call gets fresh argument arrays, as Julia's slicing does."""
+    up = fp.unitary_problem
+    na = up.nb_additional_param
+    eps, eps2 = float(up.eps), float(up.eps2)
+    errs = up.error_sources
+    ne = len(errs)
+    n = nparam + na
+    H0f, tgt = up.H0, fp.target_unitary
+    asc = np.asarray
+    for b in rows:
+        x_main, x_add, _ = split_x(up, X[b])
+        for k in range(k0, k1):
+            nt1 = k + 1
+            xk = x_main[:, k]
+            Hb = H[b, k]
+
+            def at(u, delta):  # (x_k, x_add) with gradient parameter u moved by delta
+                xp, xa = xk.copy(), x_add.copy()
+                if u < nparam:
+                    xp[u] = xk[u] + delta
+                else:
+                    xa[u - nparam] = x_add[u - nparam] + delta
+                return xp, xa
+
+            H0k = asc(H0f(nt1, xk.copy(), x_add.copy()), np.complex128)
+            Hb[0] = H0k.T
+            for u in range(n):
+                Hb[1 + u] = asc(H0f(nt1, *at(u, eps))).T
+            if ne == 0:
+                continue
+            Hx2 = []
+            for u in range(n):  # H0 at u + eps2 also feeds the mixed stencils below (same call)
+                h = asc(H0f(nt1, *at(u, eps2)), np.complex128)
+                Hx2.append(h)
+                Hb[1 + n + u] = h.T
+            for e, es in enumerate(errs):
+                base = 1 + 2 * n + e * (2 + n)
+                Hb[base] = (asc(es.Herror(nt1, xk.copy(), x_add.copy(), eps), np.complex128) + H0k).T
+                Hb[base + 1] = (asc(es.Herror(nt1, xk.copy(), x_add.copy(), eps2), np.complex128) + H0k).T
+                for u in range(n):
+                    Hb[base + 2 + u] = (asc(es.Herror(nt1, *at(u, eps2), eps2), np.complex128) + Hx2[u]).T
+        if target:
+            U0[b, 0] = asc(tgt(x_add.copy())).T
+            for q in range(na):
+                xa = x_add.copy()
+                xa[q] += eps
+                U0[b, 1 + q] = asc(tgt(xa)).T
+
+
+def table_shapes(fp, nb: int, nparam: int):
+    up = fp.unitary_problem
+    d, na = up.ndim, up.nb_additional_param
+    nv = table_variants(nparam, na, len(up.error_sources))
+    return (nb, up.ntimes, nv, d, d), (nb, 1 + na, d, d)
+
+
+def host_tables(fp, X, nparam: int):
+    """The closure tables of a batch, serially in this process: H (nb, N_t, nv, d, d) and
+    U0 (nb, 1 + na, d, d), column-major matrices (see fill_tables)."""
+    X = np.asarray(X, np.float64)
+    sh, su = table_shapes(fp, X.shape[0], nparam)
+    H, U0 = np.empty(sh, np.complex128), np.empty(su, np.complex128)
+    fill_tables(fp, X, nparam, H, U0, range(X.shape[0]), 0, fp.unitary_problem.ntimes)
+    return H, U0
+
+
+# ---------------------------------------------------------------------------
+# worker pool
+# ---------------------------------------------------------------------------
+_problems = {}   # token -> problem, in the workers (and, before a fork, in the parent)
+_shm_cache = {}  # worker-side attachments
+
+
+def _attach(name):
+    shm = _shm_cache.get(name)
+    if shm is None:
+        shm = shared_memory.SharedMemory(name=name)
+        try:  # the creating process owns the segment: keep this process's tracker off it
+            from multiprocessing import resource_tracker
+            resource_tracker.unregister(shm._name, "shared_memory")
+        except Exception:
+            pass
+        _shm_cache[name] = shm
+    return shm
+
+
+def _worker_fill(task):
+    token, blob, nparam, hname, uname, sh, su, X, rows, k0, k1, target = task
+    fp = _problems.get(token)
+    if fp is None:  # a problem registered after the fork: shipped by value
+        import cloudpickle
+        fp = cloudpickle.loads(blob)
+        _problems[token] = fp
+    H = np.ndarray(sh, np.complex128, buffer=_attach(hname).buf)
+    U0 = np.ndarray(su, np.complex128, buffer=_attach(uname).buf)
+    t = time.perf_counter()
+    fill_tables(fp, X, nparam, H, U0, rows, k0, k1, target)
+    return time.perf_counter() - t
+
+
+def _worker_release(names):
+    for n in names:
+        shm = _shm_cache.pop(n, None)
+        if shm is not None:
+            shm.close()
+    return 0
+
+
+class SharedTables:
+    """H / U0 tables in POSIX shared memory (readable by the device copy, writable by workers)."""
+
+    def __init__(self, sh, su):
+        nbytes = lambda s: int(np.prod(s)) * 16
+        self.shm_h = shared_memory.SharedMemory(create=True, size=max(16, nbytes(sh)))
+        self.shm_u = shared_memory.SharedMemory(create=True, size=max(16, nbytes(su)))
+        self.sh, self.su = sh, su
+        self.H = np.ndarray(sh, np.complex128, buffer=self.shm_h.buf)
+        self.U0 = np.ndarray(su, np.complex128, buffer=self.shm_u.buf)
+
+    def close(self):
+        self.H = self.U0 = None
+        for s in (self.shm_h, self.shm_u):
+            s.close()
+            s.unlink()
+
+
+class TableWorkers:
+    """A fork-context process pool that fills closure tables in shared memory."""
+
+    def __init__(self, nworkers: int):
+        self.n = nworkers
+        self.pool = mp.get_context("fork").Pool(nworkers)
+        self.known = set()  # tokens whose problem the workers already hold (registered before the fork)
+        self.blobs = {}     # token -> (problem, cloudpickle bytes) for problems created after the fork
+        self.lock = threading.Lock()
+
+    def can_ship(self, fp) -> bool:
+        """Whether the workers hold `fp` already or can receive it (cloudpickle)."""
+        token = id(fp)
+        if (token in self.known and _problems.get(token) is fp) or token in self.blobs:
+            return True
+        try:
+            import cloudpickle
+            self.blobs[token] = (fp, cloudpickle.dumps(fp))
+            return True
+        except Exception:
+            return False
+
+    def submit(self, fp, nparam, tabs: SharedTables, X, rows_of_chunk):
+        """Asynchronously fill the tables for the evaluations `rows_of_chunk` (indices into X and
+        into the tables' first axis); returns an AsyncResult list."""
+        token = id(fp)
+        if token in self.known and _problems.get(token) is fp:
+            blob = b""
+        else:
+            ent = self.blobs.get(token)
+            if ent is None or ent[0] is not fp:
+                import cloudpickle
+                ent = self.blobs[token] = (fp, cloudpickle.dumps(fp))
+            blob = ent[1]
+        nt = fp.unitary_problem.ntimes
+        X = np.asarray(X, np.float64)
+        nb = len(rows_of_chunk)
+        tasks = []
+        if nb >= self.n:  # split by evaluations
+            for part in np.array_split(np.arange(nb), self.n):
+                if len(part):
+                    tasks.append((part, 0, nt, True))
+        else:  # few evaluations: split each by time steps
+            per = max(1, -(-self.n // max(1, nb)))
+            for r in range(nb):
+                bounds = np.linspace(0, nt, min(per, nt) + 1).astype(int)
+                for j in range(len(bounds) - 1):
+                    tasks.append((np.array([r]), int(bounds[j]), int(bounds[j + 1]), j == 0))
+        sub = X[np.asarray(rows_of_chunk)]
+        return [self.pool.apply_async(_worker_fill, ((token, blob, nparam, tabs.shm_h.name, tabs.shm_u.name,
+                                                      tabs.sh, tabs.su, sub, rows, k0, k1, tg),))
+                for rows, k0, k1, tg in tasks]
+
+    def release(self, tabs: SharedTables):
+        names = [tabs.shm_h.name, tabs.shm_u.name]
+        for _ in range(self.n):
+            self.pool.apply(_worker_release, (names,))
+
+    def close(self):
+        self.pool.terminate()
+        self.pool.join()
+
+
+_workers = None
+_workers_lock = threading.Lock()
+
+
+def default_workers() -> int:
+    env = os.environ.get("GRAPE_TABLE_WORKERS")
+    if env is not None:
+        return max(0, int(env))
+    return min(8, os.cpu_count() or 1)
+
+
+def get_workers(fp=None):
+    """The process-wide pool (None when the fallback runs serially).  Registering `fp` first
+    lets a pool created now inherit the problem by fork instead of receiving it pickled."""
+    global _workers
+    n = default_workers()
+    if n <= 1:
+        return None
+    with _workers_lock:
+        if _workers is None:
+            if fp is not None:
+                _problems[id(fp)] = fp
+            _workers = TableWorkers(n)
+            if fp is not None:
+                _workers.known.add(id(fp))
+            atexit.register(_shutdown)
+        return _workers
+
+
+def _shutdown():
+    global _workers
+    if _workers is not None:
+        _workers.close()
+        _workers = None
