@@ -201,10 +201,13 @@ static int validate_terms(const grape_term *t, int n, int n_ops, int np, int na,
     return GRAPE_OK;
 }
 
-// The engines take C_k^-1 = C_k^dagger (unitary step propagators) and skip balancing,
-// both valid for Hermitian H only.  A term c(x) * OP keeps H Hermitian for every x when
-// its function is real-valued and scale * OP is Hermitian; anything else (e.g. a
-// -i Gamma/2 decay term) is refused rather than computed wrongly.
+// The engines take C_k^-1 = C_k^dagger for the chain C_k of the NOMINAL propagators
+// exp(-i dt H0) and skip balancing (a permutation only for Hermitian H): both need a
+// Hermitian H0.  A term c(x) * OP keeps H0 Hermitian for every x when its function is
+// real-valued and scale * OP is Hermitian; anything else (e.g. a -i Gamma/2 decay term in
+// H0) is refused rather than computed wrongly.  Error generators need no such property:
+// their propagators only enter through differences dE (UnitaryCalculations.jl:68-83) that
+// the nominal chain transports, so a non-Hermitian Herror (a decay-rate error) is served.
 static int check_hermitian_terms(const grape_desc *desc, const grape_term *t, int n, const char *what) {
     const int D = desc->ndim;
     for (int k = 0; k < n; ++k) {
@@ -370,7 +373,6 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     }
     if (!tables) {
         if ((rc = check_hermitian_terms(desc, desc->h0_terms, desc->n_h0_terms, "H0"))) return rc;
-        if ((rc = check_hermitian_terms(desc, desc->err_terms, n_err_terms, "error source"))) return rc;
     }
     // host tables: H0 / Herror are opaque closures that may read x_add, so every x_add call
     // site of the reference is tabulated (UnitaryCalculations.jl:57-64, 87-95)

@@ -244,7 +244,7 @@ class TableDescriptor:
 
 
 # the closure tables themselves: robustgrape_amd/tables.py
-from .tables import host_tables, table_variants  # noqa: E402,F401
+from .tables import check_hermitian_h0, host_tables, table_variants  # noqa: E402,F401
 
 
 def host_interaction_tables(up, x, nparam: int):
@@ -262,6 +262,7 @@ def host_interaction_tables(up, x, nparam: int):
     for k in range(nt):
         xk = x_main[:, k]
         H0[k] = np.asarray(up.H0(k + 1, xk.copy(), x_add.copy()), np.complex128).T
+        check_hermitian_h0(H0[k:k + 1])
         for e, es in enumerate(errs):
             Oerr[k, e] = ((1 / eps) * np.asarray(es.Herror(k + 1, xk.copy(), x_add.copy(), eps), np.complex128)).T
     return H0, Oerr

@@ -89,12 +89,26 @@ def fill_tables(fp, X, nparam: int, H, U0, rows, k0: int, k1: int, target: bool 
                 Hb[base + 1] = (asc(es.Herror(nt1, xk.copy(), x_add.copy(), eps2), np.complex128) + H0k).T
                 for u in range(n):
                     Hb[base + 2 + u] = (asc(es.Herror(nt1, *at(u, eps2), eps2), np.complex128) + Hx2[u]).T
+        check_hermitian_h0(H[b, k0:k1, 0], b)
         if target:
             U0[b, 0] = asc(tgt(x_add.copy())).T
             for q in range(na):
                 xa = x_add.copy()
                 xa[q] += eps
                 U0[b, 1 + q] = asc(tgt(xa)).T
+
+
+def check_hermitian_h0(H0s, row=0, rtol=1e-12):
+    """The device chains the nominal propagators with C_k^-1 = C_k^dagger and skips balancing
+    (valid for Hermitian H0 only): refuse a non-Hermitian nominal H0(nt, x, x_add) -- e.g. a
+    -i Gamma/2 decay term -- instead of computing it wrongly (error generators are exempt:
+    their propagators only enter through differences the nominal chain transports)."""
+    if H0s.size == 0:
+        return
+    dev = np.max(np.abs(H0s - np.conj(np.swapaxes(H0s, -1, -2))))
+    if not dev <= rtol * max(np.max(np.abs(H0s)), 1e-300):
+        raise ValueError(f"H0 is not Hermitian (evaluation {row}: max |H - H^dagger| = {dev:.3e}); the device "
+                         "engine needs unitary nominal propagators")
 
 
 def table_shapes(fp, nb: int, nparam: int):

@@ -17,3 +17,10 @@ def pytest_configure(config):
 def gpu_available():
     import torch
     return torch.cuda.is_available()
+
+
+# Achieved parity errors, recorded by the GPU parity tests (tests/parity_log.py) and written to
+# gpurun_out/parity_errors_<pid>.json at the end of the session when that directory exists.
+def pytest_sessionfinish(session, exitstatus):
+    from tests import parity_log
+    parity_log.dump(os.path.join(ROOT, "gpurun_out"))

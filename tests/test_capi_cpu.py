@@ -129,6 +129,12 @@ def test_non_hermitian_generators_are_refused():
     for f in bad:
         rc, msg = _create(f)
         assert rc == -2 and "Hermitian" in msg, (rc, msg)
+    # a non-Hermitian ERROR generator (decay-rate error) is accepted: only H0 chains
+    from robustgrape_amd.operators import OperatorBasisError
+    from robustgrape_amd.types import ErrorSource
+    derr = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(OperatorBasisError([Term(decay, scale=-0.5j)]))]))
+    rc, msg = _create(derr)
+    assert rc in (0, -6), (rc, msg)
     # a complex scale that keeps the term Hermitian (i * antisymmetric real) is accepted past validation
     anti = np.zeros((5, 5), complex)
     anti[0, 1], anti[1, 0] = 1.0, -1.0
@@ -168,3 +174,20 @@ def test_plan_cache_is_bounded_and_keyed_by_problem(monkeypatch):
     assert b.closed  # least recently used, evicted
     engine.clear_plans()
     assert engine.cached_plan_count() == 0 and all(p.closed for p in made)
+
+
+def test_closure_tables_refuse_non_hermitian_h0():
+    """Closure fallback: a non-Hermitian nominal H0 is refused on the host (tables.check_hermitian_h0);
+    a non-Hermitian error generator is tabulated (only differences of its propagators are used)."""
+    from robustgrape_amd.tables import host_tables
+    from robustgrape_amd.types import ErrorSource
+    fp = P.sym_problem(6, device=False)
+    up = fp.unitary_problem
+    decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
+    x = P.random_x(6, 2)
+    bad = fp.replace(unitary_problem=up.replace(H0=lambda t, p, xa: up.H0(t, p, xa) - 0.5j * decay))
+    with pytest.raises(ValueError, match="Hermitian"):
+        host_tables(bad, x[None, :], 1)
+    ok = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, p, xa, e: -0.5j * e * decay)]))
+    H, _ = host_tables(ok, x[None, :], 1)
+    assert np.isfinite(H).all()

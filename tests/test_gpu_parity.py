@@ -4,6 +4,10 @@ Tolerance tiers (FD noise analysis there):
   T0  propagators E_k              <= 1e-13 relative (max-abs / max|E|, x max(1, |A|_1) for m = 13)
   T1  U, F                         <= 1e-12 absolute
   T2  eps-FD quantities (F_dx)     <= 1e-6 * max|ref| + 1e-7
+  T2s the same on the short-step SURVEY configs (C1, C2, C4: dt |H|_1 <= 0.17, Taylor/Pade
+      degree <= 12 without squarings), where two implementations differ by ~4e-9 of max|F_dx|:
+      <= 1e-7 * max|ref| + 1e-9
+Every assertion records its achieved error (tests/parity_log.py -> gpurun_out/parity_errors_*.json).
 """
 import os
 
@@ -31,10 +35,17 @@ def _golden(name):
     return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
 
 
-def _assert_fid(F, Fdx, ref_F, ref_Fdx):
+T2S, T2S_ABS = 1e-7, 1e-9
+
+
+def _assert_fid(F, Fdx, ref_F, ref_Fdx, tight=False, test=""):
+    from tests.parity_log import record
+    t2, t2a = (T2S, T2S_ABS) if tight else (T2, T2_ABS)
+    record(test, "F", abs(F - ref_F), 1.0, T1)
     assert abs(F - ref_F) <= T1, (F, ref_F)
-    err = np.max(np.abs(Fdx - ref_Fdx))
-    assert err <= T2 * np.max(np.abs(ref_Fdx)) + T2_ABS, (err, np.max(np.abs(ref_Fdx)))
+    err, scale = np.max(np.abs(Fdx - ref_Fdx)), np.max(np.abs(ref_Fdx))
+    record(test, "F_dx", err, scale, t2 * scale + t2a)
+    assert err <= t2 * scale + t2a, (err, scale)
 
 
 def test_expm_batch_matches_oracle_every_pade_degree():
@@ -71,7 +82,7 @@ def test_fidelity_gradient_matches_golden(name, builder):
     from robustgrape_amd import calculate_fidelity_and_derivatives
     g = _golden(name)
     F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(builder(), g["x"])
-    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"], tight=True, test="golden_" + name)
     assert d2.shape == (0,) and d2dx.shape == (len(g["x"]), 0)
 
 
@@ -81,7 +92,7 @@ def test_restart_batch_matches_golden():
     g = _golden("c4")
     F, Fdx, _, _ = calculate_fidelity_and_derivatives(P.full9_problem(512), g["x"])
     for b in range(len(F)):
-        _assert_fid(F[b], Fdx[b], g["F"][b], g["F_dx"][b])
+        _assert_fid(F[b], Fdx[b], g["F"][b], g["F_dx"][b], tight=True, test=f"golden_c4_{b}")
 
 
 @pytest.mark.parametrize("d,ntimes", [(5, 1), (5, 2), (5, 7), (7, 3), (9, 1), (9, 13), (9, 57), (5, 130)])
@@ -94,7 +105,7 @@ def test_small_problems_match_live_oracle(d, ntimes):
     x = P.random_x(ntimes, 100 + ntimes)
     F0, g0, _, _ = O.calculate_fidelity_and_derivatives(mk(False), x)
     F, g, _, _ = calculate_fidelity_and_derivatives(mk(True), x)
-    _assert_fid(F, g, F0, g0)
+    _assert_fid(F, g, F0, g0, test=f"live_d{d}_nt{ntimes}")
 
 
 def test_batch_equals_single_and_ragged_batches():
@@ -141,12 +152,19 @@ def test_errors_are_loud():
 T3, T3_ABS, T3_XADD_ABS = 1e-5, 1e-7, 1e-5
 
 
-def _assert_err(fp, d2, d2dx, ref_d2, ref_d2dx):
+def _assert_err(fp, d2, d2dx, ref_d2, ref_d2dx, test=""):
+    from tests.parity_log import record
     nmain = d2dx.shape[0] - fp.unitary_problem.nb_additional_param
-    assert np.max(np.abs(d2 - ref_d2)) <= T3 * np.max(np.abs(ref_d2)) + T3_ABS, (d2, ref_d2)
-    err = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain]))
-    assert err <= T3 * np.max(np.abs(ref_d2dx[:nmain])) + T3_ABS, err
-    assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
+    e0, s0 = np.max(np.abs(d2 - ref_d2)), np.max(np.abs(ref_d2))
+    record(test, "F_d2err", e0, s0, T3 * s0 + T3_ABS)
+    assert e0 <= T3 * s0 + T3_ABS, (d2, ref_d2)
+    err, scale = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain])), np.max(np.abs(ref_d2dx[:nmain]))
+    record(test, "F_d2err_dx", err, scale, T3 * scale + T3_ABS)
+    assert err <= T3 * scale + T3_ABS, err
+    ea = np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) if d2dx.shape[0] > nmain else 0.0
+    record(test, "F_d2err_dx_add", ea, np.max(np.abs(ref_d2dx[nmain:])) if d2dx.shape[0] > nmain else 0.0,
+           T3_XADD_ABS)
+    assert ea <= T3_XADD_ABS
 
 
 @pytest.mark.parametrize("name,builder", [
@@ -160,8 +178,8 @@ def test_error_sensitivities_match_golden(name, builder):
     g = _golden(name)
     fp = builder()
     F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(fp, g["x"])
-    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
-    _assert_err(fp, d2, d2dx, g["F_d2err"], g["F_d2err_dx"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"], tight=name.startswith("c3"), test="golden_" + name)
+    _assert_err(fp, d2, d2dx, g["F_d2err"], g["F_d2err_dx"], test="golden_" + name)
 
 
 @pytest.mark.parametrize("d,ntimes,errors", [(5, 1, ("amp",)), (5, 9, ("amp", "freq")), (7, 20, ("freq",)),

@@ -130,3 +130,32 @@ def test_closure_analysis_entry_points_match_oracle():
     # the same physics through the operator basis gives the same operators
     Oob = A.calculate_interaction_error_operators(P.xadd_err_problem(5, nt).unitary_problem, x)
     assert np.max(np.abs(Oob - Odev)) <= T2 * np.max(np.abs(Oref)) + T2_ABS
+
+
+@pytest.mark.parametrize("device", [True, False], ids=["operator-basis", "closures"])
+def test_non_hermitian_error_generator_matches_oracle(device):
+    """A decay-rate error source Herror = -i (e/2) |r><r| (non-Hermitian): its propagators only
+    enter through differences transported by the unitary nominal chain, so the device serves it;
+    against the oracle (which balances with zgebal and inverts with getrf/getri, as Julia)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    from robustgrape_amd.operators import OperatorBasisError, Term
+    from robustgrape_amd.types import ErrorSource
+    nt = 24
+    decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
+    base = P.sym_problem(nt, errors=("amp",))
+    ob = ErrorSource(OperatorBasisError([Term(decay, scale=-0.5j)]))
+    cl = ErrorSource(lambda t, x, xa, e: -0.5j * e * decay)
+    fo = base.replace(unitary_problem=base.unitary_problem.replace(
+        error_sources=list(base.unitary_problem.error_sources) + [ob]))
+    fc0 = P.sym_problem(nt, errors=("amp",), device=False)
+    fc = fc0.replace(unitary_problem=fc0.unitary_problem.replace(
+        error_sources=list(fc0.unitary_problem.error_sources) + [cl]))
+    x = P.random_x(nt, 3)
+    ref = O.calculate_fidelity_and_derivatives(fc, x)
+    F, g, e, ed = calculate_fidelity_and_derivatives(fo if device else fc, x)
+    assert abs(F - ref[0]) <= T1
+    assert np.max(np.abs(g - ref[1])) <= T2 * np.max(np.abs(ref[1])) + T2_ABS
+    assert np.max(np.abs(e - ref[2])) <= T2 * np.max(np.abs(ref[2])) + T2_ABS
+    assert np.max(np.abs(ed[:-1] - ref[3][:-1])) <= T3 * np.max(np.abs(ref[3][:-1])) + T3_ABS
+    assert abs(ref[2][1]) > 1e-3  # the decay sensitivity is really exercised
