@@ -1,0 +1,95 @@
+/*
+ * abi_check.c -- a plain-C caller of libgrape.so built by gcc against include/grape.h.
+ *
+ *   abi_check layout   prints sizeof / offsetof of grape_term and grape_desc (no GPU);
+ *                      tests/test_c_abi.py compares them with the ctypes mirror
+ *                      (robustgrape_amd/operators.py) and the Julia shim's structs
+ *                      (julia/RobustGRAPEMI355X.jl)
+ *   abi_check gpu      one grape_fidelity_grad call on device 0 for a 2-level problem
+ *                      (H = cos(x) X + sin(x) Y + 0.3 Z, target X, N_t = 4, one x_add phase
+ *                      on the target) and prints F and F_dx; the GPU test compares them with
+ *                      the CPU oracle
+ */
+#include <stddef.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "grape.h"
+
+#define PRINT_OFF(T, f) printf(#T "." #f " %zu\n", offsetof(T, f))
+
+static int layout(void) {
+    printf("sizeof.grape_term %zu\n", sizeof(grape_term));
+    PRINT_OFF(grape_term, op);
+    PRINT_OFF(grape_term, var);
+    PRINT_OFF(grape_term, index);
+    PRINT_OFF(grape_term, func);
+    PRINT_OFF(grape_term, a);
+    PRINT_OFF(grape_term, b);
+    PRINT_OFF(grape_term, scale_re);
+    PRINT_OFF(grape_term, scale_im);
+    printf("sizeof.grape_desc %zu\n", sizeof(grape_desc));
+    PRINT_OFF(grape_desc, ndim);
+    PRINT_OFF(grape_desc, ntimes);
+    PRINT_OFF(grape_desc, nparam);
+    PRINT_OFF(grape_desc, nadd);
+    PRINT_OFF(grape_desc, nerr);
+    PRINT_OFF(grape_desc, n_ops);
+    PRINT_OFF(grape_desc, t0);
+    PRINT_OFF(grape_desc, eps);
+    PRINT_OFF(grape_desc, eps2);
+    PRINT_OFF(grape_desc, projector_diag);
+    PRINT_OFF(grape_desc, ops);
+    PRINT_OFF(grape_desc, n_h0_terms);
+    PRINT_OFF(grape_desc, h0_terms);
+    PRINT_OFF(grape_desc, err_term_offsets);
+    PRINT_OFF(grape_desc, err_terms);
+    PRINT_OFF(grape_desc, n_target_terms);
+    PRINT_OFF(grape_desc, target_terms);
+    PRINT_OFF(grape_desc, max_batch);
+    PRINT_OFF(grape_desc, reserved);
+    printf("abi_version %d\n", grape_abi_version());
+    return 0;
+}
+
+static int gpu(void) {
+    /* operators, column-major interleaved: X, Y, Z, I */
+    double ops[4][8];
+    memset(ops, 0, sizeof ops);
+    ops[0][2] = 1.0; ops[0][4] = 1.0;                 /* X: (1,0) = (0,1) = 1 */
+    ops[1][3] = 1.0; ops[1][5] = -1.0;                /* Y: (1,0) = i, (0,1) = -i */
+    ops[2][0] = 1.0; ops[2][6] = -1.0;                /* Z */
+    ops[3][0] = 1.0; ops[3][6] = 1.0;                 /* I */
+    grape_term h0[3] = {
+        {0, GRAPE_VAR_X, 0, GRAPE_FN_COS, 1.0, 0.0, 1.0, 0.0},
+        {1, GRAPE_VAR_X, 0, GRAPE_FN_SIN, 1.0, 0.0, 1.0, 0.0},
+        {2, GRAPE_VAR_ONE, 0, GRAPE_FN_ONE, 1.0, 0.0, 0.3, 0.0},
+    };
+    /* target = X * exp(i theta) */
+    grape_term tgt[1] = {{0, GRAPE_VAR_XADD, 0, GRAPE_FN_CIS, 1.0, 0.0, 1.0, 0.0}};
+    double pdiag[2] = {1.0, 1.0};
+    grape_desc d;
+    memset(&d, 0, sizeof d);
+    d.ndim = 2; d.ntimes = 4; d.nparam = 1; d.nadd = 1; d.nerr = 0; d.n_ops = 4;
+    d.t0 = 1.7; d.eps = 1e-8; d.eps2 = 1e-4;
+    d.projector_diag = pdiag; d.ops = &ops[0][0];
+    d.n_h0_terms = 3; d.h0_terms = h0;
+    d.n_target_terms = 1; d.target_terms = tgt;
+    d.max_batch = 1;
+    grape_plan *plan = NULL;
+    int rc = grape_plan_create(&d, 0, &plan);
+    if (rc) { fprintf(stderr, "plan_create %d: %s\n", rc, grape_last_error()); return 1; }
+    const double x[5] = {0.1, 0.7, -0.4, 1.3, 0.25};
+    double F = 0.0, Fdx[5];
+    rc = grape_fidelity_grad(plan, 1, x, &F, Fdx, NULL, NULL);
+    if (rc) { fprintf(stderr, "fidelity_grad %d: %s\n", rc, grape_last_error()); grape_plan_destroy(plan); return 1; }
+    printf("F %.17g\n", F);
+    for (int i = 0; i < 5; ++i) printf("F_dx %d %.17g\n", i, Fdx[i]);
+    grape_plan_destroy(plan);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu();
+    return layout();
+}
