@@ -11,10 +11,11 @@ namespace grape_dense {
 // ops/opsT/vs unused here); the operator basis is stored as padded 64 x 64
 // register-file images (grape_dense.hpp).
 struct DenseProblem {
-    grape::DevProblem P;
+    grape::DevProblem P;  // with error sources: P.nv variants per step, P.vs / off_* as the small engine
     const double *opimg;  // [n_ops][IMG]
     const double *W;      // [64] projector diagonal, zero-padded
     int Lc, Nc;           // chunk length / count of the prefix-product scan
+    int nz;               // error path: local-frame slots per step, np (Z1) + ne (W) + ne np (Z2)
 };
 
 struct DenseBatch {
@@ -30,6 +31,17 @@ struct DenseBatch {
     double *Fdx;      // [nb][nx]
     int *status;      // bit 0: singular Pade denominator
     int *mstats;      // optional [5]: Pade degree histogram (m = 3, 5, 7, 9, 13)
+    // error path (P.ne > 0; the algebra of grape_errpath.hpp on 64 x 64 images):
+    double *Ub;       // [nb][IMG]           U = C_Nt
+    double *Zl;       // [nb][Nt][nz][IMG]   Z1_u^T | W_e | Z2_{e,u}^T (local frame of step k)
+    double *Vc;       // [nb][ne][Nc][IMG]   Carry_c^dag (sum_chunk W) Carry_c
+    double *Sx;       // [nb][ne][Nc][IMG]   exclusive prefix of Vc over chunks
+    double *Tot;      // [nb][ne][IMG]       sum_k V^err_k
+    double *Me;       // [nb][ne][IMG]       M_e = G_e U
+    double *Mp;       // [nb][ne][Nc][IMG]   M'_{c,e} = Carry M_e Carry^dag
+    double *B0;       // [nb][ne][Nc][IMG]   B at the chunk start: [T_c, M'] + M' Ttot
+    double *Fd2;      // [nb][ne]
+    double *Fd2dx;    // [nb][ne][nx]
 };
 
 constexpr int kImgDoubles = 2 * 64 * 64;

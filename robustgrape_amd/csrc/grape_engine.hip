@@ -136,7 +136,8 @@ struct grape_plan {
     bool dense = false;
     grape_dense::DenseProblem DP{};
     double *dn_opimg = nullptr, *dn_W = nullptr, *dn_E = nullptr, *dn_Q = nullptr, *dn_Carry = nullptr,
-           *dn_M = nullptr, *dn_Mc = nullptr, *dn_Z = nullptr;
+           *dn_M = nullptr, *dn_Mc = nullptr, *dn_Z = nullptr, *dn_Ub = nullptr, *dn_Zl = nullptr, *dn_Vc = nullptr,
+           *dn_Sx = nullptr, *dn_Tot = nullptr, *dn_Me = nullptr, *dn_Mp = nullptr, *dn_B0 = nullptr;
     // grape_unitary_derivs workspace (allocated on first use)
     grape::VSpec *ud_vs = nullptr;
     cd *ud_E = nullptr, *ud_C = nullptr, *ud_V = nullptr, *ud_S = nullptr, *ud_out = nullptr;
@@ -170,6 +171,7 @@ static void free_plan(grape_plan *p) {
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_Zl, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
+                    p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf,
                     p->d_Htab, p->d_U0tab};
     for (void *b : bufs)
@@ -263,13 +265,13 @@ static void from_dense_image(const double *img, int d, double *dst) {
                 }
 }
 
-static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, double trP) {
-    const int D = desc->ndim;
-    if (desc->nerr > 0)
-        return fail(GRAPE_ERR_UNSUPPORTED, "dense engine (ndim > GRAPE_MAX_SMALL_DIM): error sources not supported");
-    if (xadd_dep) return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 must not depend on x_add");
+static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, double trP, int n_err_terms) {
+    const int D = desc->ndim, ne = desc->nerr;
+    if (xadd_dep) return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 / Herror must not depend on x_add");
     // Hermitian H0: checked for every engine in grape_plan_create (the dense no-interchange
-    // solve relies on it too, grape_dense.hpp)
+    // solve relies on it too, grape_dense.hpp).  The error variants exponentiate
+    // H0 + err Herror (err <= eps2): Hermitian error terms keep them inside that proof.
+    if (int rc = check_hermitian_terms(desc, desc->err_terms, n_err_terms, "error source (dense engine)")) return rc;
     if (grape_dense::set_lds_limits() != hipSuccess) return fail(GRAPE_ERR_HIP, "cannot raise LDS limit (dense)");
     p->dense = true;
     grape_dense::DenseProblem &DP = p->DP;
@@ -278,44 +280,91 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, do
     P.Nt = desc->ntimes;
     P.np = desc->nparam;
     P.na = desc->nadd;
-    P.ne = 0;
+    P.ne = ne;
     P.nx = desc->nparam * desc->ntimes + desc->nadd;
-    P.nv = 1;
     P.n_h0 = desc->n_h0_terms;
     P.n_tgt = desc->n_target_terms;
     P.dt = desc->t0 / desc->ntimes;
     P.eps = desc->eps;
     P.eps2 = desc->eps2;
     P.inv_eps = 1.0 / desc->eps;
+    P.inv_eps2sq = 1.0 / (desc->eps2 * desc->eps2);
     P.DD = trP * (trP + 1.0);
     P.Dtr = trP;
+    // propagator variants (the small engine's layout without x_add ones): nominal | dx (np)
+    // | ne > 0: dx2 (np) | per error: err(eps), err(eps2), mixed (np)   UnitaryCalculations.jl:45-83
+    std::vector<grape::VSpec> vs;
+    auto addv = [&](int var, int idx, double delta, int err, double errval) {
+        grape::VSpec v;
+        v.pert.var = var;
+        v.pert.index = idx;
+        v.pert.delta = delta;
+        v.err = err;
+        v.errval = errval;
+        vs.push_back(v);
+    };
+    addv(-1, 0, 0.0, -1, 0.0);
+    P.off_dx = P.off_dxa = (int)vs.size();
+    if (ne > 0)
+        for (int q = 0; q < P.np; ++q) addv(1, q, desc->eps, -1, 0.0);
+    P.off_dx2 = (int)vs.size();
+    if (ne > 0)
+        for (int q = 0; q < P.np; ++q) addv(1, q, desc->eps2, -1, 0.0);
+    P.off_err = (int)vs.size();
+    P.err_stride = 2 + P.np;
+    for (int e = 0; e < ne; ++e) {
+        addv(-1, 0, 0.0, e, desc->eps);
+        addv(-1, 0, 0.0, e, desc->eps2);
+        for (int q = 0; q < P.np; ++q) addv(1, q, desc->eps2, e, desc->eps2);
+    }
+    P.nv = (int)vs.size();  // 1 without error sources (k_dgrad exponentiates its variants in place)
+    P.nvg = P.np;
+    DP.nz = P.np * (1 + ne) + ne;
+    P.nz = DP.nz;
     // scan chunking: ~sqrt(N_t) chunks balances the chunk chains against the carry chain
     int nc = (int)std::ceil(std::sqrt((double)P.Nt));
     DP.Lc = (P.Nt + nc - 1) / nc;
     DP.Nc = (P.Nt + DP.Lc - 1) / DP.Lc;
-    const size_t IMG = grape_dense::kImgDoubles, MB = p->max_batch;
+    const size_t IMG = grape_dense::kImgDoubles, MB = p->max_batch, NE = ne;
     std::vector<double> img((size_t)desc->n_ops * IMG), W(64, 0.0);
     for (int o = 0; o < desc->n_ops; ++o) to_dense_image(desc->ops + 2 * (size_t)o * D * D, D, img.data() + o * IMG);
     for (int i = 0; i < D; ++i) W[i] = desc->projector_diag[i];
     bool ok = dalloc(&p->dn_opimg, img.size()) == hipSuccess && dalloc(&p->dn_W, (size_t)64) == hipSuccess &&
               dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
-              dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess &&
-              dalloc(&p->dn_E, MB * P.Nt * IMG) == hipSuccess && dalloc(&p->dn_Q, MB * P.Nt * IMG) == hipSuccess &&
+              dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess && dalloc(&p->d_vs, vs.size()) == hipSuccess &&
+              dalloc(&p->dn_E, MB * P.Nt * P.nv * IMG) == hipSuccess && dalloc(&p->dn_Q, MB * P.Nt * IMG) == hipSuccess &&
               dalloc(&p->dn_Carry, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_M, MB * IMG) == hipSuccess &&
-              dalloc(&p->dn_Mc, MB * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_Z, MB * P.Nt * IMG) == hipSuccess &&
+              dalloc(&p->dn_Mc, MB * DP.Nc * IMG) == hipSuccess &&
+              dalloc(&p->dn_Z, ne ? 1 : MB * P.Nt * IMG) == hipSuccess &&
               dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess;
+    if (ok && ne > 0)
+        ok = dalloc(&p->dn_Ub, MB * IMG) == hipSuccess && dalloc(&p->dn_Zl, MB * P.Nt * DP.nz * IMG) == hipSuccess &&
+             dalloc(&p->dn_Vc, MB * NE * DP.Nc * IMG) == hipSuccess &&
+             dalloc(&p->dn_Sx, MB * NE * DP.Nc * IMG) == hipSuccess && dalloc(&p->dn_Tot, MB * NE * IMG) == hipSuccess &&
+             dalloc(&p->dn_Me, MB * NE * IMG) == hipSuccess && dalloc(&p->dn_Mp, MB * NE * DP.Nc * IMG) == hipSuccess &&
+             dalloc(&p->dn_B0, MB * NE * DP.Nc * IMG) == hipSuccess && dalloc(&p->d_Fd2, MB * NE) == hipSuccess &&
+             dalloc(&p->d_Fd2dx, MB * NE * P.nx) == hipSuccess && dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess &&
+             dalloc(&p->d_err_off, NE + 1) == hipSuccess;
     if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense)");
     if (hipMemset(p->d_ctrl, 0, kCtrlInts * sizeof(int)) != hipSuccess ||
         hipMemcpy(p->dn_opimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->dn_W, W.data(), 64 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
             hipSuccess)
         return fail(GRAPE_ERR_HIP, "upload failed (dense)");
+    if (ne > 0 &&
+        (hipMemcpy(p->d_err, desc->err_terms, n_err_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(p->d_err_off, desc->err_term_offsets, (NE + 1) * sizeof(int), hipMemcpyHostToDevice) != hipSuccess))
+        return fail(GRAPE_ERR_HIP, "upload failed (dense error terms)");
     P.h0 = p->d_h0;
     P.tgt = p->d_tgt;
+    P.vs = p->d_vs;
+    P.err = p->d_err;
+    P.err_off = p->d_err_off;
     DP.opimg = p->dn_opimg;
     DP.W = p->dn_W;
     p->P = P;  // the C ABI reads nx / np / ne from the plan's problem for every engine
@@ -403,7 +452,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         return bail(fail(GRAPE_ERR_ALLOC, "pinned allocation failed"));
     *p->h_status = 0;
     if (D > GRAPE_MAX_SMALL_DIM) {
-        const int rcd = create_dense(desc, p, xadd_dep, trP);
+        const int rcd = create_dense(desc, p, xadd_dep, trP, n_err_terms);
         if (rcd) return bail(rcd);
         *out = p;
         return GRAPE_OK;
@@ -598,6 +647,16 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         DB.M = p->dn_M;
         DB.Mc = p->dn_Mc;
         DB.Z = p->dn_Z;
+        DB.Ub = p->dn_Ub;
+        DB.Zl = p->dn_Zl;
+        DB.Vc = p->dn_Vc;
+        DB.Sx = p->dn_Sx;
+        DB.Tot = p->dn_Tot;
+        DB.Me = p->dn_Me;
+        DB.Mp = p->dn_Mp;
+        DB.B0 = p->dn_B0;
+        DB.Fd2 = d_Fd2;
+        DB.Fd2dx = d_Fd2dx;
         DB.F = d_F;
         DB.Fdx = d_Fdx;
         DB.status = p->d_ctrl + 2;

@@ -56,3 +56,26 @@ def dense_problem(d=C5_DIM, ntimes=C5_NTIMES, dt=C5_DT, rank=C5_RANK, scale=1.0)
 def dense_x(ntimes=C5_NTIMES, seed=67, nparam=2):
     """x ~ U[-1, 1), x[p + k*nparam] = control p at step k."""
     return np.random.default_rng(seed).uniform(-1.0, 1.0, size=ntimes * nparam)
+
+
+def dense_error_problem(d=C5_DIM, ntimes=C5_NTIMES, dt=C5_DT, rank=C5_RANK, scale=1.0, nerr=2, phase=False):
+    """C5 with error sources (the dense engine's error path): error 0 is an amplitude error on
+    control 1 (Herror = err x_1 H_1, the reference idiom H(1 + err) - H), error 1 a static
+    Hermitian Ginibre perturbation (seed 69).  phase=True adds one additional parameter, a
+    phase theta on the first column of the target (target = Q (I - e0 e0^T) + Q e0 e0^T cis(theta)),
+    so that F_dx_add and the target part of F_d2err_dx_add are exercised too."""
+    from .operators import FN_CIS, VAR_XADD, OperatorBasisError
+    from .types import ErrorSource
+    fp = dense_problem(d, ntimes, dt, rank, scale)
+    Hd, H1, H2 = [scale * h for h in dense_operators(d)]
+    Hs = scale * _hermitian(d, 69)
+    errs = [ErrorSource(OperatorBasisError([Term(H1, var=VAR_X, index=0, func=FN_LINEAR)])),
+            ErrorSource(OperatorBasisError([Term(Hs)]))][:nerr]
+    up = fp.unitary_problem.replace(error_sources=errs, nb_additional_param=1 if phase else 0)
+    target = fp.target_unitary
+    if phase:
+        Q = dense_target(d)
+        P0 = np.zeros((d, d), complex)
+        P0[0, 0] = 1.0
+        target = OperatorBasisTarget([Term(Q @ (np.eye(d) - P0)), Term(Q @ P0, var=VAR_XADD, index=0, func=FN_CIS)])
+    return fp.replace(unitary_problem=up, target_unitary=target)

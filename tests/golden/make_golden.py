@@ -125,9 +125,22 @@ def make_xadd_err():
     print("wrote xadd_err", dct["F"], dct["F_d2err"])
 
 
+def make_c5err():
+    """C5 with two error sources (robustgrape_amd/synthetic.py dense_error_problem) at N_t = 64:
+    the dense engine's error path (~25 s of oracle time)."""
+    from robustgrape_amd import synthetic as S
+    nt = 64
+    x = S.dense_x(nt, seed=167)
+    dct = fid(S.dense_error_problem(64, nt), x)
+    np.savez_compressed(os.path.join(HERE, "c5err.npz"), ntimes=np.int64(nt), **dct)
+    print("wrote c5err", dct["F"], dct["F_d2err"])
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["c5"]:
         make_c5()
+    elif sys.argv[1:] == ["c5err"]:
+        make_c5err()
     elif sys.argv[1:] == ["xadd_err"]:
         make_xadd_err()
     else:

@@ -126,10 +126,65 @@ def test_dense_rejects_what_it_does_not_serve():
     from robustgrape_amd.types import ErrorSource
     fp = S.dense_problem(20, 4)
     up = fp.unitary_problem
-    errs = (ErrorSource(OperatorBasisError([Term(np.eye(20, dtype=complex))])),)
+    decay = np.diag([0.0] * 19 + [1.0]).astype(complex)  # a non-Hermitian error generator (dense: refused)
+    errs = (ErrorSource(OperatorBasisError([Term(decay, scale=-0.5j)])),)
     with pytest.raises(_capi.GrapeError, match="UNSUPPORTED"):
         GrapePlan(fp.replace(unitary_problem=up.replace(error_sources=errs)), nparam=2)
     H = np.triu(np.ones((20, 20), complex))  # not Hermitian
     bad = up.replace(H0=OperatorBasisHamiltonian([Term(H)]))
     with pytest.raises(_capi.GrapeError, match="UNSUPPORTED"):
         GrapePlan(fp.replace(unitary_problem=bad), nparam=2)
+
+
+# ---------------------------------------------------------------- error sources (d > 12)
+T3, T3_ABS = 1e-5, 1e-7
+
+
+def _assert_err(d2, d2dx, ref_d2, ref_d2dx, t2=T2):
+    assert np.max(np.abs(d2 - ref_d2)) <= t2 * np.max(np.abs(ref_d2)) + T2_ABS, (d2, ref_d2)
+    err = np.max(np.abs(d2dx - ref_d2dx))
+    assert err <= T3 * np.max(np.abs(ref_d2dx)) + T3_ABS, (err, np.max(np.abs(ref_d2dx)))
+
+
+@pytest.mark.parametrize("d,ntimes,nerr,phase,scale", [(13, 1, 1, False, 1.0), (16, 5, 2, True, 1.0),
+                                                       (24, 17, 1, False, 0.3), (40, 9, 2, True, 1.0),
+                                                       (64, 11, 2, False, 1.0)])
+def test_dense_error_sources_match_live_oracle(d, ntimes, nerr, phase, scale):
+    """The error path of the dense engine (k_dexp over every variant, k_dlocal, k_dwsum,
+    k_derr_scan, k_dmce, k_derr_grad) against the oracle: F, F_dx, F_d2err, F_d2err_dx
+    (UnitaryCalculations.jl:66-151, FidelityCalculations.jl:78-117)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = S.dense_error_problem(d, ntimes, rank=min(16, d - 3), scale=scale, nerr=nerr, phase=phase)
+    x = S.dense_x(ntimes, seed=400 + ntimes)
+    if phase:
+        x = np.concatenate([x, [0.7]])
+    ref = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, ref[0], ref[1])
+    _assert_err(d2, d2dx, ref[2], ref[3])
+    assert d2.shape == (nerr,) and d2dx.shape == (len(x), nerr)
+
+
+def test_c5err_matches_golden():
+    """C5 + 2 error sources at N_t = 64 (tests/golden/make_golden.py c5err)."""
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    g = dict(np.load(os.path.join(GOLDEN, "c5err.npz"), allow_pickle=False))
+    fp = S.dense_error_problem(64, int(g["ntimes"]))
+    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(fp, g["x"])
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    _assert_err(d2, d2dx, g["F_d2err"], g["F_d2err_dx"])
+
+
+def test_dense_error_batch_equals_single():
+    from robustgrape_amd.engine import GrapePlan
+    fp = S.dense_error_problem(32, 12)
+    X = np.stack([S.dense_x(12, seed=s) for s in range(3)])
+    plan = GrapePlan(fp, nparam=2, max_batch=3)
+    F, Fdx, d2, d2dx = plan.fidelity_grad(X)
+    plan.close()
+    one = GrapePlan(fp, nparam=2, max_batch=1)
+    F1, Fdx1, d21, d2dx1 = one.fidelity_grad(X)
+    one.close()
+    assert np.array_equal(F, F1) and np.array_equal(Fdx, Fdx1)
+    assert np.array_equal(d2, d21) and np.array_equal(d2dx, d2dx1)
