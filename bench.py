@@ -86,6 +86,8 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
     """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_profile.sh:
     separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), if it was
     recorded at this launch size (evaluations per device pass); else None."""
+    if path is None:
+        return None
     try:
         with open(path) as fh:
             js = json.load(fh)
@@ -299,6 +301,34 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
     return out
 
 
+def c5err_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam, ne):
+    # C5 + error sources (dense error path): per step nv = 1 + 2 np + ne (2 + np) stored variant
+    # exponentials (Pade 7 at this scale), nz = np (1 + ne) + ne local-frame images (2 products
+    # each), 2 products per (step, error) in k_derr_grad
+    fe = flops_expm(d, 7)
+    nv, nz = 1 + 2 * nparam + ne * (2 + nparam), nparam * (1 + ne) + ne
+    prod = 8 * d ** 3
+    flop_model = {"k_dexp": L * nt * nv * fe, "k_grad/k_err_local": L * nt * nz * 2 * prod,
+                  "k_err_grad": L * nt * ne * 2 * prod}
+    kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
+    out = {
+        "metric": "GRAPE gradient-evals/sec (fidelity+sensitivity+gradients), synthetic d=64 N_t=1024, 2 error sources",
+        "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C5 + 2 error sources (control-1 amplitude, static Ginibre), d=64, N_t=1024, np=2",
+                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
+        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, L, None),
+                         pipe="fp64 MFMA v_mfma_f64_16x16x4_f64"),
+        "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
+    }
+    # SURVEY.md 8d canonical FLOP per evaluation (ne > 0 form, na = 0)
+    canon = nt * nv * fe + 3 * nt * prod + 4 * nt * ne * prod + 8 * d ** 2 * nt * nparam * (1 + ne)
+    out["roofline"]["whole_eval"] = {"flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
+                                     "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    return out
+
+
 def c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam):
     # C5 draws Pade m = 7 for every exponential (tests/golden/c5.npz pade_hist); per launch:
     # k_dexp: B*nt nominal exps; k_dgrad: per step 2 products (Q_{k-1} M'_c, Z_k) and, per
@@ -431,7 +461,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=None,
                     help="evaluations per device pass (the plan's workspace; larger steps are chunked "
                          "by the C side); default 16384 (c2), 2048 (c3), 16 (c5)")
-    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c4opt", "c2-closure"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c5err", "c4opt", "c2-closure"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
                          "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
@@ -460,10 +490,13 @@ def main():
 
     from robustgrape_amd.engine import GrapePlan
     from robustgrape_amd.sweep import gather_best, shard
-    c5, c3 = args.workload == "c5", args.workload == "c3"
+    c5err = args.workload == "c5err"
+    c5, c3 = args.workload == "c5" or c5err, args.workload == "c3"
     if c5:
         from robustgrape_amd import synthetic as S
         fp, nparam, d, nt, inputs = S.dense_problem(), 2, S.C5_DIM, S.C5_NTIMES, c5_inputs
+        if c5err:
+            fp = S.dense_error_problem()
     elif c3:
         fp, nparam, d, nt, inputs = problem_c3(), 1, D, NT, restart_inputs
     else:
@@ -523,7 +556,9 @@ def main():
     ktimes = plan.kernel_times()
     if rank == 0:
         L = min(count, chunk)
-        if c5:
+        if c5err:
+            out = c5err_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam, ne)
+        elif c5:
             out = c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam)
         elif c3:
             out = c3_report(args, B, L, world, value, elapsed, ktimes, ne)
