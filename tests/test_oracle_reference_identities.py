@@ -112,7 +112,33 @@ def test_response_at_zero_frequency_matches_sensitivity(pulse500):
     np.testing.assert_allclose(resp_fft[0], resp[0], rtol=1e-10, atol=1e-12)
 
 
-@pytest.mark.parametrize("norm,m", [(0.01, 3), (0.2, 5), (0.5, 7), (1.5, 9), (4.0, 13), (60.0, 13)])
+def test_published_time_optimal_values(pulse500):
+    """docs/src/examples.md:200-240, 287-310 (examples/time_optimal_cz.jl) print, for the
+    reference's own optimised time-optimal pulse (N = 500, t0 = 7.613): infidelity 1.39e-13,
+    amplitude sensitivity -F_d2err[1]/2 = 4.211625822890814, frequency sensitivity
+    -F_d2err[2]/2 = 2.8602011006871577 and integrated Rydberg population
+    calculate_expectation_values(...)[end, 1] = 2.963973401634995 (2.963781384493184 in a
+    second run, :394 -- the optimiser's end point varies between runs).  Our fixture is a
+    different optimiser run (scipy L-BFGS, tests/golden/make_golden.py) reaching 6.7e-14, so the
+    published numbers are not bit-level vectors; they pin the oracle's conventions (sign,
+    the factor 2 of F_d2err, the eps normalisation of Herror, the time integration of the
+    expectation values) to within the spread of near-optimal pulses (measured: amp 1.9 %,
+    freq 0.31 %, Rydberg population 0.33 %)."""
+    from robustgrape_amd.types import ErrorSource
+    x = pulse500
+    fp = P.sym_problem(500, t0=P.T0_TO, errors=("amp", "freq"), device=False)
+    F, _, d2, _ = O.calculate_fidelity_and_derivatives(fp, x)
+    assert 1 - F < 1.4e-13
+    np.testing.assert_allclose(-d2[0] / 2, 4.211625822890814, rtol=0.025)
+    np.testing.assert_allclose(-d2[1] / 2, 2.8602011006871577, rtol=0.005)
+    decay = np.diag([0, 0, 0, 1.0, 1.0]).astype(complex)
+    fd = fp.replace(unitary_problem=fp.unitary_problem.replace(
+        error_sources=[ErrorSource(lambda t, p, xa, e: e * decay)]))
+    ev = O.calculate_expectation_values(fd, x)
+    np.testing.assert_allclose(ev[-1, 0], 2.963973401634995, rtol=0.005)
+
+
+@pytest.mark.parametrize("norm,m", [(0.01, 3),(0.2, 5), (0.5, 7), (1.5, 9), (4.0, 13), (60.0, 13)])
 def test_julia_exp_degree_and_accuracy(norm, m):
     """Julia exp! restatement: Pade degree thresholds and accuracy vs scipy.linalg.expm."""
     rng = np.random.default_rng(int(norm * 100))
