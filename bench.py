@@ -226,6 +226,16 @@ def _roofline(kname, flop_launch, ktimes, batch, pmc_path=PMC_SUMMARY):
             "per_launch_ms": per_launch_ms, "flop_per_launch": flop_launch}
 
 
+def _kernel_fracs(flop_model, ktimes):
+    """Fraction of the FP64 peak per modelled kernel (algorithmic FLOP per launch / mean launch time)."""
+    out = {}
+    for k, f in flop_model.items():
+        ms, n = ktimes.get(k, (0.0, 0))
+        if n and ms > 0:
+            out[k] = f / (ms / n * 1e-3) / 1e12 / FP64_PEAK_TFLOPS
+    return out
+
+
 def c2_report(args, B, L, world, value, elapsed, ktimes):
     # algorithmic flops per launch of the two exp-carrying kernels (DESIGN.md 4):
     # k_expm exps the nominal step propagators (B*NT items); k_expm_grad exps each
@@ -255,8 +265,10 @@ def c2_report(args, B, L, world, value, elapsed, ktimes):
     canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
     out["roofline"]["whole_eval"] = {
         "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
+        "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
         "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
         "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    out["kernels_frac"] = _kernel_fracs(flop_model, ktimes)
     # the scan is the HBM-heavy stage: E in, Q out (algorithmic 2 * 16 d^2 bytes per step)
     # against the 8 TB/s HBM3E peak, with the PMC bytes where the summary matches this batch
     ms_s, n_s = ktimes.get("k_scan", (0.0, 0))
@@ -277,9 +289,12 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
     # and per error source err(eps), err(eps2), (x + eps2, err eps2) -> 3 + 3 ne (Pade 5);
     # the x_add variants are skipped (H0 does not read x_add: their differences are exactly 0)
     nv = 3 + 3 * ne
-    # k_err_grad: one row group per (eval, chunk, error) walks the chunk, 8 complex d x d
-    # products per (step, error) (grape_errpath.hpp header)
-    flop_model = {"k_expm": L * NT * nv * flops_expm(D), "k_err_grad": L * NT * ne * 8 * 8 * D ** 3}
+    # k_err_local: per step nz = np (1 + ne) + ne local-frame images, 2 complex d x d products
+    # each; k_err_grad: per (step, error) 2 products (the B_k recurrence, grape_errpath.hpp)
+    nz = 1 * (1 + ne) + ne
+    prod = 8 * D ** 3
+    flop_model = {"k_expm": L * NT * nv * flops_expm(D), "k_grad/k_err_local": L * NT * nz * 2 * prod,
+                  "k_err_grad": L * NT * ne * 2 * prod}
     kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+sensitivity+gradients), Rydberg CZ d=9 N_t=512, 4 error sources",
@@ -296,8 +311,25 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
     # SURVEY.md 8d canonical C3 figure: 352.7 MFLOP per evaluation
     canon = NT * (1 + 2 + 2 + ne * (2 + 1 + 1)) * flops_expm(D) + 3 * NT * 8 * D ** 3 \
         + 4 * NT * ne * 8 * D ** 3 + 8 * D ** 2 * NT * 2 * (1 + ne)
-    out["roofline"]["whole_eval"] = {"flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
+    # FLOP of the work executed per evaluation: the stored variant exps, the nominal chain,
+    # the local-frame images, the B_k recurrence and the contractions
+    exe = NT * (nv * flops_expm(D) + prod + nz * 2 * prod + ne * 2 * prod + 8 * D ** 2 * (1 + ne))
+    out["roofline"]["whole_eval"] = {"flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
+                                     "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
+                                     "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
                                      "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    out["kernels_frac"] = _kernel_fracs(flop_model, ktimes)
+    # the error-path kernels stream the stored variants and local-frame images: their bound is
+    # HBM (PMC bytes per launch from the committed C3 summary over the mean launch time)
+    hbm = {}
+    for k, short in (("k_grad/k_err_local", "k_err_local"), ("k_err_grad", "k_err_grad"),
+                     ("k_err_scan", "k_err_scan"), ("k_scan", "k_scan")):
+        ms, n = ktimes.get(k, (0.0, 0))
+        t = pmc_traffic(short, L, PMC_SUMMARY_C3)
+        if n and ms > 0 and t:
+            gbs = t / (ms / n * 1e-3) / 1e9
+            hbm[short] = {"traffic_bytes": t, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+    out["kernels_hbm"] = hbm
     return out
 
 
@@ -326,6 +358,7 @@ def c5err_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam, ne):
     canon = nt * nv * fe + 3 * nt * prod + 4 * nt * ne * prod + 8 * d ** 2 * nt * nparam * (1 + ne)
     out["roofline"]["whole_eval"] = {"flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
                                      "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    out["kernels_frac"] = _kernel_fracs(flop_model, ktimes)
     return out
 
 
@@ -354,6 +387,7 @@ def c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam):
     canon = nt * ((1 + nparam) * fe + 3 * 8 * d ** 3 + nparam * 8 * d ** 2)
     out["roofline"]["whole_eval"] = {"flop_per_eval": canon, "achieved": canon * value / 1e12,
                                      "frac": canon * value / 1e12 / FP64_PEAK_TFLOPS}
+    out["kernels_frac"] = _kernel_fracs(flop_model, ktimes)
     return out
 
 
@@ -454,7 +488,7 @@ def c2_closure(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
                     help="restarts per GPU per step; default 65536 (c2), 4096 (c3), 16 (c5)")
