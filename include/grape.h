@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 3
+#define GRAPE_ABI_VERSION 4
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -52,7 +52,8 @@ typedef enum grape_status {
 /* Largest dimension served by the dense (MFMA) engine, used for
  * GRAPE_MAX_SMALL_DIM < ndim <= GRAPE_MAX_DENSE_DIM (zero-padded to 64).  It
  * requires a Hermitian H0 operator basis (Hermitian operators, real
- * coefficients), no error sources and an H0 independent of x_add. */
+ * coefficients) and H0 / error terms independent of x_add; error sources are
+ * served (Hermitian error operators). */
 #define GRAPE_MAX_DENSE_DIM 64
 
 /*
@@ -117,7 +118,13 @@ typedef struct grape_desc {
     int32_t n_target_terms;
     const grape_term *target_terms;  /* may only use GRAPE_VAR_ONE / GRAPE_VAR_XADD */
     int32_t max_batch;  /* largest nbatch a single call will use (workspace sizing); <=0 -> 256 */
-    int32_t reserved[7]; /* reserved[0]: flags (GRAPE_DESC_*); the rest must be 0 */
+    int32_t reserved[5]; /* reserved[0]: flags (GRAPE_DESC_*); the rest must be 0 */
+    /* ABI 4: the full projector P0 (FidelityRobustGRAPEProblem.projector, Types.jl:54), ndim x ndim
+     * complex, column-major, interleaved; any matrix, as FidelityCalculations.jl:47-51 accepts.
+     * NULL: projector_diag is used.  When given, projector_diag is ignored (may be NULL).  The
+     * struct size and the offsets of every earlier field are those of ABI 3 (a zero-filled
+     * ABI-3 descriptor reads as projector = NULL). */
+    const double *projector;
 } grape_desc;
 
 /*

@@ -29,8 +29,14 @@ struct GrapeDesc
     n_h0_terms::Int32; h0_terms::Ptr{GrapeTerm}
     err_term_offsets::Ptr{Int32}; err_terms::Ptr{GrapeTerm}
     n_target_terms::Int32; target_terms::Ptr{GrapeTerm}
-    max_batch::Int32; reserved::NTuple{7,Int32}
+    max_batch::Int32; reserved::NTuple{5,Int32}
+    projector::Ptr{ComplexF64}   # ABI 4: full projector (column-major) or C_NULL (diagonal)
 end
+
+# the projector as the descriptor takes it: its diagonal, and the full matrix when P0 is not
+# diagonal (FidelityCalculations.jl:47-51 accepts any real matrix)
+_pfull(P) = isdiag(P) ? ComplexF64[] : ComplexF64.(P)
+_pptr(v) = isempty(v) ? Ptr{ComplexF64}(C_NULL) : pointer(v)
 
 "One coefficient * operator term: scale * f(a*v + b) * op (v = 1, x[index], x_add[index] or nt)."
 struct OperatorTerm
@@ -83,11 +89,12 @@ function device_plan(fp, nparam::Int; device::Integer=0, max_batch::Integer=256)
         tgt = tr(fp.target_unitary.terms)
         opsflat = reduce(vcat, [vec(o) for o in ops])            # column-major, like the C side
         pdiag = Float64.(diag(fp.projector))
-        keep = Any[opsflat, h0, errs, offs, tgt, pdiag]
+        pfull = _pfull(fp.projector)
+        keep = Any[opsflat, h0, errs, offs, tgt, pdiag, pfull]
         desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, length(up.error_sources),
                              length(ops), up.t0, up.ϵ, up.ϵ2, pointer(pdiag), pointer(opsflat),
                              length(h0), pointer(h0), pointer(offs), isempty(errs) ? C_NULL : pointer(errs),
-                             length(tgt), pointer(tgt), max_batch, ntuple(_ -> Int32(0), 7)))
+                             length(tgt), pointer(tgt), max_batch, ntuple(_ -> Int32(0), 5), _pptr(pfull)))
         out = Ref{Ptr{Cvoid}}(C_NULL)
         GC.@preserve keep begin
             _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
@@ -107,15 +114,16 @@ function table_plan(fp, nparam::Int; device::Integer=0)
         up = fp.unitary_problem
         ne = length(up.error_sources)
         pdiag = Float64.(diag(fp.projector))
+        pfull = _pfull(fp.projector)
         desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, ne, 0, up.t0, up.ϵ, up.ϵ2,
                              pointer(pdiag), C_NULL, 0, C_NULL, C_NULL, C_NULL, 0, C_NULL, 1,
-                             (GRAPE_DESC_HOST_TABLES, ntuple(_ -> Int32(0), 6)...)))
+                             (GRAPE_DESC_HOST_TABLES, ntuple(_ -> Int32(0), 4)...), _pptr(pfull)))
         out = Ref{Ptr{Cvoid}}(C_NULL)
-        GC.@preserve pdiag begin
+        GC.@preserve pdiag pfull begin
             _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
                          desc, device, out))
         end
-        p = DevicePlan(out[], Any[pdiag], nparam * up.ntimes + up.nb_additional_param, ne)
+        p = DevicePlan(out[], Any[pdiag, pfull], nparam * up.ntimes + up.nb_additional_param, ne)
         finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
         p
     end

@@ -90,20 +90,24 @@ def _device_operators(fp, x, device):
 
 
 def _projector_parts(fp, dev):
-    W = torch.as_tensor(np.diag(np.asarray(fp.projector, dtype=np.float64)).copy(), device=dev).to(torch.complex128)
-    P = (W != 0).to(torch.complex128)
-    D = float(np.trace(np.asarray(fp.projector, dtype=np.float64)))
-    return W, P, D
+    """FidelityCalculations.jl:256-260: P0 = projector (any real matrix), P = P0 with every nonzero
+    entry set to 1, D = Re tr(P0); tr_mod(X) = tr(P0 X)."""
+    P0n = np.asarray(fp.projector, dtype=np.float64)
+    P0 = torch.as_tensor(P0n.astype(np.complex128), device=dev)
+    P = torch.as_tensor((P0n != 0).astype(np.complex128), device=dev)
+    return P0, P, float(np.trace(P0n))
 
 
-def _response_terms(A, B, W, P, D):
+def _response_terms(A, B, P0, P, D):
     """Re of the three trace terms of :268-272 / :333-337 for matching stacks A, B (..., d, d):
-    1/D tr(W A B P) - 1/(D(D+1)) tr(W A P B P) - 1/(D(D+1)) tr(W A P) tr(W B P), before Re."""
-    AB = A @ (B * P[None, :])                        # A B P
-    t1 = torch.einsum("i,...ii->...", W, AB)
-    APBP = (A * P[None, :]) @ (B * P[None, :])       # A P B P
-    t2 = torch.einsum("i,...ii->...", W, APBP)
-    t3 = torch.einsum("i,...ii->...", W, A * P[None, :]) * torch.einsum("i,...ii->...", W, B * P[None, :])
+    1/D tr_mod(A B P) - 1/(D(D+1)) tr_mod(A P B P) - 1/(D(D+1)) tr_mod(A P) tr_mod(B P), before Re,
+    with tr_mod(X) = tr(P0 X) = sum_ij P0_ij X_ji."""
+    def trm(X):
+        return torch.einsum("ij,...ji->...", P0, X)
+    AP, BP = A @ P, B @ P
+    t1 = trm(A @ BP)
+    t2 = trm(AP @ BP)
+    t3 = trm(AP) * trm(BP)
     return t1 / D - t2 / (D * (D + 1)) - t3 / (D * (D + 1))
 
 
@@ -118,7 +122,7 @@ def calculate_fidelity_response(fidelity_problem: FidelityRobustGRAPEProblem, x,
         return np.zeros((w.numel(), nerr))
     O = _device_operators(fidelity_problem, x, device)                # (ne, nt, d, d)
     dev = O.device
-    W, P, D = _projector_parts(fidelity_problem, dev)
+    P0, P, D = _projector_parts(fidelity_problem, dev)
     w = w.to(dev)
     k0 = torch.arange(nt, dtype=torch.float64, device=dev)            # time_indices (0-based, :262)
     k1 = k0 + 1.0                                                     # k = 1..ntimes (:266)
@@ -127,7 +131,7 @@ def calculate_fidelity_response(fidelity_problem: FidelityRobustGRAPEProblem, x,
         ph0 = torch.exp(-1j * w[:, None] * dt * k0[None, :])            # (nf, nt)
         S = torch.einsum("ft,tij->fij", ph0, O[e])                    # sum_error_freq per frequency
         ph1 = torch.exp(1j * w[:, None] * dt * k1[None, :])             # (nf, nt)
-        terms = _response_terms(O[e][None, :, :, :], S[:, None, :, :], W, P, D)  # (nf, nt)
+        terms = _response_terms(O[e][None, :, :, :], S[:, None, :, :], P0, P, D)  # (nf, nt)
         out[:, e] = dt ** 2 * torch.sum(torch.real(ph1 * terms), dim=1)
     return out.cpu().numpy()
 
@@ -146,12 +150,12 @@ def calculate_fidelity_response_fft(fidelity_problem: FidelityRobustGRAPEProblem
         return np.zeros((N, 0)), freqs
     O = _device_operators(fidelity_problem, x, device)
     dev = O.device
-    W, P, D = _projector_parts(fidelity_problem, dev)
+    P0, P, D = _projector_parts(fidelity_problem, dev)
     out = torch.empty(N, nerr, dtype=torch.float64, device=dev)
     for e in range(nerr):
         Oe = torch.zeros(N, up.ndim, up.ndim, dtype=torch.complex128, device=dev)
         Oe[:nt] = O[e]
         Ff = torch.fft.fft(Oe, dim=0)
         Fi = N * torch.fft.ifft(Oe, dim=0)
-        out[:, e] = dt ** 2 * torch.real(_response_terms(Fi, Ff, W, P, D))
+        out[:, e] = dt ** 2 * torch.real(_response_terms(Fi, Ff, P0, P, D))
     return out.cpu().numpy(), freqs

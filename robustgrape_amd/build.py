@@ -21,11 +21,13 @@ INST = os.path.join(CSRC, "grape_inst.hip")
 DENSE = os.path.join(CSRC, "grape_dense.hip")
 UNITARY = os.path.join(CSRC, "grape_unitary.hip")
 LBFGS = os.path.join(CSRC, "grape_lbfgs.hip")
+PROJ = os.path.join(CSRC, "grape_projector.hip")
 DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
-SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS]
+SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS, PROJ]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
                   ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp",
-                   "grape_dense.hpp", "grape_dense_api.hpp", "grape_unitary_api.hpp")] + \
+                   "grape_dense.hpp", "grape_dense_api.hpp", "grape_unitary_api.hpp",
+                   "grape_projector_api.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -49,7 +51,8 @@ def _units(defines):
     tag = "_".join(d.replace("=", "") for d in defines)
     sub = os.path.join(OBJ, tag or "default")
     units = [(DENSE, [], os.path.join(sub, "grape_dense.o")), (ENGINE, [], os.path.join(sub, "grape_engine.o")),
-             (UNITARY, [], os.path.join(sub, "grape_unitary.o")), (LBFGS, [], os.path.join(sub, "grape_lbfgs.o"))]
+             (UNITARY, [], os.path.join(sub, "grape_unitary.o")), (LBFGS, [], os.path.join(sub, "grape_lbfgs.o")),
+             (PROJ, [], os.path.join(sub, "grape_projector.o"))]
     units += [(INST, [f"-DGRAPE_INST_DIM={d}"], os.path.join(sub, f"grape_inst_d{d}.o")) for d in DIMS]
     return sub, units
 

@@ -692,6 +692,24 @@ hipError_t set_lds_limits() {
     return hipSuccess;
 }
 
+// the general-projector heads' view of a dense batch (grape_projector_api.hpp)
+static grape_proj::Heads dense_heads(const DenseProblem &P, const DenseBatch &B) {
+    grape_proj::Heads H{};
+    H.P = P.P;
+    H.dense = 1;
+    H.x = B.x;
+    H.Ub_img = B.Ub;
+    H.Tot_img = B.Tot;
+    H.M_img = B.M;
+    H.Me_img = B.Me;
+    H.F = B.F;
+    H.Fdx = B.Fdx;
+    H.Fd2 = B.Fd2;
+    H.Fd2dx = B.Fd2dx;
+    H.scr = B.gp_scr;
+    return H;
+}
+
 hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream_t st, const grape_host::KMark &mark) {
     const unsigned nsteps = (unsigned)((long)B.nb * P.P.Nt);
     const unsigned nchunks = (unsigned)((long)B.nb * P.Nc);
@@ -703,6 +721,10 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     mark(GRAPE_KERNEL_DSCAN, 1);
     mark(GRAPE_KERNEL_DCARRY, 0);
     hipLaunchKernelGGL(k_dcarry, dim3((unsigned)B.nb), dim3(NTHREADS), kLds, st, P, B);
+    if (P.P.gen_proj) {  // general projector: F, M (and F_dx_add's target part) in general form
+        const hipError_t e = grape_proj::launch_fid_head(dense_heads(P, B), B.nb, st);
+        if (e != hipSuccess) return e;
+    }
     mark(GRAPE_KERNEL_DCARRY, 1);
     mark(GRAPE_KERNEL_DMC, 0);
     hipLaunchKernelGGL(k_dmc, dim3(nchunks), dim3(NTHREADS), kLds, st, P, B);
@@ -720,6 +742,10 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     mark(GRAPE_KERNEL_ERR_SCAN, 0);
     hipLaunchKernelGGL(k_dwsum, dim3(nerr_chunks), dim3(NTHREADS), kLds, st, P, B);
     hipLaunchKernelGGL(k_derr_scan, dim3((unsigned)B.nb * P.P.ne), dim3(NTHREADS), kLds, st, P, B);
+    if (P.P.gen_proj) {
+        const hipError_t e = grape_proj::launch_err_head(dense_heads(P, B), B.nb, st);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_dmce, dim3(nerr_chunks), dim3(NTHREADS), kLds, st, P, B);
     mark(GRAPE_KERNEL_ERR_SCAN, 1);
     mark(GRAPE_KERNEL_ERR_GRAD, 0);

@@ -42,6 +42,7 @@ struct DenseBatch {
     double *B0;       // [nb][ne][Nc][IMG]   B at the chunk start: [T_c, M'] + M' Ttot
     double *Fd2;      // [nb][ne]
     double *Fd2dx;    // [nb][ne][nx]
+    grape::cd *gp_scr;  // general projector: head scratch (grape_projector_api.hpp)
 };
 
 constexpr int kImgDoubles = 2 * 64 * 64;

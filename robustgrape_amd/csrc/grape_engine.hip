@@ -132,6 +132,8 @@ struct grape_plan {
     bool tables = false;
     cd *d_Htab = nullptr, *d_U0tab = nullptr;
     cd *d_sink = nullptr;                      // DevBatch::sink
+    // general projector (FidelityCalculations.jl:47-51): P0 P, P, P0 row-major; head scratch
+    cd *d_PA = nullptr, *d_PB = nullptr, *d_P0g = nullptr, *d_gpscr = nullptr;
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -173,7 +175,7 @@ static void free_plan(grape_plan *p) {
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf,
-                    p->d_Htab, p->d_U0tab};
+                    p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -265,7 +267,78 @@ static void from_dense_image(const double *img, int d, double *dst) {
                 }
 }
 
-static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, double trP, int n_err_terms) {
+// The projector (FidelityCalculations.jl:47-51): the full matrix P0 when given, else its
+// diagonal.  A real diagonal P0 is served by the engines' specialised kernels (weights W);
+// anything else sets gen_proj and keeps A = P0 P, B = P (P = P0 with nonzeros set to 1)
+// and P0 itself, row-major, for the general heads (grape_projector.hip).
+struct ProjectorSetup {
+    std::vector<double> W;
+    std::vector<cd> A, B, P0;
+    bool general = false;
+    double trP = 0.0;
+};
+static ProjectorSetup setup_projector(const grape_desc *desc) {
+    const int D = desc->ndim;
+    ProjectorSetup ps;
+    ps.W.assign(D, 0.0);
+    if (!desc->projector) {
+        for (int i = 0; i < D; ++i) {
+            ps.W[i] = desc->projector_diag[i];
+            ps.trP += desc->projector_diag[i];
+        }
+        return ps;
+    }
+    const double *P0 = desc->projector;
+    ps.P0.resize((size_t)D * D);
+    for (int i = 0; i < D; ++i)
+        for (int j = 0; j < D; ++j) {
+            const cd v{P0[2 * ((size_t)i + (size_t)j * D)], P0[2 * ((size_t)i + (size_t)j * D) + 1]};
+            ps.P0[(size_t)i * D + j] = v;
+            if (i == j) {
+                ps.trP += v.re;
+                ps.W[i] = v.re;
+                if (v.im != 0.0) ps.general = true;
+            } else if (v.re != 0.0 || v.im != 0.0) {
+                ps.general = true;
+            }
+        }
+    if (!ps.general) return ps;
+    std::fill(ps.W.begin(), ps.W.end(), 0.0);  // the specialised results are all overwritten
+    ps.B.resize((size_t)D * D);
+    ps.A.assign((size_t)D * D, cd{0.0, 0.0});
+    for (size_t t = 0; t < ps.B.size(); ++t)
+        ps.B[t] = cd{(ps.P0[t].re != 0.0 || ps.P0[t].im != 0.0) ? 1.0 : 0.0, 0.0};
+    for (int i = 0; i < D; ++i)
+        for (int j = 0; j < D; ++j)
+            for (int l = 0; l < D; ++l) {
+                const cd a = ps.P0[(size_t)i * D + l], b = ps.B[(size_t)l * D + j];
+                ps.A[(size_t)i * D + j].re += a.re * b.re - a.im * b.im;
+                ps.A[(size_t)i * D + j].im += a.re * b.im + a.im * b.re;
+            }
+    return ps;
+}
+
+// uploads the general-projector matrices and sets P.gen_proj / PA / PB / P0g
+static int upload_projector(grape_plan *p, const ProjectorSetup &ps, DevProblem &P, size_t scratch_blocks) {
+    P.gen_proj = ps.general ? 1 : 0;
+    if (!ps.general) return GRAPE_OK;
+    const size_t T = ps.A.size();
+    if (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess || dalloc(&p->d_P0g, T) != hipSuccess ||
+        dalloc(&p->d_gpscr, scratch_blocks * grape_proj::kScratchSlots * T) != hipSuccess)
+        return fail(GRAPE_ERR_ALLOC, "device allocation failed (general projector)");
+    if (hipMemcpy(p->d_PA, ps.A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_PB, ps.B.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p->d_P0g, ps.P0.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(GRAPE_ERR_HIP, "upload failed (general projector)");
+    P.PA = p->d_PA;
+    P.PB = p->d_PB;
+    P.P0g = p->d_P0g;
+    return GRAPE_OK;
+}
+
+static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, const ProjectorSetup &ps,
+                        int n_err_terms) {
+    const double trP = ps.trP;
     const int D = desc->ndim, ne = desc->nerr;
     if (xadd_dep) return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 / Herror must not depend on x_add");
     // Hermitian H0: checked for every engine in grape_plan_create (the dense no-interchange
@@ -328,7 +401,7 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, do
     const size_t IMG = grape_dense::kImgDoubles, MB = p->max_batch, NE = ne;
     std::vector<double> img((size_t)desc->n_ops * IMG), W(64, 0.0);
     for (int o = 0; o < desc->n_ops; ++o) to_dense_image(desc->ops + 2 * (size_t)o * D * D, D, img.data() + o * IMG);
-    for (int i = 0; i < D; ++i) W[i] = desc->projector_diag[i];
+    for (int i = 0; i < D; ++i) W[i] = ps.W[i];
     bool ok = dalloc(&p->dn_opimg, img.size()) == hipSuccess && dalloc(&p->dn_W, (size_t)64) == hipSuccess &&
               dalloc(&p->d_h0, desc->n_h0_terms) == hipSuccess &&
               dalloc(&p->d_tgt, desc->n_target_terms) == hipSuccess && dalloc(&p->d_vs, vs.size()) == hipSuccess &&
@@ -347,7 +420,22 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, do
              dalloc(&p->dn_B0, MB * NE * DP.Nc * IMG) == hipSuccess && dalloc(&p->d_Fd2, MB * NE) == hipSuccess &&
              dalloc(&p->d_Fd2dx, MB * NE * P.nx) == hipSuccess && dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess &&
              dalloc(&p->d_err_off, NE + 1) == hipSuccess;
+    if (ok && ps.general && ne == 0) ok = dalloc(&p->dn_Ub, MB * IMG) == hipSuccess;
     if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense)");
+    if (ps.general) {  // the heads build the target from a row-major operator basis
+        std::vector<cd> ops((size_t)desc->n_ops * D * D);
+        for (int o = 0; o < desc->n_ops; ++o)
+            for (int r = 0; r < D; ++r)
+                for (int c = 0; c < D; ++c) {
+                    const double *src = desc->ops + 2 * ((size_t)o * D * D + r + (size_t)c * D);
+                    ops[(size_t)o * D * D + r * D + c] = cd{src[0], src[1]};
+                }
+        if (dalloc(&p->d_ops, ops.size()) != hipSuccess ||
+            hipMemcpy(p->d_ops, ops.data(), ops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense, general projector)");
+        P.ops = p->d_ops;
+    }
+    if (int rc = upload_projector(p, ps, P, MB * std::max<size_t>(NE, 1))) return rc;
     if (hipMemset(p->d_ctrl, 0, kCtrlInts * sizeof(int)) != hipSuccess ||
         hipMemcpy(p->dn_opimg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(p->dn_W, W.data(), 64 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
@@ -395,10 +483,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (tables) {
         if (D > GRAPE_MAX_SMALL_DIM)
             return fail(GRAPE_ERR_UNSUPPORTED, "host tables: ndim > GRAPE_MAX_SMALL_DIM needs an operator basis");
-        if (!desc->projector_diag) return fail(GRAPE_ERR_INVALID, "missing projector");
+        if (!desc->projector_diag && !desc->projector) return fail(GRAPE_ERR_INVALID, "missing projector");
     } else {
         if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
-        if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || !desc->projector_diag || !desc->target_terms ||
+        if (!desc->ops || !desc->h0_terms || desc->n_h0_terms < 1 || (!desc->projector_diag && !desc->projector) ||
+            !desc->target_terms ||
             desc->n_target_terms < 1)
             return fail(GRAPE_ERR_INVALID, "missing operator basis / terms / projector");
     }
@@ -430,8 +519,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         if (desc->h0_terms[k].var == 2) xadd_dep = true;
     for (int k = 0; k < n_err_terms; ++k)
         if (desc->err_terms[k].var == 2) xadd_dep = true;
-    double trP = 0.0;
-    for (int i = 0; i < D; ++i) trP += desc->projector_diag[i];
+    const ProjectorSetup ps = setup_projector(desc);
+    const double trP = ps.trP;
     if (!(trP > 0)) return fail(GRAPE_ERR_INVALID, "projector trace must be positive");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GRAPE_ERR_NO_DEVICE, "no HIP device");
@@ -452,7 +541,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         return bail(fail(GRAPE_ERR_ALLOC, "pinned allocation failed"));
     *p->h_status = 0;
     if (D > GRAPE_MAX_SMALL_DIM) {
-        const int rcd = create_dense(desc, p, xadd_dep, trP, n_err_terms);
+        const int rcd = create_dense(desc, p, xadd_dep, ps, n_err_terms);
         if (rcd) return bail(rcd);
         *out = p;
         return GRAPE_OK;
@@ -565,9 +654,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (ok && P.ne == 0)
         ok = dalloc(&p->d_ovf2, MB * P.Nt * nvg) == hipSuccess &&
              dalloc(&p->d_ovf2_slots, MB * P.Nt * nvg * T) == hipSuccess;
+    if (ok && (P.ne > 0 || ps.general))  // carries and U: the error path and the general-projector heads
+        ok = dalloc(&p->d_Carry, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, MB * T) == hipSuccess;
     if (ok && P.ne > 0)
-        ok = dalloc(&p->d_Carry, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, MB * T) == hipSuccess &&
-             dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
+        ok = dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
     if (ok && P.ne > 0) ok = dalloc(&p->d_Zl, MB * P.Nt * P.nz * T) == hipSuccess;
@@ -592,8 +682,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
           hipMemcpy(p->d_h0, desc->h0_terms, desc->n_h0_terms * sizeof(Term), hipMemcpyHostToDevice) != hipSuccess ||
           hipMemcpy(p->d_tgt, desc->target_terms, desc->n_target_terms * sizeof(Term), hipMemcpyHostToDevice) !=
               hipSuccess)) ||
-        hipMemcpy(p->d_W, desc->projector_diag, D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+        hipMemcpy(p->d_W, ps.W.data(), D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(GRAPE_ERR_HIP, "upload failed"));
+    if (int rcp = upload_projector(p, ps, P, MB * std::max(P.ne, 1))) return bail(rcp);
     P.ops = p->d_ops;
     P.opsT = p->d_opsT;
     P.h0 = p->d_h0;
@@ -661,6 +752,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         DB.Fdx = d_Fdx;
         DB.status = p->d_ctrl + 2;
         DB.mstats = nullptr;
+        DB.gp_scr = p->d_gpscr;
         HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, st, mk));
         return GRAPE_OK;
     }
@@ -678,12 +770,13 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     B.part_add = p->d_part;
     B.tgt_part = p->d_tgt_part;
     B.overflow = p->d_ovf;
+    B.Carry = p->d_Carry;  // allocated for the error path and the general-projector heads
+    B.Ub = p->d_Ub;
+    B.gp_scr = p->d_gpscr;
     if (P.ne == 0) {
         B.ovf2 = p->d_ovf2;
         B.ovf2_slots = p->d_ovf2_slots;
     } else {
-        B.Carry = p->d_Carry;
-        B.Ub = p->d_Ub;
         B.Me = p->d_Me;
         B.part_err_add = p->d_part_err;
         B.Zl = p->d_Zl;

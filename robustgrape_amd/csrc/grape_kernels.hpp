@@ -72,6 +72,12 @@ struct DevProblem {
     const int *err_off;  // [ne+1]
     const VSpec *vs;     // [nv]
     const double *W;     // projector diagonal (weights)
+    // general (non-diagonal or complex) projector P0: the diagonal-specialised results are
+    // overwritten by the heads of grape_projector.hip (FidelityCalculations.jl:47-51)
+    int gen_proj;
+    const cd *PA;        // P0 P  (row-major), P = P0 with nonzeros set to 1
+    const cd *PB;        // P     (row-major)
+    const cd *P0g;       // P0    (row-major; expectation values)
 };
 
 struct DevBatch {
@@ -102,6 +108,7 @@ struct DevBatch {
     // closure fallback (grape_fidelity_grad_tables): host-evaluated closures, per evaluation
     const cd *Htab;         // [nb][Nt][nv][D][D] column-major H at every closure call site (else null)
     const cd *U0tab;        // [nb][1 + na][D][D] column-major target at x_add, x_add + eps e_q (else null)
+    cd *gp_scr;             // general projector: head scratch (grape_projector_api.hpp)
 };
 
 __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,

@@ -7,6 +7,7 @@
 
 #include "grape.h"
 #include "grape_errpath.hpp"
+#include "grape_projector_api.hpp"
 
 namespace grape_host {
 
@@ -78,6 +79,10 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     else
         hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide),
                            st, P, B);
+    if (P.gen_proj) {  // general projector: F, M'_c (and F_dx_add's target part) redone in general form
+        const hipError_t e = grape_proj::launch_fid_head(grape_proj::small_heads(P, B), B.nb, st);
+        if (e != hipSuccess) return e;
+    }
     mark(GRAPE_KERNEL_SCAN, 1);
     if (fused) {
         const int nvg = P.np + (P.xadd_dep ? P.na : 0);
@@ -110,6 +115,10 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
         else
             hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
                                errscan_lds<D>(kScanWide), st, P, B);
+        if (P.gen_proj) {
+            const hipError_t e = grape_proj::launch_err_head(grape_proj::small_heads(P, B), B.nb, st);
+            if (e != hipSuccess) return e;
+        }
         mark(GRAPE_KERNEL_ERR_SCAN, 1);
         const long ne_items = (long)B.nb * P.nchunks * P.ne;
         mark(GRAPE_KERNEL_ERR_GRAD, 0);

@@ -1,0 +1,313 @@
+// grape_projector.hip -- fidelity and error-sensitivity heads for a GENERAL projector.
+//
+// The reference accepts any matrix as FidelityRobustGRAPEProblem.projector
+// (src/FidelityCalculations.jl:47-51):
+//     P0 = projector,  tr_mod(X) = tr(P0 X),  P = P0 with every nonzero entry set to 1,
+//     D = Re tr(P0),   F = [Re tr_mod(P K P K^dag) + |tr_mod(P K)|^2] / (D(D+1)),  K = U0^dag U.
+// The engines' hot kernels specialise to a real diagonal P0 (every test, example and
+// RydbergTools problem of the reference): tr_mod(P X) = sum_i w_i X_ii.  For any other P0
+// the plan sets DevProblem::gen_proj and these heads run right after the scans, over the
+// matrices the scans leave in HBM (U, the chunk carries, the error totals), and OVERWRITE
+// the diagonal-specialised results: F, the gradient kernel M = G U (and its per-chunk
+// images M'_c), the target part of F_dx_add, and with error sources F_d2err, M_e (and
+// M'_{c,e}) and the target part of F_d2err_dx_add.  Everything downstream (the gradient
+// contractions) is linear in M / M_e and is unchanged.
+//
+// With A = P0 P and B = P (both d x d), the reference's expressions are
+//   F       = [Re tr(A K B K^dag) + |tau|^2] / DD,  tau = tr(A K)                       (:54)
+//   dF      = Re tr(G dU),  M = G U = [(B K^dag A + B^dag K^dag A^dag) K + 2 conj(tau) A K] / DD
+//                                                                           (:58-63, linear in U_dx)
+//   F_dx_add target part = [Re tr(A Kd B K^dag) + Re tr(A K B Kd^dag) + 2 Re(conj(tau) tr(A Kd))] / DD,
+//             Kd = U0d^dag U, U0d = (U0(x_add + eps e_q) - U0) / eps                    (:34-40, 67-76)
+//   F_d2err = 2 [Re tr(A Ke B Ke^dag) - (1 + D) Re tr(A Ue^dag Ue) + |tau_e|^2] / DD,
+//             Ue = U_derr = U Tot, Ke = U0^dag Ue, tau_e = tr(A Ke)                      (:79-83)
+//   M_e     = 2 [(B Ke^dag A + B^dag Ke^dag A^dag) K + 2 conj(tau_e) A K
+//                - (1 + D)(A + A^dag) Ue^dag U] / DD                               (:85-97, linear in U_derr_dx)
+//   F_d2err_dx_add target part = 2 [Re tr(A Kde B Ke^dag) + Re tr(A Ke B Kde^dag)
+//                                   + 2 Re(conj(tau_e) tr(A Kde))] / DD, Kde = U0d^dag Ue   (:100-112)
+// (for A = diag(w), B = diag(w != 0) these are the hot kernels' formulas).
+//
+// These heads run once per evaluation (per error source), not per time step: plain
+// thread-per-element products over row-major d x d scratch matrices in HBM (L2-resident),
+// one 256-thread workgroup per evaluation, any d <= 64.
+#include "grape_projector_api.hpp"
+
+namespace grape_proj {
+
+namespace {
+
+using grape::cd;
+constexpr int BLOCK = 256;
+
+__device__ __forceinline__ cd p_add(cd a, cd b) { return cd{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cd p_sub(cd a, cd b) { return cd{a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cd p_scale(double s, cd a) { return cd{s * a.re, s * a.im}; }
+__device__ __forceinline__ cd p_mul(cd a, cd b) { return cd{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+__device__ __forceinline__ cd p_conj(cd a) { return cd{a.re, -a.im}; }
+
+// op(X)(i, l): X row-major, op = N (X) or H (X^dagger)
+template <bool H>
+__device__ __forceinline__ cd el(const cd *X, int D, int i, int l) {
+    return H ? p_conj(X[(size_t)l * D + i]) : X[(size_t)i * D + l];
+}
+
+// C = op(A) op(B); C must not alias A or B.  Ends with a workgroup barrier.
+template <bool HA, bool HB>
+__device__ void bmm(cd *C, const cd *A, const cd *B, int D) {
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        const int i = t / D, j = t % D;
+        cd s{0.0, 0.0};
+        for (int l = 0; l < D; ++l) s = p_add(s, p_mul(el<HA>(A, D, i, l), el<HB>(B, D, l, j)));
+        C[t] = s;
+    }
+    __syncthreads();
+}
+
+// workgroup sums (every thread receives the result)
+__device__ double bsum(double v, double *red) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = BLOCK / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+// tr(X) (complex)
+__device__ cd btrace(const cd *X, int D, double *red) {
+    double re = 0.0, im = 0.0;
+    for (int i = threadIdx.x; i < D; i += blockDim.x) {
+        re += X[(size_t)i * D + i].re;
+        im += X[(size_t)i * D + i].im;
+    }
+    return cd{bsum(re, red), bsum(im, red)};
+}
+// Re tr(X Y^dagger) = Re sum_ij X_ij conj(Y_ij)
+__device__ double bdot(const cd *X, const cd *Y, int D, double *red) {
+    double s = 0.0;
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) s += X[t].re * Y[t].re + X[t].im * Y[t].im;
+    return bsum(s, red);
+}
+// Re tr(X Y) = Re sum_ij X_ij Y_ji
+__device__ double btrprod(const cd *X, const cd *Y, int D, double *red) {
+    double s = 0.0;
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        const int i = t / D, j = t % D;
+        const cd a = X[t], b = Y[(size_t)j * D + i];
+        s += a.re * b.re - a.im * b.im;
+    }
+    return bsum(s, red);
+}
+
+// dense-engine register-file image (grape_engine.hip to_dense_image): element (row, col)
+__device__ __forceinline__ size_t img_off(int row, int col) {
+    const int w = col >> 4, t = row >> 4, r = (row & 15) >> 2, l = ((row & 3) << 4) | (col & 15);
+    return (size_t)((w * 4 + t) * 4 + r) * 64 + l;
+}
+// source matrix: row-major d x d (small engine) or a padded 64 x 64 image (dense engine)
+__device__ void load_mat(cd *dst, const void *src, int D, bool image) {
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        if (image) {
+            const double *img = static_cast<const double *>(src);
+            const size_t o = img_off(t / D, t % D);
+            dst[t] = cd{img[o], img[4096 + o]};
+        } else {
+            dst[t] = static_cast<const cd *>(src)[t];
+        }
+    }
+    __syncthreads();
+}
+__device__ void store_image(double *img, const cd *src, int D) {
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        const size_t o = img_off(t / D, t % D);
+        img[o] = src[t].re;
+        img[4096 + o] = src[t].im;
+    }
+    __syncthreads();
+}
+
+// U0(x_add [+ eps e_q]) row-major: from the target terms over the row-major operator basis,
+// or (closure fallback) from the host-evaluated table (column-major, slot 0 / 1 + q)
+__device__ void build_target(const grape::DevProblem &P, const cd *U0tab, int b, const double *xb, int slot,
+                             cd *dst) {
+    const int D = P.D;
+    const double *xadd = xb + (size_t)P.np * P.Nt;
+    grape::Pert pp;
+    pp.var = slot > 0 ? grape::VAR_XADD : -1;
+    pp.index = slot > 0 ? slot - 1 : 0;
+    pp.delta = slot > 0 ? P.eps : 0.0;
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        const int i = t / D, j = t % D;
+        if (U0tab) {
+            dst[t] = U0tab[((size_t)b * (1 + P.na) + slot) * D * D + i + (size_t)j * D];
+            continue;
+        }
+        cd h{0.0, 0.0};
+        for (int q = 0; q < P.n_tgt; ++q) {
+            const grape::Term tm = P.tgt[q];
+            h = p_add(h, p_mul(grape::term_coef(tm, 1, xb, xadd, pp), P.ops[(size_t)tm.op * D * D + t]));
+        }
+        dst[t] = h;
+    }
+    __syncthreads();
+}
+
+// dst = Carry src Carry^dagger (tmp: scratch)
+__device__ void conjugate_by(cd *dst, const cd *Carry, const cd *src, cd *tmp, int D) {
+    bmm<false, false>(tmp, Carry, src, D);
+    bmm<false, true>(dst, tmp, Carry, D);
+}
+
+enum { S_U, S_U0, S_K, S_X, S_Y, S_T1, S_T2, S_T3, S_M, S_UE, S_KE, S_XE, S_YE, S_TOT, S_C, kSlots };
+static_assert(kSlots <= kScratchSlots, "projector scratch");
+
+// F, M and the target part of F_dx_add for evaluation b = blockIdx.x
+__global__ __launch_bounds__(BLOCK) void k_proj_fid(Heads H) {
+    __shared__ double red[BLOCK];
+    const grape::DevProblem &P = H.P;
+    const int D = P.D, b = blockIdx.x;
+    const size_t T = (size_t)D * D;
+    cd *s = H.scr + (size_t)b * kScratchSlots * T;
+    cd *U = s + S_U * T, *U0 = s + S_U0 * T, *K = s + S_K * T, *X = s + S_X * T, *Y = s + S_Y * T;
+    cd *T1 = s + S_T1 * T, *T2 = s + S_T2 * T, *T3 = s + S_T3 * T, *M = s + S_M * T, *C = s + S_C * T;
+    const cd *A = P.PA, *Bm = P.PB;
+    const double *xb = H.x + (size_t)b * P.nx;
+    if (H.dense) load_mat(U, H.Ub_img + (size_t)b * kImg, D, true);
+    else load_mat(U, H.Ub + (size_t)b * T, D, false);
+    build_target(P, H.U0tab, b, xb, 0, U0);
+    bmm<true, false>(K, U0, U, D);   // K = U0^dag U
+    bmm<false, false>(X, A, K, D);   // A K
+    const cd tau = btrace(X, D, red);
+    bmm<false, false>(Y, X, Bm, D);  // A K B
+    const double Fv = (bdot(Y, K, D, red) + tau.re * tau.re + tau.im * tau.im) / P.DD;
+    // M = [B (K^dag A K) + B^dag ((A K)^dag K) + 2 conj(tau) A K] / DD
+    bmm<true, false>(T1, K, X, D);
+    bmm<false, false>(M, Bm, T1, D);
+    bmm<true, false>(T1, X, K, D);
+    bmm<true, false>(T2, Bm, T1, D);
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) {
+        const cd ct = p_mul(cd{tau.re, -tau.im}, X[t]);
+        M[t] = p_scale(1.0 / P.DD, p_add(p_add(M[t], T2[t]), p_scale(2.0, ct)));
+    }
+    __syncthreads();
+    for (int q = 0; q < P.na; ++q) {  // target part of F_dx_add
+        build_target(P, H.U0tab, b, xb, 1 + q, T1);
+        for (int t = threadIdx.x; t < (int)T; t += blockDim.x) T1[t] = p_scale(P.inv_eps, p_sub(T1[t], U0[t]));
+        __syncthreads();
+        bmm<true, false>(T2, T1, U, D);   // Kd
+        bmm<false, false>(T1, A, T2, D);  // A Kd
+        const cd trd = btrace(T1, D, red);
+        bmm<false, false>(T3, T1, Bm, D);  // A Kd B
+        const double sa = bdot(T3, K, D, red), sb = bdot(Y, T2, D, red);
+        const double val = (sa + sb + 2.0 * (tau.re * trd.re + tau.im * trd.im)) / P.DD;
+        if (threadIdx.x == 0) {
+            if (P.xadd_dep && H.tgt_part) H.tgt_part[(size_t)b * P.na + q] = val;
+            else H.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = val;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) H.F[b] = Fv;
+    if (H.dense) {  // k_dmc forms the per-chunk images from M
+        store_image(H.M_img + (size_t)b * kImg, M, D);
+        return;
+    }
+    for (int c = 0; c < P.nchunks; ++c) {  // M'_c = Carry_c M Carry_c^dagger
+        load_mat(C, H.Carry + ((size_t)b * P.nchunks + c) * T, D, false);
+        conjugate_by(T1, C, M, T2, D);
+        cd *dst = H.Mc + ((size_t)b * P.nchunks + c) * T;
+        for (int t = threadIdx.x; t < (int)T; t += blockDim.x) dst[t] = T1[t];
+        __syncthreads();
+    }
+}
+
+// F_d2err, M_e and the target part of F_d2err_dx_add for (b, e) = (blockIdx.x / ne, blockIdx.x % ne)
+__global__ __launch_bounds__(BLOCK) void k_proj_err(Heads H) {
+    __shared__ double red[BLOCK];
+    const grape::DevProblem &P = H.P;
+    const int D = P.D, ne = P.ne, b = blockIdx.x / ne, e = blockIdx.x % ne;
+    const size_t T = (size_t)D * D, be = (size_t)b * ne + e;
+    cd *s = H.scr + be * kScratchSlots * T;
+    cd *U = s + S_U * T, *U0 = s + S_U0 * T, *K = s + S_K * T, *X = s + S_X * T;
+    cd *T1 = s + S_T1 * T, *T2 = s + S_T2 * T, *T3 = s + S_T3 * T, *M = s + S_M * T, *C = s + S_C * T;
+    cd *Ue = s + S_UE * T, *Ke = s + S_KE * T, *Xe = s + S_XE * T, *Ye = s + S_YE * T, *Tot = s + S_TOT * T;
+    const cd *A = P.PA, *Bm = P.PB;
+    const double *xb = H.x + (size_t)b * P.nx;
+    if (H.dense) {
+        load_mat(U, H.Ub_img + (size_t)b * kImg, D, true);
+        load_mat(Tot, H.Tot_img + be * kImg, D, true);
+    } else {
+        load_mat(U, H.Ub + (size_t)b * T, D, false);
+        // chunk 0 of k_err_scan's [M', T_c, Ttot_c] triple: Carry_0 = I, so Ttot_0 = Tot
+        load_mat(Tot, H.Me + (be * P.nchunks) * 3 * T + 2 * T, D, false);
+    }
+    build_target(P, H.U0tab, b, xb, 0, U0);
+    bmm<false, false>(Ue, U, Tot, D);  // U_derr = U Tot                (UnitaryCalculations.jl:122-123)
+    bmm<true, false>(Ke, U0, Ue, D);
+    bmm<true, false>(K, U0, U, D);
+    bmm<false, false>(Xe, A, Ke, D);
+    const cd te = btrace(Xe, D, red);
+    bmm<false, false>(Ye, Xe, Bm, D);
+    const double t1 = bdot(Ye, Ke, D, red);
+    bmm<true, false>(T1, Ue, Ue, D);
+    const double t2 = btrprod(A, T1, D, red);  // Re tr(A Ue^dag Ue)
+    const double fd2 = 2.0 * (t1 - (1.0 + P.Dtr) * t2 + te.re * te.re + te.im * te.im) / P.DD;
+    // M_e = 2 [B Ke^dag (A K) + B^dag (A Ke)^dag K + 2 conj(te) A K - (1 + D)(A + A^dag) Ue^dag U] / DD
+    bmm<false, false>(X, A, K, D);
+    bmm<true, false>(T1, Ke, X, D);
+    bmm<false, false>(M, Bm, T1, D);
+    bmm<true, false>(T1, Xe, K, D);
+    bmm<true, false>(T2, Bm, T1, D);
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) {
+        M[t] = p_add(p_add(M[t], T2[t]), p_scale(2.0, p_mul(cd{te.re, -te.im}, X[t])));
+        const int i = t / D, j = t % D;
+        T2[t] = p_add(A[t], p_conj(A[(size_t)j * D + i]));  // A + A^dagger
+    }
+    __syncthreads();
+    bmm<true, false>(T1, Ue, U, D);
+    bmm<false, false>(T3, T2, T1, D);
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x)
+        M[t] = p_scale(2.0 / P.DD, p_sub(M[t], p_scale(1.0 + P.Dtr, T3[t])));
+    __syncthreads();
+    for (int q = 0; q < P.na; ++q) {  // target part of F_d2err_dx_add
+        build_target(P, H.U0tab, b, xb, 1 + q, T1);
+        for (int t = threadIdx.x; t < (int)T; t += blockDim.x) T1[t] = p_scale(P.inv_eps, p_sub(T1[t], U0[t]));
+        __syncthreads();
+        bmm<true, false>(T2, T1, Ue, D);  // Kde
+        bmm<false, false>(T1, A, T2, D);
+        const cd trd = btrace(T1, D, red);
+        bmm<false, false>(T3, T1, Bm, D);
+        const double sa = bdot(T3, Ke, D, red), sb = bdot(Ye, T2, D, red);
+        const double val = 2.0 * (sa + sb + 2.0 * (te.re * trd.re + te.im * trd.im)) / P.DD;
+        if (threadIdx.x == 0) H.Fd2dx[be * P.nx + (size_t)P.np * P.Nt + q] = val;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) H.Fd2[be] = fd2;
+    if (H.dense) {  // k_dmce forms M'_{c,e} and the chunk-start states from M_e
+        store_image(H.Me_img + be * kImg, M, D);
+        return;
+    }
+    for (int c = 0; c < P.nchunks; ++c) {  // M'_{c,e} = Carry_c M_e Carry_c^dagger
+        load_mat(C, H.Carry + ((size_t)b * P.nchunks + c) * T, D, false);
+        conjugate_by(T1, C, M, T2, D);
+        cd *dst = H.Me + ((be * P.nchunks) + c) * 3 * T;
+        for (int t = threadIdx.x; t < (int)T; t += blockDim.x) dst[t] = T1[t];
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+hipError_t launch_fid_head(const Heads &H, int nb, hipStream_t st) {
+    hipLaunchKernelGGL(k_proj_fid, dim3((unsigned)nb), dim3(BLOCK), 0, st, H);
+    return hipGetLastError();
+}
+
+hipError_t launch_err_head(const Heads &H, int nb, hipStream_t st) {
+    if (H.P.ne == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_proj_err, dim3((unsigned)(nb * H.P.ne)), dim3(BLOCK), 0, st, H);
+    return hipGetLastError();
+}
+
+}  // namespace grape_proj

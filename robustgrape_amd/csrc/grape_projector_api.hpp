@@ -1,0 +1,57 @@
+// grape_projector_api.hpp -- general-projector heads (grape_projector.hip) as seen by the
+// engines' launch sequences: what they read (U, carries, error totals) and what they
+// overwrite (F, M / M'_c, F_d2err, M_e / M'_{c,e}, the target parts of the x_add gradients).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "grape_kernels.hpp"
+
+namespace grape_proj {
+
+constexpr int kScratchSlots = 16;             // d x d scratch matrices per workgroup
+constexpr size_t kImg = 2 * 64 * 64;          // doubles per dense-engine image (grape_dense_api.hpp)
+
+struct Heads {
+    grape::DevProblem P;    // P.gen_proj, P.PA = P0 P, P.PB = P (row-major)
+    int dense;              // 1: U / Tot / M / M_e are dense-engine images
+    const double *x;        // [nb][nx]
+    const grape::cd *U0tab; // closure fallback target table (else null)
+    // small engine, row-major tiles
+    const grape::cd *Ub;    // [nb][D][D]
+    const grape::cd *Carry; // [nb][nchunks][D][D]
+    grape::cd *Mc;          // [nb][nchunks][D][D]          (overwritten)
+    grape::cd *Me;          // [nb][ne][nchunks][3][D][D]  M' slots overwritten; Ttot_0 = Tot read
+    // dense engine images
+    const double *Ub_img, *Tot_img;
+    double *M_img, *Me_img;  // (overwritten)
+    double *F, *Fdx, *tgt_part, *Fd2, *Fd2dx;
+    grape::cd *scr;          // [nb * max(ne, 1)][kScratchSlots][D][D]
+};
+
+// one workgroup per evaluation: F, M (small engine: M'_c of every chunk), F_dx_add target part
+hipError_t launch_fid_head(const Heads &H, int nb, hipStream_t st);
+// one workgroup per (evaluation, error source): F_d2err, M_e (small engine: M'_{c,e}),
+// F_d2err_dx_add target part
+hipError_t launch_err_head(const Heads &H, int nb, hipStream_t st);
+
+// the small engine's view (grape_launch.hpp)
+inline Heads small_heads(const grape::DevProblem &P, const grape::DevBatch &B) {
+    Heads H{};
+    H.P = P;
+    H.dense = 0;
+    H.x = B.x;
+    H.U0tab = B.U0tab;
+    H.Ub = B.Ub;
+    H.Carry = B.Carry;
+    H.Mc = B.Mc;
+    H.Me = B.Me;
+    H.F = B.F;
+    H.Fdx = B.Fdx;
+    H.tgt_part = B.tgt_part;
+    H.Fd2 = B.Fd2;
+    H.Fd2dx = B.Fd2dx;
+    H.scr = B.gp_scr;
+    return H;
+}
+
+}  // namespace grape_proj

@@ -257,7 +257,13 @@ __global__ void k_u_expect(grape::DevProblem P, const cd *O, double *ev) {
     const int D = P.D;
     cd acc{0.0, 0.0};
     for (int k = 0; k < P.Nt; ++k) {
-        for (int i = 0; i < D; ++i) acc = u_add(acc, u_scale(P.W[i], O[cm(D, (size_t)e * P.Nt + k, i, i)]));
+        if (P.gen_proj) {  // tr(P0 O) = sum_ij P0_ij O_ji for a general projector
+            for (int i = 0; i < D; ++i)
+                for (int j = 0; j < D; ++j)
+                    acc = u_add(acc, u_mul(P.P0g[i * D + j], O[cm(D, (size_t)e * P.Nt + k, j, i)]));
+        } else {
+            for (int i = 0; i < D; ++i) acc = u_add(acc, u_scale(P.W[i], O[cm(D, (size_t)e * P.Nt + k, i, i)]));
+        }
         ev[(size_t)e * P.Nt + k] = P.dt * acc.re / P.Dtr;
     }
 }

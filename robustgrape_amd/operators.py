@@ -141,7 +141,22 @@ class CDesc(ctypes.Structure):
                 ("err_term_offsets", ctypes.POINTER(ctypes.c_int32)),
                 ("err_terms", ctypes.POINTER(CTerm)),
                 ("n_target_terms", ctypes.c_int32), ("target_terms", ctypes.POINTER(CTerm)),
-                ("max_batch", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+                ("max_batch", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
+                ("projector", ctypes.POINTER(ctypes.c_double))]
+
+
+def projector_arrays(fp):
+    """(diagonal, full) host arrays of FidelityRobustGRAPEProblem.projector for grape_desc:
+    the diagonal always; the full matrix (complex, column-major, interleaved) only when P0 is
+    not diagonal -- then the engines run the general-projector heads (FidelityCalculations.jl:47-51)."""
+    P = np.asarray(fp.projector, np.float64)
+    pdiag = np.ascontiguousarray(np.diag(P).astype(np.float64))
+    if not np.count_nonzero(P - np.diag(np.diag(P))):
+        return pdiag, None
+    full = np.empty(2 * P.size, np.float64)
+    full[0::2] = P.reshape(-1, order="F")
+    full[1::2] = 0.0
+    return pdiag, full
 
 
 class DescriptorBuffers:
@@ -156,9 +171,6 @@ class DescriptorBuffers:
         for es in up.error_sources:
             if not isinstance(es.Herror, OperatorBasisError):
                 raise TypeError("device path needs OperatorBasisError error sources")
-        P = np.asarray(fp.projector, np.float64)
-        if np.count_nonzero(P - np.diag(np.diag(P))):
-            raise ValueError("device path supports diagonal projectors only")
         ops: List[np.ndarray] = []
         index = {}
 
@@ -193,7 +205,7 @@ class DescriptorBuffers:
             inter[k, 0::2] = flat.real
             inter[k, 1::2] = flat.imag
         self.ops = np.ascontiguousarray(inter.reshape(-1))
-        self.pdiag = np.ascontiguousarray(np.diag(P).astype(np.float64))
+        self.pdiag, self.pfull = projector_arrays(fp)
         dp = ctypes.POINTER(ctypes.c_double)
         self.desc = CDesc(
             ndim=d, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param,
@@ -202,7 +214,8 @@ class DescriptorBuffers:
             ops=self.ops.ctypes.data_as(dp), n_h0_terms=len(up.H0.terms), h0_terms=self.h0,
             err_term_offsets=self.offs, err_terms=self.err,
             n_target_terms=len(fp.target_unitary.terms), target_terms=self.target,
-            max_batch=int(max_batch))
+            max_batch=int(max_batch),
+            projector=self.pfull.ctypes.data_as(dp) if self.pfull is not None else None)
         del stack
 
 
@@ -231,16 +244,14 @@ class TableDescriptor:
 
     def __init__(self, fp, nparam: int, max_batch: int = 256):
         up = fp.unitary_problem
-        P = np.asarray(fp.projector, np.float64)
-        if np.count_nonzero(P - np.diag(np.diag(P))):
-            raise ValueError("device path supports diagonal projectors only")
-        self.pdiag = np.ascontiguousarray(np.diag(P).astype(np.float64))
+        self.pdiag, self.pfull = projector_arrays(fp)
         dp = ctypes.POINTER(ctypes.c_double)
         self.desc = CDesc(
             ndim=up.ndim, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param,
             nerr=len(up.error_sources), n_ops=0, t0=float(up.t0), eps=float(up.eps), eps2=float(up.eps2),
             projector_diag=self.pdiag.ctypes.data_as(dp), n_h0_terms=0, n_target_terms=0,
-            max_batch=int(max_batch), reserved=(ctypes.c_int32 * 7)(GRAPE_DESC_HOST_TABLES))
+            max_batch=int(max_batch), reserved=(ctypes.c_int32 * 5)(GRAPE_DESC_HOST_TABLES),
+            projector=self.pfull.ctypes.data_as(dp) if self.pfull is not None else None)
 
 
 # the closure tables themselves: robustgrape_amd/tables.py

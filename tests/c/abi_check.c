@@ -48,6 +48,7 @@ static int layout(void) {
     PRINT_OFF(grape_desc, target_terms);
     PRINT_OFF(grape_desc, max_batch);
     PRINT_OFF(grape_desc, reserved);
+    PRINT_OFF(grape_desc, projector);
     printf("abi_version %d\n", grape_abi_version());
     return 0;
 }

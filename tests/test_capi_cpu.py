@@ -95,13 +95,22 @@ def test_closure_problems_take_the_table_descriptor():
     np.testing.assert_array_equal(He[0, k, 12], mixa.T)  # freq, mixed stencil (x_add)
 
 
-def test_non_diagonal_projector_rejected():
+def test_projector_in_descriptor():
+    """A diagonal projector travels as projector_diag only; any other real matrix (the reference
+    accepts one, FidelityCalculations.jl:47-51) also as the full column-major complex matrix."""
     from robustgrape_amd.operators import DescriptorBuffers
     fp = P.sym_problem(8)
-    W = np.array(P.W_SYM)
+    buf = DescriptorBuffers(fp, nparam=1)
+    assert not buf.desc.projector and buf.pfull is None
+    W = np.array(P.W_SYM, dtype=float)
     W[0, 1] = 0.5
-    with pytest.raises(ValueError):
-        DescriptorBuffers(fp.replace(projector=W), nparam=1)
+    W[3, 2] = -0.25
+    buf = DescriptorBuffers(fp.replace(projector=W), nparam=1)
+    d = W.shape[0]
+    full = np.ctypeslib.as_array(buf.desc.projector, shape=(2 * d * d,))
+    np.testing.assert_array_equal(full[0::2].reshape(d, d, order="F"), W)
+    assert not full[1::2].any()
+    np.testing.assert_array_equal(np.ctypeslib.as_array(buf.desc.projector_diag, shape=(d,)), np.diag(W))
 
 
 def _create(fp, nparam=1):
