@@ -710,6 +710,25 @@ static grape_proj::Heads dense_heads(const DenseProblem &P, const DenseBatch &B)
     return H;
 }
 
+// padded register-file image -> row-major d x d tile, one workgroup per matrix
+__global__ __launch_bounds__(256) void k_img_rows(const double *img, grape::cd *rows, int D) {
+    const double *src = img + (size_t)blockIdx.x * IMG;
+    grape::cd *dst = rows + (size_t)blockIdx.x * D * D;
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        const int row = t / D, col = t % D;
+        const int w = col >> 4, tr = row >> 4, r = (row & 15) >> 2, l = ((row & 3) << 4) | (col & 15);
+        const size_t o = (size_t)((w * 4 + tr) * 4 + r) * 64 + l;
+        dst[t] = grape::cmake(src[o], src[IMG / 2 + o]);
+    }
+}
+
+hipError_t launch_variant_table(const DenseProblem &P, const DenseBatch &B, grape::cd *rows, hipStream_t st) {
+    const unsigned n = (unsigned)((long)B.nb * P.P.Nt * P.P.nv);
+    hipLaunchKernelGGL(k_dexp, dim3(n), dim3(NTHREADS), kLds, st, P, B);
+    hipLaunchKernelGGL(k_img_rows, dim3(n), dim3(256), 0, st, B.E, rows, P.P.D);
+    return hipGetLastError();
+}
+
 hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream_t st, const grape_host::KMark &mark) {
     const unsigned nsteps = (unsigned)((long)B.nb * P.P.Nt);
     const unsigned nchunks = (unsigned)((long)B.nb * P.Nc);

@@ -53,5 +53,9 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
 // n exponentials of padded images (grape_expm_batch for 12 < d <= 64).
 hipError_t launch_expm_raw(const double *A, double *E, int n, int *status, int *mstats, hipStream_t st);
 hipError_t set_lds_limits();
+// Every variant P.vs[0..P.nv) of every step of ONE evaluation (B.nb = 1): k_dexp into the
+// images B.E, then converted to row-major d x d tiles rows[Nt][nv][D][D] (the table the
+// materialised-derivative kernels of grape_unitary.hip read).
+hipError_t launch_variant_table(const DenseProblem &P, const DenseBatch &B, grape::cd *rows, hipStream_t st);
 
 }  // namespace grape_dense

@@ -144,6 +144,8 @@ struct grape_plan {
     grape::VSpec *ud_vs = nullptr;
     cd *ud_E = nullptr, *ud_C = nullptr, *ud_V = nullptr, *ud_S = nullptr, *ud_out = nullptr;
     int *ud_ovf = nullptr;
+    cd *ud_gscr = nullptr;     // d > 12: tile scratch of the grape_unitary kernels
+    double *ud_Eimg = nullptr; // dense engine: the variant table as register-file images
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -174,7 +176,7 @@ static void free_plan(grape_plan *p) {
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_Zl, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
-                    p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf,
+                    p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -422,7 +424,7 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
              dalloc(&p->d_err_off, NE + 1) == hipSuccess;
     if (ok && ps.general && ne == 0) ok = dalloc(&p->dn_Ub, MB * IMG) == hipSuccess;
     if (!ok) return fail(GRAPE_ERR_ALLOC, "device allocation failed (dense)");
-    if (ps.general) {  // the heads build the target from a row-major operator basis
+    {  // row-major operator basis: the general-projector heads and the analysis kernels
         std::vector<cd> ops((size_t)desc->n_ops * D * D);
         for (int o = 0; o < desc->n_ops; ++o)
             for (int r = 0; r < D; ++r)
@@ -942,10 +944,12 @@ static int ud_alloc(grape_plan *p) {
     const size_t nv = 1 + (np + na) * (ne > 0 ? 2 : 1) + ne * (2 + np + na);
     const size_t nslots = np + na + ne + ne * (np + na);
     const size_t nout = T * (np * Nt + na + ne + np * Nt * ne + na * ne + Nt * ne);
-    const bool ok = dalloc(&p->ud_vs, nv) == hipSuccess && dalloc(&p->ud_E, Nt * nv * T) == hipSuccess &&
+    bool ok = dalloc(&p->ud_vs, nv) == hipSuccess && dalloc(&p->ud_E, Nt * nv * T) == hipSuccess &&
                     dalloc(&p->ud_ovf, Nt * nv) == hipSuccess && dalloc(&p->ud_C, Nt * T) == hipSuccess &&
                     dalloc(&p->ud_V, Nt * nslots * T) == hipSuccess &&
                     dalloc(&p->ud_S, Nt * std::max<size_t>(ne, 1) * T) == hipSuccess && dalloc(&p->ud_out, nout) == hipSuccess;
+    if (ok && P.D > grape_unitary::kMaxD) ok = dalloc(&p->ud_gscr, grape_unitary::scratch_elems(P.D)) == hipSuccess;
+    if (ok && p->dense) ok = dalloc(&p->ud_Eimg, Nt * nv * grape_dense::kImgDoubles) == hipSuccess;
     return ok ? GRAPE_OK : fail(GRAPE_ERR_ALLOC, "device allocation failed (single-evaluation workspace)");
 }
 
@@ -980,7 +984,17 @@ static int ud_propagators(grape_plan *p, const double *x, const std::vector<grap
     Bu.overflow = p->ud_ovf;
     Bu.overflow_count = p->d_ctrl;
     Bu.status = p->d_ctrl + 2;
-    if (Htab) {
+    if (p->dense) {  // 12 < d <= 64: k_dexp over the variant list, images -> row-major tiles
+        grape_dense::DenseProblem DPu = p->DP;
+        DPu.P.nv = nv;
+        DPu.P.vs = p->ud_vs;
+        grape_dense::DenseBatch DB{};
+        DB.nb = 1;
+        DB.x = p->d_x;
+        DB.E = p->ud_Eimg;
+        DB.status = p->d_ctrl + 2;
+        HIPCHECK(grape_dense::launch_variant_table(DPu, DB, p->ud_E, st));
+    } else if (Htab) {
         HIPCHECK(hipMemcpyAsync(p->d_Htab, Htab, (size_t)P0.Nt * nv * T * sizeof(cd), hipMemcpyHostToDevice, st));
         Bu.Htab = p->d_Htab;
         HIPCHECK(dispatch_expm_table(P0.D, Pu, Bu, st));
@@ -1002,6 +1016,7 @@ static int ud_chain(grape_plan *p, const double *x, const double *H0tab) {
     UP.D = P0.D;
     UP.Nt = P0.Nt;
     UP.nv = 1;
+    UP.gscr = p->ud_gscr;
     HIPCHECK(grape_unitary::launch_chain(UP, p->ud_E, p->ud_C, p->stream));
     return GRAPE_OK;
 }
@@ -1015,15 +1030,14 @@ static int ud_interaction(grape_plan *p, const double *x, const double *H0tab, c
         cd *dO = p->ud_V;  // Nt * nslots >= Nt * ne tiles
         const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
         HIPCHECK(hipMemcpyAsync(dO, Oerr, n * sizeof(cd), hipMemcpyHostToDevice, p->stream));
-        HIPCHECK(grape_unitary::launch_interaction_table(p->P, dO, p->ud_C, p->ud_out, p->stream));
+        HIPCHECK(grape_unitary::launch_interaction_table(p->P, dO, p->ud_C, p->ud_out, p->ud_gscr, p->stream));
     } else {
-        HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->stream));
+        HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->ud_gscr, p->stream));
     }
     return GRAPE_OK;
 }
 
 static int analysis_check(grape_plan *p, bool tables_call, const char *what) {
-    if (p->dense) return fail(GRAPE_ERR_UNSUPPORTED, std::string(what) + ": dense engine not supported");
     if (p->tables && !tables_call)
         return fail(GRAPE_ERR_INVALID, std::string(what) + ": host-table plan: use the _tables entry point");
     if (!p->tables && tables_call)
@@ -1139,6 +1153,7 @@ static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, do
     const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
     if (int rc = ud_alloc(p)) return rc;
     if (int rc = ud_propagators(p, x, vs, Htab)) return rc;
+    UP.gscr = p->ud_gscr;
     hipStream_t st = p->stream;
     grape_unitary::UBuffers UB{};
     UB.E = p->ud_E;
@@ -1177,9 +1192,6 @@ static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, do
 int grape_unitary_derivs(grape_plan *p, const double *x, double *U, double *U_dx, double *U_dx_add, double *U_derr,
                          double *U_derr_dx, double *U_derr_dx_add) {
     if (!p || !x) return fail(GRAPE_ERR_INVALID, "null argument");
-    if (p->dense)
-        return fail(GRAPE_ERR_UNSUPPORTED, "grape_unitary_derivs: ndim > GRAPE_MAX_SMALL_DIM (dense engine) "
-                                           "is not supported; use grape_fidelity_grad");
     if (p->tables) return fail(GRAPE_ERR_INVALID, "grape_unitary_derivs: host-table plan: use grape_unitary_derivs_tables");
     return unitary_derivs(p, x, nullptr, U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add);
 }

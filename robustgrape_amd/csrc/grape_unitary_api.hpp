@@ -9,7 +9,11 @@ namespace grape_unitary {
 
 using grape::cd;
 
-constexpr int kMaxD = 12;  // GRAPE_MAX_SMALL_DIM
+constexpr int kMaxD = 12;      // GRAPE_MAX_SMALL_DIM: d x d tiles staged in LDS up to here
+constexpr int kTiles = 4;      // tiles per workgroup
+constexpr int kResident = 256; // d > kMaxD: workgroups of the grid-stride launches, each with
+                               // kTiles d x d tiles of global scratch (scratch_elems)
+inline size_t scratch_elems(int D) { return D > kMaxD ? (size_t)kResident * kTiles * D * D : 0; }
 
 // Propagator variants of one step, E[k][v] (built by the engine's k_expm):
 //   0 nominal | 1 + q, q < np + na: x_q + eps (controls, then x_add)
@@ -20,6 +24,7 @@ struct UProblem {
     int D, Nt, np, na, ne, nv, nslots;
     int off_x2, off_err;
     double inv_eps, inv_eps2sq;
+    cd *gscr;  // d > kMaxD: tile scratch (scratch_elems(D) complex), else unused
     __host__ __device__ int v_x2(int q) const { return off_x2 + q; }
     __host__ __device__ int v_err(int e) const { return off_err + e * (2 + np + na); }
     __host__ __device__ int v_err2(int e) const { return v_err(e) + 1; }
@@ -39,11 +44,13 @@ hipError_t launch_assembly(const UProblem &P, const UBuffers &B, hipStream_t st)
 hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st);
 // O[:, :, k, e] = C_{k-1}^dagger (Herror_e(k, eps) / eps) C_{k-1}, column-major (d, d, Nt, ne)
 // (UnitaryCalculations.jl:180-204); x is the plan's device copy of the control vector
-hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, hipStream_t st);
+hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, cd *gscr,
+                              hipStream_t st);
 // The same from host-evaluated closures (closure fallback): Oerr [Nt][ne][D][D] column-major
 // holds (1/eps) Herror_e(k, x_k, x_add, eps) as the reference forms it
-hipError_t launch_interaction_table(const grape::DevProblem &P, const cd *Oerr, const cd *C, cd *O, hipStream_t st);
-// ev[k + Nt e] = Re(dt tr(W sum_{j<=k} O_j,e) / D)   (FidelityCalculations.jl:368-390)
+hipError_t launch_interaction_table(const grape::DevProblem &P, const cd *Oerr, const cd *C, cd *O, cd *gscr,
+                                    hipStream_t st);
+// ev[k + Nt e] = Re(dt tr(P0 sum_{j<=k} O_j,e) / D)   (FidelityCalculations.jl:368-390)
 hipError_t launch_expectation(const grape::DevProblem &P, const cd *O, double *ev, hipStream_t st);
 
 }  // namespace grape_unitary

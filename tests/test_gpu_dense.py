@@ -188,3 +188,52 @@ def test_dense_error_batch_equals_single():
     one.close()
     assert np.array_equal(F, F1) and np.array_equal(Fdx, Fdx1)
     assert np.array_equal(d2, d21) and np.array_equal(d2dx, d2dx1)
+
+
+# ---------------------------------------------------------------- materialised tensors, analysis (d > 12)
+@pytest.mark.parametrize("d,ntimes,nerr,phase", [(13, 3, 0, False), (16, 5, 2, True), (40, 4, 1, False)])
+def test_dense_unitary_derivatives_match_oracle(d, ntimes, nerr, phase):
+    """calculate_unitary_and_derivatives (UnitaryCalculations.jl:20-155) on the dense engine:
+    the variant table from k_dexp (register-file images -> row-major tiles), then the
+    grape_unitary kernels over global-scratch tiles (f4 for 12 < d <= 64)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_unitary_and_derivatives
+    if nerr:
+        fp = S.dense_error_problem(d, ntimes, rank=min(16, d - 3), nerr=nerr, phase=phase)
+    else:
+        fp = S.dense_problem(d, ntimes, rank=min(16, d - 3))
+    x = S.dense_x(ntimes, seed=600 + ntimes)
+    if phase:
+        x = np.concatenate([x, [0.7]])
+    ref = O.calculate_unitary_and_derivatives(fp.unitary_problem, x)
+    out = calculate_unitary_and_derivatives(fp.unitary_problem, x)
+    names = ["U", "U_dx", "U_dx_add", "U_derr", "U_derr_dx", "U_derr_dx_add"]
+    tol = [1e-12, T2, T2, T2, T3, T3]
+    for name, a, r, t in zip(names, out, ref, tol):
+        assert a.shape == r.shape, name
+        if r.size == 0:
+            continue
+        err = np.max(np.abs(a - r))
+        print(name, f"{err:.2e}", f"{np.max(np.abs(r)):.2e}")
+        assert err <= t * max(1.0, np.max(np.abs(r))), name
+
+
+def test_dense_analysis_entry_points_match_oracle():
+    """calculate_interaction_error_operators, calculate_expectation_values and the fidelity
+    response (UnitaryCalculations.jl:180-204, FidelityCalculations.jl:246-390) at d = 20."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import analysis as A
+    nt = 12
+    fp = S.dense_error_problem(20, nt, rank=12, nerr=2)
+    x = S.dense_x(nt, seed=77)
+    Oref = O.calculate_interaction_error_operators(fp.unitary_problem, x)
+    Odev = A.calculate_interaction_error_operators(fp.unitary_problem, x)
+    assert Odev.shape == Oref.shape
+    assert np.max(np.abs(Odev - Oref)) <= T2 * np.max(np.abs(Oref)) + T2_ABS
+    ev0 = O.calculate_expectation_values(fp, x)
+    ev = A.calculate_expectation_values(fp, x)
+    assert np.max(np.abs(ev - ev0)) <= T2 * np.max(np.abs(ev0)) + T2_ABS
+    w = np.linspace(0.0, 1.0, 4)
+    r0 = O.calculate_fidelity_response(fp, x, w)
+    r = A.calculate_fidelity_response(fp, x, w)
+    assert np.max(np.abs(r - r0)) <= T2 * np.max(np.abs(r0)) + T2_ABS
