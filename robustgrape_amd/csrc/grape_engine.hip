@@ -457,6 +457,7 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
     P.err_off = p->d_err_off;
     DP.opimg = p->dn_opimg;
     DP.W = p->dn_W;
+    P.W = p->dn_W;  // zero-padded to 64; the analysis kernels (expectation values) read W[0..D)
     p->P = P;  // the C ABI reads nx / np / ne from the plan's problem for every engine
     return GRAPE_OK;
 }
