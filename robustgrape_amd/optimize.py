@@ -56,6 +56,7 @@ class OptimizationResult:
     x_converged: bool
     time_run: float
     stop_reason: str = ""
+    trace: list = field(default_factory=list)  # Optim's store_trace: (iteration, value, g_norm, time)
 
 
 @dataclass
@@ -79,7 +80,8 @@ class BatchResult:
         return OptimizationResult(self.minimizer[r].detach().cpu().numpy(), float(self.minimum[r]),
                                   int(self.iterations[r]), int(self.f_calls[r]), conv,
                                   bool(self.g_converged[r]), bool(self.f_converged[r]),
-                                  bool(self.x_converged[r]), self.time_run, reason)
+                                  bool(self.x_converged[r]), self.time_run, reason,
+                                  list(self.extra.get("trace", [])) if r == 0 else [])
 
 
 def minimizer(res):
@@ -163,12 +165,16 @@ def _device_direction(S, Y, rho, head, hist, gamma, g):
 
 def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.Tensor, *, m: int = 10,
                   iterations: int = 1000, g_tol: float = 1e-8, f_abstol: float = 0.0, f_reltol: float = 0.0,
-                  x_abstol: float = 0.0, time_limit: float = float("nan"),
+                  x_abstol: float = 0.0, time_limit: float = float("nan"), x_reltol: float = 0.0,
+                  g_reltol: float = 0.0, f_calls_limit: int = 0,
                   callback: Optional[Callable] = None) -> BatchResult:
     """Minimise fun row-wise from every row of X0.
 
     fun(X, rows) -> (f (r,), g (r, n)) evaluates the rows `rows` (int64 indices into the
-    batch) at control vectors X (r, n).  Rows stop independently (Optim's rules)."""
+    batch) at control vectors X (r, n).  Rows stop independently (Optim's rules: |g|_inf <=
+    max(g_tol, g_reltol |g_0|_inf), |df| <= f_abstol or f_reltol |f|, |dx|_inf <= x_abstol or
+    x_reltol |x|_inf, f_calls_limit (0: none)).  callback(X, f, g, iters) runs after the initial
+    evaluation and after every iteration; a True return stops every row (Optim's callback)."""
     t_start = time.perf_counter()
     X = X0.clone()
     R, n = X.shape
@@ -182,14 +188,18 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
     rho = torch.zeros(m, R, dtype=dt, device=dev)
     hist = torch.zeros(R, dtype=torch.int64, device=dev)     # stored pairs (<= m)
     head = torch.zeros(R, dtype=torch.int64, device=dev)     # next slot (ring buffer)
-    gconv = torch.amax(torch.abs(g), dim=1) <= g_tol
+    g_thr = torch.clamp(g_reltol * torch.amax(torch.abs(g), dim=1), min=g_tol)
+    gconv = torch.amax(torch.abs(g), dim=1) <= g_thr
     fconv = torch.zeros(R, dtype=torch.bool, device=dev)
     xconv = torch.zeros(R, dtype=torch.bool, device=dev)
     lsfail = torch.zeros(R, dtype=torch.bool, device=dev)
     gamma = torch.ones(R, dtype=dt, device=dev)
     timed_out = False
-    while True:
+    stopped = callback is not None and bool(callback(X, f, g, iters))
+    while not stopped:
         active = ~(gconv | fconv | xconv | lsfail) & (iters < iterations)
+        if f_calls_limit > 0:
+            active = active & (f_calls < f_calls_limit)
         if not math.isnan(time_limit) and time.perf_counter() - t_start > time_limit:
             timed_out = True
             break
@@ -320,12 +330,13 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
         f = torch.where(step, fn, f)
         g = torch.where(step[:, None], gn, g)
         iters = iters + step.to(iters.dtype)
-        gconv = gconv | (step & (torch.amax(torch.abs(g), dim=1) <= g_tol))
+        gconv = gconv | (step & (torch.amax(torch.abs(g), dim=1) <= g_thr))
         df = torch.abs(f - fold)
         fconv = fconv | (step & ((df <= f_abstol) | (df <= f_reltol * torch.abs(f))))
-        xconv = xconv | (step & (torch.amax(torch.abs(s), dim=1) <= x_abstol))
-        if callback is not None:
-            callback(X, f, iters)
+        dx = torch.amax(torch.abs(s), dim=1)
+        xconv = xconv | (step & ((dx <= x_abstol) | (dx <= x_reltol * torch.amax(torch.abs(X), dim=1))))
+        if callback is not None and bool(callback(X, f, g, iters)):
+            break
     if hasattr(fun, "check"):  # deferred device status of the last evaluation (RobustCost)
         fun.check()
     return BatchResult(X, f, g, iters, f_calls, gconv, fconv, xconv, lsfail,
@@ -455,11 +466,68 @@ def _checks(fp, params, nx):
     return nparam
 
 
+# Optim.Options keywords the reference forwards from fidelity_parameters.additional_parameters
+# (FidelityCalculations.jl:211-216; Optim.jl is third party, absent here).  Accepted without
+# effect: the options of Optim features this solver does not have (f increases are never
+# accepted by the strong-Wolfe search; no Hessian; one outer loop).
+_OPTIM_STOP = ("g_tol", "g_abstol", "g_reltol", "f_abstol", "f_reltol", "f_tol", "x_abstol", "x_reltol", "x_tol",
+               "f_calls_limit", "g_calls_limit")
+_OPTIM_TRACE = ("show_trace", "show_every", "store_trace", "extended_trace", "callback")
+_OPTIM_NOOP = ("allow_f_increases", "allow_outer_f_increases", "successive_f_tol", "show_warnings",
+               "h_calls_limit", "outer_iterations", "outer_x_abstol", "outer_x_reltol", "outer_f_abstol",
+               "outer_f_reltol", "outer_g_abstol", "outer_g_reltol", "trace_simplex")
+
+
+class _OptimTrace:
+    """Optim's show_trace / show_every / extended_trace printout and store_trace record for
+    restart 0 (the single optimisation of optimize_fidelity_and_error_sources), plus the
+    user's callback (Optim passes the trace state; returning true stops the run)."""
+
+    def __init__(self, show, every, store, extended, user_cb, t0):
+        self.show, self.every, self.store, self.extended = show, max(1, int(every)), store, extended
+        self.user_cb, self.t0, self.trace = user_cb, t0, []
+        self.last = -1
+
+    def __call__(self, X, f, g, iters):
+        it = int(iters[0])
+        if it == self.last:  # restart 0 did not move this round
+            return False
+        self.last = it
+        state = {"iteration": it, "value": float(f[0]), "g_norm": float(torch.amax(torch.abs(g[0]))),
+                 "time": time.perf_counter() - self.t0}
+        if self.extended:
+            state["x"] = X[0].detach().cpu().numpy().copy()
+            state["g(x)"] = g[0].detach().cpu().numpy().copy()
+        if self.store:
+            self.trace.append(state)
+        if self.show and it % self.every == 0:
+            if it == 0:
+                print("Iter     Function value   Gradient norm ")
+            print(f"{it:6d}   {state['value']:14e}   {state['g_norm']:14e}")
+            print(f" * time: {state['time']}")
+            if self.extended:
+                print(f" * x: {state['x']}")
+                print(f" * g(x): {state['g(x)']}")
+        return bool(self.user_cb(state)) if self.user_cb is not None else False
+
+
 def _solver_options(params):
-    ap = dict(params.additional_parameters)
-    return dict(iterations=int(params.iterations), time_limit=float(params.time_limit),
-                g_tol=float(ap.get("g_tol", ap.get("g_abstol", 1e-8))), f_abstol=float(ap.get("f_abstol", 0.0)),
-                f_reltol=float(ap.get("f_reltol", 0.0)), x_abstol=float(ap.get("x_abstol", 0.0)))
+    """lbfgs_batched keywords from FidelityRobustGRAPEParameters (iterations, time_limit and the
+    Optim.Options pass-through); an unknown keyword raises like Julia's keyword MethodError."""
+    ap = {str(k).lstrip(":"): v for k, v in dict(params.additional_parameters).items()}
+    unknown = sorted(set(ap) - set(_OPTIM_STOP + _OPTIM_TRACE + _OPTIM_NOOP))
+    if unknown:
+        raise TypeError(f"unsupported Optim option(s): {', '.join(unknown)}")
+    opts = dict(iterations=int(params.iterations), time_limit=float(params.time_limit),
+                g_tol=float(ap.get("g_tol", ap.get("g_abstol", 1e-8))), g_reltol=float(ap.get("g_reltol", 0.0)),
+                f_abstol=float(ap.get("f_abstol", 0.0)), f_reltol=float(ap.get("f_reltol", ap.get("f_tol", 0.0))),
+                x_abstol=float(ap.get("x_abstol", ap.get("x_tol", 0.0))), x_reltol=float(ap.get("x_reltol", 0.0)),
+                f_calls_limit=int(max(ap.get("f_calls_limit", 0), ap.get("g_calls_limit", 0))))
+    if any(ap.get(k) for k in ("show_trace", "store_trace", "extended_trace", "callback")):
+        opts["callback"] = _OptimTrace(bool(ap.get("show_trace", False)), ap.get("show_every", 1),
+                                       bool(ap.get("store_trace", False)), bool(ap.get("extended_trace", False)),
+                                       ap.get("callback"), time.perf_counter())
+    return opts
 
 
 def optimize_restarts(fidelity_problem: FidelityRobustGRAPEProblem, fidelity_parameters: FidelityRobustGRAPEParameters,
@@ -475,10 +543,13 @@ def optimize_restarts(fidelity_problem: FidelityRobustGRAPEProblem, fidelity_par
     # chunked by the C side instead of failing to allocate
     cost = RobustCost(fidelity_problem, fidelity_parameters, nparam, max_batch=min(X0.shape[0], MAX_PLAN_BATCH),
                       device=device, evaluate=evaluate)
+    opts = _solver_options(fidelity_parameters)
     try:
-        res = lbfgs_batched(cost, X0.to(cost.device), m=m, **_solver_options(fidelity_parameters))
+        res = lbfgs_batched(cost, X0.to(cost.device), m=m, **opts)
     finally:
         cost.close()
+    if isinstance(opts.get("callback"), _OptimTrace):
+        res.extra["trace"] = opts["callback"].trace
     return res
 
 

@@ -148,3 +148,49 @@ def test_reference_optimisation_testset_with_oracle():
     res = OPT.optimize_fidelity_and_error_sources(fp, params, evaluate=_oracle_eval(fp))
     F = O.calculate_fidelity_and_derivatives(fp, OPT.minimizer(res))[0]
     assert 1 - F < 1e-6 and res.iterations <= 40
+
+
+def _small_params(fp, **ap):
+    rng = np.random.default_rng(7)
+    x0 = np.concatenate([2 * np.pi * 0.01 * rng.uniform(size=fp.unitary_problem.ntimes), [0.3]])
+    return FidelityRobustGRAPEParameters(
+        x_initial=x0, regularization_functions=[REG.regularization_cost_phase], regularization_coeff1=[1e-6],
+        regularization_coeff2=[1e-6], error_source_coeff=[], iterations=6, additional_parameters=ap)
+
+
+def test_optim_trace_options(capsys):
+    """The Optim.Options the reference's examples pass through additional_parameters
+    (examples/time_optimal_cz.jl:38-42: show_trace, show_every; FidelityCalculations.jl:211-216):
+    Optim's trace table every show_every iterations, store_trace, a stopping callback."""
+    fp = P.sym_problem(16, device=False)
+    ev = _oracle_eval(fp)
+    res = OPT.optimize_fidelity_and_error_sources(
+        fp, _small_params(fp, show_trace=True, show_every=2, store_trace=True), evaluate=ev)
+    lines = capsys.readouterr().out.splitlines()
+    assert lines[0].split() == ["Iter", "Function", "value", "Gradient", "norm"]
+    rows = [ln.split() for ln in lines if ln.strip() and ln.split()[0].isdigit()]
+    assert [int(r[0]) for r in rows] == list(range(0, res.iterations + 1, 2))
+    assert [t["iteration"] for t in res.trace] == list(range(res.iterations + 1))
+    assert res.trace[-1]["value"] == pytest.approx(res.minimum, rel=0, abs=0)
+    for r, t in zip(rows, res.trace[::2]):
+        assert float(r[1]) == pytest.approx(t["value"], rel=1e-6)
+    # the callback sees every iteration and can stop the run (Optim: callback returns true)
+    seen = []
+    res = OPT.optimize_fidelity_and_error_sources(
+        fp, _small_params(fp, callback=lambda st: seen.append(st["iteration"]) or st["iteration"] >= 2),
+        evaluate=ev)
+    assert seen == [0, 1, 2] and res.iterations == 2
+
+
+def test_optim_options_stopping_and_unknown():
+    fp = P.sym_problem(16, device=False)
+    ev = _oracle_eval(fp)
+    res = OPT.optimize_fidelity_and_error_sources(fp, _small_params(fp, f_calls_limit=3), evaluate=ev)
+    assert res.f_calls <= 3 + OPT.MAX_LS_ROUNDS
+    big = OPT.optimize_fidelity_and_error_sources(fp, _small_params(fp, g_reltol=0.9), evaluate=ev)
+    assert big.g_converged and big.iterations < 6
+    with pytest.raises(TypeError, match="unsupported Optim option"):
+        OPT.optimize_fidelity_and_error_sources(fp, _small_params(fp, show_tracee=True), evaluate=ev)
+    # Julia-style symbol keys and the no-effect options are accepted
+    OPT.optimize_fidelity_and_error_sources(fp, _small_params(fp, **{":show_trace": False, "allow_f_increases": True}),
+                                            evaluate=ev)
