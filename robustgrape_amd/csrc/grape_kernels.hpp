@@ -665,7 +665,7 @@ __device__ __forceinline__ void tile_load(Group<D> &G, const cd *src, bool valid
 }
 template <int D>
 __device__ __forceinline__ void grad_kernel_col(Group<D> &G, const DevProblem &P, const DevBatch &B, int b, int k,
-                                                bool valid, cd (&z)[D]) {
+                                                bool valid, cd (&z)[D], cd (&e0)[D]) {
     constexpr int TILE = Geo<D>::TILE;
     const int c = k / P.L, j0 = k - c * P.L;
     const int i = G.i;
@@ -689,6 +689,9 @@ __device__ __forceinline__ void grad_kernel_col(Group<D> &G, const DevProblem &P
     gsync();
     mm_tile<D, true, true>(t, G.tile, z);  // conj(Q_k) t
     gsync();
+    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + i;
+#pragma unroll
+    for (int m = 0; m < D; ++m) e0[m] = E0[m * D];
 }
 
 // Group-summed Re sum_j z_j * (ev_j - e0_j) * inv_eps, written to F_dx (control
@@ -769,10 +772,7 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_GRAD_WAVES : 2)) void k_ex
     }
     if (valid && singular) atomicOr(B.status, 1);
     cd z[D], e0[D];
-    grad_kernel_col<D>(G, P, B, b, k, valid, z);
-    const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i;  // column i of E
-#pragma unroll
-    for (int m = 0; m < D; ++m) e0[m] = E0[m * D];
+    grad_kernel_col<D>(G, P, B, b, k, valid, z, e0);  // e0: column i of E_k
     grad_store<D>(G, P, B, b, k, u, z, x, e0, valid);
 }
 
@@ -802,10 +802,7 @@ __global__ __launch_bounds__(64) void k_grad_high(DevProblem P, DevBatch B) {
         gsync();
         if (valid && singular) atomicOr(B.status, 1);
         cd z[D], e0[D];
-        grad_kernel_col<D>(G, P, B, b, k, valid, z);
-        const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + G.i;
-#pragma unroll
-        for (int m = 0; m < D; ++m) e0[m] = E0[m * D];
+        grad_kernel_col<D>(G, P, B, b, k, valid, z, e0);
         grad_store<D>(G, P, B, b, k, u, z, x, e0, valid);
     }
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Parity tests on the default build, then bench every library variant in build_variants/.
+# Parity tests on the default build, then bench every library variant in $VARIANT_DIR (default build_variants/).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
@@ -12,7 +12,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 shopt -s nullglob
-for lib in robustgrape_amd/libgrape.so build_variants/*.so; do
+for lib in robustgrape_amd/libgrape.so ${VARIANT_DIR:-build_variants}/*.so; do
   name=$(basename $lib .so)
   GRAPE_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-paths ${BENCH_ARGS:-} > $OUT/bench_${TAG}_$name.log 2>&1
   rc=$?; echo "$name rc=$rc"
