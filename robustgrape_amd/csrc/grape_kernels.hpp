@@ -171,10 +171,10 @@ constexpr int kCachedTerms = 6;
 // Low-norm regime (m in {3, 5}): the solve-free Taylor evaluation (grape_device.hpp,
 // default) or, built with -DGRAPE_LOW_PADE=1, Julia's Pade 3 / 5 with the LU solve.
 #if defined(GRAPE_LOW_PADE) && GRAPE_LOW_PADE
-#define EXPM_LOW(m_) expm_low<D>(G, (m_), a, x, valid, singular, rebuild)
+#define EXPM_LOW(m_, ring_) expm_low<D>(G, (m_), a, x, valid, singular, rebuild)
 #define EXPM_GROUP_CD(D_) ::grape::Geo<D_>::GROUP_CD
 #else
-#define EXPM_LOW(m_) expm_taylor<D>(G, (m_), a, x, valid)
+#define EXPM_LOW(m_, ring_) expm_taylor<D, (ring_)>(G, (m_), a, x, valid)
 #define EXPM_GROUP_CD(D_) ::grape::Geo<D_>::LEAN_CD
 #endif
 #ifndef GRAPE_EXPM_GRAD_WAVES
@@ -258,6 +258,7 @@ __device__ __forceinline__ void park(Group<D> &G, cd *slot_row, const cd (&a)[D]
 #endif
 template <int D, bool ERR>
 __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm(DevProblem P, DevBatch B) {
+    constexpr int RING = ERR ? 2 : 3;  // LDS read ring of the products (mm_tile_ring)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     Group<D> G = make_group<D>(lds, threadIdx.x, EXPM_GROUP_CD(D));
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
         if (valid) park<D>(G, out, a, gid, B.overflow, B.overflow_count);
         return;
     }
-    if (m == 3 || m == 5) EXPM_LOW(m);
+    if (m == 3 || m == 5) EXPM_LOW(m, RING);
     if (valid) {  // E row-major: column i at stride D (coalesced across the group)
         cd *col = B.E + (size_t)gidc * D * D + G.i;
 #pragma unroll
@@ -310,6 +311,7 @@ struct TableBuilder {
 // k_expm for closure mode: every variant of every step from the H table
 template <int D>
 __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm_table(DevProblem P, DevBatch B) {
+    constexpr int RING = 3;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     Group<D> G = make_group<D>(lds, threadIdx.x, EXPM_GROUP_CD(D));
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
         if (valid) park<D>(G, out, a, gid, B.overflow, B.overflow_count);
         return;
     }
-    if (m == 3 || m == 5) EXPM_LOW(m);
+    if (m == 3 || m == 5) EXPM_LOW(m, RING);
     if (valid) {
         cd *col = B.E + (size_t)gidc * D * D + G.i;
 #pragma unroll
@@ -663,7 +665,7 @@ __device__ __forceinline__ void tile_load(Group<D> &G, const cd *src, bool valid
         for (int m = 0; m < D; ++m) G.tile[m * D + G.i] = src[m * D + G.i];
     }
 }
-template <int D>
+template <int D, int RING = 0>
 __device__ __forceinline__ void grad_kernel_col(Group<D> &G, const DevProblem &P, const DevBatch &B, int b, int k,
                                                 bool valid, cd (&z)[D], cd (&e0)[D]) {
     constexpr int TILE = Geo<D>::TILE;
@@ -679,7 +681,7 @@ __device__ __forceinline__ void grad_kernel_col(Group<D> &G, const DevProblem &P
     tile_load<D>(G, Mc, valid);
     gsync();
     if (j0 > 0) {
-        mm_tile<D>(r, G.tile, t);  // M'^T r
+        mm_tile_r<D, RING>(r, G.tile, t);  // M'^T r
     } else {
 #pragma unroll
         for (int m = 0; m < D; ++m) t[m] = G.tile[i * D + m];  // row i of M'
@@ -687,7 +689,7 @@ __device__ __forceinline__ void grad_kernel_col(Group<D> &G, const DevProblem &P
     gsync();
     tile_load<D>(G, Qk, valid);
     gsync();
-    mm_tile<D, true, true>(t, G.tile, z);  // conj(Q_k) t
+    mm_tile_r<D, RING, true, true>(t, G.tile, z);  // conj(Q_k) t
     gsync();
     const cd *E0 = B.E + (((size_t)b * P.Nt + k) * P.nv) * TILE + i;
 #pragma unroll
@@ -746,6 +748,7 @@ __global__ __launch_bounds__(64, (D <= 9 ? 4 : 2)) void k_grad(DevProblem P, Dev
 // parked (A to a slot) for k_grad_high.
 template <int D>
 __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_GRAD_WAVES : 2)) void k_expm_grad(DevProblem P, DevBatch B) {
+    constexpr int RING = 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     constexpr int TILE = Geo<D>::TILE;
@@ -765,14 +768,14 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_GRAD_WAVES : 2)) void k_ex
     rebuild(a);
     int singular = 0, s = 0;
     const int m = expm_prologue_fast<D>(G, a, x, valid, s);
-    if (m == 3 || m == 5) EXPM_LOW(m);
+    if (m == 3 || m == 5) EXPM_LOW(m, RING);
     if (m > 5) {
         if (valid) park<D>(G, B.ovf2_slots + (size_t)gidc * TILE + G.i * D, a, gid, B.ovf2, B.ovf2_count);
         return;  // group-uniform: the whole group parks
     }
     if (valid && singular) atomicOr(B.status, 1);
     cd z[D], e0[D];
-    grad_kernel_col<D>(G, P, B, b, k, valid, z, e0);  // e0: column i of E_k
+    grad_kernel_col<D, RING>(G, P, B, b, k, valid, z, e0);  // e0: column i of E_k
     grad_store<D>(G, P, B, b, k, u, z, x, e0, valid);
 }
 
