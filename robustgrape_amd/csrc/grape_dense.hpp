@@ -569,6 +569,72 @@ __device__ __forceinline__ void hm_pin(HM &M) {
 // through the Pade polynomial (register budget: 256 VGPRs at 2 waves/SIMD).
 // Uses all of LDS [0, LDS_TOTAL).  Returns the Pade degree m.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Solve-free regime (Julia's Pade 3 / 5 / 7, |A|_1 <= 0.95): the Taylor polynomial of the same
+// accuracy, degree 12 (|A|_1 <= 0.25: remainder |A|^13/13! <= 2.4e-18) or 18 (|A|_1 <= 0.95:
+// |A|^19/19! <= 3.1e-18), by Paterson-Stockmeyer in A^4:
+//   T = B0 + A4 (B1 + A4 (B2 [+ A4 (B3 + A4 B4)])),  B_j = sum_{i<4} c_{4j+i} A^i  (top block
+//   also + c_{4J} A4 for degree 12, c16 I + c17 A + c18 A^2 for degree 18).
+// Products: A^2, A^3, A^4 and 2 (degree 12) or 4 (degree 18) Horner steps, all MFMA streams --
+// no Gauss-Jordan solve, whose serial 16 x 16 block inversions left the MFMA pipe idle for
+// about as long as the Pade products took.  Agrees with exp! to a few u (inside T0).
+// ---------------------------------------------------------------------------
+__constant__ const double kDInvFact[19] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040,
+                                           1.0 / 40320, 1.0 / 362880, 1.0 / 3628800, 1.0 / 39916800,
+                                           1.0 / 479001600, 1.0 / 6227020800.0, 1.0 / 87178291200.0,
+                                           1.0 / 1307674368000.0, 1.0 / 20922789888000.0,
+                                           1.0 / 355687428096000.0, 1.0 / 6402373705728000.0};
+
+// x = c0 I + c1 A + c2 A2 + c3 A3 (+ c4 A4) for coefficients kDInvFact[b..]
+__device__ __forceinline__ void taylor_block(HM &x, int b, int n, const HM &A, const HM &A2, const HM &A3,
+                                             const HM *A4, const Lane &ln) {
+    hm_identity(x, ln, kDInvFact[b]);
+    if (n > 1) hm_axpy(x, kDInvFact[b + 1], A);
+    if (n > 2) hm_axpy(x, kDInvFact[b + 2], A2);
+    if (n > 3) hm_axpy(x, kDInvFact[b + 3], A3);
+    if (n > 4 && A4) hm_axpy(x, kDInvFact[b + 4], *A4);
+}
+
+// A is in S0 and in registers; returns X = T(A).  Uses both LDS regions.
+__device__ __forceinline__ void wg_expm_taylor(const HM &A, int degree, HM &X, double *lds, const Lane &ln) {
+    SM S0 = sm_at(lds, LDS_R0), S1 = sm_at(lds, LDS_R1);
+    HM A2, A3;
+    hm_zero(A2);
+    mm<false, false, false, false>(S0, S0, A2, ln);  // A^2
+    __syncthreads();
+    sm_store(S1, A2, ln);
+    __syncthreads();
+    hm_zero(A3);
+    mm<false, false, false, false>(S0, S1, A3, ln);  // A . A^2
+    {
+        HM A4;
+        hm_zero(A4);
+        mm<false, false, false, false>(S1, S1, A4, ln);  // A^2 . A^2
+        __syncthreads();
+        sm_store(S0, A4, ln);  // the Horner left operand from here on
+        if (degree == 12) taylor_block(X, 8, 5, A, A2, A3, &A4, ln);  // c8..c12
+        else taylor_block(X, 16, 3, A, A2, A3, nullptr, ln);          // c16..c18
+        hm_pin(X);
+    }
+    const int top = degree == 12 ? 1 : 3;  // blocks B_top .. B_0 below the initial one
+    for (int j = top; j >= 0; --j) {
+        __syncthreads();  // S1's previous contents consumed
+        sm_store(S1, X, ln);
+        __syncthreads();
+        HM P;
+        hm_zero(P);
+        mm<false, false, false, false>(S0, S1, P, ln);  // A^4 . x
+        taylor_block(X, 4 * j, 4, A, A2, A3, nullptr, ln);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            X.re[i] += P.re[i];
+            X.im[i] += P.im[i];
+        }
+        hm_pin(X);
+    }
+    __syncthreads();  // every wave done with the LDS regions
+}
+
 template <class Build>
 __device__ __forceinline__ int wg_expm(const Build &build, HM &X, double *lds, const Lane &ln, bool &singular) {
     SM S0 = sm_at(lds, LDS_R0), S1 = sm_at(lds, LDS_R1);
@@ -583,6 +649,10 @@ __device__ __forceinline__ int wg_expm(const Build &build, HM &X, double *lds, c
         __syncthreads();
         sm_store(S0, A, ln);
         __syncthreads();
+        if (m <= 7) {  // Julia's Pade 3 / 5 / 7 regime: solve-free Taylor (above)
+            wg_expm_taylor(A, m == 7 ? 18 : 12, X, lds, ln);
+            return m;
+        }
     }
     const double *C = kDPade[m_index(m)];
     if (m <= 9) {
