@@ -12,6 +12,8 @@
 //   C tile (16 x 16):     lane l, element r holds C[(l >> 4) + 4r][l & 15]
 //
 // (checked on the hardware with exact integer data, scripts/probes/mfma_probe.hip).
+// With GRAPE_DENSE_3M (default) the four real GEMMs become Gauss's three
+// (Lr Rr, Li Ri, (Lr + Li)(Rr + Ri)).
 // Element r of a C tile is therefore the B fragment of k-rows 4r..4r+3: a
 // matrix kept in registers in C-tile layout IS the right operand of the next
 // product, with no data movement.  Register matrices (HM) are distributed by
@@ -264,8 +266,47 @@ __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &
 // Software-pipelined over the 16 k-steps: the fragments of step s+1 are loaded
 // while step s's 8 MFMAs issue; the "memory" pin stops the compiler from hoisting
 // every step's loads to the top (that costs ~100 VGPRs and forces spills).
+// Gauss's 3-multiplication complex product (default): 3 real MFMA streams per complex
+// product instead of 4; rounding-level differences only (the dense parity tests hold at T0).
+// Measured at C5: 940 -> 1 064 evals/s, k_dgrad 0.52 -> 0.58 of the FP64 peak credited with
+// the algorithmic 8 d^3 per complex product (executed: 6 d^3).  -DGRAPE_DENSE_3M=0: 4 products.
+#ifndef GRAPE_DENSE_3M
+#define GRAPE_DENSE_3M 1
+#endif
 template <bool LT, bool LC, bool RT, bool RC>
 __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
+#if GRAPE_DENSE_3M
+    // Gauss's three-multiplication complex product: T1 = Lr Rr, T2 = Li Ri, T3 = (Lr + Li)(Rr + Ri),
+    // P += (T1 - T2) + i (T3 - T1 - T2): 3 MFMAs per tile and k-step instead of 4.
+    Frag fc, fn;
+    v4d t1[2], t2[2], t3[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) t1[i] = t2[i] = t3[i] = v4d{0.0, 0.0, 0.0, 0.0};
+    mm_load<LT, RT, RC>(L, R, 0, fc, ln);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        if (s < 15) mm_load<LT, RT, RC>(L, R, s + 1, fn, ln);
+        const double bs = fc.bR + fc.bI;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const double ai = LC ? -fc.aI[i] : fc.aI[i];
+            t1[i] = mfma(fc.aR[i], fc.bR, t1[i]);
+            t2[i] = mfma(ai, fc.bI, t2[i]);
+            t3[i] = mfma(fc.aR[i] + ai, bs, t3[i]);
+        }
+        if (s < 15) {
+            fc = fn;
+            asm volatile("" : "+v"(fc.aR[0]), "+v"(fc.aR[1]), "+v"(fc.aI[0]), "+v"(fc.aI[1]), "+v"(fc.bR),
+                         "+v"(fc.bI)::"memory");
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        P.re[i] += t1[i] - t2[i];
+        P.im[i] += t3[i] - t1[i] - t2[i];
+    }
+    return;
+#endif
     Frag cur, nxt;
     mm_load<LT, RT, RC>(L, R, 0, cur, ln);
 #pragma unroll
