@@ -146,6 +146,14 @@ struct grape_plan {
     int *ud_ovf = nullptr;
     cd *ud_gscr = nullptr;     // d > 12: tile scratch of the grape_unitary kernels
     double *ud_Eimg = nullptr; // dense engine: the variant table as register-file images
+    // small host-array calls (the reference's one-x-per-call pattern): the whole call --
+    // H2D copy, every launch, D2H copies -- replayed as one captured HIP graph per batch size
+    struct GraphEntry {
+        int nb;
+        hipGraphExec_t exec;
+    };
+    std::vector<GraphEntry> graphs;
+    double *h_x = nullptr, *h_F = nullptr, *h_Fdx = nullptr, *h_Fd2 = nullptr, *h_Fd2dx = nullptr;  // pinned
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -185,6 +193,9 @@ static void free_plan(grape_plan *p) {
         (void)hipEventDestroy(pe.a);
         (void)hipEventDestroy(pe.b);
     }
+    for (auto &g : p->graphs) (void)hipGraphExecDestroy(g.exec);
+    for (double *h : {p->h_x, p->h_F, p->h_Fdx, p->h_Fd2, p->h_Fd2dx})
+        if (h) (void)hipHostFree(h);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
@@ -852,6 +863,84 @@ int grape_plan_synchronize(grape_plan *p) {
     return GRAPE_OK;
 }
 
+// Host-array calls of at most kGraphBatch evaluations are latency-bound (a 1-evaluation C2
+// call is ~10 dependent launches and copies of a few KB): they are captured once per batch size
+// into a HIP graph -- pinned staging copies in, the pipeline, status and results out -- and
+// replayed with one launch.  GRAPE_NO_GRAPH=1 (or profiling) takes the stream path.
+constexpr int kGraphBatch = 64, kGraphCache = 8;
+
+static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
+    const int nx = p->P.nx, ne = p->P.ne;
+    hipStream_t st = p->stream;
+    HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    auto body = [&]() -> int {
+        HIPCHECK(hipMemcpyAsync(p->d_x, p->h_x, (size_t)nb * nx * sizeof(double), hipMemcpyHostToDevice, st));
+        if (int rc = enqueue_call(p, nb, p->d_x, p->d_F, p->d_Fdx, p->d_Fd2, p->d_Fd2dx)) return rc;
+        HIPCHECK(hipMemcpyAsync(p->h_F, p->d_F, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(p->h_Fdx, p->d_Fdx, (size_t)nb * nx * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (ne > 0) {
+            HIPCHECK(hipMemcpyAsync(p->h_Fd2, p->d_Fd2, (size_t)nb * ne * sizeof(double), hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(p->h_Fd2dx, p->d_Fd2dx, (size_t)nb * ne * nx * sizeof(double),
+                                    hipMemcpyDeviceToHost, st));
+        }
+        return GRAPE_OK;
+    };
+    const int rc = body();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(st, &g);
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    hipGraphExec_t ex = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
+    if ((int)p->graphs.size() >= kGraphCache) {
+        (void)hipGraphExecDestroy(p->graphs.front().exec);
+        p->graphs.erase(p->graphs.begin());
+    }
+    p->graphs.push_back({nb, ex});
+    *out = ex;
+    return GRAPE_OK;
+}
+
+static bool graph_path(const grape_plan *p, int nbatch) {
+    static const bool disabled = std::getenv("GRAPE_NO_GRAPH") != nullptr;
+    return !disabled && !p->profiling && !p->tables && nbatch > 0 && nbatch <= kGraphBatch &&
+           nbatch <= p->max_batch;
+}
+
+static int fidelity_grad_graph(grape_plan *p, int nb, const double *x, double *F, double *F_dx, double *F_d2err,
+                               double *F_d2err_dx) {
+    const size_t nx = p->P.nx, ne = p->P.ne, B = std::min(kGraphBatch, p->max_batch);
+    if (!p->h_x) {
+        auto pin = [](double **h, size_t n) {
+            return hipHostMalloc(reinterpret_cast<void **>(h), std::max<size_t>(n, 1) * sizeof(double),
+                                 hipHostMallocDefault) == hipSuccess;
+        };
+        if (!pin(&p->h_x, B * nx) || !pin(&p->h_F, B) || !pin(&p->h_Fdx, B * nx) || !pin(&p->h_Fd2, B * ne) ||
+            !pin(&p->h_Fd2dx, B * ne * nx))
+            return fail(GRAPE_ERR_ALLOC, "pinned allocation failed (graph path)");
+    }
+    hipGraphExec_t ex = nullptr;
+    for (auto &g : p->graphs)
+        if (g.nb == nb) ex = g.exec;
+    if (!ex)
+        if (int rc = graph_capture(p, nb, &ex)) return rc;
+    std::memcpy(p->h_x, x, (size_t)nb * nx * sizeof(double));
+    HIPCHECK(hipGraphLaunch(ex, p->stream));
+    if (int rc = grape_plan_synchronize(p)) return rc;
+    std::memcpy(F, p->h_F, (size_t)nb * sizeof(double));
+    std::memcpy(F_dx, p->h_Fdx, (size_t)nb * nx * sizeof(double));
+    if (ne > 0) {
+        std::memcpy(F_d2err, p->h_Fd2, (size_t)nb * ne * sizeof(double));
+        std::memcpy(F_d2err_dx, p->h_Fd2dx, (size_t)nb * ne * nx * sizeof(double));
+    }
+    return GRAPE_OK;
+}
+
 int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, double *F_dx, double *F_d2err,
                         double *F_d2err_dx) {
     if (!p || nbatch < 0 || (nbatch > 0 && (!x || !F || !F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
@@ -859,6 +948,7 @@ int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, d
     if (p->P.ne > 0 && nbatch > 0 && (!F_d2err || !F_d2err_dx))
         return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     HIPCHECK(hipSetDevice(p->device));
+    if (graph_path(p, nbatch)) return fidelity_grad_graph(p, nbatch, x, F, F_dx, F_d2err, F_d2err_dx);
     const int nx = p->P.nx;
     for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
         const int nb = std::min(p->max_batch, nbatch - b0);
