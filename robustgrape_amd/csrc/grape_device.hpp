@@ -112,6 +112,14 @@ __device__ __forceinline__ Group<D> make_group(cd *wave_lds, int lane, int strid
 // use row groups launch 64-thread (one-wave) workgroups or keep every wave on
 // the same barrier sequence.
 __device__ __forceinline__ void gsync() { __syncthreads(); }
+// Wave-local synchronisation for phases in which each group touches only its own tile: the
+// LDS accesses of one wave complete in order, so a fence at wavefront scope is all a group
+// needs between publishing its tile and reading it back -- no workgroup barrier.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <int D>
 __device__ __forceinline__ void tile_store_row(Group<D> &G, const cd (&r)[D], bool wr) {

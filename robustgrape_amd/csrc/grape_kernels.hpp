@@ -460,9 +460,9 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
             for (int m = 0; m < D; ++m) q[m] = e[m];
         } else {
             tile_store_row(G, e, gvalid);  // E_k column-major in the tile (lanes outside a group must not write)
-            gsync();
+            wsync();  // the chains are independent: no workgroup barrier inside Phase A (k_scan 19.0 -> 18.7 ms)
             mm_tile_pf<D>(q, G.tile, t);  // E_k . q
-            gsync();
+            wsync();
             if (act) {  // past N_t (last chunk's tail) the total stays put
 #pragma unroll
                 for (int m = 0; m < D; ++m) q[m] = t[m];
