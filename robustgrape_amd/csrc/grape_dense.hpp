@@ -12,8 +12,7 @@
 //   C tile (16 x 16):     lane l, element r holds C[(l >> 4) + 4r][l & 15]
 //
 // (checked on the hardware with exact integer data, scripts/probes/mfma_probe.hip).
-// With GRAPE_DENSE_3M (default) the four real GEMMs become Gauss's three
-// (Lr Rr, Li Ri, (Lr + Li)(Rr + Ri)).
+// The four real GEMMs run as Gauss's three (Lr Rr, Li Ri, (Lr + Li)(Rr + Ri); see mm).
 // Element r of a C tile is therefore the B fragment of k-rows 4r..4r+3: a
 // matrix kept in registers in C-tile layout IS the right operand of the next
 // product, with no data movement.  Register matrices (HM) are distributed by
@@ -224,20 +223,6 @@ __device__ __forceinline__ void sm_load(SM S, HM &M, const Lane &ln_in) {
 // P += op(L) . op(R), both operands in LDS (LT/RT: transpose, LC/RC: conjugate).
 // Wave (w, h) computes tiles (2h, w), (2h+1, w): 16 k-steps x 8 MFMAs.
 // ---------------------------------------------------------------------------
-template <bool LC>
-__device__ __forceinline__ void cmfma2(HM &P, const double (&aR)[2], const double (&aI)[2], double bR, double bI) {
-    // (aR + i aI)(bR + i bI), with aI -> -aI for conj(L)
-    const double xR = LC ? bI : -bI;  // coefficient of aI in the real part
-    const double xI = LC ? -bR : bR;  // coefficient of aI in the imaginary part
-#pragma unroll
-    for (int i = 0; i < 2; ++i) P.re[i] = mfma(aR[i], bR, P.re[i]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) P.im[i] = mfma(aR[i], bI, P.im[i]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) P.re[i] = mfma(aI[i], xR, P.re[i]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) P.im[i] = mfma(aI[i], xI, P.im[i]);
-}
 
 struct Frag {
     double aR[2], aI[2], bR, bI;
@@ -266,16 +251,12 @@ __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &
 // Software-pipelined over the 16 k-steps: the fragments of step s+1 are loaded
 // while step s's 8 MFMAs issue; the "memory" pin stops the compiler from hoisting
 // every step's loads to the top (that costs ~100 VGPRs and forces spills).
-// Gauss's 3-multiplication complex product (default): 3 real MFMA streams per complex
-// product instead of 4; rounding-level differences only (the dense parity tests hold at T0).
-// Measured at C5: 940 -> 1 064 evals/s, k_dgrad 0.52 -> 0.58 of the FP64 peak credited with
-// the algorithmic 8 d^3 per complex product (executed: 6 d^3).  -DGRAPE_DENSE_3M=0: 4 products.
-#ifndef GRAPE_DENSE_3M
-#define GRAPE_DENSE_3M 1
-#endif
+// Gauss's 3-multiplication complex product: 3 real MFMA streams per complex product instead
+// of 4; rounding-level differences only (the dense parity tests hold at T0).  Measured at C5:
+// 940 -> 1 064 evals/s, k_dgrad 0.52 -> 0.58 of the FP64 peak credited with the algorithmic
+// 8 d^3 per complex product (executed: 6 d^3).
 template <bool LT, bool LC, bool RT, bool RC>
 __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
-#if GRAPE_DENSE_3M
     // Gauss's three-multiplication complex product: T1 = Lr Rr, T2 = Li Ri, T3 = (Lr + Li)(Rr + Ri),
     // P += (T1 - T2) + i (T3 - T1 - T2): 3 MFMAs per tile and k-step instead of 4.
     Frag fc, fn;
@@ -304,20 +285,6 @@ __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
     for (int i = 0; i < 2; ++i) {
         P.re[i] += t1[i] - t2[i];
         P.im[i] += t3[i] - t1[i] - t2[i];
-    }
-    return;
-#endif
-    Frag cur, nxt;
-    mm_load<LT, RT, RC>(L, R, 0, cur, ln);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        if (s < 15) mm_load<LT, RT, RC>(L, R, s + 1, nxt, ln);
-        cmfma2<LC>(P, cur.aR, cur.aI, cur.bR, cur.bI);
-        if (s < 15) {
-            cur = nxt;
-            asm volatile("" : "+v"(cur.aR[0]), "+v"(cur.aR[1]), "+v"(cur.aI[0]), "+v"(cur.aI[1]), "+v"(cur.bR),
-                         "+v"(cur.bI)::"memory");
-        }
     }
 }
 

@@ -447,9 +447,6 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         for (int m = 0; m < D; ++m) dst[m] = src[m * D];
     };
     load_e(k0, e);
-#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 0
-    return;
-#endif
     for (int j = 0; j < P.L; ++j) {
         const int k = k0 + j;
         const bool act = gvalid && k < P.Nt;
@@ -481,9 +478,6 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     }
     tile_store_row(G, q, gvalid);  // chunk total T_c, column-major
     gsync();
-#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 1
-    return;
-#endif
     // Phase B: inclusive scan of the chunk totals, P_c = T_c ... T_0 (Hillis-Steele):
     // column i of S_c . S_{c-o} = S_c . (column i of S_{c-o})
     for (int o = 1; o < P.nchunks; o <<= 1) {
@@ -498,9 +492,6 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         if (doit) tile_store_row(G, t, true);
         gsync();
     }
-#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 2
-    return;
-#endif
     // Phase C: fidelity and M = G U on group 0 (everyone keeps the barrier sequence)
     const bool f0 = (c == 0) && G.lane_ok;
     const cd *Ut = tile_of(P.nchunks - 1);  // U column-major
@@ -590,9 +581,6 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) du[jj] = Ut[jj * D + i];
     }
-#if defined(GRAPE_SCAN_STOP) && GRAPE_SCAN_STOP == 3
-    return;
-#endif
     // Phase D: M'_c = Carry_c M Carry_c^dag, Carry_c = P_{c-1} (identity for c = 0)
     if (gvalid && B.Carry) {  // carries for the error path (identity for chunk 0)
         cd *dc = B.Carry + ((size_t)b * P.nchunks + c) * TILE + i * D;
