@@ -221,7 +221,7 @@ __device__ __forceinline__ void sm_load(SM S, HM &M, const Lane &ln_in) {
 
 // ---------------------------------------------------------------------------
 // P += op(L) . op(R), both operands in LDS (LT/RT: transpose, LC/RC: conjugate).
-// Wave (w, h) computes tiles (2h, w), (2h+1, w): 16 k-steps x 8 MFMAs.
+// Wave (w, h) computes tiles (2h, w), (2h+1, w): 16 k-steps x 6 MFMAs (Gauss 3M).
 // ---------------------------------------------------------------------------
 
 struct Frag {
