@@ -505,6 +505,9 @@ def main():
     ap.add_argument("--no-host-paths", action="store_true",
                     help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--dist", action="store_true",
+                    help="run the multi-rank path (RCCL process group, the sweep's all_gather + "
+                         "broadcast, max-over-ranks timing) even with one rank")
     args = ap.parse_args()
 
     import torch
@@ -517,7 +520,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout (one JSON line)
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -564,7 +573,7 @@ def main():
         step()
     plan.synchronize()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     plan.kernel_times(reset=True)
@@ -573,14 +582,14 @@ def main():
     for _ in range(args.steps):
         step()
     best = None
-    if world > 1:  # the sweep's exchange: all_gather of (best F, id), winner broadcasts its x
+    if use_dist:  # the sweep's exchange: all_gather of (best F, id), winner broadcasts its x
         best = gather_best(F, ids, X)
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     plan.synchronize()  # resolves the per-kernel events, raises on a singular Pade denominator
     plan.set_profiling(False)
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -622,7 +631,7 @@ def main():
                              "device_value_vs_allcores": (value / out["cpu_baseline_allcores"]["value"]
                                                           if "cpu_baseline_allcores" in out else None)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
