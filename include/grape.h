@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 4
+#define GRAPE_ABI_VERSION 5
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -315,6 +315,19 @@ typedef enum grape_kernel {
 
 int grape_plan_set_profiling(grape_plan *plan, int enable);
 int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launches, int reset);
+
+/*
+ * Sectors (ABI 5).  When every operator that H0 uses is block-diagonal in one common
+ * permutation of the basis (a conserved quantity: for rydberg_hamiltonian_full the 9 levels
+ * split into blocks of 1, 2, 2 and 4), exp, chain and contractions never leave the blocks,
+ * so grape_fidelity_grad runs each evaluation as `nsectors` independent sector problems of
+ * size `sector_dim` (blocks packed first-fit into equal sectors, padded with decoupled
+ * levels) and assembles U only for the fidelity head.  Same outputs; no API change.  Chosen
+ * at plan creation for operator-basis plans without error sources when it cuts the work at
+ * least in half; the environment variable GRAPE_NO_SECTORS=1 turns it off.  Reports
+ * (ndim, 1) when the plan runs whole matrices.
+ */
+int grape_plan_sectors(grape_plan *plan, int *sector_dim, int *nsectors);
 
 /*
  * Batched matrix exponential exp(A) of n column-major ndim x ndim complex

@@ -24,10 +24,10 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_interaction_error_operators", "grape_interaction_error_operators_device",
             "grape_expectation_values", "grape_fidelity_grad_tables",
             "grape_lbfgs_direction", "grape_unitary_derivs_tables", "grape_interaction_error_operators_tables",
-            "grape_expectation_values_tables"]
+            "grape_expectation_values_tables", "grape_plan_sectors"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad/k_err_local", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
-ABI_VERSION = 4  # GRAPE_ABI_VERSION in include/grape.h
+ABI_VERSION = 5  # GRAPE_ABI_VERSION in include/grape.h
 
 
 class GrapeError(RuntimeError):
@@ -90,6 +90,8 @@ def lib():
         L.grape_plan_set_profiling.restype = ctypes.c_int
         L.grape_plan_kernel_times.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.grape_plan_kernel_times.restype = ctypes.c_int
+        L.grape_plan_sectors.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.grape_plan_sectors.restype = ctypes.c_int
         if L.grape_abi_version() != ABI_VERSION:
             raise ImportError("libgrape.so ABI version mismatch")
         _lib = L

@@ -68,6 +68,16 @@ hipError_t dispatch_pipeline(int D, const DevProblem &P, const DevBatch &B, hipS
     }
     return hipErrorInvalidValue;
 }
+hipError_t dispatch_sector_pipeline(int S, const DevProblem &P, const DevBatch &B, const grape_proj::SectorHead &H,
+                                   hipStream_t st, const KMark &mk) {
+    switch (S) {
+#define CASE(d) \
+    case d: return grape_host::launch_sector_pipeline<d>(P, B, H, st, mk);
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
 hipError_t dispatch_expm_raw(int D, const cd *A, cd *E, int n, int *ovf, int *ovfc, int *status,
                              int *mstats, hipStream_t st) {
     switch (D) {
@@ -134,6 +144,14 @@ struct grape_plan {
     cd *d_sink = nullptr;                      // DevBatch::sink
     // general projector (FidelityCalculations.jl:47-51): P0 P, P, P0 row-major; head scratch
     cd *d_PA = nullptr, *d_PB = nullptr, *d_P0g = nullptr, *d_gpscr = nullptr;
+    // sectors (grape.h grape_plan_sectors): the fidelity path runs nsec sector problems of
+    // size S per evaluation (Ps), then the sector head over the assembled U (SH)
+    bool sectors = false;
+    DevProblem Ps{};
+    grape_proj::SectorHead SH{};
+    int *d_sidx = nullptr;
+    cd *d_sops = nullptr, *d_sopsT = nullptr, *d_Msec = nullptr;
+    double *d_sec_part = nullptr;
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -185,7 +203,8 @@ static void free_plan(grape_plan *p) {
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
-                    p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr};
+                    p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
+                    p->d_sidx, p->d_sops, p->d_sopsT, p->d_sec_part, p->d_Msec};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
@@ -347,6 +366,92 @@ static int upload_projector(grape_plan *p, const ProjectorSetup &ps, DevProblem 
     P.PB = p->d_PB;
     P.P0g = p->d_P0g;
     return GRAPE_OK;
+}
+
+// Sectors: connected components of the union sparsity pattern of every operator H0 uses
+// (the levels an evolution can ever couple).  A single level with a zero diagonal in every
+// operator never evolves (its propagator is 1 and it carries no gradient): it is "fixed" and
+// only enters the head's U.  The others are packed first-fit-decreasing into nsec sectors of
+// S = max(2, largest component) slots; sidx[w * S + a] = level in slot a of sector w, or -1
+// (padding: a decoupled level, exp(0) = 1, never reaches F), followed by the fixed levels.
+// Only for operator-basis plans without error sources (the error path keeps whole matrices),
+// and only when the sector work nsec * S^3 is at most half of d^3.
+struct SectorSetup {
+    int S = 0, nsec = 1, nfixed = 0;
+    std::vector<int> sidx;
+};
+static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
+    SectorSetup ss;
+    const int D = desc->ndim;
+    if (tables || desc->nerr > 0 || D > GRAPE_MAX_SMALL_DIM) return ss;
+    if (const char *e = std::getenv("GRAPE_NO_SECTORS"))
+        if (std::atoi(e) != 0) return ss;
+    std::vector<int> parent(D);
+    for (int i = 0; i < D; ++i) parent[i] = i;
+    auto root = [&](int i) {
+        while (parent[i] != i) i = parent[i] = parent[parent[i]];
+        return i;
+    };
+    for (int t = 0; t < desc->n_h0_terms; ++t) {
+        const double *op = desc->ops + 2 * (size_t)desc->h0_terms[t].op * D * D;
+        for (int c = 0; c < D; ++c)
+            for (int r = 0; r < D; ++r) {
+                const double *v = op + 2 * ((size_t)r + (size_t)c * D);
+                if (v[0] != 0.0 || v[1] != 0.0) parent[root(r)] = root(c);
+            }
+    }
+    std::vector<char> diag(D, 0);  // level with a nonzero diagonal entry in some operator
+    for (int t = 0; t < desc->n_h0_terms; ++t) {
+        const double *op = desc->ops + 2 * (size_t)desc->h0_terms[t].op * D * D;
+        for (int i = 0; i < D; ++i) {
+            const double *v = op + 2 * ((size_t)i + (size_t)i * D);
+            if (v[0] != 0.0 || v[1] != 0.0) diag[i] = 1;
+        }
+    }
+    std::vector<std::vector<int>> comps;
+    std::vector<int> slot(D, -1), fixed;
+    for (int i = 0; i < D; ++i) {  // levels in ascending order inside each component
+        const int r = root(i);
+        if (slot[r] < 0) {
+            slot[r] = (int)comps.size();
+            comps.emplace_back();
+        }
+        comps[slot[r]].push_back(i);
+    }
+    const size_t ncomp = comps.size();
+    comps.erase(std::remove_if(comps.begin(), comps.end(),
+                               [&](const std::vector<int> &c) {
+                                   if (c.size() != 1 || diag[c[0]]) return false;
+                                   fixed.push_back(c[0]);
+                                   return true;
+                               }),
+                comps.end());
+    if (ncomp < 2 || comps.empty()) return ss;
+    std::stable_sort(comps.begin(), comps.end(),
+                     [](const std::vector<int> &a, const std::vector<int> &b) { return a.size() > b.size(); });
+    const int S = std::max(2, (int)comps[0].size());
+    std::vector<std::vector<int>> bins;
+    for (const auto &c : comps) {
+        bool placed = false;
+        for (auto &bn : bins)
+            if ((int)(bn.size() + c.size()) <= S) {
+                bn.insert(bn.end(), c.begin(), c.end());
+                placed = true;
+                break;
+            }
+        if (!placed) bins.push_back(c);
+    }
+    const int nsec = (int)bins.size();
+    if (2L * nsec * S * S * S > (long)D * D * D || nsec * S * S > grape_proj::kSectorLds) return ss;
+    if (nsec < 2 && fixed.empty()) return ss;
+    ss.S = S;
+    ss.nsec = nsec;
+    ss.nfixed = (int)fixed.size();
+    ss.sidx.assign((size_t)nsec * S, -1);
+    for (int w = 0; w < nsec; ++w)
+        for (size_t a = 0; a < bins[w].size(); ++a) ss.sidx[(size_t)w * S + a] = bins[w][a];
+    ss.sidx.insert(ss.sidx.end(), fixed.begin(), fixed.end());
+    return ss;
 }
 
 static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, const ProjectorSetup &ps,
@@ -639,6 +744,28 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     const int nc0 = std::min(NG, P.Nt);
     P.L = (P.Nt + nc0 - 1) / nc0;
     P.nchunks = (P.Nt + P.L - 1) / P.L;
+    P.sectors = 0;
+    P.nsec = 1;
+    P.sec_ops = 0;
+    const SectorSetup ss = find_sectors(desc, tables);
+    const bool sec = ss.S > 0;
+    int s_waves = kScanWide, s_L = 0, s_nchunks = 0;
+    if (sec) {
+        if (dispatch_lds_limits(ss.S) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
+        s_waves = (long)p->max_batch * ss.nsec >= 2L * ncu ? kScanNarrow : kScanWide;
+        if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {
+            const int wv = std::atoi(w);
+            if (wv == kScanNarrow || wv == kScanWide) s_waves = wv;
+        }
+        const int ncs = std::min(s_waves * (64 / ss.S), P.Nt);
+        s_L = (P.Nt + ncs - 1) / ncs;
+        s_nchunks = (P.Nt + s_L - 1) / s_L;
+    }
+    // workspace rows / tile / chunks of the fidelity path: whole matrices, or nsec sector
+    // problems per evaluation
+    const size_t WR = sec ? (size_t)p->max_batch * ss.nsec : (size_t)p->max_batch;
+    const size_t WT = sec ? (size_t)ss.S * ss.S : (size_t)D * D;
+    const size_t WC = sec ? (size_t)s_nchunks : (size_t)P.nchunks;
 
     // operator basis: column-major interleaved -> row-major cd tiles (row builds)
     // and column-major ones (the exp kernels build columns)
@@ -656,20 +783,25 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
               dalloc(&p->d_h0, std::max(desc->n_h0_terms, 0)) == hipSuccess &&
               dalloc(&p->d_tgt, std::max(desc->n_target_terms, 0)) == hipSuccess &&
               dalloc(&p->d_W, (size_t)D) == hipSuccess &&
-              dalloc(&p->d_E, MB * P.Nt * P.nv * T) == hipSuccess && dalloc(&p->d_Q, MB * P.Nt * T) == hipSuccess &&
-              dalloc(&p->d_Mc, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
+              dalloc(&p->d_E, WR * P.Nt * P.nv * WT) == hipSuccess && dalloc(&p->d_Q, WR * P.Nt * WT) == hipSuccess &&
+              dalloc(&p->d_Mc, WR * WC * WT) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_part, MB * P.Nt * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
-              dalloc(&p->d_ovf, MB * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess &&
+              dalloc(&p->d_ovf, WR * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess &&
               dalloc(&p->d_sink, T) == hipSuccess &&
               dalloc(&p->d_vs, vs.size()) == hipSuccess;
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);
     if (ok && P.ne == 0)
-        ok = dalloc(&p->d_ovf2, MB * P.Nt * nvg) == hipSuccess &&
-             dalloc(&p->d_ovf2_slots, MB * P.Nt * nvg * T) == hipSuccess;
-    if (ok && (P.ne > 0 || ps.general))  // carries and U: the error path and the general-projector heads
-        ok = dalloc(&p->d_Carry, MB * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, MB * T) == hipSuccess;
+        ok = dalloc(&p->d_ovf2, WR * P.Nt * nvg) == hipSuccess &&
+             dalloc(&p->d_ovf2_slots, WR * P.Nt * nvg * WT) == hipSuccess;
+    if (ok && (P.ne > 0 || ps.general || sec))  // carries and U: the error path and the heads
+        ok = dalloc(&p->d_Carry, WR * WC * WT) == hipSuccess && dalloc(&p->d_Ub, WR * WT) == hipSuccess;
+    if (ok && sec)
+        ok = dalloc(&p->d_sec_part, WR * P.Nt * nvg) == hipSuccess && dalloc(&p->d_sidx, ss.sidx.size()) == hipSuccess &&
+             dalloc(&p->d_Msec, WR * WT) == hipSuccess &&
+             dalloc(&p->d_sops, (size_t)ss.nsec * n_ops * WT) == hipSuccess &&
+             dalloc(&p->d_sopsT, (size_t)ss.nsec * n_ops * WT) == hipSuccess;
     if (ok && P.ne > 0)
         ok = dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
@@ -707,7 +839,62 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.err_off = p->d_err_off;
     P.vs = p->d_vs;
     P.W = p->d_W;
+    if (sec) {  // the sector problem and the head over the assembled U
+        const int S = ss.S;
+        std::vector<cd> sops((size_t)ss.nsec * n_ops * S * S), sopsT(sops.size());
+        for (int w = 0; w < ss.nsec; ++w)
+            for (int o = 0; o < n_ops; ++o)
+                for (int a = 0; a < S; ++a)
+                    for (int c = 0; c < S; ++c) {
+                        const int gi = ss.sidx[(size_t)w * S + a], gj = ss.sidx[(size_t)w * S + c];
+                        const cd v = (gi >= 0 && gj >= 0) ? ops[(size_t)o * T + (size_t)gi * D + gj] : cd{0.0, 0.0};
+                        const size_t base = ((size_t)w * n_ops + o) * S * S;
+                        sops[base + (size_t)a * S + c] = v;
+                        sopsT[base + (size_t)c * S + a] = v;
+                    }
+        std::vector<cd> A(T, cd{0.0, 0.0}), Bm(T, cd{0.0, 0.0});  // diagonal projector: A = diag(w), B = diag(w != 0)
+        for (int i = 0; i < D; ++i) {
+            A[(size_t)i * D + i] = cd{ps.W[i], 0.0};
+            Bm[(size_t)i * D + i] = cd{ps.W[i] != 0.0 ? 1.0 : 0.0, 0.0};
+        }
+        if (!ps.general && (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess))
+            return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
+        if (hipMemcpy(p->d_sops, sops.data(), sops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(p->d_sopsT, sopsT.data(), sopsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(p->d_sidx, ss.sidx.data(), ss.sidx.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+            (!ps.general && (hipMemcpy(p->d_PA, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                             hipMemcpy(p->d_PB, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess)))
+            return bail(fail(GRAPE_ERR_HIP, "upload failed (sectors)"));
+        p->sectors = true;
+        DevProblem &Ps = p->Ps;
+        Ps = P;
+        Ps.D = S;
+        Ps.sectors = 1;
+        Ps.nsec = ss.nsec;
+        Ps.sec_ops = (size_t)n_ops * S * S;
+        Ps.ops = p->d_sops;
+        Ps.opsT = p->d_sopsT;
+        Ps.scan_waves = s_waves;
+        Ps.L = s_L;
+        Ps.nchunks = s_nchunks;
+        Ps.gen_proj = 0;
+        grape_proj::SectorHead &H = p->SH;
+        H.P = P;
+        H.P.PA = p->d_PA;
+        H.P.PB = p->d_PB;
+        H.S = S;
+        H.nsec = ss.nsec;
+        H.nfixed = ss.nfixed;
+        H.sidx = p->d_sidx;
+    }
     *out = p;
+    return GRAPE_OK;
+}
+
+int grape_plan_sectors(grape_plan *p, int *sector_dim, int *nsectors) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    if (sector_dim) *sector_dim = p->sectors ? p->Ps.D : (p->dense ? p->DP.P.D : p->P.D);
+    if (nsectors) *nsectors = p->sectors ? p->Ps.nsec : 1;
     return GRAPE_OK;
 }
 
@@ -768,6 +955,41 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         DB.mstats = nullptr;
         DB.gp_scr = p->d_gpscr;
         HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, st, mk));
+        return GRAPE_OK;
+    }
+    if (p->sectors) {
+        const DevProblem &Ps = p->Ps;
+        DevBatch B{};
+        B.nb = nb * Ps.nsec;
+        B.x = d_x;
+        B.F = d_F;
+        B.Fdx = d_Fdx;
+        B.E = p->d_E;
+        B.Q = p->d_Q;
+        B.Mc = p->d_Mc;
+        B.part_add = p->d_part;
+        B.tgt_part = p->d_tgt_part;
+        B.overflow = p->d_ovf;
+        B.Carry = p->d_Carry;
+        B.Ub = p->d_Ub;
+        B.ovf2 = p->d_ovf2;
+        B.ovf2_slots = p->d_ovf2_slots;
+        B.sec_part = p->d_sec_part;
+        B.Msec = p->d_Msec;
+        int *cnt = p->d_ctrl + 4;
+        B.overflow_count = cnt;
+        B.ovf2_count = cnt + 1;
+        B.status = p->d_ctrl + 2;
+        B.sink = p->d_sink;
+        grape_proj::SectorHead H = p->SH;
+        H.x = d_x;
+        H.Ub = p->d_Ub;
+        H.Msec = p->d_Msec;
+        H.F = d_F;
+        H.Fdx = d_Fdx;
+        H.tgt_part = p->d_tgt_part;
+        HIPCHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+        HIPCHECK(dispatch_sector_pipeline(Ps.D, Ps, B, H, st, mk));
         return GRAPE_OK;
     }
     const DevProblem &P = p->P;

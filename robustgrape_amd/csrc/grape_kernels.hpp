@@ -78,6 +78,15 @@ struct DevProblem {
     const cd *PA;        // P0 P  (row-major), P = P0 with nonzeros set to 1
     const cd *PB;        // P     (row-major)
     const cd *P0g;       // P0    (row-major; expectation values)
+    // Sectors (grape_engine.hip find_sectors): when every operator H0 uses is block-diagonal in
+    // a common permutation, one evaluation is run as nsec independent D x D sector problems
+    // (sub-evaluation b' = b * nsec + w reads x of b and the operators of sector w at
+    // ops / opsT + w * sec_ops); k_scan stops after the chunk carries, the sector head
+    // (grape_projector.hip) forms F and the blocks of M from the assembled U, and k_sec_mc the
+    // per-chunk images M'_c.  sectors = 0: whole matrices (nsec = 1).
+    int sectors;         // 1: this is the sector problem (k_scan stops after the carries)
+    int nsec;
+    size_t sec_ops;
 };
 
 struct DevBatch {
@@ -109,6 +118,8 @@ struct DevBatch {
     const cd *Htab;         // [nb][Nt][nv][D][D] column-major H at every closure call site (else null)
     const cd *U0tab;        // [nb][1 + na][D][D] column-major target at x_add, x_add + eps e_q (else null)
     cd *gp_scr;             // general projector: head scratch (grape_projector_api.hpp)
+    double *sec_part;       // sectors: [nb][Nt][nvg] per-sector F_dx terms (k_sec_reduce sums them), else null
+    const cd *Msec;         // sectors: [nb][D][D] the sector blocks of M = G U (the sector head)
 };
 
 __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,
@@ -184,6 +195,7 @@ constexpr int kCachedTerms = 6;
 template <int D, bool ERR>
 struct ItemBuilder {
     const DevProblem *P;
+    const cd *opsT;  // this item's sector of the column-major basis
     const double *xk, *xadd;
     int i, nt1;
     VSpec vs;
@@ -195,8 +207,9 @@ struct ItemBuilder {
     __device__ __forceinline__ cd gen(cd c) const { return cmake(P->dt * c.im, -(P->dt * c.re)); }
 
     __device__ __forceinline__ ItemBuilder(const DevProblem *P_, const double *xk_, const double *xadd_, int i_,
-                                           int nt1_, const VSpec &vs_, bool valid_)
-        : P(P_), xk(xk_), xadd(xadd_), i(i_), nt1(nt1_), vs(vs_), valid(valid_), o0(0), ne_t(0) {
+                                           int nt1_, const VSpec &vs_, bool valid_, int sector = 0)
+        : P(P_), opsT(P_->opsT + (size_t)sector * P_->sec_ops), xk(xk_), xadd(xadd_), i(i_), nt1(nt1_), vs(vs_),
+          valid(valid_), o0(0), ne_t(0) {
 #pragma unroll
         for (int t = 0; t < kCachedTerms; ++t)
             c0[t] = (t < P->n_h0) ? gen(term_coef(P->h0[t], nt1, xk, xadd, vs.pert)) : czero();
@@ -215,14 +228,14 @@ struct ItemBuilder {
 #pragma unroll
         for (int t = 0; t < kCachedTerms; ++t) {
             if (t < n) {
-                const cd *op = P->opsT + (size_t)terms[t].op * D * D + i * D;
+                const cd *op = opsT + (size_t)terms[t].op * D * D + i * D;
 #pragma unroll
                 for (int j = 0; j < D; ++j) cmac(h[j], cache[t], op[j]);
             }
         }
         for (int t = kCachedTerms; t < n; ++t) {  // rare: more terms than cached
             const cd c = gen(cscale(sc, term_coef(terms[t], nt1, xk, xadd, vs.pert)));
-            const cd *op = P->opsT + (size_t)terms[t].op * D * D + i * D;
+            const cd *op = opsT + (size_t)terms[t].op * D * D + i * D;
 #pragma unroll
             for (int j = 0; j < D; ++j) cmac(h[j], c, op[j]);
         }
@@ -269,9 +282,10 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
     const int v = (int)(gidc % P.nv);
     const int k = (int)((gidc / P.nv) % P.Nt);
     const int b = (int)(gidc / ((long)P.nv * P.Nt));
-    const double *xb = B.x + (size_t)b * P.nx;
+    const int ns = P.nsec > 1 ? P.nsec : 1, bx = b / ns;  // sectors: evaluation bx, sector b - bx * ns
+    const double *xb = B.x + (size_t)bx * P.nx;
     const ItemBuilder<D, ERR> rebuild(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1, P.vs[v],
-                                      valid);
+                                      valid, b - bx * ns);
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
@@ -492,6 +506,21 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         if (doit) tile_store_row(G, t, true);
         gsync();
     }
+    if (P.sectors) {  // sectors: U and the carries only; the sector head and k_sec_mc do F, M, M'_c
+        if (c == P.nchunks - 1 && G.lane_ok) {
+            const cd *Ut = tile_of(c);
+            cd *du = B.Ub + (size_t)b * TILE + i * D;
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) du[jj] = Ut[jj * D + i];
+        }
+        if (gvalid) {
+            cd *dc = B.Carry + ((size_t)b * P.nchunks + c) * TILE + i * D;
+            const cd *Cr = c > 0 ? tile_of(c - 1) : nullptr;
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) dc[jj] = Cr ? Cr[jj * D + i] : cmake(jj == i ? 1.0 : 0.0, 0.0);
+        }
+        return;
+    }
     // Phase C: fidelity and M = G U on group 0 (everyone keeps the barrier sequence)
     const bool f0 = (c == 0) && G.lane_ok;
     const cd *Ut = tile_of(P.nchunks - 1);  // U column-major
@@ -697,7 +726,8 @@ __device__ __forceinline__ void grad_store(Group<D> &G, const DevProblem &P, con
     }
     s = group_sum(G, s, valid);
     if (valid && G.i == 0) {
-        if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+        if (B.sec_part) B.sec_part[((size_t)b * P.Nt + k) * P.nvg + u] = s;  // sector term, summed by k_sec_reduce
+        else if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
         else B.part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
     }
 }
@@ -749,9 +779,10 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_GRAD_WAVES : 2)) void k_ex
     const int u = (int)(gidc % nvg);
     const int k = (int)((gidc / nvg) % P.Nt);
     const int b = (int)(gidc / ((long)nvg * P.Nt));
-    const double *xb = B.x + (size_t)b * P.nx;
+    const int ns = P.nsec > 1 ? P.nsec : 1, bx = b / ns;
+    const double *xb = B.x + (size_t)bx * P.nx;
     const ItemBuilder<D, false> rebuild(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1,
-                                        P.vs[P.off_dx + u], valid);
+                                        P.vs[P.off_dx + u], valid, b - bx * ns);
     cd a[D], x[D];
     rebuild(a);
     int singular = 0, s = 0;
@@ -820,6 +851,51 @@ __global__ void k_reduce_add(DevProblem P, DevBatch B) {
     double s = 0.0;
     for (int k = 0; k < P.Nt; ++k) s += src[(size_t)k * P.na];
     B.Fd2dx[(size_t)be * P.nx + (size_t)P.np * P.Nt + q] += s;
+}
+
+// Sectors: M'_{c,w} = Carry_{c,w} M_ww Carry_{c,w}^dagger, one thread per element (i, j) of one
+// (sub-evaluation, chunk): sum_a C[i][a] sum_e M_ww[a][e] conj(C[j][e]); consecutive threads
+// store consecutive elements.
+template <int D>
+__global__ void k_sec_mc(DevProblem P, DevBatch B) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)B.nb * P.nchunks * D * D) return;
+    const int j = (int)(t % D), i = (int)((t / D) % D);
+    const long bc = t / (D * D);  // b' * nchunks + c
+    const int b = (int)(bc / P.nchunks);
+    const cd *C = B.Carry + (size_t)bc * D * D;
+    const cd *Mw = B.Msec + (size_t)b * D * D;
+    cd ci[D], cj[D];
+#pragma unroll
+    for (int e = 0; e < D; ++e) {
+        ci[e] = C[i * D + e];
+        cj[e] = cconj(C[j * D + e]);
+    }
+    cd acc = czero();
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        cd r = czero();  // (M_ww Carry^dagger)[a][j]
+#pragma unroll
+        for (int e = 0; e < D; ++e) r = cadd(r, cmul(Mw[a * D + e], cj[e]));
+        acc = cadd(acc, cmul(ci[a], r));
+    }
+    B.Mc[(size_t)t] = acc;
+}
+
+// Sectors: F_dx[b][k, u] (or the per-step x_add term) = sum over the evaluation's sectors, in
+// sector order (deterministic).  One thread per (b, k, u).
+template <int D>
+__global__ void k_sec_reduce(DevProblem P, DevBatch B, int nb) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per = (long)P.Nt * P.nvg;
+    if (t >= (long)nb * per) return;
+    const int b = (int)(t / per);
+    const long r = t - (long)b * per;  // k * nvg + u
+    const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
+    double s = 0.0;
+    for (int w = 0; w < P.nsec; ++w) s += B.sec_part[((size_t)b * P.nsec + w) * per + r];
+    if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+    else B.part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
 }
 
 }  // namespace grape

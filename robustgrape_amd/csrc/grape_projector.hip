@@ -63,11 +63,12 @@ __device__ void bmm(cd *C, const cd *A, const cd *B, int D) {
     __syncthreads();
 }
 
-// workgroup sums (every thread receives the result)
+// workgroup sums (every thread receives the result); NT = threads of the workgroup
+template <int NT = BLOCK>
 __device__ double bsum(double v, double *red) {
     red[threadIdx.x] = v;
     __syncthreads();
-    for (int s = BLOCK / 2; s > 0; s >>= 1) {
+    for (int s = NT / 2; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
     }
@@ -76,19 +77,21 @@ __device__ double bsum(double v, double *red) {
     return r;
 }
 // tr(X) (complex)
+template <int NT = BLOCK>
 __device__ cd btrace(const cd *X, int D, double *red) {
     double re = 0.0, im = 0.0;
     for (int i = threadIdx.x; i < D; i += blockDim.x) {
         re += X[(size_t)i * D + i].re;
         im += X[(size_t)i * D + i].im;
     }
-    return cd{bsum(re, red), bsum(im, red)};
+    return cd{bsum<NT>(re, red), bsum<NT>(im, red)};
 }
 // Re tr(X Y^dagger) = Re sum_ij X_ij conj(Y_ij)
+template <int NT = BLOCK>
 __device__ double bdot(const cd *X, const cd *Y, int D, double *red) {
     double s = 0.0;
     for (int t = threadIdx.x; t < D * D; t += blockDim.x) s += X[t].re * Y[t].re + X[t].im * Y[t].im;
-    return bsum(s, red);
+    return bsum<NT>(s, red);
 }
 // Re tr(X Y) = Re sum_ij X_ij Y_ji
 __device__ double btrprod(const cd *X, const cd *Y, int D, double *red) {
@@ -297,7 +300,82 @@ __global__ __launch_bounds__(BLOCK) void k_proj_err(Heads H) {
     }
 }
 
+// Sector head, evaluation b = blockIdx.x (grape_projector_api.hpp SectorHead).  d <= 12: one
+// wave per evaluation, every d x d intermediate in LDS (9 slots).
+constexpr int SEC_BLOCK = 64;
+enum { H_U, H_U0, H_K, H_X, H_Y, H_T1, H_T2, H_T3, H_M, kHeadSlots };
+__global__ __launch_bounds__(SEC_BLOCK) void k_sec_head(SectorHead H) {
+    __shared__ double red[SEC_BLOCK];
+    extern __shared__ __attribute__((aligned(16))) unsigned char sec_smem[];
+    const grape::DevProblem &P = H.P;
+    const int D = P.D, b = blockIdx.x, S = H.S, SS = H.S * H.S, ns = H.nsec;
+    const size_t T = (size_t)D * D;
+    cd *s = reinterpret_cast<cd *>(sec_smem);
+    cd *U = s + H_U * T, *U0 = s + H_U0 * T, *K = s + H_K * T, *X = s + H_X * T, *Y = s + H_Y * T;
+    cd *T1 = s + H_T1 * T, *T2 = s + H_T2 * T, *T3 = s + H_T3 * T, *M = s + H_M * T;
+    const cd *A = P.PA, *Bm = P.PB;
+    const double *xb = H.x + (size_t)b * P.nx;
+    // U = direct sum of the sector propagators and of the identity on the levels no operator
+    // touches (exact zeros across sectors, as in the dense product)
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) U[t] = cd{0.0, 0.0};
+    __syncthreads();
+    for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
+        const int w = t / SS, r = (t % SS) / S, c = t % S;
+        const int gi = H.sidx[w * S + r], gj = H.sidx[w * S + c];
+        if (gi >= 0 && gj >= 0) U[(size_t)gi * D + gj] = H.Ub[((size_t)b * ns + w) * SS + r * S + c];
+    }
+    for (int t = threadIdx.x; t < H.nfixed; t += blockDim.x) {
+        const int g = H.sidx[ns * S + t];
+        U[(size_t)g * D + g] = cd{1.0, 0.0};
+    }
+    __syncthreads();
+    build_target(P, nullptr, b, xb, 0, U0);
+    bmm<true, false>(K, U0, U, D);   // K = U0^dag U
+    bmm<false, false>(X, A, K, D);   // A K
+    const cd tau = btrace<SEC_BLOCK>(X, D, red);
+    bmm<false, false>(Y, X, Bm, D);  // A K B
+    const double Fv = (bdot<SEC_BLOCK>(Y, K, D, red) + tau.re * tau.re + tau.im * tau.im) / P.DD;
+    bmm<true, false>(T1, K, X, D);
+    bmm<false, false>(M, Bm, T1, D);
+    bmm<true, false>(T1, X, K, D);
+    bmm<true, false>(T2, Bm, T1, D);
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) {
+        const cd ct = p_mul(cd{tau.re, -tau.im}, X[t]);
+        M[t] = p_scale(1.0 / P.DD, p_add(p_add(M[t], T2[t]), p_scale(2.0, ct)));
+    }
+    __syncthreads();
+    for (int q = 0; q < P.na; ++q) {  // target part of F_dx_add
+        build_target(P, nullptr, b, xb, 1 + q, T1);
+        for (int t = threadIdx.x; t < (int)T; t += blockDim.x) T1[t] = p_scale(P.inv_eps, p_sub(T1[t], U0[t]));
+        __syncthreads();
+        bmm<true, false>(T2, T1, U, D);   // Kd
+        bmm<false, false>(T1, A, T2, D);  // A Kd
+        const cd trd = btrace<SEC_BLOCK>(T1, D, red);
+        bmm<false, false>(T3, T1, Bm, D);  // A Kd B
+        const double sa = bdot<SEC_BLOCK>(T3, K, D, red), sb = bdot<SEC_BLOCK>(Y, T2, D, red);
+        const double val = (sa + sb + 2.0 * (tau.re * trd.re + tau.im * trd.im)) / P.DD;
+        if (threadIdx.x == 0) {
+            if (P.xadd_dep && H.tgt_part) H.tgt_part[(size_t)b * P.na + q] = val;
+            else H.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = val;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) H.F[b] = Fv;
+    // the sector blocks M_ww: the only part of M the block-diagonal contractions see
+    for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
+        const int w = t / SS, r = (t % SS) / S, c = t % S;
+        const int gi = H.sidx[w * S + r], gj = H.sidx[w * S + c];
+        H.Msec[(size_t)b * ns * SS + t] = (gi >= 0 && gj >= 0) ? M[(size_t)gi * D + gj] : cd{0.0, 0.0};
+    }
+}
+
 }  // namespace
+
+hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st) {
+    const size_t lds = (size_t)kHeadSlots * H.P.D * H.P.D * sizeof(cd);
+    hipLaunchKernelGGL(k_sec_head, dim3((unsigned)nb), dim3(SEC_BLOCK), lds, st, H);
+    return hipGetLastError();
+}
 
 hipError_t launch_fid_head(const Heads &H, int nb, hipStream_t st) {
     hipLaunchKernelGGL(k_proj_fid, dim3((unsigned)nb), dim3(BLOCK), 0, st, H);

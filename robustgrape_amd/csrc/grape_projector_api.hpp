@@ -34,6 +34,24 @@ hipError_t launch_fid_head(const Heads &H, int nb, hipStream_t st);
 // F_d2err_dx_add target part
 hipError_t launch_err_head(const Heads &H, int nb, hipStream_t st);
 
+// Sectors (DevProblem::sectors): the fidelity head of a block-diagonal problem.  The sector
+// pipeline leaves U_w of every sector (S x S, row-major); this head assembles U (d x d; the
+// identity on levels no operator touches), forms F, M = G U and the target part of F_dx_add
+// exactly as k_proj_fid does (with A = P0 P, B = P, any projector), and stores the sector
+// blocks M_ww; k_sec_mc then forms the per-chunk images M'_{c,w} = Carry M_ww Carry^dagger
+// that the sector k_expm_grad contracts.
+struct SectorHead {
+    grape::DevProblem P;    // the FULL d-dimensional problem (target terms, operators, PA / PB), d <= 12
+    int S, nsec, nfixed;    // sector size, sectors per evaluation, untouched (identity) levels
+    const int *sidx;        // [nsec][S]: level of each sector slot (-1: padding), then the nfixed levels
+    const double *x;        // [nb][nx]
+    const grape::cd *Ub;    // [nb * nsec][S][S]
+    grape::cd *Msec;        // [nb * nsec][S][S]  (written)
+    double *F, *Fdx, *tgt_part;
+};
+constexpr int kSectorLds = 2048;  // complex elements of LDS for the sector blocks M_ww (nsec * S * S)
+hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st);
+
 // the small engine's view (grape_launch.hpp)
 inline Heads small_heads(const grape::DevProblem &P, const grape::DevBatch &B) {
     Heads H{};

@@ -169,6 +169,13 @@ class GrapePlan:
     def synchronize(self):
         _capi.check(_capi.lib().grape_plan_synchronize(self.handle))
 
+    def sectors(self) -> tuple[int, int]:
+        """(sector size, sectors per evaluation) of the fidelity path; (ndim, 1) = whole matrices
+        (include/grape.h grape_plan_sectors)."""
+        S, n = ctypes.c_int(0), ctypes.c_int(0)
+        _capi.check(_capi.lib().grape_plan_sectors(self.handle, ctypes.byref(S), ctypes.byref(n)))
+        return S.value, n.value
+
 
 # Plan cache of the reference-shaped entry points (one plan per problem object, nparam and
 # device).  A plan owns HBM workspace for `max_batch` evaluations; larger batches are

@@ -1,0 +1,141 @@
+"""Sectors (include/grape.h grape_plan_sectors): problems whose H0 operators are block-diagonal
+in a common permutation run each evaluation as independent sector problems.  The Rydberg
+Hamiltonians of the reference all have this structure (the laser couples |1> <-> |r> only):
+rydberg_hamiltonian_full (d = 9) splits into blocks of 4, 2, 2 and the untouched |00> -> 2
+sectors of 4 levels, the symmetric blockaded one (d = 5) into 2, 2 (+ |00>) -> 2 sectors of 2,
+the full blockaded one (d = 7) into 2, 2, 2 (+ |00>) -> 3 sectors of 2.
+
+The sector path must give the whole-matrix path's numbers (GRAPE_NO_SECTORS=1) and the
+oracle's, for diagonal and general projectors (which mix sectors in the fidelity head),
+x_add-dependent H0, parked high-norm steps, and the graph-replayed single evaluations."""
+import numpy as np
+import pytest
+
+from tests import problems as P
+
+pytestmark = pytest.mark.gpu
+T1 = 1e-12
+T2S, T2S_ABS = 1e-7, 1e-9     # short-step eps-FD tier (test_gpu_parity.py)
+T2, T2_ABS = 1e-6, 1e-7
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _plan(fp, max_batch, monkeypatch, whole=False, nparam=1):
+    from robustgrape_amd.engine import GrapePlan
+    if whole:
+        monkeypatch.setenv("GRAPE_NO_SECTORS", "1")
+    try:
+        return GrapePlan(fp, nparam=nparam, device=0, max_batch=max_batch)
+    finally:
+        monkeypatch.delenv("GRAPE_NO_SECTORS", raising=False)
+
+
+def _both(fp, X, monkeypatch):
+    ps, pw = _plan(fp, len(X), monkeypatch), _plan(fp, len(X), monkeypatch, whole=True)
+    try:
+        return ps.sectors(), pw.sectors(), ps.fidelity_grad(X), pw.fidelity_grad(X)
+    finally:
+        ps.close()
+        pw.close()
+
+
+def _close(a, b, tight=True):
+    t2, t2a = (T2S, T2S_ABS) if tight else (T2, T2_ABS)
+    assert np.max(np.abs(a[0] - b[0])) <= T1, np.max(np.abs(a[0] - b[0]))
+    err, scale = np.max(np.abs(a[1] - b[1])), np.max(np.abs(b[1]))
+    print(f"F {np.max(np.abs(a[0] - b[0])):.2e}  F_dx {err:.2e} (scale {scale:.2e})")
+    assert err <= t2 * scale + t2a, (err, scale)
+
+
+@pytest.mark.parametrize("name,fp,layout", [
+    ("full9", lambda: P.full9_problem(40), (4, 2)),
+    ("sym5", lambda: P.sym_problem(24), (2, 2)),
+    ("fullblk7", lambda: P.fullblk_problem(24), (2, 3)),
+])
+def test_sectors_match_whole_matrices_and_oracle(name, fp, layout, monkeypatch):
+    from oracle import grape_oracle as O
+    f = fp()
+    nt, d = f.unitary_problem.ntimes, f.unitary_problem.ndim
+    X = np.stack([P.random_x(nt, 40 + s) for s in range(6)])
+    sec, whole, out, ref = _both(f, X, monkeypatch)
+    assert sec == layout and whole == (d, 1)
+    _close(out, ref)
+    for b in (0, 5):
+        F0, g0 = O.calculate_fidelity_and_derivatives(f, X[b])[:2]
+        _close((out[0][b], out[1][b]), (F0, g0))
+
+
+def test_no_sectors_with_error_sources(monkeypatch):
+    pl = _plan(P.full9_problem(16, nerr=2), 2, monkeypatch)
+    try:
+        assert pl.sectors() == (9, 1)
+    finally:
+        pl.close()
+
+
+@pytest.mark.parametrize("d", [5, 9])
+def test_sectors_with_xadd_dependent_h0(d, monkeypatch):
+    """H0 reading x_add (a diagonal term: the sectors survive): the per-step x_add terms are
+    summed over sectors, then over steps, on top of the head's target part."""
+    from oracle import grape_oracle as O
+    nt = 16
+    fp = P.xadd_err_problem(d, nt, nerr=0)
+    X = np.stack([P.xadd_x(nt, 70 + s) for s in range(4)])
+    sec, _, out, ref = _both(fp, X, monkeypatch)
+    assert sec[1] > 1
+    _close(out, ref, tight=False)  # dt = t0 / 16 with x_main = 2 pi U: long steps, the T2 tier
+    fo = P.xadd_err_problem(d, nt, nerr=0, device=False)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[2])[:2]
+    _close((out[0][2], out[1][2]), (F0, g0), tight=False)
+
+
+def test_general_projector_mixing_sectors(monkeypatch):
+    """A projector coupling levels of different sectors: only the head sees it (the sector
+    blocks of M feed the contractions)."""
+    from oracle import grape_oracle as O
+    nt = 20
+    rng = np.random.default_rng(9)
+    Qm, _ = np.linalg.qr(rng.standard_normal((9, 3)))
+    P0 = Qm @ Qm.T
+    fp = P.full9_problem(nt).replace(projector=P0)
+    X = np.stack([P.random_x(nt, 90 + s) for s in range(3)])
+    sec, _, out, ref = _both(fp, X, monkeypatch)
+    assert sec == (4, 2)
+    _close(out, ref)
+    fo = P.full9_problem(nt, device=False).replace(projector=P0)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[1])[:2]
+    _close((out[0][1], out[1][1]), (F0, g0), tight=False)
+
+
+def test_sectors_parked_high_norm_steps(monkeypatch):
+    """Long steps (|A|_1 large): the sector exponentials take Pade 7/9/13 with squarings in
+    k_expm_high / k_grad_high."""
+    from oracle import grape_oracle as O
+    nt = 6
+    fp = P.full9_problem(nt, t0=40.0)
+    X = np.stack([P.random_x(nt, 120 + s) for s in range(3)])
+    _, _, out, ref = _both(fp, X, monkeypatch)
+    _close(out, ref, tight=False)
+    fo = P.full9_problem(nt, t0=40.0, device=False)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[0])[:2]
+    _close((out[0][0], out[1][0]), (F0, g0), tight=False)
+
+
+def test_sector_single_calls_are_the_batch(monkeypatch):
+    """Graph-replayed single evaluations (<= 64 per call) and the stream path agree bitwise."""
+    fp = P.full9_problem(32)
+    X = np.stack([P.random_x(32, 200 + s) for s in range(70)])
+    pl = _plan(fp, 128, monkeypatch)
+    try:
+        ref = pl.fidelity_grad(X)
+        for b in (0, 33, 69):
+            one = pl.fidelity_grad(X[b:b + 1])
+            assert one[0][0] == ref[0][b] and np.array_equal(one[1][0], ref[1][b])
+    finally:
+        pl.close()
