@@ -95,10 +95,10 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
         return None
     if js.get("batch") != batch:
         return None
-    for name, row in js.get("kernels", {}).items():
-        if name.split("<")[0].split("::")[-1] == kernel and "hbm_bytes_per_launch" in row:
-            return row["hbm_bytes_per_launch"]
-    return None
+    # every instantiation of the kernel (the sector classes launch one each per device pass)
+    rows = [row["hbm_bytes_per_launch"] for name, row in js.get("kernels", {}).items()
+            if name.split("<")[0].split("::")[-1] == kernel and "hbm_bytes_per_launch" in row]
+    return sum(rows) if rows else None
 
 
 def _host_cpu():
@@ -236,15 +236,47 @@ def _kernel_fracs(flop_model, ktimes):
     return out
 
 
-def c2_report(args, B, L, world, value, elapsed, ktimes):
-    # algorithmic flops per launch of the two exp-carrying kernels:
-    # k_expm exps the nominal step propagators (B*NT items); k_expm_grad exps each
-    # eps-variant (np=1 control; H0 does not read x_add, so no x_add variants) and
-    # contracts it: Z_k = conj(Q_k) M'^T Q_{k-1}^T (2 complex products) + Re<Z, dE>.
+def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=None):
+    """C2 bench line.  `sectors`: GrapePlan.sectors() -- ((S, nsec), ...) per sector class, or
+    ((D, 1),) for whole matrices; `passes`: device passes in the timed region (per-pass kernel
+    times = total / passes: the sector classes launch each kernel once per class)."""
+    # algorithmic flops per device pass of the two exp-carrying kernels (DESIGN.md 4):
+    # k_expm exps the nominal step propagators; k_expm_grad exps each eps-variant (np=1
+    # control; H0 does not read x_add, so no x_add variants) and contracts it:
+    # Z_k = conj(Q_k) M'^T Q_{k-1}^T (2 complex products) + Re<Z, dE>.  With sectors every
+    # item is one S x S sector of one step (DESIGN.md 4.1).
     nvg = 1
-    flop_model = {"k_expm": L * NT * flops_expm(D),
-                  "k_expm_grad": L * NT * nvg * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)}
-    kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
+    classes = tuple(sectors) if sectors else ((D, 1),)
+    sec = classes[0][0] < D
+    per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
+    flop_model = {"k_expm": L * NT * per_step(flops_expm),
+                  "k_expm_grad": L * NT * nvg * per_step(lambda S: flops_expm(S) + 2 * 8 * S ** 3 + 8 * S ** 2)}
+    # algorithmic HBM bytes per pass: k_expm writes E; k_scan reads E, writes Q; k_expm_grad
+    # reads E_k and Q_k (Q_{k-1} is the previous step's Q_k) -- 16 S^2 bytes per tile
+    byte_model = {"k_expm": L * NT * per_step(lambda S: 16 * S * S),
+                  "k_scan": L * NT * per_step(lambda S: 2 * 16 * S * S),
+                  "k_expm_grad": L * NT * nvg * per_step(lambda S: 2 * 16 * S * S)}
+    npass = passes or max(1, ktimes.get("k_expm_grad", (0.0, 1))[1])
+    per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
+    kname = max(flop_model, key=lambda k: per_pass.get(k, 0.0))
+    ms = per_pass[kname]
+    fp = flop_model[kname] / (ms * 1e-3) / 1e12
+    hb = byte_model[kname] / (ms * 1e-3) / 1e9
+    traffic = pmc_traffic(kname, L)
+    fp_frac, hb_frac = fp / FP64_PEAK_TFLOPS, hb / HBM_PEAK_GBS
+    if hb_frac > fp_frac:
+        roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hb_frac, "traffic": traffic}
+    else:
+        roof = {"bound": "mfma", "kernel": kname, "achieved": fp, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": fp_frac, "traffic": traffic,
+                "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"}
+    roof.update({"traffic_unit": "HBM bytes per device pass (PMC)", "per_launch_ms": ms,
+                 "per_launch_note": "per device pass of evals_per_device_pass evaluations (all sector classes)",
+                 "flop_per_launch": flop_model[kname], "algorithmic_bytes_per_launch": byte_model[kname],
+                 "fp64": {"achieved_TFLOPs": fp, "frac": fp_frac},
+                 "hbm": {"achieved_GBs": hb, "frac": hb_frac,
+                         "traffic_GBs": (traffic / (ms * 1e-3) / 1e9) if traffic else None}})
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+∇), Rydberg CZ d=9 N_t=512, 1→8 GPU",
         "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
@@ -252,36 +284,84 @@ def c2_report(args, B, L, world, value, elapsed, ktimes):
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
                                "np=1, na=1, ne=0; restart sweep",
-                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
-        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, L),
-                         pipe="fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"),
+                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
+                   "sectors": [{"levels": S, "sectors": ns} for S, ns in classes] if sec else None},
+        "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
     # whole-evaluation view: FLOP of the work executed per evaluation
-    # (nominal + one eps-variant exp per step, chain + contraction products), and the
-    # survey's canonical C2 figure, which also counts the x_add-variant exps this engine
-    # skips because H0 does not read x_add (their differences are exactly zero)
-    exe = NT * ((1 + nvg) * flops_expm(D) + 3 * 8 * D ** 3 + nvg * 8 * D ** 2)
+    # (nominal + one eps-variant exp per step per sector, chain + contraction products; with
+    # sectors also the head's d x d products), and the survey's canonical whole-matrix C2 figure
+    # (which also counts the x_add-variant exps, zero differences, this engine skips)
+    exe = NT * per_step(lambda S: (1 + nvg) * flops_expm(S) + 3 * 8 * S ** 3 + nvg * 8 * S ** 2)
+    if sec:
+        exe += 16 * 8 * D ** 3
     canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
     out["roofline"]["whole_eval"] = {
         "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
         "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
-        "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
-        "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
-    out["kernels_frac"] = _kernel_fracs(flop_model, ktimes)
-    # the scan is the HBM-heavy stage: E in, Q out (algorithmic 2 * 16 d^2 bytes per step)
-    # against the 8 TB/s HBM3E peak, with the PMC bytes where the summary matches this batch
-    ms_s, n_s = ktimes.get("k_scan", (0.0, 0))
-    if n_s:
-        per_ms = ms_s / n_s
-        alg = L * NT * 2 * 16 * D * D
+        "flop_per_eval_survey": canon}
+    if sec:
+        out["roofline"]["whole_eval"]["note"] = (
+            "sectors: the executed work is the block-diagonal work; SURVEY 8d's whole-matrix "
+            "figure (flop_per_eval_survey) is not executed and is not credited")
+    else:
+        out["roofline"]["whole_eval"].update({"achieved_survey": canon * value / 1e12,
+                                              "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS})
+    out["kernels_frac"] = {k: f / (per_pass[k] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS
+                           for k, f in flop_model.items() if per_pass.get(k)}
+    out["kernels_hbm_frac"] = {k: f / (per_pass[k] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                               for k, f in byte_model.items() if per_pass.get(k)}
+    # the scan is the HBM-heavy stage: E in, Q out (algorithmic 2 * 16 S^2 bytes per step and
+    # sector) against the 8 TB/s HBM3E peak, with the PMC bytes where the summary matches
+    if per_pass.get("k_scan"):
+        per_ms = per_pass["k_scan"]
+        alg = byte_model["k_scan"]
         pmc = pmc_traffic("k_scan", L)
         out["roofline_scan"] = {"bound": "hbm", "kernel": "k_scan", "per_launch_ms": per_ms,
                                 "algorithmic_bytes": alg, "achieved": alg / (per_ms * 1e-3) / 1e9,
                                 "traffic": pmc, "achieved_traffic": (pmc / (per_ms * 1e-3) / 1e9) if pmc else None,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": alg / (per_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                                "frac": alg / (per_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                "note": "k_scan time includes the sector head" if sec else None}
     return out
+
+
+def whole_matrix_leg(fp, nparam, X, F, Fdx, L, stream, args):
+    """The same C2 step on whole 9 x 9 matrices (GRAPE_NO_SECTORS=1): the row-group kernels'
+    own efficiency, and the speed-up the sector decomposition adds on top of it."""
+    from robustgrape_amd.engine import GrapePlan
+    os.environ["GRAPE_NO_SECTORS"] = "1"
+    try:
+        plan = GrapePlan(fp, nparam=nparam, device=X.device.index or 0, max_batch=L)
+    finally:
+        del os.environ["GRAPE_NO_SECTORS"]
+    import torch
+    plan.set_stream(stream.cuda_stream)
+    n = X.shape[0]
+    steps = max(3, args.steps // 5)
+    step = lambda: plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), Fdx.data_ptr(), n, 0, 0)  # noqa: E731
+    step()
+    plan.synchronize()
+    plan.kernel_times(reset=True)
+    plan.set_profiling(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    plan.synchronize()
+    kt = plan.kernel_times()
+    plan.close()
+    passes = steps * ((n + L - 1) // L)
+    ms = kt["k_expm_grad"][0] / passes
+    fl = L * NT * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)
+    return {"value": steps * n / dt, "unit": "gradient-evals/s", "steps": steps,
+            "k_expm_grad": {"per_launch_ms": ms, "achieved_TFLOPs": fl / (ms * 1e-3) / 1e12,
+                            "frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS},
+            "kernels_ms_per_step": {k: v[0] / steps for k, v in kt.items() if v[1]},
+            "note": "same workload with sectors disabled (GRAPE_NO_SECTORS=1): whole 9 x 9 matrices"}
 
 
 def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
@@ -597,6 +677,7 @@ def main():
     evals = args.steps * B * world
     value = evals / elapsed
     ktimes = plan.kernel_times()
+    sectors = plan.sectors()
     if rank == 0:
         L = min(count, chunk)
         if c5err:
@@ -606,11 +687,14 @@ def main():
         elif c3:
             out = c3_report(args, B, L, world, value, elapsed, ktimes, ne)
         else:
-            out = c2_report(args, B, L, world, value, elapsed, ktimes)
+            out = c2_report(args, B, L, world, value, elapsed, ktimes, sectors,
+                            args.steps * ((count + L - 1) // L))
         if best is not None:
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         out["config"]["evals_per_device_pass"] = min(count, chunk)
     plan.close()
+    if rank == 0 and world == 1 and not (c3 or c5) and sectors[0][0] < d:
+        out["whole_matrix_path"] = whole_matrix_leg(fp, nparam, X, F, Fdx, min(count, chunk), stream, args)
     if rank == 0:
         if world == 1 and not args.no_host_paths:
             # the drop-in path as the reference's callers use it (host arrays, SURVEY.md 8d's

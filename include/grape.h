@@ -319,15 +319,16 @@ int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launc
 /*
  * Sectors (ABI 5).  When every operator that H0 uses is block-diagonal in one common
  * permutation of the basis (a conserved quantity: for rydberg_hamiltonian_full the 9 levels
- * split into blocks of 1, 2, 2 and 4), exp, chain and contractions never leave the blocks,
- * so grape_fidelity_grad runs each evaluation as `nsectors` independent sector problems of
- * size `sector_dim` (blocks packed first-fit into equal sectors, padded with decoupled
- * levels) and assembles U only for the fidelity head.  Same outputs; no API change.  Chosen
- * at plan creation for operator-basis plans without error sources when it cuts the work at
- * least in half; the environment variable GRAPE_NO_SECTORS=1 turns it off.  Reports
- * (ndim, 1) when the plan runs whole matrices.
+ * split into blocks of 4, 2 and 2 plus |00>, which no operator touches), exp, chain and
+ * contractions never leave the blocks, so grape_fidelity_grad runs each evaluation as
+ * independent sector problems -- one or two classes of `nsectors[c]` sectors of `sector_dims[c]`
+ * levels (blocks packed first-fit, padded with decoupled levels) -- and assembles U only for the
+ * fidelity head.  Same outputs; no API change.  Chosen at plan creation for operator-basis
+ * plans without error sources when it cuts the work at least in half; the environment
+ * variable GRAPE_NO_SECTORS=1 turns it off.  Fills up to max_classes entries and returns the
+ * number of classes; a plan that runs whole matrices reports one class (ndim, 1).
  */
-int grape_plan_sectors(grape_plan *plan, int *sector_dim, int *nsectors);
+int grape_plan_sectors(grape_plan *plan, int *sector_dims, int *nsectors, int max_classes);
 
 /*
  * Batched matrix exponential exp(A) of n column-major ndim x ndim complex

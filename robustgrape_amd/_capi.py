@@ -90,7 +90,7 @@ def lib():
         L.grape_plan_set_profiling.restype = ctypes.c_int
         L.grape_plan_kernel_times.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.grape_plan_kernel_times.restype = ctypes.c_int
-        L.grape_plan_sectors.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.grape_plan_sectors.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.grape_plan_sectors.restype = ctypes.c_int
         if L.grape_abi_version() != ABI_VERSION:
             raise ImportError("libgrape.so ABI version mismatch")

@@ -68,11 +68,21 @@ hipError_t dispatch_pipeline(int D, const DevProblem &P, const DevBatch &B, hipS
     }
     return hipErrorInvalidValue;
 }
-hipError_t dispatch_sector_pipeline(int S, const DevProblem &P, const DevBatch &B, const grape_proj::SectorHead &H,
-                                   hipStream_t st, const KMark &mk) {
+hipError_t dispatch_sector_stage(int S, int stage, const DevProblem &P, const DevBatch &B, hipStream_t st,
+                                 const KMark &mk) {
     switch (S) {
 #define CASE(d) \
-    case d: return grape_host::launch_sector_pipeline<d>(P, B, H, st, mk);
+    case d: return grape_host::launch_sector_stage<d>(stage, P, B, st, mk);
+        GRAPE_DIMS(CASE)
+#undef CASE
+    }
+    return hipErrorInvalidValue;
+}
+hipError_t dispatch_sector_reduce(int S, const DevProblem &P, const DevBatch &B, const grape::SecParts &sp, int nev,
+                                  hipStream_t st, const KMark &mk) {
+    switch (S) {
+#define CASE(d) \
+    case d: return grape_host::launch_sector_reduce<d>(P, B, sp, nev, st, mk);
         GRAPE_DIMS(CASE)
 #undef CASE
     }
@@ -144,14 +154,20 @@ struct grape_plan {
     cd *d_sink = nullptr;                      // DevBatch::sink
     // general projector (FidelityCalculations.jl:47-51): P0 P, P, P0 row-major; head scratch
     cd *d_PA = nullptr, *d_PB = nullptr, *d_P0g = nullptr, *d_gpscr = nullptr;
-    // sectors (grape.h grape_plan_sectors): the fidelity path runs nsec sector problems of
-    // size S per evaluation (Ps), then the sector head over the assembled U (SH)
-    bool sectors = false;
-    DevProblem Ps{};
+    // sectors (grape.h grape_plan_sectors): per evaluation the fidelity path runs the sector
+    // problems of ncls classes (Ps[c]: nsec sectors of S levels each, workspace sb[c]), then
+    // the sector head over the assembled U (SH)
+    struct SecBuf {
+        cd *E = nullptr, *Q = nullptr, *Mc = nullptr, *Carry = nullptr, *Ub = nullptr, *slots = nullptr,
+           *ops = nullptr, *opsT = nullptr, *Msec = nullptr;
+        int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr;
+        double *part = nullptr;
+    };
+    int ncls = 0;
+    DevProblem Ps[2]{};
+    SecBuf sb[2];
+    int *d_fixed = nullptr;
     grape_proj::SectorHead SH{};
-    int *d_sidx = nullptr;
-    cd *d_sops = nullptr, *d_sopsT = nullptr, *d_Msec = nullptr;
-    double *d_sec_part = nullptr;
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -204,9 +220,14 @@ static void free_plan(grape_plan *p) {
                     p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
-                    p->d_sidx, p->d_sops, p->d_sopsT, p->d_sec_part, p->d_Msec};
+                    p->d_fixed};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    for (auto &c : p->sb) {
+        void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part};
+        for (void *b : sbufs)
+            if (b) (void)hipFree(b);
+    }
     for (auto &e : p->ev_pool) (void)hipEventDestroy(e);
     for (auto &pe : p->pending) {
         (void)hipEventDestroy(pe.a);
@@ -371,15 +392,43 @@ static int upload_projector(grape_plan *p, const ProjectorSetup &ps, DevProblem 
 // Sectors: connected components of the union sparsity pattern of every operator H0 uses
 // (the levels an evolution can ever couple).  A single level with a zero diagonal in every
 // operator never evolves (its propagator is 1 and it carries no gradient): it is "fixed" and
-// only enters the head's U.  The others are packed first-fit-decreasing into nsec sectors of
-// S = max(2, largest component) slots; sidx[w * S + a] = level in slot a of sector w, or -1
-// (padding: a decoupled level, exp(0) = 1, never reaches F), followed by the fixed levels.
-// Only for operator-basis plans without error sources (the error path keeps whole matrices),
-// and only when the sector work nsec * S^3 is at most half of d^3.
-struct SectorSetup {
-    int S = 0, nsec = 1, nfixed = 0;
+// only enters the head's U.  The others are packed first-fit-decreasing into sectors of
+// S = max(2, largest component) slots -- one class -- or, when that costs at least a quarter
+// less work (sum of nsec S^3), into two classes: the components above a size cut in sectors of
+// their largest size, the rest in sectors of theirs (d = 9 Rydberg: one sector of 4 and two of
+// 2 instead of two of 4).  sidx[w * S + a] = level in slot a of sector w, or -1 (padding: a
+// decoupled level, exp(0) = 1, never reaches F).  Only for operator-basis plans without error
+// sources (the error path keeps whole matrices), and only when the sector work is at most half
+// of d^3.
+struct SectorClass {
+    int S = 0, nsec = 0;
     std::vector<int> sidx;
 };
+struct SectorSetup {
+    std::vector<SectorClass> cls;
+    std::vector<int> fixed;
+};
+static SectorClass pack_sectors(const std::vector<std::vector<int>> &comps) {  // comps sorted by size, desc
+    SectorClass sc;
+    sc.S = std::max(2, (int)comps[0].size());
+    std::vector<std::vector<int>> bins;
+    for (const auto &c : comps) {
+        bool placed = false;
+        for (auto &bn : bins)
+            if ((int)(bn.size() + c.size()) <= sc.S) {
+                bn.insert(bn.end(), c.begin(), c.end());
+                placed = true;
+                break;
+            }
+        if (!placed) bins.push_back(c);
+    }
+    sc.nsec = (int)bins.size();
+    sc.sidx.assign((size_t)sc.nsec * sc.S, -1);
+    for (int w = 0; w < sc.nsec; ++w)
+        for (size_t a = 0; a < bins[w].size(); ++a) sc.sidx[(size_t)w * sc.S + a] = bins[w][a];
+    return sc;
+}
+static long sector_cost(const SectorClass &c) { return (long)c.nsec * c.S * c.S * c.S; }
 static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
     SectorSetup ss;
     const int D = desc->ndim;
@@ -429,28 +478,24 @@ static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
     if (ncomp < 2 || comps.empty()) return ss;
     std::stable_sort(comps.begin(), comps.end(),
                      [](const std::vector<int> &a, const std::vector<int> &b) { return a.size() > b.size(); });
-    const int S = std::max(2, (int)comps[0].size());
-    std::vector<std::vector<int>> bins;
-    for (const auto &c : comps) {
-        bool placed = false;
-        for (auto &bn : bins)
-            if ((int)(bn.size() + c.size()) <= S) {
-                bn.insert(bn.end(), c.begin(), c.end());
-                placed = true;
-                break;
-            }
-        if (!placed) bins.push_back(c);
+    std::vector<SectorClass> best{pack_sectors(comps)};
+    long cost = sector_cost(best[0]);
+    for (size_t i = 1; i < comps.size(); ++i) {
+        if (comps[i].size() == comps[i - 1].size()) continue;
+        const std::vector<std::vector<int>> a(comps.begin(), comps.begin() + i), b(comps.begin() + i, comps.end());
+        std::vector<SectorClass> two{pack_sectors(a), pack_sectors(b)};
+        const long c2 = sector_cost(two[0]) + sector_cost(two[1]);
+        if (4 * c2 <= 3 * cost) {
+            best = two;
+            cost = c2;
+        }
     }
-    const int nsec = (int)bins.size();
-    if (2L * nsec * S * S * S > (long)D * D * D || nsec * S * S > grape_proj::kSectorLds) return ss;
-    if (nsec < 2 && fixed.empty()) return ss;
-    ss.S = S;
-    ss.nsec = nsec;
-    ss.nfixed = (int)fixed.size();
-    ss.sidx.assign((size_t)nsec * S, -1);
-    for (int w = 0; w < nsec; ++w)
-        for (size_t a = 0; a < bins[w].size(); ++a) ss.sidx[(size_t)w * S + a] = bins[w][a];
-    ss.sidx.insert(ss.sidx.end(), fixed.begin(), fixed.end());
+    if (2 * cost > (long)D * D * D) return ss;
+    for (const auto &c : best)
+        if (c.nsec * c.S * c.S > grape_proj::kSectorLds) return ss;
+    if (best.size() == 1 && best[0].nsec < 2 && fixed.empty()) return ss;
+    ss.cls = best;
+    ss.fixed = fixed;
     return ss;
 }
 
@@ -748,24 +793,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.nsec = 1;
     P.sec_ops = 0;
     const SectorSetup ss = find_sectors(desc, tables);
-    const bool sec = ss.S > 0;
-    int s_waves = kScanWide, s_L = 0, s_nchunks = 0;
-    if (sec) {
-        if (dispatch_lds_limits(ss.S) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
-        s_waves = (long)p->max_batch * ss.nsec >= 2L * ncu ? kScanNarrow : kScanWide;
-        if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {
-            const int wv = std::atoi(w);
-            if (wv == kScanNarrow || wv == kScanWide) s_waves = wv;
-        }
-        const int ncs = std::min(s_waves * (64 / ss.S), P.Nt);
-        s_L = (P.Nt + ncs - 1) / ncs;
-        s_nchunks = (P.Nt + s_L - 1) / s_L;
-    }
-    // workspace rows / tile / chunks of the fidelity path: whole matrices, or nsec sector
-    // problems per evaluation
-    const size_t WR = sec ? (size_t)p->max_batch * ss.nsec : (size_t)p->max_batch;
-    const size_t WT = sec ? (size_t)ss.S * ss.S : (size_t)D * D;
-    const size_t WC = sec ? (size_t)s_nchunks : (size_t)P.nchunks;
+    const bool sec = !ss.cls.empty();
+    const size_t FR = sec ? 0 : (size_t)p->max_batch;  // whole-matrix workspace rows (none when sectors run)
 
     // operator basis: column-major interleaved -> row-major cd tiles (row builds)
     // and column-major ones (the exp kernels build columns)
@@ -783,25 +812,20 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
               dalloc(&p->d_h0, std::max(desc->n_h0_terms, 0)) == hipSuccess &&
               dalloc(&p->d_tgt, std::max(desc->n_target_terms, 0)) == hipSuccess &&
               dalloc(&p->d_W, (size_t)D) == hipSuccess &&
-              dalloc(&p->d_E, WR * P.Nt * P.nv * WT) == hipSuccess && dalloc(&p->d_Q, WR * P.Nt * WT) == hipSuccess &&
-              dalloc(&p->d_Mc, WR * WC * WT) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
+              dalloc(&p->d_E, FR * P.Nt * P.nv * T) == hipSuccess && dalloc(&p->d_Q, FR * P.Nt * T) == hipSuccess &&
+              dalloc(&p->d_Mc, FR * P.nchunks * T) == hipSuccess && dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_part, MB * P.Nt * std::max(P.na, 1)) == hipSuccess &&
               dalloc(&p->d_tgt_part, MB * std::max(P.na, 1)) == hipSuccess &&
-              dalloc(&p->d_ovf, WR * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess &&
+              dalloc(&p->d_ovf, FR * P.Nt * P.nv) == hipSuccess && dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess &&
               dalloc(&p->d_sink, T) == hipSuccess &&
               dalloc(&p->d_vs, vs.size()) == hipSuccess;
     const int nvg = P.np + (P.xadd_dep ? P.na : 0);
     if (ok && P.ne == 0)
-        ok = dalloc(&p->d_ovf2, WR * P.Nt * nvg) == hipSuccess &&
-             dalloc(&p->d_ovf2_slots, WR * P.Nt * nvg * WT) == hipSuccess;
-    if (ok && (P.ne > 0 || ps.general || sec))  // carries and U: the error path and the heads
-        ok = dalloc(&p->d_Carry, WR * WC * WT) == hipSuccess && dalloc(&p->d_Ub, WR * WT) == hipSuccess;
-    if (ok && sec)
-        ok = dalloc(&p->d_sec_part, WR * P.Nt * nvg) == hipSuccess && dalloc(&p->d_sidx, ss.sidx.size()) == hipSuccess &&
-             dalloc(&p->d_Msec, WR * WT) == hipSuccess &&
-             dalloc(&p->d_sops, (size_t)ss.nsec * n_ops * WT) == hipSuccess &&
-             dalloc(&p->d_sopsT, (size_t)ss.nsec * n_ops * WT) == hipSuccess;
+        ok = dalloc(&p->d_ovf2, FR * P.Nt * nvg) == hipSuccess &&
+             dalloc(&p->d_ovf2_slots, FR * P.Nt * nvg * T) == hipSuccess;
+    if (ok && (P.ne > 0 || ps.general))  // carries and U: the error path and the general-projector heads
+        ok = dalloc(&p->d_Carry, FR * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, FR * T) == hipSuccess;
     if (ok && P.ne > 0)
         ok = dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
@@ -839,63 +863,93 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.err_off = p->d_err_off;
     P.vs = p->d_vs;
     P.W = p->d_W;
-    if (sec) {  // the sector problem and the head over the assembled U
-        const int S = ss.S;
-        std::vector<cd> sops((size_t)ss.nsec * n_ops * S * S), sopsT(sops.size());
-        for (int w = 0; w < ss.nsec; ++w)
-            for (int o = 0; o < n_ops; ++o)
-                for (int a = 0; a < S; ++a)
-                    for (int c = 0; c < S; ++c) {
-                        const int gi = ss.sidx[(size_t)w * S + a], gj = ss.sidx[(size_t)w * S + c];
-                        const cd v = (gi >= 0 && gj >= 0) ? ops[(size_t)o * T + (size_t)gi * D + gj] : cd{0.0, 0.0};
-                        const size_t base = ((size_t)w * n_ops + o) * S * S;
-                        sops[base + (size_t)a * S + c] = v;
-                        sopsT[base + (size_t)c * S + a] = v;
-                    }
+    if (sec) {  // the sector problems of every class and the head over the assembled U
         std::vector<cd> A(T, cd{0.0, 0.0}), Bm(T, cd{0.0, 0.0});  // diagonal projector: A = diag(w), B = diag(w != 0)
         for (int i = 0; i < D; ++i) {
             A[(size_t)i * D + i] = cd{ps.W[i], 0.0};
             Bm[(size_t)i * D + i] = cd{ps.W[i] != 0.0 ? 1.0 : 0.0, 0.0};
         }
-        if (!ps.general && (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess))
+        if (!ps.general && (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess ||
+                            hipMemcpy(p->d_PA, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                            hipMemcpy(p->d_PB, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess))
             return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
-        if (hipMemcpy(p->d_sops, sops.data(), sops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(p->d_sopsT, sopsT.data(), sopsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(p->d_sidx, ss.sidx.data(), ss.sidx.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
-            (!ps.general && (hipMemcpy(p->d_PA, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
-                             hipMemcpy(p->d_PB, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess)))
-            return bail(fail(GRAPE_ERR_HIP, "upload failed (sectors)"));
-        p->sectors = true;
-        DevProblem &Ps = p->Ps;
-        Ps = P;
-        Ps.D = S;
-        Ps.sectors = 1;
-        Ps.nsec = ss.nsec;
-        Ps.sec_ops = (size_t)n_ops * S * S;
-        Ps.ops = p->d_sops;
-        Ps.opsT = p->d_sopsT;
-        Ps.scan_waves = s_waves;
-        Ps.L = s_L;
-        Ps.nchunks = s_nchunks;
-        Ps.gen_proj = 0;
+        if (dalloc(&p->d_fixed, ss.fixed.size()) != hipSuccess ||
+            (!ss.fixed.empty() && hipMemcpy(p->d_fixed, ss.fixed.data(), ss.fixed.size() * sizeof(int),
+                                            hipMemcpyHostToDevice) != hipSuccess))
+            return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
         grape_proj::SectorHead &H = p->SH;
         H.P = P;
         H.P.PA = p->d_PA;
         H.P.PB = p->d_PB;
-        H.S = S;
-        H.nsec = ss.nsec;
-        H.nfixed = ss.nfixed;
-        H.sidx = p->d_sidx;
+        H.ncls = (int)ss.cls.size();
+        H.fixed = p->d_fixed;
+        H.nfixed = (int)ss.fixed.size();
+        for (int cl = 0; cl < (int)ss.cls.size(); ++cl) {
+            const SectorClass &sc = ss.cls[cl];
+            const int S = sc.S;
+            const size_t TS = (size_t)S * S, R = MB * sc.nsec;  // workspace rows: sub-evaluations
+            if (dispatch_lds_limits(S) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
+            DevProblem &Ps = p->Ps[cl];
+            Ps = P;
+            Ps.D = S;
+            Ps.sectors = 1;
+            Ps.nsec = sc.nsec;
+            Ps.sec_ops = (size_t)n_ops * TS;
+            Ps.gen_proj = 0;
+            Ps.scan_waves = (long)R >= 2L * ncu ? kScanNarrow : kScanWide;
+            if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {
+                const int wv = std::atoi(w);
+                if (wv == kScanNarrow || wv == kScanWide) Ps.scan_waves = wv;
+            }
+            const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
+            Ps.L = (P.Nt + ncs - 1) / ncs;
+            Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
+            grape_plan::SecBuf &b = p->sb[cl];
+            if (dalloc(&b.E, R * P.Nt * TS) != hipSuccess || dalloc(&b.Q, R * P.Nt * TS) != hipSuccess ||
+                dalloc(&b.Mc, R * Ps.nchunks * TS) != hipSuccess || dalloc(&b.Carry, R * Ps.nchunks * TS) != hipSuccess ||
+                dalloc(&b.Ub, R * TS) != hipSuccess || dalloc(&b.Msec, R * TS) != hipSuccess ||
+                dalloc(&b.slots, R * P.Nt * nvg * TS) != hipSuccess || dalloc(&b.ovf, R * P.Nt) != hipSuccess ||
+                dalloc(&b.ovf2, R * P.Nt * nvg) != hipSuccess || dalloc(&b.part, R * P.Nt * nvg) != hipSuccess ||
+                dalloc(&b.sidx, sc.sidx.size()) != hipSuccess || dalloc(&b.ops, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
+                dalloc(&b.opsT, (size_t)sc.nsec * n_ops * TS) != hipSuccess)
+                return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
+            std::vector<cd> sops((size_t)sc.nsec * n_ops * TS), sopsT(sops.size());
+            for (int w = 0; w < sc.nsec; ++w)
+                for (int o = 0; o < n_ops; ++o)
+                    for (int a = 0; a < S; ++a)
+                        for (int c = 0; c < S; ++c) {
+                            const int gi = sc.sidx[(size_t)w * S + a], gj = sc.sidx[(size_t)w * S + c];
+                            const cd v = (gi >= 0 && gj >= 0) ? ops[(size_t)o * T + (size_t)gi * D + gj] : cd{0.0, 0.0};
+                            const size_t base = ((size_t)w * n_ops + o) * TS;
+                            sops[base + (size_t)a * S + c] = v;
+                            sopsT[base + (size_t)c * S + a] = v;
+                        }
+            if (hipMemcpy(b.ops, sops.data(), sops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(b.opsT, sopsT.data(), sopsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(b.sidx, sc.sidx.data(), sc.sidx.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(GRAPE_ERR_HIP, "upload failed (sectors)"));
+            Ps.ops = b.ops;
+            Ps.opsT = b.opsT;
+            H.S[cl] = S;
+            H.nsec[cl] = sc.nsec;
+            H.sidx[cl] = b.sidx;
+            H.Ub[cl] = b.Ub;
+            H.Msec[cl] = b.Msec;
+        }
+        p->ncls = (int)ss.cls.size();
     }
     *out = p;
     return GRAPE_OK;
 }
 
-int grape_plan_sectors(grape_plan *p, int *sector_dim, int *nsectors) {
+int grape_plan_sectors(grape_plan *p, int *sector_dims, int *nsectors, int max_classes) {
     if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
-    if (sector_dim) *sector_dim = p->sectors ? p->Ps.D : (p->dense ? p->DP.P.D : p->P.D);
-    if (nsectors) *nsectors = p->sectors ? p->Ps.nsec : 1;
-    return GRAPE_OK;
+    const int n = p->ncls > 0 ? p->ncls : 1;
+    for (int c = 0; c < n && c < max_classes; ++c) {
+        if (sector_dims) sector_dims[c] = p->ncls ? p->Ps[c].D : (p->dense ? p->DP.P.D : p->P.D);
+        if (nsectors) nsectors[c] = p->ncls ? p->Ps[c].nsec : 1;
+    }
+    return n;
 }
 
 void grape_plan_destroy(grape_plan *plan) { free_plan(plan); }
@@ -957,39 +1011,47 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, st, mk));
         return GRAPE_OK;
     }
-    if (p->sectors) {
-        const DevProblem &Ps = p->Ps;
-        DevBatch B{};
-        B.nb = nb * Ps.nsec;
-        B.x = d_x;
-        B.F = d_F;
-        B.Fdx = d_Fdx;
-        B.E = p->d_E;
-        B.Q = p->d_Q;
-        B.Mc = p->d_Mc;
-        B.part_add = p->d_part;
-        B.tgt_part = p->d_tgt_part;
-        B.overflow = p->d_ovf;
-        B.Carry = p->d_Carry;
-        B.Ub = p->d_Ub;
-        B.ovf2 = p->d_ovf2;
-        B.ovf2_slots = p->d_ovf2_slots;
-        B.sec_part = p->d_sec_part;
-        B.Msec = p->d_Msec;
-        int *cnt = p->d_ctrl + 4;
-        B.overflow_count = cnt;
-        B.ovf2_count = cnt + 1;
-        B.status = p->d_ctrl + 2;
-        B.sink = p->d_sink;
+    if (p->ncls) {  // sectors: stage 0 of every class, the head, stage 1 of every class, the sum
+        DevBatch Bc[2]{};
+        grape::SecParts sp{};
+        for (int cl = 0; cl < p->ncls; ++cl) {
+            const grape_plan::SecBuf &sb = p->sb[cl];
+            DevBatch &B = Bc[cl];
+            B.nb = nb * p->Ps[cl].nsec;
+            B.x = d_x;
+            B.F = d_F;
+            B.Fdx = d_Fdx;
+            B.E = sb.E;
+            B.Q = sb.Q;
+            B.Mc = sb.Mc;
+            B.Carry = sb.Carry;
+            B.Ub = sb.Ub;
+            B.Msec = sb.Msec;
+            B.part_add = p->d_part;
+            B.tgt_part = p->d_tgt_part;
+            B.overflow = sb.ovf;
+            B.ovf2 = sb.ovf2;
+            B.ovf2_slots = sb.slots;
+            B.sec_part = sb.part;
+            B.overflow_count = p->d_ctrl + 4 + 2 * cl;  // ctrl [4..7]: two counters per class
+            B.ovf2_count = p->d_ctrl + 5 + 2 * cl;
+            B.status = p->d_ctrl + 2;
+            B.sink = p->d_sink;
+            sp.part[cl] = sb.part;
+            sp.nsec[cl] = p->Ps[cl].nsec;
+        }
+        HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));
+        for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 0, p->Ps[cl], Bc[cl], st, mk));
         grape_proj::SectorHead H = p->SH;
         H.x = d_x;
-        H.Ub = p->d_Ub;
-        H.Msec = p->d_Msec;
         H.F = d_F;
         H.Fdx = d_Fdx;
         H.tgt_part = p->d_tgt_part;
-        HIPCHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
-        HIPCHECK(dispatch_sector_pipeline(Ps.D, Ps, B, H, st, mk));
+        mk(GRAPE_KERNEL_SCAN, 0);
+        HIPCHECK(grape_proj::launch_sector_head(H, nb, st));
+        mk(GRAPE_KERNEL_SCAN, 1);
+        for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 1, p->Ps[cl], Bc[cl], st, mk));
+        HIPCHECK(dispatch_sector_reduce(p->Ps[0].D, p->Ps[0], Bc[0], sp, nb, st, mk));
         return GRAPE_OK;
     }
     const DevProblem &P = p->P;

@@ -882,10 +882,14 @@ __global__ void k_sec_mc(DevProblem P, DevBatch B) {
     B.Mc[(size_t)t] = acc;
 }
 
-// Sectors: F_dx[b][k, u] (or the per-step x_add term) = sum over the evaluation's sectors, in
-// sector order (deterministic).  One thread per (b, k, u).
+// Sectors: F_dx[b][k, u] (or the per-step x_add term) = sum over the evaluation's sectors of
+// both classes, in sector order (deterministic).  One thread per (b, k, u).
+struct SecParts {
+    const double *part[2];  // [nb][nsec_c][Nt][nvg] per sector class
+    int nsec[2];            // 0 for an absent class
+};
 template <int D>
-__global__ void k_sec_reduce(DevProblem P, DevBatch B, int nb) {
+__global__ void k_sec_reduce(DevProblem P, double *Fdx, double *part_add, SecParts S, int nb) {
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long per = (long)P.Nt * P.nvg;
     if (t >= (long)nb * per) return;
@@ -893,9 +897,10 @@ __global__ void k_sec_reduce(DevProblem P, DevBatch B, int nb) {
     const long r = t - (long)b * per;  // k * nvg + u
     const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
     double s = 0.0;
-    for (int w = 0; w < P.nsec; ++w) s += B.sec_part[((size_t)b * P.nsec + w) * per + r];
-    if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
-    else B.part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
+    for (int c = 0; c < 2; ++c)
+        for (int w = 0; w < S.nsec[c]; ++w) s += S.part[c][((size_t)b * S.nsec[c] + w) * per + r];
+    if (u < P.np) Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+    else part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
 }
 
 }  // namespace grape

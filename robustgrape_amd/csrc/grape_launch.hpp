@@ -135,38 +135,39 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     return hipGetLastError();
 }
 
-// Sectors (P.sectors, D = the sector size, B.nb = evaluations x nsec): nominal sector
-// propagators -> sector scans (U_w, carries) -> sector head (F, M'_{c,w}, target part; one
-// workgroup per evaluation) -> eps-variant sector exps contracted in place -> the per-step
-// F_dx terms summed over sectors (k_sec_reduce) [-> the x_add sum over steps].
+// Sectors (P.sectors, D = the sector size of one class, B.nb = evaluations x nsec).  Stage 0:
+// nominal sector propagators -> sector scans (U_w, carries).  Then (grape_engine.hip) the
+// sector head over every class (F, the blocks of M, target part).  Stage 1: per-chunk images
+// M'_c (k_sec_mc) -> eps-variant sector exps contracted in place.  Then k_sec_reduce sums the
+// per-step F_dx terms over the sectors of every class [-> the x_add sum over steps].
 template <int D>
-hipError_t launch_sector_pipeline(const DevProblem &P, const DevBatch &B, const grape_proj::SectorHead &H,
-                                  hipStream_t st, const KMark &mark) {
+hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B, hipStream_t st,
+                               const KMark &mark) {
     constexpr int GPW = grape::Geo<D>::GPW;
-    const int nev = B.nb / P.nsec;
-    const long nexp = (long)B.nb * P.Nt;
-    mark(GRAPE_KERNEL_EXPM, 0);
-    hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                       expm_lean_lds<D>(), st, P, B);
-    mark(GRAPE_KERNEL_EXPM, 1);
-    mark(GRAPE_KERNEL_EXPM_HIGH, 0);
-    hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
-                       B.overflow_count, B.status, 1);
-    mark(GRAPE_KERNEL_EXPM_HIGH, 1);
-    mark(GRAPE_KERNEL_SCAN, 0);
-    if (P.scan_waves == kScanNarrow)
-        hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
-                           scan_lds<D>(kScanNarrow), st, P, B);
-    else
-        hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide),
-                           st, P, B);
-    {
-        const hipError_t e = grape_proj::launch_sector_head(H, nev, st);
-        if (e != hipSuccess) return e;
+    if (stage == 0) {
+        const long nexp = (long)B.nb * P.Nt;
+        mark(GRAPE_KERNEL_EXPM, 0);
+        hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                           expm_lean_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_EXPM, 1);
+        mark(GRAPE_KERNEL_EXPM_HIGH, 0);
+        hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
+                           B.overflow_count, B.status, 1);
+        mark(GRAPE_KERNEL_EXPM_HIGH, 1);
+        mark(GRAPE_KERNEL_SCAN, 0);
+        if (P.scan_waves == kScanNarrow)
+            hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
+                               scan_lds<D>(kScanNarrow), st, P, B);
+        else
+            hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide),
+                               scan_lds<D>(kScanWide), st, P, B);
+        mark(GRAPE_KERNEL_SCAN, 1);
+        return hipGetLastError();
     }
+    mark(GRAPE_KERNEL_REDUCE, 0);
     const long nmc = (long)B.nb * P.nchunks * D * D;
     hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
-    mark(GRAPE_KERNEL_SCAN, 1);
+    mark(GRAPE_KERNEL_REDUCE, 1);
     const long ng = (long)B.nb * P.Nt * P.nvg;
     mark(GRAPE_KERNEL_EXPM_GRAD, 0);
     hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lean_lds<D>(),
@@ -175,9 +176,17 @@ hipError_t launch_sector_pipeline(const DevProblem &P, const DevBatch &B, const 
     mark(GRAPE_KERNEL_GRAD_HIGH, 0);
     hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
     mark(GRAPE_KERNEL_GRAD_HIGH, 1);
+    return hipGetLastError();
+}
+
+// The sum over sectors (and, xadd_dep, over steps) of one launch of nev evaluations.
+template <int D>
+hipError_t launch_sector_reduce(const DevProblem &P, const DevBatch &B, const grape::SecParts &S, int nev,
+                                hipStream_t st, const KMark &mark) {
     mark(GRAPE_KERNEL_REDUCE, 0);
     const long nred = (long)nev * P.Nt * P.nvg;
-    hipLaunchKernelGGL(grape::k_sec_reduce<D>, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, st, P, B, nev);
+    hipLaunchKernelGGL(grape::k_sec_reduce<D>, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, st, P, B.Fdx,
+                       B.part_add, S, nev);
     if (P.xadd_dep && P.na > 0) {
         DevBatch Be = B;  // the x_add sums run over evaluations, not sub-evaluations
         Be.nb = nev;
@@ -247,8 +256,10 @@ hipError_t set_lds_limits() {
 
 #define GRAPE_DECLARE_DIM(d, EXT)                                                                          \
     EXT template hipError_t launch_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &); \
-    EXT template hipError_t launch_sector_pipeline<d>(const DevProblem &, const DevBatch &,                   \
-                                                      const grape_proj::SectorHead &, hipStream_t, const KMark &); \
+    EXT template hipError_t launch_sector_stage<d>(int, const DevProblem &, const DevBatch &, hipStream_t,     \
+                                                   const KMark &);                                            \
+    EXT template hipError_t launch_sector_reduce<d>(const DevProblem &, const DevBatch &, const grape::SecParts &, \
+                                                    int, hipStream_t, const KMark &);                         \
     EXT template hipError_t launch_expm_raw<d>(const cd *, cd *, int, int *, int *, int *, int *, hipStream_t);  \
     EXT template hipError_t set_lds_limits<d>();                                                          \
     EXT template hipError_t launch_expm_variants<d>(const DevProblem &, const DevBatch &, hipStream_t);     \

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(SEC_BLOCK) void k_sec_head(SectorHead H) {
     __shared__ double red[SEC_BLOCK];
     extern __shared__ __attribute__((aligned(16))) unsigned char sec_smem[];
     const grape::DevProblem &P = H.P;
-    const int D = P.D, b = blockIdx.x, S = H.S, SS = H.S * H.S, ns = H.nsec;
+    const int D = P.D, b = blockIdx.x;
     const size_t T = (size_t)D * D;
     cd *s = reinterpret_cast<cd *>(sec_smem);
     cd *U = s + H_U * T, *U0 = s + H_U0 * T, *K = s + H_K * T, *X = s + H_X * T, *Y = s + H_Y * T;
@@ -319,13 +319,16 @@ __global__ __launch_bounds__(SEC_BLOCK) void k_sec_head(SectorHead H) {
     // touches (exact zeros across sectors, as in the dense product)
     for (int t = threadIdx.x; t < (int)T; t += blockDim.x) U[t] = cd{0.0, 0.0};
     __syncthreads();
-    for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
-        const int w = t / SS, r = (t % SS) / S, c = t % S;
-        const int gi = H.sidx[w * S + r], gj = H.sidx[w * S + c];
-        if (gi >= 0 && gj >= 0) U[(size_t)gi * D + gj] = H.Ub[((size_t)b * ns + w) * SS + r * S + c];
+    for (int cl = 0; cl < H.ncls; ++cl) {
+        const int S = H.S[cl], SS = S * S, ns = H.nsec[cl];
+        for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
+            const int w = t / SS, r = (t % SS) / S, c = t % S;
+            const int gi = H.sidx[cl][w * S + r], gj = H.sidx[cl][w * S + c];
+            if (gi >= 0 && gj >= 0) U[(size_t)gi * D + gj] = H.Ub[cl][((size_t)b * ns + w) * SS + r * S + c];
+        }
     }
     for (int t = threadIdx.x; t < H.nfixed; t += blockDim.x) {
-        const int g = H.sidx[ns * S + t];
+        const int g = H.fixed[t];
         U[(size_t)g * D + g] = cd{1.0, 0.0};
     }
     __syncthreads();
@@ -362,10 +365,13 @@ __global__ __launch_bounds__(SEC_BLOCK) void k_sec_head(SectorHead H) {
     }
     if (threadIdx.x == 0) H.F[b] = Fv;
     // the sector blocks M_ww: the only part of M the block-diagonal contractions see
-    for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
-        const int w = t / SS, r = (t % SS) / S, c = t % S;
-        const int gi = H.sidx[w * S + r], gj = H.sidx[w * S + c];
-        H.Msec[(size_t)b * ns * SS + t] = (gi >= 0 && gj >= 0) ? M[(size_t)gi * D + gj] : cd{0.0, 0.0};
+    for (int cl = 0; cl < H.ncls; ++cl) {
+        const int S = H.S[cl], SS = S * S, ns = H.nsec[cl];
+        for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
+            const int w = t / SS, r = (t % SS) / S, c = t % S;
+            const int gi = H.sidx[cl][w * S + r], gj = H.sidx[cl][w * S + c];
+            H.Msec[cl][(size_t)b * ns * SS + t] = (gi >= 0 && gj >= 0) ? M[(size_t)gi * D + gj] : cd{0.0, 0.0};
+        }
     }
 }
 

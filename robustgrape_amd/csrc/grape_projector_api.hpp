@@ -41,12 +41,15 @@ hipError_t launch_err_head(const Heads &H, int nb, hipStream_t st);
 // blocks M_ww; k_sec_mc then forms the per-chunk images M'_{c,w} = Carry M_ww Carry^dagger
 // that the sector k_expm_grad contracts.
 struct SectorHead {
-    grape::DevProblem P;    // the FULL d-dimensional problem (target terms, operators, PA / PB), d <= 12
-    int S, nsec, nfixed;    // sector size, sectors per evaluation, untouched (identity) levels
-    const int *sidx;        // [nsec][S]: level of each sector slot (-1: padding), then the nfixed levels
-    const double *x;        // [nb][nx]
-    const grape::cd *Ub;    // [nb * nsec][S][S]
-    grape::cd *Msec;        // [nb * nsec][S][S]  (written)
+    grape::DevProblem P;      // the FULL d-dimensional problem (target terms, operators, PA / PB), d <= 12
+    int ncls;                 // sector classes (1 or 2), each of nsec[c] sectors of S[c] slots
+    int S[2], nsec[2];
+    const int *sidx[2];       // [nsec][S]: level of each sector slot (-1: padding)
+    const grape::cd *Ub[2];   // [nb * nsec][S][S]
+    grape::cd *Msec[2];       // [nb * nsec][S][S]  (written)
+    const int *fixed;         // levels no operator touches (identity in U)
+    int nfixed;
+    const double *x;          // [nb][nx]
     double *F, *Fdx, *tgt_part;
 };
 constexpr int kSectorLds = 2048;  // complex elements of LDS for the sector blocks M_ww (nsec * S * S)

@@ -169,12 +169,13 @@ class GrapePlan:
     def synchronize(self):
         _capi.check(_capi.lib().grape_plan_synchronize(self.handle))
 
-    def sectors(self) -> tuple[int, int]:
-        """(sector size, sectors per evaluation) of the fidelity path; (ndim, 1) = whole matrices
-        (include/grape.h grape_plan_sectors)."""
-        S, n = ctypes.c_int(0), ctypes.c_int(0)
-        _capi.check(_capi.lib().grape_plan_sectors(self.handle, ctypes.byref(S), ctypes.byref(n)))
-        return S.value, n.value
+    def sectors(self) -> tuple:
+        """((sector size, sectors per evaluation), ...) per sector class of the fidelity path;
+        ((ndim, 1),) = whole matrices (include/grape.h grape_plan_sectors)."""
+        S, n = (ctypes.c_int * 2)(), (ctypes.c_int * 2)()
+        k = _capi.lib().grape_plan_sectors(self.handle, S, n, 2)
+        _capi.check(min(k, 0))
+        return tuple((S[c], n[c]) for c in range(k))
 
 
 # Plan cache of the reference-shaped entry points (one plan per problem object, nparam and

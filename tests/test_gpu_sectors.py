@@ -1,9 +1,10 @@
 """Sectors (include/grape.h grape_plan_sectors): problems whose H0 operators are block-diagonal
 in a common permutation run each evaluation as independent sector problems.  The Rydberg
 Hamiltonians of the reference all have this structure (the laser couples |1> <-> |r> only):
-rydberg_hamiltonian_full (d = 9) splits into blocks of 4, 2, 2 and the untouched |00> -> 2
-sectors of 4 levels, the symmetric blockaded one (d = 5) into 2, 2 (+ |00>) -> 2 sectors of 2,
-the full blockaded one (d = 7) into 2, 2, 2 (+ |00>) -> 3 sectors of 2.
+rydberg_hamiltonian_full (d = 9) splits into blocks of 4, 2, 2 and the untouched |00> -> one
+sector of 4 levels and two of 2 (two sector classes), the symmetric blockaded one (d = 5) into
+2, 2 (+ |00>) -> 2 sectors of 2, the full blockaded one (d = 7) into 2, 2, 2 (+ |00>) -> 3
+sectors of 2.
 
 The sector path must give the whole-matrix path's numbers (GRAPE_NO_SECTORS=1) and the
 oracle's, for diagonal and general projectors (which mix sectors in the fidelity head),
@@ -54,9 +55,9 @@ def _close(a, b, tight=True):
 
 
 @pytest.mark.parametrize("name,fp,layout", [
-    ("full9", lambda: P.full9_problem(40), (4, 2)),
-    ("sym5", lambda: P.sym_problem(24), (2, 2)),
-    ("fullblk7", lambda: P.fullblk_problem(24), (2, 3)),
+    ("full9", lambda: P.full9_problem(40), ((4, 1), (2, 2))),
+    ("sym5", lambda: P.sym_problem(24), ((2, 2),)),
+    ("fullblk7", lambda: P.fullblk_problem(24), ((2, 3),)),
 ])
 def test_sectors_match_whole_matrices_and_oracle(name, fp, layout, monkeypatch):
     from oracle import grape_oracle as O
@@ -64,7 +65,7 @@ def test_sectors_match_whole_matrices_and_oracle(name, fp, layout, monkeypatch):
     nt, d = f.unitary_problem.ntimes, f.unitary_problem.ndim
     X = np.stack([P.random_x(nt, 40 + s) for s in range(6)])
     sec, whole, out, ref = _both(f, X, monkeypatch)
-    assert sec == layout and whole == (d, 1)
+    assert sec == layout and whole == ((d, 1),)
     _close(out, ref)
     for b in (0, 5):
         F0, g0 = O.calculate_fidelity_and_derivatives(f, X[b])[:2]
@@ -74,7 +75,7 @@ def test_sectors_match_whole_matrices_and_oracle(name, fp, layout, monkeypatch):
 def test_no_sectors_with_error_sources(monkeypatch):
     pl = _plan(P.full9_problem(16, nerr=2), 2, monkeypatch)
     try:
-        assert pl.sectors() == (9, 1)
+        assert pl.sectors() == ((9, 1),)
     finally:
         pl.close()
 
@@ -88,7 +89,7 @@ def test_sectors_with_xadd_dependent_h0(d, monkeypatch):
     fp = P.xadd_err_problem(d, nt, nerr=0)
     X = np.stack([P.xadd_x(nt, 70 + s) for s in range(4)])
     sec, _, out, ref = _both(fp, X, monkeypatch)
-    assert sec[1] > 1
+    assert sec[0][0] < d
     _close(out, ref, tight=False)  # dt = t0 / 16 with x_main = 2 pi U: long steps, the T2 tier
     fo = P.xadd_err_problem(d, nt, nerr=0, device=False)
     F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[2])[:2]
@@ -106,7 +107,7 @@ def test_general_projector_mixing_sectors(monkeypatch):
     fp = P.full9_problem(nt).replace(projector=P0)
     X = np.stack([P.random_x(nt, 90 + s) for s in range(3)])
     sec, _, out, ref = _both(fp, X, monkeypatch)
-    assert sec == (4, 2)
+    assert sec == ((4, 1), (2, 2))
     _close(out, ref)
     fo = P.full9_problem(nt, device=False).replace(projector=P0)
     F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[1])[:2]
