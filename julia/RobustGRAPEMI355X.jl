@@ -30,7 +30,7 @@ struct GrapeDesc
     err_term_offsets::Ptr{Int32}; err_terms::Ptr{GrapeTerm}
     n_target_terms::Int32; target_terms::Ptr{GrapeTerm}
     max_batch::Int32; reserved::NTuple{5,Int32}
-    projector::Ptr{ComplexF64}   # ABI 4: full projector (column-major) or C_NULL (diagonal)
+    projector::Ptr{ComplexF64}   # ABI >= 4: full projector (column-major) or C_NULL (diagonal)
 end
 
 # the projector as the descriptor takes it: its diagonal, and the full matrix when P0 is not
@@ -303,6 +303,14 @@ function grape_expm_batch(As::Vector{Matrix{ComplexF64}}; device::Integer=0)
                      (Cint, Cint, Cint, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{Int32}), device, d, n, A, E, stats))
     end
     return [reshape(E[(k-1)*d*d+1:k*d*d], d, d) for k in 1:n], stats
+end
+
+"Sector layout of a plan's fidelity path (ABI 5): [(levels, sectors)] per class; [(ndim, 1)] = whole matrices."
+function plan_sectors(plan)
+    dims = zeros(Cint, 2); nsec = zeros(Cint, 2)
+    n = ccall((:grape_plan_sectors, libgrape), Cint, (Ptr{Cvoid}, Ptr{Cint}, Ptr{Cint}, Cint), plan.handle, dims, nsec, 2)
+    n < 0 && _check(n)
+    return [(Int(dims[c]), Int(nsec[c])) for c in 1:n]
 end
 
 end # module
