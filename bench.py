@@ -364,18 +364,47 @@ def whole_matrix_leg(fp, nparam, X, F, Fdx, L, stream, args):
             "note": "same workload with sectors disabled (GRAPE_NO_SECTORS=1): whole 9 x 9 matrices"}
 
 
-def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
+def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passes=None):
     # k_expm exponentiates every stored variant of every step: nominal, x + eps, x + eps2,
     # and per error source err(eps), err(eps2), (x + eps2, err eps2) -> 3 + 3 ne (Pade 5);
     # the x_add variants are skipped (H0 does not read x_add: their differences are exactly 0)
     nv = 3 + 3 * ne
-    # k_err_local: per step nz = np (1 + ne) + ne local-frame images, 2 complex d x d products
-    # each; k_err_grad: per (step, error) 2 products (the B_k recurrence, grape_errpath.hpp)
+    # k_err_local: per step nz = np (1 + ne) + ne local-frame images, 2 complex S x S products
+    # each; k_err_grad: per (step, error) 2 products (the B_k recurrence, grape_errpath.hpp).
+    # With sectors every item is one S x S sector, summed over the classes.
     nz = 1 * (1 + ne) + ne
-    prod = 8 * D ** 3
-    flop_model = {"k_expm": L * NT * nv * flops_expm(D), "k_grad/k_err_local": L * NT * nz * 2 * prod,
-                  "k_err_grad": L * NT * ne * 2 * prod}
-    kname = max(flop_model, key=lambda k: ktimes.get(k, (0.0, 0))[0])
+    classes = tuple(sectors) if sectors else ((D, 1),)
+    sec = classes[0][0] < D
+    per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
+    prod = lambda S: 8 * S ** 3  # noqa: E731
+    tile = lambda S: 16 * S * S  # noqa: E731
+    flop_model = {"k_expm": L * NT * nv * per_step(flops_expm),
+                  "k_grad/k_err_local": L * NT * nz * 2 * per_step(prod),
+                  "k_err_grad": L * NT * ne * 2 * per_step(prod)}
+    # algorithmic HBM bytes per pass: k_expm writes the nv variants; k_err_local reads them and
+    # Q_k, writes the nz images; k_err_grad reads W, Z1, Z2 per (step, error)
+    byte_model = {"k_expm": L * NT * nv * per_step(tile),
+                  "k_grad/k_err_local": L * NT * (nv + 1 + nz) * per_step(tile),
+                  "k_err_grad": L * NT * ne * 3 * per_step(tile)}
+    npass = passes or max(1, ktimes.get("k_expm", (0.0, 1))[1])
+    per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
+    kname = max(flop_model, key=lambda k: per_pass.get(k, 0.0))
+    ms = per_pass[kname]
+    fp = flop_model[kname] / (ms * 1e-3) / 1e12
+    hb = byte_model[kname] / (ms * 1e-3) / 1e9
+    short = {"k_grad/k_err_local": "k_err_local"}.get(kname, kname)
+    traffic = pmc_traffic(short, L, PMC_SUMMARY_C3)
+    if hb / HBM_PEAK_GBS > fp / FP64_PEAK_TFLOPS:
+        roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hb / HBM_PEAK_GBS}
+    else:
+        roof = {"bound": "mfma", "kernel": kname, "achieved": fp, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": fp / FP64_PEAK_TFLOPS, "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"}
+    roof.update({"traffic": traffic, "traffic_unit": "HBM bytes per device pass (PMC)", "per_launch_ms": ms,
+                 "per_launch_note": "per device pass of evals_per_device_pass evaluations (all sector classes)",
+                 "flop_per_launch": flop_model[kname], "algorithmic_bytes_per_launch": byte_model[kname],
+                 "fp64": {"achieved_TFLOPs": fp, "frac": fp / FP64_PEAK_TFLOPS},
+                 "hbm": {"achieved_GBs": hb, "frac": hb / HBM_PEAK_GBS}})
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+sensitivity+gradients), Rydberg CZ d=9 N_t=512, 4 error sources",
         "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
@@ -383,32 +412,38 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne):
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": "C3: Rydberg CZ d=9 + 4 error operators (Omega1, Omega2, delta1, delta2), N_t=512, "
                                "np=1, na=1; F, F_dx, F_d2err, F_d2err_dx",
-                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}"},
-        "roofline": dict(_roofline(kname, flop_model[kname], ktimes, L, PMC_SUMMARY_C3),
-                         pipe="fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"),
+                   "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
+                   "sectors": [{"levels": S, "sectors": ns} for S, ns in classes] if sec else None},
+        "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
-    # SURVEY.md 8d canonical C3 figure: 352.7 MFLOP per evaluation
+    # SURVEY.md 8d canonical (whole-matrix) C3 figure: 352.7 MFLOP per evaluation
     canon = NT * (1 + 2 + 2 + ne * (2 + 1 + 1)) * flops_expm(D) + 3 * NT * 8 * D ** 3 \
         + 4 * NT * ne * 8 * D ** 3 + 8 * D ** 2 * NT * 2 * (1 + ne)
     # FLOP of the work executed per evaluation: the stored variant exps, the nominal chain,
-    # the local-frame images, the B_k recurrence and the contractions
-    exe = NT * (nv * flops_expm(D) + prod + nz * 2 * prod + ne * 2 * prod + 8 * D ** 2 * (1 + ne))
+    # the local-frame images, the B_k recurrence and the contractions (+ the sector heads)
+    exe = NT * per_step(lambda S: nv * flops_expm(S) + prod(S) + nz * 2 * prod(S) + ne * 2 * prod(S)
+                        + 8 * S ** 2 * (1 + ne))
+    if sec:
+        exe += (16 + 24 * ne) * 8 * D ** 3
     out["roofline"]["whole_eval"] = {"flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
                                      "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
-                                     "flop_per_eval_survey": canon, "achieved_survey": canon * value / 1e12,
-                                     "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS}
-    out["kernels_frac"] = _kernel_fracs(flop_model, ktimes)
-    # the error-path kernels stream the stored variants and local-frame images: their bound is
-    # HBM (PMC bytes per launch from the committed C3 summary over the mean launch time)
+                                     "flop_per_eval_survey": canon}
+    if not sec:
+        out["roofline"]["whole_eval"].update({"achieved_survey": canon * value / 1e12,
+                                              "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS})
+    out["kernels_frac"] = {k: f / (per_pass[k] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS
+                           for k, f in flop_model.items() if per_pass.get(k)}
+    out["kernels_hbm_frac"] = {k: f / (per_pass[k] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                               for k, f in byte_model.items() if per_pass.get(k)}
+    # PMC bytes of the error-path kernels (committed C3 summary) over their per-pass time
     hbm = {}
-    for k, short in (("k_grad/k_err_local", "k_err_local"), ("k_err_grad", "k_err_grad"),
-                     ("k_err_scan", "k_err_scan"), ("k_scan", "k_scan")):
-        ms, n = ktimes.get(k, (0.0, 0))
-        t = pmc_traffic(short, L, PMC_SUMMARY_C3)
-        if n and ms > 0 and t:
-            gbs = t / (ms / n * 1e-3) / 1e9
-            hbm[short] = {"traffic_bytes": t, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
+    for k, sh in (("k_grad/k_err_local", "k_err_local"), ("k_err_grad", "k_err_grad"),
+                  ("k_err_scan", "k_err_scan"), ("k_scan", "k_scan")):
+        t = pmc_traffic(sh, L, PMC_SUMMARY_C3)
+        if per_pass.get(k) and t:
+            gbs = t / (per_pass[k] * 1e-3) / 1e9
+            hbm[sh] = {"traffic_bytes": t, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
     out["kernels_hbm"] = hbm
     return out
 
@@ -685,7 +720,8 @@ def main():
         elif c5:
             out = c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam)
         elif c3:
-            out = c3_report(args, B, L, world, value, elapsed, ktimes, ne)
+            out = c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors,
+                            args.steps * ((count + L - 1) // L))
         else:
             out = c2_report(args, B, L, world, value, elapsed, ktimes, sectors,
                             args.steps * ((count + L - 1) // L))

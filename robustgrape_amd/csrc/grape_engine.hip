@@ -162,6 +162,9 @@ struct grape_plan {
            *ops = nullptr, *opsT = nullptr, *Msec = nullptr;
         int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr;
         double *part = nullptr;
+        // error sources: local-frame images, per-chunk triples, Tot / M_e blocks, F_d2err_dx terms
+        cd *Zl = nullptr, *Me = nullptr, *TotS = nullptr, *MsecE = nullptr;
+        double *part_err = nullptr;
     };
     int ncls = 0;
     DevProblem Ps[2]{};
@@ -224,7 +227,8 @@ static void free_plan(grape_plan *p) {
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
-        void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part};
+        void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part,
+                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err};
         for (void *b : sbufs)
             if (b) (void)hipFree(b);
     }
@@ -432,7 +436,7 @@ static long sector_cost(const SectorClass &c) { return (long)c.nsec * c.S * c.S 
 static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
     SectorSetup ss;
     const int D = desc->ndim;
-    if (tables || desc->nerr > 0 || D > GRAPE_MAX_SMALL_DIM) return ss;
+    if (tables || D > GRAPE_MAX_SMALL_DIM) return ss;
     if (const char *e = std::getenv("GRAPE_NO_SECTORS"))
         if (std::atoi(e) != 0) return ss;
     std::vector<int> parent(D);
@@ -441,21 +445,21 @@ static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
         while (parent[i] != i) i = parent[i] = parent[parent[i]];
         return i;
     };
-    for (int t = 0; t < desc->n_h0_terms; ++t) {
-        const double *op = desc->ops + 2 * (size_t)desc->h0_terms[t].op * D * D;
+    // every operator the propagators use: H0's and the error sources'
+    std::vector<int> used;
+    for (int t = 0; t < desc->n_h0_terms; ++t) used.push_back(desc->h0_terms[t].op);
+    const int n_err_terms = desc->nerr > 0 ? desc->err_term_offsets[desc->nerr] : 0;
+    for (int t = 0; t < n_err_terms; ++t) used.push_back(desc->err_terms[t].op);
+    std::vector<char> diag(D, 0);  // level with a nonzero diagonal entry in some operator
+    for (int o : used) {
+        const double *op = desc->ops + 2 * (size_t)o * D * D;
         for (int c = 0; c < D; ++c)
             for (int r = 0; r < D; ++r) {
                 const double *v = op + 2 * ((size_t)r + (size_t)c * D);
-                if (v[0] != 0.0 || v[1] != 0.0) parent[root(r)] = root(c);
+                if (v[0] == 0.0 && v[1] == 0.0) continue;
+                parent[root(r)] = root(c);
+                if (r == c) diag[r] = 1;
             }
-    }
-    std::vector<char> diag(D, 0);  // level with a nonzero diagonal entry in some operator
-    for (int t = 0; t < desc->n_h0_terms; ++t) {
-        const double *op = desc->ops + 2 * (size_t)desc->h0_terms[t].op * D * D;
-        for (int i = 0; i < D; ++i) {
-            const double *v = op + 2 * ((size_t)i + (size_t)i * D);
-            if (v[0] != 0.0 || v[1] != 0.0) diag[i] = 1;
-        }
     }
     std::vector<std::vector<int>> comps;
     std::vector<int> slot(D, -1), fixed;
@@ -827,10 +831,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (ok && (P.ne > 0 || ps.general))  // carries and U: the error path and the general-projector heads
         ok = dalloc(&p->d_Carry, FR * P.nchunks * T) == hipSuccess && dalloc(&p->d_Ub, FR * T) == hipSuccess;
     if (ok && P.ne > 0)
-        ok = dalloc(&p->d_Me, MB * P.ne * P.nchunks * 3 * T) == hipSuccess &&
+        ok = dalloc(&p->d_Me, FR * P.ne * P.nchunks * 3 * T) == hipSuccess &&
              dalloc(&p->d_Fd2, MB * P.ne) == hipSuccess && dalloc(&p->d_Fd2dx, MB * P.ne * P.nx) == hipSuccess &&
              dalloc(&p->d_err, (size_t)n_err_terms) == hipSuccess && dalloc(&p->d_err_off, (size_t)P.ne + 1) == hipSuccess;
-    if (ok && P.ne > 0) ok = dalloc(&p->d_Zl, MB * P.Nt * P.nz * T) == hipSuccess;
+    if (ok && P.ne > 0) ok = dalloc(&p->d_Zl, FR * P.Nt * P.nz * T) == hipSuccess;
     if (ok && P.ne > 0 && P.xadd_dep)
         ok = dalloc(&p->d_part_err, MB * P.ne * P.Nt * P.na) == hipSuccess;
     if (ok && tables)
@@ -905,13 +909,17 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
             grape_plan::SecBuf &b = p->sb[cl];
-            if (dalloc(&b.E, R * P.Nt * TS) != hipSuccess || dalloc(&b.Q, R * P.Nt * TS) != hipSuccess ||
+            const size_t ne = (size_t)P.ne, R2 = P.ne > 0 ? 0 : R;  // k_expm_grad parking: no error sources only
+            if (dalloc(&b.E, R * P.Nt * P.nv * TS) != hipSuccess || dalloc(&b.Q, R * P.Nt * TS) != hipSuccess ||
                 dalloc(&b.Mc, R * Ps.nchunks * TS) != hipSuccess || dalloc(&b.Carry, R * Ps.nchunks * TS) != hipSuccess ||
                 dalloc(&b.Ub, R * TS) != hipSuccess || dalloc(&b.Msec, R * TS) != hipSuccess ||
-                dalloc(&b.slots, R * P.Nt * nvg * TS) != hipSuccess || dalloc(&b.ovf, R * P.Nt) != hipSuccess ||
-                dalloc(&b.ovf2, R * P.Nt * nvg) != hipSuccess || dalloc(&b.part, R * P.Nt * nvg) != hipSuccess ||
+                dalloc(&b.slots, R2 * P.Nt * nvg * TS) != hipSuccess || dalloc(&b.ovf, R * P.Nt * P.nv) != hipSuccess ||
+                dalloc(&b.ovf2, R2 * P.Nt * nvg) != hipSuccess || dalloc(&b.part, R * P.Nt * nvg) != hipSuccess ||
                 dalloc(&b.sidx, sc.sidx.size()) != hipSuccess || dalloc(&b.ops, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
-                dalloc(&b.opsT, (size_t)sc.nsec * n_ops * TS) != hipSuccess)
+                dalloc(&b.opsT, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
+                dalloc(&b.Zl, R * P.Nt * (ne ? P.nz : 0) * TS) != hipSuccess ||
+                dalloc(&b.Me, R * ne * Ps.nchunks * 3 * TS) != hipSuccess || dalloc(&b.TotS, R * ne * TS) != hipSuccess ||
+                dalloc(&b.MsecE, R * ne * TS) != hipSuccess || dalloc(&b.part_err, R * ne * P.Nt * nvg) != hipSuccess)
                 return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
             std::vector<cd> sops((size_t)sc.nsec * n_ops * TS), sopsT(sops.size());
             for (int w = 0; w < sc.nsec; ++w)
@@ -935,6 +943,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             H.sidx[cl] = b.sidx;
             H.Ub[cl] = b.Ub;
             H.Msec[cl] = b.Msec;
+            H.TotS[cl] = b.TotS;
+            H.MsecE[cl] = b.MsecE;
         }
         p->ncls = (int)ss.cls.size();
     }
@@ -1033,12 +1043,23 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.ovf2 = sb.ovf2;
             B.ovf2_slots = sb.slots;
             B.sec_part = sb.part;
+            B.Fd2 = d_Fd2;
+            B.Fd2dx = d_Fd2dx;
+            B.part_err_add = p->d_part_err;
+            if (p->P.ne > 0) {
+                B.Zl = sb.Zl;
+                B.Me = sb.Me;
+                B.TotS = sb.TotS;
+                B.MsecE = sb.MsecE;
+                B.sec_part_err = sb.part_err;
+            }
             B.overflow_count = p->d_ctrl + 4 + 2 * cl;  // ctrl [4..7]: two counters per class
             B.ovf2_count = p->d_ctrl + 5 + 2 * cl;
             B.status = p->d_ctrl + 2;
             B.sink = p->d_sink;
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
+            sp.part_err[cl] = sb.part_err;
         }
         HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));
         for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 0, p->Ps[cl], Bc[cl], st, mk));
@@ -1047,10 +1068,19 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         H.F = d_F;
         H.Fdx = d_Fdx;
         H.tgt_part = p->d_tgt_part;
+        H.Fd2 = d_Fd2;
+        H.Fd2dx = d_Fd2dx;
         mk(GRAPE_KERNEL_SCAN, 0);
         HIPCHECK(grape_proj::launch_sector_head(H, nb, st));
         mk(GRAPE_KERNEL_SCAN, 1);
         for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 1, p->Ps[cl], Bc[cl], st, mk));
+        if (p->P.ne > 0) {  // the sector error head, then the F_d2err_dx walks of every class
+            mk(GRAPE_KERNEL_ERR_SCAN, 0);
+            HIPCHECK(grape_proj::launch_sector_err_head(H, nb, st));
+            mk(GRAPE_KERNEL_ERR_SCAN, 1);
+            for (int cl = 0; cl < p->ncls; ++cl)
+                HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 2, p->Ps[cl], Bc[cl], st, mk));
+        }
         HIPCHECK(dispatch_sector_reduce(p->Ps[0].D, p->Ps[0], Bc[0], sp, nb, st, mk));
         return GRAPE_OK;
     }

@@ -88,9 +88,16 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
         if (doit) tile_store_row(G, x, true);
         gsync();
     }
+    const cd *Tot = tile_of(P.nchunks - 1);
+    if (P.sectors) {  // the sector error head forms F_d2err and M_e from the assembled U and Tot
+        if (c == P.nchunks - 1 && G.lane_ok) {
+            cd *dt = B.TotS + ((size_t)b * P.ne + e) * TILE + i * D;
+#pragma unroll
+            for (int jj = 0; jj < D; ++jj) dt[jj] = Tot[i * D + jj];
+        }
+    } else {
     // Phase C (group 0): Ue = U Tot, F_d2err, M_e = G_e U, target x_add part
     const bool f0 = (c == 0) && G.lane_ok;
-    const cd *Tot = tile_of(P.nchunks - 1);
     const cd *Ub = B.Ub + (size_t)b * TILE;
     const double *xb = B.x + (size_t)b * P.nx;
     const double *xadd = xb + (size_t)P.np * P.Nt;
@@ -195,7 +202,9 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
         gsync();
     }
     if (f0 && i == 0) B.Fd2[(size_t)b * P.ne + e] = fd2;
-    // Phase D: per chunk M' = Carry M_e Carry^dag, T = Carry Sc Carry^dag, Ttot = Carry Tot Carry^dag
+    }  // Phase C
+    // Phase D: per chunk M' = Carry M_e Carry^dag (sectors: k_sec_mc_err, after the head),
+    // T = Carry Sc Carry^dag, Ttot = Carry Tot Carry^dag
     cd sc[D], tot[D], cr[D];
 #pragma unroll
     for (int jj = 0; jj < D; ++jj) {
@@ -207,11 +216,13 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
     tile_store_row(G, cr, gvalid);  // own tile <- Carry_c
     gsync();
     cd *Mo = B.Me + (((size_t)b * P.ne + e) * P.nchunks + (gvalid ? c : 0)) * 3 * TILE;
-    mm_tile<D>(cr, S4, x);
-    mm_tile<D, true, true>(x, G.tile, w);  // M'
-    if (gvalid) {
+    if (!P.sectors) {
+        mm_tile<D>(cr, S4, x);
+        mm_tile<D, true, true>(x, G.tile, w);  // M'
+        if (gvalid) {
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) Mo[i * D + jj] = w[jj];
+            for (int jj = 0; jj < D; ++jj) Mo[i * D + jj] = w[jj];
+        }
     }
     // T and Ttot: (X Carry^dag) to global scratch, then Carry * that
     for (int which = 0; which < 2; ++which) {
@@ -306,7 +317,8 @@ __global__ __launch_bounds__(64, 2) void k_err_local(DevProblem P, DevBatch B) {
         }
         s = group_sum(G, s, valid);
         if (valid && i == 0) {
-            if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+            if (B.sec_part) B.sec_part[((size_t)b * P.Nt + k) * P.nvg + u] = s;  // sector term (k_sec_reduce)
+            else if (u < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
             else B.part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
         }
     }
@@ -397,7 +409,8 @@ __global__ __launch_bounds__(64, 2) void k_err_grad(DevProblem P, DevBatch B) {
             }
             s = group_sum(G, s, valid);
             if (act && i == 0) {
-                if (u < P.np) out[(size_t)k * P.np + u] = s;
+                if (B.sec_part_err) B.sec_part_err[(((size_t)b * P.ne + e) * P.Nt + k) * P.nvg + u] = s;
+                else if (u < P.np) out[(size_t)k * P.np + u] = s;
                 else B.part_err_add[(((size_t)b * P.ne + e) * P.Nt + k) * P.na + (u - P.np)] = s;
             }
         }

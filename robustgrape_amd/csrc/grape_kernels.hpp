@@ -120,6 +120,10 @@ struct DevBatch {
     cd *gp_scr;             // general projector: head scratch (grape_projector_api.hpp)
     double *sec_part;       // sectors: [nb][Nt][nvg] per-sector F_dx terms (k_sec_reduce sums them), else null
     const cd *Msec;         // sectors: [nb][D][D] the sector blocks of M = G U (the sector head)
+    // sectors with error sources
+    double *sec_part_err;   // [nb][ne][Nt][nvg] per-sector F_d2err_dx terms (k_sec_reduce_err sums them)
+    cd *TotS;               // [nb][ne][D][D] the sector blocks of Tot = sum_k V^err_k (k_err_scan)
+    const cd *MsecE;        // [nb][ne][D][D] the sector blocks of M_e = G_e U (the sector error head)
 };
 
 __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,
@@ -882,11 +886,42 @@ __global__ void k_sec_mc(DevProblem P, DevBatch B) {
     B.Mc[(size_t)t] = acc;
 }
 
+// Sectors with error sources: M'_{c,e} = Carry_c M_e,ww Carry_c^dagger into slot 0 of the error
+// path's per-chunk triple (k_err_scan wrote T_c and Ttot_c), one thread per element.
+template <int D>
+__global__ void k_sec_mc_err(DevProblem P, DevBatch B) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)B.nb * P.ne * P.nchunks * D * D) return;
+    const int j = (int)(t % D), i = (int)((t / D) % D);
+    const long bec = t / (D * D);  // (b' * ne + e) * nchunks + c
+    const int c = (int)(bec % P.nchunks);
+    const long be = bec / P.nchunks;
+    const int b = (int)(be / P.ne);
+    const cd *C = B.Carry + ((size_t)b * P.nchunks + c) * D * D;
+    const cd *Mw = B.MsecE + (size_t)be * D * D;
+    cd ci[D], cj[D];
+#pragma unroll
+    for (int e = 0; e < D; ++e) {
+        ci[e] = C[i * D + e];
+        cj[e] = cconj(C[j * D + e]);
+    }
+    cd acc = czero();
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        cd r = czero();
+#pragma unroll
+        for (int e = 0; e < D; ++e) r = cadd(r, cmul(Mw[a * D + e], cj[e]));
+        acc = cadd(acc, cmul(ci[a], r));
+    }
+    B.Me[(size_t)bec * 3 * D * D + i * D + j] = acc;
+}
+
 // Sectors: F_dx[b][k, u] (or the per-step x_add term) = sum over the evaluation's sectors of
 // both classes, in sector order (deterministic).  One thread per (b, k, u).
 struct SecParts {
-    const double *part[2];  // [nb][nsec_c][Nt][nvg] per sector class
-    int nsec[2];            // 0 for an absent class
+    const double *part[2];      // [nb][nsec_c][Nt][nvg] per sector class
+    const double *part_err[2];  // [nb][nsec_c][ne][Nt][nvg] (error sources)
+    int nsec[2];                // 0 for an absent class
 };
 template <int D>
 __global__ void k_sec_reduce(DevProblem P, double *Fdx, double *part_add, SecParts S, int nb) {
@@ -901,6 +936,24 @@ __global__ void k_sec_reduce(DevProblem P, double *Fdx, double *part_add, SecPar
         for (int w = 0; w < S.nsec[c]; ++w) s += S.part[c][((size_t)b * S.nsec[c] + w) * per + r];
     if (u < P.np) Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
     else part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
+}
+
+// The same for F_d2err_dx (or its per-step x_add term), one thread per (b, e, k, u).
+template <int D>
+__global__ void k_sec_reduce_err(DevProblem P, double *Fd2dx, double *part_err_add, SecParts S, int nb) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per = (long)P.Nt * P.nvg;
+    if (t >= (long)nb * P.ne * per) return;
+    const long be = t / per;  // b * ne + e
+    const int b = (int)(be / P.ne), e = (int)(be - (long)b * P.ne);
+    const long r = t - be * per;
+    const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
+    double s = 0.0;
+    for (int c = 0; c < 2; ++c)
+        for (int w = 0; w < S.nsec[c]; ++w)
+            s += S.part_err[c][(((size_t)b * S.nsec[c] + w) * P.ne + e) * per + r];
+    if (u < P.np) Fd2dx[(size_t)be * P.nx + (size_t)k * P.np + u] = s;
+    else part_err_add[((size_t)be * P.Nt + k) * P.na + (u - P.np)] = s;
 }
 
 }  // namespace grape

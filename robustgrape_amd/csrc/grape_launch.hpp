@@ -136,19 +136,26 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
 }
 
 // Sectors (P.sectors, D = the sector size of one class, B.nb = evaluations x nsec).  Stage 0:
-// nominal sector propagators -> sector scans (U_w, carries).  Then (grape_engine.hip) the
-// sector head over every class (F, the blocks of M, target part).  Stage 1: per-chunk images
-// M'_c (k_sec_mc) -> eps-variant sector exps contracted in place.  Then k_sec_reduce sums the
-// per-step F_dx terms over the sectors of every class [-> the x_add sum over steps].
+// nominal sector propagators (every variant with error sources) -> sector scans (U_w,
+// carries).  Then (grape_engine.hip) the sector head over every class (F, the blocks of M,
+// target part).  Stage 1: per-chunk images M'_c (k_sec_mc), then without error sources the
+// eps-variant sector exps contracted in place, with error sources the local-frame images (and
+// F_dx terms) and the sector error scans (Tot blocks, T_c, Ttot_c).  Then the sector error
+// head (F_d2err, the blocks of M_e).  Stage 2 (error sources): M'_{c,e} (k_sec_mc_err) and
+// the F_d2err_dx walks.  Finally launch_sector_reduce sums the sector terms.
 template <int D>
 hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B, hipStream_t st,
                                const KMark &mark) {
     constexpr int GPW = grape::Geo<D>::GPW;
     if (stage == 0) {
-        const long nexp = (long)B.nb * P.Nt;
+        const long nexp = (long)B.nb * P.Nt * P.nv;
         mark(GRAPE_KERNEL_EXPM, 0);
-        hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
-                           expm_lean_lds<D>(), st, P, B);
+        if (P.ne > 0)
+            hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                               expm_lean_lds<D>(), st, P, B);
+        else
+            hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
+                               expm_lean_lds<D>(), st, P, B);
         mark(GRAPE_KERNEL_EXPM, 1);
         mark(GRAPE_KERNEL_EXPM_HIGH, 0);
         hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
@@ -164,18 +171,45 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
         mark(GRAPE_KERNEL_SCAN, 1);
         return hipGetLastError();
     }
-    mark(GRAPE_KERNEL_REDUCE, 0);
-    const long nmc = (long)B.nb * P.nchunks * D * D;
-    hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
-    mark(GRAPE_KERNEL_REDUCE, 1);
-    const long ng = (long)B.nb * P.Nt * P.nvg;
-    mark(GRAPE_KERNEL_EXPM_GRAD, 0);
-    hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64), expm_lean_lds<D>(),
-                       st, P, B);
-    mark(GRAPE_KERNEL_EXPM_GRAD, 1);
-    mark(GRAPE_KERNEL_GRAD_HIGH, 0);
-    hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
-    mark(GRAPE_KERNEL_GRAD_HIGH, 1);
+    if (stage == 1) {
+        mark(GRAPE_KERNEL_REDUCE, 0);
+        const long nmc = (long)B.nb * P.nchunks * D * D;
+        hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
+        mark(GRAPE_KERNEL_REDUCE, 1);
+        if (P.ne > 0) {
+            const long ng = (long)B.nb * P.Nt;
+            mark(GRAPE_KERNEL_GRAD, 0);
+            hipLaunchKernelGGL(grape::k_err_local<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64),
+                               errpath_lds<D>(), st, P, B);
+            mark(GRAPE_KERNEL_GRAD, 1);
+            mark(GRAPE_KERNEL_ERR_SCAN, 0);
+            if (P.scan_waves == kScanNarrow)
+                hipLaunchKernelGGL((grape::k_err_scan<D, kScanNarrow>), dim3(B.nb * P.ne), dim3(64 * kScanNarrow),
+                                   errscan_lds<D>(kScanNarrow), st, P, B);
+            else
+                hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
+                                   errscan_lds<D>(kScanWide), st, P, B);
+            mark(GRAPE_KERNEL_ERR_SCAN, 1);
+            return hipGetLastError();
+        }
+        const long ng = (long)B.nb * P.Nt * P.nvg;
+        mark(GRAPE_KERNEL_EXPM_GRAD, 0);
+        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64),
+                           expm_lean_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_EXPM_GRAD, 1);
+        mark(GRAPE_KERNEL_GRAD_HIGH, 0);
+        hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
+        mark(GRAPE_KERNEL_GRAD_HIGH, 1);
+        return hipGetLastError();
+    }
+    // stage 2 (error sources)
+    mark(GRAPE_KERNEL_ERR_GRAD, 0);
+    const long nmce = (long)B.nb * P.ne * P.nchunks * D * D;
+    hipLaunchKernelGGL(grape::k_sec_mc_err<D>, dim3((unsigned)((nmce + 255) / 256)), dim3(256), 0, st, P, B);
+    const long ne_items = (long)B.nb * P.nchunks * P.ne;
+    hipLaunchKernelGGL(grape::k_err_grad<D>, dim3((unsigned)((ne_items + GPW - 1) / GPW)), dim3(64),
+                       errpath_lds<D>(), st, P, B);
+    mark(GRAPE_KERNEL_ERR_GRAD, 1);
     return hipGetLastError();
 }
 
@@ -187,10 +221,14 @@ hipError_t launch_sector_reduce(const DevProblem &P, const DevBatch &B, const gr
     const long nred = (long)nev * P.Nt * P.nvg;
     hipLaunchKernelGGL(grape::k_sec_reduce<D>, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, st, P, B.Fdx,
                        B.part_add, S, nev);
+    if (P.ne > 0)
+        hipLaunchKernelGGL(grape::k_sec_reduce_err<D>, dim3((unsigned)((nred * P.ne + 255) / 256)), dim3(256), 0, st,
+                           P, B.Fd2dx, B.part_err_add, S, nev);
     if (P.xadd_dep && P.na > 0) {
         DevBatch Be = B;  // the x_add sums run over evaluations, not sub-evaluations
         Be.nb = nev;
-        hipLaunchKernelGGL(grape::k_reduce_add<D>, dim3((nev * P.na + 255) / 256), dim3(256), 0, st, P, Be);
+        const int nr = nev * P.na * (1 + P.ne);
+        hipLaunchKernelGGL(grape::k_reduce_add<D>, dim3((nr + 255) / 256), dim3(256), 0, st, P, Be);
     }
     mark(GRAPE_KERNEL_REDUCE, 1);
     return hipGetLastError();

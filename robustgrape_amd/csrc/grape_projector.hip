@@ -375,7 +375,105 @@ __global__ __launch_bounds__(SEC_BLOCK) void k_sec_head(SectorHead H) {
     }
 }
 
+// Sector error head, (b, e) = (blockIdx.x / ne, blockIdx.x % ne): k_proj_err's formulas over
+// U and Tot assembled from the sector blocks (Tot is zero on the untouched levels).
+enum { E_U, E_U0, E_K, E_X, E_T1, E_T2, E_T3, E_M, E_UE, E_KE, E_XE, E_YE, E_TOT, kErrHeadSlots };
+__global__ __launch_bounds__(SEC_BLOCK) void k_sec_err_head(SectorHead H) {
+    __shared__ double red[SEC_BLOCK];
+    extern __shared__ __attribute__((aligned(16))) unsigned char sec_smem[];
+    const grape::DevProblem &P = H.P;
+    const int D = P.D, ne = P.ne, b = blockIdx.x / ne, e = blockIdx.x % ne;
+    const size_t T = (size_t)D * D, be = (size_t)b * ne + e;
+    cd *s = reinterpret_cast<cd *>(sec_smem);
+    cd *U = s + E_U * T, *U0 = s + E_U0 * T, *K = s + E_K * T, *X = s + E_X * T;
+    cd *T1 = s + E_T1 * T, *T2 = s + E_T2 * T, *T3 = s + E_T3 * T, *M = s + E_M * T;
+    cd *Ue = s + E_UE * T, *Ke = s + E_KE * T, *Xe = s + E_XE * T, *Ye = s + E_YE * T, *Tot = s + E_TOT * T;
+    const cd *A = P.PA, *Bm = P.PB;
+    const double *xb = H.x + (size_t)b * P.nx;
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) U[t] = Tot[t] = cd{0.0, 0.0};
+    __syncthreads();
+    for (int cl = 0; cl < H.ncls; ++cl) {
+        const int S = H.S[cl], SS = S * S, ns = H.nsec[cl];
+        for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
+            const int w = t / SS, r = (t % SS) / S, c = t % S;
+            const int gi = H.sidx[cl][w * S + r], gj = H.sidx[cl][w * S + c];
+            if (gi < 0 || gj < 0) continue;
+            const size_t bw = (size_t)b * ns + w;
+            U[(size_t)gi * D + gj] = H.Ub[cl][bw * SS + r * S + c];
+            Tot[(size_t)gi * D + gj] = H.TotS[cl][(bw * ne + e) * SS + r * S + c];
+        }
+    }
+    for (int t = threadIdx.x; t < H.nfixed; t += blockDim.x) {
+        const int g = H.fixed[t];
+        U[(size_t)g * D + g] = cd{1.0, 0.0};
+    }
+    __syncthreads();
+    build_target(P, nullptr, b, xb, 0, U0);
+    bmm<false, false>(Ue, U, Tot, D);  // U_derr = U Tot                (UnitaryCalculations.jl:122-123)
+    bmm<true, false>(Ke, U0, Ue, D);
+    bmm<true, false>(K, U0, U, D);
+    bmm<false, false>(Xe, A, Ke, D);
+    const cd te = btrace<SEC_BLOCK>(Xe, D, red);
+    bmm<false, false>(Ye, Xe, Bm, D);
+    const double t1 = bdot<SEC_BLOCK>(Ye, Ke, D, red);
+    bmm<true, false>(T1, Ue, Ue, D);
+    double tr = 0.0;  // Re tr(A Ue^dag Ue)
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) {
+        const int i = t / D, j = t % D;
+        const cd a = A[t], bb = T1[(size_t)j * D + i];
+        tr += a.re * bb.re - a.im * bb.im;
+    }
+    const double t2 = bsum<SEC_BLOCK>(tr, red);
+    const double fd2 = 2.0 * (t1 - (1.0 + P.Dtr) * t2 + te.re * te.re + te.im * te.im) / P.DD;
+    bmm<false, false>(X, A, K, D);
+    bmm<true, false>(T1, Ke, X, D);
+    bmm<false, false>(M, Bm, T1, D);
+    bmm<true, false>(T1, Xe, K, D);
+    bmm<true, false>(T2, Bm, T1, D);
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x) {
+        M[t] = p_add(p_add(M[t], T2[t]), p_scale(2.0, p_mul(cd{te.re, -te.im}, X[t])));
+        const int i = t / D, j = t % D;
+        T2[t] = p_add(A[t], p_conj(A[(size_t)j * D + i]));  // A + A^dagger
+    }
+    __syncthreads();
+    bmm<true, false>(T1, Ue, U, D);
+    bmm<false, false>(T3, T2, T1, D);
+    for (int t = threadIdx.x; t < (int)T; t += blockDim.x)
+        M[t] = p_scale(2.0 / P.DD, p_sub(M[t], p_scale(1.0 + P.Dtr, T3[t])));
+    __syncthreads();
+    for (int q = 0; q < P.na; ++q) {  // target part of F_d2err_dx_add
+        build_target(P, nullptr, b, xb, 1 + q, T1);
+        for (int t = threadIdx.x; t < (int)T; t += blockDim.x) T1[t] = p_scale(P.inv_eps, p_sub(T1[t], U0[t]));
+        __syncthreads();
+        bmm<true, false>(T2, T1, Ue, D);  // Kde
+        bmm<false, false>(T1, A, T2, D);
+        const cd trd = btrace<SEC_BLOCK>(T1, D, red);
+        bmm<false, false>(T3, T1, Bm, D);
+        const double sa = bdot<SEC_BLOCK>(T3, Ke, D, red), sb = bdot<SEC_BLOCK>(Ye, T2, D, red);
+        const double val = 2.0 * (sa + sb + 2.0 * (te.re * trd.re + te.im * trd.im)) / P.DD;
+        if (threadIdx.x == 0) H.Fd2dx[be * P.nx + (size_t)P.np * P.Nt + q] = val;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) H.Fd2[be] = fd2;
+    for (int cl = 0; cl < H.ncls; ++cl) {  // the sector blocks of M_e
+        const int S = H.S[cl], SS = S * S, ns = H.nsec[cl];
+        for (int t = threadIdx.x; t < ns * SS; t += blockDim.x) {
+            const int w = t / SS, r = (t % SS) / S, c = t % S;
+            const int gi = H.sidx[cl][w * S + r], gj = H.sidx[cl][w * S + c];
+            H.MsecE[cl][(((size_t)b * ns + w) * ne + e) * SS + r * S + c] =
+                (gi >= 0 && gj >= 0) ? M[(size_t)gi * D + gj] : cd{0.0, 0.0};
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
+    if (H.P.ne == 0) return hipSuccess;
+    const size_t lds = (size_t)kErrHeadSlots * H.P.D * H.P.D * sizeof(cd);
+    hipLaunchKernelGGL(k_sec_err_head, dim3((unsigned)(nb * H.P.ne)), dim3(SEC_BLOCK), lds, st, H);
+    return hipGetLastError();
+}
 
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st) {
     const size_t lds = (size_t)kHeadSlots * H.P.D * H.P.D * sizeof(cd);

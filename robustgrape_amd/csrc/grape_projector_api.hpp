@@ -47,13 +47,20 @@ struct SectorHead {
     const int *sidx[2];       // [nsec][S]: level of each sector slot (-1: padding)
     const grape::cd *Ub[2];   // [nb * nsec][S][S]
     grape::cd *Msec[2];       // [nb * nsec][S][S]  (written)
-    const int *fixed;         // levels no operator touches (identity in U)
+    const int *fixed;         // levels no operator touches (identity in U, zero in Tot)
     int nfixed;
     const double *x;          // [nb][nx]
     double *F, *Fdx, *tgt_part;
+    // error sources: the sector blocks of Tot (k_err_scan) in, F_d2err, the target part of
+    // F_d2err_dx_add and the sector blocks of M_e out
+    const grape::cd *TotS[2]; // [nb * nsec][ne][S][S]
+    grape::cd *MsecE[2];      // [nb * nsec][ne][S][S]  (written)
+    double *Fd2, *Fd2dx;
 };
 constexpr int kSectorLds = 2048;  // complex elements of LDS for the sector blocks M_ww (nsec * S * S)
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st);
+// one wave per (evaluation, error source): F_d2err, M_e blocks, F_d2err_dx_add target part
+hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st);
 
 // the small engine's view (grape_launch.hpp)
 inline Heads small_heads(const grape::DevProblem &P, const grape::DevBatch &B) {

@@ -72,12 +72,58 @@ def test_sectors_match_whole_matrices_and_oracle(name, fp, layout, monkeypatch):
         _close((out[0][b], out[1][b]), (F0, g0))
 
 
-def test_no_sectors_with_error_sources(monkeypatch):
-    pl = _plan(P.full9_problem(16, nerr=2), 2, monkeypatch)
-    try:
-        assert pl.sectors() == ((9, 1),)
-    finally:
-        pl.close()
+T3, T3_ABS = 1e-5, 1e-7      # eps2 mixed stencils (F_d2err_dx)
+
+
+def _close_err(a, b, label):
+    """F, F_dx, F_d2err, F_d2err_dx of two paths (T1, T2, T2, T3)."""
+    errs = {}
+    assert np.max(np.abs(a[0] - b[0])) <= T1
+    for n, (x, y, t, ta) in enumerate([(a[1], b[1], T2, T2_ABS), (a[2], b[2], T2, T2_ABS), (a[3], b[3], T3, T3_ABS)]):
+        err, scale = np.max(np.abs(x - y)), np.max(np.abs(y))
+        errs[("F_dx", "F_d2err", "F_d2err_dx")[n]] = f"{err:.2e}/{scale:.2e}"
+        assert err <= t * scale + ta, (label, n, err, scale)
+    print(label, errs)
+
+
+@pytest.mark.parametrize("name,fp,fo,layout", [
+    ("full9-C3", lambda: P.full9_problem(24, nerr=4), lambda: P.full9_problem(24, nerr=4, device=False),
+     ((4, 1), (2, 2))),
+    ("sym5-amp-freq", lambda: P.sym_problem(20, errors=("amp", "freq")),
+     lambda: P.sym_problem(20, errors=("amp", "freq"), device=False), ((2, 2),)),
+    ("fullblk7-amp", lambda: P.fullblk_problem(16, errors=("amp",)),
+     lambda: P.fullblk_problem(16, errors=("amp",), device=False), ((2, 3),)),
+])
+def test_sectors_with_error_sources(name, fp, fo, layout, monkeypatch):
+    """The error path on sectors: local-frame images, error scans and F_d2err_dx walks per
+    sector, F_d2err and M_e from the assembled U and Tot in the sector error head."""
+    from oracle import grape_oracle as O
+    f = fp()
+    nt = f.unitary_problem.ntimes
+    X = np.stack([P.random_x(nt, 300 + s) for s in range(4)])
+    sec, whole, out, ref = _both(f, X, monkeypatch)
+    assert sec == layout and whole[0][1] == 1
+    _close_err(out, ref, name + " vs whole")
+    o = O.calculate_fidelity_and_derivatives(fo(), X[1])
+    _close_err((out[0][1], out[1][1], out[2][1], out[3][1]), tuple(np.asarray(v) for v in o), name + " vs oracle")
+
+
+@pytest.mark.parametrize("d", [5, 9])
+def test_sectors_errors_xadd_and_general_projector(d, monkeypatch):
+    """Error sources with an x_add-dependent H0 / Herror (per-step x_add terms of F_dx and
+    F_d2err_dx summed over sectors and steps) and a general projector coupling sectors."""
+    from oracle import grape_oracle as O
+    nt = 12
+    rng = np.random.default_rng(d)
+    Qm, _ = np.linalg.qr(rng.standard_normal((d, 3)))
+    P0 = Qm @ Qm.T
+    fp = P.xadd_err_problem(d, nt, nerr=2).replace(projector=P0)
+    X = np.stack([P.xadd_x(nt, 400 + s) for s in range(3)])
+    sec, _, out, ref = _both(fp, X, monkeypatch)
+    assert sec[0][0] < d
+    _close_err(out, ref, f"xadd d={d} vs whole")
+    o = O.calculate_fidelity_and_derivatives(P.xadd_err_problem(d, nt, nerr=2, device=False).replace(projector=P0), X[0])
+    _close_err((out[0][0], out[1][0], out[2][0], out[3][0]), tuple(np.asarray(v) for v in o), f"xadd d={d} vs oracle")
 
 
 @pytest.mark.parametrize("d", [5, 9])
