@@ -265,7 +265,8 @@ __global__ __launch_bounds__(64, 2) void k_err_local(DevProblem P, DevBatch B) {
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
     const long gidc = valid ? gid : 0;
-    const int k = (int)(gidc % P.Nt), b = (int)(gidc / P.Nt);
+    int k, b, unused;
+    split_item(gidc, nitems, P.Nt, 1, b, unused, k);
     const int c = k / P.L;
     const bool first = k == c * P.L;  // chunk start: Q_{k-1} = I
     const int i = G.i;
@@ -352,9 +353,8 @@ __global__ __launch_bounds__(64, 2) void k_err_grad(DevProblem P, DevBatch B) {
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
     const long gc = valid ? gid : 0;
-    const int e = (int)(gc % P.ne);
-    const int c = (int)((gc / P.ne) % P.nchunks);
-    const int b = (int)(gc / ((long)P.ne * P.nchunks));
+    int e, c, b;
+    split_item(gc, nitems, P.ne, P.nchunks, b, c, e);
     const int i = G.i;
     const cd *Mo = B.Me + (((size_t)b * P.ne + e) * P.nchunks + c) * 3 * TILE;  // M', Tc, Ttot
     double *out = B.Fd2dx + ((size_t)b * P.ne + e) * P.nx;

@@ -259,6 +259,22 @@ struct ItemBuilder {
     }
 };
 
+// Item index -> (outer, mid, inner) for inner extent n1 and mid extent n2: 32-bit unsigned
+// divisions (a few instructions) whenever the launch's items fit in 32 bits -- a uniform branch --
+// instead of the 64-bit division sequence.
+__device__ __forceinline__ void split_item(long g, long nitems, int n1, int n2, int &outer, int &mid, int &inner) {
+    if (nitems <= 0xffffffffL) {
+        const unsigned u = (unsigned)g, t = u / (unsigned)n1;
+        inner = (int)(u - t * (unsigned)n1);
+        outer = (int)(t / (unsigned)n2);
+        mid = (int)(t - (unsigned)outer * (unsigned)n2);
+    } else {
+        inner = (int)(g % n1);
+        mid = (int)((g / n1) % n2);
+        outer = (int)(g / ((long)n1 * n2));
+    }
+}
+
 // Parks an item whose Pade degree is > 5: A (column i at slot + i*D) goes to
 // its output slot, the id to the list.
 template <int D>
@@ -283,9 +299,8 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_WAVES_D9 : 2)) void k_expm
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
     const long gidc = valid ? gid : 0;
-    const int v = (int)(gidc % P.nv);
-    const int k = (int)((gidc / P.nv) % P.Nt);
-    const int b = (int)(gidc / ((long)P.nv * P.Nt));
+    int v, k, b;
+    split_item(gidc, nitems, P.nv, P.Nt, b, k, v);
     const int ns = P.nsec > 1 ? P.nsec : 1, bx = b / ns;  // sectors: evaluation bx, sector b - bx * ns
     const double *xb = B.x + (size_t)bx * P.nx;
     const ItemBuilder<D, ERR> rebuild(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1, P.vs[v],
@@ -780,9 +795,8 @@ __global__ __launch_bounds__(64, (D <= 9 ? GRAPE_EXPM_GRAD_WAVES : 2)) void k_ex
     const long gid = (long)blockIdx.x * Geo<D>::GPW + G.g;
     const bool valid = G.lane_ok && gid < nitems;
     const long gidc = valid ? gid : 0;
-    const int u = (int)(gidc % nvg);
-    const int k = (int)((gidc / nvg) % P.Nt);
-    const int b = (int)(gidc / ((long)nvg * P.Nt));
+    int u, k, b;
+    split_item(gidc, nitems, nvg, P.Nt, b, k, u);
     const int ns = P.nsec > 1 ? P.nsec : 1, bx = b / ns;
     const double *xb = B.x + (size_t)bx * P.nx;
     const ItemBuilder<D, false> rebuild(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, G.i, k + 1,
