@@ -323,8 +323,8 @@ int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launc
  * contractions never leave the blocks, so grape_fidelity_grad runs each evaluation as
  * independent sector problems -- one or two classes of `nsectors[c]` sectors of `sector_dims[c]`
  * levels (blocks packed first-fit, padded with decoupled levels) -- and assembles U only for the
- * fidelity head.  Same outputs; no API change.  Chosen at plan creation for operator-basis
- * plans without error sources when it cuts the work at least in half; the environment
+ * fidelity (and error) heads.  Same outputs; no API change.  Chosen at plan creation for
+ * operator-basis plans (H0 and error operators) when it cuts the work at least in half; the environment
  * variable GRAPE_NO_SECTORS=1 turns it off.  Fills up to max_classes entries and returns the
  * number of classes; a plan that runs whole matrices reports one class (ndim, 1).
  */

@@ -401,8 +401,8 @@ static int upload_projector(grape_plan *p, const ProjectorSetup &ps, DevProblem 
 // less work (sum of nsec S^3), into two classes: the components above a size cut in sectors of
 // their largest size, the rest in sectors of theirs (d = 9 Rydberg: one sector of 4 and two of
 // 2 instead of two of 4).  sidx[w * S + a] = level in slot a of sector w, or -1 (padding: a
-// decoupled level, exp(0) = 1, never reaches F).  Only for operator-basis plans without error
-// sources (the error path keeps whole matrices), and only when the sector work is at most half
+// decoupled level, exp(0) = 1, never reaches F).  Only for operator-basis plans (the pattern
+// covers H0's and the error sources' operators), and only when the sector work is at most half
 // of d^3.
 struct SectorClass {
     int S = 0, nsec = 0;
