@@ -82,7 +82,7 @@ PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
 PMC_SUMMARY_C3 = os.path.join(ROOT, "profiles", "pmc_c3_latest.json")
 
 
-def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
+def pmc_traffic(kernel, batch, path=PMC_SUMMARY, dims=None):
     """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_profile.sh:
     separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), if it was
     recorded at this launch size (evaluations per device pass); else None."""
@@ -95,9 +95,17 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY):
         return None
     if js.get("batch") != batch:
         return None
-    # every instantiation of the kernel (the sector classes launch one each per device pass)
+    # every instantiation of the kernel (the sector classes launch one each per device pass),
+    # restricted to the template dimensions `dims` when given (the summary may also hold the
+    # whole-matrix leg's instantiation)
+    def dim(name):
+        try:
+            return int(name.split("<")[1].split(",")[0].split(">")[0])
+        except (IndexError, ValueError):
+            return None
     rows = [row["hbm_bytes_per_launch"] for name, row in js.get("kernels", {}).items()
-            if name.split("<")[0].split("::")[-1] == kernel and "hbm_bytes_per_launch" in row]
+            if name.split("<")[0].split("::")[-1] == kernel and "hbm_bytes_per_launch" in row
+            and (dims is None or dim(name) in dims)]
     return sum(rows) if rows else None
 
 
@@ -262,7 +270,7 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     ms = per_pass[kname]
     fp = flop_model[kname] / (ms * 1e-3) / 1e12
     hb = byte_model[kname] / (ms * 1e-3) / 1e9
-    traffic = pmc_traffic(kname, L)
+    traffic = pmc_traffic(kname, L, dims={S for S, _ in classes})
     fp_frac, hb_frac = fp / FP64_PEAK_TFLOPS, hb / HBM_PEAK_GBS
     if hb_frac > fp_frac:
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -317,7 +325,7 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     if per_pass.get("k_scan"):
         per_ms = per_pass["k_scan"]
         alg = byte_model["k_scan"]
-        pmc = pmc_traffic("k_scan", L)
+        pmc = pmc_traffic("k_scan", L, dims={S for S, _ in classes})
         out["roofline_scan"] = {"bound": "hbm", "kernel": "k_scan", "per_launch_ms": per_ms,
                                 "algorithmic_bytes": alg, "achieved": alg / (per_ms * 1e-3) / 1e9,
                                 "traffic": pmc, "achieved_traffic": (pmc / (per_ms * 1e-3) / 1e9) if pmc else None,
@@ -357,9 +365,11 @@ def whole_matrix_leg(fp, nparam, X, F, Fdx, L, stream, args):
     passes = steps * ((n + L - 1) // L)
     ms = kt["k_expm_grad"][0] / passes
     fl = L * NT * (flops_expm(D) + 2 * 8 * D ** 3 + 8 * D ** 2)
+    tr = pmc_traffic("k_expm_grad", L, dims={D})
     return {"value": steps * n / dt, "unit": "gradient-evals/s", "steps": steps,
             "k_expm_grad": {"per_launch_ms": ms, "achieved_TFLOPs": fl / (ms * 1e-3) / 1e12,
-                            "frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS},
+                            "frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, "traffic": tr,
+                            "traffic_GBs": (tr / (ms * 1e-3) / 1e9) if tr else None},
             "kernels_ms_per_step": {k: v[0] / steps for k, v in kt.items() if v[1]},
             "note": "same workload with sectors disabled (GRAPE_NO_SECTORS=1): whole 9 x 9 matrices"}
 
@@ -393,7 +403,7 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     fp = flop_model[kname] / (ms * 1e-3) / 1e12
     hb = byte_model[kname] / (ms * 1e-3) / 1e9
     short = {"k_grad/k_err_local": "k_err_local"}.get(kname, kname)
-    traffic = pmc_traffic(short, L, PMC_SUMMARY_C3)
+    traffic = pmc_traffic(short, L, PMC_SUMMARY_C3, dims={S for S, _ in classes})
     if hb / HBM_PEAK_GBS > fp / FP64_PEAK_TFLOPS:
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hb / HBM_PEAK_GBS}
@@ -440,7 +450,7 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     hbm = {}
     for k, sh in (("k_grad/k_err_local", "k_err_local"), ("k_err_grad", "k_err_grad"),
                   ("k_err_scan", "k_err_scan"), ("k_scan", "k_scan")):
-        t = pmc_traffic(sh, L, PMC_SUMMARY_C3)
+        t = pmc_traffic(sh, L, PMC_SUMMARY_C3, dims={S for S, _ in classes})
         if per_pass.get(k) and t:
             gbs = t / (per_pass[k] * 1e-3) / 1e9
             hbm[sh] = {"traffic_bytes": t, "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS}
@@ -606,10 +616,10 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
-                    help="restarts per GPU per step; default 65536 (c2), 4096 (c3), 16 (c5)")
+                    help="restarts per GPU per step; default 262144 (c2), 4096 (c3), 16 (c5)")
     ap.add_argument("--chunk", type=int, default=None,
                     help="evaluations per device pass (the plan's workspace; larger steps are chunked "
-                         "by the C side); default 16384 (c2), 2048 (c3), 16 (c5)")
+                         "by the C side); default 32768 (c2), 2048 (c3), 16 (c5)")
     ap.add_argument("--workload", choices=("c2", "c3", "c5", "c5err", "c4opt", "c2-closure"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
@@ -660,11 +670,12 @@ def main():
     else:
         fp, nparam, d, nt, inputs = problem(), 1, D, NT, restart_inputs
     ne = len(fp.unitary_problem.error_sources)
-    # One step = B restarts per GPU, evaluated in device passes of `chunk` (measured C2 passes:
-    # 1 024 -> 614k, 2 048 -> 673k, 4 096 -> 707k, 8 192 -> 729k evals/s).  B is
-    # sized so that the driver's 20 steps last > 2 s (its GPU-busy sampler must see them).
-    B = args.batch or (16 if c5 else 4096 if c3 else 65536)
-    chunk = args.chunk or (16 if c5 else 2048 if c3 else 16384)
+    # One step = B restarts per GPU, evaluated in device passes of `chunk` (measured C2 passes on
+    # sectors: 8 192 -> 2.64M, 16 384 -> 2.65M, 32 768 -> 2.70M, 65 536 -> 2.71M evals/s;
+    # DESIGN.md 9).  B is sized so that 20 steps last about 2 s (the driver's GPU-busy sampler
+    # must see them).
+    B = args.batch or (16 if c5 else 4096 if c3 else 262144)
+    chunk = args.chunk or (16 if c5 else 2048 if c3 else 32768)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
     plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=min(count, chunk))
     X = torch.from_numpy(inputs(first, count)).to(dev)

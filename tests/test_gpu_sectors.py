@@ -80,6 +80,8 @@ def _close_err(a, b, label):
     errs = {}
     assert np.max(np.abs(a[0] - b[0])) <= T1
     for n, (x, y, t, ta) in enumerate([(a[1], b[1], T2, T2_ABS), (a[2], b[2], T2, T2_ABS), (a[3], b[3], T3, T3_ABS)]):
+        if np.size(y) == 0:  # no error sources
+            continue
         err, scale = np.max(np.abs(x - y)), np.max(np.abs(y))
         errs[("F_dx", "F_d2err", "F_d2err_dx")[n]] = f"{err:.2e}/{scale:.2e}"
         assert err <= t * scale + ta, (label, n, err, scale)
@@ -186,3 +188,53 @@ def test_sector_single_calls_are_the_batch(monkeypatch):
             assert one[0][0] == ref[0][b] and np.array_equal(one[1][0], ref[1][b])
     finally:
         pl.close()
+
+
+@pytest.mark.parametrize("nt", [1, 3])
+def test_sectors_tiny_step_counts(nt, monkeypatch):
+    """N_t = 1 and 3: one chunk per sector, chunk starts everywhere."""
+    from oracle import grape_oracle as O
+    for nerr in (0, 2):
+        f = P.full9_problem(nt, nerr=nerr)
+        X = np.stack([P.random_x(nt, 500 + s) for s in range(3)])
+        sec, _, out, ref = _both(f, X, monkeypatch)
+        assert sec == ((4, 1), (2, 2))
+        _close_err(out, ref, f"nt={nt} ne={nerr} vs whole")
+        o = O.calculate_fidelity_and_derivatives(P.full9_problem(nt, nerr=nerr, device=False), X[2])
+        _close_err((out[0][2], out[1][2], out[2][2], out[3][2]), tuple(np.asarray(v) for v in o),
+                   f"nt={nt} ne={nerr} vs oracle")
+
+
+def test_sectors_two_controls(monkeypatch):
+    """n_p = 2 (phase and a detuning on the Rydberg levels, both read from x): two eps-variants
+    per step and sector, F_dx interleaved per step."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import rydberg as R
+    from robustgrape_amd.operators import FN_LINEAR, VAR_X, OperatorBasisHamiltonian, Term
+    from robustgrape_amd.types import FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    nt = 10
+    Nr = np.diag([0, 0, 0, 0, 1, 1, 1, 1, 2]).astype(np.complex128)
+    H0 = OperatorBasisHamiltonian(list(R.rydberg_full_operator_basis().terms)
+                                  + [Term(Nr, var=VAR_X, index=1, func=FN_LINEAR, scale=0.3)])
+    up = UnitaryRobustGRAPEProblem(t0=P.T0_TO, ntimes=nt, ndim=9, H0=H0, nb_additional_param=1)
+    fp = FidelityRobustGRAPEProblem(up, P.W_FULL9, R.cz_full_target())
+    rng = np.random.default_rng(77)
+    X = np.stack([np.concatenate([rng.uniform(-3, 3, 2 * nt), [rng.uniform(0, 6)]]) for _ in range(3)])
+    from robustgrape_amd.engine import GrapePlan
+    ps = GrapePlan(fp, nparam=2, device=0, max_batch=3)
+    monkeypatch.setenv("GRAPE_NO_SECTORS", "1")
+    pw = GrapePlan(fp, nparam=2, device=0, max_batch=3)
+    monkeypatch.delenv("GRAPE_NO_SECTORS")
+    try:
+        assert ps.sectors() == ((4, 1), (2, 2)) and pw.sectors() == ((9, 1),)
+        out, ref = ps.fidelity_grad(X), pw.fidelity_grad(X)
+    finally:
+        ps.close()
+        pw.close()
+    _close(out, ref, tight=False)
+    Hc = lambda t, x, xa: H0(t, x, xa)  # noqa: E731  (closure form for the oracle)
+    fo = FidelityRobustGRAPEProblem(UnitaryRobustGRAPEProblem(t0=P.T0_TO, ntimes=nt, ndim=9, H0=Hc,
+                                                              nb_additional_param=1),
+                                    P.W_FULL9, lambda xa: R.cz_with_1q_phase_full(xa[0]))
+    F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[1])[:2]
+    _close((out[0][1], out[1][1]), (F0, g0), tight=False)
