@@ -51,7 +51,8 @@ int fail(int code, const std::string &msg) {
             return fail(GRAPE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow;
+constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow,
+              kScanTiny = grape_host::kScanTiny;
 constexpr int kCtrlInts = 8;  // [0..1] single-eval counters, [2] status, [4..5] pipeline overflow counters
 using grape_host::KMark;
 using grape_host::launch_pipeline;
@@ -900,10 +901,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             Ps.nsec = sc.nsec;
             Ps.sec_ops = (size_t)n_ops * TS;
             Ps.gen_proj = 0;
-            Ps.scan_waves = (long)R >= 2L * ncu ? kScanNarrow : kScanWide;
+            Ps.scan_waves = (long)R >= 8L * ncu ? kScanTiny : (long)R >= 2L * ncu ? kScanNarrow : kScanWide;
             if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {
                 const int wv = std::atoi(w);
-                if (wv == kScanNarrow || wv == kScanWide) Ps.scan_waves = wv;
+                if (wv == kScanTiny || wv == kScanNarrow || wv == kScanWide) Ps.scan_waves = wv;
             }
             const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
             Ps.L = (P.Nt + ncs - 1) / ncs;

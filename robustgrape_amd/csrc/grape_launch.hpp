@@ -19,7 +19,9 @@ using grape::DevProblem;
 // of L = 10 steps at d = 9, N_t = 512) has the shortest chains; W = 4 halves
 // the LDS and registers per block so two evaluations share a CU, which wins
 // once there are more evaluations than CUs (plan-time choice, see kScanWide).
-constexpr int kScanWide = 8, kScanNarrow = 4;
+// Sector problems with many sub-evaluations per CU take W = 1: fewer chunks mean
+// fewer carries and per-chunk images to stream (C2 2.69 -> 2.80 M evals/s).
+constexpr int kScanWide = 8, kScanNarrow = 4, kScanTiny = 1;
 
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
@@ -36,6 +38,32 @@ size_t errscan_lds(int W) {
 template <int D>
 size_t scan_lds(int W) {
     return ((size_t)W * grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD + 3 * grape::Geo<D>::TILE) * sizeof(cd);
+}
+
+// k_scan / k_err_scan at the plan's width (P.scan_waves: 1, 4 or 8 waves per workgroup)
+template <int D>
+void launch_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    if (P.scan_waves == kScanTiny)
+        hipLaunchKernelGGL((grape::k_scan<D, kScanTiny>), dim3(B.nb), dim3(64 * kScanTiny), scan_lds<D>(kScanTiny), st,
+                           P, B);
+    else if (P.scan_waves == kScanNarrow)
+        hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
+                           scan_lds<D>(kScanNarrow), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide), st,
+                           P, B);
+}
+template <int D>
+void launch_err_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    if (P.scan_waves == kScanTiny)
+        hipLaunchKernelGGL((grape::k_err_scan<D, kScanTiny>), dim3(B.nb * P.ne), dim3(64 * kScanTiny),
+                           errscan_lds<D>(kScanTiny), st, P, B);
+    else if (P.scan_waves == kScanNarrow)
+        hipLaunchKernelGGL((grape::k_err_scan<D, kScanNarrow>), dim3(B.nb * P.ne), dim3(64 * kScanNarrow),
+                           errscan_lds<D>(kScanNarrow), st, P, B);
+    else
+        hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
+                           errscan_lds<D>(kScanWide), st, P, B);
 }
 
 // ---------------------------------------------------------------------------
@@ -73,12 +101,7 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
                        B.overflow_count, B.status, 1);
     mark(GRAPE_KERNEL_EXPM_HIGH, 1);
     mark(GRAPE_KERNEL_SCAN, 0);
-    if (P.scan_waves == kScanNarrow)
-        hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
-                           scan_lds<D>(kScanNarrow), st, P, B);
-    else
-        hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide),
-                           st, P, B);
+    launch_scan<D>(P, B, st);
     if (P.gen_proj) {  // general projector: F, M'_c (and F_dx_add's target part) redone in general form
         const hipError_t e = grape_proj::launch_fid_head(grape_proj::small_heads(P, B), B.nb, st);
         if (e != hipSuccess) return e;
@@ -109,12 +132,7 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     }
     if (P.ne > 0) {
         mark(GRAPE_KERNEL_ERR_SCAN, 0);
-        if (P.scan_waves == kScanNarrow)
-            hipLaunchKernelGGL((grape::k_err_scan<D, kScanNarrow>), dim3(B.nb * P.ne), dim3(64 * kScanNarrow),
-                               errscan_lds<D>(kScanNarrow), st, P, B);
-        else
-            hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
-                               errscan_lds<D>(kScanWide), st, P, B);
+        launch_err_scan<D>(P, B, st);
         if (P.gen_proj) {
             const hipError_t e = grape_proj::launch_err_head(grape_proj::small_heads(P, B), B.nb, st);
             if (e != hipSuccess) return e;
@@ -162,12 +180,7 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                            B.overflow_count, B.status, 1);
         mark(GRAPE_KERNEL_EXPM_HIGH, 1);
         mark(GRAPE_KERNEL_SCAN, 0);
-        if (P.scan_waves == kScanNarrow)
-            hipLaunchKernelGGL((grape::k_scan<D, kScanNarrow>), dim3(B.nb), dim3(64 * kScanNarrow),
-                               scan_lds<D>(kScanNarrow), st, P, B);
-        else
-            hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide),
-                               scan_lds<D>(kScanWide), st, P, B);
+        launch_scan<D>(P, B, st);
         mark(GRAPE_KERNEL_SCAN, 1);
         return hipGetLastError();
     }
@@ -183,12 +196,7 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                                errpath_lds<D>(), st, P, B);
             mark(GRAPE_KERNEL_GRAD, 1);
             mark(GRAPE_KERNEL_ERR_SCAN, 0);
-            if (P.scan_waves == kScanNarrow)
-                hipLaunchKernelGGL((grape::k_err_scan<D, kScanNarrow>), dim3(B.nb * P.ne), dim3(64 * kScanNarrow),
-                                   errscan_lds<D>(kScanNarrow), st, P, B);
-            else
-                hipLaunchKernelGGL((grape::k_err_scan<D, kScanWide>), dim3(B.nb * P.ne), dim3(64 * kScanWide),
-                                   errscan_lds<D>(kScanWide), st, P, B);
+            launch_err_scan<D>(P, B, st);
             mark(GRAPE_KERNEL_ERR_SCAN, 1);
             return hipGetLastError();
         }
@@ -286,7 +294,8 @@ hipError_t set_lds_limits_w() {
 template <int D>
 hipError_t set_lds_limits() {
     hipError_t e = set_lds_limits_w<D, kScanWide>();
-    return e != hipSuccess ? e : set_lds_limits_w<D, kScanNarrow>();
+    if (e == hipSuccess) e = set_lds_limits_w<D, kScanNarrow>();
+    return e != hipSuccess ? e : set_lds_limits_w<D, kScanTiny>();
 }
 
 
