@@ -104,7 +104,8 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY, dims=None):
         except (IndexError, ValueError):
             return None
     rows = [row["hbm_bytes_per_launch"] for name, row in js.get("kernels", {}).items()
-            if name.split("<")[0].split("::")[-1] == kernel and "hbm_bytes_per_launch" in row
+            if name.split("<")[0].split("::")[-1] in (kernel, kernel + "_lane")  # lane-matrix variants
+            and "hbm_bytes_per_launch" in row
             and (dims is None or dim(name) in dims)]
     return sum(rows) if rows else None
 

@@ -25,7 +25,7 @@ PROJ = os.path.join(CSRC, "grape_projector.hip")
 DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
 SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS, PROJ]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
-                  ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp",
+                  ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp", "grape_lane.hpp",
                    "grape_dense.hpp", "grape_dense_api.hpp", "grape_unitary_api.hpp",
                    "grape_projector_api.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
