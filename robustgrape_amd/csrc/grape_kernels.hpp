@@ -126,8 +126,22 @@ struct DevBatch {
     const cd *MsecE;        // [nb][ne][D][D] the sector blocks of M_e = G_e U (the sector error head)
 };
 
+// Trig of the last argument seen by one builder: the operator bases pair cos(arg) and sin(arg)
+// terms of one control (rydberg.py _drive_terms), so one sincos serves both (ocml's sin, cos and
+// sincos share one argument reduction and kernel: same values).
+struct TrigCache {
+    double arg = __builtin_nan("");
+    double s = 0.0, c = 0.0;
+    __device__ __forceinline__ void at(double a) {
+        if (!(a == arg)) {  // NaN never matches: recomputed
+            sincos(a, &s, &c);
+            arg = a;
+        }
+    }
+};
+
 __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,
-                                        const Pert &pp) {
+                                        const Pert &pp, TrigCache &tc) {
     double v = 1.0;
     if (t.var == VAR_X) v = xk[t.index];
     else if (t.var == VAR_XADD) v = xadd[t.index];
@@ -136,13 +150,22 @@ __device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk
     const double arg = t.a * v + t.b;  // built with -ffp-contract=off: no fusion, like Julia
     double fr = 1.0, fi = 0.0;
     if (t.func == FN_LINEAR) fr = arg;
-    else if (t.func == FN_COS) fr = cos(arg);
-    else if (t.func == FN_SIN) fr = sin(arg);
-    else if (t.func == FN_CIS) {
-        fr = cos(arg);
-        fi = sin(arg);
+    else if (t.func == FN_COS || t.func == FN_SIN || t.func == FN_CIS) {
+        tc.at(arg);
+        if (t.func == FN_COS) fr = tc.c;
+        else if (t.func == FN_SIN) fr = tc.s;
+        else {
+            fr = tc.c;
+            fi = tc.s;
+        }
     }
     return cmul(cmake(t.sre, t.sim), cmake(fr, fi));
+}
+
+__device__ __forceinline__ cd term_coef(const Term &t, int nt1, const double *xk, const double *xadd,
+                                        const Pert &pp) {  // one term on its own (same trig as the cached form)
+    TrigCache tc;
+    return term_coef(t, nt1, xk, xadd, pp, tc);
 }
 
 template <int D>
@@ -214,15 +237,16 @@ struct ItemBuilder {
                                            int nt1_, const VSpec &vs_, bool valid_, int sector = 0)
         : P(P_), opsT(P_->opsT + (size_t)sector * P_->sec_ops), xk(xk_), xadd(xadd_), i(i_), nt1(nt1_), vs(vs_),
           valid(valid_), o0(0), ne_t(0) {
+        TrigCache tc;
 #pragma unroll
         for (int t = 0; t < kCachedTerms; ++t)
-            c0[t] = (t < P->n_h0) ? gen(term_coef(P->h0[t], nt1, xk, xadd, vs.pert)) : czero();
+            c0[t] = (t < P->n_h0) ? gen(term_coef(P->h0[t], nt1, xk, xadd, vs.pert, tc)) : czero();
         if (ERR && vs.err >= 0) {
             o0 = P->err_off[vs.err];
             ne_t = P->err_off[vs.err + 1] - o0;
 #pragma unroll
             for (int t = 0; t < kCachedTerms; ++t)
-                ce[t] = (t < ne_t) ? gen(cscale(vs.errval, term_coef(P->err[o0 + t], nt1, xk, xadd, vs.pert)))
+                ce[t] = (t < ne_t) ? gen(cscale(vs.errval, term_coef(P->err[o0 + t], nt1, xk, xadd, vs.pert, tc)))
                                    : czero();
         }
     }

@@ -24,12 +24,11 @@ using grape::DevProblem;
 // fewer carries and per-chunk images to stream (C2 2.69 -> 2.80 M evals/s).
 constexpr int kScanWide = 8, kScanNarrow = 4, kScanTiny = 1;
 
-// Lane-matrix kernels (grape_lane.hpp) for d <= kLaneMaxD without error sources or host tables;
-// GRAPE_NO_LANE=1 selects the row-group kernels (A/B and the bit-identity test).  Measured per
-// instantiation (C2 sectors, 32 768 evaluations per pass, rocprof, one box): S = 2 k_expm 1.154 ->
-// 1.007 ms, k_expm_grad 1.737 -> 1.557 ms; S = 4 k_expm 1.990 -> 2.256 ms, k_expm_grad 2.900 ->
-// 5.070 ms (a 4 x 4 complex matrix per lane: 2 waves/SIMD, and the contraction's per-lane operand
-// loads are 16 B pieces 256 B apart) -- so d = 4 keeps the row groups.
+// Lane-matrix nominal exponential (grape_lane.hpp k_expm_lane) for d <= kLaneMaxD without error
+// sources or host tables; GRAPE_NO_LANE=1 selects the row-group k_expm (A/B and the bit-identity
+// test).  Measured per instantiation (C2 sectors, 32 768 evaluations per pass, rocprof, one box,
+// profiles/r02/lane): S = 2 k_expm 1.057 -> 0.957 ms; S = 4 1.99 -> 2.26 ms (a 4 x 4 complex
+// matrix per lane is 64 VGPRs: 2 waves/SIMD), so d = 4 keeps the row groups.
 constexpr int kLaneMaxD = 3;
 inline bool lane_env_ok() { return getenv("GRAPE_NO_LANE") == nullptr; }  // read per launch sequence
 template <int D>
@@ -46,18 +45,6 @@ void launch_expm_lane(const DevProblem &P, const DevBatch &B, hipStream_t st) {
     }
 #endif
 }
-template <int D>
-void launch_expm_grad_lane(const DevProblem &P, const DevBatch &B, hipStream_t st) {
-#if GRAPE_HAVE_LANE
-    if constexpr (D <= kLaneMaxD) {
-        const long n = (long)B.nb * P.Nt * (P.np + (P.xadd_dep ? P.na : 0));  // = k_expm_grad_lane's items
-        hipLaunchKernelGGL(grape::k_expm_grad_lane<D>,
-                           dim3((unsigned)((n + grape::kLaneGradBlock - 1) / grape::kLaneGradBlock)),
-                           dim3(grape::kLaneGradBlock), grape::lane_grad_lds<D>(), st, P, B);
-    }
-#endif
-}
-
 template <int D>
 size_t expm_lds() { return (size_t)grape::Geo<D>::GPW * grape::Geo<D>::GROUP_CD * sizeof(cd); }
 template <int D>  // k_expm / k_expm_grad / k_expm_table (grape_kernels.hpp EXPM_GROUP_CD)
@@ -148,11 +135,8 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
         const int nvg = P.np + (P.xadd_dep ? P.na : 0);
         const long ng = (long)B.nb * P.Nt * nvg;
         mark(GRAPE_KERNEL_EXPM_GRAD, 0);
-        if (use_lane<D>(P, B))
-            launch_expm_grad_lane<D>(P, B, st);
-        else
-            hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64),
-                               expm_lean_lds<D>(), st, P, B);
+        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64),
+                           expm_lean_lds<D>(), st, P, B);
         mark(GRAPE_KERNEL_EXPM_GRAD, 1);
         mark(GRAPE_KERNEL_GRAD_HIGH, 0);
         hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);
@@ -244,11 +228,8 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
         }
         const long ng = (long)B.nb * P.Nt * P.nvg;
         mark(GRAPE_KERNEL_EXPM_GRAD, 0);
-        if (use_lane<D>(P, B))
-            launch_expm_grad_lane<D>(P, B, st);
-        else
-            hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64),
-                               expm_lean_lds<D>(), st, P, B);
+        hipLaunchKernelGGL(grape::k_expm_grad<D>, dim3((unsigned)((ng + GPW - 1) / GPW)), dim3(64),
+                           expm_lean_lds<D>(), st, P, B);
         mark(GRAPE_KERNEL_EXPM_GRAD, 1);
         mark(GRAPE_KERNEL_GRAD_HIGH, 0);
         hipLaunchKernelGGL(grape::k_grad_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, P, B);

@@ -1,13 +1,13 @@
-"""Lane-matrix kernels (robustgrape_amd/csrc/grape_lane.hpp): for d <= 3 without error sources
-one lane owns one whole item (generator, exponential, contraction) instead of a row group of d
-lanes.  The arithmetic is the row-group kernels' operation for operation, so the two paths must
-agree BITWISE (GRAPE_NO_LANE=1 selects the row groups), and both must match the oracle
-(UnitaryCalculations.jl:45-56, FidelityCalculations.jl:56-76).
+"""Lane-matrix nominal exponential (robustgrape_amd/csrc/grape_lane.hpp k_expm_lane): for d <= 3
+without error sources one lane owns one whole propagator (generator and exponential) instead of
+a row group of d lanes.  The arithmetic is the row-group kernel's operation for operation, so
+the two paths must agree BITWISE (GRAPE_NO_LANE=1 selects the row groups), and both must match
+the oracle (UnitaryCalculations.jl:45-56, FidelityCalculations.jl:56-76).
 
 Covered: the Rydberg sector class S = 2 (d = 9 -> 4 + 2 x 2, d = 5 -> 2 x 2, d = 7 -> 3 x 2; the
 S = 4 class keeps the row groups), whole-matrix problems at d = 2, 3 (and d = 4, row groups), chunk starts (N_t = 1, 3), parked
 high-norm steps (Pade 7/9/13 items handed to k_expm_high / k_grad_high), x_add-dependent H0
-(the x_add eps-variants) and two controls."""
+(x_add eps-variants downstream of the lane propagators)."""
 import numpy as np
 import pytest
 
@@ -96,7 +96,7 @@ def test_lane_whole_matrix_dims(d, monkeypatch):
 
 
 def test_lane_xadd_dependent_h0(monkeypatch):
-    """x_add read by H0: the lane gradient kernel also runs the x_add eps-variants (u >= n_p)."""
+    """x_add read by H0 (the S = 2 sectors of the d = 5 problem take the lane propagators)."""
     f = P.xadd_err_problem(5, 12, nerr=0)
     X = np.stack([P.xadd_x(12, 30 + s) for s in range(3)])
     _bitwise(f, X, monkeypatch)
