@@ -7,7 +7,7 @@
 // exponential live in registers, with no LDS, no barrier and no group reduction -- 64
 // independent items per wave, each a stream of FMAs.
 //
-//   k_expm_lane = k_expm<D, false>  (nominal propagators, no error sources)
+//   k_expm_lane<D, ERR> = k_expm<D, ERR>  (the propagators of every stored variant)
 //
 // The arithmetic is the row-group kernel's operation for operation: the same Taylor /
 // Paterson-Stockmeyer evaluation (expm_taylor), every product element accumulated over the
@@ -43,8 +43,8 @@ __device__ __forceinline__ void lane_matvec(const cd (&X)[D][D], const cd (&v)[D
 }
 
 // A = -i dt H of one item (column c from the builder's column-c call).
-template <int D>
-__device__ __forceinline__ void lane_build(ItemBuilder<D, false> &rb, cd (&A)[D][D]) {
+template <int D, bool ERR>
+__device__ __forceinline__ void lane_build(ItemBuilder<D, ERR> &rb, cd (&A)[D][D]) {
 #pragma unroll
     for (int c = 0; c < D; ++c) {
         cd col[D];
@@ -170,8 +170,9 @@ constexpr int kLaneBlock = 256;
 #endif
 constexpr int kLaneWaves = GRAPE_LANE_WAVES;
 
-// Nominal propagators (ne = 0): one item (b, k, v) per lane, E row-major.
-template <int D>
+// Propagators of every stored variant: one item (b, k, v) per lane, E row-major.  ERR selects
+// the builder with error terms (every variant of the error-source pipeline), as k_expm<D, ERR>.
+template <int D, bool ERR>
 __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_lane(DevProblem P, DevBatch B) {
     const long nitems = (long)B.nb * P.Nt * P.nv;
     const long gid = (long)blockIdx.x * kLaneBlock + threadIdx.x;
@@ -180,10 +181,10 @@ __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_lane(DevProblem
     split_item(gid, nitems, P.nv, P.Nt, b, k, v);
     const int ns = P.nsec > 1 ? P.nsec : 1, bx = b / ns;
     const double *xb = B.x + (size_t)bx * P.nx;
-    ItemBuilder<D, false> rb(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, 0, k + 1, P.vs[v], true,
-                             b - bx * ns);
+    ItemBuilder<D, ERR> rb(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, 0, k + 1, P.vs[v], true,
+                           b - bx * ns);
     cd A[D][D], X[D][D];
-    lane_build<D>(rb, A);
+    lane_build<D, ERR>(rb, A);
     int s = 0;
     const int m = lane_prologue<D>(A, X, s);
     cd *out = B.E + (size_t)gid * D * D;

@@ -24,24 +24,25 @@ using grape::DevProblem;
 // fewer carries and per-chunk images to stream (C2 2.69 -> 2.80 M evals/s).
 constexpr int kScanWide = 8, kScanNarrow = 4, kScanTiny = 1;
 
-// Lane-matrix nominal exponential (grape_lane.hpp k_expm_lane) for d <= kLaneMaxD without error
-// sources or host tables; GRAPE_NO_LANE=1 selects the row-group k_expm (A/B and the bit-identity
+// Lane-matrix exponentials (grape_lane.hpp k_expm_lane) for d <= kLaneMaxD (operator-basis
+// builders; closure tables keep k_expm_table); GRAPE_NO_LANE=1 selects the row-group k_expm (A/B and the bit-identity
 // test).  Measured per instantiation (C2 sectors, 32 768 evaluations per pass, rocprof, one box,
 // profiles/r02/lane): S = 2 k_expm 1.057 -> 0.957 ms; S = 4 1.99 -> 2.26 ms (a 4 x 4 complex
 // matrix per lane is 64 VGPRs: 2 waves/SIMD), so d = 4 keeps the row groups.
 constexpr int kLaneMaxD = 3;
 inline bool lane_env_ok() { return getenv("GRAPE_NO_LANE") == nullptr; }  // read per launch sequence
 template <int D>
-bool use_lane(const DevProblem &P, const DevBatch &B) {
-    return GRAPE_HAVE_LANE && D <= kLaneMaxD && P.ne == 0 && B.Htab == nullptr && lane_env_ok();
+bool use_lane(const DevBatch &B) {
+    return GRAPE_HAVE_LANE && D <= kLaneMaxD && B.Htab == nullptr && lane_env_ok();
 }
-template <int D>
+template <int D, bool ERR>
 void launch_expm_lane(const DevProblem &P, const DevBatch &B, hipStream_t st) {
 #if GRAPE_HAVE_LANE
     if constexpr (D <= kLaneMaxD) {
         const long n = (long)B.nb * P.Nt * P.nv;
-        hipLaunchKernelGGL(grape::k_expm_lane<D>, dim3((unsigned)((n + grape::kLaneBlock - 1) / grape::kLaneBlock)),
-                           dim3(grape::kLaneBlock), 0, st, P, B);
+        hipLaunchKernelGGL((grape::k_expm_lane<D, ERR>),
+                           dim3((unsigned)((n + grape::kLaneBlock - 1) / grape::kLaneBlock)), dim3(grape::kLaneBlock), 0,
+                           st, P, B);
     }
 #endif
 }
@@ -111,11 +112,11 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     if (table)
         hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lean_lds<D>(), st, P, B);
+    else if (use_lane<D>(B))
+        fused ? launch_expm_lane<D, false>(P, B, st) : launch_expm_lane<D, true>(P, B, st);
     else if (!fused)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lean_lds<D>(), st, P, B);
-    else if (use_lane<D>(P, B))
-        launch_expm_lane<D>(P, B, st);
     else
         hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lean_lds<D>(), st, P, B);
@@ -192,11 +193,11 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
     if (stage == 0) {
         const long nexp = (long)B.nb * P.Nt * P.nv;
         mark(GRAPE_KERNEL_EXPM, 0);
-        if (P.ne > 0)
+        if (use_lane<D>(B))
+            P.ne > 0 ? launch_expm_lane<D, true>(P, B, st) : launch_expm_lane<D, false>(P, B, st);
+        else if (P.ne > 0)
             hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                                expm_lean_lds<D>(), st, P, B);
-        else if (use_lane<D>(P, B))
-            launch_expm_lane<D>(P, B, st);
         else
             hipLaunchKernelGGL((grape::k_expm<D, false>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                                expm_lean_lds<D>(), st, P, B);

@@ -1,13 +1,15 @@
-"""Lane-matrix nominal exponential (robustgrape_amd/csrc/grape_lane.hpp k_expm_lane): for d <= 3
-without error sources one lane owns one whole propagator (generator and exponential) instead of
-a row group of d lanes.  The arithmetic is the row-group kernel's operation for operation, so
-the two paths must agree BITWISE (GRAPE_NO_LANE=1 selects the row groups), and both must match
-the oracle (UnitaryCalculations.jl:45-56, FidelityCalculations.jl:56-76).
+"""Lane-matrix exponential (robustgrape_amd/csrc/grape_lane.hpp k_expm_lane): for d <= 3 one lane
+owns one whole propagator (generator and exponential; every stored variant: the nominal one and,
+with error sources, the FD and error variants) instead of a row group of d lanes.  The
+arithmetic is the row-group kernel's operation for operation, so the two paths must agree
+BITWISE (GRAPE_NO_LANE=1 selects the row groups), and both must match the oracle
+(UnitaryCalculations.jl:45-90, FidelityCalculations.jl:56-113).
 
 Covered: the Rydberg sector class S = 2 (d = 9 -> 4 + 2 x 2, d = 5 -> 2 x 2, d = 7 -> 3 x 2; the
-S = 4 class keeps the row groups), whole-matrix problems at d = 2, 3 (and d = 4, row groups), chunk starts (N_t = 1, 3), parked
-high-norm steps (Pade 7/9/13 items handed to k_expm_high / k_grad_high), x_add-dependent H0
-(x_add eps-variants downstream of the lane propagators)."""
+S = 4 class keeps the row groups), whole-matrix problems at d = 2, 3 (and d = 4, row groups),
+error sources (C3's 4 sources on d = 9 sectors, amplitude + frequency on d = 5: every output,
+F_d2err and F_d2err_dx included, bitwise), chunk starts (N_t = 1, 3), parked high-norm steps
+(Pade 7/9/13 items handed to k_expm_high), x_add-dependent H0."""
 import numpy as np
 import pytest
 
@@ -68,6 +70,8 @@ def _dense_problem(d, nt, seed):
     ("sym5", lambda: P.sym_problem(24), 24),
     ("fullblk7", lambda: P.fullblk_problem(24), 24),
     ("full9-parked", lambda: P.full9_problem(6, t0=40.0), 6),
+    ("full9-C3-errors", lambda: P.full9_problem(24, nerr=4), 24),
+    ("sym5-amp-freq", lambda: P.sym_problem(20, errors=("amp", "freq")), 20),
 ])
 def test_lane_bitwise_and_oracle(name, fp, nt, monkeypatch):
     from oracle import grape_oracle as O
