@@ -78,6 +78,7 @@ def flops_expm(d, m=5, s=0):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+LANE_MAX_D = 3  # csrc/grape_launch.hpp kLaneMaxD
 PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
 PMC_SUMMARY_C3 = os.path.join(ROOT, "profiles", "pmc_c3_latest.json")
 
@@ -104,7 +105,7 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY, dims=None):
         except (IndexError, ValueError):
             return None
     rows = [row["hbm_bytes_per_launch"] for name, row in js.get("kernels", {}).items()
-            if name.split("<")[0].split("::")[-1] in (kernel, kernel + "_lane")  # lane-matrix variants
+            if name.split("<")[0].split("::")[-1] in (kernel, kernel + "_lane", kernel + "_chain_lane")  # lane variants
             and "hbm_bytes_per_launch" in row
             and (dims is None or dim(name) in dims)]
     return sum(rows) if rows else None
@@ -262,8 +263,11 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                   "k_expm_grad": L * NT * nvg * per_step(lambda S: flops_expm(S) + 2 * 8 * S ** 3 + 8 * S ** 2)}
     # algorithmic HBM bytes per pass: k_expm writes E; k_scan reads E, writes Q; k_expm_grad
     # reads E_k and Q_k (Q_{k-1} is the previous step's Q_k) -- 16 S^2 bytes per tile
-    byte_model = {"k_expm": L * NT * per_step(lambda S: 16 * S * S),
-                  "k_scan": L * NT * per_step(lambda S: 2 * 16 * S * S),
+    # Sector classes of S <= LANE_MAX_D (csrc/grape_launch.hpp kLaneMaxD) run k_expm_chain_lane:
+    # the exp kernel also builds the chunk chains and writes Q, and k_scan only reads chunk totals
+    chained = lambda S: sec and S <= LANE_MAX_D and os.environ.get("GRAPE_NO_LANE") is None  # noqa: E731
+    byte_model = {"k_expm": L * NT * per_step(lambda S: (2 if chained(S) else 1) * 16 * S * S),
+                  "k_scan": L * NT * per_step(lambda S: 0 if chained(S) else 2 * 16 * S * S),
                   "k_expm_grad": L * NT * nvg * per_step(lambda S: 2 * 16 * S * S)}
     npass = passes or max(1, ktimes.get("k_expm_grad", (0.0, 1))[1])
     per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
@@ -294,7 +298,8 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
         "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
                                "np=1, na=1, ne=0; restart sweep",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
-                   "sectors": [{"levels": S, "sectors": ns} for S, ns in classes] if sec else None},
+                   "sectors": [{"levels": S, "sectors": ns, "lane_chains": bool(chained(S))}
+                               for S, ns in classes] if sec else None},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }

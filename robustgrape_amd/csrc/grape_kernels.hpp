@@ -124,6 +124,8 @@ struct DevBatch {
     double *sec_part_err;   // [nb][ne][Nt][nvg] per-sector F_d2err_dx terms (k_sec_reduce_err sums them)
     cd *TotS;               // [nb][ne][D][D] the sector blocks of Tot = sum_k V^err_k (k_err_scan)
     const cd *MsecE;        // [nb][ne][D][D] the sector blocks of M_e = G_e U (the sector error head)
+    int chains_done;        // k_scan: Phase A's chunk chains Q_k are already in Q (k_expm_chain_lane);
+                            //   a chunk whose total holds a NaN (a parked step) is rechained from E
 };
 
 // Trig of the last argument seen by one builder: the operator bases pair cos(arg) and sin(arg)
@@ -503,8 +505,20 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 #pragma unroll
         for (int m = 0; m < D; ++m) dst[m] = src[m * D];
     };
-    load_e(k0, e);
-    for (int j = 0; j < P.L; ++j) {
+    bool redo = true;
+    if (B.chains_done) {  // the chunk total is the chain's last stored step
+        const int kend = min(k0 + P.L, P.Nt) - 1;
+        const cd *src = Qb + (size_t)(gvalid ? kend : 0) * TILE + i;
+        bool bad = false;
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            q[m] = src[m * D];
+            bad = bad || q[m].re != q[m].re || q[m].im != q[m].im;
+        }
+        redo = group_any(G, gvalid && bad);  // group-uniform
+    }
+    if (redo) load_e(k0, e);
+    for (int j = 0; redo && j < P.L; ++j) {
         const int k = k0 + j;
         const bool act = gvalid && k < P.Nt;
         cd en[D];

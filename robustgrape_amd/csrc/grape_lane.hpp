@@ -211,6 +211,85 @@ __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_lane(DevProblem
     }
 }
 
+// Sectors without error sources (one stored variant): one lane per (sub-evaluation b, chunk c)
+// walks the chunk's steps, computes E_k (k_expm_lane's arithmetic) and extends the chunk chain
+// Q_k = E_k Q_{k-1} (Q = E at the chunk start) in registers -- exactly k_scan's Phase A, element
+// (j, i) summed over k in order with cmac(c, Q[k][i], E[j][k]) -- writing E_k and Q_k.  k_scan
+// then starts at the chunk totals (B.chains_done) and never streams E for the chains.  A step
+// parked for k_expm_high (Pade degree > 5) poisons the rest of its chunk's chain with NaN, and
+// k_scan rechains that chunk from E after k_expm_high has filled it in.
+template <int D>
+__global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_chain_lane(DevProblem P, DevBatch B) {
+    constexpr int TILE = D * D;
+    const long nitems = (long)B.nb * P.nchunks;
+    const long gid = (long)blockIdx.x * kLaneBlock + threadIdx.x;
+    if (gid >= nitems) return;
+    const int b = (int)(gid / P.nchunks), c = (int)(gid - (long)b * P.nchunks);
+    const int ns = P.nsec > 1 ? P.nsec : 1, bx = b / ns;
+    const double *xb = B.x + (size_t)bx * P.nx;
+    cd Q[D][D];
+    const int k0 = c * P.L, k1 = min(k0 + P.L, P.Nt);
+    for (int k = k0; k < k1; ++k) {
+        ItemBuilder<D, false> rb(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, 0, k + 1, P.vs[0], true,
+                                 b - bx * ns);
+        cd A[D][D], X[D][D];
+        lane_build<D, false>(rb, A);
+        int s = 0;
+        const int m = lane_prologue<D>(A, X, s);
+        const long item = (long)b * P.Nt + k;  // nv = 1
+        cd *out = B.E + (size_t)item * TILE;
+        if (m > 5) {
+            lane_park<D>(out, A, item, B.overflow, B.overflow_count);
+            const double nan = __builtin_nan("");
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+#pragma unroll
+                for (int cc = 0; cc < D; ++cc) X[r][cc] = cmake(nan, nan);
+            }
+        } else {
+            if (m == 3 || m == 5) {
+                cd A3[D][D];
+                lane_cube<D>(A, A3);
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    cd x[D];
+                    lane_taylor_col<D>(m, i, A, A3, x);
+#pragma unroll
+                    for (int j = 0; j < D; ++j) X[j][i] = x[j];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+#pragma unroll
+                for (int cc = 0; cc < D; ++cc) out[r * D + cc] = X[r][cc];
+            }
+        }
+        if (k == k0) {
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+#pragma unroll
+                for (int cc = 0; cc < D; ++cc) Q[r][cc] = X[r][cc];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < D; ++i) {  // column i of E_k . Q
+                cd q[D], t[D];
+#pragma unroll
+                for (int r = 0; r < D; ++r) q[r] = Q[r][i];
+                lane_matvec<D>(X, q, t);
+#pragma unroll
+                for (int r = 0; r < D; ++r) Q[r][i] = t[r];
+            }
+        }
+        cd *dq = B.Q + (size_t)item * TILE;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+#pragma unroll
+            for (int cc = 0; cc < D; ++cc) dq[r * D + cc] = Q[r][cc];
+        }
+    }
+}
+
 #else
 #define GRAPE_HAVE_LANE 0
 #endif

@@ -192,6 +192,28 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
     constexpr int GPW = grape::Geo<D>::GPW;
     if (stage == 0) {
         const long nexp = (long)B.nb * P.Nt * P.nv;
+#if GRAPE_HAVE_LANE
+        if constexpr (D <= kLaneMaxD) {
+            if (use_lane<D>(B) && P.ne == 0 && P.nv == 1) {  // propagators + chunk chains per lane
+                mark(GRAPE_KERNEL_EXPM, 0);
+                const long n = (long)B.nb * P.nchunks;
+                hipLaunchKernelGGL(grape::k_expm_chain_lane<D>,
+                                   dim3((unsigned)((n + grape::kLaneBlock - 1) / grape::kLaneBlock)),
+                                   dim3(grape::kLaneBlock), 0, st, P, B);
+                mark(GRAPE_KERNEL_EXPM, 1);
+                mark(GRAPE_KERNEL_EXPM_HIGH, 0);
+                hipLaunchKernelGGL(grape::k_expm_high<D>, dim3(64), dim3(64), expm_lds<D>(), st, B.E, B.overflow,
+                                   B.overflow_count, B.status, 1);
+                mark(GRAPE_KERNEL_EXPM_HIGH, 1);
+                mark(GRAPE_KERNEL_SCAN, 0);
+                DevBatch Bc = B;
+                Bc.chains_done = 1;
+                launch_scan<D>(P, Bc, st);
+                mark(GRAPE_KERNEL_SCAN, 1);
+                return hipGetLastError();
+            }
+        }
+#endif
         mark(GRAPE_KERNEL_EXPM, 0);
         if (use_lane<D>(B))
             P.ne > 0 ? launch_expm_lane<D, true>(P, B, st) : launch_expm_lane<D, false>(P, B, st);

@@ -9,7 +9,10 @@ Covered: the Rydberg sector class S = 2 (d = 9 -> 4 + 2 x 2, d = 5 -> 2 x 2, d =
 S = 4 class keeps the row groups), whole-matrix problems at d = 2, 3 (and d = 4, row groups),
 error sources (C3's 4 sources on d = 9 sectors, amplitude + frequency on d = 5: every output,
 F_d2err and F_d2err_dx included, bitwise), chunk starts (N_t = 1, 3), parked high-norm steps
-(Pade 7/9/13 items handed to k_expm_high), x_add-dependent H0."""
+(Pade 7/9/13 items handed to k_expm_high), x_add-dependent H0.  Sector problems without error
+sources take k_expm_chain_lane (propagators and chunk chains per lane; k_scan starts from the
+chunk totals): the chunk-start cases and the parked steps (whose chunks k_scan rechains from E)
+exercise it bitwise against k_scan's own Phase A."""
 import numpy as np
 import pytest
 
