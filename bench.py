@@ -78,7 +78,7 @@ def flops_expm(d, m=5, s=0):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
-LANE_MAX_D = 3  # csrc/grape_launch.hpp kLaneMaxD
+LANE_MAX_D = 3  # csrc/grape_launch.hpp kLaneMaxD (= kChainMaxD)
 PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
 PMC_SUMMARY_C3 = os.path.join(ROOT, "profiles", "pmc_c3_latest.json")
 
@@ -265,7 +265,8 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     # reads E_k and Q_k (Q_{k-1} is the previous step's Q_k) -- 16 S^2 bytes per tile
     # Sector classes of S <= LANE_MAX_D (csrc/grape_launch.hpp kLaneMaxD) run k_expm_chain_lane:
     # the exp kernel also builds the chunk chains and writes Q, and k_scan only reads chunk totals
-    chained = lambda S: sec and S <= LANE_MAX_D and os.environ.get("GRAPE_NO_LANE") is None  # noqa: E731
+    chained = lambda S: (sec and S <= LANE_MAX_D and os.environ.get("GRAPE_NO_LANE") is None  # noqa: E731
+                         and os.environ.get("GRAPE_NO_CHAIN") is None)
     byte_model = {"k_expm": L * NT * per_step(lambda S: (2 if chained(S) else 1) * 16 * S * S),
                   "k_scan": L * NT * per_step(lambda S: 0 if chained(S) else 2 * 16 * S * S),
                   "k_expm_grad": L * NT * nvg * per_step(lambda S: 2 * 16 * S * S)}

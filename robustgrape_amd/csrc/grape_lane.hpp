@@ -218,6 +218,9 @@ __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_lane(DevProblem
 // then starts at the chunk totals (B.chains_done) and never streams E for the chains.  A step
 // parked for k_expm_high (Pade degree > 5) poisons the rest of its chunk's chain with NaN, and
 // k_scan rechains that chunk from E after k_expm_high has filled it in.
+// Measured and dropped: the same walk at d = 4 with E re-read through the cache and the chain in
+// the lane's LDS slot (A, A^3, E and Q do not fit a lane's registers together): bitwise equal
+// but 7.32 ms per pass against 1.95 + 1.86 ms for k_expm<4> + k_scan<4> (2 waves/SIMD, spills).
 template <int D>
 __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_chain_lane(DevProblem P, DevBatch B) {
     constexpr int TILE = D * D;
@@ -230,8 +233,10 @@ __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_chain_lane(DevP
     cd Q[D][D];
     const int k0 = c * P.L, k1 = min(k0 + P.L, P.Nt);
     for (int k = k0; k < k1; ++k) {
+        int sec = b - bx * ns;
+        asm volatile("" : "+v"(sec));  // per-step opaque: the operator loads stay inside the step (no LICM)
         ItemBuilder<D, false> rb(&P, xb + (size_t)k * P.np, xb + (size_t)P.np * P.Nt, 0, k + 1, P.vs[0], true,
-                                 b - bx * ns);
+                                 sec);
         cd A[D][D], X[D][D];
         lane_build<D, false>(rb, A);
         int s = 0;

@@ -31,6 +31,15 @@ constexpr int kScanWide = 8, kScanNarrow = 4, kScanTiny = 1;
 // matrix per lane is 64 VGPRs: 2 waves/SIMD), so d = 4 keeps the row groups.
 constexpr int kLaneMaxD = 3;
 inline bool lane_env_ok() { return getenv("GRAPE_NO_LANE") == nullptr; }  // read per launch sequence
+// Sector stage 0 without error sources: propagators and chunk chains per lane up to kChainMaxD
+// (k_expm_chain_lane; a d = 4 variant measured 7.32 vs 3.81 ms and was dropped, grape_lane.hpp);
+// GRAPE_NO_CHAIN=1 keeps k_expm + k_scan.
+constexpr int kChainMaxD = kLaneMaxD;
+template <int D>
+bool use_chain(const DevBatch &B) {
+    return GRAPE_HAVE_LANE && D <= kChainMaxD && B.Htab == nullptr && lane_env_ok() &&
+           getenv("GRAPE_NO_CHAIN") == nullptr;
+}
 template <int D>
 bool use_lane(const DevBatch &B) {
     return GRAPE_HAVE_LANE && D <= kLaneMaxD && B.Htab == nullptr && lane_env_ok();
@@ -193,8 +202,8 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
     if (stage == 0) {
         const long nexp = (long)B.nb * P.Nt * P.nv;
 #if GRAPE_HAVE_LANE
-        if constexpr (D <= kLaneMaxD) {
-            if (use_lane<D>(B) && P.ne == 0 && P.nv == 1) {  // propagators + chunk chains per lane
+        if constexpr (D <= kChainMaxD) {
+            if (use_chain<D>(B) && P.ne == 0 && P.nv == 1) {  // propagators + chunk chains per lane
                 mark(GRAPE_KERNEL_EXPM, 0);
                 const long n = (long)B.nb * P.nchunks;
                 hipLaunchKernelGGL(grape::k_expm_chain_lane<D>,
