@@ -221,6 +221,8 @@ __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_lane(DevProblem
 // Measured and dropped: the same walk at d = 4 with E re-read through the cache and the chain in
 // the lane's LDS slot (A, A^3, E and Q do not fit a lane's registers together): bitwise equal
 // but 7.32 ms per pass against 1.95 + 1.86 ms for k_expm<4> + k_scan<4> (2 waves/SIMD, spills).
+// Also measured and dropped: nontemporal 16-B stores for E and Q (9.48 vs 1.77-1.91 ms), and
+// tighter launch bounds (4 waves/SIMD: 128 VGPRs with spills).
 template <int D>
 __global__ __launch_bounds__(kLaneBlock, kLaneWaves) void k_expm_chain_lane(DevProblem P, DevBatch B) {
     constexpr int TILE = D * D;
