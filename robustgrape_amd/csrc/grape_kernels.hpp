@@ -18,6 +18,8 @@
 //   k_grad       (error-source pipeline) one row group per (b, k): Z_k and the
 //                traces against every stored variant.
 //   k_reduce_add sum over k of the x_add contributions (only when H0 depends on x_add).
+//   (d <= 3: k_expm is replaced by the lane-matrix k_expm_lane and, for sector problems without
+//   error sources, k_expm + k_scan Phase A by k_expm_chain_lane -- grape_lane.hpp)
 //
 // Gradient algebra (verified against the reference formulas at rounding level):
 //   F_dx[p,k] = Re tr(G U_dx[p,k]),  G = 2(P K^dag + conj(tau) I) W U0^dag / (D(D+1)),
