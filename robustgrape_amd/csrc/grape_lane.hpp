@@ -164,7 +164,10 @@ __device__ __forceinline__ void lane_park(cd *slot, const cd (&A)[D][D], long gi
     list[atomicAdd(count, 1)] = (int)gid;
 }
 
-constexpr int kLaneBlock = 256;
+#ifndef GRAPE_LANE_BLOCK
+#define GRAPE_LANE_BLOCK 256
+#endif
+constexpr int kLaneBlock = GRAPE_LANE_BLOCK;
 #ifndef GRAPE_LANE_WAVES
 #define GRAPE_LANE_WAVES 2  // waves per SIMD (register budget 512 / 2 = 256 VGPRs)
 #endif
