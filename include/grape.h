@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 5
+#define GRAPE_ABI_VERSION 6
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -118,7 +118,9 @@ typedef struct grape_desc {
     int32_t n_target_terms;
     const grape_term *target_terms;  /* may only use GRAPE_VAR_ONE / GRAPE_VAR_XADD */
     int32_t max_batch;  /* largest nbatch a single call will use (workspace sizing); <=0 -> 256 */
-    int32_t reserved[5]; /* reserved[0]: flags (GRAPE_DESC_*); the rest must be 0 */
+    int32_t reserved[5]; /* reserved[0]: flags (GRAPE_DESC_*); [1]: engine options (GRAPE_OPT_*, ABI 6);
+                          * [2]: k_scan width override (1, 4 or 8 waves; 0 = chosen by batch size, ABI 6);
+                          * the rest must be 0 */
     /* ABI 4: the full projector P0 (FidelityRobustGRAPEProblem.projector, Types.jl:54), ndim x ndim
      * complex, column-major, interleaved; any matrix, as FidelityCalculations.jl:47-51 accepts.
      * NULL: projector_diag is used.  When given, projector_diag is ignored (may be NULL).  The
@@ -136,6 +138,19 @@ typedef struct grape_desc {
  * read x_add: every x_add call site of the reference is tabulated.
  */
 #define GRAPE_DESC_HOST_TABLES 1
+
+/*
+ * reserved[1]: engine options (ABI 6), fixed at plan creation; 0 selects the defaults.  They
+ * choose between implementations of the SAME outputs (A/B measurements, the bit-identity and
+ * cross-path tests); none changes a result beyond the parity tiers.  Nothing is read from the
+ * environment by the library.
+ */
+#define GRAPE_OPT_NO_SECTORS 1  /* whole matrices even when the operators are block-diagonal */
+#define GRAPE_OPT_NO_LANE 2     /* row-group exponentials for d <= 3 (no lane matrices) */
+#define GRAPE_OPT_NO_CHAIN 4    /* sector chunk chains through k_expm + k_scan, not k_expm_chain_lane */
+#define GRAPE_OPT_NO_WALK 8     /* sector classes of <= 4 levels through the stored-intermediate
+                                   kernels instead of the chunk walks (grape_walk.hpp) */
+#define GRAPE_OPT_NO_GRAPH 16   /* no HIP-graph replay of small host-array calls */
 
 typedef struct grape_plan grape_plan;
 
@@ -324,8 +339,8 @@ int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launc
  * independent sector problems -- one or two classes of `nsectors[c]` sectors of `sector_dims[c]`
  * levels (blocks packed first-fit, padded with decoupled levels) -- and assembles U only for the
  * fidelity (and error) heads.  Same outputs; no API change.  Chosen at plan creation for
- * operator-basis plans (H0 and error operators) when it cuts the work at least in half; the environment
- * variable GRAPE_NO_SECTORS=1 turns it off.  Fills up to max_classes entries and returns the
+ * operator-basis plans (H0 and error operators) when it cuts the work at least in half;
+ * GRAPE_OPT_NO_SECTORS turns it off.  Fills up to max_classes entries and returns the
  * number of classes; a plan that runs whole matrices reports one class (ndim, 1).
  */
 int grape_plan_sectors(grape_plan *plan, int *sector_dims, int *nsectors, int max_classes);

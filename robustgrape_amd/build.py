@@ -22,10 +22,12 @@ DENSE = os.path.join(CSRC, "grape_dense.hip")
 UNITARY = os.path.join(CSRC, "grape_unitary.hip")
 LBFGS = os.path.join(CSRC, "grape_lbfgs.hip")
 PROJ = os.path.join(CSRC, "grape_projector.hip")
+WALK = os.path.join(CSRC, "grape_walk_inst.hip")
 DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
-SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS, PROJ]
+SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS, PROJ, WALK]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
                   ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp", "grape_lane.hpp",
+                   "grape_walk.hpp", "grape_walk_api.hpp",
                    "grape_dense.hpp", "grape_dense_api.hpp", "grape_unitary_api.hpp",
                    "grape_projector_api.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
@@ -52,7 +54,9 @@ def _units(defines):
     sub = os.path.join(OBJ, tag or "default")
     units = [(DENSE, [], os.path.join(sub, "grape_dense.o")), (ENGINE, [], os.path.join(sub, "grape_engine.o")),
              (UNITARY, [], os.path.join(sub, "grape_unitary.o")), (LBFGS, [], os.path.join(sub, "grape_lbfgs.o")),
-             (PROJ, [], os.path.join(sub, "grape_projector.o"))]
+             (PROJ, [], os.path.join(sub, "grape_projector.o")),
+             # the chunk walks: no MachineLICM (grape_walk.hpp explains the register budget)
+             (WALK, ["-mllvm", "-disable-machine-licm"], os.path.join(sub, "grape_walk.o"))]
     units += [(INST, [f"-DGRAPE_INST_DIM={d}"], os.path.join(sub, f"grape_inst_d{d}.o")) for d in DIMS]
     return sub, units
 

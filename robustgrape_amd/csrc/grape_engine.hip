@@ -160,7 +160,7 @@ struct grape_plan {
     // the sector head over the assembled U (SH)
     struct SecBuf {
         cd *E = nullptr, *Q = nullptr, *Mc = nullptr, *Carry = nullptr, *Ub = nullptr, *slots = nullptr,
-           *ops = nullptr, *opsT = nullptr, *Msec = nullptr;
+           *ops = nullptr, *opsT = nullptr, *Msec = nullptr, *Tc = nullptr, *wscr = nullptr;
         int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr;
         double *part = nullptr;
         // error sources: local-frame images, per-chunk triples, Tot / M_e blocks, F_d2err_dx terms
@@ -229,7 +229,7 @@ static void free_plan(grape_plan *p) {
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
         void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part,
-                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err};
+                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr};
         for (void *b : sbufs)
             if (b) (void)hipFree(b);
     }
@@ -437,9 +437,7 @@ static long sector_cost(const SectorClass &c) { return (long)c.nsec * c.S * c.S 
 static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
     SectorSetup ss;
     const int D = desc->ndim;
-    if (tables || D > GRAPE_MAX_SMALL_DIM) return ss;
-    if (const char *e = std::getenv("GRAPE_NO_SECTORS"))
-        if (std::atoi(e) != 0) return ss;
+    if (tables || D > GRAPE_MAX_SMALL_DIM || (desc->reserved[1] & GRAPE_OPT_NO_SECTORS)) return ss;
     std::vector<int> parent(D);
     for (int i = 0; i < D; ++i) parent[i] = i;
     auto root = [&](int i) {
@@ -518,6 +516,7 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
     grape_dense::DenseProblem &DP = p->DP;
     DevProblem &P = DP.P;
     P.D = D;
+    P.opts = desc->reserved[1];
     P.Nt = desc->ntimes;
     P.np = desc->nparam;
     P.na = desc->nadd;
@@ -785,11 +784,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             ncu = prop.multiProcessorCount;
     }
+    P.opts = desc->reserved[1];
+    const int scan_override = desc->reserved[2];  // plan option: 1, 4 or 8 waves (0: by batch size)
     P.scan_waves = p->max_batch >= 2 * ncu ? kScanNarrow : kScanWide;
-    if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {  // tuning override: 4 or 8
-        const int wv = std::atoi(w);
-        if (wv == kScanNarrow || wv == kScanWide) P.scan_waves = wv;
-    }
+    if (scan_override == kScanNarrow || scan_override == kScanWide) P.scan_waves = scan_override;
     const int NG = P.scan_waves * (64 / D);
     const int nc0 = std::min(NG, P.Nt);
     P.L = (P.Nt + nc0 - 1) / nc0;
@@ -902,19 +900,25 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             Ps.sec_ops = (size_t)n_ops * TS;
             Ps.gen_proj = 0;
             Ps.scan_waves = (long)R >= 8L * ncu ? kScanTiny : (long)R >= 2L * ncu ? kScanNarrow : kScanWide;
-            if (const char *w = std::getenv("GRAPE_SCAN_WAVES")) {
-                const int wv = std::atoi(w);
-                if (wv == kScanTiny || wv == kScanNarrow || wv == kScanWide) Ps.scan_waves = wv;
-            }
+            if (scan_override == kScanTiny || scan_override == kScanNarrow || scan_override == kScanWide)
+                Ps.scan_waves = scan_override;
+            // chunk walks (grape_walk.hpp): classes of <= kWalkMaxD levels without error sources
+            Ps.walk = (S <= grape::kWalkMaxD && P.ne == 0 && P.np <= grape::kWalkMaxNpA && P.na <= grape::kWalkMaxNpA &&
+                       !(P.opts & GRAPE_OPT_NO_WALK)) ? 1 : 0;
             const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
             grape_plan::SecBuf &b = p->sb[cl];
-            const size_t ne = (size_t)P.ne, R2 = P.ne > 0 ? 0 : R;  // k_expm_grad parking: no error sources only
-            if (dalloc(&b.E, R * P.Nt * P.nv * TS) != hipSuccess || dalloc(&b.Q, R * P.Nt * TS) != hipSuccess ||
+            const size_t ne = (size_t)P.ne, R2 = (P.ne > 0 || Ps.walk) ? 0 : R;  // k_expm_grad parking: no error sources only
+            const size_t RE = Ps.walk ? 0 : R;  // the walks store no E / Q
+            if (Ps.walk && (dalloc(&b.Tc, R * Ps.nchunks * TS) != hipSuccess ||
+                            dalloc(&b.wscr, 2 * (size_t)sc.nsec * ((MB * Ps.nchunks + grape::kWalkBlockA - 1) /
+                                                                  grape::kWalkBlockA * grape::kWalkBlockA) * TS) != hipSuccess))
+                return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sector walks)"));
+            if (dalloc(&b.E, RE * P.Nt * P.nv * TS) != hipSuccess || dalloc(&b.Q, RE * P.Nt * TS) != hipSuccess ||
                 dalloc(&b.Mc, R * Ps.nchunks * TS) != hipSuccess || dalloc(&b.Carry, R * Ps.nchunks * TS) != hipSuccess ||
                 dalloc(&b.Ub, R * TS) != hipSuccess || dalloc(&b.Msec, R * TS) != hipSuccess ||
-                dalloc(&b.slots, R2 * P.Nt * nvg * TS) != hipSuccess || dalloc(&b.ovf, R * P.Nt * P.nv) != hipSuccess ||
+                dalloc(&b.slots, R2 * P.Nt * nvg * TS) != hipSuccess || dalloc(&b.ovf, RE * P.Nt * P.nv) != hipSuccess ||
                 dalloc(&b.ovf2, R2 * P.Nt * nvg) != hipSuccess || dalloc(&b.part, R * P.Nt * nvg) != hipSuccess ||
                 dalloc(&b.sidx, sc.sidx.size()) != hipSuccess || dalloc(&b.ops, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
                 dalloc(&b.opsT, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
@@ -1058,6 +1062,8 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.ovf2_count = p->d_ctrl + 5 + 2 * cl;
             B.status = p->d_ctrl + 2;
             B.sink = p->d_sink;
+            B.Tc = sb.Tc;  // chunk walks (null otherwise)
+            B.wscr = sb.wscr;
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
             sp.part_err[cl] = sb.part_err;
@@ -1222,7 +1228,7 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
 }
 
 static bool graph_path(const grape_plan *p, int nbatch) {
-    static const bool disabled = std::getenv("GRAPE_NO_GRAPH") != nullptr;
+    const bool disabled = (p->P.opts & GRAPE_OPT_NO_GRAPH) != 0;
     return !disabled && !p->profiling && !p->tables && nbatch > 0 && nbatch <= kGraphBatch &&
            nbatch <= p->max_batch;
 }

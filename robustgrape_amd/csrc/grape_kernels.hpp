@@ -89,6 +89,8 @@ struct DevProblem {
     int sectors;         // 1: this is the sector problem (k_scan stops after the carries)
     int nsec;
     size_t sec_ops;
+    int walk;            // sector class served by the chunk walks (grape_walk.hpp: k_walk_fwd / k_walk_grad)
+    int opts;            // grape_desc.reserved[1]: GRAPE_OPT_* (fixed at plan creation)
 };
 
 struct DevBatch {
@@ -128,6 +130,9 @@ struct DevBatch {
     const cd *MsecE;        // [nb][ne][D][D] the sector blocks of M_e = G_e U (the sector error head)
     int chains_done;        // k_scan: Phase A's chunk chains Q_k are already in Q (k_expm_chain_lane);
                             //   a chunk whose total holds a NaN (a parked step) is rechained from E
+    // chunk walks (grape_walk.hpp): k_scan starts from the chunk totals in Tc when it is set
+    cd *Tc;                 // [nb][nchunks][D][D] row-major chunk totals T_c (k_walk_fwd), else null
+    cd *wscr;               // [nsec][nb / nsec][nchunks][2][D][D] per-lane scratch of the squaring path
 };
 
 // Trig of the last argument seen by one builder: the operator bases pair cos(arg) and sin(arg)
@@ -508,7 +513,12 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
         for (int m = 0; m < D; ++m) dst[m] = src[m * D];
     };
     bool redo = true;
-    if (B.chains_done) {  // the chunk total is the chain's last stored step
+    if (B.Tc) {  // chunk walks: the totals are given (column i of T_c, row-major storage)
+        const cd *src = B.Tc + ((size_t)b * P.nchunks + (gvalid ? c : 0)) * TILE + i;
+#pragma unroll
+        for (int m = 0; m < D; ++m) q[m] = src[m * D];
+        redo = false;
+    } else if (B.chains_done) {  // the chunk total is the chain's last stored step
         const int kend = min(k0 + P.L, P.Nt) - 1;
         const cd *src = Qb + (size_t)(gvalid ? kend : 0) * TILE + i;
         bool bad = false;

@@ -8,6 +8,7 @@
 #include "grape.h"
 #include "grape_errpath.hpp"
 #include "grape_lane.hpp"
+#include "grape_walk_api.hpp"
 #include "grape_projector_api.hpp"
 
 namespace grape_host {
@@ -25,24 +26,23 @@ using grape::DevProblem;
 constexpr int kScanWide = 8, kScanNarrow = 4, kScanTiny = 1;
 
 // Lane-matrix exponentials (grape_lane.hpp k_expm_lane) for d <= kLaneMaxD (operator-basis
-// builders; closure tables keep k_expm_table); GRAPE_NO_LANE=1 selects the row-group k_expm (A/B and the bit-identity
-// test).  Measured per instantiation (C2 sectors, 32 768 evaluations per pass, rocprof, one box,
-// profiles/r02/lane): S = 2 k_expm 1.057 -> 0.957 ms; S = 4 1.99 -> 2.26 ms (a 4 x 4 complex
-// matrix per lane is 64 VGPRs: 2 waves/SIMD), so d = 4 keeps the row groups.
+// builders; closure tables keep k_expm_table); GRAPE_OPT_NO_LANE selects the row-group k_expm (A/B and
+// the bit-identity test).  Measured per instantiation (C2 sectors, 32 768 evaluations per pass,
+// rocprof, one box, profiles/r02/lane): S = 2 k_expm 1.057 -> 0.957 ms; S = 4 1.99 -> 2.26 ms (a
+// 4 x 4 complex matrix per lane is 64 VGPRs: 2 waves/SIMD), so d = 4 keeps the row groups.
 constexpr int kLaneMaxD = 3;
-inline bool lane_env_ok() { return getenv("GRAPE_NO_LANE") == nullptr; }  // read per launch sequence
 // Sector stage 0 without error sources: propagators and chunk chains per lane up to kChainMaxD
 // (k_expm_chain_lane; a d = 4 variant measured 7.32 vs 3.81 ms and was dropped, grape_lane.hpp);
-// GRAPE_NO_CHAIN=1 keeps k_expm + k_scan.
+// GRAPE_OPT_NO_CHAIN keeps k_expm + k_scan.  (Both are the fallbacks of the chunk walks,
+// grape_walk.hpp, which serve these classes by default.)
 constexpr int kChainMaxD = kLaneMaxD;
 template <int D>
-bool use_chain(const DevBatch &B) {
-    return GRAPE_HAVE_LANE && D <= kChainMaxD && B.Htab == nullptr && lane_env_ok() &&
-           getenv("GRAPE_NO_CHAIN") == nullptr;
+bool use_chain(const DevProblem &P, const DevBatch &B) {
+    return GRAPE_HAVE_LANE && D <= kChainMaxD && B.Htab == nullptr && !(P.opts & (GRAPE_OPT_NO_LANE | GRAPE_OPT_NO_CHAIN));
 }
 template <int D>
-bool use_lane(const DevBatch &B) {
-    return GRAPE_HAVE_LANE && D <= kLaneMaxD && B.Htab == nullptr && lane_env_ok();
+bool use_lane(const DevProblem &P, const DevBatch &B) {
+    return GRAPE_HAVE_LANE && D <= kLaneMaxD && B.Htab == nullptr && !(P.opts & GRAPE_OPT_NO_LANE);
 }
 template <int D, bool ERR>
 void launch_expm_lane(const DevProblem &P, const DevBatch &B, hipStream_t st) {
@@ -121,7 +121,7 @@ hipError_t launch_pipeline(const DevProblem &P, const DevBatch &B, hipStream_t s
     if (table)
         hipLaunchKernelGGL(grape::k_expm_table<D>, dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
                            expm_lean_lds<D>(), st, P, B);
-    else if (use_lane<D>(B))
+    else if (use_lane<D>(P, B))
         fused ? launch_expm_lane<D, false>(P, B, st) : launch_expm_lane<D, true>(P, B, st);
     else if (!fused)
         hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),
@@ -199,11 +199,37 @@ template <int D>
 hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B, hipStream_t st,
                                const KMark &mark) {
     constexpr int GPW = grape::Geo<D>::GPW;
+    if constexpr (D >= 2 && D <= grape::kWalkMaxD) {
+        if (P.walk) {  // chunk walks (grape_walk.hpp): no E / Q intermediates
+            if (stage == 0) {
+                mark(GRAPE_KERNEL_EXPM, 0);
+                const hipError_t e = grape_walk::launch<D>(0, P, B, st);
+                mark(GRAPE_KERNEL_EXPM, 1);
+                if (e != hipSuccess) return e;
+                mark(GRAPE_KERNEL_SCAN, 0);
+                launch_scan<D>(P, B, st);
+                mark(GRAPE_KERNEL_SCAN, 1);
+                return hipGetLastError();
+            }
+            if (stage == 1) {
+                mark(GRAPE_KERNEL_REDUCE, 0);
+                const long nmc = (long)B.nb * P.nchunks * D * D;
+                hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
+                mark(GRAPE_KERNEL_REDUCE, 1);
+                mark(GRAPE_KERNEL_EXPM_GRAD, 0);
+                const hipError_t e = grape_walk::launch<D>(1, P, B, st);
+                mark(GRAPE_KERNEL_EXPM_GRAD, 1);
+                if (e != hipSuccess) return e;
+                return hipGetLastError();
+            }
+            return hipErrorInvalidValue;  // no stage 2 without error sources
+        }
+    }
     if (stage == 0) {
         const long nexp = (long)B.nb * P.Nt * P.nv;
 #if GRAPE_HAVE_LANE
         if constexpr (D <= kChainMaxD) {
-            if (use_chain<D>(B) && P.ne == 0 && P.nv == 1) {  // propagators + chunk chains per lane
+            if (use_chain<D>(P, B) && P.ne == 0 && P.nv == 1) {  // propagators + chunk chains per lane
                 mark(GRAPE_KERNEL_EXPM, 0);
                 const long n = (long)B.nb * P.nchunks;
                 hipLaunchKernelGGL(grape::k_expm_chain_lane<D>,
@@ -224,7 +250,7 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
         }
 #endif
         mark(GRAPE_KERNEL_EXPM, 0);
-        if (use_lane<D>(B))
+        if (use_lane<D>(P, B))
             P.ne > 0 ? launch_expm_lane<D, true>(P, B, st) : launch_expm_lane<D, false>(P, B, st);
         else if (P.ne > 0)
             hipLaunchKernelGGL((grape::k_expm<D, true>), dim3((unsigned)((nexp + GPW - 1) / GPW)), dim3(64),

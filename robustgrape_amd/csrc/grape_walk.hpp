@@ -1,0 +1,638 @@
+// grape_walk.hpp -- chunk walks: the sector pipeline without HBM intermediates (round 3).
+//
+// For sector classes of D <= kWalkMaxD levels without error sources (the Rydberg sectors of
+// 4 and 2 levels), ONE LANE OWNS ONE (sub-evaluation b', chunk c) and walks the chunk's
+// steps twice:
+//
+//   k_walk_fwd   E_k = exp(A_k) and the chunk chain Q <- E_k Q, in registers; writes only
+//                the chunk total T_c (k_scan then scans the totals: B.Tc).
+//                                                     UnitaryCalculations.jl:45-47,99
+//   k_walk_grad  X = M'_c = Carry_c M Carry_c^dag (k_sec_mc) and per step
+//                  E_k again, Y_k = X E_k^dag, and for every gradient parameter u the
+//                  eps-variant E'_k contracted on the spot,
+//                  F_dx[u,k] = Re tr(Y_k (E'_k - E_k)/eps)    (FidelityCalculations.jl:56-76),
+//                  then X <- E_k Y_k.
+//
+// Algebra (grape_kernels.hpp): F_dx[u,k] = Re tr(C_{k-1} M C_k^dag dE_{k,u}) with
+// C_k = E_k C_{k-1}, so with X_{k-1} = C_{k-1} M C_{k-1}^dag (= M'_c at a chunk start) the
+// gradient kernel of step k is Y_k = X_{k-1} E_k^dag and X_k = E_k X_{k-1} E_k^dag = E_k Y_k.
+// The nominal propagator is recomputed in the second walk instead of being stored: at 4
+// levels one exponential costs ~1.2 k FMAs per lane, storing and re-reading it 512 B of HBM
+// traffic, and the round-2 pipeline moved 1.08 MB of E / Q intermediates per evaluation.
+//
+// Arithmetic.  A = -i dt H is skew-Hermitian (grape_plan_create checks that H0's terms are
+// Hermitian), A^2 Hermitian and A^3 skew-Hermitian, so each is kept COMPRESSED: its diagonal
+// (the imaginary / real parts) and strict upper triangle -- 16 instead of 32 doubles at D = 4,
+// and every product with a diagonal entry is 2 FMAs instead of 4.  The exponential is the
+// row-group kernels' solve-free Taylor evaluation (Paterson-Stockmeyer in A^3; degree 12, or 6
+// when the |re|+|im| column bound is <= 0.015), column by column: column i of exp(A) needs
+// only column i of A, A^2 and the running vector, so no full matrix is materialised for it.
+// Above the Taylor-12 range (exact 1-norm > 0.25) the lane scales A by 2^-s so that
+// |A / 2^s|_1 <= 0.25 and squares s times (Higham's scaling and squaring on the same Taylor
+// approximant) -- where the row-group path parks the item for Julia's Pade 7 / 9 / 13.  Both are
+// exp(A) to a few ulps (T0); the FD differences keep the reference's (E' - E) / eps form,
+// element by element, before the contraction.
+//
+// Registers (D = 4): X 64 VGPRs across the walk, the A / A^2 / A^3 set 96, one vector of
+// temporaries; in k_walk_grad E lives in the lane's private LDS slot (17 complex, padded so
+// that the 16-B reads of 16 lanes hit 64 distinct banks).  The walks are compiled in their own
+// translation unit (grape_walk_inst.hip) without MachineLICM: hoisting the trig / log
+// polynomial constants of the inlined ocml calls out of the step loop pinned ~50 VGPRs and
+// spilled the walk state (k_walk_grad<2>: 128 VGPRs + 18 spilled -> 98, none spilled).
+#pragma once
+#include "grape_kernels.hpp"
+#include "grape_walk_api.hpp"
+
+namespace grape {
+
+constexpr int kWalkBlock = kWalkBlockA;
+// Waves per SIMD the launch bounds ask for (register budget 512 / w).  k_walk_grad at D = 4
+// holds X (64 VGPRs), the A / A^2 / A^3 set of the eps-variant (96) and a column of E' with its
+// Horner temporaries while E sits in LDS: ~290 registers, so it runs one wave per SIMD (the
+// overflow goes to AGPRs, not to scratch); everything else fits two or more.
+template <int D, bool GRAD>
+struct WalkWaves {
+    static constexpr int value = D <= 2 ? 4 : D == 3 ? (GRAD ? 2 : 3) : GRAD ? 1 : 2;
+};
+template <int D, bool GRAD>
+struct WalkLds {  // E in the lane's LDS slot (k_walk_grad, D = 4) or in registers
+    static constexpr bool value = GRAD && D >= 4;
+    static constexpr int stride = D * D + 1;  // complex elements per lane slot
+};
+
+// 1/k! as literals (the column kernels index them with compile-time constants)
+__device__ __forceinline__ constexpr double inv_fact(int k) {
+    return k == 0 ? 1.0 : k == 1 ? 1.0 : k == 2 ? 0.5 : k == 3 ? 1.0 / 6 : k == 4 ? 1.0 / 24 : k == 5 ? 1.0 / 120
+         : k == 6 ? 1.0 / 720 : k == 7 ? 1.0 / 5040 : k == 8 ? 1.0 / 40320 : k == 9 ? 1.0 / 362880
+         : k == 10 ? 1.0 / 3628800 : k == 11 ? 1.0 / 39916800 : 1.0 / 479001600;
+}
+
+// ---------------------------------------------------------------------------
+// compressed (skew-)Hermitian matrices
+// ---------------------------------------------------------------------------
+template <int D>
+struct SM {
+    static constexpr int NU = D * (D - 1) / 2;
+    double d[D];  // diagonal: imaginary parts (skew-Hermitian) or real parts (Hermitian)
+    cd u[NU];     // strict upper triangle, row by row
+};
+__host__ __device__ constexpr int uix(int D, int j, int k) { return j * D - j * (j + 1) / 2 + (k - j - 1); }
+
+// element (j, k) (compile-time indices after unrolling)
+template <int D, bool HERM>
+__device__ __forceinline__ cd sm_el(const SM<D> &M, int j, int k) {
+    if (j == k) return HERM ? cmake(M.d[j], 0.0) : cmake(0.0, M.d[j]);
+    if (j < k) return M.u[uix(D, j, k)];
+    const cd t = M.u[uix(D, k, j)];
+    return HERM ? cmake(t.re, -t.im) : cmake(-t.re, t.im);
+}
+// c += M[j][k] v: 2 FMAs for a diagonal entry, 4 otherwise
+template <int D, bool HERM>
+__device__ __forceinline__ void sm_mac(cd &c, const SM<D> &M, int j, int k, cd v) {
+    if (j == k) {
+        const double s = M.d[j];
+        if (HERM) {
+            c.re = fma(s, v.re, c.re);
+            c.im = fma(s, v.im, c.im);
+        } else {
+            c.re = fma(-s, v.im, c.re);
+            c.im = fma(s, v.re, c.im);
+        }
+    } else {
+        cmac(c, sm_el<D, HERM>(M, j, k), v);
+    }
+}
+template <int D, bool HERM>
+__device__ __forceinline__ void sm_matvec(const SM<D> &M, const cd (&v)[D], cd (&out)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        cd c = czero();
+#pragma unroll
+        for (int k = 0; k < D; ++k) sm_mac<D, HERM>(c, M, j, k, v[k]);
+        out[j] = c;
+    }
+}
+
+// A^2 (Hermitian) and A^3 = A A^2 (skew-Hermitian) of a skew-Hermitian A
+template <int D>
+__device__ __forceinline__ void sm_cube(const SM<D> &A, SM<D> &A2, SM<D> &A3) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {  // (A^2)_jj = -sum_m |A_jm|^2
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            if (m == j) {
+                s = fma(A.d[j], A.d[j], s);
+            } else {
+                const cd a = sm_el<D, false>(A, j, m);
+                s = fma(a.re, a.re, s);
+                s = fma(a.im, a.im, s);
+            }
+        }
+        A2.d[j] = -s;
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int k = j + 1; k < D; ++k) {
+            cd c = czero();
+#pragma unroll
+            for (int m = 0; m < D; ++m) sm_mac<D, false>(c, A, j, m, sm_el<D, false>(A, m, k));
+            A2.u[uix(D, j, k)] = c;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) {  // Im (A^3)_jj
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            const cd b = sm_el<D, true>(A2, m, j);
+            if (m == j) {
+                s = fma(A.d[j], b.re, s);
+            } else {
+                const cd a = sm_el<D, false>(A, j, m);
+                s = fma(a.re, b.im, s);
+                s = fma(a.im, b.re, s);
+            }
+        }
+        A3.d[j] = s;
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int k = j + 1; k < D; ++k) {
+            cd c = czero();
+#pragma unroll
+            for (int m = 0; m < D; ++m) sm_mac<D, false>(c, A, j, m, sm_el<D, true>(A2, m, k));
+            A3.u[uix(D, j, k)] = c;
+        }
+    }
+}
+
+// x = column i of the Taylor polynomial, Paterson-Stockmeyer in A^3 (grape_device.hpp
+// expm_taylor): degree 12, or degree 6 when `small`.  B_j = c_3j I + c_3j+1 A + c_3j+2 A^2.
+template <int D>
+__device__ __forceinline__ void sm_taylor_col(bool small, int i, const SM<D> &A, const SM<D> &A2, const SM<D> &A3,
+                                              cd (&x)[D]) {
+    {
+        const double k0 = small ? inv_fact(3) : inv_fact(9), k1 = small ? inv_fact(4) : inv_fact(10),
+                     k2 = small ? inv_fact(5) : inv_fact(11), k3 = small ? inv_fact(6) : inv_fact(12);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, sm_el<D, true>(A2, j, i), cscale(k3, sm_el<D, false>(A3, j, i))));
+            if (j == i) x[j].re += k0;
+        }
+    }
+#pragma unroll
+    for (int st = 2; st >= 0; --st) {
+        if (st == 0 || !small) {
+            cd t[D];
+            sm_matvec<D, false>(A3, x, t);
+            const double k0 = inv_fact(3 * st), k1 = inv_fact(3 * st + 1), k2 = inv_fact(3 * st + 2);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, sm_el<D, true>(A2, j, i), t[j]));
+                if (j == i) x[j].re += k0;
+            }
+        }
+    }
+    pin<D>(x);  // the column is final here: nothing of the next one is scheduled into it
+}
+
+// Degree choice (grape_device.hpp expm_prologue_fast, per lane): 0 = diagonal (isdiag), 3 =
+// Taylor 6, 5 = Taylor 12, 13 = Taylor 12 of A / 2^s (A scaled here) and s squarings.
+template <int D>
+__device__ __forceinline__ int sm_regime(SM<D> &A, int &s) {
+    s = 0;
+    bool off = false;
+#pragma unroll
+    for (int t = 0; t < SM<D>::NU; ++t) off = off || A.u[t].re != 0.0 || A.u[t].im != 0.0;
+    if (!off) return 0;
+    double nub = 0.0;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+        double ub = 0.0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd a = sm_el<D, false>(A, j, c);
+            ub += fabs(a.re) + fabs(a.im);
+        }
+        nub = c == 0 ? ub : fmax(nub, ub);
+    }
+    if (nub <= 0.015) return 3;
+    if (nub <= 0.25) return 5;
+    double nA = 0.0;  // Julia's opnorm(A, 1)
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+        double cs = 0.0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd a = sm_el<D, false>(A, j, c);
+            cs += sqrt(a.re * a.re + a.im * a.im);
+        }
+        nA = c == 0 ? cs : fmax(nA, cs);
+    }
+    if (nA <= 0.015) return 3;
+    if (nA <= 0.25) return 5;
+    if (!(nA <= 1e300)) return 5;  // NaN / Inf: propagates through the polynomial
+    s = (int)ceil(log2(nA * 4.0));  // |A / 2^s|_1 <= 0.25
+    const double f = ldexp(1.0, -s);  // exact
+#pragma unroll
+    for (int j = 0; j < D; ++j) A.d[j] *= f;
+#pragma unroll
+    for (int t = 0; t < SM<D>::NU; ++t) A.u[t] = cscale(f, A.u[t]);
+    return 13;
+}
+
+// exp(A), column by column into sink(i, column i).  The squaring path (kind 13, rare) parks
+// the scaled approximant in the lane's global scratch slot `scr` (two D x D column-major
+// tiles) and squares it there element by element, so that it adds no live registers to the
+// common path.
+template <int D, class Sink>
+__device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
+    int s = 0;
+    const int kind = sm_regime<D>(A, s);
+    if (kind == 0) {  // isdiag(A): exp of the diagonal (Julia's fast path)
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            cd x[D];
+            const double sn = sin(A.d[i]), cn = cos(A.d[i]);  // exp(0) (cos, sin), as the row-group path
+#pragma unroll
+            for (int j = 0; j < D; ++j) x[j] = (j == i) ? cmake(cn, sn) : czero();
+            pin<D>(x);
+            sink(i, x);
+        }
+        return;
+    }
+    SM<D> A2, A3;
+    sm_cube<D>(A, A2, A3);
+    if (kind != 13) {
+        const bool small = kind == 3;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            cd x[D];
+            sm_taylor_col<D>(small, i, A, A2, A3, x);
+            sink(i, x);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
+    cd *T = scr, *R = scr + D * D;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {  // (unrolled: register arrays are only ever indexed by constants)
+        cd x[D];
+        sm_taylor_col<D>(false, i, A, A2, A3, x);
+#pragma unroll
+        for (int j = 0; j < D; ++j) T[i * D + j] = x[j];
+    }
+#pragma unroll 1
+    for (int r = 0; r < s; ++r) {  // T <- T T, column-major tiles
+        __threadfence_block();
+#pragma unroll 1
+        for (int i = 0; i < D; ++i) {
+#pragma unroll 1
+            for (int j = 0; j < D; ++j) {
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, T[m * D + j], T[i * D + m]);
+                R[i * D + j] = c;
+            }
+        }
+        cd *t = T;
+        T = R;
+        R = t;
+    }
+    __threadfence_block();
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        cd x[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = T[i * D + j];
+        pin<D>(x);
+        sink(i, x);
+    }
+}
+
+// Problem data every lane reads at the same address (term tables, the sector's operators) is
+// read through the constant address space: scalar loads into SGPRs from the scalar cache, off
+// the vector-memory counter (through a flat pointer the compiler cannot rule out that the
+// kernel's own stores alias them and issues per-lane vector loads, a dependent chain of them per
+// term -- the round-3 first cut spent 74 % of k_walk_fwd<2>'s wave cycles waiting on it).
+template <class T>
+using cptr = const __attribute__((address_space(4))) T *;
+template <class T>
+__device__ __forceinline__ cptr<T> as_constant(const T *p) {
+    return (cptr<T>)(p);
+}
+// field-wise copies out of the constant address space (a reference cannot bind across spaces)
+__device__ __forceinline__ cd cload(cptr<cd> p, size_t i) { return cmake(p[i].re, p[i].im); }
+__device__ __forceinline__ Term tload(cptr<Term> p, int i) {
+    Term t;
+    t.op = p[i].op;
+    t.var = p[i].var;
+    t.index = p[i].index;
+    t.func = p[i].func;
+    t.a = p[i].a;
+    t.b = p[i].b;
+    t.sre = p[i].sre;
+    t.sim = p[i].sim;
+    return t;
+}
+__device__ __forceinline__ Pert pload(cptr<VSpec> p, int i) {
+    Pert q;
+    q.var = p[i].pert.var;
+    q.index = p[i].pert.index;
+    q.delta = p[i].pert.delta;
+    return q;
+}
+
+// The step's controls x[:, k] (np <= kWalkMaxNp) and x_add (na <= kWalkMaxNa) in registers:
+// the next step's controls are loaded one step ahead, so the build never waits on memory.
+struct WalkX {  // four named registers each (an array picked by index would be demoted to scratch)
+    double k0, k1, k2, k3;  // x[:, k]
+    double a0, a1, a2, a3;  // x_add
+    __device__ __forceinline__ double xk(int i) const { return i == 0 ? k0 : i == 1 ? k1 : i == 2 ? k2 : k3; }
+    __device__ __forceinline__ double xa(int i) const { return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : a3; }
+};
+struct X4 {
+    double v0, v1, v2, v3;
+};
+__device__ __forceinline__ X4 walk_load_x(int n, const double *xs) {  // n (uniform) <= 4 values
+    X4 r;
+    r.v0 = n > 0 ? xs[0] : 0.0;
+    r.v1 = n > 1 ? xs[1] : 0.0;
+    r.v2 = n > 2 ? xs[2] : 0.0;
+    r.v3 = n > 3 ? xs[3] : 0.0;
+    return r;
+}
+__device__ __forceinline__ void walk_set_xk(WalkX &X, const X4 &r) {
+    X.k0 = r.v0;
+    X.k1 = r.v1;
+    X.k2 = r.v2;
+    X.k3 = r.v3;
+}
+__device__ __forceinline__ void walk_set_xa(WalkX &X, const X4 &r) {
+    X.a0 = r.v0;
+    X.a1 = r.v1;
+    X.a2 = r.v2;
+    X.a3 = r.v3;
+}
+
+// term_coef (grape_kernels.hpp) with the variable read from registers
+__device__ __forceinline__ cd walk_coef(const Term &t, int nt1, const WalkX &X, const Pert &pp, TrigCache &tc) {
+    double v = 1.0;
+    if (t.var == VAR_X) v = X.xk(t.index);
+    else if (t.var == VAR_XADD) v = X.xa(t.index);
+    else if (t.var == VAR_TSTEP) v = (double)nt1;
+    if (t.var == pp.var && t.index == pp.index) v = v + pp.delta;
+    const double arg = t.a * v + t.b;  // built with -ffp-contract=off: no fusion, like Julia
+    double fr = 1.0, fi = 0.0;
+    if (t.func == FN_LINEAR) fr = arg;
+    else if (t.func == FN_COS || t.func == FN_SIN || t.func == FN_CIS) {
+        tc.at(arg);
+        if (t.func == FN_COS) fr = tc.c;
+        else if (t.func == FN_SIN) fr = tc.s;
+        else {
+            fr = tc.c;
+            fi = tc.s;
+        }
+    }
+    return cmul(cmake(t.sre, t.sim), cmake(fr, fi));
+}
+
+// A = -i dt H(x_k perturbed by pp), compressed: the builder of ItemBuilder with the sector's
+// row-major operators, term by term in order (the same cmac operand roles), diagonal as the
+// imaginary part of the same complex MAC.
+template <int D>
+__device__ __forceinline__ void walk_build(const DevProblem &P, cptr<cd> ops, const WalkX &X, int nt1, const Pert &pp,
+                                           SM<D> &A) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) A.d[j] = 0.0;
+#pragma unroll
+    for (int t = 0; t < SM<D>::NU; ++t) A.u[t] = czero();
+    TrigCache tc;
+    const cptr<Term> terms = as_constant(P.h0);
+#pragma unroll 1
+    for (int t = 0; t < P.n_h0; ++t) {
+        const Term tm = tload(terms, t);
+        const cd c = walk_coef(tm, nt1, X, pp, tc);
+        const cd g = cmake(P.dt * c.im, -(P.dt * c.re));  // -i dt c
+        const cptr<cd> op = ops + (size_t)tm.op * D * D;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd o = cload(op, j * D + j);
+            A.d[j] = fma(g.im, o.re, fma(g.re, o.im, A.d[j]));
+#pragma unroll
+            for (int k = j + 1; k < D; ++k) cmac(A.u[uix(D, j, k)], g, cload(op, j * D + k));
+        }
+    }
+}
+
+// The lane's E_k: registers (D <= 3) or its LDS slot (row-major, D = 4).
+template <int D, bool LDS>
+struct EStore;
+template <int D>
+struct EStore<D, false> {
+    cd e[D][D];
+    __device__ __forceinline__ void put_col(int i, const cd (&x)[D]) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) e[j][i] = x[j];
+    }
+    __device__ __forceinline__ cd at(int j, int k) const { return e[j][k]; }
+    __device__ __forceinline__ const EStore &opaque() const { return *this; }
+};
+template <int D>
+struct EStore<D, true> {
+    cd *p;
+    __device__ __forceinline__ void put_col(int i, const cd (&x)[D]) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) p[j * D + i] = x[j];
+    }
+    __device__ __forceinline__ cd at(int j, int k) const { return p[j * D + k]; }
+    // a copy whose address the compiler cannot see through: its loads stay where they are
+    // written (no hoisting of E's 64 VGPRs out of a loop or across an exponential)
+    __device__ __forceinline__ EStore opaque() const {
+        EStore o{p};
+        asm volatile("" : "+v"(o.p));
+        return o;
+    }
+};
+
+// lane -> (sector w = blockIdx.y, evaluation be, chunk c); sub-evaluation bp = be * nsec + w.
+// Lanes past the end (ok = false) run the walk on clamped indices and store nothing, so that
+// every loop in the walks has a wave-uniform trip count (scalar loads of the term tables).
+struct WalkLane {
+    int w, be, c, bp;
+    long slot;  // (w, be, c) index: the lane's scratch slot
+    bool ok;
+};
+__device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatch &B) {
+    WalkLane L;
+    const int ns = P.nsec > 1 ? P.nsec : 1;
+    const long per = (long)(B.nb / ns) * P.nchunks;
+    const long g = (long)blockIdx.x * kWalkBlock + threadIdx.x;
+    L.w = blockIdx.y;
+    L.ok = g < per;
+    const long gg = L.ok ? g : 0;
+    L.be = (int)(gg / P.nchunks);
+    L.c = (int)(gg - (long)L.be * P.nchunks);
+    L.bp = L.be * ns + L.w;
+    // own scratch slot for every lane, past-the-end ones included (they walk lane 0's inputs)
+    const long per_pad = (per + kWalkBlock - 1) / kWalkBlock * kWalkBlock;
+    L.slot = (long)L.w * per_pad + g;
+    return L;
+}
+
+template <int D>
+__global__ __launch_bounds__(kWalkBlock, (WalkWaves<D, false>::value)) void k_walk_fwd(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    constexpr bool ELDS = WalkLds<D, false>::value;
+    const WalkLane L = walk_lane(P, B);
+    const double *xb = B.x + (size_t)L.be * P.nx;
+    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w * P.sec_ops;
+    cd *scr = B.wscr + (size_t)L.slot * 2 * TS;
+    Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    EStore<D, ELDS> E;
+    if constexpr (ELDS) {
+        __shared__ cd lds[kWalkBlock * WalkLds<D, ELDS>::stride];
+        E.p = lds + threadIdx.x * WalkLds<D, ELDS>::stride;
+    }
+    WalkX X;
+    walk_set_xa(X, walk_load_x(P.na, xb + (size_t)P.np * P.Nt));  // x_add
+    const int k0 = L.c * P.L;
+    X4 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
+    cd Q[D][D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) Q[j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+    }
+#pragma unroll 1
+    for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t leave Q alone
+        const int k = min(k0 + jj, P.Nt - 1);
+        const bool act = k0 + jj < P.Nt;
+        walk_set_xk(X, xn);
+        xn = walk_load_x(P.np, xb + (size_t)min(k + 1, P.Nt - 1) * P.np);  // next step's controls
+        SM<D> A;
+        walk_build<D>(P, ops, X, k + 1, none, A);
+        walk_expm<D>(A, scr, [&](int i, const cd (&x)[D]) { E.put_col(i, x); });
+#pragma unroll
+        for (int i = 0; i < D; ++i) {  // column i of E_k Q (in place: it reads only column i)
+            cd q[D], t[D];
+#pragma unroll
+            for (int m = 0; m < D; ++m) q[m] = Q[m][i];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, q[m], E.at(j, m));
+                t[j] = c;
+            }
+#pragma unroll
+            for (int j = 0; j < D; ++j) Q[j][i] = cmake(act ? t[j].re : Q[j][i].re, act ? t[j].im : Q[j][i].im);
+        }
+    }
+    if (L.ok) {
+        cd *dst = B.Tc + ((size_t)L.bp * P.nchunks + L.c) * TS;  // row-major chunk total
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) dst[j * D + i] = Q[j][i];
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kWalkBlock, (WalkWaves<D, true>::value)) void k_walk_grad(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    constexpr bool ELDS = WalkLds<D, true>::value;
+    const WalkLane L = walk_lane(P, B);
+    const double *xb = B.x + (size_t)L.be * P.nx;
+    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w * P.sec_ops;
+    cd *scr = B.wscr + (size_t)L.slot * 2 * TS;
+    Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    EStore<D, ELDS> E;
+    if constexpr (ELDS) {
+        __shared__ cd lds[kWalkBlock * WalkLds<D, ELDS>::stride];
+        E.p = lds + threadIdx.x * WalkLds<D, ELDS>::stride;
+    }
+    cd X[D][D];  // X_{k-1} = C_{k-1} M C_{k-1}^dag in the sector; M'_c at the chunk start
+    {
+        const cd *mc = B.Mc + ((size_t)L.bp * P.nchunks + L.c) * TS;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) X[j][i] = mc[j * D + i];
+        }
+    }
+    WalkX XV;
+    walk_set_xa(XV, walk_load_x(P.na, xb + (size_t)P.np * P.Nt));
+    const int k0 = L.c * P.L;
+    X4 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
+    const cptr<VSpec> vs = as_constant(P.vs);
+#pragma unroll 1
+    for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store nothing
+        const int k = min(k0 + jj, P.Nt - 1);
+        const bool act = L.ok && k0 + jj < P.Nt;
+        walk_set_xk(XV, xn);
+        xn = walk_load_x(P.np, xb + (size_t)min(k + 1, P.Nt - 1) * P.np);  // next step's controls
+        SM<D> A;
+        walk_build<D>(P, ops, XV, k + 1, none, A);
+        walk_expm<D>(A, scr, [&](int i, const cd (&x)[D]) { E.put_col(i, x); });
+        // Y = X E^dag, in place row by row (row r of Y reads row r of X only)
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            cd y[D];
+#pragma unroll
+            for (int cc = 0; cc < D; ++cc) {
+                cd s = czero();
+#pragma unroll
+                for (int j = 0; j < D; ++j) cmac(s, X[r][j], cconj(E.at(cc, j)));
+                y[cc] = s;
+            }
+#pragma unroll
+            for (int cc = 0; cc < D; ++cc) X[r][cc] = y[cc];
+        }
+        // eps-variants: F_dx[u, k] = Re tr(Y (E' - E)) / eps, column j of E' against row j of Y
+#pragma unroll 1
+        for (int u = 0; u < P.nvg; ++u) {
+            SM<D> Ap;
+            walk_build<D>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
+            double s = 0.0;
+            walk_expm<D>(Ap, scr, [&](int j, const cd (&x)[D]) {
+                const auto &Ej = E.opaque();  // column j of E read here, after column j of E'
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+                    const cd de = cscale(P.inv_eps, csub(x[r], Ej.at(r, j)));  // (1/eps) (E' - E)
+                    s = fma(X[j][r].re, de.re, s);
+                    s = fma(-X[j][r].im, de.im, s);
+                }
+            });
+            if (act) B.sec_part[((size_t)L.bp * P.Nt + k) * P.nvg + u] = s;
+        }
+        // X <- E Y, in place column by column
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            cd y[D], t[D];
+#pragma unroll
+            for (int m = 0; m < D; ++m) y[m] = X[m][i];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, E.at(j, m), y[m]);
+                t[j] = c;
+            }
+#pragma unroll
+            for (int j = 0; j < D; ++j) X[j][i] = t[j];
+        }
+    }
+}
+
+}  // namespace grape

@@ -1,0 +1,19 @@
+// grape_walk_api.hpp -- host launchers of the chunk walks (grape_walk.hpp), compiled in their own
+// translation unit (grape_walk_inst.hip, built without MachineLICM; see grape_walk.hpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace grape {
+struct DevProblem;
+struct DevBatch;
+constexpr int kWalkMaxD = 4;  // sector classes of at most this many levels take the walks
+constexpr int kWalkMaxNpA = 4;  // ... with at most this many controls per step and x_add entries
+constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBlock)
+}  // namespace grape
+
+namespace grape_walk {
+// one lane per (sector, evaluation, chunk) of the class: stage 0 = k_walk_fwd (chunk totals to
+// B.Tc), stage 1 = k_walk_grad (per-sector F_dx terms to B.sec_part)
+template <int D>
+hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
+}  // namespace grape_walk

@@ -22,7 +22,10 @@ from .types import FidelityRobustGRAPEProblem, split_x
 class GrapePlan:
     """One device plan for one problem (grape_plan_create / grape_plan_destroy)."""
 
-    def __init__(self, fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 256):
+    def __init__(self, fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 256,
+                 options: int = 0, scan_waves: int = 0):
+        """options: GRAPE_OPT_* flags (operators.OPT_*), scan_waves: k_scan width override --
+        plan-creation choices between implementations of the same outputs (include/grape.h)."""
         L = _capi.lib()
         self.fp = fp
         self.up = fp.unitary_problem
@@ -31,14 +34,15 @@ class GrapePlan:
         self.nx = self.nparam * self.up.ntimes + self.up.nb_additional_param
         self.nerr = len(self.up.error_sources)
         self.max_batch = int(max_batch)
+        self.options = int(options)
         self.lock = threading.Lock()  # one evaluation at a time (the plan's buffers are shared)
         self._shared = None  # closure fallback: double-buffered shared-memory tables
         # operator bases -> the fused device path; plain closures -> the host-table fallback
         self.tables = not has_operator_basis(fp)
         if self.tables:
-            self._bufs = TableDescriptor(fp, self.nparam, self.max_batch)
+            self._bufs = TableDescriptor(fp, self.nparam, self.max_batch, options, scan_waves)
         else:
-            self._bufs = DescriptorBuffers(fp, self.nparam, self.max_batch)
+            self._bufs = DescriptorBuffers(fp, self.nparam, self.max_batch, options, scan_waves)
         h = ctypes.c_void_p()
         _capi.check(L.grape_plan_create(ctypes.byref(self._bufs.desc), self.device, ctypes.byref(h)))
         self.handle = h

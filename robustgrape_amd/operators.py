@@ -159,10 +159,21 @@ def projector_arrays(fp):
     return pdiag, full
 
 
+# grape_desc.reserved[1] engine options (include/grape.h GRAPE_OPT_*): implementations of the
+# same outputs, fixed at plan creation (A/B measurements and cross-path tests)
+OPT_NO_SECTORS, OPT_NO_LANE, OPT_NO_CHAIN, OPT_NO_WALK, OPT_NO_GRAPH = 1, 2, 4, 8, 16
+
+
+def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):
+    if scan_waves not in (0, 1, 4, 8):
+        raise ValueError("scan_waves must be 0 (by batch size), 1, 4 or 8")
+    return (ctypes.c_int32 * 5)(int(flags), int(options), int(scan_waves), 0, 0)
+
+
 class DescriptorBuffers:
     """Owns the host arrays a CDesc points into (keep alive while the C call runs)."""
 
-    def __init__(self, fp, nparam: int, max_batch: int = 256):
+    def __init__(self, fp, nparam: int, max_batch: int = 256, options: int = 0, scan_waves: int = 0):
         up = fp.unitary_problem
         if not isinstance(up.H0, OperatorBasisHamiltonian):
             raise TypeError("device path needs an OperatorBasisHamiltonian H0")
@@ -214,7 +225,7 @@ class DescriptorBuffers:
             ops=self.ops.ctypes.data_as(dp), n_h0_terms=len(up.H0.terms), h0_terms=self.h0,
             err_term_offsets=self.offs, err_terms=self.err,
             n_target_terms=len(fp.target_unitary.terms), target_terms=self.target,
-            max_batch=int(max_batch),
+            max_batch=int(max_batch), reserved=_reserved(0, options, scan_waves),
             projector=self.pfull.ctypes.data_as(dp) if self.pfull is not None else None)
         del stack
 
@@ -242,7 +253,7 @@ class TableDescriptor:
     """grape_desc of a closure problem: no operator basis; the host evaluates the closures
     (host_tables) and the device does the rest (the SURVEY.md 8b fallback)."""
 
-    def __init__(self, fp, nparam: int, max_batch: int = 256):
+    def __init__(self, fp, nparam: int, max_batch: int = 256, options: int = 0, scan_waves: int = 0):
         up = fp.unitary_problem
         self.pdiag, self.pfull = projector_arrays(fp)
         dp = ctypes.POINTER(ctypes.c_double)
@@ -250,7 +261,7 @@ class TableDescriptor:
             ndim=up.ndim, ntimes=up.ntimes, nparam=nparam, nadd=up.nb_additional_param,
             nerr=len(up.error_sources), n_ops=0, t0=float(up.t0), eps=float(up.eps), eps2=float(up.eps2),
             projector_diag=self.pdiag.ctypes.data_as(dp), n_h0_terms=0, n_target_terms=0,
-            max_batch=int(max_batch), reserved=(ctypes.c_int32 * 5)(GRAPE_DESC_HOST_TABLES),
+            max_batch=int(max_batch), reserved=_reserved(GRAPE_DESC_HOST_TABLES, options, scan_waves),
             projector=self.pfull.ctypes.data_as(dp) if self.pfull is not None else None)
 
 

@@ -94,6 +94,46 @@ def evered_pulse(ntimes=1000):
     return np.concatenate([phis, [theta]])
 
 
+def max_step_norm(fp, X, nparam=1):
+    """max over rows of X and steps k of |dt H0(k, x_k, x_add)|_1: the exponentials' regime.
+    Up to 0.25 every implementation here and the reference evaluate exp without squaring (Taylor
+    12 / Pade 5); above it the engines differ in algorithm (the chunk walks square a scaled
+    Taylor 12, the row groups and Julia take Pade 7 / 9 / 13), so eps-FD results agree only to
+    the long-step T2 tier."""
+    up = fp.unitary_problem
+    dt = up.t0 / up.ntimes
+    X = np.atleast_2d(np.asarray(X, np.float64))
+    na = up.nb_additional_param
+    best = 0.0
+    for x in X:
+        xm = x[:len(x) - na].reshape(up.ntimes, nparam)
+        xa = x[len(x) - na:]
+        for k in range(up.ntimes):
+            H = np.asarray(up.H0(k + 1, xm[k], xa))
+            best = max(best, dt * np.abs(H).sum(axis=0).max())
+    return best
+
+
+def short_steps(fp, X, nparam=1):
+    """True when every step of every row is in the no-squaring range (the T2s tier applies)."""
+    return max_step_norm(fp, X, nparam) <= 0.25
+
+
+def fd_tier(fp, X, nparam=1):
+    """(relative, absolute) tolerance of eps-FD quantities (F_dx) for these rows: the short-step
+    T2s tier (1e-7 max|ref| + 1e-9) when no step needs squaring, else the long-step T2 tier
+    (1e-6 max|ref| + 1e-7) scaled by max(1, max_k |dt H_k|_1): with s squarings the rounding of
+    each exponential -- and so the u / eps noise of (E' - E) / eps -- grows like 2^s ~ |A|_1 in
+    any implementation, and two implementations with different s (Julia: Pade 13 from
+    |A|_1 > 5.4; the chunk walks: Taylor 12 from |A|_1 > 0.25) differ by that much (the same
+    factor the unitary-derivative tests apply)."""
+    n = max_step_norm(fp, X, nparam)
+    if n <= 0.25:
+        return 1e-7, 1e-9
+    f = max(1.0, n)
+    return 1e-6 * f, 1e-7 * f
+
+
 def random_x(ntimes, seed, nparam=1, small=False):
     """x_main = 2pi*U (runtests.jl:335) or 2pi*0.001*U (examples/time_optimal_cz.jl:32); theta = 2pi*U."""
     rng = np.random.default_rng(seed)

@@ -2,7 +2,7 @@
 owns one whole propagator (generator and exponential; every stored variant: the nominal one and,
 with error sources, the FD and error variants) instead of a row group of d lanes.  The
 arithmetic is the row-group kernel's operation for operation, so the two paths must agree
-BITWISE (GRAPE_NO_LANE=1 selects the row groups), and both must match the oracle
+BITWISE (GRAPE_OPT_NO_LANE selects the row groups), and both must match the oracle
 (UnitaryCalculations.jl:45-90, FidelityCalculations.jl:56-113).
 
 Covered: the Rydberg sector class S = 2 (d = 9 -> 4 + 2 x 2, d = 5 -> 2 x 2, d = 7 -> 3 x 2; the
@@ -12,7 +12,9 @@ F_d2err and F_d2err_dx included, bitwise), chunk starts (N_t = 1, 3), parked hig
 (Pade 7/9/13 items handed to k_expm_high), x_add-dependent H0.  Sector problems without error
 sources take k_expm_chain_lane (propagators and chunk chains per lane; k_scan starts from the
 chunk totals): the chunk-start cases and the parked steps (whose chunks k_scan rechains from E)
-exercise it bitwise against k_scan's own Phase A."""
+exercise it bitwise against k_scan's own Phase A.  Both runs turn the chunk walks off
+(GRAPE_OPT_NO_WALK): the walks serve the no-error sector classes by default and are tested in
+tests/test_gpu_walk.py."""
 import numpy as np
 import pytest
 
@@ -30,14 +32,13 @@ def _need_gpu():
 
 def _run(fp, X, monkeypatch, lane, nparam=1):
     from robustgrape_amd.engine import GrapePlan
-    if not lane:
-        monkeypatch.setenv("GRAPE_NO_LANE", "1")
-    pl = GrapePlan(fp, nparam=nparam, device=0, max_batch=max(len(X), 65))  # > 64: stream path
+    from robustgrape_amd.operators import OPT_NO_LANE, OPT_NO_WALK
+    opts = OPT_NO_WALK | (0 if lane else OPT_NO_LANE)
+    pl = GrapePlan(fp, nparam=nparam, device=0, max_batch=max(len(X), 65), options=opts)  # > 64: stream path
     try:
         return pl.fidelity_grad(np.concatenate([X] * (65 // len(X) + 1))[:65])
     finally:
         pl.close()
-        monkeypatch.delenv("GRAPE_NO_LANE", raising=False)
 
 
 def _bitwise(fp, X, monkeypatch, nparam=1):

@@ -225,20 +225,19 @@ def test_error_batch_matches_single():
         assert np.array_equal(d2s, d2[b]) and np.array_equal(d2dxs, d2dx[b])
 
 
-@pytest.mark.parametrize("waves", ["4", "8"])
-def test_scan_widths_match_golden(waves, monkeypatch):
-    """Both k_scan / k_err_scan widths (the plan picks 4 waves for large batches): C2 golden and
-    the C3 (4 error sources) golden through a plan forced to each width."""
+@pytest.mark.parametrize("waves", [1, 4, 8])
+def test_scan_widths_match_golden(waves):
+    """Every k_scan / k_err_scan width (the plan picks 1 or 4 waves for large batches): C2 golden
+    and the C3 (4 error sources) golden through a plan forced to each width."""
     from robustgrape_amd.engine import GrapePlan
-    monkeypatch.setenv("GRAPE_SCAN_WAVES", waves)
     g = _golden("c2")
-    plan = GrapePlan(P.full9_problem(512), nparam=1, max_batch=8)
+    plan = GrapePlan(P.full9_problem(512), nparam=1, max_batch=8, scan_waves=waves)
     F, Fdx, _, _ = plan.fidelity_grad(g["x"][None, :])
     plan.close()
     _assert_fid(F[0], Fdx[0], float(g["F"]), g["F_dx"])
     g = _golden("c3n64")
     fp = P.full9_problem(64, nerr=4)
-    plan = GrapePlan(fp, nparam=1, max_batch=8)
+    plan = GrapePlan(fp, nparam=1, max_batch=8, scan_waves=waves)
     F, Fdx, d2, d2dx = plan.fidelity_grad(g["x"][None, :])
     plan.close()
     _assert_fid(F[0], Fdx[0], float(g["F"]), g["F_dx"])

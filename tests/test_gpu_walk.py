@@ -1,0 +1,228 @@
+"""Chunk walks (robustgrape_amd/csrc/grape_walk.hpp) and the kernel configurations the bench times.
+
+The walks serve the sector classes of <= 4 levels without error sources (the Rydberg C1 / C2 /
+C4 problems): one lane per (sub-evaluation, chunk) recomputes the propagators of its chunk, once
+for the chunk total and once for the gradient walk X <- E X E^dag with the eps-variants
+contracted on the spot (UnitaryCalculations.jl:44-56, FidelityCalculations.jl:54-76).
+
+Bench-size plans: the bench evaluates 32 768 evaluations per device pass; a plan of
+max_batch >= 2048 already selects the same kernel configuration (one-wave k_scan<S,1> /
+k_err_scan<S,1> once the sub-evaluations reach 8 x CUs, the walks' 16 chunks of 32 steps at
+S = 4 and 32 chunks of 16 steps at S = 2), so these plans are checked against the goldens
+(C2, C4 and C3) and the oracle -- with the walks and with the round-2 stored-intermediate
+kernels (GRAPE_OPT_NO_WALK: k_expm_chain_lane's 16-step chunk chains, k_expm_grad), including
+high-norm steps inside multi-step chunks (the walks' scaling-and-squaring path; the
+stored-intermediate path's parked steps, NaN-poisoned chunk chains and k_scan's rechain)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import problems as P
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+T1 = 1e-12
+T2, T2_ABS = 1e-6, 1e-7
+T2S, T2S_ABS = 1e-7, 1e-9
+T3, T3_ABS, T3_XADD_ABS = 1e-5, 1e-7, 1e-5
+BIG = 2048  # >= 8 x 256 CUs sub-evaluations: the bench's kernel configuration
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _golden(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+
+
+def _plan(fp, max_batch, options=0, nparam=1):
+    from robustgrape_amd.engine import GrapePlan
+    return GrapePlan(fp, nparam=nparam, device=0, max_batch=max_batch, options=options)
+
+
+def _check(test, F, Fdx, F0, g0, tight):
+    """tight: True (T2s), False (T2) or a (relative, absolute) pair (tests/problems.py fd_tier)."""
+    from tests.parity_log import record
+    if isinstance(tight, tuple):
+        t2, t2a = tight
+    else:
+        t2, t2a = (T2S, T2S_ABS) if tight else (T2, T2_ABS)
+    ef = abs(float(F) - float(F0))
+    record(test, "F", ef, 1.0, T1)
+    assert ef <= T1, (test, F, F0)
+    err, scale = float(np.max(np.abs(Fdx - g0))), float(np.max(np.abs(g0)))
+    record(test, "F_dx", err, scale, t2 * scale + t2a)
+    print(f"{test}: |dF| {ef:.2e}  max|dF_dx| {err:.2e} (scale {scale:.2e}, rel {err / scale:.2e})")
+    assert err <= t2 * scale + t2a, (test, err, scale)
+
+
+@pytest.mark.parametrize("name,fp,layout", [
+    ("full9", lambda: P.full9_problem(40), ((4, 1), (2, 2))),
+    ("full9-one-step", lambda: P.full9_problem(1), ((4, 1), (2, 2))),
+    ("full9-chunk-starts", lambda: P.full9_problem(3), ((4, 1), (2, 2))),
+    ("sym5", lambda: P.sym_problem(24), ((2, 2),)),
+    ("fullblk7", lambda: P.fullblk_problem(24), ((2, 3),)),
+    ("c1-evered", lambda: P.sym_problem(1000), ((2, 2),)),
+])
+def test_walk_matches_oracle_and_stored_path(name, fp, layout):
+    """Walks vs the oracle and vs the stored-intermediate sector kernels (GRAPE_OPT_NO_WALK)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_WALK
+    f = fp()
+    nt = f.unitary_problem.ntimes
+    X = np.stack([P.evered_pulse(nt) if name == "c1-evered" and s == 0 else P.random_x(nt, 700 + s)
+                  for s in range(5)])
+    pw, ps = _plan(f, len(X)), _plan(f, len(X), OPT_NO_WALK)
+    try:
+        assert pw.sectors() == layout
+        out, ref = pw.fidelity_grad(X), ps.fidelity_grad(X)
+    finally:
+        pw.close()
+        ps.close()
+    for b in range(len(X)):
+        tier = P.fd_tier(f, X[b])  # long steps: the scaled T2 tier (tests/problems.py fd_tier)
+        _check(f"walk_vs_stored_{name}_{b}", out[0][b], out[1][b], ref[0][b], ref[1][b], tier)
+    for b in (0, 3):
+        F0, g0 = O.calculate_fidelity_and_derivatives(f, X[b])[:2]
+        tier = P.fd_tier(f, X[b])
+        if name == "c1-evered" and b == 0:  # at the optimum max|F_dx| ~ 2e-4: the absolute FD floor
+            tier = (tier[0], 1e-8)         # u / eps ~ 1.1e-8 of the reference itself decides
+        _check(f"walk_vs_oracle_{name}_{b}", out[0][b], out[1][b], F0, g0, tier)
+    if name == "c1-evered":  # runtests.jl:115-165 known answer through the walks
+        assert out[0][0] > 0.9999 and abs(out[0][0] - 0.999996184760959) < 1e-12
+
+
+@pytest.mark.parametrize("walk", [True, False])
+def test_bench_size_plan_matches_goldens(walk):
+    """C2 and C4 goldens inside one 2 048-evaluation launch (the bench's kernel configuration),
+    at scattered batch positions, with the walks and with the round-2 stored-intermediate path."""
+    from robustgrape_amd.operators import OPT_NO_WALK
+    g2, g4 = _golden("c2"), _golden("c4")
+    rng = np.random.default_rng(5)
+    X = np.stack([P.random_x(512, 3000 + s, small=True) for s in range(BIG)])
+    pos2 = [0, 1023, BIG - 1]
+    pos4 = [17, 640, 1500, 2046]
+    for p in pos2:
+        X[p] = g2["x"]
+    for j, p in enumerate(pos4):
+        X[p] = g4["x"][j]
+    pl = _plan(P.full9_problem(512), BIG, 0 if walk else OPT_NO_WALK)
+    try:
+        assert pl.sectors() == ((4, 1), (2, 2))
+        F, Fdx, _, _ = pl.fidelity_grad(X)
+    finally:
+        pl.close()
+    tag = "walk" if walk else "stored"
+    for p in pos2:
+        _check(f"big_{tag}_c2_at{p}", F[p], Fdx[p], g2["F"], g2["F_dx"], tight=True)
+    for j, p in enumerate(pos4):
+        _check(f"big_{tag}_c4_{j}_at{p}", F[p], Fdx[p], g4["F"][j], g4["F_dx"][j], tight=True)
+    # the rest of the batch: rows are independent and deterministic -> a re-run of a slice in a
+    # small plan (other kernel widths) agrees at the T2s tier
+    idx = rng.choice(BIG, size=6, replace=False)
+    small = _plan(P.full9_problem(512), 8, 0 if walk else OPT_NO_WALK)
+    try:
+        Fs, gs, _, _ = small.fidelity_grad(X[idx])
+    finally:
+        small.close()
+    for j, b in enumerate(idx):
+        _check(f"big_{tag}_vs_small_{b}", F[b], Fdx[b], Fs[j], gs[j], P.fd_tier(P.full9_problem(512), X[b]))
+
+
+def test_bench_size_plan_c3_golden():
+    """C3 (4 error sources) at a 2 048-evaluation pass: k_err_scan<S,1> and the sector error path."""
+    from tests.parity_log import record
+    g = _golden("c3")
+    fp = P.full9_problem(512, nerr=4)
+    X = np.stack([P.random_x(512, 5000 + s, small=True) for s in range(BIG)])
+    pos = [3, 1111, BIG - 1]
+    for p in pos:
+        X[p] = g["x"]
+    pl = _plan(fp, BIG)
+    try:
+        F, Fdx, d2, d2dx = pl.fidelity_grad(X)
+    finally:
+        pl.close()
+    nmain = 512
+    for p in pos:
+        _check(f"big_c3_at{p}", F[p], Fdx[p], g["F"], g["F_dx"], tight=True)
+        e0, s0 = np.max(np.abs(d2[p] - g["F_d2err"])), np.max(np.abs(g["F_d2err"]))
+        record(f"big_c3_at{p}", "F_d2err", e0, s0, T3 * s0 + T3_ABS)
+        assert e0 <= T3 * s0 + T3_ABS
+        err, sc = np.max(np.abs(d2dx[p][:nmain] - g["F_d2err_dx"][:nmain])), np.max(np.abs(g["F_d2err_dx"][:nmain]))
+        record(f"big_c3_at{p}", "F_d2err_dx", err, sc, T3 * sc + T3_ABS)
+        assert err <= T3 * sc + T3_ABS
+        ea = np.max(np.abs(d2dx[p][nmain:] - g["F_d2err_dx"][nmain:]))
+        record(f"big_c3_at{p}", "F_d2err_dx_add", ea, 0.0, T3_XADD_ABS)
+        assert ea <= T3_XADD_ABS
+
+
+def _high_norm_problem(nt):
+    """C2's model plus a detuning control on the Rydberg levels (n_p = 2): x[1, k] = +-900 at a few
+    steps gives |dt H|_1 ~ 27 there (Pade 13 with squarings in the reference; the walks' scaling
+    and squaring), every other step is C2's ordinary low-norm step."""
+    from robustgrape_amd import rydberg as R
+    from robustgrape_amd.operators import FN_LINEAR, VAR_X, OperatorBasisHamiltonian, Term
+    from robustgrape_amd.types import FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    Nr = np.diag([0, 0, 0, 0, 1, 1, 1, 1, 2]).astype(np.complex128)
+    H0 = OperatorBasisHamiltonian(list(R.rydberg_full_operator_basis().terms)
+                                  + [Term(Nr, var=VAR_X, index=1, func=FN_LINEAR)])
+    up = UnitaryRobustGRAPEProblem(t0=P.T0_TO, ntimes=nt, ndim=9, H0=H0, nb_additional_param=1)
+    fp = FidelityRobustGRAPEProblem(up, P.W_FULL9, R.cz_full_target())
+    Hc = lambda t, x, xa: H0(t, x, xa)  # noqa: E731
+    fo = FidelityRobustGRAPEProblem(UnitaryRobustGRAPEProblem(t0=P.T0_TO, ntimes=nt, ndim=9, H0=Hc,
+                                                              nb_additional_param=1),
+                                    P.W_FULL9, lambda xa: R.cz_with_1q_phase_full(xa[0]))
+    return fp, fo
+
+
+@pytest.mark.parametrize("walk", [True, False])
+def test_high_norm_steps_inside_long_chunks(walk):
+    """N_t = 512 in a 2 048-evaluation plan (chunks of 32 / 16 steps) with five high-norm steps
+    scattered through the chunks: the walks square inside the lane; the stored path parks the
+    steps for k_expm_high / k_grad_high, poisons the S = 2 chunk chains after them with NaN and
+    k_scan rechains those chunks from E.  Checked against the oracle (long steps: T2 tier)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_WALK
+    nt = 512
+    fp, fo = _high_norm_problem(nt)
+    rng = np.random.default_rng(11)
+    hot = [5, 40, 200, 333, 511]
+
+    def mkx(seed, with_hot):
+        r = np.random.default_rng(seed)
+        xm = np.stack([2 * np.pi * r.uniform(size=nt), r.uniform(-0.5, 0.5, size=nt)])
+        if with_hot:
+            xm[1, hot] = r.choice([-900.0, 900.0], size=len(hot))
+        return np.concatenate([xm.T.reshape(-1), [2 * np.pi * r.uniform()]])
+    X = np.stack([mkx(100 + s, s % 3 == 0) for s in range(BIG)])
+    pl = _plan(fp, BIG, 0 if walk else OPT_NO_WALK, nparam=2)
+    try:
+        F, Fdx, _, _ = pl.fidelity_grad(X)
+    finally:
+        pl.close()
+    tag = "walk" if walk else "stored"
+    for b in (0, 1, 999, BIG - 2):  # hot rows (b % 3 == 0) and ordinary rows
+        F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[b])[:2]
+        _check(f"hot_{tag}_{b}", F[b], Fdx[b], F0, g0, P.fd_tier(fp, X[b], nparam=2))
+    assert np.all(np.isfinite(F)) and np.all(np.isfinite(Fdx))
+    del rng
+
+
+def test_walk_single_calls_are_the_batch():
+    """Graph-replayed single evaluations through the walks are bitwise the batch's rows."""
+    fp = P.full9_problem(64)
+    X = np.stack([P.random_x(64, 40 + s) for s in range(70)])
+    pl = _plan(fp, 128)
+    try:
+        ref = pl.fidelity_grad(X)
+        for b in (0, 31, 69):
+            one = pl.fidelity_grad(X[b:b + 1])
+            assert one[0][0] == ref[0][b] and np.array_equal(one[1][0], ref[1][b])
+    finally:
+        pl.close()
