@@ -151,6 +151,8 @@ typedef struct grape_desc {
 #define GRAPE_OPT_NO_WALK 8     /* sector classes of <= 4 levels through the stored-intermediate
                                    kernels instead of the chunk walks (grape_walk.hpp) */
 #define GRAPE_OPT_NO_GRAPH 16   /* no HIP-graph replay of small host-array calls */
+#define GRAPE_OPT_WALK_RECOMPUTE 32 /* chunk walks: the gradient walk of the 4-level class recomputes the
+                                       nominal propagators instead of reading the forward walk's copy */
 
 typedef struct grape_plan grape_plan;
 

@@ -1,17 +1,29 @@
 # RobustGRAPEMI355X.jl -- ccall shim that routes RobustGRAPE.jl's hot path to libgrape.so.
 #
-# Keeps the reference's names (src/RobustGRAPE.jl:6-13): a FidelityRobustGRAPEProblem
-# whose H0 / error sources / target are `OperatorBasis` objects evaluates on the MI355X
-# through include/grape.h.  Julia is not installed in the build image, so this file is
-# not executed there; the same C entry points are exercised from Python by tests/.
+# Keeps the reference's names and argument types (src/RobustGRAPE.jl:6-13): the entry points
+# take the reference's own problem structs (src/Types.jl:12-56), and an `OperatorBasis` is a
+# `Function`, so it can be stored in their `H0::Function`, `Herror::Function` and
+# `target_unitary::Function` fields (Types.jl:13,35,55).  A FidelityRobustGRAPEProblem whose H0,
+# error sources and target are OperatorBasis objects evaluates on the MI355X through
+# include/grape.h; plain closures take the host-table fallback.  Julia is not installed in the
+# build image, so this file is not executed there; the same C entry points are exercised from
+# Python by tests/ and tests/test_julia_shim.py checks this file's signatures statically.
 module RobustGRAPEMI355X
 
 using LinearAlgebra
+import RobustGRAPE
+using RobustGRAPE: ErrorSource, UnitaryRobustGRAPEProblem, FidelityRobustGRAPEProblem
 
 export OperatorTerm, OperatorBasis, calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
        calculate_interaction_error_operators, calculate_expectation_values, grape_expm_batch
 
 const libgrape = normpath(joinpath(@__DIR__, "..", "robustgrape_amd", "libgrape.so"))
+const GRAPE_ABI_VERSION = 6  # include/grape.h
+
+function __init__()
+    v = ccall((:grape_abi_version, libgrape), Cint, ())
+    v == GRAPE_ABI_VERSION || error("libgrape ABI $v, this shim speaks $GRAPE_ABI_VERSION")
+end
 
 # grape_var / grape_func (include/grape.h)
 const VAR_ONE, VAR_X, VAR_XADD, VAR_TSTEP = Int32(0), Int32(1), Int32(2), Int32(3)
@@ -47,10 +59,11 @@ end
 OperatorTerm(op; var=VAR_ONE, index=1, func=FN_ONE, a=1.0, b=0.0, scale=1.0) =
     OperatorTerm(ComplexF64.(op), var, Int32(index - 1), func, a, b, ComplexF64(scale))
 
-"Callable like the reference's closures: H0(nt, x, x_add) / Herror(nt, x, x_add, err) / target(x_add)."
-struct OperatorBasis
+"""Callable like the reference's closures: H0(nt, x, x_add) / Herror(nt, x, x_add, err) /
+target(x_add).  A subtype of `Function`, so it fits the reference's `H0::Function`,
+`Herror::Function` and `target_unitary::Function` fields (src/Types.jl:13,35,55)."""
+struct OperatorBasis <: Function
     terms::Vector{OperatorTerm}
-    scaled_by_err::Bool
 end
 function _coef(t::OperatorTerm, nt, x, x_add)
     v = t.var == VAR_ONE ? 1.0 : t.var == VAR_X ? x[t.index+1] : t.var == VAR_XADD ? x_add[t.index+1] : Float64(nt)
@@ -71,12 +84,27 @@ mutable struct DevicePlan
     handle::Ptr{Cvoid}
     keep::Vector{Any}      # arrays the descriptor points into
     nx::Int; nerr::Int
+    problem::Any           # the problem the plan was built for (guards the objectid key)
 end
 
-const _plans = IdDict{Any,DevicePlan}()
+# One plan per (problem, nparam, kind): :device (operator-basis fidelity path, max_batch 256),
+# :unitary (operator-basis single-x analysis entries, max_batch 1) and :table (closure fallback).
+const _plans = Dict{Tuple{UInt,Int,Symbol},DevicePlan}()
 
-function device_plan(fp, nparam::Int; device::Integer=0, max_batch::Integer=256)
-    get!(_plans, fp) do
+function _cached(make, problem, nparam::Int, kind::Symbol)
+    key = (objectid(problem), nparam, kind)
+    p = get(_plans, key, nothing)
+    if p === nothing || p.problem !== problem
+        p = make()
+        p.problem = problem
+        _plans[key] = p
+    end
+    return p
+end
+
+function device_plan(fp::FidelityRobustGRAPEProblem, nparam::Int; device::Integer=0, max_batch::Integer=256,
+                     kind::Symbol=:device)
+    _cached(fp, nparam, kind) do
         up = fp.unitary_problem
         ops = Matrix{ComplexF64}[]
         tr(terms) = [GrapeTerm((push!(ops, t.op); Int32(length(ops) - 1)), t.var, t.index, t.func,
@@ -100,7 +128,7 @@ function device_plan(fp, nparam::Int; device::Integer=0, max_batch::Integer=256)
             _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
                          desc, device, out))
         end
-        p = DevicePlan(out[], keep, nparam * up.ntimes + up.nb_additional_param, length(up.error_sources))
+        p = DevicePlan(out[], keep, nparam * up.ntimes + up.nb_additional_param, length(up.error_sources), nothing)
         finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
         p
     end
@@ -109,8 +137,8 @@ end
 const GRAPE_DESC_HOST_TABLES = Int32(1)
 
 # Closure fallback (grape.h GRAPE_DESC_HOST_TABLES): no operator basis in the descriptor.
-function table_plan(fp, nparam::Int; device::Integer=0)
-    get!(_plans, fp) do
+function table_plan(fp::FidelityRobustGRAPEProblem, nparam::Int; device::Integer=0)
+    _cached(fp, nparam, :table) do
         up = fp.unitary_problem
         ne = length(up.error_sources)
         pdiag = Float64.(diag(fp.projector))
@@ -123,7 +151,7 @@ function table_plan(fp, nparam::Int; device::Integer=0)
             _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
                          desc, device, out))
         end
-        p = DevicePlan(out[], Any[pdiag, pfull], nparam * up.ntimes + up.nb_additional_param, ne)
+        p = DevicePlan(out[], Any[pdiag, pfull], nparam * up.ntimes + up.nb_additional_param, ne, nothing)
         finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
         p
     end
@@ -183,11 +211,28 @@ function closure_interaction_tables(up, x::Vector{Float64}, np::Int)
     return H0, Oerr
 end
 
-is_operator_basis(fp) = fp.unitary_problem.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis &&
-                        all(es.Herror isa OperatorBasis for es in fp.unitary_problem.error_sources)
+is_operator_basis(fp::FidelityRobustGRAPEProblem) =
+    fp.unitary_problem.H0 isa OperatorBasis && fp.target_unitary isa OperatorBasis &&
+    all(es.Herror isa OperatorBasis for es in fp.unitary_problem.error_sources)
+
+# The unitary-level entry points take a UnitaryRobustGRAPEProblem (UnitaryCalculations.jl:20,180);
+# the descriptor needs a projector and a target, neither of which enters their outputs: wrap the
+# problem with the identity (an OperatorBasis when H0 is one, so the device path serves it).
+const _wrapped = Dict{UInt,Tuple{UnitaryRobustGRAPEProblem,FidelityRobustGRAPEProblem}}()
+function fidelity_wrapper(problem::UnitaryRobustGRAPEProblem)
+    w = get(_wrapped, objectid(problem), nothing)
+    w !== nothing && w[1] === problem && return w[2]
+    d = problem.ndim
+    eye = Matrix{ComplexF64}(I, d, d)
+    ob = problem.H0 isa OperatorBasis && all(es.Herror isa OperatorBasis for es in problem.error_sources)
+    target = ob ? OperatorBasis([OperatorTerm(eye)]) : (x_add -> eye)
+    fp = FidelityRobustGRAPEProblem(unitary_problem=problem, projector=Matrix{Float64}(I, d, d), target_unitary=target)
+    _wrapped[objectid(problem)] = (problem, fp)
+    return fp
+end
 
 "Drop-in for src/FidelityCalculations.jl:19-119: (F, F_dx_tot, F_d2err, F_d2err_dx_tot)."
-function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
+function calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::Vector{<:Real})
     up = fp.unitary_problem
     xm = length(x) - up.nb_additional_param
     @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
@@ -217,8 +262,9 @@ function calculate_fidelity_and_derivatives(fp, x::AbstractVector{<:Real})
 end
 
 "Drop-in for src/UnitaryCalculations.jl:20-155: (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add)."
-function calculate_unitary_and_derivatives(fp, x::AbstractVector{<:Real})
-    up = fp.unitary_problem
+function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
+    fp = fidelity_wrapper(problem)
+    up = problem
     d, nt, na, ne = up.ndim, up.ntimes, up.nb_additional_param, length(up.error_sources)
     xm = length(x) - na
     @assert mod(xm, nt) == 0 "Control parameter size must be a multiple of time steps"
@@ -237,7 +283,7 @@ function calculate_unitary_and_derivatives(fp, x::AbstractVector{<:Real})
         end
         return outs
     end
-    p = device_plan(fp, np; max_batch=1)
+    p = device_plan(fp, np; max_batch=1, kind=:unitary)
     GC.@preserve xv outs begin
         _check(ccall((:grape_unitary_derivs, libgrape), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64},
@@ -247,8 +293,9 @@ function calculate_unitary_and_derivatives(fp, x::AbstractVector{<:Real})
 end
 
 "Drop-in for src/UnitaryCalculations.jl:180-204: (ndim, ndim, ntimes, nerr)."
-function calculate_interaction_error_operators(fp, x::AbstractVector{<:Real})
-    up = fp.unitary_problem
+function calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
+    fp = fidelity_wrapper(problem)
+    up = problem
     np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
     O = zeros(ComplexF64, up.ndim, up.ndim, up.ntimes, length(up.error_sources))
@@ -262,7 +309,7 @@ function calculate_interaction_error_operators(fp, x::AbstractVector{<:Real})
         end
         return O
     end
-    p = device_plan(fp, np; max_batch=1)
+    p = device_plan(fp, np; max_batch=1, kind=:unitary)
     GC.@preserve xv O begin
         _check(ccall((:grape_interaction_error_operators, libgrape), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}), p.handle, xv, O))
@@ -271,7 +318,7 @@ function calculate_interaction_error_operators(fp, x::AbstractVector{<:Real})
 end
 
 "Drop-in for src/FidelityCalculations.jl:368-390: (ntimes, nerr)."
-function calculate_expectation_values(fp, x::AbstractVector{<:Real})
+function calculate_expectation_values(fp::FidelityRobustGRAPEProblem, x::Vector{<:Real})
     up = fp.unitary_problem
     np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
@@ -286,7 +333,7 @@ function calculate_expectation_values(fp, x::AbstractVector{<:Real})
         end
         return ev
     end
-    p = device_plan(fp, np; max_batch=1)
+    p = device_plan(fp, np; max_batch=1, kind=:unitary)
     GC.@preserve xv ev begin
         _check(ccall((:grape_expectation_values, libgrape), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), p.handle, xv, ev))

@@ -160,7 +160,7 @@ struct grape_plan {
     // the sector head over the assembled U (SH)
     struct SecBuf {
         cd *E = nullptr, *Q = nullptr, *Mc = nullptr, *Carry = nullptr, *Ub = nullptr, *slots = nullptr,
-           *ops = nullptr, *opsT = nullptr, *Msec = nullptr, *Tc = nullptr, *wscr = nullptr;
+           *ops = nullptr, *opsT = nullptr, *Msec = nullptr, *Tc = nullptr, *wscr = nullptr, *Ew = nullptr;
         int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr;
         double *part = nullptr;
         // error sources: local-frame images, per-chunk triples, Tot / M_e blocks, F_d2err_dx terms
@@ -229,7 +229,7 @@ static void free_plan(grape_plan *p) {
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
         void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part,
-                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr};
+                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr, c.Ew};
         for (void *b : sbufs)
             if (b) (void)hipFree(b);
     }
@@ -905,12 +905,19 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // chunk walks (grape_walk.hpp): classes of <= kWalkMaxD levels without error sources
             Ps.walk = (S <= grape::kWalkMaxD && P.ne == 0 && P.np <= grape::kWalkMaxNpA && P.na <= grape::kWalkMaxNpA &&
                        !(P.opts & GRAPE_OPT_NO_WALK)) ? 1 : 0;
+            // the forward walk hands its propagators to the gradient walk (HBM, lane-minor) where the
+            // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
+            // 6.52 M evals/s; for the 2-level class it lost, 0.72 -> 1.01 ms per pass)
+            Ps.walk_store_e = Ps.walk && S == grape::kWalkMaxD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
             const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
             grape_plan::SecBuf &b = p->sb[cl];
             const size_t ne = (size_t)P.ne, R2 = (P.ne > 0 || Ps.walk) ? 0 : R;  // k_expm_grad parking: no error sources only
             const size_t RE = Ps.walk ? 0 : R;  // the walks store no E / Q
+            const size_t lanes_pad = (MB * Ps.nchunks + grape::kWalkBlockA - 1) / grape::kWalkBlockA * grape::kWalkBlockA;
+            if (Ps.walk_store_e && dalloc(&b.Ew, (size_t)sc.nsec * Ps.L * TS * lanes_pad) != hipSuccess)
+                return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sector walks)"));
             if (Ps.walk && (dalloc(&b.Tc, R * Ps.nchunks * TS) != hipSuccess ||
                             dalloc(&b.wscr, 2 * (size_t)sc.nsec * ((MB * Ps.nchunks + grape::kWalkBlockA - 1) /
                                                                   grape::kWalkBlockA * grape::kWalkBlockA) * TS) != hipSuccess))
@@ -1064,6 +1071,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.sink = p->d_sink;
             B.Tc = sb.Tc;  // chunk walks (null otherwise)
             B.wscr = sb.wscr;
+            B.Ew = sb.Ew;
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
             sp.part_err[cl] = sb.part_err;

@@ -90,6 +90,8 @@ struct DevProblem {
     int nsec;
     size_t sec_ops;
     int walk;            // sector class served by the chunk walks (grape_walk.hpp: k_walk_fwd / k_walk_grad)
+    int walk_store_e;    // ... k_walk_fwd stores the nominal propagators for k_walk_grad (B.Ew) instead of
+                         //     k_walk_grad recomputing them
     int opts;            // grape_desc.reserved[1]: GRAPE_OPT_* (fixed at plan creation)
 };
 
@@ -133,6 +135,7 @@ struct DevBatch {
     // chunk walks (grape_walk.hpp): k_scan starts from the chunk totals in Tc when it is set
     cd *Tc;                 // [nb][nchunks][D][D] row-major chunk totals T_c (k_walk_fwd), else null
     cd *wscr;               // [nsec][nb / nsec][nchunks][2][D][D] per-lane scratch of the squaring path
+    cd *Ew;                 // walk_store_e: [nsec/NS][L][NS][D*D][lanes] nominal E_k, lane-minor (coalesced)
 };
 
 // Trig of the last argument seen by one builder: the operator bases pair cos(arg) and sin(arg)

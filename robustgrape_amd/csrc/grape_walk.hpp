@@ -46,20 +46,6 @@
 namespace grape {
 
 constexpr int kWalkBlock = kWalkBlockA;
-// Waves per SIMD the launch bounds ask for (register budget 512 / w).  k_walk_grad at D = 4
-// holds X (64 VGPRs), the A / A^2 / A^3 set of the eps-variant (96) and a column of E' with its
-// Horner temporaries while E sits in LDS: ~290 registers, so it runs one wave per SIMD (the
-// overflow goes to AGPRs, not to scratch); everything else fits two or more.
-template <int D, bool GRAD>
-struct WalkWaves {
-    static constexpr int value = D <= 2 ? 4 : D == 3 ? (GRAD ? 2 : 3) : GRAD ? 1 : 2;
-};
-template <int D, bool GRAD>
-struct WalkLds {  // E in the lane's LDS slot (k_walk_grad, D = 4) or in registers
-    static constexpr bool value = GRAD && D >= 4;
-    static constexpr int stride = D * D + 1;  // complex elements per lane slot
-};
-
 // 1/k! as literals (the column kernels index them with compile-time constants)
 __device__ __forceinline__ constexpr double inv_fact(int k) {
     return k == 0 ? 1.0 : k == 1 ? 1.0 : k == 2 ? 0.5 : k == 3 ? 1.0 / 6 : k == 4 ? 1.0 / 24 : k == 5 ? 1.0 / 120
@@ -244,11 +230,50 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s) {
     return 13;
 }
 
+// x = column i of the same polynomial without a stored A^2: column i of A^2 is A (A e_i), one
+// matrix-vector product per column (+56 FMAs at D = 4) for 32 fewer live registers.
+template <int D>
+__device__ __forceinline__ void sm_taylor_col_na2(bool small, int i, const SM<D> &A, const SM<D> &A3, cd (&x)[D]) {
+    cd a2[D];  // column i of A is read from A itself (no copy)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        cd c = czero();
+#pragma unroll
+        for (int k = 0; k < D; ++k) sm_mac<D, false>(c, A, j, k, sm_el<D, false>(A, k, i));
+        a2[j] = c;
+    }
+    {
+        const double k0 = small ? inv_fact(3) : inv_fact(9), k1 = small ? inv_fact(4) : inv_fact(10),
+                     k2 = small ? inv_fact(5) : inv_fact(11), k3 = small ? inv_fact(6) : inv_fact(12);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, a2[j], cscale(k3, sm_el<D, false>(A3, j, i))));
+            if (j == i) x[j].re += k0;
+        }
+    }
+#pragma unroll
+    for (int st = 2; st >= 0; --st) {
+        if (st == 0 || !small) {
+            cd t[D];
+            sm_matvec<D, false>(A3, x, t);
+            const double k0 = inv_fact(3 * st), k1 = inv_fact(3 * st + 1), k2 = inv_fact(3 * st + 2);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, a2[j], t[j]));
+                if (j == i) x[j].re += k0;
+            }
+        }
+    }
+    pin<D>(x);
+}
+
 // exp(A), column by column into sink(i, column i).  The squaring path (kind 13, rare) parks
 // the scaled approximant in the lane's global scratch slot `scr` (two D x D column-major
 // tiles) and squares it there element by element, so that it adds no live registers to the
-// common path.
-template <int D, class Sink>
+// common path.  FENCE: pin every column and keep the scheduler from overlapping them (register
+// discipline at D = 4; at D <= 3 the columns and sectors may interleave for ILP).  KEEP_A2:
+// keep A^2 through the column loop (else regenerate its columns, sm_taylor_col_na2).
+template <int D, bool FENCE, bool KEEP_A2, class Sink>
 __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
     int s = 0;
     const int kind = sm_regime<D>(A, s);
@@ -259,21 +284,25 @@ __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
             const double sn = sin(A.d[i]), cn = cos(A.d[i]);  // exp(0) (cos, sin), as the row-group path
 #pragma unroll
             for (int j = 0; j < D; ++j) x[j] = (j == i) ? cmake(cn, sn) : czero();
-            pin<D>(x);
+            if (FENCE) pin<D>(x);
             sink(i, x);
         }
         return;
     }
     SM<D> A2, A3;
     sm_cube<D>(A, A2, A3);
+    auto col = [&](bool small, int i, cd (&x)[D]) {
+        if constexpr (KEEP_A2) sm_taylor_col<D>(small, i, A, A2, A3, x);
+        else sm_taylor_col_na2<D>(small, i, A, A3, x);
+    };
     if (kind != 13) {
         const bool small = kind == 3;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             cd x[D];
-            sm_taylor_col<D>(small, i, A, A2, A3, x);
+            col(small, i, x);
             sink(i, x);
-            __builtin_amdgcn_sched_barrier(0);
+            if (FENCE) __builtin_amdgcn_sched_barrier(0);
         }
         return;
     }
@@ -281,7 +310,7 @@ __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {  // (unrolled: register arrays are only ever indexed by constants)
         cd x[D];
-        sm_taylor_col<D>(false, i, A, A2, A3, x);
+        col(false, i, x);
 #pragma unroll
         for (int j = 0; j < D; ++j) T[i * D + j] = x[j];
     }
@@ -308,7 +337,7 @@ __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
         cd x[D];
 #pragma unroll
         for (int j = 0; j < D; ++j) x[j] = T[i * D + j];
-        pin<D>(x);
+        if (FENCE) pin<D>(x);
         sink(i, x);
     }
 }
@@ -346,36 +375,34 @@ __device__ __forceinline__ Pert pload(cptr<VSpec> p, int i) {
     return q;
 }
 
-// The step's controls x[:, k] (np <= kWalkMaxNp) and x_add (na <= kWalkMaxNa) in registers:
+// The step's controls x[:, k] (np <= 2) and x_add (na <= 2) in registers:
 // the next step's controls are loaded one step ahead, so the build never waits on memory.
-struct WalkX {  // four named registers each (an array picked by index would be demoted to scratch)
-    double k0, k1, k2, k3;  // x[:, k]
-    double a0, a1, a2, a3;  // x_add
-    __device__ __forceinline__ double xk(int i) const { return i == 0 ? k0 : i == 1 ? k1 : i == 2 ? k2 : k3; }
-    __device__ __forceinline__ double xa(int i) const { return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : a3; }
+struct WalkX {  // named registers (an array picked by index would be demoted to scratch)
+    double k0, k1;  // x[:, k]  (np <= kWalkMaxNpA = 2)
+    double a0, a1;  // x_add    (na <= 2)
+    __device__ __forceinline__ double xk(int i) const { return i == 0 ? k0 : k1; }
+    __device__ __forceinline__ double xa(int i) const { return i == 0 ? a0 : a1; }
 };
-struct X4 {
-    double v0, v1, v2, v3;
+struct X2 {
+    double v0, v1;
 };
-__device__ __forceinline__ X4 walk_load_x(int n, const double *xs) {  // n (uniform) <= 4 values
-    X4 r;
-    r.v0 = n > 0 ? xs[0] : 0.0;
-    r.v1 = n > 1 ? xs[1] : 0.0;
-    r.v2 = n > 2 ? xs[2] : 0.0;
-    r.v3 = n > 3 ? xs[3] : 0.0;
+// Unconditional loads (the second one clamped into the vector): a load under a branch leaves the
+// compiler without a static count of the outstanding vector-memory operations, and it then waits
+// with vmcnt(0) -- for every store of the step too -- before the prefetched value is used.
+__device__ __forceinline__ X2 walk_load_x(int n, const double *xs) {  // n (uniform, >= 1 here) <= 2 values
+    X2 r;
+    const double a = xs[0], b = xs[n > 1 ? 1 : 0];
+    r.v0 = n > 0 ? a : 0.0;
+    r.v1 = n > 1 ? b : 0.0;
     return r;
 }
-__device__ __forceinline__ void walk_set_xk(WalkX &X, const X4 &r) {
+__device__ __forceinline__ void walk_set_xk(WalkX &X, const X2 &r) {
     X.k0 = r.v0;
     X.k1 = r.v1;
-    X.k2 = r.v2;
-    X.k3 = r.v3;
 }
-__device__ __forceinline__ void walk_set_xa(WalkX &X, const X4 &r) {
+__device__ __forceinline__ void walk_set_xa(WalkX &X, const X2 &r) {
     X.a0 = r.v0;
     X.a1 = r.v1;
-    X.a2 = r.v2;
-    X.a3 = r.v3;
 }
 
 // term_coef (grape_kernels.hpp) with the variable read from registers
@@ -400,16 +427,20 @@ __device__ __forceinline__ cd walk_coef(const Term &t, int nt1, const WalkX &X, 
     return cmul(cmake(t.sre, t.sim), cmake(fr, fi));
 }
 
-// A = -i dt H(x_k perturbed by pp), compressed: the builder of ItemBuilder with the sector's
-// row-major operators, term by term in order (the same cmac operand roles), diagonal as the
-// imaginary part of the same complex MAC.
-template <int D>
+// A_w = -i dt H_w(x_k perturbed by pp) for the NS sectors w of this lane, compressed: the
+// builder of ItemBuilder with each sector's row-major operators, term by term in order (the same
+// cmac operand roles), diagonal as the imaginary part of the same complex MAC.  The term
+// coefficients (the trig of the controls) are computed once for all NS sectors.
+template <int D, int NS>
 __device__ __forceinline__ void walk_build(const DevProblem &P, cptr<cd> ops, const WalkX &X, int nt1, const Pert &pp,
-                                           SM<D> &A) {
+                                           SM<D> (&A)[NS]) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) A.d[j] = 0.0;
+    for (int w = 0; w < NS; ++w) {
 #pragma unroll
-    for (int t = 0; t < SM<D>::NU; ++t) A.u[t] = czero();
+        for (int j = 0; j < D; ++j) A[w].d[j] = 0.0;
+#pragma unroll
+        for (int t = 0; t < SM<D>::NU; ++t) A[w].u[t] = czero();
+    }
     TrigCache tc;
     const cptr<Term> terms = as_constant(P.h0);
 #pragma unroll 1
@@ -417,98 +448,137 @@ __device__ __forceinline__ void walk_build(const DevProblem &P, cptr<cd> ops, co
         const Term tm = tload(terms, t);
         const cd c = walk_coef(tm, nt1, X, pp, tc);
         const cd g = cmake(P.dt * c.im, -(P.dt * c.re));  // -i dt c
-        const cptr<cd> op = ops + (size_t)tm.op * D * D;
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const cd o = cload(op, j * D + j);
-            A.d[j] = fma(g.im, o.re, fma(g.re, o.im, A.d[j]));
+        for (int w = 0; w < NS; ++w) {
+            const cptr<cd> op = ops + (size_t)w * P.sec_ops + (size_t)tm.op * D * D;
 #pragma unroll
-            for (int k = j + 1; k < D; ++k) cmac(A.u[uix(D, j, k)], g, cload(op, j * D + k));
+            for (int j = 0; j < D; ++j) {
+                const cd o = cload(op, j * D + j);
+                A[w].d[j] = fma(g.im, o.re, fma(g.re, o.im, A[w].d[j]));
+#pragma unroll
+                for (int k = j + 1; k < D; ++k) cmac(A[w].u[uix(D, j, k)], g, cload(op, j * D + k));
+            }
         }
     }
 }
 
-// The lane's E_k: registers (D <= 3) or its LDS slot (row-major, D = 4).
+// A lane's D x D matrix: registers, or (D = 4, where registers run out) its private LDS slot,
+// row-major, 17 complex apart so that the 16-B accesses of 16 lanes hit 64 distinct banks.
 template <int D, bool LDS>
-struct EStore;
+struct MStore;
 template <int D>
-struct EStore<D, false> {
+struct MStore<D, false> {
     cd e[D][D];
-    __device__ __forceinline__ void put_col(int i, const cd (&x)[D]) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) e[j][i] = x[j];
-    }
     __device__ __forceinline__ cd at(int j, int k) const { return e[j][k]; }
-    __device__ __forceinline__ const EStore &opaque() const { return *this; }
+    __device__ __forceinline__ void set(int j, int k, cd v) { e[j][k] = v; }
+    __device__ __forceinline__ const MStore &opaque() const { return *this; }
 };
+using lds_cd = __attribute__((address_space(3))) cd;  // typed LDS pointer: ds_read / ds_write, never flat
 template <int D>
-struct EStore<D, true> {
-    cd *p;
-    __device__ __forceinline__ void put_col(int i, const cd (&x)[D]) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) p[j * D + i] = x[j];
+struct MStore<D, true> {
+    static constexpr int kStride = D * D + 1;
+    lds_cd *p;
+    __device__ __forceinline__ cd at(int j, int k) const { return cmake(p[j * D + k].re, p[j * D + k].im); }
+    __device__ __forceinline__ void set(int j, int k, cd v) {
+        p[j * D + k].re = v.re;
+        p[j * D + k].im = v.im;
     }
-    __device__ __forceinline__ cd at(int j, int k) const { return p[j * D + k]; }
+    __device__ __forceinline__ static lds_cd *slot(cd *lds_base) {  // this lane's slot
+        return (lds_cd *)(lds_base) + threadIdx.x * kStride;
+    }
     // a copy whose address the compiler cannot see through: its loads stay where they are
-    // written (no hoisting of E's 64 VGPRs out of a loop or across an exponential)
-    __device__ __forceinline__ EStore opaque() const {
-        EStore o{p};
+    // written (no hoisting of 64 VGPRs of LDS reads out of a loop or across an exponential)
+    __device__ __forceinline__ MStore opaque() const {
+        MStore o{p};
         asm volatile("" : "+v"(o.p));
         return o;
     }
 };
 
-// lane -> (sector w = blockIdx.y, evaluation be, chunk c); sub-evaluation bp = be * nsec + w.
-// Lanes past the end (ok = false) run the walk on clamped indices and store nothing, so that
-// every loop in the walks has a wave-uniform trip count (scalar loads of the term tables).
+// Launch geometry: one lane per (evaluation be, chunk c) and group of NS sectors (w0 = NS *
+// blockIdx.y); sub-evaluation of sector w: be * nsec + w.  Lanes past the end (ok = false) run
+// the walk on clamped indices and store nothing, so that every loop in the walks has a
+// wave-uniform trip count (scalar loads of the term tables).
 struct WalkLane {
-    int w, be, c, bp;
-    long slot;  // (w, be, c) index: the lane's scratch slot
+    int w0, be, c;
+    long slot;  // the lane's scratch slot (NS consecutive pairs of D x D tiles)
     bool ok;
 };
+template <int NS>
 __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatch &B) {
     WalkLane L;
     const int ns = P.nsec > 1 ? P.nsec : 1;
     const long per = (long)(B.nb / ns) * P.nchunks;
     const long g = (long)blockIdx.x * kWalkBlock + threadIdx.x;
-    L.w = blockIdx.y;
+    L.w0 = blockIdx.y * NS;
     L.ok = g < per;
     const long gg = L.ok ? g : 0;
     L.be = (int)(gg / P.nchunks);
     L.c = (int)(gg - (long)L.be * P.nchunks);
-    L.bp = L.be * ns + L.w;
     // own scratch slot for every lane, past-the-end ones included (they walk lane 0's inputs)
     const long per_pad = (per + kWalkBlock - 1) / kWalkBlock * kWalkBlock;
-    L.slot = (long)L.w * per_pad + g;
+    L.slot = (long)blockIdx.y * per_pad + g;
     return L;
 }
 
-template <int D>
-__global__ __launch_bounds__(kWalkBlock, (WalkWaves<D, false>::value)) void k_walk_fwd(DevProblem P, DevBatch B) {
+#ifndef GRAPE_WALK_G4_KEEP_A2_NOM
+#define GRAPE_WALK_G4_KEEP_A2_NOM 1
+#endif
+#ifndef GRAPE_WALK_G4_WAVES
+#define GRAPE_WALK_G4_WAVES 1
+#endif
+#ifndef GRAPE_WALK_G4S_WAVES  // k_walk_grad<4> with stored propagators
+#define GRAPE_WALK_G4S_WAVES 1
+#endif
+#ifndef GRAPE_WALK_G4_XLDS  // k_walk_grad<4>: 1 = X / Y in the LDS slot and E in registers, 0 = the reverse
+#define GRAPE_WALK_G4_XLDS 1
+#endif
+template <int D, int NS>
+struct WalkCfg {
+    static constexpr bool FENCE = D >= 4;        // per-column scheduling fences (register discipline)
+    static constexpr bool E_LDS_FWD = false;     // k_walk_fwd keeps E in registers
+    static constexpr bool X_LDS = D >= 4 && NS == 1 && GRAPE_WALK_G4_XLDS;  // k_walk_grad: X / Y in LDS
+    static constexpr bool E_LDS_GRAD = D >= 4 && NS == 1 && !GRAPE_WALK_G4_XLDS;  // ... or E in LDS
+    static constexpr bool KEEP_A2_GRAD = D < 4;  // k_walk_grad<4>: regenerate A^2 columns (registers)
+    static constexpr bool KEEP_A2_NOM = D < 4 || GRAPE_WALK_G4_KEEP_A2_NOM;
+    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : 3) : 2;
+    static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? 3 : 2) : D == 3 ? (NS == 1 ? 2 : 1)
+                                                                              : GRAPE_WALK_G4_WAVES;
+    static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? 1 : GRAPE_WALK_G4S_WAVES;
+};
+
+// STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
+template <int D, int NS, bool STORE>
+__global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_walk_fwd(DevProblem P, DevBatch B) {
+    using C = WalkCfg<D, NS>;
     constexpr int TS = D * D;
-    constexpr bool ELDS = WalkLds<D, false>::value;
-    const WalkLane L = walk_lane(P, B);
+    const WalkLane L = walk_lane<NS>(P, B);
+    const int ns = P.nsec > 1 ? P.nsec : 1;
     const double *xb = B.x + (size_t)L.be * P.nx;
-    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w * P.sec_ops;
-    cd *scr = B.wscr + (size_t)L.slot * 2 * TS;
+    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
+    cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
     Pert none;
     none.var = -1;
     none.index = 0;
     none.delta = 0.0;
-    EStore<D, ELDS> E;
-    if constexpr (ELDS) {
-        __shared__ cd lds[kWalkBlock * WalkLds<D, ELDS>::stride];
-        E.p = lds + threadIdx.x * WalkLds<D, ELDS>::stride;
+    const size_t lanes = (size_t)gridDim.x * kWalkBlock, lane = (size_t)blockIdx.x * kWalkBlock + threadIdx.x;
+    MStore<D, C::E_LDS_FWD> E;
+    if constexpr (C::E_LDS_FWD) {
+        __shared__ cd lds[kWalkBlock * MStore<D, true>::kStride];
+        E.p = MStore<D, true>::slot(lds);
     }
     WalkX X;
     walk_set_xa(X, walk_load_x(P.na, xb + (size_t)P.np * P.Nt));  // x_add
     const int k0 = L.c * P.L;
-    X4 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
-    cd Q[D][D];
+    X2 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
+    cd Q[NS][D][D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
+    for (int w = 0; w < NS; ++w) {
 #pragma unroll
-        for (int i = 0; i < D; ++i) Q[j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) Q[w][j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+        }
     }
 #pragma unroll 1
     for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t leave Q alone
@@ -516,65 +586,109 @@ __global__ __launch_bounds__(kWalkBlock, (WalkWaves<D, false>::value)) void k_wa
         const bool act = k0 + jj < P.Nt;
         walk_set_xk(X, xn);
         xn = walk_load_x(P.np, xb + (size_t)min(k + 1, P.Nt - 1) * P.np);  // next step's controls
-        SM<D> A;
-        walk_build<D>(P, ops, X, k + 1, none, A);
-        walk_expm<D>(A, scr, [&](int i, const cd (&x)[D]) { E.put_col(i, x); });
+        SM<D> A[NS];
+        walk_build<D, NS>(P, ops, X, k + 1, none, A);
 #pragma unroll
-        for (int i = 0; i < D; ++i) {  // column i of E_k Q (in place: it reads only column i)
-            cd q[D], t[D];
+        for (int w = 0; w < NS; ++w) {
+            walk_expm<D, C::FENCE, true>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
 #pragma unroll
-            for (int m = 0; m < D; ++m) q[m] = Q[m][i];
+                for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
+            });
+            if constexpr (STORE) {  // the gradient walk's copy: lane-minor, one coalesced 1-KB store per element
+                cd *ew = B.Ew + ((((size_t)blockIdx.y * P.L + jj) * NS + w) * TS) * lanes + lane;
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
-                cd c = czero();
+                for (int j = 0; j < D; ++j) {
 #pragma unroll
-                for (int m = 0; m < D; ++m) cmac(c, q[m], E.at(j, m));
-                t[j] = c;
+                    for (int i = 0; i < D; ++i) ew[(size_t)(j * D + i) * lanes] = E.at(j, i);
+                }
             }
 #pragma unroll
-            for (int j = 0; j < D; ++j) Q[j][i] = cmake(act ? t[j].re : Q[j][i].re, act ? t[j].im : Q[j][i].im);
+            for (int i = 0; i < D; ++i) {  // column i of E_k Q (in place: it reads only column i)
+                cd q[D], t[D];
+#pragma unroll
+                for (int m = 0; m < D; ++m) q[m] = Q[w][m][i];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    cd c = czero();
+#pragma unroll
+                    for (int m = 0; m < D; ++m) cmac(c, q[m], E.at(j, m));
+                    t[j] = c;
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    Q[w][j][i] = cmake(act ? t[j].re : Q[w][j][i].re, act ? t[j].im : Q[w][j][i].im);
+            }
         }
     }
     if (L.ok) {
-        cd *dst = B.Tc + ((size_t)L.bp * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
+        for (int w = 0; w < NS; ++w) {
+            cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
-            for (int i = 0; i < D; ++i) dst[j * D + i] = Q[j][i];
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int i = 0; i < D; ++i) dst[j * D + i] = Q[w][j][i];
+            }
         }
     }
 }
 
-template <int D>
-__global__ __launch_bounds__(kWalkBlock, (WalkWaves<D, true>::value)) void k_walk_grad(DevProblem P, DevBatch B) {
+// STORED: the nominal propagators come from the forward walk's copy (B.Ew, prefetched one step
+// ahead) instead of being recomputed -- one exponential of the three per step saved for 512 B of
+// HBM traffic per step and sector.
+// NVG: the number of gradient parameters when known at compile time (1: C1 / C2 / C4), else 0
+// (a runtime loop) -- a static count of the F_dx stores per step keeps the prefetch waits exact.
+template <int D, int NS, bool STORED, int NVG>
+__global__ __launch_bounds__(kWalkBlock, (STORED ? WalkCfg<D, NS>::WAVES_GRAD_STORED : WalkCfg<D, NS>::WAVES_GRAD))
+void k_walk_grad(DevProblem P, DevBatch B) {
+    using C = WalkCfg<D, NS>;
     constexpr int TS = D * D;
-    constexpr bool ELDS = WalkLds<D, true>::value;
-    const WalkLane L = walk_lane(P, B);
+    const WalkLane L = walk_lane<NS>(P, B);
+    const int ns = P.nsec > 1 ? P.nsec : 1;
     const double *xb = B.x + (size_t)L.be * P.nx;
-    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w * P.sec_ops;
-    cd *scr = B.wscr + (size_t)L.slot * 2 * TS;
+    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
+    cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
     Pert none;
     none.var = -1;
     none.index = 0;
     none.delta = 0.0;
-    EStore<D, ELDS> E;
-    if constexpr (ELDS) {
-        __shared__ cd lds[kWalkBlock * WalkLds<D, ELDS>::stride];
-        E.p = lds + threadIdx.x * WalkLds<D, ELDS>::stride;
+    // X_{k-1} = C_{k-1} M C_{k-1}^dag of every sector (M'_c at the chunk start); Y_k in place
+    constexpr bool XL = C::X_LDS && !STORED, EL = C::E_LDS_GRAD && !STORED;
+    MStore<D, XL> X[NS];
+    MStore<D, EL> E[NS];
+    if constexpr (XL || EL) {
+        static_assert(NS == 1 && !(XL && EL), "one LDS slot per lane");
+        __shared__ cd lds[kWalkBlock * MStore<D, true>::kStride];
+        if constexpr (XL) X[0].p = MStore<D, true>::slot(lds);
+        else E[0].p = MStore<D, true>::slot(lds);
     }
-    cd X[D][D];  // X_{k-1} = C_{k-1} M C_{k-1}^dag in the sector; M'_c at the chunk start
-    {
-        const cd *mc = B.Mc + ((size_t)L.bp * P.nchunks + L.c) * TS;
+    const size_t lanes = (size_t)gridDim.x * kWalkBlock, lane = (size_t)blockIdx.x * kWalkBlock + threadIdx.x;
+    auto ew = [&](int jj, int w) { return B.Ew + ((((size_t)blockIdx.y * P.L + jj) * NS + w) * TS) * lanes + lane; };
+    cd En[STORED ? NS : 1][D][D];  // the next step's stored propagators (STORED)
+    if constexpr (STORED) {
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            const cd *src = ew(0, w);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int i = 0; i < D; ++i) En[w][j][i] = src[(size_t)(j * D + i) * lanes];
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+        const cd *mc = B.Mc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
 #pragma unroll
-            for (int i = 0; i < D; ++i) X[j][i] = mc[j * D + i];
+            for (int i = 0; i < D; ++i) X[w].set(j, i, mc[j * D + i]);
         }
     }
     WalkX XV;
     walk_set_xa(XV, walk_load_x(P.na, xb + (size_t)P.np * P.Nt));
     const int k0 = L.c * P.L;
-    X4 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
+    X2 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
     const cptr<VSpec> vs = as_constant(P.vs);
 #pragma unroll 1
     for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store nothing
@@ -582,55 +696,97 @@ __global__ __launch_bounds__(kWalkBlock, (WalkWaves<D, true>::value)) void k_wal
         const bool act = L.ok && k0 + jj < P.Nt;
         walk_set_xk(XV, xn);
         xn = walk_load_x(P.np, xb + (size_t)min(k + 1, P.Nt - 1) * P.np);  // next step's controls
-        SM<D> A;
-        walk_build<D>(P, ops, XV, k + 1, none, A);
-        walk_expm<D>(A, scr, [&](int i, const cd (&x)[D]) { E.put_col(i, x); });
+        if constexpr (STORED) {  // this step's propagators; the next step's loads go out now
+#pragma unroll
+            for (int w = 0; w < NS; ++w) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+#pragma unroll
+                    for (int i = 0; i < D; ++i) E[w].set(j, i, En[w][j][i]);
+                }
+            }
+            const int jn = jj + 1 < P.L ? jj + 1 : jj;
+#pragma unroll
+            for (int w = 0; w < NS; ++w) {
+                const cd *src = ew(jn, w);
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+#pragma unroll
+                    for (int i = 0; i < D; ++i) En[w][j][i] = src[(size_t)(j * D + i) * lanes];
+                }
+            }
+        } else {
+            SM<D> A[NS];
+            walk_build<D, NS>(P, ops, XV, k + 1, none, A);
+#pragma unroll
+            for (int w = 0; w < NS; ++w)
+                walk_expm<D, C::FENCE, C::KEEP_A2_NOM>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) E[w].set(j, i, x[j]);
+                });
+        }
         // Y = X E^dag, in place row by row (row r of Y reads row r of X only)
 #pragma unroll
-        for (int r = 0; r < D; ++r) {
-            cd y[D];
+        for (int w = 0; w < NS; ++w) {
 #pragma unroll
-            for (int cc = 0; cc < D; ++cc) {
-                cd s = czero();
+            for (int r = 0; r < D; ++r) {
+                cd xr[D], y[D];
 #pragma unroll
-                for (int j = 0; j < D; ++j) cmac(s, X[r][j], cconj(E.at(cc, j)));
-                y[cc] = s;
+                for (int j = 0; j < D; ++j) xr[j] = X[w].at(r, j);
+#pragma unroll
+                for (int cc = 0; cc < D; ++cc) {
+                    cd s = czero();
+#pragma unroll
+                    for (int j = 0; j < D; ++j) cmac(s, xr[j], cconj(E[w].at(cc, j)));
+                    y[cc] = s;
+                }
+#pragma unroll
+                for (int cc = 0; cc < D; ++cc) X[w].set(r, cc, y[cc]);
             }
-#pragma unroll
-            for (int cc = 0; cc < D; ++cc) X[r][cc] = y[cc];
         }
         // eps-variants: F_dx[u, k] = Re tr(Y (E' - E)) / eps, column j of E' against row j of Y
 #pragma unroll 1
-        for (int u = 0; u < P.nvg; ++u) {
-            SM<D> Ap;
-            walk_build<D>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
-            double s = 0.0;
-            walk_expm<D>(Ap, scr, [&](int j, const cd (&x)[D]) {
-                const auto &Ej = E.opaque();  // column j of E read here, after column j of E'
+        for (int u = 0; u < (NVG > 0 ? NVG : P.nvg); ++u) {
+            SM<D> Ap[NS];
+            walk_build<D, NS>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
 #pragma unroll
-                for (int r = 0; r < D; ++r) {
-                    const cd de = cscale(P.inv_eps, csub(x[r], Ej.at(r, j)));  // (1/eps) (E' - E)
-                    s = fma(X[j][r].re, de.re, s);
-                    s = fma(-X[j][r].im, de.im, s);
-                }
-            });
-            if (act) B.sec_part[((size_t)L.bp * P.Nt + k) * P.nvg + u] = s;
+            for (int w = 0; w < NS; ++w) {
+                double s = 0.0;
+                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(Ap[w], scr + (size_t)w * 2 * TS, [&](int j, const cd (&x)[D]) {
+                    const auto &Yj = X[w].opaque();  // row j of Y and column j of E read here, after
+                    const auto &Ej = E[w].opaque();  // column j of E'
+#pragma unroll
+                    for (int r = 0; r < D; ++r) {
+                        const cd de = cscale(P.inv_eps, csub(x[r], Ej.at(r, j)));  // (1/eps) (E' - E)
+                        const cd y = Yj.at(j, r);
+                        s = fma(y.re, de.re, s);
+                        s = fma(-y.im, de.im, s);
+                    }
+                });
+                // unconditional store (inactive lanes write the sink): exact vmcnt accounting
+                double *dst = act ? B.sec_part + ((((size_t)L.be * ns + L.w0 + w) * P.Nt) + k) * P.nvg + u
+                                  : reinterpret_cast<double *>(B.sink);
+                *dst = s;
+            }
         }
         // X <- E Y, in place column by column
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-            cd y[D], t[D];
+        for (int w = 0; w < NS; ++w) {
 #pragma unroll
-            for (int m = 0; m < D; ++m) y[m] = X[m][i];
+            for (int i = 0; i < D; ++i) {
+                cd y[D], t[D];
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
-                cd c = czero();
+                for (int m = 0; m < D; ++m) y[m] = X[w].at(m, i);
 #pragma unroll
-                for (int m = 0; m < D; ++m) cmac(c, E.at(j, m), y[m]);
-                t[j] = c;
+                for (int j = 0; j < D; ++j) {
+                    cd c = czero();
+#pragma unroll
+                    for (int m = 0; m < D; ++m) cmac(c, E[w].at(j, m), y[m]);
+                    t[j] = c;
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j) X[w].set(j, i, t[j]);
             }
-#pragma unroll
-            for (int j = 0; j < D; ++j) X[j][i] = t[j];
         }
     }
 }

@@ -7,7 +7,7 @@ namespace grape {
 struct DevProblem;
 struct DevBatch;
 constexpr int kWalkMaxD = 4;  // sector classes of at most this many levels take the walks
-constexpr int kWalkMaxNpA = 4;  // ... with at most this many controls per step and x_add entries
+constexpr int kWalkMaxNpA = 2;  // ... with at most this many controls per step and x_add entries
 constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBlock)
 }  // namespace grape
 

@@ -5,16 +5,46 @@
 
 namespace grape_walk {
 
+template <int D, int NS>
+void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st) {
+    const int ns = P.nsec > 1 ? P.nsec : 1;
+    const long lanes = (long)(B.nb / ns) * P.nchunks;
+    const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
+    const dim3 blk(grape::kWalkBlock);
+    // stored propagators: the 4-level class only (engine: P.walk_store_e)
+    constexpr bool CAN_STORE = D >= 4;
+    const bool store = CAN_STORE && P.walk_store_e;
+    if (stage == 0) {
+        if (store) hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, CAN_STORE>), grid, blk, 0, st, P, B);
+        else hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, false>), grid, blk, 0, st, P, B);
+        return;
+    }
+    if (store) {
+        if (P.nvg == 1) hipLaunchKernelGGL((grape::k_walk_grad<D, NS, CAN_STORE, 1>), grid, blk, 0, st, P, B);
+        else hipLaunchKernelGGL((grape::k_walk_grad<D, NS, CAN_STORE, 0>), grid, blk, 0, st, P, B);
+    } else {
+        if (P.nvg == 1) hipLaunchKernelGGL((grape::k_walk_grad<D, NS, false, 1>), grid, blk, 0, st, P, B);
+        else hipLaunchKernelGGL((grape::k_walk_grad<D, NS, false, 0>), grid, blk, 0, st, P, B);
+    }
+}
+
+// sectors per lane: all of the class's sectors (<= 3) for D <= 3 -- one set of control trig for
+// all of them and independent chains to interleave -- one sector per lane at D = 4 (registers)
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st) {
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const long lanes = (long)(B.nb / ns) * P.nchunks;
-    if (lanes <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)ns);
-    if (stage == 0)
-        hipLaunchKernelGGL(grape::k_walk_fwd<D>, grid, dim3(grape::kWalkBlock), 0, st, P, B);
-    else
-        hipLaunchKernelGGL(grape::k_walk_grad<D>, grid, dim3(grape::kWalkBlock), 0, st, P, B);
+    if ((long)(B.nb / ns) * P.nchunks <= 0) return hipSuccess;
+    if constexpr (D == 2) {  // (the Rydberg two-level classes; a three-level class takes one sector per lane)
+        if (ns == 2) {
+            launch_ns<D, 2>(stage, P, B, st);
+            return hipGetLastError();
+        }
+        if (ns == 3) {
+            launch_ns<D, 3>(stage, P, B, st);
+            return hipGetLastError();
+        }
+    }
+    launch_ns<D, 1>(stage, P, B, st);
     return hipGetLastError();
 }
 

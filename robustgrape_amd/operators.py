@@ -162,6 +162,7 @@ def projector_arrays(fp):
 # grape_desc.reserved[1] engine options (include/grape.h GRAPE_OPT_*): implementations of the
 # same outputs, fixed at plan creation (A/B measurements and cross-path tests)
 OPT_NO_SECTORS, OPT_NO_LANE, OPT_NO_CHAIN, OPT_NO_WALK, OPT_NO_GRAPH = 1, 2, 4, 8, 16
+OPT_WALK_RECOMPUTE = 32
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):

@@ -14,7 +14,7 @@ faulted "$OUT/walk_tests_$TAG.log" && { echo FAULT; exit 99; }
 fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-    python3 "$ROOT/scripts/probes/walk_ab.py" --opts ${AB_OPTS:-0,8} --steps 4 > "$OUT/rocprof_$TAG.log" 2>&1
+    python3 "$ROOT/scripts/probes/walk_ab.py" --opts ${AB_OPTS:-0,32} --steps 4 > "$OUT/rocprof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/rocprof_$TAG.log"
 faulted "$OUT/rocprof_$TAG.log" && { echo FAULT; exit 99; }
 [ $rc -ne 0 ] && exit $rc

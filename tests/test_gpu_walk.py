@@ -226,3 +226,28 @@ def test_walk_single_calls_are_the_batch():
             assert one[0][0] == ref[0][b] and np.array_equal(one[1][0], ref[1][b])
     finally:
         pl.close()
+
+
+@pytest.mark.parametrize("name,fp", [("full9", lambda: P.full9_problem(96)), ("sym5", lambda: P.sym_problem(40)),
+                                     ("full9-hot", lambda: _high_norm_problem(64)[0])])
+def test_walk_propagator_modes_bitwise(name, fp):
+    """The gradient walk reading the forward walk's stored propagators (default for the 4-level class)
+    and recomputing them (GRAPE_OPT_WALK_RECOMPUTE) run the same exponential code on the same inputs:
+    F and F_dx agree bit for bit."""
+    from robustgrape_amd.operators import OPT_WALK_RECOMPUTE
+    f = fp()
+    nparam = 2 if name == "full9-hot" else 1
+    nt = f.unitary_problem.ntimes
+    rng = np.random.default_rng(3)
+    X = rng.uniform(0, 2 * np.pi, size=(300, nparam * nt + 1))
+    if name == "full9-hot":
+        X[::7, 1::2][:, 5] = 700.0  # one high-norm step in every 7th row (the squaring path)
+    outs = []
+    for opts in (0, OPT_WALK_RECOMPUTE):
+        pl = _plan(f, 300, opts, nparam=nparam)
+        try:
+            outs.append(pl.fidelity_grad(X)[:2])
+        finally:
+            pl.close()
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
