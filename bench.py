@@ -78,7 +78,7 @@ def flops_expm(d, m=5, s=0):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
-LANE_MAX_D = 3  # csrc/grape_launch.hpp kLaneMaxD (= kChainMaxD)
+WALK_STORE_LEVELS = 4  # csrc/grape_walk_api.hpp kWalkMaxD: the sector class whose walk stores E
 PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
 PMC_SUMMARY_C3 = os.path.join(ROOT, "profiles", "pmc_c3_latest.json")
 
@@ -109,6 +109,38 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY, dims=None):
             and "hbm_bytes_per_launch" in row
             and (dims is None or dim(name) in dims)]
     return sum(rows) if rows else None
+
+
+def pmc_pipeline(batch, per_pass_kernel, dims, path=PMC_SUMMARY):
+    """PMC HBM bytes of one whole device pass: every kernel's mean bytes per dispatch times its
+    dispatches per pass (dispatch count over that of `per_pass_kernel`, which runs once per pass
+    per sector class), over kernels of the sector dimensions `dims` and the dimension-free ones."""
+    try:
+        with open(path) as fh:
+            js = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if js.get("batch") != batch:
+        return None
+    ks = js.get("kernels", {})
+    def dim(name):
+        try:
+            return int(name.split("<")[1].split(",")[0].split(">")[0])
+        except (IndexError, ValueError):
+            return None
+    ref = [r.get("dispatches") for n, r in ks.items()
+           if n.split("<")[0].split("::")[-1] == per_pass_kernel and dim(n) in dims]
+    if not ref or not ref[0]:
+        return None
+    total = 0.0
+    for n, r in ks.items():
+        if "hbm_bytes_per_launch" not in r or not r.get("dispatches"):
+            continue
+        dn = dim(n)
+        if dn is not None and dn not in dims:
+            continue
+        total += r["hbm_bytes_per_launch"] * r["dispatches"] / ref[0]
+    return total
 
 
 def _host_cpu():
@@ -250,33 +282,41 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     """C2 bench line.  `sectors`: GrapePlan.sectors() -- ((S, nsec), ...) per sector class, or
     ((D, 1),) for whole matrices; `passes`: device passes in the timed region (per-pass kernel
     times = total / passes: the sector classes launch each kernel once per class)."""
-    # algorithmic flops per device pass of the two exp-carrying kernels (DESIGN.md 4):
-    # k_expm exps the nominal step propagators; k_expm_grad exps each eps-variant (np=1
-    # control; H0 does not read x_add, so no x_add variants) and contracts it:
-    # Z_k = conj(Q_k) M'^T Q_{k-1}^T (2 complex products) + Re<Z, dE>.  With sectors every
-    # item is one S x S sector of one step (DESIGN.md 4.1).
-    nvg = 1
+    nvg = 1  # np = 1 control; H0 does not read x_add, so no x_add variants
     classes = tuple(sectors) if sectors else ((D, 1),)
     sec = classes[0][0] < D
     per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
-    flop_model = {"k_expm": L * NT * per_step(flops_expm),
-                  "k_expm_grad": L * NT * nvg * per_step(lambda S: flops_expm(S) + 2 * 8 * S ** 3 + 8 * S ** 2)}
-    # algorithmic HBM bytes per pass: k_expm writes E; k_scan reads E, writes Q; k_expm_grad
-    # reads E_k and Q_k (Q_{k-1} is the previous step's Q_k) -- 16 S^2 bytes per tile
-    # Sector classes of S <= LANE_MAX_D (csrc/grape_launch.hpp kLaneMaxD) run k_expm_chain_lane:
-    # the exp kernel also builds the chunk chains and writes Q, and k_scan only reads chunk totals
-    chained = lambda S: (sec and S <= LANE_MAX_D and os.environ.get("GRAPE_NO_LANE") is None  # noqa: E731
-                         and os.environ.get("GRAPE_NO_CHAIN") is None)
-    byte_model = {"k_expm": L * NT * per_step(lambda S: (2 if chained(S) else 1) * 16 * S * S),
-                  "k_scan": L * NT * per_step(lambda S: 0 if chained(S) else 2 * 16 * S * S),
-                  "k_expm_grad": L * NT * nvg * per_step(lambda S: 2 * 16 * S * S)}
-    npass = passes or max(1, ktimes.get("k_expm_grad", (0.0, 1))[1])
+    walk = ktimes.get("k_walk_grad", (0.0, 0))[1] > 0
+    xbytes = L * 8 * (NT + 1)  # the x rows every per-step kernel streams
+    if walk:
+        # chunk walks (grape_walk.hpp, DESIGN.md 4.2), algorithmic work per device pass:
+        # k_walk_fwd: one nominal S x S exp per (step, sector) + the chain product Q <- E Q;
+        # k_walk_grad: one eps-variant exp per (step, sector), Y = X E^dagger, X <- E Y and the
+        # contraction Re tr(Y dE).  The 2-level classes recompute E in the gradient walk
+        # (executed, not credited); the 4-level class stores E once (walk_store_e) and the
+        # gradient walk reads it back -- the only per-step HBM intermediate left
+        store = lambda S: S == WALK_STORE_LEVELS  # noqa: E731
+        flop_model = {"k_walk_fwd": L * NT * per_step(lambda S: flops_expm(S) + 8 * S ** 3),
+                      "k_walk_grad": L * NT * nvg * per_step(lambda S: flops_expm(S) + 2 * 8 * S ** 3 + 8 * S ** 2)}
+        byte_model = {"k_walk_fwd": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0),
+                      "k_walk_grad": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0)}
+    else:
+        # stored-intermediate pipeline (GRAPE_OPT_NO_WALK / whole matrices): k_expm writes E;
+        # k_scan reads E, writes Q; k_expm_grad reads E_k and Q_k
+        flop_model = {"k_expm": L * NT * per_step(flops_expm),
+                      "k_expm_grad": L * NT * nvg * per_step(lambda S: flops_expm(S) + 2 * 8 * S ** 3 + 8 * S ** 2)}
+        byte_model = {"k_expm": L * NT * per_step(lambda S: 16 * S * S),
+                      "k_scan": L * NT * per_step(lambda S: 2 * 16 * S * S),
+                      "k_expm_grad": L * NT * nvg * per_step(lambda S: 2 * 16 * S * S)}
+    grad_name = "k_walk_grad" if walk else "k_expm_grad"
+    npass = passes or max(1, ktimes.get(grad_name, (0.0, 1))[1])
     per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
     kname = max(flop_model, key=lambda k: per_pass.get(k, 0.0))
     ms = per_pass[kname]
     fp = flop_model[kname] / (ms * 1e-3) / 1e12
     hb = byte_model[kname] / (ms * 1e-3) / 1e9
-    traffic = pmc_traffic(kname, L, dims={S for S, _ in classes})
+    dims = {S for S, _ in classes}
+    traffic = pmc_traffic(kname, L, dims=dims)
     fp_frac, hb_frac = fp / FP64_PEAK_TFLOPS, hb / HBM_PEAK_GBS
     if hb_frac > fp_frac:
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -291,6 +331,13 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                  "fp64": {"achieved_TFLOPs": fp, "frac": fp_frac},
                  "hbm": {"achieved_GBs": hb, "frac": hb_frac,
                          "traffic_GBs": (traffic / (ms * 1e-3) / 1e9) if traffic else None}})
+    pipe = pmc_pipeline(L, grad_name, dims)
+    if pipe is not None:
+        total_ms = sum(per_pass.values())
+        roof["pipeline_traffic"] = {"bytes_per_pass": pipe, "bytes_per_eval": pipe / L,
+                                    "GBs_over_pass": pipe / (total_ms * 1e-3) / 1e9,
+                                    "note": "PMC HBM bytes of every kernel of one device pass (sector classes, "
+                                            "scans, head, reductions), over the summed kernel time"}
     out = {
         "metric": "GRAPE gradient-evals/sec (fidelity+∇), Rydberg CZ d=9 N_t=512, 1→8 GPU",
         "value": value, "unit": "gradient-evals/s", "n_gpus": world, "steps": args.steps,
@@ -299,10 +346,12 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
         "config": {"workload": "C2/C4: Rydberg CZ d=9 (rydberg_hamiltonian_full, B=10), N_t=512, "
                                "np=1, na=1, ne=0; restart sweep",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
-                   "sectors": [{"levels": S, "sectors": ns, "lane_chains": bool(chained(S))}
+                   "pipeline": "chunk walks" if walk else ("sector kernels" if sec else "whole matrices"),
+                   "sectors": [{"levels": S, "sectors": ns, "stored_propagators": bool(walk and store(S))}
                                for S, ns in classes] if sec else None},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
+        "kernels_ms_per_pass": per_pass,
     }
     # whole-evaluation view: FLOP of the work executed per evaluation
     # (nominal + one eps-variant exp per step per sector, chain + contraction products; with
@@ -327,31 +376,16 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                            for k, f in flop_model.items() if per_pass.get(k)}
     out["kernels_hbm_frac"] = {k: f / (per_pass[k] * 1e-3) / 1e9 / HBM_PEAK_GBS
                                for k, f in byte_model.items() if per_pass.get(k)}
-    # the scan is the HBM-heavy stage: E in, Q out (algorithmic 2 * 16 S^2 bytes per step and
-    # sector) against the 8 TB/s HBM3E peak, with the PMC bytes where the summary matches
-    if per_pass.get("k_scan"):
-        per_ms = per_pass["k_scan"]
-        alg = byte_model["k_scan"]
-        pmc = pmc_traffic("k_scan", L, dims={S for S, _ in classes})
-        out["roofline_scan"] = {"bound": "hbm", "kernel": "k_scan", "per_launch_ms": per_ms,
-                                "algorithmic_bytes": alg, "achieved": alg / (per_ms * 1e-3) / 1e9,
-                                "traffic": pmc, "achieved_traffic": (pmc / (per_ms * 1e-3) / 1e9) if pmc else None,
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": alg / (per_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                "note": "k_scan time includes the sector head" if sec else None}
     return out
 
 
 def whole_matrix_leg(fp, nparam, X, F, Fdx, L, stream, args):
-    """The same C2 step on whole 9 x 9 matrices (GRAPE_NO_SECTORS=1): the row-group kernels'
+    """The same C2 step on whole 9 x 9 matrices (plan option GRAPE_OPT_NO_SECTORS): the row-group kernels'
     own efficiency, and the speed-up the sector decomposition adds on top of it."""
     from robustgrape_amd.engine import GrapePlan
-    os.environ["GRAPE_NO_SECTORS"] = "1"
-    try:
-        plan = GrapePlan(fp, nparam=nparam, device=X.device.index or 0, max_batch=L)
-    finally:
-        del os.environ["GRAPE_NO_SECTORS"]
+    from robustgrape_amd.operators import OPT_NO_SECTORS
     import torch
+    plan = GrapePlan(fp, nparam=nparam, device=X.device.index or 0, max_batch=L, options=OPT_NO_SECTORS)
     plan.set_stream(stream.cuda_stream)
     n = X.shape[0]
     steps = max(3, args.steps // 5)
@@ -378,7 +412,39 @@ def whole_matrix_leg(fp, nparam, X, F, Fdx, L, stream, args):
                             "frac": fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, "traffic": tr,
                             "traffic_GBs": (tr / (ms * 1e-3) / 1e9) if tr else None},
             "kernels_ms_per_step": {k: v[0] / steps for k, v in kt.items() if v[1]},
-            "note": "same workload with sectors disabled (GRAPE_NO_SECTORS=1): whole 9 x 9 matrices"}
+            "note": "same workload with sectors disabled (GRAPE_OPT_NO_SECTORS): whole 9 x 9 matrices"}
+
+
+def c4_points(fp, nparam, inputs, dev, batches=(256, 32), seconds=1.5):
+    """BASELINE C4 as specified: 256 restarts over 8 GPUs = 32 per GPU (and the whole 256 on one
+    GPU), device-resident x, one plan sized to the batch, back-to-back steps on one stream."""
+    import torch
+    from robustgrape_amd.engine import GrapePlan
+    out = {}
+    for b in batches:
+        plan = GrapePlan(fp, nparam=nparam, device=dev.index or 0, max_batch=b)
+        st = torch.cuda.Stream(device=dev)
+        plan.set_stream(st.cuda_stream)
+        X = torch.from_numpy(inputs(0, b)).to(dev)
+        F = torch.empty(b, dtype=torch.float64, device=dev)
+        G = torch.empty(b, X.shape[1], dtype=torch.float64, device=dev)
+        step = lambda: plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), G.data_ptr(), b, 0, 0)  # noqa: E731
+        for _ in range(3):
+            step()
+        plan.synchronize()
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(10):
+                step()
+            n += 10
+            plan.synchronize()
+        dt = time.perf_counter() - t0
+        plan.close()
+        out[f"batch_{b}"] = {"value": n * b / dt, "unit": "gradient-evals/s", "ms_per_step": dt / n * 1e3,
+                             "steps": n}
+    out["note"] = ("C4 as BASELINE names it: 256 restarts / 8 GPUs = 32 per GPU; per-GPU rate at that batch "
+                   "(x resident in HBM, steps queued back to back on the plan's stream)")
+    return out
 
 
 def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passes=None):
@@ -637,6 +703,8 @@ def main():
     ap.add_argument("--no-host-paths", action="store_true",
                     help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-whole-matrix", action="store_true",
+                    help="skip the C2 whole-matrix comparison leg (PMC passes: one pipeline per run)")
     ap.add_argument("--dist", action="store_true",
                     help="run the multi-rank path (RCCL process group, the sweep's all_gather + "
                          "broadcast, max-over-ranks timing) even with one rank")
@@ -747,7 +815,7 @@ def main():
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         out["config"]["evals_per_device_pass"] = min(count, chunk)
     plan.close()
-    if rank == 0 and world == 1 and not (c3 or c5) and sectors[0][0] < d:
+    if rank == 0 and world == 1 and not (c3 or c5) and sectors[0][0] < d and not args.no_whole_matrix:
         out["whole_matrix_path"] = whole_matrix_leg(fp, nparam, X, F, Fdx, min(count, chunk), stream, args)
     if rank == 0:
         if world == 1 and not args.no_host_paths:
@@ -756,6 +824,8 @@ def main():
             Xh = inputs(0, min(4096, B))
             out["host_path"] = host_path(fp, nparam, Xh, reps=3 if c5 else 10, label=args.workload.upper())
             out["single_eval"] = single_eval(fp, nparam, Xh[0])
+            if not (c3 or c5):
+                out["c4_points"] = c4_points(fp, nparam, inputs, dev)
         if world == 1 and not args.no_cpu_baseline and not c5:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, fp if c3 else None, "C3" if c3 else "C2")
             if not c3:

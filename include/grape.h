@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 6
+#define GRAPE_ABI_VERSION 7
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -327,7 +327,9 @@ typedef enum grape_kernel {
     GRAPE_KERNEL_DCARRY = 11,   /* dense engine: carries, U, F, M = G U */
     GRAPE_KERNEL_DMC = 12,      /* dense engine: per-chunk M'_c */
     GRAPE_KERNEL_DGRAD = 13,    /* dense engine: eps-variant propagators contracted in place */
-    GRAPE_NUM_KERNELS = 14
+    GRAPE_KERNEL_WALK_FWD = 14, /* sector chunk walks: propagators + chunk totals (grape_walk.hpp) */
+    GRAPE_KERNEL_WALK_GRAD = 15,/* sector chunk walks: eps-variants contracted along the chunk */
+    GRAPE_NUM_KERNELS = 16
 } grape_kernel;
 
 int grape_plan_set_profiling(grape_plan *plan, int enable);

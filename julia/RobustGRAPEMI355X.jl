@@ -18,7 +18,7 @@ export OperatorTerm, OperatorBasis, calculate_fidelity_and_derivatives, calculat
        calculate_interaction_error_operators, calculate_expectation_values, grape_expm_batch
 
 const libgrape = normpath(joinpath(@__DIR__, "..", "robustgrape_amd", "libgrape.so"))
-const GRAPE_ABI_VERSION = 6  # include/grape.h
+const GRAPE_ABI_VERSION = 7  # include/grape.h
 
 function __init__()
     v = ccall((:grape_abi_version, libgrape), Cint, ())

@@ -26,8 +26,9 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_lbfgs_direction", "grape_unitary_derivs_tables", "grape_interaction_error_operators_tables",
             "grape_expectation_values_tables", "grape_plan_sectors"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad/k_err_local", "k_reduce_add", "k_err_scan", "k_err_grad",
-                "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad"]
-ABI_VERSION = 6  # GRAPE_ABI_VERSION in include/grape.h
+                "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad",
+                "k_walk_fwd", "k_walk_grad"]
+ABI_VERSION = 7  # GRAPE_ABI_VERSION in include/grape.h
 
 
 class GrapeError(RuntimeError):

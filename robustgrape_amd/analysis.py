@@ -19,27 +19,26 @@ import numpy as np
 import torch
 
 from . import _capi
-from .engine import fidelity_wrapper, get_plan
+from .engine import fidelity_wrapper, locked_plan
 from .operators import host_interaction_tables
 from .types import FidelityRobustGRAPEProblem, split_x
 
-def _plan(fp_or_up, x, device):
-    if isinstance(fp_or_up, FidelityRobustGRAPEProblem):
-        fp = fp_or_up
-    else:  # a UnitaryRobustGRAPEProblem: the descriptor needs a projector and target (unused here)
-        fp = fidelity_wrapper(fp_or_up)
+def _problem(fp_or_up, x):
+    """(fidelity problem, nparam): a UnitaryRobustGRAPEProblem is wrapped (the descriptor needs a
+    projector and a target, unused here)."""
+    fp = fp_or_up if isinstance(fp_or_up, FidelityRobustGRAPEProblem) else fidelity_wrapper(fp_or_up)
     _, _, nparam = split_x(fp.unitary_problem, x)
-    return fp, get_plan(fp, nparam, device, max_batch=1)
+    return fp, nparam
 
 
 def calculate_interaction_error_operators(unitary_problem, x, device: int = 0) -> np.ndarray:
     """(ndim, ndim, ntimes, nerr) complex, like the reference's permuted tensor."""
     x = np.ascontiguousarray(x, dtype=np.float64)
-    fp, plan = _plan(unitary_problem, x, device)
+    fp, nparam = _problem(unitary_problem, x)
     up = fp.unitary_problem
     O = np.zeros((up.ndim, up.ndim, up.ntimes, len(up.error_sources)), dtype=np.complex128, order="F")
     if O.size:
-        with plan.lock:
+        with locked_plan(fp, nparam, device) as plan:
             if plan.tables:  # closure problem: H0 / Herror evaluated here (the reference's calls)
                 H0, Oerr = host_interaction_tables(up, x, plan.nparam)
                 _capi.check(_capi.lib().grape_interaction_error_operators_tables(
@@ -53,11 +52,11 @@ def calculate_interaction_error_operators(unitary_problem, x, device: int = 0) -
 def calculate_expectation_values(fidelity_problem: FidelityRobustGRAPEProblem, x, device: int = 0) -> np.ndarray:
     """(ntimes, nerr) real."""
     x = np.ascontiguousarray(x, dtype=np.float64)
-    fp, plan = _plan(fidelity_problem, x, device)
+    fp, nparam = _problem(fidelity_problem, x)
     up = fp.unitary_problem
     ev = np.zeros((up.ntimes, len(up.error_sources)), dtype=np.float64, order="F")
     if ev.size:
-        with plan.lock:
+        with locked_plan(fp, nparam, device) as plan:
             if plan.tables:
                 H0, Oerr = host_interaction_tables(up, x, plan.nparam)
                 _capi.check(_capi.lib().grape_expectation_values_tables(
@@ -72,13 +71,13 @@ def _device_operators(fp, x, device):
     kernels straight into device memory (grape_interaction_error_operators_device): they never
     visit the host."""
     x = np.ascontiguousarray(x, dtype=np.float64)
-    fp, plan = _plan(fp, x, device)
+    fp, nparam = _problem(fp, x)
     up = fp.unitary_problem
     d, nt, ne = up.ndim, up.ntimes, len(up.error_sources)
     # the reference's column-major (d, d, nt, ne) tensor is the C-order (ne, nt, d_col, d_row) one
     O = torch.empty(ne, nt, d, d, dtype=torch.complex128, device=torch.device("cuda", device))
     torch.cuda.synchronize(O.device)
-    with plan.lock:
+    with locked_plan(fp, nparam, device) as plan:
         if plan.tables:
             H0, Oerr = host_interaction_tables(up, x, plan.nparam)
             _capi.check(_capi.lib().grape_interaction_error_operators_tables(

@@ -202,9 +202,9 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
     if constexpr (D >= 2 && D <= grape::kWalkMaxD) {
         if (P.walk) {  // chunk walks (grape_walk.hpp): no E / Q intermediates
             if (stage == 0) {
-                mark(GRAPE_KERNEL_EXPM, 0);
+                mark(GRAPE_KERNEL_WALK_FWD, 0);
                 const hipError_t e = grape_walk::launch<D>(0, P, B, st);
-                mark(GRAPE_KERNEL_EXPM, 1);
+                mark(GRAPE_KERNEL_WALK_FWD, 1);
                 if (e != hipSuccess) return e;
                 mark(GRAPE_KERNEL_SCAN, 0);
                 launch_scan<D>(P, B, st);
@@ -216,9 +216,9 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                 const long nmc = (long)B.nb * P.nchunks * D * D;
                 hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
                 mark(GRAPE_KERNEL_REDUCE, 1);
-                mark(GRAPE_KERNEL_EXPM_GRAD, 0);
+                mark(GRAPE_KERNEL_WALK_GRAD, 0);
                 const hipError_t e = grape_walk::launch<D>(1, P, B, st);
-                mark(GRAPE_KERNEL_EXPM_GRAD, 1);
+                mark(GRAPE_KERNEL_WALK_GRAD, 1);
                 if (e != hipSuccess) return e;
                 return hipGetLastError();
             }

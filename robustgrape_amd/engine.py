@@ -7,6 +7,7 @@ src/UnitaryCalculations.jl:22) and additionally accepts a 2-D ``x`` of shape
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import threading
 from collections import OrderedDict
@@ -15,7 +16,7 @@ import numpy as np
 
 from . import _capi
 from .operators import DescriptorBuffers, TableDescriptor, has_operator_basis
-from .tables import SharedTables, get_workers, host_tables, table_shapes
+from .tables import SharedTables, get_workers, host_tables, table_batch_cap, table_shapes
 from .types import FidelityRobustGRAPEProblem, split_x
 
 
@@ -34,12 +35,16 @@ class GrapePlan:
         self.nx = self.nparam * self.up.ntimes + self.up.nb_additional_param
         self.nerr = len(self.up.error_sources)
         self.max_batch = int(max_batch)
+        self.requested_batch = self.max_batch  # before the closure-table byte cap (get_plan's key)
         self.options = int(options)
         self.lock = threading.Lock()  # one evaluation at a time (the plan's buffers are shared)
         self._shared = None  # closure fallback: double-buffered shared-memory tables
         # operator bases -> the fused device path; plain closures -> the host-table fallback
         self.tables = not has_operator_basis(fp)
         if self.tables:
+            # closure tables (device d_Htab and the two shared-memory buffers) hold nv d x d
+            # matrices per step per evaluation: bound the evaluations per pass by bytes
+            self.max_batch = max(1, min(self.max_batch, table_batch_cap(fp, self.nparam)))
             self._bufs = TableDescriptor(fp, self.nparam, self.max_batch, options, scan_waves)
         else:
             self._bufs = DescriptorBuffers(fp, self.nparam, self.max_batch, options, scan_waves)
@@ -104,34 +109,55 @@ class GrapePlan:
         fill chunk j + 1 while the device evaluates chunk j."""
         L = _capi.lib()
         nb = X.shape[0]
-        W = get_workers(self.fp)
-        if W is not None and not W.can_ship(self.fp):
-            W = None  # closures cloudpickle cannot serialise: evaluate them here
-        if W is None:  # serial
-            H, U0 = host_tables(self.fp, X, self.nparam)
-            _capi.check(L.grape_fidelity_grad_tables(
-                self.handle, nb, _capi.dptr(X), _capi.dptr(H), _capi.dptr(U0), _capi.dptr(F), _capi.dptr(Fdx),
-                _capi.dptr(Fd2), _capi.dptr(Fd2dx)))
-            return
         C = self.max_batch
-        if self._shared is None:
-            sh, su = table_shapes(self.fp, C, self.nparam)
-            self._shared = [SharedTables(sh, su) for _ in range(2)]
-            self._workers = W
         chunks = [(b0, min(C, nb - b0)) for b0 in range(0, nb, C)]
-        pending = {0: W.submit(self.fp, self.nparam, self._shared[0], X, range(chunks[0][0], sum(chunks[0])))}
         sl = lambda a, b0, n: None if a is None else a[b0:b0 + n]
-        for j, (b0, n) in enumerate(chunks):
-            if j + 1 < len(chunks):  # the other buffer's chunk (j - 1) is done on the device
-                c0, cn = chunks[j + 1]
-                pending[j + 1] = W.submit(self.fp, self.nparam, self._shared[(j + 1) % 2], X, range(c0, c0 + cn))
-            for r in pending.pop(j):
-                r.get()
-            tabs = self._shared[j % 2]
-            _capi.check(L.grape_fidelity_grad_tables(
-                self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(tabs.H), _capi.dptr(tabs.U0),
-                _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
-                _capi.dptr(sl(Fd2dx, b0, n))))
+        W = get_workers(self.fp)
+        shipped = W.prepare(self.fp) if W is not None else None  # the closures' current state
+        if shipped is not None and self._shared is None:
+            sh, su = table_shapes(self.fp, C, self.nparam)
+            try:
+                self._shared = [SharedTables(sh, su)]
+                self._shared.append(SharedTables(sh, su))
+                self._workers = W
+            except MemoryError:  # /dev/shm too small for two chunks: evaluate the closures here
+                for t in self._shared or ():
+                    t.close()
+                self._shared = None
+        if shipped is None or self._shared is None:  # serial, chunk by chunk
+            for b0, n in chunks:
+                H, U0 = host_tables(self.fp, X[b0:b0 + n], self.nparam)
+                _capi.check(L.grape_fidelity_grad_tables(
+                    self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(H), _capi.dptr(U0),
+                    _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
+                    _capi.dptr(sl(Fd2dx, b0, n))))
+            return
+        pending = {}
+        try:
+            pending[0] = W.submit(shipped, self.nparam, self._shared[0], X, range(chunks[0][0], sum(chunks[0])))
+            for j, (b0, n) in enumerate(chunks):
+                if j + 1 < len(chunks):  # the other buffer's chunk (j - 1) is done on the device
+                    c0, cn = chunks[j + 1]
+                    pending[j + 1] = W.submit(shipped, self.nparam, self._shared[(j + 1) % 2], X,
+                                              range(c0, c0 + cn))
+                for r in pending[j]:
+                    r.get()
+                del pending[j]  # kept until every task of the chunk is done: drained below on error
+                tabs = self._shared[j % 2]
+                _capi.check(L.grape_fidelity_grad_tables(
+                    self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(tabs.H), _capi.dptr(tabs.U0),
+                    _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
+                    _capi.dptr(sl(Fd2dx, b0, n))))
+        except BaseException:
+            # a worker or the device call failed: every task still writing into the two shared
+            # buffers must finish before the next call may refill them (ADVICE r2)
+            for rs in pending.values():
+                for r in rs:
+                    try:
+                        r.wait()
+                    except BaseException:
+                        pass
+            raise
 
     def fidelity_grad_device_async(self, x_ptr: int, F_ptr: int, Fdx_ptr: int, nbatch: int,
                                    Fd2_ptr: int = 0, Fd2dx_ptr: int = 0):
@@ -187,7 +213,7 @@ class GrapePlan:
 # chunked by the C side, so one plan serves every batch size: it is recreated larger only
 # up to PLAN_BATCH_CAP.  At most MAX_CACHED_PLANS plans live at once (least recently used
 # evicted and destroyed).  Evaluations on one plan are serialised by its lock, so cached
-# plans may be shared by threads.
+# plans may be shared by threads (locked_plan: fetch and lock in one step).
 PLAN_BATCH_CAP = 256
 MAX_CACHED_PLANS = 8
 _cache_lock = threading.Lock()
@@ -201,7 +227,7 @@ def get_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_b
     key = (id(fp), int(nparam), int(device))
     with _cache_lock:
         ent = _plan_cache.get(key)
-        if ent is not None and ent.fp is fp and ent.max_batch >= want:
+        if ent is not None and ent.fp is fp and ent.requested_batch >= want:
             _plan_cache.move_to_end(key)
             return ent
         if ent is not None:
@@ -209,7 +235,7 @@ def get_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_b
             with ent.lock:
                 ent.close()
             if ent.fp is fp:
-                want = max(want, ent.max_batch)
+                want = max(want, ent.requested_batch)
         plan = GrapePlan(fp, nparam, device, want)
         _plan_cache[key] = plan
         while len(_plan_cache) > MAX_CACHED_PLANS:
@@ -217,6 +243,18 @@ def get_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_b
             with old.lock:
                 old.close()
         return plan
+
+
+@contextlib.contextmanager
+def locked_plan(fp: FidelityRobustGRAPEProblem, nparam: int, device: int = 0, max_batch: int = 1):
+    """get_plan, with the plan's lock held for the block: a plan another thread evicted or
+    regrew between get_plan and the lock (it is closed then) is fetched again."""
+    while True:
+        plan = get_plan(fp, nparam, device, max_batch)
+        with plan.lock:
+            if plan.handle is not None:
+                yield plan
+                return
 
 
 def cached_plan_count() -> int:
@@ -267,8 +305,7 @@ def calculate_fidelity_and_derivatives(fidelity_problem: FidelityRobustGRAPEProb
     batched = x.ndim == 2
     X = x if batched else x[None, :]
     _, _, nparam = split_x(fidelity_problem.unitary_problem, X[0])
-    plan = get_plan(fidelity_problem, nparam, device, max_batch=X.shape[0])
-    with plan.lock:
+    with locked_plan(fidelity_problem, nparam, device, max_batch=X.shape[0]) as plan:
         F, Fdx, Fd2, Fd2dx = plan.fidelity_grad(X)
     if batched:
         return F, Fdx, Fd2, Fd2dx
@@ -282,6 +319,5 @@ def calculate_unitary_and_derivatives(unitary_problem, x, device: int = 0):
     (d,d), (d,d,np,N_t), (d,d,na), (d,d,ne), (d,d,np,N_t,ne), (d,d,na,ne)."""
     x = np.asarray(x, dtype=np.float64)
     _, _, nparam = split_x(unitary_problem, x)
-    plan = get_plan(fidelity_wrapper(unitary_problem), nparam, device, max_batch=1)
-    with plan.lock:
+    with locked_plan(fidelity_wrapper(unitary_problem), nparam, device, max_batch=1) as plan:
         return plan.unitary_derivs(x)

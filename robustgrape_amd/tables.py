@@ -7,8 +7,8 @@ src/FidelityCalculations.jl:32-38) and hands the tables to
 ``grape_fidelity_grad_tables``; everything else runs on the device.
 
 The closure calls are the reference's own cost (one Python call per call site), so
-this module spreads them over worker processes: ``TableWorkers`` forks a pool once
-(before the tables are needed: the workers never touch the GPU), splits a batch by
+this module spreads them over worker processes: ``TableWorkers`` spawns a pool once
+(the workers never touch the GPU), ships them the problem by value with every call, splits a batch by
 evaluations -- or a single evaluation by time steps -- and the workers write straight
 into shared-memory tables that the device call then copies to HBM.  While the device
 evaluates one chunk of a batch, the workers fill the next (``GrapePlan.fidelity_grad``).
@@ -118,6 +118,20 @@ def table_shapes(fp, nb: int, nparam: int):
     return (nb, up.ntimes, nv, d, d), (nb, 1 + na, d, d)
 
 
+TABLE_CHUNK_BYTES = 256 << 20  # per table buffer (GRAPE_TABLE_CHUNK_MB overrides)
+
+
+def table_batch_cap(fp, nparam: int) -> int:
+    """Evaluations per closure-table chunk: one chunk's H + U0 tables within TABLE_CHUNK_BYTES
+    (the plan holds one chunk on the device and two in /dev/shm; e.g. d = 9, N_t = 100 with
+    4 error sources is ~2.7 MB per evaluation -> 94 evaluations)."""
+    sh, su = table_shapes(fp, 1, nparam)
+    per = (int(np.prod(sh)) + int(np.prod(su))) * 16
+    env = os.environ.get("GRAPE_TABLE_CHUNK_MB")
+    budget = int(float(env) * (1 << 20)) if env else TABLE_CHUNK_BYTES
+    return max(1, budget // per)
+
+
 def host_tables(fp, X, nparam: int):
     """The closure tables of a batch, serially in this process: H (nb, N_t, nv, d, d) and
     U0 (nb, 1 + na, d, d), column-major matrices (see fill_tables)."""
@@ -131,8 +145,15 @@ def host_tables(fp, X, nparam: int):
 # ---------------------------------------------------------------------------
 # worker pool
 # ---------------------------------------------------------------------------
-_problems = {}   # token -> problem, in the workers (and, before a fork, in the parent)
-_shm_cache = {}  # worker-side attachments
+# Workers receive the problem by value (cloudpickle) with every call and cache it under the
+# digest of those bytes: a closure whose captured state changed between calls pickles to new
+# bytes, so a worker can never evaluate a stale copy (the serial path and the reference call the
+# live closure).  Functions of importable modules travel by reference, as pickle does: a worker
+# sees such a module as imported, so closures that read MUTABLE module globals must run serially
+# (GRAPE_TABLE_WORKERS=0).
+_problems = {}   # worker side: digest -> problem (small LRU)
+_shm_cache = {}  # worker side: attachments
+_KEEP_PROBLEMS = 8
 
 
 def _attach(name):
@@ -150,11 +171,20 @@ def _attach(name):
 
 def _worker_fill(task):
     token, blob, nparam, hname, uname, sh, su, X, rows, k0, k1, target = task
-    fp = _problems.get(token)
-    if fp is None:  # a problem registered after the fork: shipped by value
+    fp = _problems.pop(token, None)
+    if fp is None:
         import cloudpickle
         fp = cloudpickle.loads(blob)
-        _problems[token] = fp
+    _problems[token] = fp  # most recent last
+    while len(_problems) > _KEEP_PROBLEMS:
+        _problems.pop(next(iter(_problems)))
+    # keep the most recently named attachments only (a plan's two double buffers, a few plans):
+    # a closed or regrown plan's segments are unmapped here, so their tmpfs pages can be freed
+    for n in (hname, uname):
+        if n in _shm_cache:
+            _shm_cache[n] = _shm_cache.pop(n)  # most recent last
+    while len(_shm_cache) > 4 * _KEEP_PROBLEMS:
+        _shm_cache.pop(next(iter(_shm_cache))).close()
     H = np.ndarray(sh, np.complex128, buffer=_attach(hname).buf)
     U0 = np.ndarray(su, np.complex128, buffer=_attach(uname).buf)
     t = time.perf_counter()
@@ -175,6 +205,10 @@ class SharedTables:
 
     def __init__(self, sh, su):
         nbytes = lambda s: int(np.prod(s)) * 16
+        need = nbytes(sh) + nbytes(su)
+        free = shm_free_bytes()  # tmpfs accepts an oversized ftruncate and SIGBUSes the writer later
+        if free is not None and need > free:
+            raise MemoryError(f"closure tables need {need / 2**20:.1f} MiB of /dev/shm, {free / 2**20:.1f} MiB free")
         self.shm_h = shared_memory.SharedMemory(create=True, size=max(16, nbytes(sh)))
         self.shm_u = shared_memory.SharedMemory(create=True, size=max(16, nbytes(su)))
         self.sh, self.su = sh, su
@@ -188,41 +222,43 @@ class SharedTables:
             s.unlink()
 
 
+def shm_free_bytes():
+    try:
+        st = os.statvfs("/dev/shm")
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return None
+
+
 class TableWorkers:
-    """A fork-context process pool that fills closure tables in shared memory."""
+    """A process pool that fills closure tables in shared memory.  Spawned, not forked: the pool
+    may first be needed after this process has initialised HIP, and a fork would copy that
+    state into the workers (they never touch the GPU)."""
 
     def __init__(self, nworkers: int):
         self.n = nworkers
-        self.pool = mp.get_context("fork").Pool(nworkers)
-        self.known = set()  # tokens whose problem the workers already hold (registered before the fork)
-        self.blobs = {}     # token -> (problem, cloudpickle bytes) for problems created after the fork
+        self.pool = mp.get_context("spawn").Pool(nworkers)
         self.lock = threading.Lock()
 
-    def can_ship(self, fp) -> bool:
-        """Whether the workers hold `fp` already or can receive it (cloudpickle)."""
-        token = id(fp)
-        if (token in self.known and _problems.get(token) is fp) or token in self.blobs:
-            return True
+    @staticmethod
+    def prepare(fp):
+        """(token, bytes) of the problem as the workers will evaluate it, or None when cloudpickle
+        cannot serialise its closures (then the caller evaluates them serially).  Called once per
+        evaluation call, so the workers always see the closures' current state."""
         try:
             import cloudpickle
-            self.blobs[token] = (fp, cloudpickle.dumps(fp))
-            return True
+            import hashlib
+            blob = cloudpickle.dumps(fp)
         except Exception:
-            return False
+            return None
+        return hashlib.blake2b(blob, digest_size=16).hexdigest(), blob
 
-    def submit(self, fp, nparam, tabs: SharedTables, X, rows_of_chunk):
+    def submit(self, shipped, nparam, tabs: SharedTables, X, rows_of_chunk):
         """Asynchronously fill the tables for the evaluations `rows_of_chunk` (indices into X and
-        into the tables' first axis); returns an AsyncResult list."""
-        token = id(fp)
-        if token in self.known and _problems.get(token) is fp:
-            blob = b""
-        else:
-            ent = self.blobs.get(token)
-            if ent is None or ent[0] is not fp:
-                import cloudpickle
-                ent = self.blobs[token] = (fp, cloudpickle.dumps(fp))
-            blob = ent[1]
-        nt = fp.unitary_problem.ntimes
+        into the tables' first axis) of the problem `shipped` (from prepare); returns an
+        AsyncResult list."""
+        token, blob = shipped
+        nt = tabs.sh[1]
         X = np.asarray(X, np.float64)
         nb = len(rows_of_chunk)
         tasks = []
@@ -242,9 +278,15 @@ class TableWorkers:
                 for rows, k0, k1, tg in tasks]
 
     def release(self, tabs: SharedTables):
+        """Best effort: workers that run one of these calls drop their mappings now; the others
+        drop them at their next fill (_worker_fill keeps only recently named segments)."""
         names = [tabs.shm_h.name, tabs.shm_u.name]
-        for _ in range(self.n):
-            self.pool.apply(_worker_release, (names,))
+        rs = [self.pool.apply_async(_worker_release, (names,)) for _ in range(self.n)]
+        for r in rs:
+            try:
+                r.get(timeout=10)
+            except Exception:
+                pass
 
     def close(self):
         self.pool.terminate()
@@ -263,19 +305,14 @@ def default_workers() -> int:
 
 
 def get_workers(fp=None):
-    """The process-wide pool (None when the fallback runs serially).  Registering `fp` first
-    lets a pool created now inherit the problem by fork instead of receiving it pickled."""
+    """The process-wide pool (None when the fallback runs serially)."""
     global _workers
     n = default_workers()
     if n <= 1:
         return None
     with _workers_lock:
         if _workers is None:
-            if fp is not None:
-                _problems[id(fp)] = fp
             _workers = TableWorkers(n)
-            if fp is not None:
-                _workers.known.add(id(fp))
             atexit.register(_shutdown)
         return _workers
 

@@ -58,6 +58,7 @@ def main():
             continue
         waves = cs.get("SQ_WAVES", 0.0)
         row = {c: v for c, v in cs.items() if not c.startswith("_")}
+        row["dispatches"] = max((v for c, v in cs.items() if c.startswith("_dispatches_")), default=0)
         if waves:
             for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
                       "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):

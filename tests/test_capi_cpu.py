@@ -28,7 +28,8 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert L.grape_abi_version() == _capi.ABI_VERSION
-    assert len(_capi.KERNEL_NAMES) == 14  # GRAPE_NUM_KERNELS
+    src = open(os.path.join(ROOT, "include", "grape.h")).read()
+    assert len(_capi.KERNEL_NAMES) == int(re.search(r"GRAPE_NUM_KERNELS = (\d+)", src).group(1))
 
 
 def test_descriptor_packing_roundtrip():
@@ -163,10 +164,11 @@ def test_plan_cache_is_bounded_and_keyed_by_problem(monkeypatch):
         def __init__(self, fp, nparam, device, max_batch):
             import threading
             self.fp, self.max_batch, self.closed, self.lock = fp, max_batch, False, threading.Lock()
+            self.requested_batch, self.handle = max_batch, object()
             made.append(self)
 
         def close(self):
-            self.closed = True
+            self.closed, self.handle = True, None
 
     monkeypatch.setattr(engine, "GrapePlan", FakePlan)
     engine.clear_plans()

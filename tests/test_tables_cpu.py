@@ -1,0 +1,86 @@
+"""Closure-table worker pool on the CPU (robustgrape_amd/tables.py): the pool's tables equal the
+serial ones, and equal them again after the closures' captured state changed between calls
+(workers receive the problem by value with every call); the chunk byte cap."""
+import numpy as np
+
+from tests import problems as P
+
+
+def test_pool_tables_follow_the_closures_current_state():
+    from robustgrape_amd import tables as TB
+    fp = P.sym_problem(6, errors=("amp",), device=False)
+    up = fp.unitary_problem
+    base = up.H0
+    state = {"scale": 1.0}
+
+    def h0(t, p, xa):  # reads a captured mutable: the reference calls it live at every site
+        return state["scale"] * np.asarray(base(t, p, xa))
+
+    fp2 = fp.replace(unitary_problem=up.replace(H0=h0))
+    X = np.stack([P.random_x(6, s) for s in range(3)])
+    W = TB.TableWorkers(2)
+    sh, su = TB.table_shapes(fp2, len(X), 1)
+    tabs = TB.SharedTables(sh, su)
+    try:
+        for scale in (1.0, 1.7, 1.0):
+            state["scale"] = scale
+            shipped = W.prepare(fp2)
+            assert shipped is not None
+            for r in W.submit(shipped, 1, tabs, X, range(len(X))):
+                r.get(timeout=120)
+            H, U0 = TB.host_tables(fp2, X, 1)
+            np.testing.assert_array_equal(tabs.H, H)
+            np.testing.assert_array_equal(tabs.U0, U0)
+        # one evaluation split by time steps over the workers
+        tabs1 = TB.SharedTables(*TB.table_shapes(fp2, 1, 1))
+        try:
+            state["scale"] = 0.5
+            for r in W.submit(W.prepare(fp2), 1, tabs1, X, range(1)):
+                r.get(timeout=120)
+            H, U0 = TB.host_tables(fp2, X[:1], 1)
+            np.testing.assert_array_equal(tabs1.H, H)
+            np.testing.assert_array_equal(tabs1.U0, U0)
+        finally:
+            W.release(tabs1)
+            tabs1.close()
+    finally:
+        W.release(tabs)
+        tabs.close()
+        W.close()
+
+
+def test_worker_errors_reach_the_caller():
+    """A non-Hermitian nominal H0 is refused inside the worker; the error surfaces in get()."""
+    from robustgrape_amd import tables as TB
+    fp = P.sym_problem(4, device=False)
+    up = fp.unitary_problem
+    decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
+    bad = fp.replace(unitary_problem=up.replace(H0=lambda t, p, xa: up.H0(t, p, xa) - 0.5j * decay))
+    X = P.random_x(4, 2)[None, :]
+    W = TB.TableWorkers(2)
+    tabs = TB.SharedTables(*TB.table_shapes(bad, 1, 1))
+    try:
+        rs = W.submit(W.prepare(bad), 1, tabs, X, range(1))
+        errs = 0
+        for r in rs:
+            try:
+                r.get(timeout=120)
+            except ValueError as e:
+                assert "Hermitian" in str(e)
+                errs += 1
+        assert errs >= 1
+    finally:
+        tabs.close()
+        W.close()
+
+
+def test_table_chunk_cap_by_bytes(monkeypatch):
+    from robustgrape_amd import tables as TB
+    fp = P.sym_problem(8, errors=("amp", "freq"), device=False)
+    sh, su = TB.table_shapes(fp, 1, 1)
+    per = (int(np.prod(sh)) + int(np.prod(su))) * 16
+    assert TB.table_batch_cap(fp, 1) == max(1, TB.TABLE_CHUNK_BYTES // per)
+    monkeypatch.setenv("GRAPE_TABLE_CHUNK_MB", str(3 * per / 2 ** 20))
+    assert TB.table_batch_cap(fp, 1) == 3
+    monkeypatch.setenv("GRAPE_TABLE_CHUNK_MB", "0")
+    assert TB.table_batch_cap(fp, 1) == 1
