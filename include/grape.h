@@ -153,6 +153,15 @@ typedef struct grape_desc {
 #define GRAPE_OPT_NO_GRAPH 16   /* no HIP-graph replay of small host-array calls */
 #define GRAPE_OPT_WALK_RECOMPUTE 32 /* chunk walks: the gradient walk of the 4-level class recomputes the
                                        nominal propagators instead of reading the forward walk's copy */
+/*
+ * General (non-Hermitian) H0, e.g. a -i Gamma/2 decay term (ABI 7): the chain C_k is inverted
+ * by LU as the reference does (UnitaryCalculations.jl:47, inv(cum_evo)) instead of C_k^dagger,
+ * and the fidelity path runs from the materialised unitary derivatives, one evaluation at a
+ * time (FidelityCalculations.jl:19-119).  Selected automatically for an operator-basis H0
+ * that is not Hermitian; host-table plans (closures) set it when the host sees a
+ * non-Hermitian H0 table.  ndim <= GRAPE_MAX_SMALL_DIM.
+ */
+#define GRAPE_OPT_GENERAL_H0 64
 
 typedef struct grape_plan grape_plan;
 

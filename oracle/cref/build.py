@@ -19,9 +19,9 @@ def build(force=False):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = ["g++", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared", "-fopenmp",
-           "-I" + os.path.join(ROOT, "include"), SRC, "-o", OUT + ".tmp"]
+           "-I" + os.path.join(ROOT, "include"), SRC, "-o", f"{OUT}.{os.getpid()}.tmp"]
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(f"{OUT}.{os.getpid()}.tmp", OUT)  # per-process temporary: parallel test workers may race
     return OUT
 
 

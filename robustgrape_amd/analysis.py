@@ -41,6 +41,7 @@ def calculate_interaction_error_operators(unitary_problem, x, device: int = 0) -
         with locked_plan(fp, nparam, device) as plan:
             if plan.tables:  # closure problem: H0 / Herror evaluated here (the reference's calls)
                 H0, Oerr = host_interaction_tables(up, x, plan.nparam)
+                plan.general_h0_for(H0)
                 _capi.check(_capi.lib().grape_interaction_error_operators_tables(
                     plan.handle, _capi.dptr(x), _capi.dptr(H0), _capi.dptr(Oerr), O.ctypes.data, 0))
             else:
@@ -59,6 +60,7 @@ def calculate_expectation_values(fidelity_problem: FidelityRobustGRAPEProblem, x
         with locked_plan(fp, nparam, device) as plan:
             if plan.tables:
                 H0, Oerr = host_interaction_tables(up, x, plan.nparam)
+                plan.general_h0_for(H0)
                 _capi.check(_capi.lib().grape_expectation_values_tables(
                     plan.handle, _capi.dptr(x), _capi.dptr(H0), _capi.dptr(Oerr), _capi.dptr(ev)))
             else:
@@ -80,6 +82,7 @@ def _device_operators(fp, x, device):
     with locked_plan(fp, nparam, device) as plan:
         if plan.tables:
             H0, Oerr = host_interaction_tables(up, x, plan.nparam)
+            plan.general_h0_for(H0)
             _capi.check(_capi.lib().grape_interaction_error_operators_tables(
                 plan.handle, _capi.dptr(x), _capi.dptr(H0), _capi.dptr(Oerr), O.data_ptr(), 1))
         else:

@@ -148,6 +148,7 @@ struct grape_plan {
     double *d_Fd2 = nullptr, *d_Fd2dx = nullptr, *d_part_err = nullptr;
     cd *d_Zl = nullptr;
     double *d_x = nullptr, *d_F = nullptr, *d_Fdx = nullptr, *d_part = nullptr, *d_tgt_part = nullptr;
+    double *d_xT = nullptr;  // chunk walks: the launch's controls transposed ([nx][nb])
     int *d_ovf = nullptr, *d_ctrl = nullptr;  // ctrl: [0], [1] overflow counts, [2] status
     // closure mode (GRAPE_DESC_HOST_TABLES): host-evaluated H and target tables
     bool tables = false;
@@ -183,6 +184,12 @@ struct grape_plan {
     cd *ud_E = nullptr, *ud_C = nullptr, *ud_V = nullptr, *ud_S = nullptr, *ud_out = nullptr;
     int *ud_ovf = nullptr;
     cd *ud_gscr = nullptr;     // d > 12: tile scratch of the grape_unitary kernels
+    // general (non-Hermitian) H0, e.g. a -i Gamma/2 decay term: the chain is inverted by LU
+    // (UnitaryCalculations.jl:47) and the fidelity path runs from the materialised derivatives
+    // (grape_unitary.hip k_u_fid_head / k_u_fid_contract), one evaluation at a time
+    bool general_h0 = false;
+    cd *ud_Ci = nullptr, *d_G = nullptr;
+    std::vector<grape::VSpec> ud_vs_host;  // the variant list in ud_vs (general H0 batches)
     double *ud_Eimg = nullptr; // dense engine: the variant table as register-file images
     // small host-array calls (the reference's one-x-per-call pattern): the whole call --
     // H2D copy, every launch, D2H copies -- replayed as one captured HIP graph per batch size
@@ -223,6 +230,7 @@ static void free_plan(grape_plan *p) {
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
+                    p->ud_Ci, p->d_G, p->d_xT,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
                     p->d_fixed};
     for (void *b : bufs)
@@ -263,11 +271,12 @@ static int validate_terms(const grape_term *t, int n, int n_ops, int np, int na,
     return GRAPE_OK;
 }
 
-// The engines take C_k^-1 = C_k^dagger for the chain C_k of the NOMINAL propagators
+// The fused engines take C_k^-1 = C_k^dagger for the chain C_k of the NOMINAL propagators
 // exp(-i dt H0) and skip balancing (a permutation only for Hermitian H): both need a
 // Hermitian H0.  A term c(x) * OP keeps H0 Hermitian for every x when its function is
 // real-valued and scale * OP is Hermitian; anything else (e.g. a -i Gamma/2 decay term in
-// H0) is refused rather than computed wrongly.  Error generators need no such property:
+// H0) selects the general-H0 path (LU inverse of the chain, grape_unitary.hip) on the small
+// engine and is refused by the dense one.  Error generators need no such property:
 // their propagators only enter through differences dE (UnitaryCalculations.jl:68-83) that
 // the nominal chain transports, so a non-Hermitian Herror (a decay-rate error) is served.
 static int check_hermitian_terms(const grape_desc *desc, const grape_term *t, int n, const char *what) {
@@ -677,9 +686,13 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                                  "error source")))
             return rc;
     }
-    if (!tables) {
-        if ((rc = check_hermitian_terms(desc, desc->h0_terms, desc->n_h0_terms, "H0"))) return rc;
+    bool general_h0 = (desc->reserved[1] & GRAPE_OPT_GENERAL_H0) != 0;
+    if (!tables && !general_h0 && (rc = check_hermitian_terms(desc, desc->h0_terms, desc->n_h0_terms, "H0"))) {
+        if (rc != GRAPE_ERR_UNSUPPORTED || D > GRAPE_MAX_SMALL_DIM) return rc;
+        general_h0 = true;  // non-Hermitian H0: the general path serves it
     }
+    if (general_h0 && D > GRAPE_MAX_SMALL_DIM)
+        return fail(GRAPE_ERR_UNSUPPORTED, "general (non-Hermitian) H0: ndim <= GRAPE_MAX_SMALL_DIM only");
     // host tables: H0 / Herror are opaque closures that may read x_add, so every x_add call
     // site of the reference is tabulated (UnitaryCalculations.jl:57-64, 87-95)
     bool xadd_dep = tables && desc->nadd > 0;
@@ -795,9 +808,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.sectors = 0;
     P.nsec = 1;
     P.sec_ops = 0;
-    const SectorSetup ss = find_sectors(desc, tables);
+    p->general_h0 = general_h0;
+    const SectorSetup ss = general_h0 ? SectorSetup{} : find_sectors(desc, tables);
     const bool sec = !ss.cls.empty();
-    const size_t FR = sec ? 0 : (size_t)p->max_batch;  // whole-matrix workspace rows (none when sectors run)
+    // whole-matrix workspace rows (none when sectors or the general-H0 path run)
+    const size_t FR = (sec || general_h0) ? 0 : (size_t)p->max_batch;
 
     // operator basis: column-major interleaved -> row-major cd tiles (row builds)
     // and column-major ones (the exp kernels build columns)
@@ -866,6 +881,23 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.err_off = p->d_err_off;
     P.vs = p->d_vs;
     P.W = p->d_W;
+    if (general_h0) {  // the fidelity heads need P0 P and P as tiles (a diagonal projector: diag(w), diag(w != 0))
+        if (!ps.general) {
+            std::vector<cd> A(T, cd{0.0, 0.0}), Bm(T, cd{0.0, 0.0});
+            for (int i = 0; i < D; ++i) {
+                A[(size_t)i * D + i] = cd{ps.W[i], 0.0};
+                Bm[(size_t)i * D + i] = cd{ps.W[i] != 0.0 ? 1.0 : 0.0, 0.0};
+            }
+            if (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess ||
+                hipMemcpy(p->d_PA, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(p->d_PB, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (general H0)"));
+            P.PA = p->d_PA;
+            P.PB = p->d_PB;
+        }
+        if (dalloc(&p->ud_Ci, (size_t)P.Nt * T) != hipSuccess || dalloc(&p->d_G, (1 + (size_t)P.ne) * T) != hipSuccess)
+            return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (general H0)"));
+    }
     if (sec) {  // the sector problems of every class and the head over the assembled U
         std::vector<cd> A(T, cd{0.0, 0.0}), Bm(T, cd{0.0, 0.0});  // diagonal projector: A = diag(w), B = diag(w != 0)
         for (int i = 0; i < D; ++i) {
@@ -917,6 +949,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             const size_t RE = Ps.walk ? 0 : R;  // the walks store no E / Q
             const size_t lanes_pad = (MB * Ps.nchunks + grape::kWalkBlockA - 1) / grape::kWalkBlockA * grape::kWalkBlockA;
             if (Ps.walk_store_e && dalloc(&b.Ew, (size_t)sc.nsec * Ps.L * TS * lanes_pad) != hipSuccess)
+                return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sector walks)"));
+            if (Ps.walk && !p->d_xT && dalloc(&p->d_xT, MB * P.nx) != hipSuccess)
                 return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sector walks)"));
             if (Ps.walk && (dalloc(&b.Tc, R * Ps.nchunks * TS) != hipSuccess ||
                             dalloc(&b.wscr, 2 * (size_t)sc.nsec * ((MB * Ps.nchunks + grape::kWalkBlockA - 1) /
@@ -984,6 +1018,13 @@ int grape_plan_set_stream(grape_plan *plan, void *stream) {
     return GRAPE_OK;
 }
 
+static std::vector<grape::VSpec> ud_variants(const DevProblem &P0, grape_unitary::UProblem &UP);
+static std::vector<grape::VSpec> ud_setup(grape_plan *p, grape_unitary::UProblem &UP, grape_unitary::UBuffers &UB);
+static int ud_alloc(grape_plan *p);
+static int ud_propagators_dev(grape_plan *p, const double *d_x, int nv, const cd *d_Htab);
+static int enqueue_general(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
+                           double *d_Fd2dx, const KMark &mk);
+
 // One launch sequence of `nb` evaluations on the plan's stream over workspace rows
 // [0, nb).  The caller copies the status word afterwards.
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
@@ -1005,6 +1046,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             }
         };
     }
+    if (p->general_h0) return enqueue_general(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx, mk);
     if (p->dense) {
         grape_dense::DenseBatch DB{};
         DB.nb = nb;
@@ -1072,11 +1114,18 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.Tc = sb.Tc;  // chunk walks (null otherwise)
             B.wscr = sb.wscr;
             B.Ew = sb.Ew;
+            B.xT = p->d_xT;
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
+            sp.lane_major[cl] = p->Ps[cl].walk;
             sp.part_err[cl] = sb.part_err;
         }
         HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));
+        if (p->d_xT) {  // the walks read the controls transposed (one coalesced row per step)
+            mk(GRAPE_KERNEL_WALK_FWD, 0);
+            HIPCHECK(grape_walk::transpose_x(d_x, p->d_xT, nb, p->P.nx, st));
+            mk(GRAPE_KERNEL_WALK_FWD, 1);
+        }
         for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 0, p->Ps[cl], Bc[cl], st, mk));
         grape_proj::SectorHead H = p->SH;
         H.x = d_x;
@@ -1140,6 +1189,51 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     return GRAPE_OK;
 }
 
+// General H0 (p->general_h0): every evaluation of the launch through the materialised
+// derivatives -- its propagator table, the chain and its LU inverses, the assembly
+// (UnitaryCalculations.jl:44-155) -- then F, F_dx, F_d2err, F_d2err_dx from them
+// (FidelityCalculations.jl:19-119), on the plan's stream, one evaluation after another in
+// the single-evaluation workspace.
+static int enqueue_general(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
+                           double *d_Fd2dx, const KMark &mk) {
+    if (int rc = ud_alloc(p)) return rc;
+    const DevProblem &P = p->P;
+    const size_t T = (size_t)P.D * P.D, nx = P.nx;
+    hipStream_t st = p->stream;
+    grape_unitary::UProblem UP;
+    grape_unitary::UBuffers UB;
+    const std::vector<grape::VSpec> vs = ud_setup(p, UP, UB);
+    p->ud_vs_host = vs;  // the async copy reads this plan-owned copy
+    HIPCHECK(hipMemcpyAsync(p->ud_vs, p->ud_vs_host.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice, st));
+    grape_unitary::FidArgs FA{};
+    FA.P = P;
+    FA.U = p->ud_C + (size_t)(P.Nt - 1) * T;
+    FA.Udx = UB.Udx;
+    FA.Udxa = UB.Udxa;
+    FA.Ue = UB.Ue;
+    FA.Uedx = UB.Uedx;
+    FA.Uedxa = UB.Uedxa;
+    FA.G = p->d_G;
+    for (int b = 0; b < nb; ++b) {
+        const double *xb = d_x + (size_t)b * nx;
+        mk(GRAPE_KERNEL_EXPM, 0);
+        if (int rc = ud_propagators_dev(p, xb, UP.nv,
+                                        p->tables ? p->d_Htab + (size_t)b * P.Nt * UP.nv * T : nullptr)) return rc;
+        mk(GRAPE_KERNEL_EXPM, 1);
+        mk(GRAPE_KERNEL_GRAD, 0);
+        HIPCHECK(grape_unitary::launch_assembly(UP, UB, st));
+        FA.x = xb;
+        FA.U0tab = p->tables ? p->d_U0tab + (size_t)b * (1 + P.na) * T : nullptr;
+        FA.F = d_F + b;
+        FA.Fdx = d_Fdx + (size_t)b * nx;
+        FA.Fd2 = P.ne ? d_Fd2 + (size_t)b * P.ne : nullptr;
+        FA.Fd2dx = P.ne ? d_Fd2dx + (size_t)b * P.ne * nx : nullptr;
+        HIPCHECK(grape_unitary::launch_fidelity(FA, st));
+        mk(GRAPE_KERNEL_GRAD, 1);
+    }
+    return GRAPE_OK;
+}
+
 // Enqueue one call's batch, then copy the status word to pinned memory on the plan's stream.
 static int enqueue_call(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
                         double *d_Fd2dx) {
@@ -1184,10 +1278,11 @@ int grape_plan_synchronize(grape_plan *p) {
     HIPCHECK(hipStreamSynchronize(p->stream));
     resolve_events(p);
     const int st = *p->h_status;
-    if (st & 1) {
+    if (st & 3) {
         *p->h_status = 0;
         HIPCHECK(hipMemset(p->d_ctrl + 2, 0, sizeof(int)));
-        return fail(GRAPE_ERR_SINGULAR, "singular Pade denominator (Julia gesv! would throw SingularException)");
+        return fail(GRAPE_ERR_SINGULAR, (st & 2) ? "singular propagator chain C_k (Julia inv would throw SingularException)"
+                                                 : "singular Pade denominator (Julia gesv! would throw SingularException)");
     }
     return GRAPE_OK;
 }
@@ -1237,7 +1332,7 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
 
 static bool graph_path(const grape_plan *p, int nbatch) {
     const bool disabled = (p->P.opts & GRAPE_OPT_NO_GRAPH) != 0;
-    return !disabled && !p->profiling && !p->tables && nbatch > 0 && nbatch <= kGraphBatch &&
+    return !disabled && !p->profiling && !p->tables && !p->general_h0 && nbatch > 0 && nbatch <= kGraphBatch &&
            nbatch <= p->max_batch;
 }
 
@@ -1383,23 +1478,20 @@ static hipError_t dispatch_expm_table(int D, const DevProblem &P, const DevBatch
     return hipErrorInvalidValue;
 }
 
-// Propagator table E[k][v] of ONE x into the ud workspace: from the operator basis for the
-// variant list vs (Htab == nullptr), or -- closure fallback -- from the host-evaluated H table
-// Htab [Nt][nv][D][D] column-major, whose variant layout is vs's.
-static int ud_propagators(grape_plan *p, const double *x, const std::vector<grape::VSpec> &vs, const double *Htab) {
+// Propagator table E[k][v] of ONE x into the ud workspace, for the variant list already in
+// ud_vs (nv entries): from the operator basis (d_Htab == nullptr), or -- closure fallback --
+// from the device copy of the host-evaluated H table [Nt][nv][D][D] column-major, whose
+// variant layout is ud_vs's.  d_x: the evaluation's controls on the device.
+static int ud_propagators_dev(grape_plan *p, const double *d_x, int nv, const cd *d_Htab) {
     const DevProblem &P0 = p->P;
-    const int nv = (int)vs.size();
     hipStream_t st = p->stream;
-    const size_t T = (size_t)P0.D * P0.D;
-    HIPCHECK(hipMemcpyAsync(p->ud_vs, vs.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(p->d_ctrl, 0, 2 * sizeof(int), st));
     DevProblem Pu = P0;
     Pu.nv = nv;
     Pu.vs = p->ud_vs;
     DevBatch Bu{};
     Bu.nb = 1;
-    Bu.x = p->d_x;
+    Bu.x = d_x;
     Bu.E = p->ud_E;
     Bu.overflow = p->ud_ovf;
     Bu.overflow_count = p->d_ctrl;
@@ -1410,18 +1502,30 @@ static int ud_propagators(grape_plan *p, const double *x, const std::vector<grap
         DPu.P.vs = p->ud_vs;
         grape_dense::DenseBatch DB{};
         DB.nb = 1;
-        DB.x = p->d_x;
+        DB.x = d_x;
         DB.E = p->ud_Eimg;
         DB.status = p->d_ctrl + 2;
         HIPCHECK(grape_dense::launch_variant_table(DPu, DB, p->ud_E, st));
-    } else if (Htab) {
-        HIPCHECK(hipMemcpyAsync(p->d_Htab, Htab, (size_t)P0.Nt * nv * T * sizeof(cd), hipMemcpyHostToDevice, st));
-        Bu.Htab = p->d_Htab;
+    } else if (d_Htab) {
+        Bu.Htab = d_Htab;
         HIPCHECK(dispatch_expm_table(P0.D, Pu, Bu, st));
     } else {
         HIPCHECK(dispatch_expm_variants(P0.D, Pu, Bu, st));
     }
     return GRAPE_OK;
+}
+
+// The same for a host x (and host H table): uploads the variant list, x and the table first.
+static int ud_propagators(grape_plan *p, const double *x, const std::vector<grape::VSpec> &vs, const double *Htab) {
+    const DevProblem &P0 = p->P;
+    const int nv = (int)vs.size();
+    hipStream_t st = p->stream;
+    const size_t T = (size_t)P0.D * P0.D;
+    p->ud_vs_host = vs;  // the async copy reads this plan-owned copy
+    HIPCHECK(hipMemcpyAsync(p->ud_vs, p->ud_vs_host.data(), vs.size() * sizeof(grape::VSpec), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)P0.nx * sizeof(double), hipMemcpyHostToDevice, st));
+    if (Htab) HIPCHECK(hipMemcpyAsync(p->d_Htab, Htab, (size_t)P0.Nt * nv * T * sizeof(cd), hipMemcpyHostToDevice, st));
+    return ud_propagators_dev(p, p->d_x, nv, Htab ? p->d_Htab : nullptr);
 }
 
 // nominal propagators E_k and the chain C_k of one x into the ud workspace (H0tab: the
@@ -1446,13 +1550,21 @@ static int ud_chain(grape_plan *p, const double *x, const double *H0tab) {
 static int ud_interaction(grape_plan *p, const double *x, const double *H0tab, const double *Oerr) {
     if (int rc = ud_alloc(p)) return rc;
     if (int rc = ud_chain(p, x, H0tab)) return rc;
+    const cd *Ci = nullptr;
+    if (p->general_h0) {  // cum_evo_inv = inv(cum_evo) (UnitaryCalculations.jl:194)
+        grape_unitary::UProblem UP{};
+        UP.D = p->P.D;
+        UP.Nt = p->P.Nt;
+        HIPCHECK(grape_unitary::launch_inverse(UP, p->ud_C, p->ud_Ci, p->d_ctrl + 2, p->stream));
+        Ci = p->ud_Ci;
+    }
     if (Oerr) {
         cd *dO = p->ud_V;  // Nt * nslots >= Nt * ne tiles
         const size_t n = (size_t)p->P.D * p->P.D * p->P.Nt * p->P.ne;
         HIPCHECK(hipMemcpyAsync(dO, Oerr, n * sizeof(cd), hipMemcpyHostToDevice, p->stream));
-        HIPCHECK(grape_unitary::launch_interaction_table(p->P, dO, p->ud_C, p->ud_out, p->ud_gscr, p->stream));
+        HIPCHECK(grape_unitary::launch_interaction_table(p->P, dO, p->ud_C, Ci, p->ud_out, p->ud_gscr, p->stream));
     } else {
-        HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, p->ud_out, p->ud_gscr, p->stream));
+        HIPCHECK(grape_unitary::launch_interaction(p->P, p->d_x, p->ud_C, Ci, p->ud_out, p->ud_gscr, p->stream));
     }
     return GRAPE_OK;
 }
@@ -1552,14 +1664,14 @@ static std::vector<grape::VSpec> ud_variants(const DevProblem &P0, grape_unitary
     return vs;
 }
 
-static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, double *U, double *U_dx,
-                          double *U_dx_add, double *U_derr, double *U_derr_dx, double *U_derr_dx_add) {
-    HIPCHECK(hipSetDevice(p->device));
+// The assembly problem and buffers of the ud workspace (outputs packed in ud_out:
+// U_dx | U_dx_add | U_derr | U_derr_dx | U_derr_dx_add); returns the variant list.
+static std::vector<grape::VSpec> ud_setup(grape_plan *p, grape_unitary::UProblem &UP, grape_unitary::UBuffers &UB) {
     const DevProblem &P0 = p->P;
     const int D = P0.D, Nt = P0.Nt, np = P0.np, na = P0.na, ne = P0.ne;
     const size_t T = (size_t)D * D;
-    grape_unitary::UProblem UP{};
-    const std::vector<grape::VSpec> vs = ud_variants(P0, UP);
+    UP = grape_unitary::UProblem{};
+    std::vector<grape::VSpec> vs = ud_variants(P0, UP);
     UP.D = D;
     UP.Nt = Nt;
     UP.np = np;
@@ -1569,15 +1681,13 @@ static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, do
     UP.nslots = np + na + ne + ne * (np + na);
     UP.inv_eps = P0.inv_eps;
     UP.inv_eps2sq = 1.0 / (P0.eps2 * P0.eps2);
-    // outputs, packed: U_dx | U_dx_add | U_derr | U_derr_dx | U_derr_dx_add
-    const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
-    if (int rc = ud_alloc(p)) return rc;
-    if (int rc = ud_propagators(p, x, vs, Htab)) return rc;
     UP.gscr = p->ud_gscr;
-    hipStream_t st = p->stream;
-    grape_unitary::UBuffers UB{};
+    const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne;
+    UB = grape_unitary::UBuffers{};
     UB.E = p->ud_E;
     UB.C = p->ud_C;
+    UB.Ci = p->general_h0 ? p->ud_Ci : nullptr;
+    UB.status = p->d_ctrl + 2;
     UB.V = p->ud_V;
     UB.S = p->ud_S;
     UB.Udx = p->ud_out;
@@ -1585,6 +1695,22 @@ static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, do
     UB.Ue = UB.Udxa + n_dxa;
     UB.Uedx = UB.Ue + n_e;
     UB.Uedxa = UB.Uedx + n_edx;
+    return vs;
+}
+
+static int unitary_derivs(grape_plan *p, const double *x, const double *Htab, double *U, double *U_dx,
+                          double *U_dx_add, double *U_derr, double *U_derr_dx, double *U_derr_dx_add) {
+    HIPCHECK(hipSetDevice(p->device));
+    const DevProblem &P0 = p->P;
+    const int D = P0.D, Nt = P0.Nt, np = P0.np, na = P0.na, ne = P0.ne;
+    const size_t T = (size_t)D * D;
+    if (int rc = ud_alloc(p)) return rc;
+    grape_unitary::UProblem UP;
+    grape_unitary::UBuffers UB;
+    const std::vector<grape::VSpec> vs = ud_setup(p, UP, UB);
+    const size_t n_dx = T * np * Nt, n_dxa = T * na, n_e = T * ne, n_edx = T * np * Nt * ne, n_edxa = T * na * ne;
+    if (int rc = ud_propagators(p, x, vs, Htab)) return rc;
+    hipStream_t st = p->stream;
     HIPCHECK(grape_unitary::launch_assembly(UP, UB, st));
     std::vector<cd> Ulast(T);
     HIPCHECK(hipMemcpyAsync(Ulast.data(), p->ud_C + (size_t)(Nt - 1) * T, T * sizeof(cd), hipMemcpyDeviceToHost, st));

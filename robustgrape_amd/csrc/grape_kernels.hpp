@@ -124,7 +124,9 @@ struct DevBatch {
     const cd *Htab;         // [nb][Nt][nv][D][D] column-major H at every closure call site (else null)
     const cd *U0tab;        // [nb][1 + na][D][D] column-major target at x_add, x_add + eps e_q (else null)
     cd *gp_scr;             // general projector: head scratch (grape_projector_api.hpp)
-    double *sec_part;       // sectors: [nb][Nt][nvg] per-sector F_dx terms (k_sec_reduce sums them), else null
+    double *sec_part;       // sectors: [nb][Nt][nvg] per-sector F_dx terms (k_sec_reduce sums them), else null;
+                            // chunk walks: [nsec][Nt][nvg][nb / nsec], the evaluation fastest (coalesced)
+    const double *xT;       // chunk walks: the controls transposed, [nx][nb / nsec] (coalesced lane reads)
     const cd *Msec;         // sectors: [nb][D][D] the sector blocks of M = G U (the sector head)
     // sectors with error sources
     double *sec_part_err;   // [nb][ne][Nt][nvg] per-sector F_d2err_dx terms (k_sec_reduce_err sums them)
@@ -984,25 +986,45 @@ __global__ void k_sec_mc_err(DevProblem P, DevBatch B) {
 }
 
 // Sectors: F_dx[b][k, u] (or the per-step x_add term) = sum over the evaluation's sectors of
-// both classes, in sector order (deterministic).  One thread per (b, k, u).
+// both classes, in sector order (deterministic).  A class's terms are laid out per evaluation
+// ([nb][nsec][Nt][nvg]) or, from the chunk walks, evaluation-fastest ([nsec][Nt][nvg][nb]);
+// one workgroup transposes a 32 x 32 tile of (evaluation, k * nvg + u) through LDS so that both
+// the walk layout's reads and the F_dx rows' writes are coalesced.
 struct SecParts {
-    const double *part[2];      // [nb][nsec_c][Nt][nvg] per sector class
+    const double *part[2];      // per sector class, layout by lane_major
     const double *part_err[2];  // [nb][nsec_c][ne][Nt][nvg] (error sources)
     int nsec[2];                // 0 for an absent class
+    int lane_major[2];          // 1: [nsec][Nt][nvg][nb] (chunk walks)
 };
+constexpr int kRedTile = 32;
 template <int D>
-__global__ void k_sec_reduce(DevProblem P, double *Fdx, double *part_add, SecParts S, int nb) {
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_sec_reduce(DevProblem P, double *Fdx, double *part_add, SecParts S, int nb) {
+    __shared__ double tile[kRedTile][kRedTile + 1];
     const long per = (long)P.Nt * P.nvg;
-    if (t >= (long)nb * per) return;
-    const int b = (int)(t / per);
-    const long r = t - (long)b * per;  // k * nvg + u
-    const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
-    double s = 0.0;
-    for (int c = 0; c < 2; ++c)
-        for (int w = 0; w < S.nsec[c]; ++w) s += S.part[c][((size_t)b * S.nsec[c] + w) * per + r];
-    if (u < P.np) Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
-    else part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
+    const int b0 = blockIdx.x * kRedTile;
+    const long r0 = (long)blockIdx.y * kRedTile;
+    const int tx = threadIdx.x % kRedTile, ty = threadIdx.x / kRedTile;
+    for (int i = ty; i < kRedTile; i += 256 / kRedTile) {  // reads: the evaluation fastest
+        const int b = b0 + tx;
+        const long r = r0 + i;
+        double s = 0.0;
+        if (b < nb && r < per)
+            for (int c = 0; c < 2; ++c)
+                for (int w = 0; w < S.nsec[c]; ++w)
+                    s += S.lane_major[c] ? S.part[c][((size_t)w * per + r) * nb + b]
+                                         : S.part[c][((size_t)b * S.nsec[c] + w) * per + r];
+        tile[i][tx] = s;
+    }
+    __syncthreads();
+    for (int i = ty; i < kRedTile; i += 256 / kRedTile) {  // writes: k * nvg + u fastest
+        const int b = b0 + i;
+        const long r = r0 + tx;
+        if (b >= nb || r >= per) continue;
+        const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
+        const double s = tile[tx][i];
+        if (u < P.np) Fdx[(size_t)b * P.nx + (size_t)k * P.np + u] = s;
+        else part_add[((size_t)b * P.Nt + k) * P.na + (u - P.np)] = s;
+    }
 }
 
 // The same for F_d2err_dx (or its per-step x_add term), one thread per (b, e, k, u).

@@ -310,9 +310,11 @@ template <int D>
 hipError_t launch_sector_reduce(const DevProblem &P, const DevBatch &B, const grape::SecParts &S, int nev,
                                 hipStream_t st, const KMark &mark) {
     mark(GRAPE_KERNEL_REDUCE, 0);
-    const long nred = (long)nev * P.Nt * P.nvg;
-    hipLaunchKernelGGL(grape::k_sec_reduce<D>, dim3((unsigned)((nred + 255) / 256)), dim3(256), 0, st, P, B.Fdx,
-                       B.part_add, S, nev);
+    const long nred = (long)nev * P.Nt * P.nvg, per = (long)P.Nt * P.nvg;
+    hipLaunchKernelGGL(grape::k_sec_reduce<D>,
+                       dim3((unsigned)((nev + grape::kRedTile - 1) / grape::kRedTile),
+                            (unsigned)((per + grape::kRedTile - 1) / grape::kRedTile)),
+                       dim3(256), 0, st, P, B.Fdx, B.part_add, S, nev);
     if (P.ne > 0)
         hipLaunchKernelGGL(grape::k_sec_reduce_err<D>, dim3((unsigned)((nred * P.ne + 255) / 256)), dim3(256), 0, st,
                            P, B.Fd2dx, B.part_err_add, S, nev);

@@ -34,22 +34,42 @@ struct UProblem {
 struct UBuffers {
     const cd *E;  // [Nt][nv][D][D] row-major
     cd *C;        // [Nt][D][D]     C_k
+    cd *Ci;       // [Nt][D][D]     C_k^-1 (general H0; null: C_k^dagger, Hermitian H0)
+    int *status;  // bit 1: a singular C_k (general H0)
     cd *V;        // [Nt][nslots][D][D]
     cd *S;        // [Nt][ne][D][D] cumulative sums of V^err
     cd *Udx, *Uedx, *Udxa, *Ue, *Uedxa;  // outputs, reference column-major layouts
 };
 
 hipError_t launch_assembly(const UProblem &P, const UBuffers &B, hipStream_t st);
+// Ci_k = C_k^-1 by Gauss-Jordan with partial pivoting (general H0, UnitaryCalculations.jl:47);
+// status bit 1 on a singular C_k
+hipError_t launch_inverse(const UProblem &P, const cd *C, cd *Ci, int *status, hipStream_t st);
 // C_k = E_k C_{k-1} for the nominal table E[k][0] (P.nv variants per step)
 hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st);
-// O[:, :, k, e] = C_{k-1}^dagger (Herror_e(k, eps) / eps) C_{k-1}, column-major (d, d, Nt, ne)
-// (UnitaryCalculations.jl:180-204); x is the plan's device copy of the control vector
-hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, cd *O, cd *gscr,
-                              hipStream_t st);
+// O[:, :, k, e] = C_{k-1}^-1 (Herror_e(k, eps) / eps) C_{k-1}, column-major (d, d, Nt, ne)
+// (UnitaryCalculations.jl:180-204; C^-1 = Ci when given, else C^dagger); x is the plan's device
+// copy of the control vector
+hipError_t launch_interaction(const grape::DevProblem &P, const double *x, const cd *C, const cd *Ci, cd *O,
+                              cd *gscr, hipStream_t st);
 // The same from host-evaluated closures (closure fallback): Oerr [Nt][ne][D][D] column-major
 // holds (1/eps) Herror_e(k, x_k, x_add, eps) as the reference forms it
-hipError_t launch_interaction_table(const grape::DevProblem &P, const cd *Oerr, const cd *C, cd *O, cd *gscr,
-                                    hipStream_t st);
+hipError_t launch_interaction_table(const grape::DevProblem &P, const cd *Oerr, const cd *C, const cd *Ci, cd *O,
+                                    cd *gscr, hipStream_t st);
+// General H0 (non-Hermitian, e.g. a -i Gamma/2 decay term): F, F_dx, F_d2err, F_d2err_dx of ONE
+// evaluation from its materialised derivatives (launch_assembly's outputs, reference layouts),
+// FidelityCalculations.jl:19-119.  P.PA / P.PB: the projector's P0 P and P (row-major; for a
+// diagonal projector diag(w), diag(w != 0)).
+struct FidArgs {
+    grape::DevProblem P;
+    const double *x;     // [nx] this evaluation's controls (operator-basis target terms)
+    const cd *U0tab;     // [1 + na][D][D] column-major host target table (closures), else null
+    const cd *U;         // [D][D] row-major C_Nt
+    const cd *Udx, *Udxa, *Ue, *Uedx, *Uedxa;  // launch_assembly outputs
+    cd *G;               // [1 + ne][D][D] scratch: the functionals of the controls and of each error
+    double *F, *Fdx, *Fd2, *Fd2dx;  // this evaluation's outputs ([1], [nx], [ne], [ne][nx])
+};
+hipError_t launch_fidelity(const FidArgs &A, hipStream_t st);
 // ev[k + Nt e] = Re(dt tr(P0 sum_{j<=k} O_j,e) / D)   (FidelityCalculations.jl:368-390)
 hipError_t launch_expectation(const grape::DevProblem &P, const cd *O, double *ev, hipStream_t st);
 

@@ -389,9 +389,10 @@ struct X2 {
 // Unconditional loads (the second one clamped into the vector): a load under a branch leaves the
 // compiler without a static count of the outstanding vector-memory operations, and it then waits
 // with vmcnt(0) -- for every store of the step too -- before the prefetched value is used.
-__device__ __forceinline__ X2 walk_load_x(int n, const double *xs) {  // n (uniform, >= 1 here) <= 2 values
+// xs: the transposed controls (B.xT) at this lane's evaluation, consecutive values `stride` apart
+__device__ __forceinline__ X2 walk_load_x(int n, const double *xs, int stride) {  // n (uniform) <= 2 values
     X2 r;
-    const double a = xs[0], b = xs[n > 1 ? 1 : 0];
+    const double a = xs[0], b = xs[n > 1 ? stride : 0];
     r.v0 = n > 0 ? a : 0.0;
     r.v1 = n > 1 ? b : 0.0;
     return r;
@@ -495,26 +496,29 @@ struct MStore<D, true> {
     }
 };
 
-// Launch geometry: one lane per (evaluation be, chunk c) and group of NS sectors (w0 = NS *
-// blockIdx.y); sub-evaluation of sector w: be * nsec + w.  Lanes past the end (ok = false) run
-// the walk on clamped indices and store nothing, so that every loop in the walks has a
-// wave-uniform trip count (scalar loads of the term tables).
+// Launch geometry: one lane per (chunk c, evaluation be) -- the evaluation fastest, so that a
+// wave's per-step reads of the transposed controls (B.xT) and stores of its F_dx terms (B.sec_part,
+// evaluation-fastest) are contiguous -- and group of NS sectors (w0 = NS * blockIdx.y);
+// sub-evaluation of sector w: be * nsec + w.  Lanes past the end (ok = false) run the walk on
+// clamped indices and store nothing, so that every loop in the walks has a wave-uniform trip
+// count (scalar loads of the term tables).
 struct WalkLane {
-    int w0, be, c;
-    long slot;  // the lane's scratch slot (NS consecutive pairs of D x D tiles)
+    int w0, be, c, nbe;  // nbe: evaluations of the launch (the stride of B.xT and B.sec_part)
+    long slot;           // the lane's scratch slot (NS consecutive pairs of D x D tiles)
     bool ok;
 };
 template <int NS>
 __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatch &B) {
     WalkLane L;
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const long per = (long)(B.nb / ns) * P.nchunks;
+    L.nbe = B.nb / ns;
+    const long per = (long)L.nbe * P.nchunks;
     const long g = (long)blockIdx.x * kWalkBlock + threadIdx.x;
     L.w0 = blockIdx.y * NS;
     L.ok = g < per;
     const long gg = L.ok ? g : 0;
-    L.be = (int)(gg / P.nchunks);
-    L.c = (int)(gg - (long)L.be * P.nchunks);
+    L.c = (int)(gg / L.nbe);
+    L.be = (int)(gg - (long)L.c * L.nbe);
     // own scratch slot for every lane, past-the-end ones included (they walk lane 0's inputs)
     const long per_pad = (per + kWalkBlock - 1) / kWalkBlock * kWalkBlock;
     L.slot = (long)blockIdx.y * per_pad + g;
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B);
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const double *xb = B.x + (size_t)L.be * P.nx;
+    const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
     cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
     Pert none;
@@ -568,9 +572,9 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
         E.p = MStore<D, true>::slot(lds);
     }
     WalkX X;
-    walk_set_xa(X, walk_load_x(P.na, xb + (size_t)P.np * P.Nt));  // x_add
+    walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));  // x_add
     const int k0 = L.c * P.L;
-    X2 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
+    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
     cd Q[NS][D][D];
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
@@ -585,7 +589,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = k0 + jj < P.Nt;
         walk_set_xk(X, xn);
-        xn = walk_load_x(P.np, xb + (size_t)min(k + 1, P.Nt - 1) * P.np);  // next step's controls
+        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
         SM<D> A[NS];
         walk_build<D, NS>(P, ops, X, k + 1, none, A);
 #pragma unroll
@@ -645,7 +649,7 @@ void k_walk_grad(DevProblem P, DevBatch B) {
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B);
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const double *xb = B.x + (size_t)L.be * P.nx;
+    const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
     cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
     Pert none;
@@ -686,16 +690,16 @@ void k_walk_grad(DevProblem P, DevBatch B) {
         }
     }
     WalkX XV;
-    walk_set_xa(XV, walk_load_x(P.na, xb + (size_t)P.np * P.Nt));
+    walk_set_xa(XV, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));
     const int k0 = L.c * P.L;
-    X2 xn = walk_load_x(P.np, xb + (size_t)min(k0, P.Nt - 1) * P.np);
+    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
     const cptr<VSpec> vs = as_constant(P.vs);
 #pragma unroll 1
     for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store nothing
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = L.ok && k0 + jj < P.Nt;
         walk_set_xk(XV, xn);
-        xn = walk_load_x(P.np, xb + (size_t)min(k + 1, P.Nt - 1) * P.np);  // next step's controls
+        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
         if constexpr (STORED) {  // this step's propagators; the next step's loads go out now
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
@@ -764,7 +768,7 @@ void k_walk_grad(DevProblem P, DevBatch B) {
                     }
                 });
                 // unconditional store (inactive lanes write the sink): exact vmcnt accounting
-                double *dst = act ? B.sec_part + ((((size_t)L.be * ns + L.w0 + w) * P.Nt) + k) * P.nvg + u
+                double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
                                   : reinterpret_cast<double *>(B.sink);
                 *dst = s;
             }

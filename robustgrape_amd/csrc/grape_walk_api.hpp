@@ -16,4 +16,6 @@ namespace grape_walk {
 // B.Tc), stage 1 = k_walk_grad (per-sector F_dx terms to B.sec_part)
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
+// the walks' controls: x [nb][nx] -> xT [nx][nb] (B.xT), once per launch for every walk class
+hipError_t transpose_x(const double *x, double *xT, int nb, int nx, hipStream_t st);
 }  // namespace grape_walk

@@ -48,6 +48,28 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
     return hipGetLastError();
 }
 
+// x [nb][nx] -> xT [nx][nb] through a 32 x 32 LDS tile (both sides coalesced)
+__global__ __launch_bounds__(256) void k_transpose_x(const double *x, double *xT, int nb, int nx) {
+    __shared__ double t[32][33];
+    const int b0 = blockIdx.x * 32, q0 = blockIdx.y * 32, tx = threadIdx.x % 32, ty = threadIdx.x / 32;
+    for (int i = ty; i < 32; i += 8) {
+        const int b = b0 + i, q = q0 + tx;
+        if (b < nb && q < nx) t[i][tx] = x[(size_t)b * nx + q];
+    }
+    __syncthreads();
+    for (int i = ty; i < 32; i += 8) {
+        const int q = q0 + i, b = b0 + tx;
+        if (b < nb && q < nx) xT[(size_t)q * nb + b] = t[tx][i];
+    }
+}
+
+hipError_t transpose_x(const double *x, double *xT, int nb, int nx, hipStream_t st) {
+    if (nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_transpose_x, dim3((unsigned)((nb + 31) / 32), (unsigned)((nx + 31) / 32)), dim3(256), 0, st, x,
+                       xT, nb, nx);
+    return hipGetLastError();
+}
+
 template hipError_t launch<2>(int, const grape::DevProblem &, const grape::DevBatch &, hipStream_t);
 template hipError_t launch<3>(int, const grape::DevProblem &, const grape::DevBatch &, hipStream_t);
 template hipError_t launch<4>(int, const grape::DevProblem &, const grape::DevBatch &, hipStream_t);

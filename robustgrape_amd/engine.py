@@ -15,8 +15,8 @@ from collections import OrderedDict
 import numpy as np
 
 from . import _capi
-from .operators import DescriptorBuffers, TableDescriptor, has_operator_basis
-from .tables import SharedTables, get_workers, host_tables, table_batch_cap, table_shapes
+from .operators import OPT_GENERAL_H0, DescriptorBuffers, TableDescriptor, has_operator_basis
+from .tables import SharedTables, get_workers, host_tables, is_hermitian_h0, table_batch_cap, table_shapes
 from .types import FidelityRobustGRAPEProblem, split_x
 
 
@@ -51,6 +51,23 @@ class GrapePlan:
         h = ctypes.c_void_p()
         _capi.check(L.grape_plan_create(ctypes.byref(self._bufs.desc), self.device, ctypes.byref(h)))
         self.handle = h
+        self._stream_ptr = None
+
+    def general_h0_for(self, H0s):
+        """Closure plans: the host sees H0 only as tables; a non-Hermitian nominal H0 (e.g. a
+        -i Gamma/2 decay term) recreates the plan on the general-H0 path (GRAPE_OPT_GENERAL_H0,
+        the reference's LU-inverted chain, UnitaryCalculations.jl:47) before the device call.
+        H0s: nominal H0 matrices (any leading shape, either storage order)."""
+        if not self.tables or (self.options & OPT_GENERAL_H0) or is_hermitian_h0(H0s):
+            return
+        self.options |= OPT_GENERAL_H0
+        self._bufs.desc.reserved[1] = self.options
+        h = ctypes.c_void_p()
+        _capi.check(_capi.lib().grape_plan_create(ctypes.byref(self._bufs.desc), self.device, ctypes.byref(h)))
+        _capi.lib().grape_plan_destroy(self.handle)
+        self.handle = h
+        if self._stream_ptr:
+            self.set_stream(self._stream_ptr)
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
@@ -79,6 +96,7 @@ class GrapePlan:
         None / 0 selects the plan's own stream -- so torch's default (null) stream cannot be
         joined this way: use a side stream and wait_stream (optimize.RobustCost does)."""
         _capi.check(_capi.lib().grape_plan_set_stream(self.handle, ctypes.c_void_p(stream_ptr or None)))
+        self._stream_ptr = stream_ptr
 
     def fidelity_grad(self, X):
         """Host arrays in/out. X: (nbatch, n_x). Returns F (nb,), F_dx (nb, n_x),
@@ -127,6 +145,7 @@ class GrapePlan:
         if shipped is None or self._shared is None:  # serial, chunk by chunk
             for b0, n in chunks:
                 H, U0 = host_tables(self.fp, X[b0:b0 + n], self.nparam)
+                self.general_h0_for(H[:, :, 0])
                 _capi.check(L.grape_fidelity_grad_tables(
                     self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(H), _capi.dptr(U0),
                     _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
@@ -144,6 +163,7 @@ class GrapePlan:
                     r.get()
                 del pending[j]  # kept until every task of the chunk is done: drained below on error
                 tabs = self._shared[j % 2]
+                self.general_h0_for(tabs.H[:n, :, 0])
                 _capi.check(L.grape_fidelity_grad_tables(
                     self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(tabs.H), _capi.dptr(tabs.U0),
                     _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
@@ -179,6 +199,7 @@ class GrapePlan:
         ptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if a.size else None
         if self.tables:  # closure problem: every closure call site evaluated here
             H, _ = host_tables(self.fp, x[None, :], self.nparam)
+            self.general_h0_for(H[:, :, 0])
             _capi.check(_capi.lib().grape_unitary_derivs_tables(self.handle, _capi.dptr(x), _capi.dptr(H),
                                                                 *[ptr(a) for a in outs]))
         else:

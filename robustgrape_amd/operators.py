@@ -163,6 +163,7 @@ def projector_arrays(fp):
 # same outputs, fixed at plan creation (A/B measurements and cross-path tests)
 OPT_NO_SECTORS, OPT_NO_LANE, OPT_NO_CHAIN, OPT_NO_WALK, OPT_NO_GRAPH = 1, 2, 4, 8, 16
 OPT_WALK_RECOMPUTE = 32
+OPT_GENERAL_H0 = 64  # non-Hermitian H0: LU-inverted chain, fidelity from the materialised derivatives
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):
@@ -267,7 +268,7 @@ class TableDescriptor:
 
 
 # the closure tables themselves: robustgrape_amd/tables.py
-from .tables import check_hermitian_h0, host_tables, table_variants  # noqa: E402,F401
+from .tables import host_tables, is_hermitian_h0, table_variants  # noqa: E402,F401
 
 
 def host_interaction_tables(up, x, nparam: int):
@@ -285,7 +286,6 @@ def host_interaction_tables(up, x, nparam: int):
     for k in range(nt):
         xk = x_main[:, k]
         H0[k] = np.asarray(up.H0(k + 1, xk.copy(), x_add.copy()), np.complex128).T
-        check_hermitian_h0(H0[k:k + 1])
         for e, es in enumerate(errs):
             Oerr[k, e] = ((1 / eps) * np.asarray(es.Herror(k + 1, xk.copy(), x_add.copy(), eps), np.complex128)).T
     return H0, Oerr

@@ -89,7 +89,6 @@ def fill_tables(fp, X, nparam: int, H, U0, rows, k0: int, k1: int, target: bool 
                 Hb[base + 1] = (asc(es.Herror(nt1, xk.copy(), x_add.copy(), eps2), np.complex128) + H0k).T
                 for u in range(n):
                     Hb[base + 2 + u] = (asc(es.Herror(nt1, *at(u, eps2), eps2), np.complex128) + Hx2[u]).T
-        check_hermitian_h0(H[b, k0:k1, 0], b)
         if target:
             U0[b, 0] = asc(tgt(x_add.copy())).T
             for q in range(na):
@@ -98,17 +97,17 @@ def fill_tables(fp, X, nparam: int, H, U0, rows, k0: int, k1: int, target: bool 
                 U0[b, 1 + q] = asc(tgt(xa)).T
 
 
-def check_hermitian_h0(H0s, row=0, rtol=1e-12):
-    """The device chains the nominal propagators with C_k^-1 = C_k^dagger and skips balancing
-    (valid for Hermitian H0 only): refuse a non-Hermitian nominal H0(nt, x, x_add) -- e.g. a
-    -i Gamma/2 decay term -- instead of computing it wrongly (error generators are exempt:
-    their propagators only enter through differences the nominal chain transports)."""
+def is_hermitian_h0(H0s, rtol=1e-12) -> bool:
+    """Whether the tabulated nominal H0(nt, x, x_add) matrices are Hermitian.  The fused device
+    path chains the nominal propagators with C_k^-1 = C_k^dagger; a non-Hermitian H0 -- e.g. a
+    -i Gamma/2 decay term -- moves the plan to the general-H0 path (GRAPE_OPT_GENERAL_H0: the LU
+    inverse of UnitaryCalculations.jl:47).  Error generators need no such property: their
+    propagators only enter through differences the nominal chain transports."""
+    H0s = np.asarray(H0s)
     if H0s.size == 0:
-        return
+        return True
     dev = np.max(np.abs(H0s - np.conj(np.swapaxes(H0s, -1, -2))))
-    if not dev <= rtol * max(np.max(np.abs(H0s)), 1e-300):
-        raise ValueError(f"H0 is not Hermitian (evaluation {row}: max |H - H^dagger| = {dev:.3e}); the device "
-                         "engine needs unitary nominal propagators")
+    return bool(dev <= rtol * max(np.max(np.abs(H0s)), 1e-300))
 
 
 def table_shapes(fp, nb: int, nparam: int):
@@ -159,12 +158,9 @@ _KEEP_PROBLEMS = 8
 def _attach(name):
     shm = _shm_cache.get(name)
     if shm is None:
+        # attaching registers the name with the resource tracker the spawned workers share with
+        # the creating process (a set: no second entry); the creator's unlink unregisters it
         shm = shared_memory.SharedMemory(name=name)
-        try:  # the creating process owns the segment: keep this process's tracker off it
-            from multiprocessing import resource_tracker
-            resource_tracker.unregister(shm._name, "shared_memory")
-        except Exception:
-            pass
         _shm_cache[name] = shm
     return shm
 

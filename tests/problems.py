@@ -175,3 +175,20 @@ def xadd_x(ntimes, seed):
     """Control vector of xadd_err_problem: x_main = 2pi U, theta = 2pi U, detuning U[-0.5, 0.5)."""
     rng = np.random.default_rng(seed)
     return np.concatenate([2 * math.pi * rng.uniform(size=ntimes), [2 * math.pi * rng.uniform(), rng.uniform(-0.5, 0.5)]])
+
+
+def with_decay(fp, gamma=0.4, levels=(4,), device=True):
+    """fp with a non-Hermitian H0: -i gamma/2 on each of `levels` (a Rydberg-decay term, the
+    reference accepts any H0: UnitaryCalculations.jl:45-47 exponentiates and LU-inverts it).
+    Device form: one more OperatorBasisHamiltonian term; oracle form: a wrapped closure."""
+    up = fp.unitary_problem
+    G = np.zeros((up.ndim, up.ndim), np.complex128)
+    for l in levels:
+        G[l, l] = 1.0
+    if device:
+        from robustgrape_amd.operators import OperatorBasisHamiltonian, Term
+        H0 = OperatorBasisHamiltonian(list(up.H0.terms) + [Term(G, scale=-0.5j * gamma)])
+    else:
+        h = up.H0
+        H0 = lambda t, p, xa: np.asarray(h(t, p, xa), np.complex128) - 0.5j * gamma * G  # noqa: E731
+    return fp.replace(unitary_problem=up.replace(H0=H0))

@@ -125,32 +125,37 @@ def _create(fp, nparam=1):
     return rc, _capi.lib().grape_last_error().decode()
 
 
-def test_non_hermitian_generators_are_refused():
-    """The engines use C_k^-1 = C_k^dagger: a non-Hermitian H (a -i Gamma/2 decay term, a complex
-    scale on a Hermitian operator) must be refused at plan creation, not computed wrongly."""
+def test_non_hermitian_h0_selects_the_general_path():
+    """A non-Hermitian H0 (a -i Gamma/2 decay term, a non-Hermitian scale * operator) passes
+    validation on the small engine (the general-H0 path: LU-inverted chain, include/grape.h
+    GRAPE_OPT_GENERAL_H0) -- here the device lookup then reports -6 -- and is refused by the
+    dense engine (d > 12), whose solve relies on a Hermitian H."""
     from robustgrape_amd.operators import OperatorBasisHamiltonian, Term
     fp = P.sym_problem(8)
     up = fp.unitary_problem
     decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
     terms = list(up.H0.terms)
-    bad = [fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(terms + [Term(decay, scale=-0.5j)]))),
-           fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(
-               terms + [Term(np.triu(np.ones((5, 5))).astype(complex))])))]
-    for f in bad:
+    for f in [fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(terms + [Term(decay, scale=-0.5j)]))),
+              fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(
+                  terms + [Term(np.triu(np.ones((5, 5))).astype(complex))])))]:
         rc, msg = _create(f)
-        assert rc == -2 and "Hermitian" in msg, (rc, msg)
+        assert rc in (0, -6), (rc, msg)
     # a non-Hermitian ERROR generator (decay-rate error) is accepted: only H0 chains
     from robustgrape_amd.operators import OperatorBasisError
     from robustgrape_amd.types import ErrorSource
     derr = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(OperatorBasisError([Term(decay, scale=-0.5j)]))]))
     rc, msg = _create(derr)
     assert rc in (0, -6), (rc, msg)
-    # a complex scale that keeps the term Hermitian (i * antisymmetric real) is accepted past validation
-    anti = np.zeros((5, 5), complex)
-    anti[0, 1], anti[1, 0] = 1.0, -1.0
-    ok = fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(terms + [Term(anti, scale=1j)])))
-    rc, msg = _create(ok)
-    assert rc in (0, -6), (rc, msg)  # -6: no device on this host
+    # dense engine: refused with the reason
+    from robustgrape_amd import synthetic as S
+    dfp = S.dense_problem(d=16, ntimes=4)
+    dup = dfp.unitary_problem
+    dterms = list(dup.H0.terms)
+    ddecay = np.zeros((16, 16), complex)
+    ddecay[3, 3] = 1.0
+    bad = dfp.replace(unitary_problem=dup.replace(H0=OperatorBasisHamiltonian(dterms + [Term(ddecay, scale=-0.5j)])))
+    rc, msg = _create(bad, nparam=2)  # the C5 family's two controls
+    assert rc == -2 and "Hermitian" in msg, (rc, msg)
 
 
 def test_plan_cache_is_bounded_and_keyed_by_problem(monkeypatch):
@@ -187,18 +192,21 @@ def test_plan_cache_is_bounded_and_keyed_by_problem(monkeypatch):
     assert engine.cached_plan_count() == 0 and all(p.closed for p in made)
 
 
-def test_closure_tables_refuse_non_hermitian_h0():
-    """Closure fallback: a non-Hermitian nominal H0 is refused on the host (tables.check_hermitian_h0);
-    a non-Hermitian error generator is tabulated (only differences of its propagators are used)."""
-    from robustgrape_amd.tables import host_tables
+def test_closure_tables_detect_non_hermitian_h0():
+    """Closure fallback: a non-Hermitian nominal H0 is tabulated and detected on the host
+    (tables.is_hermitian_h0 -> GrapePlan.general_h0_for moves the plan to the general-H0 path);
+    a non-Hermitian error generator is tabulated as is."""
+    from robustgrape_amd.tables import host_tables, is_hermitian_h0
     from robustgrape_amd.types import ErrorSource
     fp = P.sym_problem(6, device=False)
     up = fp.unitary_problem
     decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
     x = P.random_x(6, 2)
     bad = fp.replace(unitary_problem=up.replace(H0=lambda t, p, xa: up.H0(t, p, xa) - 0.5j * decay))
-    with pytest.raises(ValueError, match="Hermitian"):
-        host_tables(bad, x[None, :], 1)
+    H, _ = host_tables(bad, x[None, :], 1)
+    assert np.isfinite(H).all() and not is_hermitian_h0(H[:, :, 0])
+    H, _ = host_tables(fp, x[None, :], 1)
+    assert is_hermitian_h0(H[:, :, 0])
     ok = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, p, xa, e: -0.5j * e * decay)]))
     H, _ = host_tables(ok, x[None, :], 1)
-    assert np.isfinite(H).all()
+    assert np.isfinite(H).all() and is_hermitian_h0(H[:, :, 0])

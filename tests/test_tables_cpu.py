@@ -50,12 +50,17 @@ def test_pool_tables_follow_the_closures_current_state():
 
 
 def test_worker_errors_reach_the_caller():
-    """A non-Hermitian nominal H0 is refused inside the worker; the error surfaces in get()."""
+    """A closure that raises inside a worker: the error surfaces in get()."""
     from robustgrape_amd import tables as TB
     fp = P.sym_problem(4, device=False)
     up = fp.unitary_problem
-    decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
-    bad = fp.replace(unitary_problem=up.replace(H0=lambda t, p, xa: up.H0(t, p, xa) - 0.5j * decay))
+
+    def h0(t, p, xa):
+        if t == 3:
+            raise ValueError("closure failed at step 3")
+        return up.H0(t, p, xa)
+
+    bad = fp.replace(unitary_problem=up.replace(H0=h0))
     X = P.random_x(4, 2)[None, :]
     W = TB.TableWorkers(2)
     tabs = TB.SharedTables(*TB.table_shapes(bad, 1, 1))
@@ -66,7 +71,7 @@ def test_worker_errors_reach_the_caller():
             try:
                 r.get(timeout=120)
             except ValueError as e:
-                assert "Hermitian" in str(e)
+                assert "step 3" in str(e)
                 errs += 1
         assert errs >= 1
     finally:
