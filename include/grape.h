@@ -134,8 +134,10 @@ typedef struct grape_desc {
  * H0 and the target stay opaque host closures (the reference's own idiom,
  * src/Types.jl:10,50); the caller evaluates them at every call site of the
  * reference and passes the tables to grape_fidelity_grad_tables.  ops / terms
- * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_SMALL_DIM.  The closures may
- * read x_add: every x_add call site of the reference is tabulated.
+ * may then be NULL (n_ops = 0); ndim <= GRAPE_MAX_DENSE_DIM (above GRAPE_MAX_SMALL_DIM the
+ * tables go through the general path below with the dense engine's exponential, which needs
+ * Hermitian tabulated generators -- the Python host checks).  The closures may read x_add:
+ * every x_add call site of the reference is tabulated.
  */
 #define GRAPE_DESC_HOST_TABLES 1
 
@@ -159,7 +161,8 @@ typedef struct grape_desc {
  * and the fidelity path runs from the materialised unitary derivatives, one evaluation at a
  * time (FidelityCalculations.jl:19-119).  Selected automatically for an operator-basis H0
  * that is not Hermitian; host-table plans (closures) set it when the host sees a
- * non-Hermitian H0 table.  ndim <= GRAPE_MAX_SMALL_DIM.
+ * non-Hermitian H0 table.  Operator bases: ndim <= GRAPE_MAX_SMALL_DIM; host-table plans above
+ * GRAPE_MAX_SMALL_DIM always take this path (Hermitian tables only).
  */
 #define GRAPE_OPT_GENERAL_H0 64
 
@@ -254,6 +257,45 @@ int grape_fidelity_grad_tables(grape_plan *plan, int nbatch, const double *x, co
 int grape_lbfgs_direction(int R, int n, int m, const double *S, const double *Y, const double *rho,
                           const int64_t *head, const int64_t *hist, const double *gamma,
                           const double *g, double *D, void *stream);
+
+/*
+ * The rest of one L-BFGS iteration of every restart on the device (ABI 7): the strong-Wolfe
+ * line search's state machine (Nocedal & Wright alg. 3.5 / 3.6, c1 = 1e-4, c2 = 0.9) and the
+ * ring-buffer update with Optim's stopping rules, as optimize.py lbfgs_batched runs them.  All
+ * pointers are DEVICE memory for R rows (vectors [R][n], ring [m][R][n]); flags int32, counters
+ * int64.  Per iteration: grape_lbfgs_direction, grape_lbfgs_ls_init (active rows, descent check,
+ * the search state at a = 1), then per round grape_lbfgs_ls_begin (the searching rows in row
+ * order -> rows[0, *count), their trial points -> Xt, f_calls += 1), the caller evaluates the
+ * compact batch (ft [count], gt [count][n]), grape_lbfgs_ls_end; finally grape_lbfgs_step.
+ */
+typedef struct grape_lbfgs_state {
+    int R, n, m, reserved0;
+    double *X, *f, *g, *D, *Xn, *fn, *gn, *Xt;
+    double *f0, *dphi0, *a_cur, *a_prev, *f_prev, *dp_prev, *a_lo, *f_lo, *dp_lo, *a_hi, *f_hi, *dp_hi;
+    double *S, *Y, *rho, *gamma, *g_thr;
+    int64_t *f_calls, *iters, *hist, *head, *rows;
+    int32_t *phase, *first, *accepted, *gconv, *fconv, *xconv, *lsfail, *active, *count;
+    double f_abstol, f_reltol, x_abstol, x_reltol;
+    int64_t iterations, f_calls_limit;
+} grape_lbfgs_state;
+int grape_lbfgs_ls_init(const grape_lbfgs_state *state, void *stream);
+int grape_lbfgs_ls_begin(const grape_lbfgs_state *state, void *stream);
+int grape_lbfgs_ls_end(const grape_lbfgs_state *state, int count, const double *ft, const double *gt, void *stream);
+int grape_lbfgs_step(const grape_lbfgs_state *state, void *stream);
+
+/*
+ * The optimiser's cost of R restarts in one launch (calculate_common!, FidelityCalculations.jl:
+ * 172-196; ABI 7): cost = 1 - F + sum_e c_e F_d2err_e^2 + sum_p (c1_p reg1_p + c2_p reg2_p),
+ * grad = -F_dx + 2 sum_e c_e F_d2err_e F_d2err_dx[e] + the regulariser gradients on each control's
+ * entries.  reg_kind[p]: 0 none, 1 regularization_cost(x_p), 2 regularization_cost_phase(x_p)
+ * (Regularization.jl:26-48, :111-115; 4 <= ntimes <= 4096).  DEVICE pointers: X, F_dx, grad
+ * [R][n_x]; F, cost [R]; F_d2err [R][nerr]; F_d2err_dx [R][nerr][n_x] (the device layout of
+ * grape_fidelity_grad_device_async); err_coeff [nerr], coeff1 / coeff2 / reg_kind [nparam].
+ */
+int grape_robust_cost(int R, int nparam, int ntimes, int nadd, int nerr, const double *X, const double *F,
+                      const double *F_dx, const double *F_d2err, const double *F_d2err_dx, const double *err_coeff,
+                      const double *coeff1, const double *coeff2, const int32_t *reg_kind, double *cost,
+                      double *grad, void *stream);
 
 /* Block until all work enqueued on the plan's stream finished; reports device-side errors. */
 int grape_plan_synchronize(grape_plan *plan);

@@ -773,6 +773,29 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     return hipGetLastError();
 }
 
+// A = -i dt H of host-tabulated H (closure fallback, column-major d x d), zero-padded images
+__global__ __launch_bounds__(256) void k_tab_images(const grape::cd *H, double *img, int D, double dt) {
+    const grape::cd *src = H + (size_t)blockIdx.x * D * D;
+    double *dst = img + (size_t)blockIdx.x * IMG;
+    for (int o = threadIdx.x; o < 64 * 64; o += blockDim.x) {
+        const int l = o & 63, r = (o >> 6) & 3, t = (o >> 8) & 3, w = o >> 10;
+        const int row = 16 * t + (l >> 4) + 4 * r, col = 16 * w + (l & 15);
+        const bool in = row < D && col < D;
+        const grape::cd h = in ? src[(size_t)row + (size_t)col * D] : grape::cmake(0.0, 0.0);
+        dst[o] = dt * h.im;             // -i dt (re + i im) = dt im - i dt re
+        dst[IMG / 2 + o] = -(dt * h.re);
+    }
+}
+
+hipError_t launch_table_variants(const grape::cd *H, int D, int n, double dt, double *Aimg, double *Eimg,
+                                 grape::cd *rows, int *status, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tab_images, dim3((unsigned)n), dim3(256), 0, st, H, Aimg, D, dt);
+    hipLaunchKernelGGL(k_dexp_raw, dim3((unsigned)n), dim3(NTHREADS), kLds, st, Aimg, Eimg, status, nullptr);
+    hipLaunchKernelGGL(k_img_rows, dim3((unsigned)n), dim3(256), 0, st, Eimg, rows, D);
+    return hipGetLastError();
+}
+
 hipError_t launch_expm_raw(const double *A, double *E, int n, int *status, int *mstats, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_dexp_raw, dim3((unsigned)n), dim3(NTHREADS), kLds, st, A, E, status, mstats);

@@ -57,5 +57,10 @@ hipError_t set_lds_limits();
 // images B.E, then converted to row-major d x d tiles rows[Nt][nv][D][D] (the table the
 // materialised-derivative kernels of grape_unitary.hip read).
 hipError_t launch_variant_table(const DenseProblem &P, const DenseBatch &B, grape::cd *rows, hipStream_t st);
+// Closure fallback above GRAPE_MAX_SMALL_DIM: n host-tabulated H (column-major d x d) -> exp(-i dt H)
+// as row-major d x d tiles (`rows`), through the padded images Aimg / Eimg (n images each); the
+// no-interchange solve needs a Hermitian H (checked on the host, robustgrape_amd/engine.py)
+hipError_t launch_table_variants(const grape::cd *H, int D, int n, double dt, double *Aimg, double *Eimg,
+                                 grape::cd *rows, int *status, hipStream_t st);
 
 }  // namespace grape_dense

@@ -189,6 +189,8 @@ struct grape_plan {
     // (grape_unitary.hip k_u_fid_head / k_u_fid_contract), one evaluation at a time
     bool general_h0 = false;
     cd *ud_Ci = nullptr, *d_G = nullptr;
+    cd *d_fscr = nullptr;        // d > 12: the fidelity head's tiles (global scratch)
+    double *ud_Aimg = nullptr;   // closures at d > 12: the tabulated generators as padded images
     std::vector<grape::VSpec> ud_vs_host;  // the variant list in ud_vs (general H0 batches)
     double *ud_Eimg = nullptr; // dense engine: the variant table as register-file images
     // small host-array calls (the reference's one-x-per-call pattern): the whole call --
@@ -230,7 +232,7 @@ static void free_plan(grape_plan *p) {
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
                     p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
-                    p->ud_Ci, p->d_G, p->d_xT,
+                    p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
                     p->d_fixed};
     for (void *b : bufs)
@@ -657,9 +659,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         (!tables && desc->n_ops < 1))
         return fail(GRAPE_ERR_INVALID, "bad dimensions in descriptor");
     if (D > GRAPE_MAX_DENSE_DIM) return fail(GRAPE_ERR_UNSUPPORTED, "ndim > GRAPE_MAX_DENSE_DIM");
-    if (tables) {
-        if (D > GRAPE_MAX_SMALL_DIM)
-            return fail(GRAPE_ERR_UNSUPPORTED, "host tables: ndim > GRAPE_MAX_SMALL_DIM needs an operator basis");
+    if (tables) {  // above GRAPE_MAX_SMALL_DIM: the general path with the dense exponential of the tables
         if (!desc->projector_diag && !desc->projector) return fail(GRAPE_ERR_INVALID, "missing projector");
     } else {
         if (desc->nerr > 0 && !desc->err_term_offsets) return fail(GRAPE_ERR_INVALID, "missing err_term_offsets");
@@ -691,8 +691,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         if (rc != GRAPE_ERR_UNSUPPORTED || D > GRAPE_MAX_SMALL_DIM) return rc;
         general_h0 = true;  // non-Hermitian H0: the general path serves it
     }
-    if (general_h0 && D > GRAPE_MAX_SMALL_DIM)
+    if (general_h0 && D > GRAPE_MAX_SMALL_DIM && !tables)
         return fail(GRAPE_ERR_UNSUPPORTED, "general (non-Hermitian) H0: ndim <= GRAPE_MAX_SMALL_DIM only");
+    // closures above the small engine: host tables through the general path (materialised
+    // derivatives), each tabulated generator exponentiated by the dense engine (grape_dense.hip
+    // launch_table_variants; the host checks that the tables are Hermitian)
+    if (tables && D > GRAPE_MAX_SMALL_DIM) general_h0 = true;
     // host tables: H0 / Herror are opaque closures that may read x_add, so every x_add call
     // site of the reference is tabulated (UnitaryCalculations.jl:57-64, 87-95)
     bool xadd_dep = tables && desc->nadd > 0;
@@ -721,13 +725,14 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (hipHostMalloc(reinterpret_cast<void **>(&p->h_status), sizeof(int), hipHostMallocDefault) != hipSuccess)
         return bail(fail(GRAPE_ERR_ALLOC, "pinned allocation failed"));
     *p->h_status = 0;
-    if (D > GRAPE_MAX_SMALL_DIM) {
+    if (D > GRAPE_MAX_SMALL_DIM && !tables) {
         const int rcd = create_dense(desc, p, xadd_dep, ps, n_err_terms);
         if (rcd) return bail(rcd);
         *out = p;
         return GRAPE_OK;
     }
-    if (dispatch_lds_limits(D) != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
+    if (D <= GRAPE_MAX_SMALL_DIM && dispatch_lds_limits(D) != hipSuccess)
+        return bail(fail(GRAPE_ERR_HIP, "cannot raise LDS limit"));
 
     DevProblem &P = p->P;
     p->tables = tables;
@@ -895,7 +900,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             P.PA = p->d_PA;
             P.PB = p->d_PB;
         }
-        if (dalloc(&p->ud_Ci, (size_t)P.Nt * T) != hipSuccess || dalloc(&p->d_G, (1 + (size_t)P.ne) * T) != hipSuccess)
+        if (dalloc(&p->ud_Ci, (size_t)P.Nt * T) != hipSuccess || dalloc(&p->d_G, (1 + (size_t)P.ne) * T) != hipSuccess ||
+            (D > grape_unitary::kMaxD && dalloc(&p->d_fscr, (size_t)grape_unitary::kFidTiles * T) != hipSuccess))
             return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (general H0)"));
     }
     if (sec) {  // the sector problems of every class and the head over the assembled U
@@ -1214,6 +1220,7 @@ static int enqueue_general(grape_plan *p, int nb, const double *d_x, double *d_F
     FA.Uedx = UB.Uedx;
     FA.Uedxa = UB.Uedxa;
     FA.G = p->d_G;
+    FA.scr = p->d_fscr;
     for (int b = 0; b < nb; ++b) {
         const double *xb = d_x + (size_t)b * nx;
         mk(GRAPE_KERNEL_EXPM, 0);
@@ -1464,7 +1471,10 @@ static int ud_alloc(grape_plan *p) {
                     dalloc(&p->ud_V, Nt * nslots * T) == hipSuccess &&
                     dalloc(&p->ud_S, Nt * std::max<size_t>(ne, 1) * T) == hipSuccess && dalloc(&p->ud_out, nout) == hipSuccess;
     if (ok && P.D > grape_unitary::kMaxD) ok = dalloc(&p->ud_gscr, grape_unitary::scratch_elems(P.D)) == hipSuccess;
-    if (ok && p->dense) ok = dalloc(&p->ud_Eimg, Nt * nv * grape_dense::kImgDoubles) == hipSuccess;
+    if (ok && (p->dense || P.D > GRAPE_MAX_SMALL_DIM))
+        ok = dalloc(&p->ud_Eimg, Nt * nv * grape_dense::kImgDoubles) == hipSuccess;
+    if (ok && p->tables && P.D > GRAPE_MAX_SMALL_DIM)
+        ok = dalloc(&p->ud_Aimg, Nt * nv * grape_dense::kImgDoubles) == hipSuccess;
     return ok ? GRAPE_OK : fail(GRAPE_ERR_ALLOC, "device allocation failed (single-evaluation workspace)");
 }
 
@@ -1506,6 +1516,9 @@ static int ud_propagators_dev(grape_plan *p, const double *d_x, int nv, const cd
         DB.E = p->ud_Eimg;
         DB.status = p->d_ctrl + 2;
         HIPCHECK(grape_dense::launch_variant_table(DPu, DB, p->ud_E, st));
+    } else if (d_Htab && P0.D > GRAPE_MAX_SMALL_DIM) {  // closures above the small engine
+        HIPCHECK(grape_dense::launch_table_variants(d_Htab, P0.D, P0.Nt * nv, P0.dt, p->ud_Aimg, p->ud_Eimg, p->ud_E,
+                                                   p->d_ctrl + 2, st));
     } else if (d_Htab) {
         Bu.Htab = d_Htab;
         HIPCHECK(dispatch_expm_table(P0.D, Pu, Bu, st));
@@ -1555,6 +1568,7 @@ static int ud_interaction(grape_plan *p, const double *x, const double *H0tab, c
         grape_unitary::UProblem UP{};
         UP.D = p->P.D;
         UP.Nt = p->P.Nt;
+        UP.gscr = p->ud_gscr;
         HIPCHECK(grape_unitary::launch_inverse(UP, p->ud_C, p->ud_Ci, p->d_ctrl + 2, p->stream));
         Ci = p->ud_Ci;
     }

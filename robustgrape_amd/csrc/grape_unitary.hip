@@ -98,14 +98,14 @@ __global__ __launch_bounds__(BLOCK) void k_u_chain(UProblem P, const cd *E, cd *
 // A zero pivot (singular chain) sets status bit 1 (Julia's inv throws SingularException).
 __global__ __launch_bounds__(BLOCK) void k_u_inverse(UProblem P, const cd *C, cd *Ci, int *status) {
     __shared__ cd lds[kTiles * kMaxD * kMaxD];
-    __shared__ cd fac[kMaxD];
+    __shared__ cd fac[64];
     __shared__ int piv;
     const int D = P.D, DD = D * D, t0 = threadIdx.x;
-    cd *sA = lds, *sI = lds + DD;
+    cd *sA = tiles(lds, P.gscr, D), *sI = sA + DD;
     for (long k = blockIdx.x; k < P.Nt; k += gridDim.x) {
         load_tile(sA, C + (size_t)k * DD, D);
         identity_tile(sI, D);
-        __syncthreads();
+        tsync();
         bool singular = false;
         for (int c = 0; c < D; ++c) {
             if (t0 == 0) {
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(BLOCK) void k_u_inverse(UProblem P, const cd *C, cd
                 }
                 piv = bv > 0.0 ? best : -1;
             }
-            __syncthreads();
+            tsync();
             const int pr = piv;
             if (pr < 0) {
                 singular = true;
@@ -134,24 +134,24 @@ __global__ __launch_bounds__(BLOCK) void k_u_inverse(UProblem P, const cd *C, cd
                     M[c * D + j] = M[pr * D + j];
                     M[pr * D + j] = a;
                 }
-            __syncthreads();
+            tsync();
             const cd pv = sA[c * D + c];
             const double den = pv.re * pv.re + pv.im * pv.im;
             const cd rp{pv.re / den, -pv.im / den};
-            __syncthreads();
+            tsync();
             for (int t = t0; t < 2 * D; t += blockDim.x) {  // pivot row * (1 / pivot)
                 cd *M = t < D ? sA : sI;
                 const int j = t < D ? t : t - D;
                 M[c * D + j] = u_mul(M[c * D + j], rp);
             }
             for (int i = t0; i < D; i += blockDim.x) fac[i] = i == c ? cd{0.0, 0.0} : sA[i * D + c];
-            __syncthreads();
+            tsync();
             for (int t = t0; t < 2 * DD; t += blockDim.x) {  // eliminate column c from every other row
                 cd *M = t < DD ? sA : sI;
                 const int e = t < DD ? t : t - DD, i = e / D, j = e % D;
                 if (i != c) M[e] = u_sub(M[e], u_mul(fac[i], M[c * D + j]));
             }
-            __syncthreads();
+            tsync();
         }
         if (singular) {
             if (t0 == 0) atomicOr(status, 2);
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(BLOCK) void k_u_inverse(UProblem P, const cd *C, cd
         } else {
             for (int t = t0; t < DD; t += blockDim.x) Ci[(size_t)k * DD + t] = sI[t];
         }
-        __syncthreads();
+        tsync();
     }
 }
 
@@ -432,19 +432,19 @@ __device__ void mm(cd *C, const cd *A, int ha, const cd *B, int hb, int D) {
         }
         C[t] = s;
     }
-    __syncthreads();
+    tsync();
 }
 
 // block sum of one complex value per thread (red: blockDim.x scratch)
 __device__ cd bsum(cd v, cd *red) {
     red[threadIdx.x] = v;
-    __syncthreads();
+    tsync();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) red[threadIdx.x] = u_add(red[threadIdx.x], red[threadIdx.x + w]);
-        __syncthreads();
+        tsync();
     }
     const cd r = red[0];
-    __syncthreads();
+    tsync();
     return r;
 }
 // tr(A B) = sum_ij A_ij B_ji
@@ -462,7 +462,7 @@ __device__ cd trace_abh(const cd *A, const cd *B, int D, cd *red) {
 // column-major global matrix -> row-major LDS tile
 __device__ void load_cm(cd *dst, const cd *src, int D) {
     for (int t = threadIdx.x; t < D * D; t += blockDim.x) dst[t] = src[(t / D) + (t % D) * D];
-    __syncthreads();
+    tsync();
 }
 // U0(x_add [+ eps e_q]) of this evaluation: operator-basis target terms, or the host table (slot)
 __device__ void target(cd *dst, const FidArgs &A, int slot) {
@@ -485,17 +485,18 @@ __device__ void target(cd *dst, const FidArgs &A, int slot) {
         }
         dst[t] = h;
     }
-    __syncthreads();
+    tsync();
 }
 
 }  // namespace fid
 
 __global__ __launch_bounds__(BLOCK) void k_u_fid_head(FidArgs A) {
-    constexpr int MT = kMaxD * kMaxD;
-    __shared__ cd sm[14 * MT];
+    __shared__ cd lds_sm[kFidTiles * kMaxD * kMaxD];
     __shared__ cd red[BLOCK];
     const grape::DevProblem &P = A.P;
     const int D = P.D, DD = D * D, np = P.np, na = P.na, ne = P.ne, Nt = P.Nt, nx = P.nx;
+    const int MT = D <= kMaxD ? kMaxD * kMaxD : DD;
+    cd *sm = D <= kMaxD ? lds_sm : A.scr;  // d > kMaxD: kFidTiles tiles of global scratch
     const double Dn = P.DD, Dtr = P.Dtr;
     cd *U = sm, *U0 = sm + MT, *PA = sm + 2 * MT, *PB = sm + 3 * MT, *K = sm + 4 * MT, *R = sm + 5 * MT,
        *T1 = sm + 6 * MT, *T2 = sm + 7 * MT, *T3 = sm + 8 * MT, *Ue = sm + 9 * MT, *Ke = sm + 10 * MT,
@@ -505,7 +506,7 @@ __global__ __launch_bounds__(BLOCK) void k_u_fid_head(FidArgs A) {
         PA[t] = P.PA[t];
         PB[t] = P.PB[t];
     }
-    __syncthreads();
+    tsync();
     fid::target(U0, A, 0);
     fid::mm(K, U0, 1, U, 0, D);    // K = U0^dag U
     const cd tau = fid::trace_ab(PA, K, D, red);
@@ -520,15 +521,15 @@ __global__ __launch_bounds__(BLOCK) void k_u_fid_head(FidArgs A) {
     fid::mm(T3, PB, 1, T1, 0, D);
     for (int t = threadIdx.x; t < DD; t += blockDim.x)
         T1[t] = u_add(u_add(T2[t], T3[t]), u_mul(cd{2.0 * tau.re, -2.0 * tau.im}, PA[t]));
-    __syncthreads();
+    tsync();
     fid::mm(T2, T1, 0, U0, 1, D);
     for (int t = threadIdx.x; t < DD; t += blockDim.x) A.G[t] = u_scale(1.0 / Dn, T2[t]);
-    __syncthreads();
+    tsync();
     // x_add: F_dx_add[q] = Re tr(U_dx_add[q] G) + target-derivative terms (:66-76)
     for (int q = 0; q < na; ++q) {
         fid::target(U0d, A, 1 + q);
         for (int t = threadIdx.x; t < DD; t += blockDim.x) U0d[t] = u_scale(P.inv_eps, u_sub(U0d[t], U0[t]));
-        __syncthreads();
+        tsync();
         fid::mm(Kd, U0d, 1, U, 0, D);  // Kd = U0d^dag U
         fid::mm(T1, Kd, 0, PB, 0, D);
         fid::mm(T3, PA, 0, T1, 0, D);  // PA Kd PB
@@ -558,25 +559,25 @@ __global__ __launch_bounds__(BLOCK) void k_u_fid_head(FidArgs A) {
         fid::mm(T3, PB, 1, T1, 0, D);
         for (int t = threadIdx.x; t < DD; t += blockDim.x)
             T1[t] = u_add(u_add(T2[t], T3[t]), u_mul(cd{2.0 * sg.re, -2.0 * sg.im}, PA[t]));
-        __syncthreads();
+        tsync();
         fid::mm(T2, T1, 0, U0, 1, D);
         for (int t = threadIdx.x; t < DD; t += blockDim.x) {  // (PA^dag + PA)
             const int i = t / D, j = t % D;
             T1[t] = u_add(cd{PA[j * D + i].re, -PA[j * D + i].im}, PA[t]);
         }
-        __syncthreads();
+        tsync();
         fid::mm(T3, T1, 0, Ue, 1, D);
         cd *Ge = A.G + (size_t)(1 + e) * DD;
         for (int t = threadIdx.x; t < DD; t += blockDim.x) {
             T2[t] = u_scale(2.0 / Dn, u_sub(T2[t], u_scale(1.0 + Dtr, T3[t])));  // kept for the x_add entries
             Ge[t] = T2[t];
         }
-        __syncthreads();
+        tsync();
         // F_d2err_dx_add[q, e] = Re tr(U_derr_dx_add[q, e] G_e) + target-derivative terms (:99-113)
         for (int q = 0; q < na; ++q) {
             fid::target(U0d, A, 1 + q);
             for (int t = threadIdx.x; t < DD; t += blockDim.x) U0d[t] = u_scale(P.inv_eps, u_sub(U0d[t], U0[t]));
-            __syncthreads();
+            tsync();
             fid::mm(Kd, U0d, 1, Ue, 0, D);  // Ked = U0d^dag Ue
             fid::mm(T1, Kd, 0, PB, 0, D);
             fid::mm(T3, PA, 0, T1, 0, D);   // PA Ked PB
@@ -629,8 +630,8 @@ hipError_t launch_chain(const UProblem &P, const cd *E, cd *C, hipStream_t st) {
 }
 
 hipError_t launch_inverse(const UProblem &P, const cd *C, cd *Ci, int *status, hipStream_t st) {
-    if (P.D > kMaxD) return hipErrorInvalidValue;  // general H0: small engine only (LDS tiles)
-    hipLaunchKernelGGL(k_u_inverse, dim3((unsigned)std::min<long>(P.Nt, 1024)), dim3(BLOCK), 0, st, P, C, Ci, status);
+    if (P.D > kMaxD && !P.gscr) return hipErrorInvalidValue;  // d > kMaxD: the tiles live in P.gscr
+    hipLaunchKernelGGL(k_u_inverse, dim3(grid_for(P.D, P.Nt)), dim3(BLOCK), 0, st, P, C, Ci, status);
     return hipGetLastError();
 }
 
@@ -654,7 +655,7 @@ hipError_t launch_expectation(const grape::DevProblem &P, const cd *O, double *e
 }
 
 hipError_t launch_fidelity(const FidArgs &A, hipStream_t st) {
-    if (A.P.D > kMaxD) return hipErrorInvalidValue;
+    if (A.P.D > kMaxD && !A.scr) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_u_fid_head, dim3(1), dim3(BLOCK), 0, st, A);
     const long items = (long)A.P.Nt * A.P.np * (1 + A.P.ne);
     const long per = BLOCK / 64;

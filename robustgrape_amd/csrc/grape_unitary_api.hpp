@@ -11,6 +11,7 @@ using grape::cd;
 
 constexpr int kMaxD = 12;      // GRAPE_MAX_SMALL_DIM: d x d tiles staged in LDS up to here
 constexpr int kTiles = 4;      // tiles per workgroup
+constexpr int kFidTiles = 14;  // the general-H0 fidelity head's tiles
 constexpr int kResident = 256; // d > kMaxD: workgroups of the grid-stride launches, each with
                                // kTiles d x d tiles of global scratch (scratch_elems)
 inline size_t scratch_elems(int D) { return D > kMaxD ? (size_t)kResident * kTiles * D * D : 0; }
@@ -67,6 +68,7 @@ struct FidArgs {
     const cd *U;         // [D][D] row-major C_Nt
     const cd *Udx, *Udxa, *Ue, *Uedx, *Uedxa;  // launch_assembly outputs
     cd *G;               // [1 + ne][D][D] scratch: the functionals of the controls and of each error
+    cd *scr;             // d > kMaxD: kFidTiles D x D tiles of global scratch for the head (else unused)
     double *F, *Fdx, *Fd2, *Fd2dx;  // this evaluation's outputs ([1], [nx], [ne], [ne][nx])
 };
 hipError_t launch_fidelity(const FidArgs &A, hipStream_t st);

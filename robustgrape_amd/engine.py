@@ -53,12 +53,21 @@ class GrapePlan:
         self.handle = h
         self._stream_ptr = None
 
-    def general_h0_for(self, H0s):
+    def general_h0_for(self, H0s, Hall=None):
         """Closure plans: the host sees H0 only as tables; a non-Hermitian nominal H0 (e.g. a
         -i Gamma/2 decay term) recreates the plan on the general-H0 path (GRAPE_OPT_GENERAL_H0,
         the reference's LU-inverted chain, UnitaryCalculations.jl:47) before the device call.
-        H0s: nominal H0 matrices (any leading shape, either storage order)."""
-        if not self.tables or (self.options & OPT_GENERAL_H0) or is_hermitian_h0(H0s):
+        Above 12 levels every tabulated generator Hall (default H0s) goes through the dense
+        engine's interchange-free solve, which needs it Hermitian: anything else is refused.
+        H0s / Hall: matrices (any leading shape, either storage order)."""
+        if not self.tables:
+            return
+        if self.up.ndim > 12:
+            if not is_hermitian_h0(H0s if Hall is None else Hall):
+                raise ValueError("closure problems above 12 levels need Hermitian H0 / H0 + Herror tables "
+                                 "(the dense engine's exponential); non-Hermitian generators are served up to 12 levels")
+            return
+        if (self.options & OPT_GENERAL_H0) or is_hermitian_h0(H0s):
             return
         self.options |= OPT_GENERAL_H0
         self._bufs.desc.reserved[1] = self.options
@@ -145,7 +154,7 @@ class GrapePlan:
         if shipped is None or self._shared is None:  # serial, chunk by chunk
             for b0, n in chunks:
                 H, U0 = host_tables(self.fp, X[b0:b0 + n], self.nparam)
-                self.general_h0_for(H[:, :, 0])
+                self.general_h0_for(H[:, :, 0], H)
                 _capi.check(L.grape_fidelity_grad_tables(
                     self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(H), _capi.dptr(U0),
                     _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
@@ -163,7 +172,7 @@ class GrapePlan:
                     r.get()
                 del pending[j]  # kept until every task of the chunk is done: drained below on error
                 tabs = self._shared[j % 2]
-                self.general_h0_for(tabs.H[:n, :, 0])
+                self.general_h0_for(tabs.H[:n, :, 0], tabs.H[:n])
                 _capi.check(L.grape_fidelity_grad_tables(
                     self.handle, n, _capi.dptr(X[b0:b0 + n]), _capi.dptr(tabs.H), _capi.dptr(tabs.U0),
                     _capi.dptr(F[b0:b0 + n]), _capi.dptr(Fdx[b0:b0 + n]), _capi.dptr(sl(Fd2, b0, n)),
@@ -199,7 +208,7 @@ class GrapePlan:
         ptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if a.size else None
         if self.tables:  # closure problem: every closure call site evaluated here
             H, _ = host_tables(self.fp, x[None, :], self.nparam)
-            self.general_h0_for(H[:, :, 0])
+            self.general_h0_for(H[:, :, 0], H)
             _capi.check(_capi.lib().grape_unitary_derivs_tables(self.handle, _capi.dptr(x), _capi.dptr(H),
                                                                 *[ptr(a) for a in outs]))
         else:

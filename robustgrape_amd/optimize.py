@@ -163,6 +163,107 @@ def _device_direction(S, Y, rho, head, hist, gamma, g):
     return D
 
 
+_TORCH_LS = bool(os.environ.get("GRAPE_TORCH_LS"))  # A/B switch: the torch line search on the GPU too
+
+
+class _CLbfgsState:  # filled lazily (ctypes import only with a GPU run)
+    cls = None
+
+    @classmethod
+    def get(cls):
+        if cls.cls is None:
+            import ctypes
+            vp = ctypes.c_void_p
+            fields = [("R", ctypes.c_int), ("n", ctypes.c_int), ("m", ctypes.c_int), ("reserved0", ctypes.c_int)]
+            fields += [(nm, vp) for nm in _LS_F64 + _LS_I64 + _LS_I32]
+            fields += [(nm, ctypes.c_double) for nm in ("f_abstol", "f_reltol", "x_abstol", "x_reltol")]
+            fields += [("iterations", ctypes.c_int64), ("f_calls_limit", ctypes.c_int64)]
+            cls.cls = type("grape_lbfgs_state", (ctypes.Structure,), {"_fields_": fields})
+        return cls.cls
+
+
+# include/grape.h grape_lbfgs_state, pointer fields in declaration order
+_LS_F64 = ("X", "f", "g", "D", "Xn", "fn", "gn", "Xt", "f0", "dphi0", "a_cur", "a_prev", "f_prev", "dp_prev",
+           "a_lo", "f_lo", "dp_lo", "a_hi", "f_hi", "dp_hi", "S", "Y", "rho", "gamma", "g_thr")
+_LS_I64 = ("f_calls", "iters", "hist", "head", "rows")
+_LS_I32 = ("phase", "first", "accepted", "gconv", "fconv", "xconv", "lsfail", "active", "count")
+
+
+def _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, time_limit, x_reltol, g_reltol,
+                  f_calls_limit, callback) -> BatchResult:
+    """lbfgs_batched on the GPU: the same algorithm with its per-round state machine, the descent
+    check and the L-BFGS update as HIP kernels (csrc/grape_lbfgs.hip, include/grape.h
+    grape_lbfgs_state), one host sync per line-search round (the count of searching rows)."""
+    import ctypes
+
+    from . import _capi
+    L = _capi.lib()
+    t_start = time.perf_counter()
+    X = X0.clone().contiguous()
+    R, n = X.shape
+    dev, dt = X.device, torch.float64
+    t = {}
+    t["X"] = X
+    f, g = fun(X, torch.arange(R, device=dev))
+    t["f"], t["g"] = f.to(dt).contiguous().clone(), g.to(dt).contiguous().clone()
+    for nm in ("D", "Xn", "gn", "Xt"):
+        t[nm] = torch.zeros(R, n, dtype=dt, device=dev)
+    for nm in ("fn", "f0", "dphi0", "a_cur", "a_prev", "f_prev", "dp_prev", "a_lo", "f_lo", "dp_lo", "a_hi", "f_hi",
+               "dp_hi"):
+        t[nm] = torch.zeros(R, dtype=dt, device=dev)
+    t["S"] = torch.zeros(m, R, n, dtype=dt, device=dev)
+    t["Y"] = torch.zeros(m, R, n, dtype=dt, device=dev)
+    t["rho"] = torch.zeros(m, R, dtype=dt, device=dev)
+    t["gamma"] = torch.ones(R, dtype=dt, device=dev)
+    gabs = torch.amax(torch.abs(t["g"]), dim=1)
+    t["g_thr"] = torch.clamp(g_reltol * gabs, min=g_tol)
+    for nm in _LS_I64:
+        t[nm] = torch.zeros(R, dtype=torch.int64, device=dev)
+    t["f_calls"] += 1
+    for nm in _LS_I32:
+        t[nm] = torch.zeros(max(R, 1), dtype=torch.int32, device=dev)
+    t["gconv"] = (gabs <= t["g_thr"]).to(torch.int32)
+    st = _CLbfgsState.get()()
+    st.R, st.n, st.m = R, n, m
+    for nm in _LS_F64 + _LS_I64 + _LS_I32:
+        setattr(st, nm, t[nm].data_ptr())
+    st.f_abstol, st.f_reltol, st.x_abstol, st.x_reltol = f_abstol, f_reltol, x_abstol, x_reltol
+    st.iterations = int(min(iterations, 2 ** 62))
+    st.f_calls_limit = int(f_calls_limit)
+    sp = ctypes.byref(st)
+    stream = lambda: ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+    timed_out = False
+    stopped = callback is not None and bool(callback(t["X"], t["f"], t["g"], t["iters"]))
+    while not stopped:
+        if not math.isnan(time_limit) and time.perf_counter() - t_start > time_limit:
+            timed_out = True
+            break
+        _capi.check(L.grape_lbfgs_direction(R, n, m, *[ctypes.c_void_p(t[k].data_ptr()) for k in
+                                                          ("S", "Y", "rho", "head", "hist", "gamma", "g", "D")],
+                                             stream()))
+        _capi.check(L.grape_lbfgs_ls_init(sp, stream()))
+        cnt = 0
+        for rnd in range(MAX_LS_ROUNDS):
+            _capi.check(L.grape_lbfgs_ls_begin(sp, stream()))
+            cnt = int(t["count"][0].item())  # the round's one host sync
+            if cnt == 0:
+                break
+            ft, gt = fun(t["Xt"][:cnt], t["rows"][:cnt])
+            ft, gt = ft.to(dt).contiguous(), gt.to(dt).contiguous()
+            _capi.check(L.grape_lbfgs_ls_end(sp, cnt, ctypes.c_void_p(ft.data_ptr()), ctypes.c_void_p(gt.data_ptr()),
+                                             stream()))
+        if rnd == 0 and cnt == 0:  # no row searches any more
+            break
+        _capi.check(L.grape_lbfgs_step(sp, stream()))
+        if callback is not None and bool(callback(t["X"], t["f"], t["g"], t["iters"])):
+            break
+    if hasattr(fun, "check"):  # deferred device status of the last evaluation (RobustCost)
+        fun.check()
+    b = lambda k: t[k][:R].bool()  # noqa: E731
+    return BatchResult(t["X"], t["f"], t["g"], t["iters"], t["f_calls"], b("gconv"), b("fconv"), b("xconv"),
+                       b("lsfail"), time.perf_counter() - t_start, {"timed_out": timed_out, "device_ls": True})
+
+
 def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.Tensor, *, m: int = 10,
                   iterations: int = 1000, g_tol: float = 1e-8, f_abstol: float = 0.0, f_reltol: float = 0.0,
                   x_abstol: float = 0.0, time_limit: float = float("nan"), x_reltol: float = 0.0,
@@ -175,6 +276,9 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
     max(g_tol, g_reltol |g_0|_inf), |df| <= f_abstol or f_reltol |f|, |dx|_inf <= x_abstol or
     x_reltol |x|_inf, f_calls_limit (0: none)).  callback(X, f, g, iters) runs after the initial
     evaluation and after every iteration; a True return stops every row (Optim's callback)."""
+    if X0.is_cuda and not _TORCH_LS and not _TORCH_TWO_LOOP and X0.dtype == torch.float64 and m <= 64:
+        return _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, time_limit, x_reltol,
+                             g_reltol, f_calls_limit, callback)
     t_start = time.perf_counter()
     X = X0.clone()
     R, n = X.shape
@@ -368,10 +472,22 @@ class RobustCost:
         self._unchecked = False
         self._stream = None
         self.plan = None
+        self._fused = None
         if evaluate is None:
             from .engine import GrapePlan
             self.plan = GrapePlan(fp, nparam, device=device, max_batch=max_batch)
             self.device = torch.device("cuda", device)
+            # the reference's own regularisers (no user transform) and an operator-basis plan:
+            # the whole cost in one launch (grape_robust_cost); anything else stays in torch
+            from . import regularization as REG
+            kinds = [2 if fn is REG.regularization_cost_phase else 1 if fn is REG.regularization_cost else -1
+                     for fn in self.regs]
+            if not self.plan.tables and all(k > 0 for k in kinds) and 4 <= self.ntimes <= 4096:
+                dev = self.device
+                self._fused = {"kind": torch.tensor(kinds, dtype=torch.int32, device=dev),
+                               "c1": torch.tensor(self.c1, dtype=torch.float64, device=dev),
+                               "c2": torch.tensor(self.c2, dtype=torch.float64, device=dev),
+                               "ce": torch.tensor(self.ce + [0.0], dtype=torch.float64, device=dev)}
         else:
             self.device = torch.device("cpu")
 
@@ -387,8 +503,9 @@ class RobustCost:
             self.plan.close()
             self.plan = None
 
-    def fidelity_terms(self, X: torch.Tensor):
-        """(F (r,), F_dx (r,nx), F_d2err (r,ne), F_d2err_dx (r,nx,ne)) for the rows of X."""
+    def fidelity_terms(self, X: torch.Tensor, raw: bool = False):
+        """(F (r,), F_dx (r,nx), F_d2err (r,ne), F_d2err_dx (r,nx,ne)) for the rows of X
+        (raw: F_d2err_dx in the engine's (r, ne, nx) layout, F_d2err (r, max(ne, 1)))."""
         if self._evaluate is not None:
             return self._evaluate(X)
         X = X.contiguous()
@@ -418,11 +535,15 @@ class RobustCost:
         # raises on a singular Pade denominator (a deferred check measured slower: 99k vs 118k)
         self._unchecked = True
         self.check()
+        if raw:
+            return F, Fdx, Fd2, Fd2dx
         if not self.nerr:
             return F, Fdx, Fd2[:, :0], Fd2dx[:, :0, :].transpose(1, 2)
         return F, Fdx, Fd2, Fd2dx.transpose(1, 2)
 
     def __call__(self, X: torch.Tensor, rows=None):
+        if self._fused is not None and X.is_cuda:
+            return self._fused_cost(X)
         F, Fdx, Fd2, Fd2dx = self.fidelity_terms(X)
         cost = 1.0 - F
         grad = -Fdx
@@ -441,6 +562,24 @@ class RobustCost:
         cost = cost + reg_cost
         grad = grad.clone()
         grad[:, :nm] += reg_grad.reshape(X.shape[0], nm)
+        return cost, grad
+
+    def _fused_cost(self, X):
+        """cost and gradient of the rows of X with one launch after the engine (grape_robust_cost)."""
+        import ctypes
+
+        from . import _capi
+        X = X.contiguous()
+        F, Fdx, Fd2, Fd2dx = self.fidelity_terms(X, raw=True)
+        r = X.shape[0]
+        cost = torch.empty(r, dtype=torch.float64, device=X.device)
+        grad = torch.empty(r, self.nx, dtype=torch.float64, device=X.device)
+        fz = self._fused
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _capi.check(_capi.lib().grape_robust_cost(
+            r, self.nparam, self.ntimes, self.na, self.nerr, p(X), p(F), p(Fdx), p(Fd2), p(Fd2dx), p(fz["ce"]),
+            p(fz["c1"]), p(fz["c2"]), p(fz["kind"]), p(cost), p(grad),
+            ctypes.c_void_p(torch.cuda.current_stream(X.device).cuda_stream)))
         return cost, grad
 
 

@@ -21,6 +21,7 @@ cost = OPT.RobustCost(fp, params, nparam=1, max_batch=B, device=0)
 dev = torch.device("cuda", 0)
 X = torch.as_tensor(X0, device=dev)
 calls = [0, 0.0]
+per_call = []
 
 
 def timed(Xs, rows=None):
@@ -30,6 +31,7 @@ def timed(Xs, rows=None):
     torch.cuda.synchronize()
     calls[0] += 1
     calls[1] += time.perf_counter() - t
+    per_call.append((Xs.shape[0], time.perf_counter() - t))
     return r
 
 
@@ -42,6 +44,7 @@ torch.cuda.synchronize()
 tot = time.perf_counter() - t0
 print(f"B={B}: 10 iterations {tot * 1e3:.1f} ms, {calls[0]} cost calls taking {calls[1] * 1e3:.1f} ms "
       f"(evals {int(res.f_calls.sum())})", flush=True)
+print("per call (rows, ms):", [(n, round(dt * 1e3, 3)) for n, dt in per_call[-40:]], flush=True)
 with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
     OPT.lbfgs_batched(cost, res.minimizer, iterations=3, g_tol=0.0)
 print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=25))

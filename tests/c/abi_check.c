@@ -49,6 +49,55 @@ static int layout(void) {
     PRINT_OFF(grape_desc, max_batch);
     PRINT_OFF(grape_desc, reserved);
     PRINT_OFF(grape_desc, projector);
+    printf("sizeof.grape_lbfgs_state %zu\n", sizeof(grape_lbfgs_state));
+    PRINT_OFF(grape_lbfgs_state, R);
+    PRINT_OFF(grape_lbfgs_state, n);
+    PRINT_OFF(grape_lbfgs_state, m);
+    PRINT_OFF(grape_lbfgs_state, X);
+    PRINT_OFF(grape_lbfgs_state, f);
+    PRINT_OFF(grape_lbfgs_state, g);
+    PRINT_OFF(grape_lbfgs_state, D);
+    PRINT_OFF(grape_lbfgs_state, Xn);
+    PRINT_OFF(grape_lbfgs_state, fn);
+    PRINT_OFF(grape_lbfgs_state, gn);
+    PRINT_OFF(grape_lbfgs_state, Xt);
+    PRINT_OFF(grape_lbfgs_state, f0);
+    PRINT_OFF(grape_lbfgs_state, dphi0);
+    PRINT_OFF(grape_lbfgs_state, a_cur);
+    PRINT_OFF(grape_lbfgs_state, a_prev);
+    PRINT_OFF(grape_lbfgs_state, f_prev);
+    PRINT_OFF(grape_lbfgs_state, dp_prev);
+    PRINT_OFF(grape_lbfgs_state, a_lo);
+    PRINT_OFF(grape_lbfgs_state, f_lo);
+    PRINT_OFF(grape_lbfgs_state, dp_lo);
+    PRINT_OFF(grape_lbfgs_state, a_hi);
+    PRINT_OFF(grape_lbfgs_state, f_hi);
+    PRINT_OFF(grape_lbfgs_state, dp_hi);
+    PRINT_OFF(grape_lbfgs_state, S);
+    PRINT_OFF(grape_lbfgs_state, Y);
+    PRINT_OFF(grape_lbfgs_state, rho);
+    PRINT_OFF(grape_lbfgs_state, gamma);
+    PRINT_OFF(grape_lbfgs_state, g_thr);
+    PRINT_OFF(grape_lbfgs_state, f_calls);
+    PRINT_OFF(grape_lbfgs_state, iters);
+    PRINT_OFF(grape_lbfgs_state, hist);
+    PRINT_OFF(grape_lbfgs_state, head);
+    PRINT_OFF(grape_lbfgs_state, rows);
+    PRINT_OFF(grape_lbfgs_state, phase);
+    PRINT_OFF(grape_lbfgs_state, first);
+    PRINT_OFF(grape_lbfgs_state, accepted);
+    PRINT_OFF(grape_lbfgs_state, gconv);
+    PRINT_OFF(grape_lbfgs_state, fconv);
+    PRINT_OFF(grape_lbfgs_state, xconv);
+    PRINT_OFF(grape_lbfgs_state, lsfail);
+    PRINT_OFF(grape_lbfgs_state, active);
+    PRINT_OFF(grape_lbfgs_state, count);
+    PRINT_OFF(grape_lbfgs_state, f_abstol);
+    PRINT_OFF(grape_lbfgs_state, f_reltol);
+    PRINT_OFF(grape_lbfgs_state, x_abstol);
+    PRINT_OFF(grape_lbfgs_state, x_reltol);
+    PRINT_OFF(grape_lbfgs_state, iterations);
+    PRINT_OFF(grape_lbfgs_state, f_calls_limit);
     printf("abi_version %d\n", grape_abi_version());
     return 0;
 }

@@ -192,3 +192,15 @@ def with_decay(fp, gamma=0.4, levels=(4,), device=True):
         h = up.H0
         H0 = lambda t, p, xa: np.asarray(h(t, p, xa), np.complex128) - 0.5j * gamma * G  # noqa: E731
     return fp.replace(unitary_problem=up.replace(H0=H0))
+
+
+def as_closures(fp):
+    """The same problem with plain-function H0 / Herror / target (the reference's idiom,
+    Types.jl:13,25,55): the engine then takes the host-table (closure) path."""
+    from robustgrape_amd.types import ErrorSource as ES
+    up = fp.unitary_problem
+    h, tgt = up.H0, fp.target_unitary
+    wrap_err = lambda f: (lambda t, p, xa, e: f(t, p, xa, e))  # noqa: E731
+    errs = [ES(wrap_err(es.Herror)) for es in up.error_sources]
+    up2 = up.replace(H0=lambda t, p, xa: h(t, p, xa), error_sources=errs)
+    return fp.replace(unitary_problem=up2, target_unitary=lambda xa: tgt(xa))

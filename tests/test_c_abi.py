@@ -66,6 +66,13 @@ def test_c_layout_matches_ctypes_and_julia_shim():
             off = lay[f"{cname}.{field}"]
             assert off == getattr(cty, field).offset, (cname, field)
             assert off == joffs[field], (cname, field, joffs[field])
+    # the device L-BFGS state (robustgrape_amd/optimize.py mirror; not part of the Julia shim)
+    from robustgrape_amd.optimize import _CLbfgsState
+    cst = _CLbfgsState.get()
+    assert lay["sizeof.grape_lbfgs_state"] == ctypes.sizeof(cst)
+    for field, _ in cst._fields_:
+        if field != "reserved0":
+            assert lay[f"grape_lbfgs_state.{field}"] == getattr(cst, field).offset, field
 
 
 @pytest.mark.gpu

@@ -138,3 +138,76 @@ def test_optimiser_on_closure_problem():
     assert np.max(np.abs(costs[1][1] - costs[0][1])) <= T3 * np.max(np.abs(costs[0][1])) + T2_ABS
     res = OPT.optimize_fidelity_and_error_sources(fph, _params(X[0], nerr=1, iterations=3))
     assert np.isfinite(res.minimum)
+
+
+def _rosen(X, rows=None):
+    a, b = X[:, :-1], X[:, 1:]
+    f = torch.sum(100 * (b - a * a) ** 2 + (1 - a) ** 2, dim=1)
+    g = torch.zeros_like(X)
+    g[:, :-1] += -400 * a * (b - a * a) - 2 * (1 - a)
+    g[:, 1:] += 200 * (b - a * a)
+    return f, g
+
+
+def test_device_line_search_matches_torch_line_search(monkeypatch):
+    """grape_lbfgs_ls_* / grape_lbfgs_step (the state machine as HIP kernels, one sync per round)
+    against the torch implementation on the same GPU tensors: the same iterates and call counts
+    over the first iterations (row sums reduce in a different order: 1e-12), the same stopping
+    behaviour over whole runs, and rows independent of the batch."""
+    rng = np.random.default_rng(5)
+    X0 = torch.as_tensor(rng.uniform(-2, 2, size=(9, 6)), device="cuda")
+    short = {}
+    for torch_ls in (False, True):
+        monkeypatch.setattr(OPT, "_TORCH_LS", torch_ls)
+        res = OPT.lbfgs_batched(_rosen, X0, iterations=4)
+        assert bool(res.extra.get("device_ls", False)) == (not torch_ls)
+        short[torch_ls] = res
+    a, b = short[False], short[True]
+    assert torch.equal(a.iterations, b.iterations) and torch.equal(a.f_calls, b.f_calls)
+    assert torch.allclose(a.minimizer, b.minimizer, rtol=1e-10, atol=1e-12)
+    monkeypatch.setattr(OPT, "_TORCH_LS", False)
+    X2 = X0[:, :2].contiguous()  # 2-D: one minimum, at (1, 1) (from 4-D on there is a second one)
+    full = OPT.lbfgs_batched(_rosen, X2, iterations=2000, g_tol=1e-8)
+    assert bool(full.g_converged.all())
+    assert torch.max(torch.abs(full.minimizer - 1)) < 1e-6
+    for r in (0, 5):  # a row's run does not depend on its batch
+        one = OPT.lbfgs_batched(_rosen, X2[r:r + 1], iterations=2000, g_tol=1e-8)
+        assert int(one.iterations[0]) == int(full.iterations[r])
+        assert torch.equal(one.minimizer[0], full.minimizer[r])
+    # stopping rules: iteration cap, converged at x0
+    res = OPT.lbfgs_batched(_rosen, torch.full((2, 4), -1.5, dtype=torch.float64, device="cuda"), iterations=3)
+    assert list(res.iterations.cpu()) == [3, 3] and not bool(res.g_converged.any())
+    res = OPT.lbfgs_batched(_rosen, torch.ones(1, 4, dtype=torch.float64, device="cuda"))
+    assert int(res.iterations[0]) == 0 and bool(res.g_converged[0])
+
+
+@pytest.mark.parametrize("case", ["sym_err_phase", "dense2_plain"])
+def test_fused_cost_matches_torch_cost(case):
+    """grape_robust_cost (cost assembly + the reference's regularisers in one launch) against the
+    torch assembly of the same engine outputs: error penalty, regularization_cost_phase and
+    regularization_cost, two controls per step."""
+    from robustgrape_amd import synthetic as S
+    if case == "sym_err_phase":
+        fp = P.sym_problem(40, errors=("amp", "freq"))
+        X = np.stack([P.random_x(40, s) for s in range(5)])
+        regs, ce = [REG.regularization_cost_phase], [0.3, 0.7]
+    else:
+        fp = S.dense_problem(d=6, ntimes=16, dt=0.5, rank=3)
+        X = np.stack([S.dense_x(ntimes=16, seed=s) for s in range(5)])
+        regs, ce = [REG.regularization_cost, REG.regularization_cost_phase], []
+    np_ = len(regs)
+    params = FidelityRobustGRAPEParameters(x_initial=X[0], regularization_functions=regs,
+                                           regularization_coeff1=[1e-3] * np_, regularization_coeff2=[2e-3] * np_,
+                                           error_source_coeff=ce)
+    cost = OPT.RobustCost(fp, params, nparam=np_, max_batch=8)
+    try:
+        assert cost._fused is not None
+        Xd = torch.as_tensor(X, device="cuda")
+        c_f, g_f = cost(Xd)
+        fused, cost._fused = cost._fused, None
+        c_t, g_t = cost(Xd)
+        cost._fused = fused
+    finally:
+        cost.close()
+    assert torch.allclose(c_f, c_t, rtol=1e-13, atol=1e-15), float((c_f - c_t).abs().max())
+    assert torch.allclose(g_f, g_t, rtol=1e-12, atol=1e-14), float((g_f - g_t).abs().max())
