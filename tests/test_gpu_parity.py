@@ -141,10 +141,11 @@ def test_errors_are_loud():
         calculate_fidelity_and_derivatives(P.full9_problem(64), np.zeros(64 + 2))
     from robustgrape_amd._capi import GrapeError
     from robustgrape_amd.types import FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
-    up13 = UnitaryRobustGRAPEProblem(t0=1.0, ntimes=4, ndim=13, H0=lambda t, x, xa: np.eye(13) * x[0],
-                                     nb_additional_param=0)
-    with pytest.raises(GrapeError):  # closures above the small-d engine: GRAPE_ERR_UNSUPPORTED
-        calculate_fidelity_and_derivatives(FidelityRobustGRAPEProblem(up13, np.eye(13), lambda xa: np.eye(13)),
+    d = 65  # closures run up to GRAPE_MAX_DENSE_DIM levels; above it GRAPE_ERR_UNSUPPORTED
+    up = UnitaryRobustGRAPEProblem(t0=1.0, ntimes=4, ndim=d, H0=lambda t, x, xa: np.eye(d) * x[0],
+                                   nb_additional_param=0)
+    with pytest.raises(GrapeError):
+        calculate_fidelity_and_derivatives(FidelityRobustGRAPEProblem(up, np.eye(d), lambda xa: np.eye(d)),
                                            np.zeros(4))
 
 
