@@ -461,21 +461,33 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
     prod = lambda S: 8 * S ** 3  # noqa: E731
     tile = lambda S: 16 * S * S  # noqa: E731
-    flop_model = {"k_expm": L * NT * nv * per_step(flops_expm),
-                  "k_grad/k_err_local": L * NT * nz * 2 * per_step(prod),
-                  "k_err_grad": L * NT * ne * 2 * per_step(prod)}
-    # algorithmic HBM bytes per pass: k_expm writes the nv variants; k_err_local reads them and
-    # Q_k, writes the nz images; k_err_grad reads W, Z1, Z2 per (step, error)
-    byte_model = {"k_expm": L * NT * nv * per_step(tile),
-                  "k_grad/k_err_local": L * NT * (nv + 1 + nz) * per_step(tile),
-                  "k_err_grad": L * NT * ne * 3 * per_step(tile)}
-    npass = passes or max(1, ktimes.get("k_expm", (0.0, 1))[1])
+    walk = ktimes.get("k_walk_fwd", (0.0, 0))[1] > 0
+    if walk:
+        # image walk (grape_walk.hpp k_walk_img) per (step, sector): the nv variant
+        # exponentials, the chain product Q <- E Q and per image Z = E^dag dX, Y = Q^dag Z Q (3
+        # products); HBM: the x row and the nz images written.  k_img_fdx (reported under
+        # "k_grad/k_err_local") reads Z1 and M'_c; k_err_grad reads W, Z1, Z2 per (step, error).
+        flop_model = {"k_walk_fwd": L * NT * per_step(lambda S: nv * flops_expm(S) + prod(S) * (1 + 3 * nz)),
+                      "k_err_grad": L * NT * ne * 2 * per_step(prod)}
+        byte_model = {"k_walk_fwd": L * 8 * (NT + 1) + L * NT * nz * per_step(tile),
+                      "k_grad/k_err_local": L * NT * per_step(tile),
+                      "k_err_grad": L * NT * ne * 3 * per_step(tile)}
+    else:
+        flop_model = {"k_expm": L * NT * nv * per_step(flops_expm),
+                      "k_grad/k_err_local": L * NT * nz * 2 * per_step(prod),
+                      "k_err_grad": L * NT * ne * 2 * per_step(prod)}
+        # algorithmic HBM bytes per pass: k_expm writes the nv variants; k_err_local reads them and
+        # Q_k, writes the nz images; k_err_grad reads W, Z1, Z2 per (step, error)
+        byte_model = {"k_expm": L * NT * nv * per_step(tile),
+                      "k_grad/k_err_local": L * NT * (nv + 1 + nz) * per_step(tile),
+                      "k_err_grad": L * NT * ne * 3 * per_step(tile)}
+    npass = passes or max(1, ktimes.get("k_walk_fwd" if walk else "k_expm", (0.0, 1))[1])
     per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
     kname = max(flop_model, key=lambda k: per_pass.get(k, 0.0))
     ms = per_pass[kname]
     fp = flop_model[kname] / (ms * 1e-3) / 1e12
     hb = byte_model[kname] / (ms * 1e-3) / 1e9
-    short = {"k_grad/k_err_local": "k_err_local"}.get(kname, kname)
+    short = {"k_grad/k_err_local": "k_err_local", "k_walk_fwd": "k_walk_img"}.get(kname, kname)
     traffic = pmc_traffic(short, L, PMC_SUMMARY_C3, dims={S for S, _ in classes})
     if hb / HBM_PEAK_GBS > fp / FP64_PEAK_TFLOPS:
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -504,8 +516,10 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     canon = NT * (1 + 2 + 2 + ne * (2 + 1 + 1)) * flops_expm(D) + 3 * NT * 8 * D ** 3 \
         + 4 * NT * ne * 8 * D ** 3 + 8 * D ** 2 * NT * 2 * (1 + ne)
     # FLOP of the work executed per evaluation: the stored variant exps, the nominal chain,
-    # the local-frame images, the B_k recurrence and the contractions (+ the sector heads)
-    exe = NT * per_step(lambda S: nv * flops_expm(S) + prod(S) + nz * 2 * prod(S) + ne * 2 * prod(S)
+    # the local-frame images (3 products each in the image walk: E^dag dX, Q^dag . Q), the B_k
+    # recurrence and the contractions (+ the sector heads)
+    nimg = 3 if walk else 2
+    exe = NT * per_step(lambda S: nv * flops_expm(S) + prod(S) + nz * nimg * prod(S) + ne * 2 * prod(S)
                         + 8 * S ** 2 * (1 + ne))
     if sec:
         exe += (16 + 24 * ne) * 8 * D ** 3

@@ -940,13 +940,14 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             Ps.scan_waves = (long)R >= 8L * ncu ? kScanTiny : (long)R >= 2L * ncu ? kScanNarrow : kScanWide;
             if (scan_override == kScanTiny || scan_override == kScanNarrow || scan_override == kScanWide)
                 Ps.scan_waves = scan_override;
-            // chunk walks (grape_walk.hpp): classes of <= kWalkMaxD levels without error sources
-            Ps.walk = (S <= grape::kWalkMaxD && P.ne == 0 && P.np <= grape::kWalkMaxNpA && P.na <= grape::kWalkMaxNpA &&
-                       !(P.opts & GRAPE_OPT_NO_WALK)) ? 1 : 0;
+            // chunk walks (grape_walk.hpp): classes of <= kWalkMaxD levels; with error sources the
+            // image walk (k_walk_img), which keeps the eps2 propagators of one gradient parameter
+            Ps.walk = (S <= grape::kWalkMaxD && (P.ne == 0 || P.nvg == 1) && P.np <= grape::kWalkMaxNpA &&
+                       P.na <= grape::kWalkMaxNpA && !(P.opts & GRAPE_OPT_NO_WALK)) ? 1 : 0;
             // the forward walk hands its propagators to the gradient walk (HBM, lane-minor) where the
             // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
             // 6.52 M evals/s; for the 2-level class it lost, 0.72 -> 1.01 ms per pass)
-            Ps.walk_store_e = Ps.walk && S == grape::kWalkMaxD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
+            Ps.walk_store_e = Ps.walk && P.ne == 0 && S == grape::kWalkMaxD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
             const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
@@ -1123,7 +1124,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.xT = p->d_xT;
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
-            sp.lane_major[cl] = p->Ps[cl].walk;
+            sp.lane_major[cl] = p->Ps[cl].walk && p->P.ne == 0;  // k_walk_grad's layout (k_img_fdx: row layout)
             sp.part_err[cl] = sb.part_err;
         }
         HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));

@@ -216,13 +216,20 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                 const long nmc = (long)B.nb * P.nchunks * D * D;
                 hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
                 mark(GRAPE_KERNEL_REDUCE, 1);
-                mark(GRAPE_KERNEL_WALK_GRAD, 0);
+                const int kid = P.ne > 0 ? GRAPE_KERNEL_GRAD : GRAPE_KERNEL_WALK_GRAD;  // k_img_fdx / k_walk_grad
+                mark(kid, 0);
                 const hipError_t e = grape_walk::launch<D>(1, P, B, st);
-                mark(GRAPE_KERNEL_WALK_GRAD, 1);
+                mark(kid, 1);
                 if (e != hipSuccess) return e;
+                if (P.ne > 0) {  // the error scans read the walk's images (B.Zl)
+                    mark(GRAPE_KERNEL_ERR_SCAN, 0);
+                    launch_err_scan<D>(P, B, st);
+                    mark(GRAPE_KERNEL_ERR_SCAN, 1);
+                }
                 return hipGetLastError();
             }
-            return hipErrorInvalidValue;  // no stage 2 without error sources
+            if (P.ne == 0) return hipErrorInvalidValue;  // no stage 2 without error sources
+            // stage 2 with error sources: the common F_d2err_dx walks below
         }
     }
     if (stage == 0) {

@@ -428,13 +428,31 @@ __device__ __forceinline__ cd walk_coef(const Term &t, int nt1, const WalkX &X, 
     return cmul(cmake(t.sre, t.sim), cmake(fr, fi));
 }
 
+// A_w += g H_w-term for the NS sectors of this lane (compressed; diagonal as the imaginary part
+// of the same complex MAC)
+template <int D, int NS>
+__device__ __forceinline__ void walk_add_term(const DevProblem &P, cptr<cd> ops, int op_index, cd g, SM<D> (&A)[NS]) {
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+        const cptr<cd> op = ops + (size_t)w * P.sec_ops + (size_t)op_index * D * D;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd o = cload(op, j * D + j);
+            A[w].d[j] = fma(g.im, o.re, fma(g.re, o.im, A[w].d[j]));
+#pragma unroll
+            for (int k = j + 1; k < D; ++k) cmac(A[w].u[uix(D, j, k)], g, cload(op, j * D + k));
+        }
+    }
+}
+
 // A_w = -i dt H_w(x_k perturbed by pp) for the NS sectors w of this lane, compressed: the
 // builder of ItemBuilder with each sector's row-major operators, term by term in order (the same
-// cmac operand roles), diagonal as the imaginary part of the same complex MAC.  The term
-// coefficients (the trig of the controls) are computed once for all NS sectors.
+// cmac operand roles).  The term coefficients (the trig of the controls) are computed once for all
+// NS sectors.  err >= 0 adds errval Herror_err (perturbed by pp too) after H0's terms, as
+// ItemBuilder<D, true> does (UnitaryCalculations.jl:67-68, 71-72, 77-78).
 template <int D, int NS>
 __device__ __forceinline__ void walk_build(const DevProblem &P, cptr<cd> ops, const WalkX &X, int nt1, const Pert &pp,
-                                           SM<D> (&A)[NS]) {
+                                           SM<D> (&A)[NS], int err = -1, double errval = 0.0) {
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
 #pragma unroll
@@ -448,17 +466,17 @@ __device__ __forceinline__ void walk_build(const DevProblem &P, cptr<cd> ops, co
     for (int t = 0; t < P.n_h0; ++t) {
         const Term tm = tload(terms, t);
         const cd c = walk_coef(tm, nt1, X, pp, tc);
-        const cd g = cmake(P.dt * c.im, -(P.dt * c.re));  // -i dt c
-#pragma unroll
-        for (int w = 0; w < NS; ++w) {
-            const cptr<cd> op = ops + (size_t)w * P.sec_ops + (size_t)tm.op * D * D;
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                const cd o = cload(op, j * D + j);
-                A[w].d[j] = fma(g.im, o.re, fma(g.re, o.im, A[w].d[j]));
-#pragma unroll
-                for (int k = j + 1; k < D; ++k) cmac(A[w].u[uix(D, j, k)], g, cload(op, j * D + k));
-            }
+        walk_add_term<D, NS>(P, ops, tm.op, cmake(P.dt * c.im, -(P.dt * c.re)), A);  // -i dt c
+    }
+    if (err >= 0) {  // (wave-uniform)
+        const cptr<int> off = as_constant(P.err_off);
+        const int o0 = off[err], o1 = off[err + 1];
+        const cptr<Term> et = as_constant(P.err);
+#pragma unroll 1
+        for (int t = o0; t < o1; ++t) {
+            const Term tm = tload(et, t);
+            const cd c = cscale(errval, walk_coef(tm, nt1, X, pp, tc));
+            walk_add_term<D, NS>(P, ops, tm.op, cmake(P.dt * c.im, -(P.dt * c.re)), A);
         }
     }
 }
@@ -549,6 +567,7 @@ struct WalkCfg {
     static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? 3 : 2) : D == 3 ? (NS == 1 ? 2 : 1)
                                                                               : GRAPE_WALK_G4_WAVES;
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? 1 : GRAPE_WALK_G4S_WAVES;
+    static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? 3 : 2) : 1;  // k_walk_img (error sources)
 };
 
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
@@ -793,6 +812,215 @@ void k_walk_grad(DevProblem P, DevBatch B) {
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Error sources: the image walk (k_walk_img, stage 0) and its F_dx traces (k_img_fdx, stage 1)
+// ---------------------------------------------------------------------------
+// With error sources the error kernels (grape_errpath.hpp: k_err_scan, k_err_grad) consume, per
+// step, the local-frame images Y(dX) = Q_k^dag dX Q_{k-1} of every finite difference dX:
+//   Z1_u = Y((E(x_u + eps) - E) / eps),  W_e = Y((E(err_e eps) - E) / eps),
+//   Z2_{e,u} = Y((E(x_u + eps2, err_e eps2) + E - E(err_e eps2) - E(x_u + eps2)) / eps2^2)
+// (UnitaryCalculations.jl:48-95).  Round 2 stored every variant propagator of the step (k_expm:
+// 15 at C3) and Q_k (k_scan), and read them back (k_err_local): 2.95 MB of E per evaluation
+// written and re-read.  The image walk forms the images in the lane that walks the chunk:
+// per step the nominal E_k, then every variant's exponential column by column, its difference
+// column dX e_i and at once column i of Z = E_k^dag dX, then
+//   Y = Q_k^dag dX Q_{k-1} = Q_{k-1}^dag Z Q_{k-1}      (Q_k = E_k Q_{k-1}, unitary)
+// column by column into its Zl slot, and finally Q <- E_k Q.  Only the images (9 tiles per step
+// at C3) and the chunk totals T_c (k_scan's input, as k_walk_fwd) reach HBM.  The eps2
+// propagators E(x_u + eps2) and E(err_e eps2) that the mixed stencil needs stay in registers:
+// the walk serves nvg == 1 (one gradient parameter per step: np = 1 without x_add-dependent
+// H0 -- C3); other problems keep the round-2 kernels.
+struct VArg {
+    Pert p;
+    int err;
+    double errval;
+};
+__device__ __forceinline__ VArg vload(cptr<VSpec> p, int i) {
+    VArg a;
+    a.p.var = p[i].pert.var;
+    a.p.index = p[i].pert.index;
+    a.p.delta = p[i].pert.delta;
+    a.err = p[i].err;
+    a.errval = p[i].errval;
+    return a;
+}
+
+enum { IMG_DIFF = 0, IMG_MIX = 1, IMG_KEEP_D2 = 2, IMG_KEEP_E2 = 3 };
+template <int K>
+struct ImgKind {
+    static constexpr int value = K;
+};
+
+template <int D, int NS>
+__global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_walk_img(DevProblem P, DevBatch B) {
+    using C = WalkCfg<D, NS>;
+    constexpr int TS = D * D;
+    const WalkLane L = walk_lane<NS>(P, B);
+    const int ns = P.nsec > 1 ? P.nsec : 1;
+    const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
+    const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
+    const cptr<VSpec> vs = as_constant(P.vs);
+    cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
+    Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    WalkX X;
+    walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));  // x_add
+    const int k0 = L.c * P.L;
+    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
+    // Q_{k-1} (chunk-local), E_k, and the step's eps2 propagators E(x + eps2), E(err_e eps2)
+    cd Q[NS][D][D], E[NS][D][D], Ed2[NS][D][D], Ee2[NS][D][D];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) Q[w][j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+        }
+    }
+#pragma unroll 1
+    for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store into the sink
+        const int k = min(k0 + jj, P.Nt - 1);
+        const bool act = L.ok && k0 + jj < P.Nt;
+        walk_set_xk(X, xn);
+        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
+        {
+            SM<D> A[NS];
+            walk_build<D, NS>(P, ops, X, k + 1, none, A);
+#pragma unroll
+            for (int w = 0; w < NS; ++w)
+                walk_expm<D, C::FENCE, true>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) E[w][j][i] = x[j];
+                });
+        }
+        // one variant: its exponential, and (IMG_DIFF / IMG_MIX) the image of its difference to slot
+        auto variant = [&](auto kind, int v, int slot) {
+            constexpr int KIND = decltype(kind)::value;
+            const VArg va = vload(vs, v);
+            SM<D> A[NS];
+            walk_build<D, NS>(P, ops, X, k + 1, va.p, A, va.err, va.errval);
+#pragma unroll
+            for (int w = 0; w < NS; ++w) {
+                if constexpr (KIND == IMG_KEEP_D2 || KIND == IMG_KEEP_E2) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            if constexpr (KIND == IMG_KEEP_D2) Ed2[w][j][i] = x[j];
+                            else Ee2[w][j][i] = x[j];
+                        }
+                    });
+                } else {
+                    cd Z[D][D];  // E_k^dag dX, column by column as the variant's columns come out
+                    walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+                        cd dx[D];
+#pragma unroll
+                        for (int r = 0; r < D; ++r) {
+                            if constexpr (KIND == IMG_DIFF) dx[r] = cscale(P.inv_eps, csub(x[r], E[w][r][i]));  // (E' - E) / eps
+                            else  // (E(u + eps2, err eps2) + E - E(err eps2) - E(u + eps2)) / eps2^2, left to right
+                                dx[r] = cscale(P.inv_eps2sq, csub(csub(cadd(x[r], E[w][r][i]), Ee2[w][r][i]), Ed2[w][r][i]));
+                        }
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            cd c = czero();
+#pragma unroll
+                            for (int r = 0; r < D; ++r) cmac(c, cconj(E[w][r][j]), dx[r]);
+                            Z[j][i] = c;
+                        }
+                    });
+                    // Y = Q^dag Z Q column by column: t = Z q_c, y = Q^dag t; row-major slot tile
+                    cd *dst = act ? B.Zl + ((((size_t)L.be * ns + L.w0 + w) * P.Nt + k) * P.nz + slot) * TS : B.sink;
+#pragma unroll
+                    for (int cc = 0; cc < D; ++cc) {
+                        cd t[D];
+#pragma unroll
+                        for (int m = 0; m < D; ++m) {
+                            cd c = czero();
+#pragma unroll
+                            for (int n = 0; n < D; ++n) cmac(c, Z[m][n], Q[w][n][cc]);
+                            t[m] = c;
+                        }
+#pragma unroll
+                        for (int r = 0; r < D; ++r) {
+                            cd c = czero();
+#pragma unroll
+                            for (int m = 0; m < D; ++m) cmac(c, cconj(Q[w][m][r]), t[m]);
+                            dst[r * D + cc] = c;
+                        }
+                    }
+                }
+            }
+        };
+        // the variant table of grape_plan_create (nvg == 1: u = 0)
+        variant(ImgKind<IMG_DIFF>{}, P.off_dx, 0);          // Z1
+        variant(ImgKind<IMG_KEEP_D2>{}, P.off_dx2, 0);      // E(x + eps2)
+#pragma unroll 1
+        for (int e = 0; e < P.ne; ++e) {
+            const int ve = P.off_err + e * P.err_stride;
+            variant(ImgKind<IMG_DIFF>{}, ve, P.nvg + e);                   // W_e
+            variant(ImgKind<IMG_KEEP_E2>{}, ve + 1, 0);                    // E(err_e eps2)
+            variant(ImgKind<IMG_MIX>{}, ve + 2, P.nvg + P.ne + e * P.nvg);  // Z2_{e,0}
+        }
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) {  // column i of E_k Q (in place: it reads only column i)
+                cd q[D], t[D];
+#pragma unroll
+                for (int m = 0; m < D; ++m) q[m] = Q[w][m][i];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    cd c = czero();
+#pragma unroll
+                    for (int m = 0; m < D; ++m) cmac(c, q[m], E[w][j][m]);
+                    t[j] = c;
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    Q[w][j][i] = cmake(act ? t[j].re : Q[w][j][i].re, act ? t[j].im : Q[w][j][i].im);
+            }
+        }
+    }
+    if (L.ok) {
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int i = 0; i < D; ++i) dst[j * D + i] = Q[w][j][i];
+            }
+        }
+    }
+}
+
+// F_dx terms of the image walk, one thread per (sub-evaluation, step, parameter):
+// F_dx[u, k] (sector part) = Re tr(M'_c Z1_u)   (k_err_local's trace; FidelityCalculations.jl:56-76)
+template <int D>
+__global__ __launch_bounds__(256) void k_img_fdx(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    const long n = (long)B.nb * P.Nt * P.nvg;
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    const int u = (int)(g % P.nvg);
+    const long bk = g / P.nvg;
+    const int k = (int)(bk % P.Nt);
+    const long b = bk / P.Nt;
+    const cd *Z = B.Zl + ((size_t)bk * P.nz + u) * TS;
+    const cd *Mc = B.Mc + ((size_t)b * P.nchunks + k / P.L) * TS;
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const cd z = Z[i * D + j], m = Mc[j * D + i];
+            s += z.re * m.re - z.im * m.im;
+        }
+    }
+    B.sec_part[g] = s;  // [(b Nt + k) nvg + u]
 }
 
 }  // namespace grape

@@ -13,7 +13,9 @@ constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBl
 
 namespace grape_walk {
 // one lane per (sector, evaluation, chunk) of the class: stage 0 = k_walk_fwd (chunk totals to
-// B.Tc), stage 1 = k_walk_grad (per-sector F_dx terms to B.sec_part)
+// B.Tc), stage 1 = k_walk_grad (per-sector F_dx terms to B.sec_part, evaluation-fastest).  With
+// error sources (P.ne > 0, nvg == 1): stage 0 = k_walk_img (chunk totals and the local-frame images
+// to B.Zl), stage 1 = k_img_fdx (per-sector F_dx terms to B.sec_part, [nb][Nt][nvg])
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
 // the walks' controls: x [nb][nx] -> xT [nx][nb] (B.xT), once per launch for every walk class

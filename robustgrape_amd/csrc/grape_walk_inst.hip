@@ -11,6 +11,15 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
     const long lanes = (long)(B.nb / ns) * P.nchunks;
     const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
     const dim3 blk(grape::kWalkBlock);
+    if (P.ne > 0) {  // error sources: the image walk, then (stage 1) the F_dx traces of its Z1 images
+        if (stage == 0) {
+            hipLaunchKernelGGL((grape::k_walk_img<D, NS>), grid, blk, 0, st, P, B);
+        } else {
+            const long n = (long)B.nb * P.Nt * P.nvg;
+            hipLaunchKernelGGL(grape::k_img_fdx<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, B);
+        }
+        return;
+    }
     // stored propagators: the 4-level class only (engine: P.walk_store_e)
     constexpr bool CAN_STORE = D >= 4;
     const bool store = CAN_STORE && P.walk_store_e;
