@@ -703,10 +703,10 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
-                    help="restarts per GPU per step; default 262144 (c2), 4096 (c3), 16 (c5)")
+                    help="restarts per GPU per step; default 262144 (c2), 16384 (c3), 16 (c5)")
     ap.add_argument("--chunk", type=int, default=None,
                     help="evaluations per device pass (the plan's workspace; larger steps are chunked "
-                         "by the C side); default 32768 (c2), 2048 (c3), 16 (c5)")
+                         "by the C side); default 32768 (c2), 8192 (c3), 16 (c5)")
     ap.add_argument("--workload", choices=("c2", "c3", "c5", "c5err", "c4opt", "c2-closure"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
@@ -763,8 +763,8 @@ def main():
     # sectors: 8 192 -> 2.64M, 16 384 -> 2.65M, 32 768 -> 2.70M, 65 536 -> 2.71M evals/s;
     # DESIGN.md 9).  B is sized so that 20 steps last about 2 s (the driver's GPU-busy sampler
     # must see them).
-    B = args.batch or (16 if c5 else 4096 if c3 else 262144)
-    chunk = args.chunk or (16 if c5 else 2048 if c3 else 32768)
+    B = args.batch or (16 if c5 else 16384 if c3 else 262144)
+    chunk = args.chunk or (16 if c5 else 8192 if c3 else 32768)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
     plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=min(count, chunk))
     X = torch.from_numpy(inputs(first, count)).to(dev)

@@ -555,6 +555,9 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #ifndef GRAPE_WALK_G4_XLDS  // k_walk_grad<4>: 1 = X / Y in the LDS slot and E in registers, 0 = the reverse
 #define GRAPE_WALK_G4_XLDS 1
 #endif
+#ifndef GRAPE_WALK_IMG_LDS
+#define GRAPE_WALK_IMG_LDS 1
+#endif
 template <int D, int NS>
 struct WalkCfg {
     static constexpr bool FENCE = D >= 4;        // per-column scheduling fences (register discipline)
@@ -568,6 +571,7 @@ struct WalkCfg {
                                                                               : GRAPE_WALK_G4_WAVES;
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? 1 : GRAPE_WALK_G4S_WAVES;
     static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? 3 : 2) : 1;  // k_walk_img (error sources)
+    static constexpr bool IMG_LDS = D >= 4 && GRAPE_WALK_IMG_LDS;      // k_walk_img: eps2 propagators in LDS
 };
 
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
@@ -871,8 +875,17 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));  // x_add
     const int k0 = L.c * P.L;
     X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
-    // Q_{k-1} (chunk-local), E_k, and the step's eps2 propagators E(x + eps2), E(err_e eps2)
-    cd Q[NS][D][D], E[NS][D][D], Ed2[NS][D][D], Ee2[NS][D][D];
+    // Q_{k-1} (chunk-local), E_k, and the step's eps2 propagators E(x + eps2), E(err_e eps2) (the
+    // latter two in the lane's LDS slots at D = 4, where the registers run out)
+    cd Q[NS][D][D], E[NS][D][D];
+    constexpr bool EL = C::IMG_LDS;
+    MStore<D, EL> Ed2[NS], Ee2[NS];
+    if constexpr (EL) {
+        static_assert(NS == 1, "one pair of LDS slots per lane");
+        __shared__ cd lds_d2[kWalkBlock * MStore<D, true>::kStride], lds_e2[kWalkBlock * MStore<D, true>::kStride];
+        Ed2[0].p = MStore<D, true>::slot(lds_d2);
+        Ee2[0].p = MStore<D, true>::slot(lds_e2);
+    }
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
 #pragma unroll
@@ -909,19 +922,21 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
                     walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                         for (int j = 0; j < D; ++j) {
-                            if constexpr (KIND == IMG_KEEP_D2) Ed2[w][j][i] = x[j];
-                            else Ee2[w][j][i] = x[j];
+                            if constexpr (KIND == IMG_KEEP_D2) Ed2[w].set(j, i, x[j]);
+                            else Ee2[w].set(j, i, x[j]);
                         }
                     });
                 } else {
                     cd Z[D][D];  // E_k^dag dX, column by column as the variant's columns come out
                     walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
                         cd dx[D];
+                        const auto &e2 = Ee2[w].opaque();  // (LDS reads issued here, not hoisted)
+                        const auto &d2 = Ed2[w].opaque();
 #pragma unroll
                         for (int r = 0; r < D; ++r) {
                             if constexpr (KIND == IMG_DIFF) dx[r] = cscale(P.inv_eps, csub(x[r], E[w][r][i]));  // (E' - E) / eps
                             else  // (E(u + eps2, err eps2) + E - E(err eps2) - E(u + eps2)) / eps2^2, left to right
-                                dx[r] = cscale(P.inv_eps2sq, csub(csub(cadd(x[r], E[w][r][i]), Ee2[w][r][i]), Ed2[w][r][i]));
+                                dx[r] = cscale(P.inv_eps2sq, csub(csub(cadd(x[r], E[w][r][i]), e2.at(r, i)), d2.at(r, i)));
                         }
 #pragma unroll
                         for (int j = 0; j < D; ++j) {
