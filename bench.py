@@ -620,7 +620,8 @@ def c4opt(args):
     params = FidelityRobustGRAPEParameters(
         x_initial=X0[0], regularization_functions=[REG.regularization_cost_phase], regularization_coeff1=[1e-7],
         regularization_coeff2=[1e-7], error_source_coeff=[], iterations=10 ** 9)
-    cost = OPT.RobustCost(fp, params, nparam=1, max_batch=B, device=0)
+    cost = OPT.RobustCost(fp, params, nparam=1, max_batch=B, device=0, scan_waves=args.scan_waves,
+                          options=args.plan_options)
     dev = torch.device("cuda", 0)
     opts = OPT._solver_options(params)
     opts.update(g_tol=0.0)  # no early stop: every restart iterates through the timed region
@@ -713,6 +714,10 @@ def main():
                          "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
                          "batched L-BFGS (one step = one iteration of every restart); c2-closure: C2 as "
                          "plain Python closures through the host-table fallback")
+    ap.add_argument("--scan-waves", type=int, default=None, choices=(0, 1, 4, 8),
+                    help="c4opt: the plan's scan width (chunking); 0 = by batch size, default: RobustCost's choice")
+    ap.add_argument("--plan-options", type=int, default=0,
+                    help="c4opt: GRAPE_OPT_* flags of the optimiser's plan (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-paths", action="store_true",
                     help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")

@@ -165,6 +165,10 @@ typedef struct grape_desc {
  * GRAPE_MAX_SMALL_DIM always take this path (Hermitian tables only).
  */
 #define GRAPE_OPT_GENERAL_H0 64
+/* Calls of at most 4096 evaluations on a plan with two sector classes run the second class on an
+ * auxiliary stream beside the first (joined before the sector heads; latency-bound calls such as
+ * the optimiser's line-search rounds).  This option keeps every call on the plan's one stream. */
+#define GRAPE_OPT_NO_FORK 128
 
 typedef struct grape_plan grape_plan;
 

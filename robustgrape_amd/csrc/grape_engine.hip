@@ -53,6 +53,8 @@ int fail(int code, const std::string &msg) {
 
 constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow,
               kScanTiny = grape_host::kScanTiny;
+// calls of at most this many evaluations run the two sector classes on two streams (enqueue)
+constexpr int kForkMaxBatch = 4096;
 constexpr int kCtrlInts = 8;  // [0..1] single-eval counters, [2] status, [4..5] pipeline overflow counters
 using grape_host::KMark;
 using grape_host::launch_pipeline;
@@ -173,6 +175,12 @@ struct grape_plan {
     SecBuf sb[2];
     int *d_fixed = nullptr;
     grape_proj::SectorHead SH{};
+    // small calls with two sector classes: the second class runs on an auxiliary stream beside the
+    // first (fork / join events; the classes are independent until the sector heads)
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool capturing = false;  // graph_capture in progress: no fork (one-stream graphs; events captured in a
+                             // graph and recorded outside it crashed the runtime, round 3)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -252,6 +260,9 @@ static void free_plan(grape_plan *p) {
     for (double *h : {p->h_x, p->h_F, p->h_Fdx, p->h_Fd2, p->h_Fd2dx})
         if (h) (void)hipHostFree(h);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+    if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
 }
@@ -281,11 +292,11 @@ static int validate_terms(const grape_term *t, int n, int n_ops, int np, int na,
 // engine and is refused by the dense one.  Error generators need no such property:
 // their propagators only enter through differences dE (UnitaryCalculations.jl:68-83) that
 // the nominal chain transports, so a non-Hermitian Herror (a decay-rate error) is served.
-static int check_hermitian_terms(const grape_desc *desc, const grape_term *t, int n, const char *what) {
+// 0: every term keeps H Hermitian; 1: a complex-valued coefficient; 2: scale * operator not Hermitian
+static int hermitian_terms(const grape_desc *desc, const grape_term *t, int n) {
     const int D = desc->ndim;
     for (int k = 0; k < n; ++k) {
-        if (t[k].func == GRAPE_FN_CIS)
-            return fail(GRAPE_ERR_UNSUPPORTED, std::string(what) + ": complex-valued coefficient (H must be Hermitian)");
+        if (t[k].func == GRAPE_FN_CIS) return 1;
         const double *op = desc->ops + 2 * (size_t)t[k].op * D * D;
         const double sr = t[k].scale_re, si = t[k].scale_im;
         double mx = 0.0, dev = 0.0;
@@ -298,10 +309,16 @@ static int check_hermitian_terms(const grape_desc *desc, const grape_term *t, in
                 mx = std::max(mx, std::hypot(sr * a[0] - si * a[1], sr * a[1] + si * a[0]));
                 dev = std::max(dev, std::hypot(re, im));
             }
-        if (dev > 1e-12 * std::max(mx, 1e-300))
-            return fail(GRAPE_ERR_UNSUPPORTED,
-                        std::string(what) + ": scale * operator is not Hermitian (non-unitary propagators are not supported)");
+        if (dev > 1e-12 * std::max(mx, 1e-300)) return 2;
     }
+    return 0;
+}
+static int check_hermitian_terms(const grape_desc *desc, const grape_term *t, int n, const char *what) {
+    const int h = hermitian_terms(desc, t, n);
+    if (h == 1) return fail(GRAPE_ERR_UNSUPPORTED, std::string(what) + ": complex-valued coefficient (H must be Hermitian)");
+    if (h == 2)
+        return fail(GRAPE_ERR_UNSUPPORTED,
+                    std::string(what) + ": scale * operator is not Hermitian (non-unitary propagators are not supported)");
     return GRAPE_OK;
 }
 
@@ -704,6 +721,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         if (desc->h0_terms[k].var == 2) xadd_dep = true;
     for (int k = 0; k < n_err_terms; ++k)
         if (desc->err_terms[k].var == 2) xadd_dep = true;
+    // Hermitian error generators (the image walk's exponential is skew-Hermitian, grape_walk.hpp)
+    const bool err_herm = tables || hermitian_terms(desc, desc->err_terms, n_err_terms) == 0;
     const ProjectorSetup ps = setup_projector(desc);
     const double trP = ps.trP;
     if (!(trP > 0)) return fail(GRAPE_ERR_INVALID, "projector trace must be positive");
@@ -942,7 +961,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                 Ps.scan_waves = scan_override;
             // chunk walks (grape_walk.hpp): classes of <= kWalkMaxD levels; with error sources the
             // image walk (k_walk_img), which keeps the eps2 propagators of one gradient parameter
-            Ps.walk = (S <= grape::kWalkMaxD && (P.ne == 0 || P.nvg == 1) && P.np <= grape::kWalkMaxNpA &&
+            // (its exponential keeps A skew-Hermitian in compressed form: Hermitian error generators only;
+            // a decay-rate error, -i e/2 |r><r|, keeps the stored-variant kernels)
+            Ps.walk = (S <= grape::kWalkMaxD && (P.ne == 0 || (P.nvg == 1 && err_herm)) && P.np <= grape::kWalkMaxNpA &&
                        P.na <= grape::kWalkMaxNpA && !(P.opts & GRAPE_OPT_NO_WALK)) ? 1 : 0;
             // the forward walk hands its propagators to the gradient walk (HBM, lane-minor) where the
             // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
@@ -1000,6 +1021,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             H.MsecE[cl] = b.MsecE;
         }
         p->ncls = (int)ss.cls.size();
+        if (p->ncls == 2 && (hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess ||
+                             hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                             hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess))
+            return bail(fail(GRAPE_ERR_HIP, "cannot create the auxiliary stream"));
     }
     *out = p;
     return GRAPE_OK;
@@ -1133,7 +1158,29 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             HIPCHECK(grape_walk::transpose_x(d_x, p->d_xT, nb, p->P.nx, st));
             mk(GRAPE_KERNEL_WALK_FWD, 1);
         }
-        for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 0, p->Ps[cl], Bc[cl], st, mk));
+        // Small calls (latency-bound: the optimiser's line-search rounds, single evaluations) run
+        // the second sector class on the auxiliary stream beside the first; large ones keep one
+        // stream (no gain there, DESIGN 4.1, and per-kernel event times stay per kernel).
+        const bool fork = p->aux_stream && !p->capturing && nb <= kForkMaxBatch && !(p->P.opts & GRAPE_OPT_NO_FORK);
+        auto stage = [&](int s) -> hipError_t {  // stage s of every class (class 1 forked when `fork`)
+            if (!fork) {
+                for (int cl = 0; cl < p->ncls; ++cl) {
+                    const hipError_t e = dispatch_sector_stage(p->Ps[cl].D, s, p->Ps[cl], Bc[cl], st, mk);
+                    if (e != hipSuccess) return e;
+                }
+                return hipSuccess;
+            }
+            hipError_t e = hipEventRecord(p->ev_fork, st);
+            if (e == hipSuccess) e = hipStreamWaitEvent(p->aux_stream, p->ev_fork, 0);
+            if (e == hipSuccess) e = dispatch_sector_stage(p->Ps[0].D, s, p->Ps[0], Bc[0], st, mk);
+            p->cur_stream = p->aux_stream;
+            if (e == hipSuccess) e = dispatch_sector_stage(p->Ps[1].D, s, p->Ps[1], Bc[1], p->aux_stream, mk);
+            p->cur_stream = st;
+            if (e == hipSuccess) e = hipEventRecord(p->ev_join, p->aux_stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(st, p->ev_join, 0);
+            return e;
+        };
+        HIPCHECK(stage(0));
         grape_proj::SectorHead H = p->SH;
         H.x = d_x;
         H.F = d_F;
@@ -1144,13 +1191,12 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         mk(GRAPE_KERNEL_SCAN, 0);
         HIPCHECK(grape_proj::launch_sector_head(H, nb, st));
         mk(GRAPE_KERNEL_SCAN, 1);
-        for (int cl = 0; cl < p->ncls; ++cl) HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 1, p->Ps[cl], Bc[cl], st, mk));
+        HIPCHECK(stage(1));
         if (p->P.ne > 0) {  // the sector error head, then the F_d2err_dx walks of every class
             mk(GRAPE_KERNEL_ERR_SCAN, 0);
             HIPCHECK(grape_proj::launch_sector_err_head(H, nb, st));
             mk(GRAPE_KERNEL_ERR_SCAN, 1);
-            for (int cl = 0; cl < p->ncls; ++cl)
-                HIPCHECK(dispatch_sector_stage(p->Ps[cl].D, 2, p->Ps[cl], Bc[cl], st, mk));
+            HIPCHECK(stage(2));
         }
         HIPCHECK(dispatch_sector_reduce(p->Ps[0].D, p->Ps[0], Bc[0], sp, nb, st, mk));
         return GRAPE_OK;
@@ -1317,7 +1363,9 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
         }
         return GRAPE_OK;
     };
+    p->capturing = true;
     const int rc = body();
+    p->capturing = false;
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(st, &g);
     if (rc) {

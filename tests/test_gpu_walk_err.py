@@ -153,3 +153,17 @@ def test_image_walk_not_for_two_gradient_parameters():
     fp = P.xadd_err_problem(9, 16)
     X = np.stack([P.xadd_x(16, s) for s in range(3)])
     _run(fp, X, expect_walk=False)
+
+
+def test_image_walk_not_for_non_hermitian_error_generator():
+    """A decay-rate error source (-i e/2 |r><r|) makes the error variants non-unitary: the image
+    walk's exponential is the skew-Hermitian one, so the plan keeps the stored-variant kernels
+    (which the oracle test in tests/test_gpu_xadd_err.py checks)."""
+    from robustgrape_amd.operators import OperatorBasisError, Term
+    from robustgrape_amd.types import ErrorSource
+    decay = np.diag([0, 0, 0, 0, 1.0]).astype(complex)
+    base = P.sym_problem(12, errors=("amp",))
+    fo = base.replace(unitary_problem=base.unitary_problem.replace(
+        error_sources=list(base.unitary_problem.error_sources) + [ErrorSource(OperatorBasisError([Term(decay, scale=-0.5j)]))]))
+    X = np.stack([P.random_x(12, s) for s in range(2)])
+    _run(fo, X, expect_walk=False)
