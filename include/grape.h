@@ -169,6 +169,10 @@ typedef struct grape_desc {
  * auxiliary stream beside the first (joined before the sector heads; latency-bound calls such as
  * the optimiser's line-search rounds).  This option keeps every call on the plan's one stream. */
 #define GRAPE_OPT_NO_FORK 128
+/* Sector problems with a diagonal projector and a diagonal target form F and M with a
+ * one-thread-per-evaluation head over the sector blocks; this option keeps the general
+ * (d x d products) sector head for every problem (A/B and parity checks). */
+#define GRAPE_OPT_GENERAL_HEAD 256
 
 typedef struct grape_plan grape_plan;
 

@@ -944,6 +944,17 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         H.ncls = (int)ss.cls.size();
         H.fixed = p->d_fixed;
         H.nfixed = (int)ss.fixed.size();
+        // diagonal projector and target, classes of <= 4 levels: the one-thread-per-evaluation head
+        // (grape_projector.hip k_sec_head_diag)
+        H.diag = !ps.general && !tables && !(P.opts & GRAPE_OPT_GENERAL_HEAD);
+        for (const SectorClass &sc : ss.cls) H.diag = H.diag && sc.S <= 4;
+        for (int k = 0; H.diag && k < desc->n_target_terms; ++k) {
+            const double *op = desc->ops + 2 * (size_t)desc->target_terms[k].op * D * D;
+            for (int i = 0; i < D; ++i)
+                for (int j = 0; j < D; ++j)
+                    if (i != j && (op[2 * (i + (size_t)j * D)] != 0.0 || op[2 * (i + (size_t)j * D) + 1] != 0.0))
+                        H.diag = 0;
+        }
         for (int cl = 0; cl < (int)ss.cls.size(); ++cl) {
             const SectorClass &sc = ss.cls[cl];
             const int S = sc.S;

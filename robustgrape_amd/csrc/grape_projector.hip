@@ -475,7 +475,163 @@ hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Diagonal projector and diagonal target (H.diag: the Rydberg CZ problems).  Every matrix of the
+// head is then block-diagonal with the sectors, and k_sec_head's products reduce to sums over
+// the sector blocks of U, one THREAD per evaluation (k_sec_head: one wave per evaluation, ten
+// LDS-staged d x d products; 0.41 ms of a 4.6-ms C2 pass):
+//   K = U0^dag U: K_ij = conj(u0_i) U_ij,   tau = sum_i w_i K_ii,
+//   F = [sum_ij w_i p_j |K_ij|^2 + |tau|^2] / DD                      (FidelityCalculations.jl:54)
+//   M_ij = 2 [p_i (K^dag W K)_ij + conj(tau) w_i K_ij] / DD   (i, j in one sector; k_sec_head's
+//          B (K^dag A K) + B^dag ((A K)^dag K) + 2 conj(tau) A K with A = diag(w), B = diag(p))
+//   target part of F_dx_add (:34-40, 67-76), d = (u0(x_add + eps e_q) - u0) / eps:
+//   [2 sum_ij w_i p_j Re(conj(d_i) U_ij conj(K_ij)) + 2 Re(conj(tau) sum_i w_i conj(d_i) U_ii)] / DD
+// The untouched levels g contribute U_gg = 1.  Sector classes of at most kDiagMaxS levels.
+constexpr int kDiagBlock = 64, kDiagMaxS = 4;
+// u[i] = diagonal of the target at x_add (perturbed by pp), i < D, in this thread's LDS row
+__device__ void target_diag(const grape::DevProblem &P, const double *xb, const grape::Pert &pp, cd *u) {
+    const double *xadd = xb + (size_t)P.np * P.Nt;
+    for (int i = 0; i < P.D; ++i) u[i] = cd{0.0, 0.0};
+    for (int q = 0; q < P.n_tgt; ++q) {
+        const grape::Term tm = P.tgt[q];
+        const cd c = grape::term_coef(tm, 1, xb, xadd, pp);
+        const cd *op = P.ops + (size_t)tm.op * P.D * P.D;
+        for (int i = 0; i < P.D; ++i) u[i] = p_add(u[i], p_mul(c, op[(size_t)i * P.D + i]));
+    }
+}
+__device__ __forceinline__ double pdiag(const grape::DevProblem &P, int g) { return P.W[g] != 0.0 ? 1.0 : 0.0; }
+
+// pass 0: F's sum and tau; pass 1: the blocks M_ww; pass 2: the F_dx_add sums against d
+template <int S>
+__device__ void diag_blocks(const SectorHead &H, int cl, int b, int pass, const cd *u0, const cd *d, cd tau,
+                            double &fsum, cd &acc) {
+    const grape::DevProblem &P = H.P;
+    const int ns = H.nsec[cl];
+    const double sc = 2.0 / P.DD;
+    for (int w = 0; w < ns; ++w) {
+        const cd *Ub = H.Ub[cl] + ((size_t)b * ns + w) * S * S;
+        int g[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) g[r] = H.sidx[cl][w * S + r];
+        cd K[S][S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+#pragma unroll
+            for (int c = 0; c < S; ++c) {
+                const bool ok = g[r] >= 0 && g[c] >= 0;
+                K[r][c] = ok ? p_mul(p_conj(u0[g[r] >= 0 ? g[r] : 0]), Ub[r * S + c]) : cd{0.0, 0.0};
+            }
+        }
+        if (pass == 0) {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                if (g[r] < 0) continue;
+                const double wr = P.W[g[r]];
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    if (g[c] < 0) continue;
+                    fsum += wr * pdiag(P, g[c]) * (K[r][c].re * K[r][c].re + K[r][c].im * K[r][c].im);
+                }
+                acc = p_add(acc, p_scale(wr, K[r][r]));
+            }
+        } else if (pass == 1) {
+            cd *dst = H.Msec[cl] + ((size_t)b * ns + w) * S * S;
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    cd m{0.0, 0.0};
+                    if (g[r] >= 0 && g[c] >= 0) {
+                        cd s{0.0, 0.0};
+#pragma unroll
+                        for (int k = 0; k < S; ++k)
+                            if (g[k] >= 0) s = p_add(s, p_scale(P.W[g[k]], p_mul(p_conj(K[k][r]), K[k][c])));
+                        m = p_scale(sc, p_add(p_scale(pdiag(P, g[r]), s),
+                                              p_scale(P.W[g[r]], p_mul(cd{tau.re, -tau.im}, K[r][c]))));
+                    }
+                    dst[r * S + c] = m;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                if (g[r] < 0) continue;
+                const double wr = P.W[g[r]];
+                const cd dr = p_conj(d[g[r]]);
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    if (g[c] < 0) continue;
+                    const cd kd = p_mul(dr, Ub[r * S + c]);  // Kd_rc
+                    fsum += wr * pdiag(P, g[c]) * (kd.re * K[r][c].re + kd.im * K[r][c].im);
+                }
+                acc = p_add(acc, p_scale(wr, p_mul(dr, Ub[r * S + r])));
+            }
+        }
+    }
+}
+__device__ void diag_class(const SectorHead &H, int cl, int b, int pass, const cd *u0, const cd *d, cd tau,
+                           double &fsum, cd &acc) {
+    switch (H.S[cl]) {
+    case 2: diag_blocks<2>(H, cl, b, pass, u0, d, tau, fsum, acc); break;
+    case 3: diag_blocks<3>(H, cl, b, pass, u0, d, tau, fsum, acc); break;
+    default: diag_blocks<4>(H, cl, b, pass, u0, d, tau, fsum, acc); break;
+    }
+}
+
+__global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int nb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char diag_smem[];
+    const grape::DevProblem &P = H.P;
+    const int b = blockIdx.x * kDiagBlock + threadIdx.x;
+    if (b >= nb) return;
+    cd *u0 = reinterpret_cast<cd *>(diag_smem) + (size_t)threadIdx.x * 2 * P.D, *d = u0 + P.D;
+    const double *xb = H.x + (size_t)b * P.nx;
+    grape::Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    target_diag(P, xb, none, u0);
+    double fsum = 0.0;
+    cd tau{0.0, 0.0};
+    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, cl, b, 0, u0, d, tau, fsum, tau);
+    for (int t = 0; t < H.nfixed; ++t) {  // U_gg = 1: K_gg = conj(u0_g)
+        const int g = H.fixed[t];
+        const cd k = p_conj(u0[g]);
+        fsum += P.W[g] * pdiag(P, g) * (k.re * k.re + k.im * k.im);
+        tau = p_add(tau, p_scale(P.W[g], k));
+    }
+    H.F[b] = (fsum + tau.re * tau.re + tau.im * tau.im) / P.DD;
+    double unused = 0.0;
+    cd unused_c{0.0, 0.0};
+    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, cl, b, 1, u0, d, tau, unused, unused_c);
+    for (int q = 0; q < P.na; ++q) {  // target part of F_dx_add
+        grape::Pert pq;
+        pq.var = grape::VAR_XADD;
+        pq.index = q;
+        pq.delta = P.eps;
+        target_diag(P, xb, pq, d);
+        for (int i = 0; i < P.D; ++i) d[i] = p_scale(P.inv_eps, p_sub(d[i], u0[i]));
+        double sa = 0.0;
+        cd trd{0.0, 0.0};
+        for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, cl, b, 2, u0, d, tau, sa, trd);
+        for (int t = 0; t < H.nfixed; ++t) {
+            const int g = H.fixed[t];
+            const cd kd = p_conj(d[g]), k = p_conj(u0[g]);
+            sa += P.W[g] * pdiag(P, g) * (kd.re * k.re + kd.im * k.im);
+            trd = p_add(trd, p_scale(P.W[g], kd));
+        }
+        const double val = (2.0 * sa + 2.0 * (tau.re * trd.re + tau.im * trd.im)) / P.DD;
+        if (P.xadd_dep && H.tgt_part) H.tgt_part[(size_t)b * P.na + q] = val;
+        else H.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = val;
+    }
+}
+
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st) {
+    if (H.diag) {
+        const size_t lds = (size_t)kDiagBlock * 2 * H.P.D * sizeof(cd);
+        hipLaunchKernelGGL(k_sec_head_diag, dim3((unsigned)((nb + kDiagBlock - 1) / kDiagBlock)), dim3(kDiagBlock), lds,
+                           st, H, nb);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)kHeadSlots * H.P.D * H.P.D * sizeof(cd);
     hipLaunchKernelGGL(k_sec_head, dim3((unsigned)nb), dim3(SEC_BLOCK), lds, st, H);
     return hipGetLastError();

@@ -56,6 +56,8 @@ struct SectorHead {
     const grape::cd *TotS[2]; // [nb * nsec][ne][S][S]
     grape::cd *MsecE[2];      // [nb * nsec][ne][S][S]  (written)
     double *Fd2, *Fd2dx;
+    int diag;                 // diagonal projector and target, sector classes of <= 4 levels: the
+                              // fidelity head runs one thread per evaluation on the sector blocks
 };
 constexpr int kSectorLds = 2048;  // complex elements of LDS for the sector blocks M_ww (nsec * S * S)
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st);

@@ -165,6 +165,7 @@ OPT_NO_SECTORS, OPT_NO_LANE, OPT_NO_CHAIN, OPT_NO_WALK, OPT_NO_GRAPH = 1, 2, 4, 
 OPT_WALK_RECOMPUTE = 32
 OPT_GENERAL_H0 = 64  # non-Hermitian H0: LU-inverted chain, fidelity from the materialised derivatives
 OPT_NO_FORK = 128  # every call on the plan's one stream (no auxiliary stream for the second sector class)
+OPT_GENERAL_HEAD = 256  # the general sector head even for a diagonal projector and target
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):

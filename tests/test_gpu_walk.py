@@ -251,3 +251,28 @@ def test_walk_propagator_modes_bitwise(name, fp):
             pl.close()
     for o in outs[1:]:
         assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
+
+
+@pytest.mark.parametrize("name,fp", [("full9", lambda: P.full9_problem(64)), ("sym5", lambda: P.sym_problem(40)),
+                                     ("fullblk7", lambda: P.fullblk_problem(40)),
+                                     ("c3", lambda: P.full9_problem(40, nerr=4))])
+def test_diagonal_head_matches_general_head(name, fp):
+    """Diagonal projector and target (every Rydberg CZ problem): the one-thread-per-evaluation sector
+    head (grape_projector.hip k_sec_head_diag) against the general d x d head (GRAPE_OPT_GENERAL_HEAD)
+    -- F, the target part of F_dx_add and, through M, every F_dx / F_d2err / F_d2err_dx entry, at the
+    rounding level of the two summation orders."""
+    from robustgrape_amd.operators import OPT_GENERAL_HEAD
+    f = fp()
+    nt = f.unitary_problem.ntimes
+    X = np.stack([P.random_x(nt, 4000 + s, small=(s % 2 == 0)) for s in range(130)])
+    outs = []
+    for opts in (0, OPT_GENERAL_HEAD):
+        pl = _plan(f, len(X), opts)
+        try:
+            outs.append(pl.fidelity_grad(X))
+        finally:
+            pl.close()
+    for a, b in zip(outs[0], outs[1]):
+        if a.size:
+            scale = max(float(np.max(np.abs(b))), 1e-300)
+            assert float(np.max(np.abs(a - b))) <= 1e-12 * scale + 1e-15, (name, float(np.max(np.abs(a - b))), scale)
