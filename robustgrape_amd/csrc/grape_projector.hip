@@ -468,12 +468,6 @@ __global__ __launch_bounds__(SEC_BLOCK) void k_sec_err_head(SectorHead H) {
 
 }  // namespace
 
-hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
-    if (H.P.ne == 0) return hipSuccess;
-    const size_t lds = (size_t)kErrHeadSlots * H.P.D * H.P.D * sizeof(cd);
-    hipLaunchKernelGGL(k_sec_err_head, dim3((unsigned)(nb * H.P.ne)), dim3(SEC_BLOCK), lds, st, H);
-    return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------
 // Diagonal projector and diagonal target (H.diag: the Rydberg CZ problems).  Every matrix of the
@@ -623,6 +617,153 @@ __global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int 
         if (P.xadd_dep && H.tgt_part) H.tgt_part[(size_t)b * P.na + q] = val;
         else H.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = val;
     }
+}
+
+// The error head in the same diagonal form, one thread per (evaluation, error source): with
+// Ue = U Tot (block-diagonal, zero on the untouched levels), Ke = U0^dag Ue and K = U0^dag U,
+// k_sec_err_head's products reduce to (A = diag(w), B = diag(p); FidelityCalculations.jl:78-113)
+//   te = sum_i w_i Ke_ii,  t1 = sum_ij w_i p_j |Ke_ij|^2,  t2 = sum_i w_i (Ue^dag Ue)_ii,
+//   F_d2err = 2 [t1 - (1 + D) t2 + |te|^2] / DD,
+//   M_e,ij = (2/DD) [2 p_i (Ke^dag W K)_ij + 2 conj(te) w_i K_ij - 2 (1 + D) w_i (Ue^dag U)_ij],
+//   target part of F_d2err_dx_add: 2 [2 sum_ij w_i p_j Re(conj(d_i) Ue_ij conj(Ke_ij))
+//                                     + 2 Re(conj(te) sum_i w_i conj(d_i) Ue_ii)] / DD.
+// pass 0: te, t1, t2; pass 1: the blocks of M_e; pass 2: the F_d2err_dx_add sums against d.
+template <int S>
+__device__ void diag_err_blocks(const SectorHead &H, int cl, int b, int e, int pass, const cd *u0, const cd *d, cd te,
+                                double &t1, double &t2, cd &acc) {
+    const grape::DevProblem &P = H.P;
+    const int ns = H.nsec[cl], ne = P.ne;
+    const double sc = 2.0 / P.DD;
+    for (int w = 0; w < ns; ++w) {
+        const size_t bw = (size_t)b * ns + w;
+        const cd *Ub = H.Ub[cl] + bw * S * S, *Tb = H.TotS[cl] + (bw * ne + e) * S * S;
+        int g[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) g[r] = H.sidx[cl][w * S + r];
+        cd Ue[S][S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+#pragma unroll
+            for (int c = 0; c < S; ++c) {
+                cd v{0.0, 0.0};
+#pragma unroll
+                for (int m = 0; m < S; ++m) v = p_add(v, p_mul(Ub[r * S + m], Tb[m * S + c]));
+                Ue[r][c] = (g[r] >= 0 && g[c] >= 0) ? v : cd{0.0, 0.0};
+            }
+        }
+        auto cu0 = [&](int r) { return p_conj(u0[g[r] >= 0 ? g[r] : 0]); };
+        if (pass == 0) {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                if (g[r] < 0) continue;
+                const double wr = P.W[g[r]];
+                double col = 0.0;  // (Ue^dag Ue)_rr
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    if (g[c] < 0) continue;
+                    const cd ke = p_mul(cu0(r), Ue[r][c]);
+                    t1 += wr * pdiag(P, g[c]) * (ke.re * ke.re + ke.im * ke.im);
+                    col += Ue[c][r].re * Ue[c][r].re + Ue[c][r].im * Ue[c][r].im;
+                }
+                t2 += wr * col;
+                acc = p_add(acc, p_scale(wr, p_mul(cu0(r), Ue[r][r])));
+            }
+        } else if (pass == 1) {
+            cd *dst = H.MsecE[cl] + (bw * ne + e) * S * S;
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    cd m{0.0, 0.0};
+                    if (g[r] >= 0 && g[c] >= 0) {
+                        cd kwk{0.0, 0.0}, uu{0.0, 0.0};  // (Ke^dag W K)_rc, (Ue^dag U)_rc
+#pragma unroll
+                        for (int k = 0; k < S; ++k) {
+                            if (g[k] < 0) continue;
+                            const cd kk = p_mul(cu0(k), Ub[k * S + c]), ke = p_mul(cu0(k), Ue[k][r]);
+                            kwk = p_add(kwk, p_scale(P.W[g[k]], p_mul(p_conj(ke), kk)));
+                            uu = p_add(uu, p_mul(p_conj(Ue[k][r]), Ub[k * S + c]));
+                        }
+                        const double wr = P.W[g[r]];
+                        const cd krc = p_mul(cu0(r), Ub[r * S + c]);
+                        m = p_add(p_scale(2.0 * pdiag(P, g[r]), kwk), p_scale(2.0 * wr, p_mul(cd{te.re, -te.im}, krc)));
+                        m = p_scale(sc, p_sub(m, p_scale(2.0 * (1.0 + P.Dtr) * wr, uu)));
+                    }
+                    dst[r * S + c] = m;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                if (g[r] < 0) continue;
+                const double wr = P.W[g[r]];
+                const cd dr = p_conj(d[g[r]]);
+#pragma unroll
+                for (int c = 0; c < S; ++c) {
+                    if (g[c] < 0) continue;
+                    const cd kde = p_mul(dr, Ue[r][c]), ke = p_mul(cu0(r), Ue[r][c]);
+                    t1 += wr * pdiag(P, g[c]) * (kde.re * ke.re + kde.im * ke.im);
+                }
+                acc = p_add(acc, p_scale(wr, p_mul(dr, Ue[r][r])));
+            }
+        }
+    }
+}
+__device__ void diag_err_class(const SectorHead &H, int cl, int b, int e, int pass, const cd *u0, const cd *d, cd te,
+                               double &t1, double &t2, cd &acc) {
+    switch (H.S[cl]) {
+    case 2: diag_err_blocks<2>(H, cl, b, e, pass, u0, d, te, t1, t2, acc); break;
+    case 3: diag_err_blocks<3>(H, cl, b, e, pass, u0, d, te, t1, t2, acc); break;
+    default: diag_err_blocks<4>(H, cl, b, e, pass, u0, d, te, t1, t2, acc); break;
+    }
+}
+
+__global__ __launch_bounds__(kDiagBlock) void k_sec_err_head_diag(SectorHead H, int nb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char diag_smem[];
+    const grape::DevProblem &P = H.P;
+    const int be = blockIdx.x * kDiagBlock + threadIdx.x;
+    if (be >= nb * P.ne) return;
+    const int b = be / P.ne, e = be - b * P.ne;
+    cd *u0 = reinterpret_cast<cd *>(diag_smem) + (size_t)threadIdx.x * 2 * P.D, *d = u0 + P.D;
+    const double *xb = H.x + (size_t)b * P.nx;
+    grape::Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    target_diag(P, xb, none, u0);
+    double t1 = 0.0, t2 = 0.0;
+    cd te{0.0, 0.0};
+    for (int cl = 0; cl < H.ncls; ++cl) diag_err_class(H, cl, b, e, 0, u0, d, te, t1, t2, te);
+    H.Fd2[be] = 2.0 * (t1 - (1.0 + P.Dtr) * t2 + te.re * te.re + te.im * te.im) / P.DD;
+    double u1 = 0.0, u2 = 0.0;
+    cd uc{0.0, 0.0};
+    for (int cl = 0; cl < H.ncls; ++cl) diag_err_class(H, cl, b, e, 1, u0, d, te, u1, u2, uc);
+    for (int q = 0; q < P.na; ++q) {  // target part of F_d2err_dx_add
+        grape::Pert pq;
+        pq.var = grape::VAR_XADD;
+        pq.index = q;
+        pq.delta = P.eps;
+        target_diag(P, xb, pq, d);
+        for (int i = 0; i < P.D; ++i) d[i] = p_scale(P.inv_eps, p_sub(d[i], u0[i]));
+        double sa = 0.0, unused = 0.0;
+        cd trd{0.0, 0.0};
+        for (int cl = 0; cl < H.ncls; ++cl) diag_err_class(H, cl, b, e, 2, u0, d, te, sa, unused, trd);
+        H.Fd2dx[(size_t)be * P.nx + (size_t)P.np * P.Nt + q] = 2.0 * (2.0 * sa + 2.0 * (te.re * trd.re + te.im * trd.im)) / P.DD;
+    }
+}
+
+hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
+    if (H.P.ne == 0) return hipSuccess;
+    if (H.diag) {
+        const int n = nb * H.P.ne;
+        const size_t lds = (size_t)kDiagBlock * 2 * H.P.D * sizeof(cd);
+        hipLaunchKernelGGL(k_sec_err_head_diag, dim3((unsigned)((n + kDiagBlock - 1) / kDiagBlock)), dim3(kDiagBlock),
+                           lds, st, H, nb);
+        return hipGetLastError();
+    }
+    const size_t lds = (size_t)kErrHeadSlots * H.P.D * H.P.D * sizeof(cd);
+    hipLaunchKernelGGL(k_sec_err_head, dim3((unsigned)(nb * H.P.ne)), dim3(SEC_BLOCK), lds, st, H);
+    return hipGetLastError();
 }
 
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st) {

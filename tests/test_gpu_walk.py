@@ -255,10 +255,13 @@ def test_walk_propagator_modes_bitwise(name, fp):
 
 @pytest.mark.parametrize("name,fp", [("full9", lambda: P.full9_problem(64)), ("sym5", lambda: P.sym_problem(40)),
                                      ("fullblk7", lambda: P.fullblk_problem(40)),
-                                     ("c3", lambda: P.full9_problem(40, nerr=4))])
+                                     ("c3", lambda: P.full9_problem(40, nerr=4)),
+                                     ("sym5-amp-freq", lambda: P.sym_problem(30, errors=("amp", "freq"))),
+                                     ("fullblk7-amp", lambda: P.fullblk_problem(30, errors=("amp",)))])
 def test_diagonal_head_matches_general_head(name, fp):
     """Diagonal projector and target (every Rydberg CZ problem): the one-thread-per-evaluation sector
-    head (grape_projector.hip k_sec_head_diag) against the general d x d head (GRAPE_OPT_GENERAL_HEAD)
+    heads (grape_projector.hip k_sec_head_diag, k_sec_err_head_diag) against the general d x d heads
+    (GRAPE_OPT_GENERAL_HEAD)
     -- F, the target part of F_dx_add and, through M, every F_dx / F_d2err / F_d2err_dx entry, at the
     rounding level of the two summation orders."""
     from robustgrape_amd.operators import OPT_GENERAL_HEAD
