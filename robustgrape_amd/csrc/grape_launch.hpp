@@ -212,10 +212,12 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                 return hipGetLastError();
             }
             if (stage == 1) {
-                mark(GRAPE_KERNEL_REDUCE, 0);
-                const long nmc = (long)B.nb * P.nchunks * D * D;
-                hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
-                mark(GRAPE_KERNEL_REDUCE, 1);
+                if (P.ne > 0) {  // k_img_fdx reads M'_c (k_walk_grad forms it in the lane)
+                    mark(GRAPE_KERNEL_REDUCE, 0);
+                    const long nmc = (long)B.nb * P.nchunks * D * D;
+                    hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
+                    mark(GRAPE_KERNEL_REDUCE, 1);
+                }
                 const int kid = P.ne > 0 ? GRAPE_KERNEL_GRAD : GRAPE_KERNEL_WALK_GRAD;  // k_img_fdx / k_walk_grad
                 mark(kid, 0);
                 const hipError_t e = grape_walk::launch<D>(1, P, B, st);

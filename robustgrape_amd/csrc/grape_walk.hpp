@@ -7,7 +7,7 @@
 //   k_walk_fwd   E_k = exp(A_k) and the chunk chain Q <- E_k Q, in registers; writes only
 //                the chunk total T_c (k_scan then scans the totals: B.Tc).
 //                                                     UnitaryCalculations.jl:45-47,99
-//   k_walk_grad  X = M'_c = Carry_c M Carry_c^dag (k_sec_mc) and per step
+//   k_walk_grad  X = M'_c = Carry_c M Carry_c^dag (formed in the lane) and per step
 //                  E_k again, Y_k = X E_k^dag, and for every gradient parameter u the
 //                  eps-variant E'_k contracted on the spot,
 //                  F_dx[u,k] = Re tr(Y_k (E'_k - E_k)/eps)    (FidelityCalculations.jl:56-76),
@@ -703,13 +703,29 @@ void k_walk_grad(DevProblem P, DevBatch B) {
             }
         }
     }
+    // X = M'_c = Carry_c M_ww Carry_c^dagger from the carry and the head's sector block (k_sec_mc's
+    // arithmetic, element by element: the same values, and one launch less per sector class)
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
-        const cd *mc = B.Mc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;
+        const size_t bw = (size_t)L.be * ns + L.w0 + w;
+        const cd *Cr = B.Carry + (bw * P.nchunks + L.c) * TS, *Mw = B.Msec + bw * TS;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
+            cd r[D];  // column j of M_ww Carry^dagger
 #pragma unroll
-            for (int i = 0; i < D; ++i) X[w].set(j, i, mc[j * D + i]);
+            for (int a = 0; a < D; ++a) {
+                cd v = czero();
+#pragma unroll
+                for (int e = 0; e < D; ++e) v = cadd(v, cmul(Mw[a * D + e], cconj(Cr[j * D + e])));
+                r[a] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                cd acc = czero();
+#pragma unroll
+                for (int a = 0; a < D; ++a) acc = cadd(acc, cmul(Cr[i * D + a], r[a]));
+                X[w].set(i, j, acc);
+            }
         }
     }
     WalkX XV;
