@@ -119,7 +119,7 @@ typedef struct grape_desc {
     const grape_term *target_terms;  /* may only use GRAPE_VAR_ONE / GRAPE_VAR_XADD */
     int32_t max_batch;  /* largest nbatch a single call will use (workspace sizing); <=0 -> 256 */
     int32_t reserved[5]; /* reserved[0]: flags (GRAPE_DESC_*); [1]: engine options (GRAPE_OPT_*, ABI 6);
-                          * [2]: k_scan width override (1, 4 or 8 waves; 0 = chosen by batch size, ABI 6);
+                          * [2]: k_scan width override (1, 4, 8 or 16 waves -- 16 for the chunk-walk classes only; 0 = chosen by batch size, ABI 6);
                           * the rest must be 0 */
     /* ABI 4: the full projector P0 (FidelityRobustGRAPEProblem.projector, Types.jl:54), ndim x ndim
      * complex, column-major, interleaved; any matrix, as FidelityCalculations.jl:47-51 accepts.

@@ -52,7 +52,7 @@ int fail(int code, const std::string &msg) {
     } while (0)
 
 constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow,
-              kScanTiny = grape_host::kScanTiny;
+              kScanTiny = grape_host::kScanTiny, kScanLatency = grape_host::kScanLatency;
 // calls of at most this many evaluations run the two sector classes on two streams (enqueue)
 constexpr int kForkMaxBatch = 4096;
 constexpr int kCtrlInts = 8;  // [0..1] single-eval counters, [2] status, [4..5] pipeline overflow counters
@@ -208,7 +208,10 @@ struct grape_plan {
         hipGraphExec_t exec;
     };
     std::vector<GraphEntry> graphs;
-    double *h_x = nullptr, *h_F = nullptr, *h_Fdx = nullptr, *h_Fd2 = nullptr, *h_Fd2dx = nullptr;  // pinned
+    double *h_x = nullptr, *h_F = nullptr, *h_Fd2 = nullptr, *h_Fd2dx = nullptr;  // pinned
+    // graph path: F ([kGraphBatch]) and F_dx ([nb][nx]) of a call side by side in one device block
+    // (h_F is its pinned image), so one D2H copy returns both
+    double *d_gout = nullptr;
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -242,7 +245,7 @@ static void free_plan(grape_plan *p) {
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
                     p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
-                    p->d_fixed};
+                    p->d_fixed, p->d_gout};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
@@ -257,7 +260,7 @@ static void free_plan(grape_plan *p) {
         (void)hipEventDestroy(pe.b);
     }
     for (auto &g : p->graphs) (void)hipGraphExecDestroy(g.exec);
-    for (double *h : {p->h_x, p->h_F, p->h_Fdx, p->h_Fd2, p->h_Fd2dx})
+    for (double *h : {p->h_x, p->h_F, p->h_Fd2, p->h_Fd2dx})
         if (h) (void)hipHostFree(h);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
@@ -822,7 +825,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             ncu = prop.multiProcessorCount;
     }
     P.opts = desc->reserved[1];
-    const int scan_override = desc->reserved[2];  // plan option: 1, 4 or 8 waves (0: by batch size)
+    const int scan_override = desc->reserved[2];  // plan option: 1, 4, 8 or 16 waves (0: by batch size)
     P.scan_waves = p->max_batch >= 2 * ncu ? kScanNarrow : kScanWide;
     if (scan_override == kScanNarrow || scan_override == kScanWide) P.scan_waves = scan_override;
     const int NG = P.scan_waves * (64 / D);
@@ -980,6 +983,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
             // 6.52 M evals/s; for the 2-level class it lost, 0.72 -> 1.01 ms per pass)
             Ps.walk_store_e = Ps.walk && P.ne == 0 && S == grape::kWalkMaxD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
+            // latency-bound walk classes (fewer sub-evaluations than CUs, or the option): 16-wave scans,
+            // half-length walks (grape_launch.hpp kScanLatency)
+            if (Ps.walk && P.ne == 0 &&
+                (scan_override == kScanLatency || (scan_override == 0 && (long)R < (long)ncu)))
+                Ps.scan_waves = kScanLatency;
             const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
@@ -1157,14 +1165,16 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.Tc = sb.Tc;  // chunk walks (null otherwise)
             B.wscr = sb.wscr;
             B.Ew = sb.Ew;
-            B.xT = p->d_xT;
+            B.xT = nb == 1 ? d_x : p->d_xT;  // one evaluation: x[q] is already [nx][1]
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
             sp.lane_major[cl] = p->Ps[cl].walk && p->P.ne == 0;  // k_walk_grad's layout (k_img_fdx: row layout)
             sp.part_err[cl] = sb.part_err;
         }
-        HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));
-        if (p->d_xT) {  // the walks read the controls transposed (one coalesced row per step)
+        bool parks = false;  // the chunk walks never park a step for k_expm_high: no counters to clear
+        for (int cl = 0; cl < p->ncls; ++cl) parks = parks || !p->Ps[cl].walk;
+        if (parks) HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));
+        if (p->d_xT && nb > 1) {  // the walks read the controls transposed (one coalesced row per step)
             mk(GRAPE_KERNEL_WALK_FWD, 0);
             HIPCHECK(grape_walk::transpose_x(d_x, p->d_xT, nb, p->P.nx, st));
             mk(GRAPE_KERNEL_WALK_FWD, 1);
@@ -1300,10 +1310,19 @@ static int enqueue_general(grape_plan *p, int nb, const double *d_x, double *d_F
 }
 
 // Enqueue one call's batch, then copy the status word to pinned memory on the plan's stream.
+// (Sector plans whose every class walks set no status bit -- no Pade solve, no parked step, no
+// LU -- and skip that copy.)
+static bool status_free(const grape_plan *p) {
+    if (!p->ncls || p->general_h0 || p->dense || p->tables) return false;
+    for (int cl = 0; cl < p->ncls; ++cl)
+        if (!p->Ps[cl].walk) return false;
+    return true;
+}
 static int enqueue_call(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
                         double *d_Fd2dx) {
     if (int rc = enqueue(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx)) return rc;
-    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+    if (!status_free(p))
+        HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return GRAPE_OK;
 }
 
@@ -1364,9 +1383,9 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     auto body = [&]() -> int {
         HIPCHECK(hipMemcpyAsync(p->d_x, p->h_x, (size_t)nb * nx * sizeof(double), hipMemcpyHostToDevice, st));
-        if (int rc = enqueue_call(p, nb, p->d_x, p->d_F, p->d_Fdx, p->d_Fd2, p->d_Fd2dx)) return rc;
-        HIPCHECK(hipMemcpyAsync(p->h_F, p->d_F, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(p->h_Fdx, p->d_Fdx, (size_t)nb * nx * sizeof(double), hipMemcpyDeviceToHost, st));
+        const size_t B = std::min(kGraphBatch, p->max_batch);
+        if (int rc = enqueue_call(p, nb, p->d_x, p->d_gout, p->d_gout + B, p->d_Fd2, p->d_Fd2dx)) return rc;
+        HIPCHECK(hipMemcpyAsync(p->h_F, p->d_gout, (B + (size_t)nb * nx) * sizeof(double), hipMemcpyDeviceToHost, st));
         if (ne > 0) {
             HIPCHECK(hipMemcpyAsync(p->h_Fd2, p->d_Fd2, (size_t)nb * ne * sizeof(double), hipMemcpyDeviceToHost, st));
             HIPCHECK(hipMemcpyAsync(p->h_Fd2dx, p->d_Fd2dx, (size_t)nb * ne * nx * sizeof(double),
@@ -1411,9 +1430,11 @@ static int fidelity_grad_graph(grape_plan *p, int nb, const double *x, double *F
             return hipHostMalloc(reinterpret_cast<void **>(h), std::max<size_t>(n, 1) * sizeof(double),
                                  hipHostMallocDefault) == hipSuccess;
         };
-        if (!pin(&p->h_x, B * nx) || !pin(&p->h_F, B) || !pin(&p->h_Fdx, B * nx) || !pin(&p->h_Fd2, B * ne) ||
+        if (!pin(&p->h_x, B * nx) || !pin(&p->h_F, B * (1 + nx)) || !pin(&p->h_Fd2, B * ne) ||
             !pin(&p->h_Fd2dx, B * ne * nx))
             return fail(GRAPE_ERR_ALLOC, "pinned allocation failed (graph path)");
+        if (dalloc(&p->d_gout, B * (1 + nx)) != hipSuccess)
+            return fail(GRAPE_ERR_ALLOC, "device allocation failed (graph path)");
     }
     hipGraphExec_t ex = nullptr;
     for (auto &g : p->graphs)
@@ -1424,7 +1445,7 @@ static int fidelity_grad_graph(grape_plan *p, int nb, const double *x, double *F
     HIPCHECK(hipGraphLaunch(ex, p->stream));
     if (int rc = grape_plan_synchronize(p)) return rc;
     std::memcpy(F, p->h_F, (size_t)nb * sizeof(double));
-    std::memcpy(F_dx, p->h_Fdx, (size_t)nb * nx * sizeof(double));
+    std::memcpy(F_dx, p->h_F + B, (size_t)nb * nx * sizeof(double));
     if (ne > 0) {
         std::memcpy(F_d2err, p->h_Fd2, (size_t)nb * ne * sizeof(double));
         std::memcpy(F_d2err_dx, p->h_Fd2dx, (size_t)nb * ne * nx * sizeof(double));

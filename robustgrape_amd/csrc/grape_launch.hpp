@@ -24,6 +24,11 @@ using grape::DevProblem;
 // Sector problems with many sub-evaluations per CU take W = 1: fewer chunks mean
 // fewer carries and per-chunk images to stream (C2 2.69 -> 2.80 M evals/s).
 constexpr int kScanWide = 8, kScanNarrow = 4, kScanTiny = 1;
+// Latency-bound calls (fewer sub-evaluations than CUs: single evaluations, C4's 32 restarts per
+// GPU, the optimiser's tail rounds) of the chunk-walk classes (<= kWalkMaxD levels, no error
+// sources) take 16-wave scans: twice the chunks of kScanWide, so each walk lane steps half as far
+// (L = 2 at 4 levels, L = 1 at 2 levels for N_t = 512).
+constexpr int kScanLatency = 16;
 
 // Lane-matrix exponentials (grape_lane.hpp k_expm_lane) for d <= kLaneMaxD (operator-basis
 // builders; closure tables keep k_expm_table); GRAPE_OPT_NO_LANE selects the row-group k_expm (A/B and
@@ -75,6 +80,13 @@ size_t scan_lds(int W) {
 // k_scan / k_err_scan at the plan's width (P.scan_waves: 1, 4 or 8 waves per workgroup)
 template <int D>
 void launch_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    if constexpr (D <= grape::kWalkMaxD) {
+        if (P.scan_waves == kScanLatency) {
+            hipLaunchKernelGGL((grape::k_scan<D, kScanLatency>), dim3(B.nb), dim3(64 * kScanLatency),
+                               scan_lds<D>(kScanLatency), st, P, B);
+            return;
+        }
+    }
     if (P.scan_waves == kScanTiny)
         hipLaunchKernelGGL((grape::k_scan<D, kScanTiny>), dim3(B.nb), dim3(64 * kScanTiny), scan_lds<D>(kScanTiny), st,
                            P, B);
@@ -389,6 +401,11 @@ hipError_t set_lds_limits_w() {
 template <int D>
 hipError_t set_lds_limits() {
     hipError_t e = set_lds_limits_w<D, kScanWide>();
+    if constexpr (D <= grape::kWalkMaxD) {
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, kScanLatency>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>(kScanLatency));
+    }
     if (e == hipSuccess) e = set_lds_limits_w<D, kScanNarrow>();
     return e != hipSuccess ? e : set_lds_limits_w<D, kScanTiny>();
 }

@@ -495,18 +495,69 @@ __device__ void target_diag(const grape::DevProblem &P, const double *xb, const 
 }
 __device__ __forceinline__ double pdiag(const grape::DevProblem &P, int g) { return P.W[g] != 0.0 ? 1.0 : 0.0; }
 
+// Staging.  A head thread used to chase ~45 dependent rounds of global loads (term records,
+// operator diagonals, weights, slot maps, its U blocks): 30 us for a one-evaluation call, 20 % of
+// the single-evaluation latency.  The workgroup now copies every table it reads and its
+// evaluations' U blocks and x_add values into LDS in one coalesced pass; the arithmetic is
+// unchanged (same operations in the same order: the same results, bit for bit).
+struct DiagLayout {
+    size_t terms, tdiag, W, sidx[2], fixed, xa, Ub[2], u, total;
+};
+__host__ __device__ inline DiagLayout diag_layout(const SectorHead &H) {
+    DiagLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += (bytes + 15) / 16 * 16;
+        return at;
+    };
+    const grape::DevProblem &P = H.P;
+    L.terms = take((size_t)P.n_tgt * sizeof(grape::Term));
+    L.tdiag = take((size_t)P.n_tgt * P.D * sizeof(cd));
+    L.W = take((size_t)P.D * sizeof(double));
+    for (int cl = 0; cl < 2; ++cl) L.sidx[cl] = take(cl < H.ncls ? (size_t)H.nsec[cl] * H.S[cl] * sizeof(int) : 0);
+    L.fixed = take((size_t)H.nfixed * sizeof(int));
+    L.xa = take((size_t)kDiagBlock * P.na * sizeof(double));
+    for (int cl = 0; cl < 2; ++cl)
+        L.Ub[cl] = take(cl < H.ncls ? (size_t)kDiagBlock * H.nsec[cl] * H.S[cl] * H.S[cl] * sizeof(cd) : 0);
+    L.u = take((size_t)kDiagBlock * 2 * P.D * sizeof(cd));
+    L.total = o;
+    return L;
+}
+struct DiagStage {  // the workgroup's LDS copies
+    const grape::Term *terms;  // [n_tgt]
+    const cd *tdiag;           // [n_tgt][D]: the diagonal of each target operator
+    const double *W;           // [D]
+    const int *sidx[2];        // [nsec][S]
+    const int *fixed;          // [nfixed]
+    const cd *Ub[2];           // [kDiagBlock * nsec][S][S] (this workgroup's evaluations)
+};
+// u[i] = diagonal of the target at x_add (perturbed by pp); target_diag's operations
+__device__ void target_diag_st(const grape::DevProblem &P, const DiagStage &St, const double *xb, const double *xadd,
+                               const grape::Pert &pp, cd *u) {
+    for (int i = 0; i < P.D; ++i) u[i] = cd{0.0, 0.0};
+    for (int q = 0; q < P.n_tgt; ++q) {
+        const grape::Term tm = St.terms[q];
+        const cd c = grape::term_coef(tm, 1, xb, xadd, pp);
+        const cd *od = St.tdiag + (size_t)q * P.D;
+        for (int i = 0; i < P.D; ++i) u[i] = p_add(u[i], p_mul(c, od[i]));
+    }
+}
+
 // pass 0: F's sum and tau; pass 1: the blocks M_ww; pass 2: the F_dx_add sums against d
+// (t: the thread's evaluation within the workgroup, b = b0 + t)
 template <int S>
-__device__ void diag_blocks(const SectorHead &H, int cl, int b, int pass, const cd *u0, const cd *d, cd tau,
-                            double &fsum, cd &acc) {
+__device__ void diag_blocks(const SectorHead &H, const DiagStage &St, int cl, int t, size_t b, int pass, const cd *u0,
+                            const cd *d, cd tau, double &fsum, cd &acc) {
     const grape::DevProblem &P = H.P;
     const int ns = H.nsec[cl];
     const double sc = 2.0 / P.DD;
+    auto pd = [&](int g) { return St.W[g] != 0.0 ? 1.0 : 0.0; };
     for (int w = 0; w < ns; ++w) {
-        const cd *Ub = H.Ub[cl] + ((size_t)b * ns + w) * S * S;
+        const cd *Ub = St.Ub[cl] + ((size_t)t * ns + w) * S * S;
         int g[S];
 #pragma unroll
-        for (int r = 0; r < S; ++r) g[r] = H.sidx[cl][w * S + r];
+        for (int r = 0; r < S; ++r) g[r] = St.sidx[cl][w * S + r];
         cd K[S][S];
 #pragma unroll
         for (int r = 0; r < S; ++r) {
@@ -520,16 +571,16 @@ __device__ void diag_blocks(const SectorHead &H, int cl, int b, int pass, const 
 #pragma unroll
             for (int r = 0; r < S; ++r) {
                 if (g[r] < 0) continue;
-                const double wr = P.W[g[r]];
+                const double wr = St.W[g[r]];
 #pragma unroll
                 for (int c = 0; c < S; ++c) {
                     if (g[c] < 0) continue;
-                    fsum += wr * pdiag(P, g[c]) * (K[r][c].re * K[r][c].re + K[r][c].im * K[r][c].im);
+                    fsum += wr * pd(g[c]) * (K[r][c].re * K[r][c].re + K[r][c].im * K[r][c].im);
                 }
                 acc = p_add(acc, p_scale(wr, K[r][r]));
             }
         } else if (pass == 1) {
-            cd *dst = H.Msec[cl] + ((size_t)b * ns + w) * S * S;
+            cd *dst = H.Msec[cl] + (b * ns + w) * S * S;
 #pragma unroll
             for (int r = 0; r < S; ++r) {
 #pragma unroll
@@ -539,9 +590,9 @@ __device__ void diag_blocks(const SectorHead &H, int cl, int b, int pass, const 
                         cd s{0.0, 0.0};
 #pragma unroll
                         for (int k = 0; k < S; ++k)
-                            if (g[k] >= 0) s = p_add(s, p_scale(P.W[g[k]], p_mul(p_conj(K[k][r]), K[k][c])));
-                        m = p_scale(sc, p_add(p_scale(pdiag(P, g[r]), s),
-                                              p_scale(P.W[g[r]], p_mul(cd{tau.re, -tau.im}, K[r][c]))));
+                            if (g[k] >= 0) s = p_add(s, p_scale(St.W[g[k]], p_mul(p_conj(K[k][r]), K[k][c])));
+                        m = p_scale(sc, p_add(p_scale(pd(g[r]), s),
+                                              p_scale(St.W[g[r]], p_mul(cd{tau.re, -tau.im}, K[r][c]))));
                     }
                     dst[r * S + c] = m;
                 }
@@ -550,72 +601,114 @@ __device__ void diag_blocks(const SectorHead &H, int cl, int b, int pass, const 
 #pragma unroll
             for (int r = 0; r < S; ++r) {
                 if (g[r] < 0) continue;
-                const double wr = P.W[g[r]];
+                const double wr = St.W[g[r]];
                 const cd dr = p_conj(d[g[r]]);
 #pragma unroll
                 for (int c = 0; c < S; ++c) {
                     if (g[c] < 0) continue;
                     const cd kd = p_mul(dr, Ub[r * S + c]);  // Kd_rc
-                    fsum += wr * pdiag(P, g[c]) * (kd.re * K[r][c].re + kd.im * K[r][c].im);
+                    fsum += wr * pd(g[c]) * (kd.re * K[r][c].re + kd.im * K[r][c].im);
                 }
                 acc = p_add(acc, p_scale(wr, p_mul(dr, Ub[r * S + r])));
             }
         }
     }
 }
-__device__ void diag_class(const SectorHead &H, int cl, int b, int pass, const cd *u0, const cd *d, cd tau,
-                           double &fsum, cd &acc) {
+__device__ void diag_class(const SectorHead &H, const DiagStage &St, int cl, int t, size_t b, int pass, const cd *u0,
+                           const cd *d, cd tau, double &fsum, cd &acc) {
     switch (H.S[cl]) {
-    case 2: diag_blocks<2>(H, cl, b, pass, u0, d, tau, fsum, acc); break;
-    case 3: diag_blocks<3>(H, cl, b, pass, u0, d, tau, fsum, acc); break;
-    default: diag_blocks<4>(H, cl, b, pass, u0, d, tau, fsum, acc); break;
+    case 2: diag_blocks<2>(H, St, cl, t, b, pass, u0, d, tau, fsum, acc); break;
+    case 3: diag_blocks<3>(H, St, cl, t, b, pass, u0, d, tau, fsum, acc); break;
+    default: diag_blocks<4>(H, St, cl, t, b, pass, u0, d, tau, fsum, acc); break;
     }
 }
 
 __global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int nb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char diag_smem[];
     const grape::DevProblem &P = H.P;
-    const int b = blockIdx.x * kDiagBlock + threadIdx.x;
-    if (b >= nb) return;
-    cd *u0 = reinterpret_cast<cd *>(diag_smem) + (size_t)threadIdx.x * 2 * P.D, *d = u0 + P.D;
-    const double *xb = H.x + (size_t)b * P.nx;
+    const DiagLayout Lo = diag_layout(H);
+    const int t = threadIdx.x, b0 = blockIdx.x * kDiagBlock, nloc = min(kDiagBlock, nb - b0);
+    // stage (every thread of the workgroup; coalesced where the source is contiguous)
+    {
+        grape::Term *terms = reinterpret_cast<grape::Term *>(diag_smem + Lo.terms);
+        cd *tdiag = reinterpret_cast<cd *>(diag_smem + Lo.tdiag);
+        const int nti = P.n_tgt * (int)(sizeof(grape::Term) / sizeof(int));
+        for (int i = t; i < nti; i += kDiagBlock)
+            reinterpret_cast<int *>(terms)[i] = reinterpret_cast<const int *>(P.tgt)[i];
+        for (int i = t; i < P.n_tgt * P.D; i += kDiagBlock) {
+            const int q = i / P.D, j = i - q * P.D;
+            tdiag[i] = P.ops[((size_t)P.tgt[q].op * P.D + j) * P.D + j];
+        }
+        double *W = reinterpret_cast<double *>(diag_smem + Lo.W);
+        for (int i = t; i < P.D; i += kDiagBlock) W[i] = P.W[i];
+        for (int cl = 0; cl < H.ncls; ++cl) {
+            int *sx = reinterpret_cast<int *>(diag_smem + Lo.sidx[cl]);
+            for (int i = t; i < H.nsec[cl] * H.S[cl]; i += kDiagBlock) sx[i] = H.sidx[cl][i];
+            const size_t SS = (size_t)H.S[cl] * H.S[cl], n = (size_t)nloc * H.nsec[cl] * SS;
+            const cd *src = H.Ub[cl] + (size_t)b0 * H.nsec[cl] * SS;
+            cd *ub = reinterpret_cast<cd *>(diag_smem + Lo.Ub[cl]);
+            for (size_t i = t; i < n; i += kDiagBlock) ub[i] = src[i];
+        }
+        int *fx = reinterpret_cast<int *>(diag_smem + Lo.fixed);
+        for (int i = t; i < H.nfixed; i += kDiagBlock) fx[i] = H.fixed[i];
+        double *xa = reinterpret_cast<double *>(diag_smem + Lo.xa);
+        for (int i = t; i < nloc * P.na; i += kDiagBlock) {
+            const int l = i / P.na, q = i - l * P.na;
+            xa[i] = H.x[(size_t)(b0 + l) * P.nx + (size_t)P.np * P.Nt + q];
+        }
+    }
+    __syncthreads();
+    if (t >= nloc) return;
+    DiagStage St;
+    St.terms = reinterpret_cast<const grape::Term *>(diag_smem + Lo.terms);
+    St.tdiag = reinterpret_cast<const cd *>(diag_smem + Lo.tdiag);
+    St.W = reinterpret_cast<const double *>(diag_smem + Lo.W);
+    St.fixed = reinterpret_cast<const int *>(diag_smem + Lo.fixed);
+    for (int cl = 0; cl < 2; ++cl) {
+        St.sidx[cl] = reinterpret_cast<const int *>(diag_smem + Lo.sidx[cl]);
+        St.Ub[cl] = reinterpret_cast<const cd *>(diag_smem + Lo.Ub[cl]);
+    }
+    const size_t b = (size_t)b0 + t;
+    cd *u0 = reinterpret_cast<cd *>(diag_smem + Lo.u) + (size_t)t * 2 * P.D, *d = u0 + P.D;
+    const double *xb = H.x + b * P.nx;
+    const double *xadd = reinterpret_cast<const double *>(diag_smem + Lo.xa) + (size_t)t * P.na;
     grape::Pert none;
     none.var = -1;
     none.index = 0;
     none.delta = 0.0;
-    target_diag(P, xb, none, u0);
+    target_diag_st(P, St, xb, xadd, none, u0);
     double fsum = 0.0;
     cd tau{0.0, 0.0};
-    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, cl, b, 0, u0, d, tau, fsum, tau);
-    for (int t = 0; t < H.nfixed; ++t) {  // U_gg = 1: K_gg = conj(u0_g)
-        const int g = H.fixed[t];
+    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, St, cl, t, b, 0, u0, d, tau, fsum, tau);
+    for (int q = 0; q < H.nfixed; ++q) {  // U_gg = 1: K_gg = conj(u0_g)
+        const int g = St.fixed[q];
         const cd k = p_conj(u0[g]);
-        fsum += P.W[g] * pdiag(P, g) * (k.re * k.re + k.im * k.im);
-        tau = p_add(tau, p_scale(P.W[g], k));
+        fsum += St.W[g] * (St.W[g] != 0.0 ? 1.0 : 0.0) * (k.re * k.re + k.im * k.im);
+        tau = p_add(tau, p_scale(St.W[g], k));
     }
     H.F[b] = (fsum + tau.re * tau.re + tau.im * tau.im) / P.DD;
     double unused = 0.0;
     cd unused_c{0.0, 0.0};
-    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, cl, b, 1, u0, d, tau, unused, unused_c);
+    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, St, cl, t, b, 1, u0, d, tau, unused, unused_c);
     for (int q = 0; q < P.na; ++q) {  // target part of F_dx_add
         grape::Pert pq;
         pq.var = grape::VAR_XADD;
         pq.index = q;
         pq.delta = P.eps;
-        target_diag(P, xb, pq, d);
+        target_diag_st(P, St, xb, xadd, pq, d);
         for (int i = 0; i < P.D; ++i) d[i] = p_scale(P.inv_eps, p_sub(d[i], u0[i]));
         double sa = 0.0;
         cd trd{0.0, 0.0};
-        for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, cl, b, 2, u0, d, tau, sa, trd);
-        for (int t = 0; t < H.nfixed; ++t) {
-            const int g = H.fixed[t];
+        for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, St, cl, t, b, 2, u0, d, tau, sa, trd);
+        for (int r = 0; r < H.nfixed; ++r) {
+            const int g = St.fixed[r];
             const cd kd = p_conj(d[g]), k = p_conj(u0[g]);
-            sa += P.W[g] * pdiag(P, g) * (kd.re * k.re + kd.im * k.im);
-            trd = p_add(trd, p_scale(P.W[g], kd));
+            sa += St.W[g] * (St.W[g] != 0.0 ? 1.0 : 0.0) * (kd.re * k.re + kd.im * k.im);
+            trd = p_add(trd, p_scale(St.W[g], kd));
         }
         const double val = (2.0 * sa + 2.0 * (tau.re * trd.re + tau.im * trd.im)) / P.DD;
-        if (P.xadd_dep && H.tgt_part) H.tgt_part[(size_t)b * P.na + q] = val;
-        else H.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] = val;
+        if (P.xadd_dep && H.tgt_part) H.tgt_part[b * P.na + q] = val;
+        else H.Fdx[b * P.nx + (size_t)P.np * P.Nt + q] = val;
     }
 }
 
@@ -768,7 +861,7 @@ hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
 
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st) {
     if (H.diag) {
-        const size_t lds = (size_t)kDiagBlock * 2 * H.P.D * sizeof(cd);
+        const size_t lds = diag_layout(H).total;
         hipLaunchKernelGGL(k_sec_head_diag, dim3((unsigned)((nb + kDiagBlock - 1) / kDiagBlock)), dim3(kDiagBlock), lds,
                            st, H, nb);
         return hipGetLastError();

@@ -169,8 +169,8 @@ OPT_GENERAL_HEAD = 256  # the general sector head even for a diagonal projector 
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):
-    if scan_waves not in (0, 1, 4, 8):
-        raise ValueError("scan_waves must be 0 (by batch size), 1, 4 or 8")
+    if scan_waves not in (0, 1, 4, 8, 16):
+        raise ValueError("scan_waves must be 0 (by batch size), 1, 4, 8 or 16 (chunk-walk classes only)")
     return (ctypes.c_int32 * 5)(int(flags), int(options), int(scan_waves), 0, 0)
 
 

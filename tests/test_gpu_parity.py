@@ -244,10 +244,12 @@ def test_error_batch_matches_single():
         assert np.array_equal(d2s, d2[b]) and np.array_equal(d2dxs, d2dx[b])
 
 
-@pytest.mark.parametrize("waves", [1, 4, 8])
+@pytest.mark.parametrize("waves", [1, 4, 8, 16])
 def test_scan_widths_match_golden(waves):
-    """Every k_scan / k_err_scan width (the plan picks 1 or 4 waves for large batches): C2 golden
-    and the C3 (4 error sources) golden through a plan forced to each width."""
+    """Every k_scan / k_err_scan width (the plan picks 1 or 4 waves for large batches, 16 for the
+    latency-bound chunk walks): C2 golden and the C3 (4 error sources) golden through a plan
+    forced to each width (16 applies to the walk classes without error sources; C3 keeps its
+    batch-size choice)."""
     from robustgrape_amd.engine import GrapePlan
     g = _golden("c2")
     plan = GrapePlan(P.full9_problem(512), nparam=1, max_batch=8, scan_waves=waves)
