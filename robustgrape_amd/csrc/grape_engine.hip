@@ -950,7 +950,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         // diagonal projector and target, classes of <= 4 levels: the one-thread-per-evaluation head
         // (grape_projector.hip k_sec_head_diag)
         H.diag = !ps.general && !tables && !(P.opts & GRAPE_OPT_GENERAL_HEAD);
-        for (const SectorClass &sc : ss.cls) H.diag = H.diag && sc.S <= 4;
+        int rows = 0;  // the row-parallel head's lanes per evaluation (grape_projector.hip diag_group)
+        for (const SectorClass &sc : ss.cls) {
+            H.diag = H.diag && sc.S <= 4;
+            rows += sc.nsec * sc.S;
+        }
+        H.diag = H.diag && rows <= 32;
         for (int k = 0; H.diag && k < desc->n_target_terms; ++k) {
             const double *op = desc->ops + 2 * (size_t)desc->target_terms[k].op * D * D;
             for (int i = 0; i < D; ++i)

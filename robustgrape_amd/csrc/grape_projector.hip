@@ -495,16 +495,33 @@ __device__ void target_diag(const grape::DevProblem &P, const double *xb, const 
 }
 __device__ __forceinline__ double pdiag(const grape::DevProblem &P, int g) { return P.W[g] != 0.0 ? 1.0 : 0.0; }
 
-// Staging.  A head thread used to chase ~45 dependent rounds of global loads (term records,
-// operator diagonals, weights, slot maps, its U blocks): 30 us for a one-evaluation call, 20 % of
-// the single-evaluation latency.  The workgroup now copies every table it reads and its
-// evaluations' U blocks and x_add values into LDS in one coalesced pass; the arithmetic is
-// unchanged (same operations in the same order: the same results, bit for bit).
+// Row-parallel form (latency).  One thread per evaluation spent 25-30 us on a one-evaluation call:
+// ~3 k dependent FP64 operations and ~100 dependent LDS / global loads in a single lane.  Now a
+// GROUP of G lanes serves one evaluation (G = the sector rows sum_c nsec_c S_c rounded up to a
+// power of two: 8 at C2), lane r one row of one sector block; the row sums of F, tau and the
+// F_dx_add terms meet in a shuffle tree (fixed order: deterministic), and each lane writes its
+// row of M_ww.  The workgroup first copies every table it reads and its evaluations' U blocks and
+// x_add values into LDS in one coalesced pass.  Per element the operations are diag_blocks's of
+// round 3's first cut (the same K, M and target entries); only the order of the sums over rows
+// changed.
+__host__ __device__ inline int diag_rows(const SectorHead &H) {
+    int n = 0;
+    for (int cl = 0; cl < H.ncls; ++cl) n += H.nsec[cl] * H.S[cl];
+    return n;
+}
+__host__ __device__ inline int diag_group(const SectorHead &H) {
+    int g = 1;
+    while (g < diag_rows(H)) g <<= 1;
+    return g;
+}
 struct DiagLayout {
-    size_t terms, tdiag, W, sidx[2], fixed, xa, Ub[2], u, total;
+    size_t terms, tdiag, W, sidx[2], fixed, xa, Ub[2], u, cq, total;
+    int G, EB;  // lanes per evaluation, evaluations per workgroup
 };
 __host__ __device__ inline DiagLayout diag_layout(const SectorHead &H) {
     DiagLayout L{};
+    L.G = diag_group(H);
+    L.EB = kDiagBlock / L.G;
     size_t o = 0;
     auto take = [&](size_t bytes) {
         const size_t at = o;
@@ -517,10 +534,11 @@ __host__ __device__ inline DiagLayout diag_layout(const SectorHead &H) {
     L.W = take((size_t)P.D * sizeof(double));
     for (int cl = 0; cl < 2; ++cl) L.sidx[cl] = take(cl < H.ncls ? (size_t)H.nsec[cl] * H.S[cl] * sizeof(int) : 0);
     L.fixed = take((size_t)H.nfixed * sizeof(int));
-    L.xa = take((size_t)kDiagBlock * P.na * sizeof(double));
+    L.xa = take((size_t)L.EB * P.na * sizeof(double));
     for (int cl = 0; cl < 2; ++cl)
-        L.Ub[cl] = take(cl < H.ncls ? (size_t)kDiagBlock * H.nsec[cl] * H.S[cl] * H.S[cl] * sizeof(cd) : 0);
-    L.u = take((size_t)kDiagBlock * 2 * P.D * sizeof(cd));
+        L.Ub[cl] = take(cl < H.ncls ? (size_t)L.EB * H.nsec[cl] * H.S[cl] * H.S[cl] * sizeof(cd) : 0);
+    L.u = take((size_t)L.EB * 2 * P.D * sizeof(cd));
+    L.cq = take((size_t)L.EB * P.n_tgt * sizeof(cd));
     L.total = o;
     return L;
 }
@@ -528,98 +546,97 @@ struct DiagStage {  // the workgroup's LDS copies
     const grape::Term *terms;  // [n_tgt]
     const cd *tdiag;           // [n_tgt][D]: the diagonal of each target operator
     const double *W;           // [D]
-    const int *sidx[2];        // [nsec][S]
+    const int *sidx0, *sidx1;  // [nsec][S] of each class
     const int *fixed;          // [nfixed]
-    const cd *Ub[2];           // [kDiagBlock * nsec][S][S] (this workgroup's evaluations)
+    const cd *Ub0, *Ub1;       // [EB * nsec][S][S] of each class (this workgroup's evaluations)
+    // (named fields, picked by value: an array indexed by the class would live in scratch)
+    __device__ __forceinline__ const int *sidx(int cl) const { return cl == 0 ? sidx0 : sidx1; }
+    __device__ __forceinline__ const cd *Ub(int cl) const { return cl == 0 ? Ub0 : Ub1; }
 };
-// u[i] = diagonal of the target at x_add (perturbed by pp); target_diag's operations
-__device__ void target_diag_st(const grape::DevProblem &P, const DiagStage &St, const double *xb, const double *xadd,
-                               const grape::Pert &pp, cd *u) {
-    for (int i = 0; i < P.D; ++i) u[i] = cd{0.0, 0.0};
-    for (int q = 0; q < P.n_tgt; ++q) {
-        const grape::Term tm = St.terms[q];
-        const cd c = grape::term_coef(tm, 1, xb, xadd, pp);
-        const cd *od = St.tdiag + (size_t)q * P.D;
-        for (int i = 0; i < P.D; ++i) u[i] = p_add(u[i], p_mul(c, od[i]));
-    }
+// entry i of the target's diagonal from the term coefficients cq (target_diag's operations)
+__device__ __forceinline__ cd target_entry(const grape::DevProblem &P, const DiagStage &St, const cd *cq, int i) {
+    cd u{0.0, 0.0};
+    for (int q = 0; q < P.n_tgt; ++q) u = p_add(u, p_mul(cq[q], St.tdiag[(size_t)q * P.D + i]));
+    return u;
+}
+// group sum over G lanes (fixed tree)
+__device__ __forceinline__ double group_add(double v, int G) {
+    for (int o = G >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o, G);
+    return v;
 }
 
-// pass 0: F's sum and tau; pass 1: the blocks M_ww; pass 2: the F_dx_add sums against d
-// (t: the thread's evaluation within the workgroup, b = b0 + t)
+// Row r of sector block w of class cl (S levels) of the thread's evaluation (el in the workgroup):
+// pass 0: F's row sum and tau's term; pass 1: row r of M_ww; pass 2: the F_dx_add row terms against d
 template <int S>
-__device__ void diag_blocks(const SectorHead &H, const DiagStage &St, int cl, int t, size_t b, int pass, const cd *u0,
-                            const cd *d, cd tau, double &fsum, cd &acc) {
+__device__ __forceinline__ void diag_row(const SectorHead &H, const DiagStage &St, int cl, int w, int r, int el, size_t b, int pass,
+                         const cd *u0, const cd *d, cd tau, double &fsum, cd &acc) {
     const grape::DevProblem &P = H.P;
     const int ns = H.nsec[cl];
     const double sc = 2.0 / P.DD;
     auto pd = [&](int g) { return St.W[g] != 0.0 ? 1.0 : 0.0; };
-    for (int w = 0; w < ns; ++w) {
-        const cd *Ub = St.Ub[cl] + ((size_t)t * ns + w) * S * S;
-        int g[S];
+    const cd *Ub = St.Ub(cl) + ((size_t)el * ns + w) * S * S;
+    int g[S];
 #pragma unroll
-        for (int r = 0; r < S; ++r) g[r] = St.sidx[cl][w * S + r];
-        cd K[S][S];
+    for (int k = 0; k < S; ++k) g[k] = St.sidx(cl)[w * S + k];
+    const int gr = St.sidx(cl)[w * S + r];
+    // K_kc = conj(u0_{g_k}) U_kc (zero on padding slots)
+    auto Kel = [&](int k, int gk, int c, int gc) -> cd {
+        return (gk >= 0 && gc >= 0) ? p_mul(p_conj(u0[gk >= 0 ? gk : 0]), Ub[k * S + c]) : cd{0.0, 0.0};
+    };
+    if (pass == 0) {
+        if (gr < 0) return;
+        const double wr = St.W[gr];
 #pragma unroll
-        for (int r = 0; r < S; ++r) {
-#pragma unroll
-            for (int c = 0; c < S; ++c) {
-                const bool ok = g[r] >= 0 && g[c] >= 0;
-                K[r][c] = ok ? p_mul(p_conj(u0[g[r] >= 0 ? g[r] : 0]), Ub[r * S + c]) : cd{0.0, 0.0};
-            }
+        for (int c = 0; c < S; ++c) {
+            if (g[c] < 0) continue;
+            const cd K = Kel(r, gr, c, g[c]);
+            fsum += wr * pd(g[c]) * (K.re * K.re + K.im * K.im);
         }
-        if (pass == 0) {
+        acc = p_add(acc, p_scale(wr, Kel(r, gr, r, gr)));
+    } else if (pass == 1) {
+        cd *dst = H.Msec[cl] + (b * ns + w) * S * S + (size_t)r * S;
+        cd Kr[S];  // column r of K
 #pragma unroll
-            for (int r = 0; r < S; ++r) {
-                if (g[r] < 0) continue;
-                const double wr = St.W[g[r]];
+        for (int k = 0; k < S; ++k) Kr[k] = Kel(k, g[k], r, gr);
 #pragma unroll
-                for (int c = 0; c < S; ++c) {
-                    if (g[c] < 0) continue;
-                    fsum += wr * pd(g[c]) * (K[r][c].re * K[r][c].re + K[r][c].im * K[r][c].im);
-                }
-                acc = p_add(acc, p_scale(wr, K[r][r]));
+        for (int c = 0; c < S; ++c) {
+            cd m{0.0, 0.0};
+            if (gr >= 0 && g[c] >= 0) {
+                cd s{0.0, 0.0};
+#pragma unroll
+                for (int k = 0; k < S; ++k)
+                    if (g[k] >= 0) s = p_add(s, p_scale(St.W[g[k]], p_mul(p_conj(Kr[k]), Kel(k, g[k], c, g[c]))));
+                m = p_scale(sc, p_add(p_scale(pd(gr), s), p_scale(St.W[gr], p_mul(cd{tau.re, -tau.im}, Kel(r, gr, c, g[c])))));
             }
-        } else if (pass == 1) {
-            cd *dst = H.Msec[cl] + (b * ns + w) * S * S;
-#pragma unroll
-            for (int r = 0; r < S; ++r) {
-#pragma unroll
-                for (int c = 0; c < S; ++c) {
-                    cd m{0.0, 0.0};
-                    if (g[r] >= 0 && g[c] >= 0) {
-                        cd s{0.0, 0.0};
-#pragma unroll
-                        for (int k = 0; k < S; ++k)
-                            if (g[k] >= 0) s = p_add(s, p_scale(St.W[g[k]], p_mul(p_conj(K[k][r]), K[k][c])));
-                        m = p_scale(sc, p_add(p_scale(pd(g[r]), s),
-                                              p_scale(St.W[g[r]], p_mul(cd{tau.re, -tau.im}, K[r][c]))));
-                    }
-                    dst[r * S + c] = m;
-                }
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < S; ++r) {
-                if (g[r] < 0) continue;
-                const double wr = St.W[g[r]];
-                const cd dr = p_conj(d[g[r]]);
-#pragma unroll
-                for (int c = 0; c < S; ++c) {
-                    if (g[c] < 0) continue;
-                    const cd kd = p_mul(dr, Ub[r * S + c]);  // Kd_rc
-                    fsum += wr * pd(g[c]) * (kd.re * K[r][c].re + kd.im * K[r][c].im);
-                }
-                acc = p_add(acc, p_scale(wr, p_mul(dr, Ub[r * S + r])));
-            }
+            dst[c] = m;
         }
+    } else {
+        if (gr < 0) return;
+        const double wr = St.W[gr];
+        const cd dr = p_conj(d[gr]);
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            if (g[c] < 0) continue;
+            const cd kd = p_mul(dr, Ub[r * S + c]);  // Kd_rc
+            const cd K = Kel(r, gr, c, g[c]);
+            fsum += wr * pd(g[c]) * (kd.re * K.re + kd.im * K.im);
+        }
+        acc = p_add(acc, p_scale(wr, p_mul(dr, Ub[r * S + r])));
     }
 }
-__device__ void diag_class(const SectorHead &H, const DiagStage &St, int cl, int t, size_t b, int pass, const cd *u0,
-                           const cd *d, cd tau, double &fsum, cd &acc) {
-    switch (H.S[cl]) {
-    case 2: diag_blocks<2>(H, St, cl, t, b, pass, u0, d, tau, fsum, acc); break;
-    case 3: diag_blocks<3>(H, St, cl, t, b, pass, u0, d, tau, fsum, acc); break;
-    default: diag_blocks<4>(H, St, cl, t, b, pass, u0, d, tau, fsum, acc); break;
+__device__ __forceinline__ void diag_row_any(const SectorHead &H, const DiagStage &St, int row, int el, size_t b, int pass,
+                             const cd *u0, const cd *d, cd tau, double &fsum, cd &acc) {
+    int cl = 0;
+    if (row >= H.nsec[0] * H.S[0]) {
+        row -= H.nsec[0] * H.S[0];
+        cl = 1;
+        if (cl >= H.ncls || row >= H.nsec[1] * H.S[1]) return;  // padding lane of the group
+    }
+    const int S = H.S[cl], w = row / S, r = row - w * S;
+    switch (S) {
+    case 2: diag_row<2>(H, St, cl, w, r, el, b, pass, u0, d, tau, fsum, acc); break;
+    case 3: diag_row<3>(H, St, cl, w, r, el, b, pass, u0, d, tau, fsum, acc); break;
+    default: diag_row<4>(H, St, cl, w, r, el, b, pass, u0, d, tau, fsum, acc); break;
     }
 }
 
@@ -627,7 +644,9 @@ __global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int 
     extern __shared__ __attribute__((aligned(16))) unsigned char diag_smem[];
     const grape::DevProblem &P = H.P;
     const DiagLayout Lo = diag_layout(H);
-    const int t = threadIdx.x, b0 = blockIdx.x * kDiagBlock, nloc = min(kDiagBlock, nb - b0);
+    const int G = Lo.G, EB = Lo.EB;
+    const int t = threadIdx.x, el = t / G, row = t - el * G;
+    const int b0 = blockIdx.x * EB, nloc = min(EB, nb - b0);
     // stage (every thread of the workgroup; coalesced where the source is contiguous)
     {
         grape::Term *terms = reinterpret_cast<grape::Term *>(diag_smem + Lo.terms);
@@ -642,11 +661,12 @@ __global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int 
         double *W = reinterpret_cast<double *>(diag_smem + Lo.W);
         for (int i = t; i < P.D; i += kDiagBlock) W[i] = P.W[i];
         for (int cl = 0; cl < H.ncls; ++cl) {
-            int *sx = reinterpret_cast<int *>(diag_smem + Lo.sidx[cl]);
+            // (offsets picked by value: a layout array indexed by the class would live in scratch)
+            int *sx = reinterpret_cast<int *>(diag_smem + (cl == 0 ? Lo.sidx[0] : Lo.sidx[1]));
             for (int i = t; i < H.nsec[cl] * H.S[cl]; i += kDiagBlock) sx[i] = H.sidx[cl][i];
             const size_t SS = (size_t)H.S[cl] * H.S[cl], n = (size_t)nloc * H.nsec[cl] * SS;
             const cd *src = H.Ub[cl] + (size_t)b0 * H.nsec[cl] * SS;
-            cd *ub = reinterpret_cast<cd *>(diag_smem + Lo.Ub[cl]);
+            cd *ub = reinterpret_cast<cd *>(diag_smem + (cl == 0 ? Lo.Ub[0] : Lo.Ub[1]));
             for (size_t i = t; i < n; i += kDiagBlock) ub[i] = src[i];
         }
         int *fx = reinterpret_cast<int *>(diag_smem + Lo.fixed);
@@ -658,48 +678,66 @@ __global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int 
         }
     }
     __syncthreads();
-    if (t >= nloc) return;
     DiagStage St;
     St.terms = reinterpret_cast<const grape::Term *>(diag_smem + Lo.terms);
     St.tdiag = reinterpret_cast<const cd *>(diag_smem + Lo.tdiag);
     St.W = reinterpret_cast<const double *>(diag_smem + Lo.W);
     St.fixed = reinterpret_cast<const int *>(diag_smem + Lo.fixed);
-    for (int cl = 0; cl < 2; ++cl) {
-        St.sidx[cl] = reinterpret_cast<const int *>(diag_smem + Lo.sidx[cl]);
-        St.Ub[cl] = reinterpret_cast<const cd *>(diag_smem + Lo.Ub[cl]);
-    }
-    const size_t b = (size_t)b0 + t;
-    cd *u0 = reinterpret_cast<cd *>(diag_smem + Lo.u) + (size_t)t * 2 * P.D, *d = u0 + P.D;
+    St.sidx0 = reinterpret_cast<const int *>(diag_smem + Lo.sidx[0]);
+    St.sidx1 = reinterpret_cast<const int *>(diag_smem + Lo.sidx[1]);
+    St.Ub0 = reinterpret_cast<const cd *>(diag_smem + Lo.Ub[0]);
+    St.Ub1 = reinterpret_cast<const cd *>(diag_smem + Lo.Ub[1]);
+    const bool ok = el < nloc;  // group-uniform
+    const size_t b = (size_t)b0 + (ok ? el : 0);
+    cd *u0 = reinterpret_cast<cd *>(diag_smem + Lo.u) + (size_t)el * 2 * P.D, *d = u0 + P.D;
     const double *xb = H.x + b * P.nx;
-    const double *xadd = reinterpret_cast<const double *>(diag_smem + Lo.xa) + (size_t)t * P.na;
+    const double *xadd = reinterpret_cast<const double *>(diag_smem + Lo.xa) + (size_t)(ok ? el : 0) * P.na;
     grape::Pert none;
     none.var = -1;
     none.index = 0;
     none.delta = 0.0;
-    target_diag_st(P, St, xb, xadd, none, u0);
+    // the target's term coefficients (one lane per term), then its diagonal (one lane per entry)
+    cd *cq = reinterpret_cast<cd *>(diag_smem + Lo.cq) + (size_t)el * P.n_tgt;
+    if (ok)
+        for (int q = row; q < P.n_tgt; q += G) cq[q] = grape::term_coef(St.terms[q], 1, xb, xadd, none);
+    __syncthreads();
+    if (ok)
+        for (int i = row; i < P.D; i += G) u0[i] = target_entry(P, St, cq, i);
+    __syncthreads();
     double fsum = 0.0;
     cd tau{0.0, 0.0};
-    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, St, cl, t, b, 0, u0, d, tau, fsum, tau);
+    if (ok) diag_row_any(H, St, row, el, b, 0, u0, d, tau, fsum, tau);
+    fsum = group_add(fsum, G);
+    tau.re = group_add(tau.re, G);
+    tau.im = group_add(tau.im, G);
     for (int q = 0; q < H.nfixed; ++q) {  // U_gg = 1: K_gg = conj(u0_g)
         const int g = St.fixed[q];
         const cd k = p_conj(u0[g]);
         fsum += St.W[g] * (St.W[g] != 0.0 ? 1.0 : 0.0) * (k.re * k.re + k.im * k.im);
         tau = p_add(tau, p_scale(St.W[g], k));
     }
-    H.F[b] = (fsum + tau.re * tau.re + tau.im * tau.im) / P.DD;
+    if (ok && row == 0) H.F[b] = (fsum + tau.re * tau.re + tau.im * tau.im) / P.DD;
     double unused = 0.0;
     cd unused_c{0.0, 0.0};
-    for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, St, cl, t, b, 1, u0, d, tau, unused, unused_c);
+    if (ok) diag_row_any(H, St, row, el, b, 1, u0, d, tau, unused, unused_c);
     for (int q = 0; q < P.na; ++q) {  // target part of F_dx_add
         grape::Pert pq;
         pq.var = grape::VAR_XADD;
         pq.index = q;
         pq.delta = P.eps;
-        target_diag_st(P, St, xb, xadd, pq, d);
-        for (int i = 0; i < P.D; ++i) d[i] = p_scale(P.inv_eps, p_sub(d[i], u0[i]));
+        __syncthreads();  // every lane is done with the previous d and cq
+        if (ok)
+            for (int k = row; k < P.n_tgt; k += G) cq[k] = grape::term_coef(St.terms[k], 1, xb, xadd, pq);
+        __syncthreads();
+        if (ok)
+            for (int i = row; i < P.D; i += G) d[i] = p_scale(P.inv_eps, p_sub(target_entry(P, St, cq, i), u0[i]));
+        __syncthreads();
         double sa = 0.0;
         cd trd{0.0, 0.0};
-        for (int cl = 0; cl < H.ncls; ++cl) diag_class(H, St, cl, t, b, 2, u0, d, tau, sa, trd);
+        if (ok) diag_row_any(H, St, row, el, b, 2, u0, d, tau, sa, trd);
+        sa = group_add(sa, G);
+        trd.re = group_add(trd.re, G);
+        trd.im = group_add(trd.im, G);
         for (int r = 0; r < H.nfixed; ++r) {
             const int g = St.fixed[r];
             const cd kd = p_conj(d[g]), k = p_conj(u0[g]);
@@ -707,8 +745,10 @@ __global__ __launch_bounds__(kDiagBlock) void k_sec_head_diag(SectorHead H, int 
             trd = p_add(trd, p_scale(St.W[g], kd));
         }
         const double val = (2.0 * sa + 2.0 * (tau.re * trd.re + tau.im * trd.im)) / P.DD;
-        if (P.xadd_dep && H.tgt_part) H.tgt_part[b * P.na + q] = val;
-        else H.Fdx[b * P.nx + (size_t)P.np * P.Nt + q] = val;
+        if (ok && row == 0) {
+            if (P.xadd_dep && H.tgt_part) H.tgt_part[b * P.na + q] = val;
+            else H.Fdx[b * P.nx + (size_t)P.np * P.Nt + q] = val;
+        }
     }
 }
 
@@ -861,9 +901,9 @@ hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
 
 hipError_t launch_sector_head(const SectorHead &H, int nb, hipStream_t st) {
     if (H.diag) {
-        const size_t lds = diag_layout(H).total;
-        hipLaunchKernelGGL(k_sec_head_diag, dim3((unsigned)((nb + kDiagBlock - 1) / kDiagBlock)), dim3(kDiagBlock), lds,
-                           st, H, nb);
+        const DiagLayout L = diag_layout(H);  // G lanes per evaluation (G <= 16: d <= 12, sectors of <= 4 levels)
+        hipLaunchKernelGGL(k_sec_head_diag, dim3((unsigned)((nb + L.EB - 1) / L.EB)), dim3(kDiagBlock), L.total, st, H,
+                           nb);
         return hipGetLastError();
     }
     const size_t lds = (size_t)kHeadSlots * H.P.D * H.P.D * sizeof(cd);
