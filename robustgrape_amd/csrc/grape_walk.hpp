@@ -543,6 +543,18 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
     return L;
 }
 
+#ifndef GRAPE_WALK_G4_KEEP_A2_GRAD  // k_walk_grad<4>: keep A'^2 of the eps-variant (0: regenerate its columns)
+#define GRAPE_WALK_G4_KEEP_A2_GRAD 1
+#endif
+#ifndef GRAPE_WALK_IMG4_KEEP_A2  // k_walk_img<4>: keep each variant's A^2 (0: regenerate its columns)
+#define GRAPE_WALK_IMG4_KEEP_A2 0
+#endif
+#ifndef GRAPE_WALK_F4_WAVES  // k_walk_fwd<4>: waves per SIMD
+#define GRAPE_WALK_F4_WAVES 2
+#endif
+#ifndef GRAPE_WALK_F4_FENCE  // k_walk_fwd<4>: fence the exponential's columns
+#define GRAPE_WALK_F4_FENCE 1
+#endif
 #ifndef GRAPE_WALK_G4_KEEP_A2_NOM
 #define GRAPE_WALK_G4_KEEP_A2_NOM 1
 #endif
@@ -564,9 +576,13 @@ struct WalkCfg {
     static constexpr bool E_LDS_FWD = false;     // k_walk_fwd keeps E in registers
     static constexpr bool X_LDS = D >= 4 && NS == 1 && GRAPE_WALK_G4_XLDS;  // k_walk_grad: X / Y in LDS
     static constexpr bool E_LDS_GRAD = D >= 4 && NS == 1 && !GRAPE_WALK_G4_XLDS;  // ... or E in LDS
-    static constexpr bool KEEP_A2_GRAD = D < 4;  // k_walk_grad<4>: regenerate A^2 columns (registers)
+    // k_walk_grad<4> keeps A'^2 too (round 3: 2.28-2.32 -> 2.20 ms per C2 pass; the stored-propagator
+    // kernel has the registers at one wave per SIMD); the image walk regenerates its columns
+    static constexpr bool KEEP_A2_GRAD = D < 4 || GRAPE_WALK_G4_KEEP_A2_GRAD;
+    static constexpr bool KEEP_A2_IMG = D < 4 || GRAPE_WALK_IMG4_KEEP_A2;
     static constexpr bool KEEP_A2_NOM = D < 4 || GRAPE_WALK_G4_KEEP_A2_NOM;
-    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : 3) : 2;
+    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : 3) : D == 3 ? 2 : GRAPE_WALK_F4_WAVES;
+    static constexpr bool FENCE_FWD = D >= 4 && GRAPE_WALK_F4_FENCE;
     static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? 3 : 2) : D == 3 ? (NS == 1 ? 2 : 1)
                                                                               : GRAPE_WALK_G4_WAVES;
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? 1 : GRAPE_WALK_G4S_WAVES;
@@ -617,7 +633,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
         walk_build<D, NS>(P, ops, X, k + 1, none, A);
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
-            walk_expm<D, C::FENCE, true>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+            walk_expm<D, C::FENCE_FWD, true>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
             });
@@ -935,7 +951,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
                 if constexpr (KIND == IMG_KEEP_D2 || KIND == IMG_KEEP_E2) {
-                    walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                         for (int j = 0; j < D; ++j) {
                             if constexpr (KIND == IMG_KEEP_D2) Ed2[w].set(j, i, x[j]);
@@ -944,7 +960,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
                     });
                 } else {
                     cd Z[D][D];  // E_k^dag dX, column by column as the variant's columns come out
-                    walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
                         cd dx[D];
                         const auto &e2 = Ee2[w].opaque();  // (LDS reads issued here, not hoisted)
                         const auto &d2 = Ed2[w].opaque();

@@ -8,7 +8,7 @@ faulted() { grep -qE "HSA_STATUS_ERROR|illegal memory access|Memory access fault
 for v in "$@"; do
   if [ "$v" = base ]; then unset GRAPE_LIB; else export GRAPE_LIB=$PWD/abvar/libgrape_$v.so; fi
   if [ -n "${TESTS:-}" ]; then
-    timeout -k 10 300 python -u -m pytest tests/test_gpu_walk.py -x -q --timeout 120 --timeout-method thread > $O/ab_tests_${TAG}_$v.log 2>&1
+    timeout -k 10 300 python -u -m pytest ${TESTFILE:-tests/test_gpu_walk.py} -x -q --timeout 120 --timeout-method thread > $O/ab_tests_${TAG}_$v.log 2>&1
     rc=$?; echo "$v tests rc=$rc"; tail -2 $O/ab_tests_${TAG}_$v.log
     faulted $O/ab_tests_${TAG}_$v.log && { echo FAULT; exit 99; }
     [ $rc -ne 0 ] && exit $rc
