@@ -547,7 +547,7 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #define GRAPE_WALK_G4_KEEP_A2_GRAD 1
 #endif
 #ifndef GRAPE_WALK_IMG4_KEEP_A2  // k_walk_img<4>: keep each variant's A^2 (0: regenerate its columns)
-#define GRAPE_WALK_IMG4_KEEP_A2 0
+#define GRAPE_WALK_IMG4_KEEP_A2 1
 #endif
 #ifndef GRAPE_WALK_F4_WAVES  // k_walk_fwd<4>: waves per SIMD
 #define GRAPE_WALK_F4_WAVES 2
