@@ -173,6 +173,10 @@ typedef struct grape_desc {
  * one-thread-per-evaluation head over the sector blocks; this option keeps the general
  * (d x d products) sector head for every problem (A/B and parity checks). */
 #define GRAPE_OPT_GENERAL_HEAD 256
+/* Latency-bound calls (16-wave scans: fewer sub-evaluations than CUs) of the Rydberg sector layout
+ * (one 4-level sector + two 2-level sectors, no error sources) run both sector classes' walks and
+ * scans in one launch per stage; this option keeps one launch per class. */
+#define GRAPE_OPT_NO_PAIR 512
 
 typedef struct grape_plan grape_plan;
 

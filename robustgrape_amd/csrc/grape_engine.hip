@@ -26,6 +26,7 @@ namespace grape_host {
 #define GRAPE_EXTERN_DIM(d) GRAPE_DECLARE_DIM(d, extern)
 GRAPE_DIMS(GRAPE_EXTERN_DIM)
 #undef GRAPE_EXTERN_DIM
+GRAPE_DECLARE_SCAN_PAIR(extern)
 }  // namespace grape_host
 
 using grape::cd;
@@ -1188,8 +1189,26 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         // the second sector class on the auxiliary stream beside the first; large ones keep one
         // stream (no gain there, DESIGN 4.1, and per-kernel event times stay per kernel).
         const bool fork = p->aux_stream && !p->capturing && nb <= kForkMaxBatch && !(p->P.opts & GRAPE_OPT_NO_FORK);
+        // Latency-bound calls of the Rydberg layout: both classes' walks (and scans) in ONE launch per
+        // stage (grape_walk_api.hpp launch_pair) -- neither a graph branch nor a second stream overlaps
+        // them inside a captured graph on this runtime.  pa: the 4-level class, pb: the 2-level one.
+        int pa = 0, pb = 1;
+        if (p->ncls == 2 && grape_walk::pair_ok(p->Ps[1], p->Ps[0])) std::swap(pa, pb);
+        const bool pair = p->ncls == 2 && !(p->P.opts & GRAPE_OPT_NO_PAIR) && p->Ps[0].scan_waves == kScanLatency &&
+                          p->Ps[1].scan_waves == kScanLatency && grape_walk::pair_ok(p->Ps[pa], p->Ps[pb]);
         auto stage = [&](int s) -> hipError_t {  // stage s of every class (class 1 forked when `fork`)
-            if (!fork) {
+            if (pair && s < 2) {
+                mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 0);
+                hipError_t e = grape_walk::launch_pair(s, p->Ps[pa], Bc[pa], p->Ps[pb], Bc[pb], st);
+                mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 1);
+                if (e == hipSuccess && s == 0) {
+                    mk(GRAPE_KERNEL_SCAN, 0);
+                    e = grape_host::launch_scan_pair<4, 2>(p->Ps[pa], Bc[pa], p->Ps[pb], Bc[pb], st);
+                    mk(GRAPE_KERNEL_SCAN, 1);
+                }
+                return e;
+            }
+            if (!fork || pair) {
                 for (int cl = 0; cl < p->ncls; ++cl) {
                     const hipError_t e = dispatch_sector_stage(p->Ps[cl].D, s, p->Ps[cl], Bc[cl], st, mk);
                     if (e != hipSuccess) return e;

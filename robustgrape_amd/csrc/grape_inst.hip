@@ -9,4 +9,7 @@
 
 namespace grape_host {
 GRAPE_DECLARE_DIM(GRAPE_INST_DIM, )
+#if GRAPE_INST_DIM == 4
+GRAPE_DECLARE_SCAN_PAIR()
+#endif
 }  // namespace grape_host

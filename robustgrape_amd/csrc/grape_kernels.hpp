@@ -486,7 +486,7 @@ __global__ __launch_bounds__(64) void k_expm_raw(const cd *A, cd *E, int n, int 
 // totals live in the groups' LDS tiles COLUMN-major (tile[j*D + i] = S[i][j]).
 // ---------------------------------------------------------------------------
 template <int D, int W>
-__global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
+__device__ __forceinline__ void scan_body(const DevProblem &P, const DevBatch &B, const int b) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     cd *lds = reinterpret_cast<cd *>(smem_raw);
     constexpr int GPW = Geo<D>::GPW, GCD = Geo<D>::GROUP_CD, TILE = Geo<D>::TILE;
@@ -495,7 +495,6 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
     cd *S1 = lds + W * GPW * GCD, *S2 = S1 + TILE, *S3 = S2 + TILE;
     const int c = wave * GPW + G.g;  // chunk owned by this group
     const int i = G.i;
-    const int b = blockIdx.x;
     const bool gvalid = G.lane_ok && c < P.nchunks;
     auto tile_of = [&](int cc) -> cd * {
         return lds + (cc / GPW) * GPW * GCD + (cc % GPW) * GCD;
@@ -707,6 +706,17 @@ __global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
 #pragma unroll
         for (int jj = 0; jj < D; ++jj) dst[jj] = mc[jj];
     }
+}
+template <int D, int W>
+__global__ __launch_bounds__(64 * W) void k_scan(DevProblem P, DevBatch B) {
+    scan_body<D, W>(P, B, blockIdx.x);
+}
+// Two sector classes' scans in one launch (latency-bound calls): workgroups [0, B0.nb) scan class 0,
+// the rest class 1 (dynamic LDS: the larger of the two)
+template <int D0, int D1, int W>
+__global__ __launch_bounds__(64 * W) void k_scan_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1) {
+    if ((int)blockIdx.x < B0.nb) scan_body<D0, W>(P0, B0, blockIdx.x);
+    else scan_body<D1, W>(P1, B1, blockIdx.x - B0.nb);
 }
 
 // ---------------------------------------------------------------------------

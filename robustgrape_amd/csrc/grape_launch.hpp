@@ -5,6 +5,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "grape.h"
 #include "grape_errpath.hpp"
 #include "grape_lane.hpp"
@@ -96,6 +98,24 @@ void launch_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
     else
         hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide), st,
                            P, B);
+}
+// the latency scans of two walk classes in one launch (D0 = 4, D1 = 2: the Rydberg layout)
+template <int D0, int D1>
+hipError_t launch_scan_pair(const DevProblem &P0, const DevBatch &B0, const DevProblem &P1, const DevBatch &B1,
+                            hipStream_t st) {
+    const size_t lds = std::max(scan_lds<D0>(kScanLatency), scan_lds<D1>(kScanLatency));
+    static unsigned long long limit_set = 0;  // per device (idempotent: a race only repeats the call)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev >= 64) return hipErrorInvalidDevice;
+    if (!((limit_set >> dev) & 1ull)) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan_pair<D0, D1, kScanLatency>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        limit_set |= 1ull << dev;
+    }
+    hipLaunchKernelGGL((grape::k_scan_pair<D0, D1, kScanLatency>), dim3((unsigned)(B0.nb + B1.nb)),
+                       dim3(64 * kScanLatency), lds, st, P0, B0, P1, B1);
+    return hipGetLastError();
 }
 template <int D>
 void launch_err_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
@@ -412,6 +432,10 @@ hipError_t set_lds_limits() {
 
 
 #define GRAPE_DIMS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+// (the scan pair is instantiated in the D = 4 translation unit)
+#define GRAPE_DECLARE_SCAN_PAIR(EXT)                                                                       \
+    EXT template hipError_t launch_scan_pair<4, 2>(const DevProblem &, const DevBatch &, const DevProblem &, \
+                                                    const DevBatch &, hipStream_t);
 
 #define GRAPE_DECLARE_DIM(d, EXT)                                                                          \
     EXT template hipError_t launch_pipeline<d>(const DevProblem &, const DevBatch &, hipStream_t, const KMark &); \

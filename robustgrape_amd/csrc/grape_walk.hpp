@@ -525,21 +525,27 @@ struct WalkLane {
     long slot;           // the lane's scratch slot (NS consecutive pairs of D x D tiles)
     bool ok;
 };
+// The workgroup's place in the class's launch grid: the hardware block, or (pair kernels, two
+// sector classes in one launch for latency-bound calls) a block of one class's part of the grid.
+struct VBlock {
+    int x, y, gx;  // blockIdx.x, blockIdx.y, gridDim.x of the class's own grid
+};
+__device__ __forceinline__ VBlock hw_block() { return VBlock{(int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x}; }
 template <int NS>
-__device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatch &B) {
+__device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatch &B, const VBlock &vb) {
     WalkLane L;
     const int ns = P.nsec > 1 ? P.nsec : 1;
     L.nbe = B.nb / ns;
     const long per = (long)L.nbe * P.nchunks;
-    const long g = (long)blockIdx.x * kWalkBlock + threadIdx.x;
-    L.w0 = blockIdx.y * NS;
+    const long g = (long)vb.x * kWalkBlock + threadIdx.x;
+    L.w0 = vb.y * NS;
     L.ok = g < per;
     const long gg = L.ok ? g : 0;
     L.c = (int)(gg / L.nbe);
     L.be = (int)(gg - (long)L.c * L.nbe);
     // own scratch slot for every lane, past-the-end ones included (they walk lane 0's inputs)
     const long per_pad = (per + kWalkBlock - 1) / kWalkBlock * kWalkBlock;
-    L.slot = (long)blockIdx.y * per_pad + g;
+    L.slot = (long)vb.y * per_pad + g;
     return L;
 }
 
@@ -592,10 +598,10 @@ struct WalkCfg {
 
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
 template <int D, int NS, bool STORE>
-__global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_walk_fwd(DevProblem P, DevBatch B) {
+__device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
     using C = WalkCfg<D, NS>;
     constexpr int TS = D * D;
-    const WalkLane L = walk_lane<NS>(P, B);
+    const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1;
     const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
@@ -604,7 +610,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
     none.var = -1;
     none.index = 0;
     none.delta = 0.0;
-    const size_t lanes = (size_t)gridDim.x * kWalkBlock, lane = (size_t)blockIdx.x * kWalkBlock + threadIdx.x;
+    const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
     MStore<D, C::E_LDS_FWD> E;
     if constexpr (C::E_LDS_FWD) {
         __shared__ cd lds[kWalkBlock * MStore<D, true>::kStride];
@@ -638,7 +644,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
                 for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
             });
             if constexpr (STORE) {  // the gradient walk's copy: lane-minor, one coalesced 1-KB store per element
-                cd *ew = B.Ew + ((((size_t)blockIdx.y * P.L + jj) * NS + w) * TS) * lanes + lane;
+                cd *ew = B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * TS) * lanes + lane;
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
 #pragma unroll
@@ -676,17 +682,21 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
     }
 }
 
+template <int D, int NS, bool STORE>
+__global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_walk_fwd(DevProblem P, DevBatch B) {
+    walk_fwd_body<D, NS, STORE>(P, B, hw_block());
+}
+
 // STORED: the nominal propagators come from the forward walk's copy (B.Ew, prefetched one step
 // ahead) instead of being recomputed -- one exponential of the three per step saved for 512 B of
 // HBM traffic per step and sector.
 // NVG: the number of gradient parameters when known at compile time (1: C1 / C2 / C4), else 0
 // (a runtime loop) -- a static count of the F_dx stores per step keeps the prefetch waits exact.
 template <int D, int NS, bool STORED, int NVG>
-__global__ __launch_bounds__(kWalkBlock, (STORED ? WalkCfg<D, NS>::WAVES_GRAD_STORED : WalkCfg<D, NS>::WAVES_GRAD))
-void k_walk_grad(DevProblem P, DevBatch B) {
+__device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
     using C = WalkCfg<D, NS>;
     constexpr int TS = D * D;
-    const WalkLane L = walk_lane<NS>(P, B);
+    const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1;
     const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
@@ -705,8 +715,8 @@ void k_walk_grad(DevProblem P, DevBatch B) {
         if constexpr (XL) X[0].p = MStore<D, true>::slot(lds);
         else E[0].p = MStore<D, true>::slot(lds);
     }
-    const size_t lanes = (size_t)gridDim.x * kWalkBlock, lane = (size_t)blockIdx.x * kWalkBlock + threadIdx.x;
-    auto ew = [&](int jj, int w) { return B.Ew + ((((size_t)blockIdx.y * P.L + jj) * NS + w) * TS) * lanes + lane; };
+    const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
+    auto ew = [&](int jj, int w) { return B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * TS) * lanes + lane; };
     cd En[STORED ? NS : 1][D][D];  // the next step's stored propagators (STORED)
     if constexpr (STORED) {
 #pragma unroll
@@ -850,6 +860,32 @@ void k_walk_grad(DevProblem P, DevBatch B) {
     }
 }
 
+template <int D, int NS, bool STORED, int NVG>
+__global__ __launch_bounds__(kWalkBlock, (STORED ? WalkCfg<D, NS>::WAVES_GRAD_STORED : WalkCfg<D, NS>::WAVES_GRAD))
+void k_walk_grad(DevProblem P, DevBatch B) {
+    walk_grad_body<D, NS, STORED, NVG>(P, B, hw_block());
+}
+
+// Pair kernels (latency-bound calls): two sector classes' walks in ONE launch -- the first
+// n0 = gx0 * gy0 workgroups walk class 0 (D0, NS0; STORE0: its stored propagators), the rest class 1
+// -- so a single evaluation's classes run side by side instead of one launch after the other
+// (graph branches do not run concurrently on this runtime: scripts/probes/graph_branch_probe.hip).
+// The registers are the larger class's; at these sizes the grid is a few workgroups.
+template <int D0, int NS0, bool ST0, int D1, int NS1>
+__global__ __launch_bounds__(kWalkBlock, 1) void k_walk_fwd_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1,
+                                                                 int gx0, int gy0, int gx1) {
+    const int id = blockIdx.x, n0 = gx0 * gy0;
+    if (id < n0) walk_fwd_body<D0, NS0, ST0>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
+    else walk_fwd_body<D1, NS1, false>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+}
+template <int D0, int NS0, bool ST0, int D1, int NS1>
+__global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1,
+                                                                  int gx0, int gy0, int gx1) {
+    const int id = blockIdx.x, n0 = gx0 * gy0;
+    if (id < n0) walk_grad_body<D0, NS0, ST0, 1>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
+    else walk_grad_body<D1, NS1, false, 1>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+}
+
 // ---------------------------------------------------------------------------
 // Error sources: the image walk (k_walk_img, stage 0) and its F_dx traces (k_img_fdx, stage 1)
 // ---------------------------------------------------------------------------
@@ -893,7 +929,7 @@ template <int D, int NS>
 __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_walk_img(DevProblem P, DevBatch B) {
     using C = WalkCfg<D, NS>;
     constexpr int TS = D * D;
-    const WalkLane L = walk_lane<NS>(P, B);
+    const WalkLane L = walk_lane<NS>(P, B, hw_block());
     const int ns = P.nsec > 1 ? P.nsec : 1;
     const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;

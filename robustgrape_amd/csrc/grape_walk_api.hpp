@@ -18,6 +18,13 @@ namespace grape_walk {
 // to B.Zl), stage 1 = k_img_fdx (per-sector F_dx terms to B.sec_part, [nb][Nt][nvg])
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
+// Latency-bound calls of the Rydberg layout -- class 0: one 4-level sector with stored propagators,
+// class 1: two 2-level sectors, no error sources, one gradient parameter -- run both classes' walks
+// of a stage in ONE launch (k_walk_fwd_pair / k_walk_grad_pair).  pair_ok tells whether the layout
+// fits; launch_pair(stage, ...) then replaces launch<4>(stage, class 0) + launch<2>(stage, class 1).
+bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1);
+hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevBatch &B0, const grape::DevProblem &P1,
+                       const grape::DevBatch &B1, hipStream_t st);
 // the walks' controls: x [nb][nx] -> xT [nx][nb] (B.xT), once per launch for every walk class
 hipError_t transpose_x(const double *x, double *xT, int nb, int nx, hipStream_t st);
 }  // namespace grape_walk

@@ -57,6 +57,27 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
     return hipGetLastError();
 }
 
+bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1) {
+    return P0.walk && P1.walk && P0.ne == 0 && P0.nvg == 1 && P0.D == 4 && P0.nsec == 1 && P0.walk_store_e &&
+           P1.D == 2 && P1.nsec == 2 && P1.nvg == 1 && !P1.walk_store_e;
+}
+hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevBatch &B0, const grape::DevProblem &P1,
+                       const grape::DevBatch &B1, hipStream_t st) {
+    if (!pair_ok(P0, P1)) return hipErrorInvalidValue;
+    auto gx = [](const grape::DevProblem &P, const grape::DevBatch &B) {
+        const int ns = P.nsec > 1 ? P.nsec : 1;
+        const long lanes = (long)(B.nb / ns) * P.nchunks;
+        return (int)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock);
+    };
+    const int gx0 = gx(P0, B0), gy0 = 1, gx1 = gx(P1, B1);  // class 0: one sector per lane; class 1: both per lane
+    const dim3 grid((unsigned)(gx0 * gy0 + gx1)), blk(grape::kWalkBlock);
+    if (stage == 0)
+        hipLaunchKernelGGL((grape::k_walk_fwd_pair<4, 1, true, 2, 2>), grid, blk, 0, st, P0, B0, P1, B1, gx0, gy0, gx1);
+    else
+        hipLaunchKernelGGL((grape::k_walk_grad_pair<4, 1, true, 2, 2>), grid, blk, 0, st, P0, B0, P1, B1, gx0, gy0, gx1);
+    return hipGetLastError();
+}
+
 // x [nb][nx] -> xT [nx][nb] through a 32 x 32 LDS tile (both sides coalesced)
 __global__ __launch_bounds__(256) void k_transpose_x(const double *x, double *xT, int nb, int nx) {
     __shared__ double t[32][33];

@@ -279,3 +279,39 @@ def test_diagonal_head_matches_general_head(name, fp):
         if a.size:
             scale = max(float(np.max(np.abs(b))), 1e-300)
             assert float(np.max(np.abs(a - b))) <= 1e-12 * scale + 1e-15, (name, float(np.max(np.abs(a - b))), scale)
+
+
+@pytest.mark.parametrize("name,fp,nparam", [("full9", lambda: P.full9_problem(512), 1),
+                                            ("full9-hot", lambda: _high_norm_problem(64)[0], 2)])
+def test_pair_launches_bitwise(name, fp, nparam):
+    """Latency-bound calls (16-wave scans) of the Rydberg layout run both sector classes' walks and
+    scans in one launch per stage (k_walk_fwd_pair, k_scan_pair, k_walk_grad_pair): the same
+    arithmetic as one launch per class (GRAPE_OPT_NO_PAIR), so F and F_dx agree bit for bit --
+    batched (stream path) and single (graph path) calls; the C2-size problem also against the
+    oracle at the T2s tier."""
+    from robustgrape_amd.operators import OPT_NO_PAIR
+    f = fp()
+    nt = f.unitary_problem.ntimes
+    rng = np.random.default_rng(11)
+    X = rng.uniform(0, 2 * np.pi, size=(5, nparam * nt + 1))
+    if name == "full9":
+        X[:, :nt] *= 0.001  # the C2 start: a 2 pi 0.001 U pulse
+    elif name == "full9-hot":
+        X[::2, 1::2][:, 5] = 700.0  # a high-norm step (squaring path) in every other row
+    outs = []
+    for opts in (0, OPT_NO_PAIR):
+        pl = _plan(f, 8, opts, nparam=nparam)
+        try:
+            batch = pl.fidelity_grad(X)[:2]
+            single = pl.fidelity_grad(X[3:4])[:2]
+            outs.append((batch, single))
+        finally:
+            pl.close()
+    (b0, s0), (b1, s1) = outs
+    assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
+    assert np.array_equal(s0[0], s1[0]) and np.array_equal(s0[1], s1[1])
+    assert s0[0][0] == b0[0][3] and np.array_equal(s0[1][0], b0[1][3])
+    if name == "full9":
+        from oracle import grape_oracle as O
+        F0, g0 = O.calculate_fidelity_and_derivatives(f, X[0])[:2]
+        _check("pair_full9", b0[0][0], b0[1][0], F0, g0, True)
