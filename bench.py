@@ -714,7 +714,7 @@ def main():
                          "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
                          "batched L-BFGS (one step = one iteration of every restart); c2-closure: C2 as "
                          "plain Python closures through the host-table fallback")
-    ap.add_argument("--scan-waves", type=int, default=None, choices=(0, 1, 4, 8),
+    ap.add_argument("--scan-waves", type=int, default=None, choices=(0, 1, 4, 8, 16),
                     help="c4opt: the plan's scan width (chunking); 0 = by batch size, default: RobustCost's choice")
     ap.add_argument("--plan-options", type=int, default=0,
                     help="c4opt: GRAPE_OPT_* flags of the optimiser's plan (A/B runs)")

@@ -56,6 +56,9 @@ constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScan
               kScanTiny = grape_host::kScanTiny, kScanLatency = grape_host::kScanLatency;
 // calls of at most this many evaluations run the two sector classes on two streams (enqueue)
 constexpr int kForkMaxBatch = 4096;
+// Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
+// (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
+constexpr int kPairMaxBatch = 64;
 constexpr int kCtrlInts = 8;  // [0..1] single-eval counters, [2] status, [4..5] pipeline overflow counters
 using grape_host::KMark;
 using grape_host::launch_pipeline;
@@ -1194,7 +1197,9 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         // them inside a captured graph on this runtime.  pa: the 4-level class, pb: the 2-level one.
         int pa = 0, pb = 1;
         if (p->ncls == 2 && grape_walk::pair_ok(p->Ps[1], p->Ps[0])) std::swap(pa, pb);
-        const bool pair = p->ncls == 2 && !(p->P.opts & GRAPE_OPT_NO_PAIR) && p->Ps[0].scan_waves == kScanLatency &&
+        // (small calls only: a pair kernel runs the 2-level class at the 4-level class's occupancy)
+        const bool pair = p->ncls == 2 && nb <= kPairMaxBatch && !(p->P.opts & GRAPE_OPT_NO_PAIR) &&
+                          p->Ps[0].scan_waves == kScanLatency &&
                           p->Ps[1].scan_waves == kScanLatency && grape_walk::pair_ok(p->Ps[pa], p->Ps[pb]);
         auto stage = [&](int s) -> hipError_t {  // stage s of every class (class 1 forked when `fork`)
             if (pair && s < 2) {
