@@ -231,6 +231,19 @@ int grape_fidelity_grad_device_async(grape_plan *plan, int nbatch, const double 
                                      double *d_F, double *d_F_dx,
                                      double *d_F_d2err, double *d_F_d2err_dx);
 
+/* Time sharding of ONE evaluation over devices (robustgrape_amd/timeshard.py).
+ * The plan is created for a time SLICE of the problem: ntimes = the slice's steps, t0 = dt * steps,
+ * the slice's controls as x (np * steps values, no x_add); dense engine (12 < ndim <= 64) without
+ * error sources, general projector or step-index terms (else GRAPE_ERR_UNSUPPORTED).
+ * grape_slice_forward: the slice total U_slice = E_last ... E_first (ndim x ndim complex,
+ *   column-major interleaved, host); the slice's propagators and chunk prefixes stay in the plan.
+ * grape_slice_gradient: given M' = B M B^dagger (same layout) -- B the product of the earlier
+ *   slices' totals, M = G U for the whole evaluation's U (FidelityCalculations.jl:56-65 as
+ *   F_dx = Re tr(G U_dx)) -- the slice's F_dx entries (np x steps, x's layout), from the
+ *   propagators of the last grape_slice_forward on this plan.  Both synchronous. */
+int grape_slice_forward(grape_plan *plan, const double *x, double *U_slice);
+int grape_slice_gradient(grape_plan *plan, const double *M_prime, double *F_dx);
+
 /*
  * Closure fallback (plans created with GRAPE_DESC_HOST_TABLES): the outputs of
  * grape_fidelity_grad for problems whose H0 / target are host closures.  The

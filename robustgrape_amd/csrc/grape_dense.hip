@@ -773,6 +773,43 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     return hipGetLastError();
 }
 
+// padded image <-> column-major d x d complex (the C ABI's layout), one workgroup per matrix
+__global__ __launch_bounds__(256) void k_img_cols(const double *img, grape::cd *cols, int D) {
+    for (int t = threadIdx.x; t < D * D; t += blockDim.x) {
+        const int col = t / D, row = t % D;
+        const int w = col >> 4, tr = row >> 4, r = (row & 15) >> 2, l = ((row & 3) << 4) | (col & 15);
+        const size_t o = (size_t)((w * 4 + tr) * 4 + r) * 64 + l;
+        cols[t] = grape::cmake(img[o], img[IMG / 2 + o]);
+    }
+}
+__global__ __launch_bounds__(256) void k_cols_img(const grape::cd *cols, double *img, int D) {
+    for (int o = threadIdx.x; o < 64 * 64; o += blockDim.x) {
+        const int l = o & 63, r = (o >> 6) & 3, t = (o >> 8) & 3, w = o >> 10;
+        const int row = 16 * t + (l >> 4) + 4 * r, col = 16 * w + (l & 15);
+        const bool in = row < D && col < D;
+        const grape::cd v = in ? cols[(size_t)row + (size_t)col * D] : grape::cmake(0.0, 0.0);
+        img[o] = v.re;
+        img[IMG / 2 + o] = v.im;
+    }
+}
+
+hipError_t launch_slice_forward(const DenseProblem &P, const DenseBatch &B, grape::cd *Ucols, hipStream_t st) {
+    if (B.nb != 1 || !B.Ub) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_dexp, dim3((unsigned)P.P.Nt * (unsigned)P.P.nv), dim3(NTHREADS), kLds, st, P, B);
+    hipLaunchKernelGGL(k_dscan, dim3((unsigned)P.Nc), dim3(NTHREADS), kLds, st, P, B);
+    hipLaunchKernelGGL(k_dcarry, dim3(1), dim3(NTHREADS), kLds, st, P, B);  // carries and U (F, M unused)
+    hipLaunchKernelGGL(k_img_cols, dim3(1), dim3(256), 0, st, B.Ub, Ucols, P.P.D);
+    return hipGetLastError();
+}
+
+hipError_t launch_slice_gradient(const DenseProblem &P, const DenseBatch &B, const grape::cd *Mcols, hipStream_t st) {
+    if (B.nb != 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_cols_img, dim3(1), dim3(256), 0, st, Mcols, B.M, P.P.D);
+    hipLaunchKernelGGL(k_dmc, dim3((unsigned)P.Nc), dim3(NTHREADS), kLds, st, P, B);
+    hipLaunchKernelGGL(k_dgrad, dim3((unsigned)P.P.Nt), dim3(NTHREADS), kLds, st, P, B);
+    return hipGetLastError();
+}
+
 // A = -i dt H of host-tabulated H (closure fallback, column-major d x d), zero-padded images
 __global__ __launch_bounds__(256) void k_tab_images(const grape::cd *H, double *img, int D, double dt) {
     const grape::cd *src = H + (size_t)blockIdx.x * D * D;

@@ -57,6 +57,12 @@ hipError_t set_lds_limits();
 // images B.E, then converted to row-major d x d tiles rows[Nt][nv][D][D] (the table the
 // materialised-derivative kernels of grape_unitary.hip read).
 hipError_t launch_variant_table(const DenseProblem &P, const DenseBatch &B, grape::cd *rows, hipStream_t st);
+// Time sharding: one evaluation (B.nb = 1) of a slice plan.  Forward: the slice's
+// propagators, chunk prefixes and carries (kept in B) and its total U_slice into Ucols (column-major
+// d x d).  Gradient: M' (column-major) replaces the plan's M = G U, then k_dmc / k_dgrad give the
+// slice's F_dx entries (B.Fdx).  Uses B.Ub.
+hipError_t launch_slice_forward(const DenseProblem &P, const DenseBatch &B, grape::cd *Ucols, hipStream_t st);
+hipError_t launch_slice_gradient(const DenseProblem &P, const DenseBatch &B, const grape::cd *Mcols, hipStream_t st);
 // Closure fallback above GRAPE_MAX_SMALL_DIM: n host-tabulated H (column-major d x d) -> exp(-i dt H)
 // as row-major d x d tiles (`rows`), through the padded images Aimg / Eimg (n images each); the
 // no-interchange solve needs a Hermitian H (checked on the host, robustgrape_amd/engine.py)

@@ -216,6 +216,9 @@ struct grape_plan {
     // graph path: F ([kGraphBatch]) and F_dx ([nb][nx]) of a call side by side in one device block
     // (h_F is its pinned image), so one D2H copy returns both
     double *d_gout = nullptr;
+    // time-sharded evaluations (grape_slice_*): column-major U_slice / M' staging (2 d x d)
+    cd *d_slice = nullptr;
+    bool uses_tstep = false;  // some H0 term reads the step index (slices would need its offset)
     // optional per-kernel timing with HIP events on the plan's stream
     bool profiling = false;
     struct Pending {
@@ -249,7 +252,7 @@ static void free_plan(grape_plan *p) {
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
                     p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
-                    p->d_fixed, p->d_gout};
+                    p->d_fixed, p->d_gout, p->d_slice};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
@@ -738,6 +741,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (device < 0 || device >= ndev) return fail(GRAPE_ERR_NO_DEVICE, "device index out of range");
 
     grape_plan *p = new grape_plan();
+    for (int k = 0; k < (tables ? 0 : desc->n_h0_terms); ++k)
+        if (desc->h0_terms[k].var == GRAPE_VAR_TSTEP) p->uses_tstep = true;
     p->device = device;
     p->max_batch = desc->max_batch > 0 ? desc->max_batch : 256;
     auto bail = [&](int code) {
@@ -1085,6 +1090,36 @@ static int ud_propagators_dev(grape_plan *p, const double *d_x, int nv, const cd
 static int enqueue_general(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
                            double *d_Fd2dx, const KMark &mk);
 
+// the dense engine's view of one launch (plan workspaces + the call's inputs and outputs)
+static grape_dense::DenseBatch dense_batch(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx,
+                                           double *d_Fd2, double *d_Fd2dx) {
+    grape_dense::DenseBatch DB{};
+    DB.nb = nb;
+    DB.x = d_x;
+    DB.E = p->dn_E;
+    DB.Q = p->dn_Q;
+    DB.Carry = p->dn_Carry;
+    DB.M = p->dn_M;
+    DB.Mc = p->dn_Mc;
+    DB.Z = p->dn_Z;
+    DB.Ub = p->dn_Ub;
+    DB.Zl = p->dn_Zl;
+    DB.Vc = p->dn_Vc;
+    DB.Sx = p->dn_Sx;
+    DB.Tot = p->dn_Tot;
+    DB.Me = p->dn_Me;
+    DB.Mp = p->dn_Mp;
+    DB.B0 = p->dn_B0;
+    DB.Fd2 = d_Fd2;
+    DB.Fd2dx = d_Fd2dx;
+    DB.F = d_F;
+    DB.Fdx = d_Fdx;
+    DB.status = p->d_ctrl + 2;
+    DB.mstats = nullptr;
+    DB.gp_scr = p->d_gpscr;
+    return DB;
+}
+
 // One launch sequence of `nb` evaluations on the plan's stream over workspace rows
 // [0, nb).  The caller copies the status word afterwards.
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
@@ -1108,30 +1143,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     }
     if (p->general_h0) return enqueue_general(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx, mk);
     if (p->dense) {
-        grape_dense::DenseBatch DB{};
-        DB.nb = nb;
-        DB.x = d_x;
-        DB.E = p->dn_E;
-        DB.Q = p->dn_Q;
-        DB.Carry = p->dn_Carry;
-        DB.M = p->dn_M;
-        DB.Mc = p->dn_Mc;
-        DB.Z = p->dn_Z;
-        DB.Ub = p->dn_Ub;
-        DB.Zl = p->dn_Zl;
-        DB.Vc = p->dn_Vc;
-        DB.Sx = p->dn_Sx;
-        DB.Tot = p->dn_Tot;
-        DB.Me = p->dn_Me;
-        DB.Mp = p->dn_Mp;
-        DB.B0 = p->dn_B0;
-        DB.Fd2 = d_Fd2;
-        DB.Fd2dx = d_Fd2dx;
-        DB.F = d_F;
-        DB.Fdx = d_Fdx;
-        DB.status = p->d_ctrl + 2;
-        DB.mstats = nullptr;
-        DB.gp_scr = p->d_gpscr;
+        const grape_dense::DenseBatch DB = dense_batch(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx);
         HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, st, mk));
         return GRAPE_OK;
     }
@@ -1511,6 +1523,48 @@ int grape_fidelity_grad(grape_plan *p, int nbatch, const double *x, double *F, d
         if (rc) return rc;
     }
     return GRAPE_OK;
+}
+
+// Time sharding of one evaluation: see include/grape.h.
+static int slice_check(grape_plan *p) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    if (!p->dense || p->general_h0 || p->tables || p->P.ne > 0 || p->P.na > 0 || p->P.gen_proj || p->uses_tstep)
+        return fail(GRAPE_ERR_UNSUPPORTED, "time slices: dense-engine operator-basis plans without error sources, "
+                                           "x_add, a general projector or step-index terms");
+    const size_t T = (size_t)p->P.D * p->P.D;
+    if (!p->dn_Ub && dalloc(&p->dn_Ub, (size_t)p->max_batch * grape_dense::kImgDoubles) != hipSuccess)
+        return fail(GRAPE_ERR_ALLOC, "device allocation failed (time slices)");
+    if (!p->d_slice && dalloc(&p->d_slice, 2 * T) != hipSuccess)
+        return fail(GRAPE_ERR_ALLOC, "device allocation failed (time slices)");
+    return GRAPE_OK;
+}
+
+int grape_slice_forward(grape_plan *p, const double *x, double *U_slice) {
+    if (!p || !x || !U_slice) return fail(GRAPE_ERR_INVALID, "bad argument");
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = slice_check(p)) return rc;
+    const size_t T = (size_t)p->P.D * p->P.D;
+    hipStream_t st = p->stream;
+    HIPCHECK(hipMemcpyAsync(p->d_x, x, (size_t)p->P.nx * sizeof(double), hipMemcpyHostToDevice, st));
+    const grape_dense::DenseBatch DB = dense_batch(p, 1, p->d_x, p->d_F, p->d_Fdx, nullptr, nullptr);
+    HIPCHECK(grape_dense::launch_slice_forward(p->DP, DB, p->d_slice, st));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(U_slice, p->d_slice, T * sizeof(cd), hipMemcpyDeviceToHost, st));
+    return grape_plan_synchronize(p);
+}
+
+int grape_slice_gradient(grape_plan *p, const double *M_prime, double *F_dx) {
+    if (!p || !M_prime || !F_dx) return fail(GRAPE_ERR_INVALID, "bad argument");
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = slice_check(p)) return rc;
+    const size_t T = (size_t)p->P.D * p->P.D;
+    hipStream_t st = p->stream;
+    HIPCHECK(hipMemcpyAsync(p->d_slice + T, M_prime, T * sizeof(cd), hipMemcpyHostToDevice, st));
+    const grape_dense::DenseBatch DB = dense_batch(p, 1, p->d_x, p->d_F, p->d_Fdx, nullptr, nullptr);
+    HIPCHECK(grape_dense::launch_slice_gradient(p->DP, DB, p->d_slice + T, st));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(F_dx, p->d_Fdx, (size_t)p->P.np * p->P.Nt * sizeof(double), hipMemcpyDeviceToHost, st));
+    return grape_plan_synchronize(p);
 }
 
 int grape_fidelity_grad_tables(grape_plan *p, int nbatch, const double *x, const double *H, const double *U0,

@@ -1,0 +1,85 @@
+"""Time-sharded single evaluations on the MI355X (robustgrape_amd/timeshard.py,
+grape_slice_forward / grape_slice_gradient of include/grape.h).
+
+Slices run one after another on the one device ("virtual ranks"; the exchange over ranks is the
+gloo-tested code of tests/test_timeshard_cpu.py): F and F_dx of the sliced evaluation against the
+oracle (UnitaryCalculations.jl:20-155, FidelityCalculations.jl:19-119) and against a
+whole-evaluation call of the dense engine -- the same algebra with the chain products associated
+slice by slice, so F within T1 and F_dx within the FD tier."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+T1 = 1e-12
+T2, T2_ABS = 1e-6, 1e-7
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _check(test, F, Fdx, F0, g0, t2=T2, t2a=T2_ABS):
+    from tests.parity_log import record
+    ef = abs(float(F) - float(F0))
+    record(test, "F", ef, 1.0, T1)
+    assert ef <= T1, (test, F, F0)
+    err, scale = float(np.max(np.abs(Fdx - g0))), float(np.max(np.abs(g0)))
+    record(test, "F_dx", err, scale, t2 * scale + t2a)
+    print(f"{test}: |dF| {ef:.2e}  max|dF_dx| {err:.2e} (scale {scale:.2e})")
+    assert err <= t2 * scale + t2a, (test, err, scale)
+
+
+@pytest.mark.parametrize("nslices", [1, 2, 3, 4])
+def test_sliced_evaluation_matches_oracle_and_whole_call(nslices):
+    from oracle import grape_oracle as O
+    from robustgrape_amd.engine import GrapePlan
+    from robustgrape_amd.synthetic import dense_problem, dense_x
+    from robustgrape_amd.timeshard import time_sharded_fidelity_grad
+    fp = dense_problem(d=16, ntimes=48, dt=0.3, rank=6)
+    x = dense_x(ntimes=48, seed=5)
+    F, Fdx = time_sharded_fidelity_grad(fp, x, nparam=2, nslices=nslices)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fp, x)[:2]
+    _check(f"timeshard_d16_s{nslices}_oracle", F, Fdx, F0, np.asarray(g0))
+    pl = GrapePlan(fp, 2, max_batch=1)
+    try:
+        Fw, gw = pl.fidelity_grad(x[None, :])[:2]
+    finally:
+        pl.close()
+    _check(f"timeshard_d16_s{nslices}_whole", F, Fdx, Fw[0], gw[0])
+
+
+def test_c5_sliced_eight_ways_matches_whole_call():
+    """C5 itself (d = 64, N_t = 1 024, np = 2) in 8 slices of 128 steps -- the 8-GPU layout --
+    against one whole-evaluation call and the committed C5 golden."""
+    import os
+    from robustgrape_amd.engine import GrapePlan
+    from robustgrape_amd.synthetic import dense_problem
+    from robustgrape_amd.timeshard import time_sharded_fidelity_grad
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5.npz"),
+                     allow_pickle=False))
+    fp = dense_problem()
+    x = g["x"]
+    F, Fdx = time_sharded_fidelity_grad(fp, x, nparam=2, nslices=8)
+    _check("timeshard_c5_golden", F, Fdx, float(g["F"]), g["F_dx"])
+    pl = GrapePlan(fp, 2, max_batch=1)
+    try:
+        Fw, gw = pl.fidelity_grad(x[None, :])[:2]
+    finally:
+        pl.close()
+    _check("timeshard_c5_whole", F, Fdx, Fw[0], gw[0])
+
+
+def test_slices_refuse_unsupported_plans():
+    """Slice calls need the dense engine (12 < d <= 64) without x_add / error sources."""
+    from robustgrape_amd._capi import GrapeError
+    from robustgrape_amd.synthetic import dense_problem
+    from robustgrape_amd.timeshard import SlicePlan
+    sp = SlicePlan(dense_problem(d=8, ntimes=8, dt=0.3, rank=4), 2, 0, 8)  # d <= 12: the small engine
+    try:
+        with pytest.raises(GrapeError):
+            sp.forward(np.zeros(16))
+    finally:
+        sp.close()
