@@ -55,7 +55,10 @@ int fail(int code, const std::string &msg) {
 constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScanNarrow,
               kScanTiny = grape_host::kScanTiny, kScanLatency = grape_host::kScanLatency;
 // calls of at most this many evaluations run the two sector classes on two streams (enqueue)
-constexpr int kForkMaxBatch = 4096;
+#ifndef GRAPE_FORK_MAX_BATCH
+#define GRAPE_FORK_MAX_BATCH 4096
+#endif
+constexpr int kForkMaxBatch = GRAPE_FORK_MAX_BATCH;
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
