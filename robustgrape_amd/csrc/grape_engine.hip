@@ -1012,7 +1012,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             const size_t ne = (size_t)P.ne, R2 = (P.ne > 0 || Ps.walk) ? 0 : R;  // k_expm_grad parking: no error sources only
             const size_t RE = Ps.walk ? 0 : R;  // the walks store no E / Q
             const size_t lanes_pad = (MB * Ps.nchunks + grape::kWalkBlockA - 1) / grape::kWalkBlockA * grape::kWalkBlockA;
-            if (Ps.walk_store_e && dalloc(&b.Ew, (size_t)sc.nsec * Ps.L * TS * lanes_pad) != hipSuccess)
+            // stored propagators: D*D elements + the diagonal shift per (step, sector) (grape_walk.hpp kEwStride)
+            if (Ps.walk_store_e && dalloc(&b.Ew, (size_t)sc.nsec * Ps.L * (TS + 1) * lanes_pad) != hipSuccess)
                 return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sector walks)"));
             if (Ps.walk && !p->d_xT && dalloc(&p->d_xT, MB * P.nx) != hipSuccess)
                 return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sector walks)"));

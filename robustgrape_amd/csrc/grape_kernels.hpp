@@ -137,7 +137,7 @@ struct DevBatch {
     // chunk walks (grape_walk.hpp): k_scan starts from the chunk totals in Tc when it is set
     cd *Tc;                 // [nb][nchunks][D][D] row-major chunk totals T_c (k_walk_fwd), else null
     cd *wscr;               // [nsec][nb / nsec][nchunks][2][D][D] per-lane scratch of the squaring path
-    cd *Ew;                 // walk_store_e: [nsec/NS][L][NS][D*D][lanes] nominal E_k, lane-minor (coalesced)
+    cd *Ew;                 // walk_store_e: [nsec/NS][L][NS][D*D + 1][lanes] shifted E~_k and its shift, lane-minor
 };
 
 // Trig of the last argument seen by one builder: the operator bases pair cos(arg) and sin(arg)

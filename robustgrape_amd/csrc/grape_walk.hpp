@@ -24,8 +24,9 @@
 // Hermitian), A^2 Hermitian and A^3 skew-Hermitian, so each is kept COMPRESSED: its diagonal
 // (the imaginary / real parts) and strict upper triangle -- 16 instead of 32 doubles at D = 4,
 // and every product with a diagonal entry is 2 FMAs instead of 4.  The exponential is the
-// row-group kernels' solve-free Taylor evaluation (Paterson-Stockmeyer in A^3; degree 12, or 6
-// when the |re|+|im| column bound is <= 0.015), column by column: column i of exp(A) needs
+// row-group kernels' solve-free Taylor evaluation (Paterson-Stockmeyer in A^3; degree 12, 9 or 6
+// by the |re|+|im| column bound of A shifted by the midpoint of its diagonal, sm_regime), column
+// by column: column i of exp(A) needs
 // only column i of A, A^2 and the running vector, so no full matrix is materialised for it.
 // Above the Taylor-12 range (exact 1-norm > 0.25) the lane scales A by 2^-s so that
 // |A / 2^s|_1 <= 0.25 and squares s times (Higham's scaling and squaring on the same Taylor
@@ -155,14 +156,19 @@ __device__ __forceinline__ void sm_cube(const SM<D> &A, SM<D> &A2, SM<D> &A3) {
     }
 }
 
+// The top coefficients of a Paterson-Stockmeyer evaluation in A^3 with nst Horner steps
+// (degree 3 nst + 3: nst = 1, 2, 3 -> Taylor 6, 9, 12)
+__device__ __forceinline__ double ps_top(int nst, int m) {
+    return nst == 1 ? inv_fact(3 + m) : nst == 2 ? inv_fact(6 + m) : inv_fact(9 + m);
+}
+
 // x = column i of the Taylor polynomial, Paterson-Stockmeyer in A^3 (grape_device.hpp
-// expm_taylor): degree 12, or degree 6 when `small`.  B_j = c_3j I + c_3j+1 A + c_3j+2 A^2.
+// expm_taylor): degree 3 nst + 3 (12, 9 or 6).  B_j = c_3j I + c_3j+1 A + c_3j+2 A^2.
 template <int D>
-__device__ __forceinline__ void sm_taylor_col(bool small, int i, const SM<D> &A, const SM<D> &A2, const SM<D> &A3,
+__device__ __forceinline__ void sm_taylor_col(int nst, int i, const SM<D> &A, const SM<D> &A2, const SM<D> &A3,
                                               cd (&x)[D]) {
     {
-        const double k0 = small ? inv_fact(3) : inv_fact(9), k1 = small ? inv_fact(4) : inv_fact(10),
-                     k2 = small ? inv_fact(5) : inv_fact(11), k3 = small ? inv_fact(6) : inv_fact(12);
+        const double k0 = ps_top(nst, 0), k1 = ps_top(nst, 1), k2 = ps_top(nst, 2), k3 = ps_top(nst, 3);
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, sm_el<D, true>(A2, j, i), cscale(k3, sm_el<D, false>(A3, j, i))));
@@ -171,7 +177,7 @@ __device__ __forceinline__ void sm_taylor_col(bool small, int i, const SM<D> &A,
     }
 #pragma unroll
     for (int st = 2; st >= 0; --st) {
-        if (st == 0 || !small) {
+        if (st < nst) {
             cd t[D];
             sm_matvec<D, false>(A3, x, t);
             const double k0 = inv_fact(3 * st), k1 = inv_fact(3 * st + 1), k2 = inv_fact(3 * st + 2);
@@ -186,14 +192,44 @@ __device__ __forceinline__ void sm_taylor_col(bool small, int i, const SM<D> &A,
 }
 
 // Degree choice (grape_device.hpp expm_prologue_fast, per lane): 0 = diagonal (isdiag), 3 =
-// Taylor 6, 5 = Taylor 12, 13 = Taylor 12 of A / 2^s (A scaled here) and s squarings.
+// Taylor 6, 4 = Taylor 9, 5 = Taylor 12, 13 = Taylor 12 of A / 2^s (A scaled here) and s squarings.
+//
+// Diagonal shift (GRAPE_WALK_SHIFT): the walks exponentiate A - i mu I, i.e. they compute
+// E~ = e^{-i mu} exp(A), with mu (`choose`) the midpoint of the diagonal's imaginary parts, which
+// minimises the largest diagonal modulus -- the Rydberg 4-level sector (diagonal 0, 0, 0, B = 10)
+// drops from |A|_1 ~ 0.17 to ~ 0.09 and takes Taylor 9 (two Horner steps per column instead of
+// three).  The phase e^{i mu} is never multiplied in per step: every eps-variant of a step is
+// shifted by the nominal propagator's mu (choose = false), so E' - E = e^{i mu} (E~' - E~) and the
+// phase cancels in every sandwich the walks form (Y = X E^dag, X E^dag (E' - E), E X E^dag,
+// E^dag dX); only the chunk totals take e^{i sum mu} (walk_phase).  The thresholds bound the
+// Taylor remainder sum_{k > m} |A|^k / k! by ~3e-17 (0.015 at m = 6, 0.1 at m = 9; 2.4e-18 at
+// 0.25, m = 12).  A diagonal A (kind 0) keeps mu = 0 when choosing.
+#ifndef GRAPE_WALK_SHIFT
+#define GRAPE_WALK_SHIFT 1
+#endif
 template <int D>
-__device__ __forceinline__ int sm_regime(SM<D> &A, int &s) {
+__device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choose) {
     s = 0;
     bool off = false;
 #pragma unroll
     for (int t = 0; t < SM<D>::NU; ++t) off = off || A.u[t].re != 0.0 || A.u[t].im != 0.0;
-    if (!off) return 0;
+    if (choose) {
+        mu = 0.0;
+#if GRAPE_WALK_SHIFT
+        if (off) {
+            double lo = A.d[0], hi = A.d[0];
+#pragma unroll
+            for (int j = 1; j < D; ++j) {
+                lo = fmin(lo, A.d[j]);
+                hi = fmax(hi, A.d[j]);
+            }
+            mu = 0.5 * (lo + hi);
+        }
+#endif
+    }
+    if (!off) return 0;  // (walk_expm shifts the diagonal itself)
+#pragma unroll
+    for (int j = 0; j < D; ++j) A.d[j] -= mu;  // exact for mu = 0
     double nub = 0.0;
 #pragma unroll
     for (int c = 0; c < D; ++c) {
@@ -206,6 +242,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s) {
         nub = c == 0 ? ub : fmax(nub, ub);
     }
     if (nub <= 0.015) return 3;
+    if (GRAPE_WALK_SHIFT && nub <= 0.1) return 4;
     if (nub <= 0.25) return 5;
     double nA = 0.0;  // Julia's opnorm(A, 1)
 #pragma unroll
@@ -219,6 +256,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s) {
         nA = c == 0 ? cs : fmax(nA, cs);
     }
     if (nA <= 0.015) return 3;
+    if (GRAPE_WALK_SHIFT && nA <= 0.1) return 4;
     if (nA <= 0.25) return 5;
     if (!(nA <= 1e300)) return 5;  // NaN / Inf: propagates through the polynomial
     s = (int)ceil(log2(nA * 4.0));  // |A / 2^s|_1 <= 0.25
@@ -233,7 +271,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s) {
 // x = column i of the same polynomial without a stored A^2: column i of A^2 is A (A e_i), one
 // matrix-vector product per column (+56 FMAs at D = 4) for 32 fewer live registers.
 template <int D>
-__device__ __forceinline__ void sm_taylor_col_na2(bool small, int i, const SM<D> &A, const SM<D> &A3, cd (&x)[D]) {
+__device__ __forceinline__ void sm_taylor_col_na2(int nst, int i, const SM<D> &A, const SM<D> &A3, cd (&x)[D]) {
     cd a2[D];  // column i of A is read from A itself (no copy)
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -243,8 +281,7 @@ __device__ __forceinline__ void sm_taylor_col_na2(bool small, int i, const SM<D>
         a2[j] = c;
     }
     {
-        const double k0 = small ? inv_fact(3) : inv_fact(9), k1 = small ? inv_fact(4) : inv_fact(10),
-                     k2 = small ? inv_fact(5) : inv_fact(11), k3 = small ? inv_fact(6) : inv_fact(12);
+        const double k0 = ps_top(nst, 0), k1 = ps_top(nst, 1), k2 = ps_top(nst, 2), k3 = ps_top(nst, 3);
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, a2[j], cscale(k3, sm_el<D, false>(A3, j, i))));
@@ -253,7 +290,7 @@ __device__ __forceinline__ void sm_taylor_col_na2(bool small, int i, const SM<D>
     }
 #pragma unroll
     for (int st = 2; st >= 0; --st) {
-        if (st == 0 || !small) {
+        if (st < nst) {
             cd t[D];
             sm_matvec<D, false>(A3, x, t);
             const double k0 = inv_fact(3 * st), k1 = inv_fact(3 * st + 1), k2 = inv_fact(3 * st + 2);
@@ -273,15 +310,18 @@ __device__ __forceinline__ void sm_taylor_col_na2(bool small, int i, const SM<D>
 // common path.  FENCE: pin every column and keep the scheduler from overlapping them (register
 // discipline at D = 4; at D <= 3 the columns and sectors may interleave for ILP).  KEEP_A2:
 // keep A^2 through the column loop (else regenerate its columns, sm_taylor_col_na2).
+// mu: the diagonal shift (sm_regime): chosen here and returned (choose), or the nominal's (an
+// eps-variant); the columns are those of E~ = exp(A - i mu I).
 template <int D, bool FENCE, bool KEEP_A2, class Sink>
-__device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
+__device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, double &mu, bool choose, Sink &&sink) {
     int s = 0;
-    const int kind = sm_regime<D>(A, s);
+    const int kind = sm_regime<D>(A, s, mu, choose);
     if (kind == 0) {  // isdiag(A): exp of the diagonal (Julia's fast path)
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             cd x[D];
-            const double sn = sin(A.d[i]), cn = cos(A.d[i]);  // exp(0) (cos, sin), as the row-group path
+            const double a = A.d[i] - mu;  // (exact for mu = 0)
+            const double sn = sin(a), cn = cos(a);  // exp(0) (cos, sin), as the row-group path
 #pragma unroll
             for (int j = 0; j < D; ++j) x[j] = (j == i) ? cmake(cn, sn) : czero();
             if (FENCE) pin<D>(x);
@@ -291,16 +331,16 @@ __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
     }
     SM<D> A2, A3;
     sm_cube<D>(A, A2, A3);
-    auto col = [&](bool small, int i, cd (&x)[D]) {
-        if constexpr (KEEP_A2) sm_taylor_col<D>(small, i, A, A2, A3, x);
-        else sm_taylor_col_na2<D>(small, i, A, A3, x);
+    auto col = [&](int nst, int i, cd (&x)[D]) {
+        if constexpr (KEEP_A2) sm_taylor_col<D>(nst, i, A, A2, A3, x);
+        else sm_taylor_col_na2<D>(nst, i, A, A3, x);
     };
     if (kind != 13) {
-        const bool small = kind == 3;
+        const int nst = kind == 3 ? 1 : kind == 4 ? 2 : 3;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             cd x[D];
-            col(small, i, x);
+            col(nst, i, x);
             sink(i, x);
             if (FENCE) __builtin_amdgcn_sched_barrier(0);
         }
@@ -310,7 +350,7 @@ __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, Sink &&sink) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {  // (unrolled: register arrays are only ever indexed by constants)
         cd x[D];
-        col(false, i, x);
+        col(3, i, x);
 #pragma unroll
         for (int j = 0; j < D; ++j) T[i * D + j] = x[j];
     }
@@ -596,6 +636,33 @@ struct WalkCfg {
     static constexpr bool IMG_LDS = D >= 4 && GRAPE_WALK_IMG_LDS;      // k_walk_img: eps2 propagators in LDS
 };
 
+// The chunk's phase: sum of the steps' diagonal shifts (sm_regime), TwoSum-compensated; the chunk
+// total is e^{i phi} Q~ with Q~ the product of the shifted propagators.
+struct WalkPhase {
+    double hi = 0.0, lo = 0.0;
+    __device__ __forceinline__ void add(double m) {  // (adding 0 is exact: steps past N_t)
+        const double t = hi + m, bp = t - hi;
+        lo += (hi - (t - bp)) + (m - bp);
+        hi = t;
+    }
+};
+template <int D>
+__device__ __forceinline__ void walk_phase(const WalkPhase &ph, cd (&Q)[D][D]) {
+    const double phi = ph.hi + ph.lo;
+    if (phi == 0.0) return;  // (no shift: Q~ is the total)
+    double sn, cn;
+    sincos(phi, &sn, &cn);
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) Q[j][i] = cmul(cmake(cn, sn), Q[j][i]);
+    }
+}
+// Stored propagators (B.Ew): per (step, sector) the D*D elements of E~ and, as element D*D, the
+// shift mu (real part), each element one coalesced row over the launch's lanes.
+template <int D>
+constexpr int kEwStride = D * D + 1;
+
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
 template <int D, int NS, bool STORE>
 __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
@@ -621,6 +688,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     const int k0 = L.c * P.L;
     X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
     cd Q[NS][D][D];
+    WalkPhase ph[NS];
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
 #pragma unroll
@@ -639,17 +707,20 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         walk_build<D, NS>(P, ops, X, k + 1, none, A);
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
-            walk_expm<D, C::FENCE_FWD, true>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+            double mu;
+            walk_expm<D, C::FENCE_FWD, true>(A[w], scr + (size_t)w * 2 * TS, mu, true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
             });
+            ph[w].add(act ? mu : 0.0);
             if constexpr (STORE) {  // the gradient walk's copy: lane-minor, one coalesced 1-KB store per element
-                cd *ew = B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * TS) * lanes + lane;
+                cd *ew = B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * kEwStride<D>) * lanes + lane;
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
 #pragma unroll
                     for (int i = 0; i < D; ++i) ew[(size_t)(j * D + i) * lanes] = E.at(j, i);
                 }
+                ew[(size_t)TS * lanes] = cmake(mu, 0.0);
             }
 #pragma unroll
             for (int i = 0; i < D; ++i) {  // column i of E_k Q (in place: it reads only column i)
@@ -672,6 +743,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     if (L.ok) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
+            walk_phase<D>(ph[w], Q[w]);
             cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
             for (int j = 0; j < D; ++j) {
@@ -716,8 +788,9 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
         else E[0].p = MStore<D, true>::slot(lds);
     }
     const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
-    auto ew = [&](int jj, int w) { return B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * TS) * lanes + lane; };
+    auto ew = [&](int jj, int w) { return B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * kEwStride<D>) * lanes + lane; };
     cd En[STORED ? NS : 1][D][D];  // the next step's stored propagators (STORED)
+    double mun[NS], mu[NS];        // ... and their shifts; this step's shifts
     if constexpr (STORED) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
@@ -727,6 +800,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
                 for (int i = 0; i < D; ++i) En[w][j][i] = src[(size_t)(j * D + i) * lanes];
             }
+            mun[w] = src[(size_t)TS * lanes].re;
         }
     }
     // X = M'_c = Carry_c M_ww Carry_c^dagger from the carry and the head's sector block (k_sec_mc's
@@ -773,6 +847,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
                     for (int i = 0; i < D; ++i) E[w].set(j, i, En[w][j][i]);
                 }
+                mu[w] = mun[w];
             }
             const int jn = jj + 1 < P.L ? jj + 1 : jj;
 #pragma unroll
@@ -783,13 +858,14 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
                     for (int i = 0; i < D; ++i) En[w][j][i] = src[(size_t)(j * D + i) * lanes];
                 }
+                mun[w] = src[(size_t)TS * lanes].re;
             }
         } else {
             SM<D> A[NS];
             walk_build<D, NS>(P, ops, XV, k + 1, none, A);
 #pragma unroll
             for (int w = 0; w < NS; ++w)
-                walk_expm<D, C::FENCE, C::KEEP_A2_NOM>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+                walk_expm<D, C::FENCE, C::KEEP_A2_NOM>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                     for (int j = 0; j < D; ++j) E[w].set(j, i, x[j]);
                 });
@@ -821,7 +897,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
                 double s = 0.0;
-                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(Ap[w], scr + (size_t)w * 2 * TS, [&](int j, const cd (&x)[D]) {
+                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(Ap[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int j, const cd (&x)[D]) {
                     const auto &Yj = X[w].opaque();  // row j of Y and column j of E read here, after
                     const auto &Ej = E[w].opaque();  // column j of E'
 #pragma unroll
@@ -946,6 +1022,8 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     // Q_{k-1} (chunk-local), E_k, and the step's eps2 propagators E(x + eps2), E(err_e eps2) (the
     // latter two in the lane's LDS slots at D = 4, where the registers run out)
     cd Q[NS][D][D], E[NS][D][D];
+    WalkPhase ph[NS];
+    double mu[NS];  // this step's diagonal shifts (every variant takes the nominal's)
     constexpr bool EL = C::IMG_LDS;
     MStore<D, EL> Ed2[NS], Ee2[NS];
     if constexpr (EL) {
@@ -972,11 +1050,13 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
             SM<D> A[NS];
             walk_build<D, NS>(P, ops, X, k + 1, none, A);
 #pragma unroll
-            for (int w = 0; w < NS; ++w)
-                walk_expm<D, C::FENCE, true>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+            for (int w = 0; w < NS; ++w) {
+                walk_expm<D, C::FENCE, true>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                     for (int j = 0; j < D; ++j) E[w][j][i] = x[j];
                 });
+                ph[w].add(act ? mu[w] : 0.0);
+            }
         }
         // one variant: its exponential, and (IMG_DIFF / IMG_MIX) the image of its difference to slot
         auto variant = [&](auto kind, int v, int slot) {
@@ -987,7 +1067,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
                 if constexpr (KIND == IMG_KEEP_D2 || KIND == IMG_KEEP_E2) {
-                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                         for (int j = 0; j < D; ++j) {
                             if constexpr (KIND == IMG_KEEP_D2) Ed2[w].set(j, i, x[j]);
@@ -996,7 +1076,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
                     });
                 } else {
                     cd Z[D][D];  // E_k^dag dX, column by column as the variant's columns come out
-                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, [&](int i, const cd (&x)[D]) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int i, const cd (&x)[D]) {
                         cd dx[D];
                         const auto &e2 = Ee2[w].opaque();  // (LDS reads issued here, not hoisted)
                         const auto &d2 = Ed2[w].opaque();
@@ -1070,6 +1150,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     if (L.ok) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
+            walk_phase<D>(ph[w], Q[w]);
             cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
             for (int j = 0; j < D; ++j) {
