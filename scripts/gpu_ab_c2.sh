@@ -19,6 +19,6 @@ for v in "$@"; do
   python3 -c "
 import json
 d=json.loads([l for l in open('$O/ab_${TAG}_$v.log') if l.startswith('{')][-1])
-print('$v', round(d['value']), {k: round(x,3) for k,x in d['kernels_ms_per_pass'].items()}, round(d['roofline']['frac'],3))
+k = d.get('kernels_ms_per_pass') or d.get('kernels_ms_per_step', {}); print('$v', round(d['value']), {n: round(x, 3) for n, x in k.items()}, round(d['roofline']['frac'], 3) if 'roofline' in d else d.get('kernels_frac'))
 "
 done
