@@ -177,7 +177,7 @@ __device__ __forceinline__ void sm_taylor_col(int nst, int i, const SM<D> &A, co
     }
 #pragma unroll
     for (int st = 2; st >= 0; --st) {
-        if (st < nst) {
+        if (st == 0 || st < nst) {  // (the last step unconditionally: no branch around it)
             cd t[D];
             sm_matvec<D, false>(A3, x, t);
             const double k0 = inv_fact(3 * st), k1 = inv_fact(3 * st + 1), k2 = inv_fact(3 * st + 2);
@@ -207,7 +207,7 @@ __device__ __forceinline__ void sm_taylor_col(int nst, int i, const SM<D> &A, co
 #ifndef GRAPE_WALK_SHIFT
 #define GRAPE_WALK_SHIFT 1
 #endif
-template <int D>
+template <int D, bool SHIFT>
 __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choose) {
     s = 0;
     bool off = false;
@@ -216,7 +216,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choo
     if (choose) {
         mu = 0.0;
 #if GRAPE_WALK_SHIFT
-        if (off) {
+        if (SHIFT && off) {
             double lo = A.d[0], hi = A.d[0];
 #pragma unroll
             for (int j = 1; j < D; ++j) {
@@ -228,8 +228,10 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choo
 #endif
     }
     if (!off) return 0;  // (walk_expm shifts the diagonal itself)
+    if (SHIFT) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) A.d[j] -= mu;  // exact for mu = 0
+        for (int j = 0; j < D; ++j) A.d[j] -= mu;  // exact for mu = 0
+    }
     double nub = 0.0;
 #pragma unroll
     for (int c = 0; c < D; ++c) {
@@ -242,7 +244,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choo
         nub = c == 0 ? ub : fmax(nub, ub);
     }
     if (nub <= 0.015) return 3;
-    if (GRAPE_WALK_SHIFT && nub <= 0.1) return 4;
+    if (GRAPE_WALK_SHIFT && SHIFT && nub <= 0.1) return 4;
     if (nub <= 0.25) return 5;
     double nA = 0.0;  // Julia's opnorm(A, 1)
 #pragma unroll
@@ -256,7 +258,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choo
         nA = c == 0 ? cs : fmax(nA, cs);
     }
     if (nA <= 0.015) return 3;
-    if (GRAPE_WALK_SHIFT && nA <= 0.1) return 4;
+    if (GRAPE_WALK_SHIFT && SHIFT && nA <= 0.1) return 4;
     if (nA <= 0.25) return 5;
     if (!(nA <= 1e300)) return 5;  // NaN / Inf: propagates through the polynomial
     s = (int)ceil(log2(nA * 4.0));  // |A / 2^s|_1 <= 0.25
@@ -290,7 +292,7 @@ __device__ __forceinline__ void sm_taylor_col_na2(int nst, int i, const SM<D> &A
     }
 #pragma unroll
     for (int st = 2; st >= 0; --st) {
-        if (st < nst) {
+        if (st == 0 || st < nst) {  // (the last step unconditionally: no branch around it)
             cd t[D];
             sm_matvec<D, false>(A3, x, t);
             const double k0 = inv_fact(3 * st), k1 = inv_fact(3 * st + 1), k2 = inv_fact(3 * st + 2);
@@ -312,10 +314,10 @@ __device__ __forceinline__ void sm_taylor_col_na2(int nst, int i, const SM<D> &A
 // keep A^2 through the column loop (else regenerate its columns, sm_taylor_col_na2).
 // mu: the diagonal shift (sm_regime): chosen here and returned (choose), or the nominal's (an
 // eps-variant); the columns are those of E~ = exp(A - i mu I).
-template <int D, bool FENCE, bool KEEP_A2, class Sink>
+template <int D, bool FENCE, bool KEEP_A2, bool SHIFT, class Sink>
 __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, double &mu, bool choose, Sink &&sink) {
     int s = 0;
-    const int kind = sm_regime<D>(A, s, mu, choose);
+    const int kind = sm_regime<D, SHIFT>(A, s, mu, choose);
     if (kind == 0) {  // isdiag(A): exp of the diagonal (Julia's fast path)
 #pragma unroll
         for (int i = 0; i < D; ++i) {
@@ -634,6 +636,10 @@ struct WalkCfg {
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? 1 : GRAPE_WALK_G4S_WAVES;
     static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? 3 : 2) : 1;  // k_walk_img (error sources)
     static constexpr bool IMG_LDS = D >= 4 && GRAPE_WALK_IMG_LDS;      // k_walk_img: eps2 propagators in LDS
+    // the diagonal shift + Taylor 9 (sm_regime) for the 4-level class only: it pays where the
+    // Taylor-12 columns dominate; the smaller classes (Taylor 6 at C2) measured slower with its
+    // bookkeeping (k_walk_fwd<2,2> 0.295 -> 0.34 ms per pass) and keep the unshifted walk bitwise
+    static constexpr bool SHIFT = D >= 4;
 };
 
 // The chunk's phase: sum of the steps' diagonal shifts (sm_regime), TwoSum-compensated; the chunk
@@ -708,11 +714,11 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
             double mu;
-            walk_expm<D, C::FENCE_FWD, true>(A[w], scr + (size_t)w * 2 * TS, mu, true, [&](int i, const cd (&x)[D]) {
+            walk_expm<D, C::FENCE_FWD, true, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu, true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
             });
-            ph[w].add(act ? mu : 0.0);
+            if constexpr (C::SHIFT) ph[w].add(act ? mu : 0.0);
             if constexpr (STORE) {  // the gradient walk's copy: lane-minor, one coalesced 1-KB store per element
                 cd *ew = B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * kEwStride<D>) * lanes + lane;
 #pragma unroll
@@ -743,7 +749,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     if (L.ok) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
-            walk_phase<D>(ph[w], Q[w]);
+            if constexpr (C::SHIFT) walk_phase<D>(ph[w], Q[w]);
             cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
             for (int j = 0; j < D; ++j) {
@@ -865,7 +871,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
             walk_build<D, NS>(P, ops, XV, k + 1, none, A);
 #pragma unroll
             for (int w = 0; w < NS; ++w)
-                walk_expm<D, C::FENCE, C::KEEP_A2_NOM>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
+                walk_expm<D, C::FENCE, C::KEEP_A2_NOM, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                     for (int j = 0; j < D; ++j) E[w].set(j, i, x[j]);
                 });
@@ -897,7 +903,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
                 double s = 0.0;
-                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD>(Ap[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int j, const cd (&x)[D]) {
+                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD, C::SHIFT>(Ap[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int j, const cd (&x)[D]) {
                     const auto &Yj = X[w].opaque();  // row j of Y and column j of E read here, after
                     const auto &Ej = E[w].opaque();  // column j of E'
 #pragma unroll
@@ -1051,11 +1057,11 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
             walk_build<D, NS>(P, ops, X, k + 1, none, A);
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
-                walk_expm<D, C::FENCE, true>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
+                walk_expm<D, C::FENCE, true, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                     for (int j = 0; j < D; ++j) E[w][j][i] = x[j];
                 });
-                ph[w].add(act ? mu[w] : 0.0);
+                if constexpr (C::SHIFT) ph[w].add(act ? mu[w] : 0.0);
             }
         }
         // one variant: its exponential, and (IMG_DIFF / IMG_MIX) the image of its difference to slot
@@ -1067,7 +1073,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
                 if constexpr (KIND == IMG_KEEP_D2 || KIND == IMG_KEEP_E2) {
-                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int i, const cd (&x)[D]) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                         for (int j = 0; j < D; ++j) {
                             if constexpr (KIND == IMG_KEEP_D2) Ed2[w].set(j, i, x[j]);
@@ -1076,7 +1082,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
                     });
                 } else {
                     cd Z[D][D];  // E_k^dag dX, column by column as the variant's columns come out
-                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG>(A[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int i, const cd (&x)[D]) {
+                    walk_expm<D, C::FENCE, C::KEEP_A2_IMG, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int i, const cd (&x)[D]) {
                         cd dx[D];
                         const auto &e2 = Ee2[w].opaque();  // (LDS reads issued here, not hoisted)
                         const auto &d2 = Ed2[w].opaque();
@@ -1150,7 +1156,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     if (L.ok) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
-            walk_phase<D>(ph[w], Q[w]);
+            if constexpr (C::SHIFT) walk_phase<D>(ph[w], Q[w]);
             cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
             for (int j = 0; j < D; ++j) {
