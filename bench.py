@@ -322,7 +322,7 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hb_frac, "traffic": traffic}
     else:
-        roof = {"bound": "mfma", "kernel": kname, "achieved": fp, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        roof = {"bound": "fp64-valu", "kernel": kname, "achieved": fp, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": fp_frac, "traffic": traffic,
                 "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"}
     roof.update({"traffic_unit": "HBM bytes per device pass (PMC)", "per_launch_ms": ms,
@@ -493,7 +493,7 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hb / HBM_PEAK_GBS}
     else:
-        roof = {"bound": "mfma", "kernel": kname, "achieved": fp, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        roof = {"bound": "fp64-valu", "kernel": kname, "achieved": fp, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": fp / FP64_PEAK_TFLOPS, "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"}
     roof.update({"traffic": traffic, "traffic_unit": "HBM bytes per device pass (PMC)", "per_launch_ms": ms,
                  "per_launch_note": "per device pass of evals_per_device_pass evaluations (all sector classes)",

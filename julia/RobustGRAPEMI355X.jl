@@ -1,21 +1,38 @@
 # RobustGRAPEMI355X.jl -- ccall shim that routes RobustGRAPE.jl's hot path to libgrape.so.
 #
-# Keeps the reference's names and argument types (src/RobustGRAPE.jl:6-13): the entry points
-# take the reference's own problem structs (src/Types.jl:12-56), and an `OperatorBasis` is a
-# `Function`, so it can be stored in their `H0::Function`, `Herror::Function` and
-# `target_unitary::Function` fields (Types.jl:13,35,55).  A FidelityRobustGRAPEProblem whose H0,
-# error sources and target are OperatorBasis objects evaluates on the MI355X through
-# include/grape.h; plain closures take the host-table fallback.  Julia is not installed in the
-# build image, so this file is not executed there; the same C entry points are exercised from
-# Python by tests/ and tests/test_julia_shim.py checks this file's signatures statically.
+# The shim EXTENDS the reference's generic functions (src/RobustGRAPE.jl:9-10) with methods for
+# `x::Vector{Float64}` -- more specific than the reference's `x::Vector{<:Real}`
+# (UnitaryCalculations.jl:20,180, FidelityCalculations.jl:19,368), so dispatch picks them for every
+# Float64 control vector, including the calls the reference makes itself:
+#   optimize_fidelity_and_error_sources -> calculate_common! -> calculate_fidelity_and_derivatives
+#                                                             (FidelityCalculations.jl:174-216, :177)
+#   calculate_fidelity_response(_fft) -> calculate_interaction_error_operators (:246-343)
+# so `using RobustGRAPE, RobustGRAPEMI355X` is all a user adds (INTEGRATION.md section 2).  Other
+# element types (e.g. Vector{Int}) keep the reference's CPU methods; convert with Float64.(x).
+# This is deliberate type piracy on RobustGRAPE's own generics: the shim's purpose is to replace
+# their implementation.  The entry points take the reference's own problem structs
+# (src/Types.jl:12-56), and an `OperatorBasis` is a `Function`, so it can be stored in their
+# `H0::Function`, `Herror::Function` and `target_unitary::Function` fields (Types.jl:13,35,55).
+# A FidelityRobustGRAPEProblem whose H0, error sources and target are OperatorBasis objects
+# evaluates on the MI355X through include/grape.h; plain closures take the host-table fallback
+# (the closures run on the host, the exponentials and traces on the device).  Julia is not
+# installed in the build image, so this file is not executed there; the same C entry points are
+# exercised from Python by tests/, and tests/test_julia_shim.py checks this file statically.
 module RobustGRAPEMI355X
 
 using LinearAlgebra
 import RobustGRAPE
-using RobustGRAPE: ErrorSource, UnitaryRobustGRAPEProblem, FidelityRobustGRAPEProblem
+using RobustGRAPE: ErrorSource, UnitaryRobustGRAPEProblem, FidelityRobustGRAPEProblem,
+                   FidelityRobustGRAPEParameters, optimize_fidelity_and_error_sources
+# the reference's generics: methods are ADDED to these (no new functions of the same names)
+import RobustGRAPE: calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
+                    calculate_interaction_error_operators, calculate_expectation_values
 
-export OperatorTerm, OperatorBasis, calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
-       calculate_interaction_error_operators, calculate_expectation_values, grape_expm_batch
+# (the re-exported names are RobustGRAPE's own bindings: no clash with `using RobustGRAPE`)
+export OperatorTerm, OperatorBasis, grape_expm_batch, plan_sectors, rydberg_full_operator_basis, cz_full_target,
+       calculate_fidelity_and_derivatives, calculate_unitary_and_derivatives,
+       calculate_interaction_error_operators, calculate_expectation_values,
+       optimize_fidelity_and_error_sources
 
 const libgrape = normpath(joinpath(@__DIR__, "..", "robustgrape_amd", "libgrape.so"))
 const GRAPE_ABI_VERSION = 7  # include/grape.h
@@ -76,6 +93,33 @@ end
 (B::OperatorBasis)(nt, x, x_add, err) = err * sum(_coef(t, nt, x, x_add) * t.op for t in B.terms)
 (B::OperatorBasis)(x_add) = sum(_coef(t, 1, Float64[], x_add) * t.op for t in B.terms)
 
+# Operator-basis forms of the reference's d = 9 Rydberg model and CZ target
+# (src/RydbergTools.jl:118-130, 197-203), as robustgrape_amd/rydberg.py builds them:
+# H(ϕ) = cos ϕ Hc + sin ϕ Hs + Hd, the e^{-iϕ} couplings above the diagonal.
+const _FULL_COUPLINGS = ((2, 5, 1), (3, 6, 2), (4, 7, 1), (4, 8, 2), (7, 9, 2), (8, 9, 1))  # (row, col, which Ω)
+"rydberg_hamiltonian_full(x[param], Ω1, Ω2, δ1, δ2, B) as an OperatorBasis (RydbergTools.jl:118)."
+function rydberg_full_operator_basis(; Ω1::Real=1.0, Ω2::Real=1.0, δ1::Real=0.0, δ2::Real=0.0, B::Real=10.0,
+                                     param::Integer=1)
+    Hc = zeros(ComplexF64, 9, 9); Hs = zeros(ComplexF64, 9, 9)
+    for (r, c, w) in _FULL_COUPLINGS
+        s = (w == 1 ? Ω1 : Ω2) / 2
+        Hc[r, c] += s; Hc[c, r] += s
+        Hs[r, c] += -im * s; Hs[c, r] += im * s
+    end
+    terms = [OperatorTerm(Hc; var=VAR_X, index=param, func=FN_COS), OperatorTerm(Hs; var=VAR_X, index=param, func=FN_SIN)]
+    hd = ComplexF64[0, 0, 0, 0, δ1, δ2, δ1, δ2, δ1 + δ2 + B]
+    any(!iszero, hd) && push!(terms, OperatorTerm(Matrix(Diagonal(hd))))
+    return OperatorBasis(terms)
+end
+"cz_with_1q_phase_full(x_add[index]) as an OperatorBasis (RydbergTools.jl:197-203)."
+function cz_full_target(; index::Integer=1, rydberg_dimension::Integer=5)
+    n = 4 + rydberg_dimension
+    e(ks) = Matrix{ComplexF64}(Diagonal([i in ks ? 1.0 : 0.0 for i in 1:n]))
+    return OperatorBasis([OperatorTerm(e((1,))),
+                          OperatorTerm(e((2, 3)); var=VAR_XADD, index=index, func=FN_CIS),
+                          OperatorTerm(e((4,)); var=VAR_XADD, index=index, func=FN_CIS, a=2.0, b=Float64(π))])
+end
+
 function _check(rc)
     rc == 0 || error("libgrape: " * unsafe_string(ccall((:grape_last_error, libgrape), Cstring, ())))
 end
@@ -135,17 +179,21 @@ function device_plan(fp::FidelityRobustGRAPEProblem, nparam::Int; device::Intege
 end
 
 const GRAPE_DESC_HOST_TABLES = Int32(1)
+const GRAPE_OPT_GENERAL_H0 = Int32(64)   # include/grape.h: the LU-inverted chain (UnitaryCalculations.jl:47)
 
-# Closure fallback (grape.h GRAPE_DESC_HOST_TABLES): no operator basis in the descriptor.
-function table_plan(fp::FidelityRobustGRAPEProblem, nparam::Int; device::Integer=0)
-    _cached(fp, nparam, :table) do
+# Closure fallback (grape.h GRAPE_DESC_HOST_TABLES): no operator basis in the descriptor.  The host
+# sees H0 only as tables, so `general` (a non-Hermitian nominal H0, e.g. a -iΓ/2 decay term:
+# _closure_options) selects the general-H0 path, as robustgrape_amd/engine.py general_h0_for does.
+function table_plan(fp::FidelityRobustGRAPEProblem, nparam::Int; device::Integer=0, general::Bool=false)
+    _cached(fp, nparam, general ? :table_general : :table) do
         up = fp.unitary_problem
         ne = length(up.error_sources)
         pdiag = Float64.(diag(fp.projector))
         pfull = _pfull(fp.projector)
+        opts = general ? GRAPE_OPT_GENERAL_H0 : Int32(0)
         desc = Ref(GrapeDesc(up.ndim, up.ntimes, nparam, up.nb_additional_param, ne, 0, up.t0, up.ϵ, up.ϵ2,
                              pointer(pdiag), C_NULL, 0, C_NULL, C_NULL, C_NULL, 0, C_NULL, 1,
-                             (GRAPE_DESC_HOST_TABLES, ntuple(_ -> Int32(0), 4)...), _pptr(pfull)))
+                             (GRAPE_DESC_HOST_TABLES, opts, Int32(0), Int32(0), Int32(0)), _pptr(pfull)))
         out = Ref{Ptr{Cvoid}}(C_NULL)
         GC.@preserve pdiag pfull begin
             _check(ccall((:grape_plan_create, libgrape), Cint, (Ref{GrapeDesc}, Cint, Ref{Ptr{Cvoid}}),
@@ -155,6 +203,28 @@ function table_plan(fp::FidelityRobustGRAPEProblem, nparam::Int; device::Integer
         finalizer(q -> ccall((:grape_plan_destroy, libgrape), Cvoid, (Ptr{Cvoid},), q.handle), p)
         p
     end
+end
+
+# Hermitian within rtol of the largest entry (robustgrape_amd/tables.py is_hermitian_h0); tables
+# of shape (d, d, ...)
+function _is_hermitian(H::AbstractArray{<:Complex}; rtol::Float64=1e-12)
+    isempty(H) && return true
+    d = size(H, 1); Hr = reshape(H, d, d, :)
+    dev = maximum(abs.(Hr .- conj.(permutedims(Hr, (2, 1, 3)))))
+    return dev <= rtol * max(maximum(abs.(Hr)), 1e-300)
+end
+
+# Which table plan a closure problem needs (engine.py general_h0_for): the fused kernels chain
+# with C_k^-1 = C_k^dagger, so a non-Hermitian nominal H0 takes the general path (up to 12
+# levels); above 12 levels every tabulated generator goes through the dense engine's
+# interchange-free solve, which needs them Hermitian, so anything else is refused.
+function _closure_general(up, H0s::AbstractArray, Hall::AbstractArray)
+    if up.ndim > 12
+        _is_hermitian(Hall) || error("closure problems above 12 levels need Hermitian H0 / H0 + Herror tables " *
+                                     "(the dense engine's exponential); non-Hermitian generators are served up to 12 levels")
+        return false
+    end
+    return !_is_hermitian(H0s)
 end
 
 # The closure calls of UnitaryCalculations.jl:45-95 and FidelityCalculations.jl:32-38, tabulated
@@ -232,15 +302,15 @@ function fidelity_wrapper(problem::UnitaryRobustGRAPEProblem)
 end
 
 "Drop-in for src/FidelityCalculations.jl:19-119: (F, F_dx_tot, F_d2err, F_d2err_dx_tot)."
-function calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::Vector{<:Real})
+function calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::Vector{Float64})
     up = fp.unitary_problem
     xm = length(x) - up.nb_additional_param
     @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
     if !is_operator_basis(fp)          # closure fallback
         np = xm ÷ up.ntimes
-        p = table_plan(fp, np)
         xv = Vector{Float64}(x)
         H, U0 = closure_tables(fp, xv, np)
+        p = table_plan(fp, np; general=_closure_general(up, H[:, :, 1, :], H))
         F = Ref{Float64}(0.0); F_dx = zeros(p.nx); F_d2err = zeros(p.nerr); F_d2err_dx = zeros(p.nx, p.nerr)
         GC.@preserve xv H U0 F_dx F_d2err F_d2err_dx begin
             _check(ccall((:grape_fidelity_grad_tables, libgrape), Cint,
@@ -262,7 +332,7 @@ function calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::V
 end
 
 "Drop-in for src/UnitaryCalculations.jl:20-155: (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add)."
-function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
+function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64})
     fp = fidelity_wrapper(problem)
     up = problem
     d, nt, na, ne = up.ndim, up.ntimes, up.nb_additional_param, length(up.error_sources)
@@ -273,8 +343,8 @@ function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x
     outs = (zeros(ComplexF64, d, d), zeros(ComplexF64, d, d, np, nt), zeros(ComplexF64, d, d, na),
             zeros(ComplexF64, d, d, ne), zeros(ComplexF64, d, d, np, nt, ne), zeros(ComplexF64, d, d, na, ne))
     if !is_operator_basis(fp)          # closure fallback
-        p = table_plan(fp, np)
         H, _ = closure_tables(fp, xv, np)
+        p = table_plan(fp, np; general=_closure_general(up, H[:, :, 1, :], H))
         GC.@preserve xv H outs begin
             _check(ccall((:grape_unitary_derivs_tables, libgrape), Cint,
                          (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64},
@@ -293,15 +363,15 @@ function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x
 end
 
 "Drop-in for src/UnitaryCalculations.jl:180-204: (ndim, ndim, ntimes, nerr)."
-function calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
+function calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64})
     fp = fidelity_wrapper(problem)
     up = problem
     np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
     O = zeros(ComplexF64, up.ndim, up.ndim, up.ntimes, length(up.error_sources))
     if !is_operator_basis(fp)          # closure fallback
-        p = table_plan(fp, np)
         H0, Oerr = closure_interaction_tables(up, xv, np)
+        p = table_plan(fp, np; general=_closure_general(up, H0, H0))
         GC.@preserve xv H0 Oerr O begin
             _check(ccall((:grape_interaction_error_operators_tables, libgrape), Cint,
                          (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Cint),
@@ -318,14 +388,14 @@ function calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProble
 end
 
 "Drop-in for src/FidelityCalculations.jl:368-390: (ntimes, nerr)."
-function calculate_expectation_values(fp::FidelityRobustGRAPEProblem, x::Vector{<:Real})
+function calculate_expectation_values(fp::FidelityRobustGRAPEProblem, x::Vector{Float64})
     up = fp.unitary_problem
     np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
     ev = zeros(Float64, up.ntimes, length(up.error_sources))
     if !is_operator_basis(fp)          # closure fallback
-        p = table_plan(fp, np)
         H0, Oerr = closure_interaction_tables(up, xv, np)
+        p = table_plan(fp, np; general=_closure_general(up, H0, H0))
         GC.@preserve xv H0 Oerr ev begin
             _check(ccall((:grape_expectation_values_tables, libgrape), Cint,
                          (Ptr{Cvoid}, Ptr{Float64}, Ptr{ComplexF64}, Ptr{ComplexF64}, Ptr{Float64}),

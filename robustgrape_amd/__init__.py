@@ -17,8 +17,8 @@ from . import rydberg as RydbergTools
 from .analysis import (calculate_expectation_values, calculate_fidelity_response, calculate_fidelity_response_fft,
                        calculate_interaction_error_operators)
 from .regularization import regularization_cost, regularization_cost_phase
-from .optimize import (OptimizationResult, minimizer, minimum, optimize_fidelity_and_error_sources,
-                       optimize_restarts)
+from .optimize import (LBFGS, GradientDescent, OptimizationResult, minimizer, minimum,
+                       optimize_fidelity_and_error_sources, optimize_restarts)
 
 # north-star aliases (BASELINE.json)
 FidelityOptimProblem = FidelityRobustGRAPEProblem
@@ -26,6 +26,7 @@ compute_fidelity_and_gradient = calculate_fidelity_and_derivatives
 compute_unitary_and_derivatives = calculate_unitary_and_derivatives
 
 __all__ = [
+    "LBFGS", "GradientDescent",
     "ErrorSource", "UnitaryRobustGRAPEProblem", "FidelityRobustGRAPEProblem", "FidelityRobustGRAPEParameters",
     "calculate_fidelity_and_derivatives", "calculate_unitary_and_derivatives", "GrapePlan", "get_plan",
     "clear_plans", "OperatorBasisHamiltonian", "OperatorBasisError", "OperatorBasisTarget", "Term",

@@ -299,6 +299,8 @@ def clear_plans():
                 p.close()
         _plan_cache.clear()
         _wrapped.clear()
+    from .timeshard import clear_slice_plans
+    clear_slice_plans()
 
 
 # UnitaryRobustGRAPEProblem -> a FidelityRobustGRAPEProblem around it (the descriptor needs

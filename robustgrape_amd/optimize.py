@@ -190,7 +190,7 @@ _LS_I32 = ("phase", "first", "accepted", "gconv", "fconv", "xconv", "lsfail", "a
 
 
 def _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, time_limit, x_reltol, g_reltol,
-                  f_calls_limit, callback) -> BatchResult:
+                  f_calls_limit, callback, steepest=False) -> BatchResult:
     """lbfgs_batched on the GPU: the same algorithm with its per-round state machine, the descent
     check and the L-BFGS update as HIP kernels (csrc/grape_lbfgs.hip, include/grape.h
     grape_lbfgs_state), one host sync per line-search round (the count of searching rows)."""
@@ -255,6 +255,9 @@ def _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, t
         if rnd == 0 and cnt == 0:  # no row searches any more
             break
         _capi.check(L.grape_lbfgs_step(sp, stream()))
+        if steepest:  # GradientDescent: drop the pair just stored (stream-ordered torch ops)
+            t["hist"].zero_()
+            t["gamma"].fill_(1.0)
         if callback is not None and bool(callback(t["X"], t["f"], t["g"], t["iters"])):
             break
     if hasattr(fun, "check"):  # deferred device status of the last evaluation (RobustCost)
@@ -268,17 +271,19 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
                   iterations: int = 1000, g_tol: float = 1e-8, f_abstol: float = 0.0, f_reltol: float = 0.0,
                   x_abstol: float = 0.0, time_limit: float = float("nan"), x_reltol: float = 0.0,
                   g_reltol: float = 0.0, f_calls_limit: int = 0,
-                  callback: Optional[Callable] = None) -> BatchResult:
+                  callback: Optional[Callable] = None, steepest: bool = False) -> BatchResult:
     """Minimise fun row-wise from every row of X0.
 
     fun(X, rows) -> (f (r,), g (r, n)) evaluates the rows `rows` (int64 indices into the
     batch) at control vectors X (r, n).  Rows stop independently (Optim's rules: |g|_inf <=
     max(g_tol, g_reltol |g_0|_inf), |df| <= f_abstol or f_reltol |f|, |dx|_inf <= x_abstol or
     x_reltol |x|_inf, f_calls_limit (0: none)).  callback(X, f, g, iters) runs after the initial
-    evaluation and after every iteration; a True return stops every row (Optim's callback)."""
+    evaluation and after every iteration; a True return stops every row (Optim's callback).
+    steepest: gradient descent (GradientDescent): the history is cleared after every step, so the
+    two-loop recursion returns D = -g (gamma = 1) and the same line search runs along it."""
     if X0.is_cuda and not _TORCH_LS and not _TORCH_TWO_LOOP and X0.dtype == torch.float64 and m <= 64:
         return _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, time_limit, x_reltol,
-                             g_reltol, f_calls_limit, callback)
+                             g_reltol, f_calls_limit, callback, steepest)
     t_start = time.perf_counter()
     X = X0.clone()
     R, n = X.shape
@@ -429,6 +434,9 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
         head = torch.where(upd, (head + 1) % m, head)
         hist = torch.where(upd, torch.clamp(hist + 1, max=m), hist)
         gamma = torch.where(upd, sy / _rowdot(y, y), gamma)
+        if steepest:  # GradientDescent: no curvature pairs, D = -g next iteration
+            hist = torch.zeros_like(hist)
+            gamma = torch.ones_like(gamma)
         fold = f.clone()
         X = torch.where(step[:, None], Xn, X)
         f = torch.where(step, fn, f)
@@ -600,6 +608,46 @@ def _call_reg(fn, xp: torch.Tensor):
             t([o[2] for o in outs]), torch.stack([t(o[3]) for o in outs]))
 
 
+@dataclass(frozen=True)
+class LBFGS:
+    """Optim.LBFGS(; m = 10) (the reference's default solver_algorithm, Types.jl:82): limited-memory
+    BFGS with m correction pairs and the s.y/y.y initial inverse-Hessian scaling."""
+    m: int = 10
+
+
+@dataclass(frozen=True)
+class GradientDescent:
+    """Optim.GradientDescent(): steepest descent, direction -g (no preconditioner), with this
+    module's strong-Wolfe line search in place of Optim's Hager-Zhang."""
+
+
+_SOLVER_NAMES = {"LBFGS": LBFGS, "GradientDescent": GradientDescent}
+
+
+def solver_config(algorithm):
+    """(history m, steepest) for FidelityRobustGRAPEParameters.solver_algorithm (Types.jl:82, used
+    at FidelityCalculations.jl:211-213).  Accepts LBFGS(m=...) / GradientDescent() instances, the
+    classes, or their names ("LBFGS", "LBFGS()", "GradientDescent", "GradientDescent()").  Any
+    other Optim.FirstOrderOptimizer (BFGS, ConjugateGradient, Momentum, ...) is not implemented
+    here and raises TypeError rather than silently running L-BFGS."""
+    alg = algorithm
+    if isinstance(alg, str):
+        name = alg.strip()
+        name = name[:-2] if name.endswith("()") else name
+        if name not in _SOLVER_NAMES:
+            raise TypeError(f"unsupported solver_algorithm {algorithm!r}: LBFGS(m=...) or GradientDescent()")
+        alg = _SOLVER_NAMES[name]
+    if isinstance(alg, type) and alg in (LBFGS, GradientDescent):
+        alg = alg()
+    if isinstance(alg, LBFGS):
+        if not (isinstance(alg.m, (int, np.integer)) and alg.m >= 1):
+            raise ValueError("LBFGS memory m must be a positive integer")
+        return int(alg.m), False
+    if isinstance(alg, GradientDescent):
+        return 1, True
+    raise TypeError(f"unsupported solver_algorithm {algorithm!r}: LBFGS(m=...) or GradientDescent()")
+
+
 def _checks(fp, params, nx):
     up = fp.unitary_problem
     nerr = len(up.error_sources)
@@ -677,21 +725,24 @@ def _solver_options(params):
 
 
 def optimize_restarts(fidelity_problem: FidelityRobustGRAPEProblem, fidelity_parameters: FidelityRobustGRAPEParameters,
-                      X0, device: int = 0, evaluate: Optional[Callable] = None, m: int = 10) -> BatchResult:
+                      X0, device: int = 0, evaluate: Optional[Callable] = None, m: Optional[int] = None) -> BatchResult:
     """Batched restarts: every row of X0 (R, n_x) is one optimisation of the reference's
-    problem; all of them advance together on the GPU (see the module docstring)."""
+    problem; all of them advance together on the GPU (see the module docstring).  The solver is
+    fidelity_parameters.solver_algorithm (solver_config); `m` overrides its L-BFGS memory."""
     X0 = torch.as_tensor(np.asarray(X0, dtype=np.float64) if not isinstance(X0, torch.Tensor) else X0,
                          dtype=torch.float64)
     if X0.dim() != 2:
         raise AssertionError("X0 must be (restarts, n_x)")
     nparam = _checks(fidelity_problem, fidelity_parameters, X0.shape[1])
+    m_alg, steepest = solver_config(fidelity_parameters.solver_algorithm)
+    m = m_alg if m is None else int(m)
+    opts = _solver_options(fidelity_parameters)  # (raises on unknown options before any device work)
     # workspace for at most MAX_PLAN_BATCH restarts per device pass: larger sweeps are
     # chunked by the C side instead of failing to allocate
     cost = RobustCost(fidelity_problem, fidelity_parameters, nparam, max_batch=min(X0.shape[0], MAX_PLAN_BATCH),
                       device=device, evaluate=evaluate)
-    opts = _solver_options(fidelity_parameters)
     try:
-        res = lbfgs_batched(cost, X0.to(cost.device), m=m, **opts)
+        res = lbfgs_batched(cost, X0.to(cost.device), m=m, steepest=steepest, **opts)
     finally:
         cost.close()
     if isinstance(opts.get("callback"), _OptimTrace):

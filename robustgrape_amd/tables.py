@@ -19,8 +19,10 @@ min(8, cpu_count)).
 from __future__ import annotations
 
 import atexit
+import contextlib
 import multiprocessing as mp
 import os
+import sys
 import threading
 import time
 from multiprocessing import shared_memory
@@ -226,14 +228,39 @@ def shm_free_bytes():
         return None
 
 
+@contextlib.contextmanager
+def _main_hidden():
+    """Hide the parent's __main__ from spawned children while a pool starts.  A spawned child
+    re-imports the parent's main script (multiprocessing.spawn get_preparation_data: __spec__.name
+    or __file__) and runs its top-level code; a user script without an
+    `if __name__ == "__main__"` guard (the reference's example style) would then build GRAPE
+    plans -- initialising HIP in a worker -- and start a nested pool in every worker.  The workers
+    need only this module and the problem, which cloudpickle ships by value (__main__ closures
+    included), so they start without the main module."""
+    main = sys.modules.get("__main__")
+    if main is None:
+        yield
+        return
+    saved = {k: main.__dict__[k] for k in ("__file__", "__spec__") if k in main.__dict__}
+    main.__dict__.pop("__file__", None)
+    main.__dict__["__spec__"] = None
+    try:
+        yield
+    finally:
+        main.__dict__.pop("__spec__", None)
+        main.__dict__.update(saved)
+
+
 class TableWorkers:
     """A process pool that fills closure tables in shared memory.  Spawned, not forked: the pool
     may first be needed after this process has initialised HIP, and a fork would copy that
-    state into the workers (they never touch the GPU)."""
+    state into the workers (they never touch the GPU).  The workers start without the parent's
+    main module (_main_hidden)."""
 
     def __init__(self, nworkers: int):
         self.n = nworkers
-        self.pool = mp.get_context("spawn").Pool(nworkers)
+        with _main_hidden():
+            self.pool = mp.get_context("spawn").Pool(nworkers)
         self.lock = threading.Lock()
 
     @staticmethod
@@ -308,7 +335,12 @@ def get_workers(fp=None):
         return None
     with _workers_lock:
         if _workers is None:
-            _workers = TableWorkers(n)
+            try:
+                _workers = TableWorkers(n)
+            except Exception as e:  # no pool (e.g. a process limit): the tables fill serially
+                import warnings
+                warnings.warn(f"closure-table worker pool unavailable ({e!r}); filling tables serially")
+                return None
             atexit.register(_shutdown)
         return _workers
 

@@ -63,6 +63,7 @@ class SlicePlan:
     def __init__(self, fp: FidelityRobustGRAPEProblem, nparam: int, k0: int, k1: int, device: int = 0):
         from .engine import GrapePlan
         self.k0, self.k1, self.nparam = int(k0), int(k1), int(nparam)
+        self.source = fp  # the problem the plan was built for (kept alive: _slice_plan's key is its id)
         self.d = fp.unitary_problem.ndim
         self.plan = GrapePlan(slice_problem(fp, k0, k1), nparam, device=device, max_batch=1)
 
@@ -112,15 +113,28 @@ _plans: "OrderedDict[tuple, SlicePlan]" = OrderedDict()
 _KEEP = 16
 
 
-def _slice_plan(fp, nparam, k0, k1, device):
+def _slice_plan(fp, nparam, k0, k1, device, keep=_KEEP):
+    """The cached slice plan of (fp, nparam, [k0, k1), device).  The key holds id(fp); the plan
+    holds fp itself (`source`), so the id cannot be recycled while the entry lives, and an entry
+    whose source is not fp (or whose plan was closed) is rebuilt -- as engine.get_plan guards
+    with `ent.fp is fp`.  `keep`: entries the caller needs alive at once (a call over nslices
+    plans on one device), so the LRU never closes a plan of the call in progress."""
     key = (id(fp), nparam, k0, k1, device)
     sp = _plans.pop(key, None)
-    if sp is None or sp.plan.handle is None:
+    if sp is not None and (sp.source is not fp or sp.plan.handle is None):
+        sp.close()
+        sp = None
+    if sp is None:
         sp = SlicePlan(fp, nparam, k0, k1, device)
     _plans[key] = sp
-    while len(_plans) > _KEEP:
+    while len(_plans) > max(_KEEP, keep):
         _plans.popitem(last=False)[1].close()
     return sp
+
+
+def clear_slice_plans():
+    while _plans:
+        _plans.popitem()[1].close()
 
 
 def _chain(mats, d):
@@ -152,7 +166,7 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
         rank = dist.get_rank(group)
     bounds = slice_bounds(up.ntimes, nslices)
     if dist is None:  # virtual ranks: every slice here, in order
-        plans = [_slice_plan(fp, nparam, a, b, device) for a, b in bounds]
+        plans = [_slice_plan(fp, nparam, a, b, device, keep=nslices) for a, b in bounds]
         totals = [sp.forward(x[a * nparam:b * nparam]) for sp, (a, b) in zip(plans, bounds)]
         F, M = fidelity_head(fp, _chain(totals, up.ndim))
         grads = []

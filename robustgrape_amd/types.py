@@ -75,7 +75,7 @@ class FidelityRobustGRAPEParameters:
     error_source_coeff: Sequence[float]
     time_limit: float = float("nan")
     iterations: int = 1000
-    solver_algorithm: str = "LBFGS"
+    solver_algorithm: Any = "LBFGS"  # optimize.LBFGS(m) / optimize.GradientDescent() or their names
     additional_parameters: Dict[str, Any] = field(default_factory=dict)
 
 

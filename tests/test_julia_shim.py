@@ -2,15 +2,24 @@
 interface.  Julia is not in the image, so the shim cannot run here; these checks pin what a
 reference caller relies on:
 
-* the exported entry points take the reference's argument types, first argument included:
-    calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
+* the entry points are METHODS OF THE REFERENCE'S OWN GENERICS (imported with
+  `import RobustGRAPE: ...`), with a signature strictly more specific than the reference's, so
+  the reference's own callers (optimize_fidelity_and_error_sources, FidelityCalculations.jl:177;
+  the fidelity response, :246-343) dispatch to the device:
+    reference: calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
         -- src/UnitaryCalculations.jl:20
-    calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
+    reference: calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{<:Real})
         -- src/UnitaryCalculations.jl:180
-    calculate_fidelity_and_derivatives(fidelity_problem::FidelityRobustGRAPEProblem, x::Vector{<:Real})
+    reference: calculate_fidelity_and_derivatives(fidelity_problem::FidelityRobustGRAPEProblem, x::Vector{<:Real})
         -- src/FidelityCalculations.jl:19
-    calculate_expectation_values(fidelity_problem::FidelityRobustGRAPEProblem, x::Vector{<:Real})
+    reference: calculate_expectation_values(fidelity_problem::FidelityRobustGRAPEProblem, x::Vector{<:Real})
         -- src/FidelityCalculations.jl:368
+    shim: the same first argument, x::Vector{Float64} (never Vector{<:Real}: that would overwrite
+    the reference's method instead of adding one);
+* the shim defines no optimiser of its own: the reference's driver is re-exported and reaches the
+  device through dispatch;
+* closure tables with a non-Hermitian nominal H0 select the general-H0 plan (GRAPE_OPT_GENERAL_H0),
+  above 12 levels non-Hermitian tables are refused (robustgrape_amd/engine.py general_h0_for);
 * those types are the reference's own (imported from RobustGRAPE, not redefined);
 * OperatorBasis is a Function, so it fits H0::Function / Herror::Function /
   target_unitary::Function (src/Types.jl:13,35,55);
@@ -24,11 +33,12 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHIM = os.path.join(ROOT, "julia", "RobustGRAPEMI355X.jl")
 
+# reference generic -> first-argument type of its method (x::Vector{<:Real} in every case)
 REFERENCE_SIGNATURES = {
-    "calculate_unitary_and_derivatives": ("UnitaryRobustGRAPEProblem", "Vector{<:Real}"),      # UnitaryCalculations.jl:20
-    "calculate_interaction_error_operators": ("UnitaryRobustGRAPEProblem", "Vector{<:Real}"),  # UnitaryCalculations.jl:180
-    "calculate_fidelity_and_derivatives": ("FidelityRobustGRAPEProblem", "Vector{<:Real}"),    # FidelityCalculations.jl:19
-    "calculate_expectation_values": ("FidelityRobustGRAPEProblem", "Vector{<:Real}"),          # FidelityCalculations.jl:368
+    "calculate_unitary_and_derivatives": "UnitaryRobustGRAPEProblem",      # UnitaryCalculations.jl:20
+    "calculate_interaction_error_operators": "UnitaryRobustGRAPEProblem",  # UnitaryCalculations.jl:180
+    "calculate_fidelity_and_derivatives": "FidelityRobustGRAPEProblem",    # FidelityCalculations.jl:19
+    "calculate_expectation_values": "FidelityRobustGRAPEProblem",          # FidelityCalculations.jl:368
 }
 
 
@@ -46,14 +56,44 @@ def _signatures(src):
     return sigs
 
 
-def test_exported_entry_points_take_the_reference_types():
+def _imported_generics(src):
+    m = re.search(r"^import RobustGRAPE: (.*?)\n(?!\s)", src, re.M | re.S)
+    assert m, "the shim must import the reference's generics to extend them"
+    return {n.strip() for n in m.group(1).replace("\n", " ").split(",") if n.strip()}
+
+
+def test_entry_points_extend_the_reference_generics():
     src = _src()
-    exported = re.search(r"export (.*?)\n\n", src, re.S).group(1)
+    imported = _imported_generics(src)
     sigs = _signatures(src)
-    for name, (t0, t1) in REFERENCE_SIGNATURES.items():
-        assert name in exported, name
-        assert name in sigs, name
-        assert [t0, t1] in sigs[name], (name, sigs[name])
+    exported = re.search(r"export (.*?)\n\n", src, re.S).group(1)
+    for name, t0 in REFERENCE_SIGNATURES.items():
+        assert name in imported, name          # a method of RobustGRAPE.<name>, not a new function
+        assert name in exported, name          # re-exported: the same binding as RobustGRAPE's
+        assert [t0, "Vector{Float64}"] in sigs[name], (name, sigs[name])
+        # Vector{<:Real} would REPLACE the reference's method (same signature), not add one
+        assert [t0, "Vector{<:Real}"] not in sigs[name], (name, sigs[name])
+
+
+def test_reference_driver_reaches_the_device_by_dispatch():
+    src = _src()
+    # no optimiser of the shim's own: RobustGRAPE.optimize_fidelity_and_error_sources calls
+    # calculate_fidelity_and_derivatives(fidelity_problem, x) with x::Vector{Float64}
+    # (FidelityCalculations.jl:177,209-211), which is the method above
+    assert not re.search(r"^function optimize_fidelity_and_error_sources", src, re.M)
+    assert re.search(r"^using RobustGRAPE: .*\boptimize_fidelity_and_error_sources\b", src, re.M | re.S)
+    assert "optimize_fidelity_and_error_sources" in re.search(r"export (.*?)\n\n", src, re.S).group(1)
+
+
+def test_closure_tables_check_hermiticity():
+    from robustgrape_amd.operators import OPT_GENERAL_H0
+    src = _src()
+    m = re.search(r"const GRAPE_OPT_GENERAL_H0 = Int32\((\d+)\)", src)
+    assert m and int(m.group(1)) == OPT_GENERAL_H0
+    # every closure entry point picks its table plan from the tables it built
+    assert src.count("table_plan(fp, np; general=_closure_general(") == 4
+    assert "table_plan(fp, np)" not in src
+    assert re.search(r"up\.ndim > 12", src) and "_is_hermitian(Hall)" in src
 
 
 def test_reference_types_are_imported_not_redefined():
@@ -77,7 +117,8 @@ def test_plan_cache_is_keyed_by_problem_nparam_and_kind():
     assert re.search(r"const _plans = Dict\{Tuple\{UInt,Int,Symbol\},DevicePlan\}\(\)", src)
     assert "key = (objectid(problem), nparam, kind)" in src
     kinds = set(re.findall(r"kind=:(\w+)", src)) | set(re.findall(r"_cached\(fp, nparam, :(\w+)\)", src))
-    assert {"unitary", "table"} <= kinds, kinds
+    kinds |= set(re.findall(r":(table\w*)", src))
+    assert {"unitary", "table", "table_general"} <= kinds, kinds
     # the unitary-level entry points wrap a UnitaryRobustGRAPEProblem (identity projector / target)
     assert "function fidelity_wrapper(problem::UnitaryRobustGRAPEProblem)" in src
 

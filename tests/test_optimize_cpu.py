@@ -194,3 +194,50 @@ def test_optim_options_stopping_and_unknown():
     # Julia-style symbol keys and the no-effect options are accepted
     OPT.optimize_fidelity_and_error_sources(fp, _small_params(fp, **{":show_trace": False, "allow_f_increases": True}),
                                             evaluate=ev)
+
+
+def test_solver_algorithm_is_honoured():
+    """FidelityRobustGRAPEParameters.solver_algorithm (Types.jl:82, FidelityCalculations.jl:211-213):
+    LBFGS(m) sets the memory, GradientDescent() steps along -g, anything else raises TypeError
+    instead of silently running L-BFGS."""
+    assert OPT.solver_config("LBFGS") == (10, False)
+    assert OPT.solver_config("LBFGS()") == (10, False)
+    assert OPT.solver_config(OPT.LBFGS(m=3)) == (3, False)
+    assert OPT.solver_config(OPT.GradientDescent) == (1, True)
+    assert OPT.solver_config("GradientDescent()") == (1, True)
+    for bad in ("BFGS", "ConjugateGradient()", "NelderMead", 42, OPT.LBFGS(m=0)):
+        with pytest.raises((TypeError, ValueError)):
+            OPT.solver_config(bad)
+    fp = P.sym_problem(16, device=False)
+    ev = _oracle_eval(fp)
+    with pytest.raises(TypeError, match="solver_algorithm"):
+        p = _small_params(fp)
+        p.solver_algorithm = "ConjugateGradient()"
+        OPT.optimize_fidelity_and_error_sources(fp, p, evaluate=ev)
+    # GradientDescent: every accepted step is a multiple of -g at the previous iterate
+    seen = []
+    rec = lambda X, f, g, it: seen.append((X[0].clone(), g[0].clone())) and False  # noqa: E731
+    X0 = torch.full((1, 4), -1.2, dtype=torch.float64)
+    res = OPT.lbfgs_batched(_rosenbrock, X0, iterations=8, steepest=True, callback=rec)
+    assert int(res.iterations[0]) == 8
+    for (x0, g0), (x1, _) in zip(seen, seen[1:]):
+        step = x1 - x0
+        a = -float(step @ g0) / float(g0 @ g0)
+        assert a > 0 and torch.max(torch.abs(step + a * g0)) <= 1e-12 * max(1.0, float(torch.max(torch.abs(step))))
+    # ... and L-BFGS does not (curvature pairs change the direction after the first step)
+    seen.clear()
+    OPT.lbfgs_batched(_rosenbrock, X0, iterations=8, callback=rec)
+    (x0, g0), (x1, _), (x2, g1) = seen[0], seen[1], seen[2]
+    step = x2 - x1
+    a = -float(step @ g1) / float(g1 @ g1)
+    assert torch.max(torch.abs(step + a * g1)) > 1e-6
+    # through the driver: GradientDescent lowers the cost from x_initial; LBFGS(m=3) is m = 3
+    p = _small_params(fp)
+    p.solver_algorithm = OPT.GradientDescent()
+    r_gd = OPT.optimize_fidelity_and_error_sources(fp, p, evaluate=ev)
+    c0 = O.optimization_cost(fp, p.x_initial, [O.regularization_cost_phase], [1e-6], [1e-6], [])[0]
+    assert r_gd.minimum < c0
+    p.solver_algorithm = OPT.LBFGS(m=3)
+    r3 = OPT.optimize_restarts(fp, p, p.x_initial[None, :], evaluate=ev)
+    r3b = OPT.optimize_restarts(fp, _small_params(fp), p.x_initial[None, :], evaluate=ev, m=3)
+    assert torch.equal(r3.minimizer, r3b.minimizer)

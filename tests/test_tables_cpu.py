@@ -89,3 +89,47 @@ def test_table_chunk_cap_by_bytes(monkeypatch):
     assert TB.table_batch_cap(fp, 1) == 3
     monkeypatch.setenv("GRAPE_TABLE_CHUNK_MB", "0")
     assert TB.table_batch_cap(fp, 1) == 1
+
+
+UNGUARDED_SCRIPT = """
+import os, sys
+import numpy as np
+sys.path.insert(0, {root!r})
+with open({marker!r}, "a") as fh:      # top-level code: must run once, in this process only
+    fh.write("%d\\n" % os.getpid())
+from robustgrape_amd import tables as TB
+from tests import problems as P
+fp = P.sym_problem(4, device=False)
+up = fp.unitary_problem
+base = up.H0
+h0 = lambda t, p, xa: 1.0 * np.asarray(base(t, p, xa))   # a __main__ closure (shipped by value)
+fp2 = fp.replace(unitary_problem=up.replace(H0=h0))
+X = np.stack([P.random_x(4, s) for s in range(2)])
+W = TB.TableWorkers(2)
+tabs = TB.SharedTables(*TB.table_shapes(fp2, len(X), 1))
+for r in W.submit(W.prepare(fp2), 1, tabs, X, range(len(X))):
+    r.get(timeout=120)
+H, U0 = TB.host_tables(fp2, X, 1)
+assert np.array_equal(tabs.H, H) and np.array_equal(tabs.U0, U0)
+W.release(tabs)
+tabs.close()
+W.close()
+print("UNGUARDED-OK")
+"""
+
+
+def test_pool_from_a_script_without_main_guard(tmp_path):
+    """spawned workers must not re-run an unguarded user script's top-level code
+    (robustgrape_amd/tables.py _main_hidden)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    marker = tmp_path / "marker.txt"
+    script = tmp_path / "user_script.py"
+    script.write_text(UNGUARDED_SCRIPT.format(root=root, marker=str(marker)))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=300,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "UNGUARDED-OK" in r.stdout
+    assert len(marker.read_text().split()) == 1, marker.read_text()

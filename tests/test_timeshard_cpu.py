@@ -67,7 +67,7 @@ class NumpySlice:
 
 @pytest.fixture
 def numpy_slices(monkeypatch):
-    monkeypatch.setattr(TS, "_slice_plan", lambda fp, nparam, k0, k1, device: NumpySlice(fp, nparam, k0, k1))
+    monkeypatch.setattr(TS, "_slice_plan", lambda fp, nparam, k0, k1, device, keep=0: NumpySlice(fp, nparam, k0, k1))
     TS._plans.clear()
 
 
@@ -115,6 +115,44 @@ def test_virtual_slices_match_oracle(numpy_slices, nslices):
     _check(F, Fdx, F0, np.asarray(g0))
 
 
+class CachedNumpySlice(NumpySlice):
+    """NumpySlice as the plan cache sees a SlicePlan: `source`, `plan.handle`, close()."""
+
+    def __init__(self, fp, nparam, k0, k1, device=0):
+        super().__init__(fp, nparam, k0, k1, device)
+        self.source = fp
+
+    def forward(self, xs):
+        assert self.handle is not None, "forward on a closed slice plan"
+        return super().forward(xs)
+
+    def close(self):
+        self.handle = None
+
+
+def test_slice_plan_cache_keeps_the_calls_plans_and_checks_the_problem(monkeypatch):
+    """More slices than the LRU keeps (robustgrape_amd/timeshard.py _KEEP = 16) on one device: no
+    plan of the call is closed before its forward; a cached entry whose problem is not the
+    caller's (a recycled id) is rebuilt."""
+    from oracle import grape_oracle as O
+    monkeypatch.setattr(TS, "SlicePlan", CachedNumpySlice)
+    TS._plans.clear()
+    fp = _problem(ntimes=20)
+    x = np.random.default_rng(11).uniform(-1, 1, size=40)
+    F, Fdx = TS.time_sharded_fidelity_grad(fp, x, nparam=2, nslices=20)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fp, x)[:2]
+    _check(F, Fdx, F0, np.asarray(g0))
+    assert len(TS._plans) == 20
+    # an entry under fp2's id built for another problem (what a recycled id would leave behind)
+    fp2 = _problem(ntimes=20, dt=0.2)
+    other = CachedNumpySlice(fp, 2, 0, 1)
+    TS._plans[(id(fp2), 2, 0, 1, 0)] = other
+    sp = TS._slice_plan(fp2, 2, 0, 1, 0)
+    assert sp is not other and sp.source is fp2 and other.handle is None
+    TS.clear_slice_plans()
+    assert not TS._plans
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -127,7 +165,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        TS._slice_plan = lambda fp, nparam, k0, k1, device: NumpySlice(fp, nparam, k0, k1)
+        TS._slice_plan = lambda fp, nparam, k0, k1, device, keep=0: NumpySlice(fp, nparam, k0, k1)
         fp = _problem()
         x = np.random.default_rng(7).uniform(-1, 1, size=24)
         F, Fdx = TS.time_sharded_fidelity_grad(fp, x, nparam=2)
