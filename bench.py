@@ -717,7 +717,7 @@ def main():
     ap.add_argument("--scan-waves", type=int, default=None, choices=(0, 1, 4, 8, 16),
                     help="c4opt: the plan's scan width (chunking); 0 = by batch size, default: RobustCost's choice")
     ap.add_argument("--plan-options", type=int, default=0,
-                    help="c4opt: GRAPE_OPT_* flags of the optimiser's plan (A/B runs)")
+                    help="GRAPE_OPT_* flags of the timed plan (A/B runs; c2/c3/c5 device legs and c4opt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-paths", action="store_true",
                     help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")
@@ -771,7 +771,7 @@ def main():
     B = args.batch or (16 if c5 else 16384 if c3 else 262144)
     chunk = args.chunk or (16 if c5 else 8192 if c3 else 32768)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
-    plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=min(count, chunk))
+    plan = GrapePlan(fp, nparam=nparam, device=local, max_batch=min(count, chunk), options=args.plan_options)
     X = torch.from_numpy(inputs(first, count)).to(dev)
     F = torch.empty(count, dtype=torch.float64, device=dev)
     Fdx = torch.empty(count, X.shape[1], dtype=torch.float64, device=dev)

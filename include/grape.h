@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 7
+#define GRAPE_ABI_VERSION 8
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -177,6 +177,13 @@ typedef struct grape_desc {
  * (one 4-level sector + two 2-level sectors, no error sources) run both sector classes' walks and
  * scans in one launch per stage; this option keeps one launch per class. */
 #define GRAPE_OPT_NO_PAIR 512
+/* Symmetry-adapted sectors (ABI 8): when a unitary change of basis V splits the operators'
+ * sparsity components further (the commutant of the operator algebra; e.g. the atom-swap symmetry
+ * of rydberg_hamiltonian_full with equal Rabi frequencies and detunings: a 3-level sector and a
+ * dark level instead of a 4-level sector), the sector path runs in that basis -- operators, target
+ * and projector rotated (V^dag X V), the outputs (traces) unchanged.  This option keeps the
+ * permutation sectors. */
+#define GRAPE_OPT_NO_SYMMETRY 1024
 
 typedef struct grape_plan grape_plan;
 
@@ -424,6 +431,18 @@ int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launc
  * number of classes; a plan that runs whole matrices reports one class (ndim, 1).
  */
 int grape_plan_sectors(grape_plan *plan, int *sector_dims, int *nsectors, int max_classes);
+
+/*
+ * Symmetry-adapted basis (ABI 8, host only: no device needed).  The unitary V (ndim x ndim,
+ * column-major interleaved complex, caller-owned) that grape_plan_create would use for the sector
+ * path of `desc` (GRAPE_OPT_NO_SYMMETRY above): per sparsity component of H0's and the error
+ * sources' operators, the minimal invariant subspaces of the algebra they generate, each with the
+ * basis closest to the unit vectors.  block (optional, ndim ints) receives the invariant-subspace id
+ * of each column.  Returns 1 when V splits some component further than its sparsity pattern (V may
+ * still be returned as the identity when the plan would not use it), 0 when V is the identity,
+ * negative on errors.  Plans use V only when the rotated sectors cost less work.
+ */
+int grape_symmetry_basis(const grape_desc *desc, double *V, int *block);
 
 /*
  * Batched matrix exponential exp(A) of n column-major ndim x ndim complex

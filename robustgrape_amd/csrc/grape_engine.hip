@@ -20,6 +20,7 @@
 #include "grape_launch.hpp"
 #include "grape_dense_api.hpp"
 #include "grape_unitary_api.hpp"
+#include "grape_symmetry.hpp"
 
 // instantiated in grape_inst.hip (one translation unit per dimension)
 namespace grape_host {
@@ -182,6 +183,10 @@ struct grape_plan {
     SecBuf sb[2];
     int *d_fixed = nullptr;
     grape_proj::SectorHead SH{};
+    // symmetry-adapted sectors (grape_symmetry.hpp): the head's rotated operators, projector, weights
+    bool symmetry = false;
+    cd *d_ops_sym = nullptr, *d_opsT_sym = nullptr, *d_PA_sym = nullptr, *d_PB_sym = nullptr;
+    double *d_W_sym = nullptr;
     // small calls with two sector classes: the second class runs on an auxiliary stream beside the
     // first (fork / join events; the classes are independent until the sector heads)
     hipStream_t aux_stream = nullptr;
@@ -255,7 +260,8 @@ static void free_plan(grape_plan *p) {
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
                     p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
-                    p->d_fixed, p->d_gout, p->d_slice};
+                    p->d_fixed, p->d_gout, p->d_slice, p->d_ops_sym, p->d_opsT_sym, p->d_PA_sym, p->d_PB_sym,
+                    p->d_W_sym};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
@@ -541,6 +547,135 @@ static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
     ss.cls = best;
     ss.fixed = fixed;
     return ss;
+}
+
+// Symmetry-adapted sectors (grape_symmetry.hpp): the sector path's view of the problem in the basis
+// V that splits the sparsity components further -- every operator V^dag O V (grape_desc layout;
+// H0's and the error sources' operators with their off-block residue set to exact zeros, the others
+// with rounding residue below 1e-15 of their largest entry snapped to 0), and the head's projector:
+// P0' = V^dag P0 V with the pattern P' = V^dag P V of the ORIGINAL P0 (P = P0 .!= 0,
+// FidelityCalculations.jl:47-51 -- the pattern of P0' is not P' in general).  On only when the
+// rotated sectors cost less work (sum nsec S^3) than the permutation sectors.
+struct SymSetup {
+    bool on = false;
+    grape_sym::Split split;
+    std::vector<double> ops;  // n_ops * d * d complex, column-major interleaved
+    ProjectorSetup ps;        // the rotated projector (A = P0' P', B = P' when not diagonal)
+    grape_desc view(const grape_desc *d) const {
+        grape_desc v = *d;
+        v.ops = ops.data();
+        return v;
+    }
+};
+static std::vector<const double *> used_operators(const grape_desc *desc) {
+    std::vector<const double *> u;
+    const int D = desc->ndim;
+    for (int t = 0; t < desc->n_h0_terms; ++t) u.push_back(desc->ops + 2 * (size_t)desc->h0_terms[t].op * D * D);
+    const int ne = desc->nerr > 0 ? desc->err_term_offsets[desc->nerr] : 0;
+    for (int t = 0; t < ne; ++t) u.push_back(desc->ops + 2 * (size_t)desc->err_terms[t].op * D * D);
+    return u;
+}
+static void snap_residue(double *m, int D, double rel) {  // m: D x D interleaved
+    double big = 0.0;
+    for (int t = 0; t < 2 * D * D; ++t) big = std::max(big, std::fabs(m[t]));
+    for (int t = 0; t < 2 * D * D; ++t)
+        if (std::fabs(m[t]) <= rel * big) m[t] = 0.0;
+}
+static SymSetup symmetry_setup(const grape_desc *desc) {
+    SymSetup sy;
+    const int D = desc->ndim;
+    if (D > GRAPE_MAX_SMALL_DIM || (desc->reserved[1] & (GRAPE_OPT_NO_SYMMETRY | GRAPE_OPT_NO_SECTORS))) return sy;
+    sy.split = grape_sym::symmetry_split(D, used_operators(desc));
+    if (!sy.split.rotated) return sy;
+    const size_t T2 = 2 * (size_t)D * D;
+    sy.ops.assign((size_t)desc->n_ops * T2, 0.0);
+    std::vector<char> used(desc->n_ops, 0);
+    for (int t = 0; t < desc->n_h0_terms; ++t) used[desc->h0_terms[t].op] = 1;
+    const int ne = desc->nerr > 0 ? desc->err_term_offsets[desc->nerr] : 0;
+    for (int t = 0; t < ne; ++t) used[desc->err_terms[t].op] = 1;
+    for (int o = 0; o < desc->n_ops; ++o) {
+        double *r = sy.ops.data() + (size_t)o * T2;
+        grape_sym::rotate(sy.split, desc->ops + (size_t)o * T2, r);
+        if (used[o])  // off the invariant blocks: zero by construction (checked in symmetry_split)
+            for (int j = 0; j < D; ++j)
+                for (int i = 0; i < D; ++i)
+                    if (sy.split.block[i] != sy.split.block[j]) r[2 * (i + (size_t)j * D)] = r[2 * (i + (size_t)j * D) + 1] = 0.0;
+        snap_residue(r, D, 1e-15);
+    }
+    // the projector P0 and its pattern P in the rotated basis
+    std::vector<double> P0(T2, 0.0), Pp(T2, 0.0), P0r(T2), Ppr(T2);
+    for (int j = 0; j < D; ++j)
+        for (int i = 0; i < D; ++i) {
+            const size_t t = 2 * (i + (size_t)j * D);
+            if (desc->projector) {
+                P0[t] = desc->projector[t];
+                P0[t + 1] = desc->projector[t + 1];
+            } else if (i == j) {
+                P0[t] = desc->projector_diag[i];
+            }
+            Pp[t] = (P0[t] != 0.0 || P0[t + 1] != 0.0) ? 1.0 : 0.0;
+        }
+    grape_sym::rotate(sy.split, P0.data(), P0r.data());
+    grape_sym::rotate(sy.split, Pp.data(), Ppr.data());
+    snap_residue(P0r.data(), D, 1e-15);
+    snap_residue(Ppr.data(), D, 1e-15);
+    ProjectorSetup &ps = sy.ps;
+    ps.W.assign(D, 0.0);
+    ps.P0.resize((size_t)D * D);
+    std::vector<cd> Br((size_t)D * D);
+    for (int i = 0; i < D; ++i)
+        for (int j = 0; j < D; ++j) {  // row-major tiles
+            const size_t t = 2 * (i + (size_t)j * D);
+            ps.P0[(size_t)i * D + j] = cd{P0r[t], P0r[t + 1]};
+            Br[(size_t)i * D + j] = cd{Ppr[t], Ppr[t + 1]};
+            if (i == j) {
+                ps.trP += P0r[t];
+                ps.W[i] = P0r[t];
+                // the diagonal specialisation needs P' = diag(P0' != 0) exactly
+                const double pat = P0r[t] != 0.0 ? 1.0 : 0.0;
+                if (P0r[t + 1] != 0.0 || Ppr[t + 1] != 0.0 || std::fabs(Ppr[t] - pat) > 1e-14) ps.general = true;
+            } else if (P0r[t] != 0.0 || P0r[t + 1] != 0.0 || Ppr[t] != 0.0 || Ppr[t + 1] != 0.0) {
+                ps.general = true;
+            }
+        }
+    if (ps.general) {
+        std::fill(ps.W.begin(), ps.W.end(), 0.0);
+        ps.B = Br;
+        ps.A.assign((size_t)D * D, cd{0.0, 0.0});
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j)
+                for (int l = 0; l < D; ++l) {
+                    const cd a = ps.P0[(size_t)i * D + l], b = Br[(size_t)l * D + j];
+                    ps.A[(size_t)i * D + j].re += a.re * b.re - a.im * b.im;
+                    ps.A[(size_t)i * D + j].im += a.re * b.im + a.im * b.re;
+                }
+    }
+    // worth it only when the rotated sectors are cheaper than the permutation ones
+    const grape_desc rv = sy.view(desc);
+    const SectorSetup rot = find_sectors(&rv, false), perm = find_sectors(desc, false);
+    if (rot.cls.empty()) return sy;
+    long crot = 0, cperm = 0;
+    for (const SectorClass &c : rot.cls) crot += sector_cost(c);
+    for (const SectorClass &c : perm.cls) cperm += sector_cost(c);
+    if (perm.cls.empty()) cperm = (long)D * D * D;
+    sy.on = crot < cperm;
+    return sy;
+}
+
+extern "C" int grape_symmetry_basis(const grape_desc *desc, double *V, int *block) {
+    if (!desc || !V || desc->ndim < 1 || desc->ndim > GRAPE_MAX_SMALL_DIM || !desc->ops || desc->n_ops < 1)
+        return fail(GRAPE_ERR_INVALID, "grape_symmetry_basis: operator-basis descriptor with 1 <= ndim <= 12");
+    const int D = desc->ndim;
+    for (int t = 0; t < desc->n_h0_terms; ++t)
+        if (desc->h0_terms[t].op < 0 || desc->h0_terms[t].op >= desc->n_ops) return fail(GRAPE_ERR_INVALID, "bad op index");
+    const grape_sym::Split sp = grape_sym::symmetry_split(D, used_operators(desc));
+    for (size_t t = 0; t < sp.V.size(); ++t) {
+        V[2 * t] = sp.V[t].real();
+        V[2 * t + 1] = sp.V[t].imag();
+    }
+    if (block)
+        for (int i = 0; i < D; ++i) block[i] = sp.block[i];
+    return sp.rotated ? 1 : 0;
 }
 
 static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, const ProjectorSetup &ps,
@@ -848,8 +983,14 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     P.nsec = 1;
     P.sec_ops = 0;
     p->general_h0 = general_h0;
-    const SectorSetup ss = general_h0 ? SectorSetup{} : find_sectors(desc, tables);
+    // symmetry-adapted sectors: the sector path (operators, head) in the rotated basis when that
+    // splits the sectors further; the whole-matrix problem P keeps the caller's basis
+    const SymSetup sym = (general_h0 || tables) ? SymSetup{} : symmetry_setup(desc);
+    const grape_desc sdesc = sym.on ? sym.view(desc) : *desc;
+    const ProjectorSetup &sps = sym.on ? sym.ps : ps;
+    const SectorSetup ss = general_h0 ? SectorSetup{} : find_sectors(&sdesc, tables);
     const bool sec = !ss.cls.empty();
+    p->symmetry = sym.on;
     // whole-matrix workspace rows (none when sectors or the general-H0 path run)
     const size_t FR = (sec || general_h0) ? 0 : (size_t)p->max_batch;
 
@@ -941,12 +1082,34 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
     if (sec) {  // the sector problems of every class and the head over the assembled U
         std::vector<cd> A(T, cd{0.0, 0.0}), Bm(T, cd{0.0, 0.0});  // diagonal projector: A = diag(w), B = diag(w != 0)
         for (int i = 0; i < D; ++i) {
-            A[(size_t)i * D + i] = cd{ps.W[i], 0.0};
-            Bm[(size_t)i * D + i] = cd{ps.W[i] != 0.0 ? 1.0 : 0.0, 0.0};
+            A[(size_t)i * D + i] = cd{sps.W[i], 0.0};
+            Bm[(size_t)i * D + i] = cd{sps.W[i] != 0.0 ? 1.0 : 0.0, 0.0};
         }
-        if (!ps.general && (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess ||
-                            hipMemcpy(p->d_PA, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
-                            hipMemcpy(p->d_PB, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess))
+        if (sym.on && sps.general) {
+            A = sps.A;
+            Bm = sps.B;
+        }
+        if (sym.on) {  // the head's own rotated projector tiles, weights and operators
+            std::vector<cd> rops((size_t)n_ops * T), ropsT(rops.size());
+            for (int o = 0; o < n_ops; ++o)
+                for (int r = 0; r < D; ++r)
+                    for (int c = 0; c < D; ++c) {
+                        const double *src = sym.ops.data() + 2 * ((size_t)o * T + r + (size_t)c * D);
+                        rops[(size_t)o * T + r * D + c] = cd{src[0], src[1]};
+                        ropsT[(size_t)o * T + c * D + r] = cd{src[0], src[1]};
+                    }
+            if (dalloc(&p->d_PA_sym, T) != hipSuccess || dalloc(&p->d_PB_sym, T) != hipSuccess ||
+                dalloc(&p->d_W_sym, (size_t)D) != hipSuccess || dalloc(&p->d_ops_sym, rops.size()) != hipSuccess ||
+                dalloc(&p->d_opsT_sym, ropsT.size()) != hipSuccess ||
+                hipMemcpy(p->d_PA_sym, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(p->d_PB_sym, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(p->d_W_sym, sps.W.data(), D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(p->d_ops_sym, rops.data(), rops.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(p->d_opsT_sym, ropsT.data(), ropsT.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (symmetry sectors)"));
+        } else if (!ps.general && (dalloc(&p->d_PA, T) != hipSuccess || dalloc(&p->d_PB, T) != hipSuccess ||
+                                   hipMemcpy(p->d_PA, A.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess ||
+                                   hipMemcpy(p->d_PB, Bm.data(), T * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess))
             return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
         if (dalloc(&p->d_fixed, ss.fixed.size()) != hipSuccess ||
             (!ss.fixed.empty() && hipMemcpy(p->d_fixed, ss.fixed.data(), ss.fixed.size() * sizeof(int),
@@ -954,14 +1117,19 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
         grape_proj::SectorHead &H = p->SH;
         H.P = P;
-        H.P.PA = p->d_PA;
-        H.P.PB = p->d_PB;
+        H.P.PA = sym.on ? p->d_PA_sym : p->d_PA;
+        H.P.PB = sym.on ? p->d_PB_sym : p->d_PB;
+        if (sym.on) {
+            H.P.W = p->d_W_sym;
+            H.P.ops = p->d_ops_sym;
+            H.P.opsT = p->d_opsT_sym;
+        }
         H.ncls = (int)ss.cls.size();
         H.fixed = p->d_fixed;
         H.nfixed = (int)ss.fixed.size();
         // diagonal projector and target, classes of <= 4 levels: the one-thread-per-evaluation head
         // (grape_projector.hip k_sec_head_diag)
-        H.diag = !ps.general && !tables && !(P.opts & GRAPE_OPT_GENERAL_HEAD);
+        H.diag = !sps.general && !tables && !(P.opts & GRAPE_OPT_GENERAL_HEAD);
         int rows = 0;  // the row-parallel head's lanes per evaluation (grape_projector.hip diag_group)
         for (const SectorClass &sc : ss.cls) {
             H.diag = H.diag && sc.S <= 4;
@@ -969,7 +1137,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
         }
         H.diag = H.diag && rows <= 32;
         for (int k = 0; H.diag && k < desc->n_target_terms; ++k) {
-            const double *op = desc->ops + 2 * (size_t)desc->target_terms[k].op * D * D;
+            const double *op = sdesc.ops + 2 * (size_t)desc->target_terms[k].op * D * D;
             for (int i = 0; i < D; ++i)
                 for (int j = 0; j < D; ++j)
                     if (i != j && (op[2 * (i + (size_t)j * D)] != 0.0 || op[2 * (i + (size_t)j * D) + 1] != 0.0))
@@ -999,7 +1167,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // the forward walk hands its propagators to the gradient walk (HBM, lane-minor) where the
             // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
             // 6.52 M evals/s; for the 2-level class it lost, 0.72 -> 1.01 ms per pass)
-            Ps.walk_store_e = Ps.walk && P.ne == 0 && S == grape::kWalkMaxD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
+            Ps.walk_store_e =
+                Ps.walk && P.ne == 0 && S >= grape::kWalkStoreMinD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
             // latency-bound walk classes (fewer sub-evaluations than CUs, or the option): 16-wave scans,
             // half-length walks (grape_launch.hpp kScanLatency)
             if (Ps.walk && P.ne == 0 &&
@@ -1038,7 +1207,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                     for (int a = 0; a < S; ++a)
                         for (int c = 0; c < S; ++c) {
                             const int gi = sc.sidx[(size_t)w * S + a], gj = sc.sidx[(size_t)w * S + c];
-                            const cd v = (gi >= 0 && gj >= 0) ? ops[(size_t)o * T + (size_t)gi * D + gj] : cd{0.0, 0.0};
+                            cd v{0.0, 0.0};
+                            if (gi >= 0 && gj >= 0) {  // (rotated) column-major operator
+                                const double *sv = sdesc.ops + 2 * ((size_t)o * T + gi + (size_t)gj * D);
+                                v = cd{sv[0], sv[1]};
+                            }
                             const size_t base = ((size_t)w * n_ops + o) * TS;
                             sops[base + (size_t)a * S + c] = v;
                             sopsT[base + (size_t)c * S + a] = v;
@@ -1210,7 +1383,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         const bool fork = p->aux_stream && !p->capturing && nb <= kForkMaxBatch && !(p->P.opts & GRAPE_OPT_NO_FORK);
         // Latency-bound calls of the Rydberg layout: both classes' walks (and scans) in ONE launch per
         // stage (grape_walk_api.hpp launch_pair) -- neither a graph branch nor a second stream overlaps
-        // them inside a captured graph on this runtime.  pa: the 4-level class, pb: the 2-level one.
+        // them inside a captured graph on this runtime.  pa: the 4- (or 3-) level class, pb: the 2-level one.
         int pa = 0, pb = 1;
         if (p->ncls == 2 && grape_walk::pair_ok(p->Ps[1], p->Ps[0])) std::swap(pa, pb);
         // (small calls only: a pair kernel runs the 2-level class at the 4-level class's occupancy)
@@ -1224,7 +1397,8 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
                 mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 1);
                 if (e == hipSuccess && s == 0) {
                     mk(GRAPE_KERNEL_SCAN, 0);
-                    e = grape_host::launch_scan_pair<4, 2>(p->Ps[pa], Bc[pa], p->Ps[pb], Bc[pb], st);
+                    e = p->Ps[pa].D == 4 ? grape_host::launch_scan_pair<4, 2>(p->Ps[pa], Bc[pa], p->Ps[pb], Bc[pb], st)
+                                         : grape_host::launch_scan_pair<3, 2>(p->Ps[pa], Bc[pa], p->Ps[pb], Bc[pb], st);
                     mk(GRAPE_KERNEL_SCAN, 1);
                 }
                 return e;

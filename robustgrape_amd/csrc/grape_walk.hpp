@@ -618,6 +618,18 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #ifndef GRAPE_WALK_IMG_LDS
 #define GRAPE_WALK_IMG_LDS 1
 #endif
+#ifndef GRAPE_WALK_SHIFT_MIN_D  // the diagonal shift for classes of >= this many levels
+#define GRAPE_WALK_SHIFT_MIN_D 3
+#endif
+#ifndef GRAPE_WALK_F3_WAVES  // k_walk_fwd<3>: waves per SIMD
+#define GRAPE_WALK_F3_WAVES 2
+#endif
+#ifndef GRAPE_WALK_G3_WAVES  // k_walk_grad<3, 1> (recomputed propagators)
+#define GRAPE_WALK_G3_WAVES 2
+#endif
+#ifndef GRAPE_WALK_G3S_WAVES  // k_walk_grad<3, 1> with stored propagators
+#define GRAPE_WALK_G3S_WAVES 1
+#endif
 template <int D, int NS>
 struct WalkCfg {
     static constexpr bool FENCE = D >= 4;        // per-column scheduling fences (register discipline)
@@ -629,17 +641,17 @@ struct WalkCfg {
     static constexpr bool KEEP_A2_GRAD = D < 4 || GRAPE_WALK_G4_KEEP_A2_GRAD;
     static constexpr bool KEEP_A2_IMG = D < 4 || GRAPE_WALK_IMG4_KEEP_A2;
     static constexpr bool KEEP_A2_NOM = D < 4 || GRAPE_WALK_G4_KEEP_A2_NOM;
-    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : 3) : D == 3 ? 2 : GRAPE_WALK_F4_WAVES;
+    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : 3) : D == 3 ? GRAPE_WALK_F3_WAVES : GRAPE_WALK_F4_WAVES;
     static constexpr bool FENCE_FWD = D >= 4 && GRAPE_WALK_F4_FENCE;
-    static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? 3 : 2) : D == 3 ? (NS == 1 ? 2 : 1)
-                                                                              : GRAPE_WALK_G4_WAVES;
-    static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? 1 : GRAPE_WALK_G4S_WAVES;
+    static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? 3 : 2)
+                                    : D == 3 ? (NS == 1 ? GRAPE_WALK_G3_WAVES : 1) : GRAPE_WALK_G4_WAVES;
+    static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? GRAPE_WALK_G3S_WAVES : GRAPE_WALK_G4S_WAVES;
     static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? 3 : 2) : 1;  // k_walk_img (error sources)
     static constexpr bool IMG_LDS = D >= 4 && GRAPE_WALK_IMG_LDS;      // k_walk_img: eps2 propagators in LDS
     // the diagonal shift + Taylor 9 (sm_regime) for the 4-level class only: it pays where the
     // Taylor-12 columns dominate; the smaller classes (Taylor 6 at C2) measured slower with its
     // bookkeeping (k_walk_fwd<2,2> 0.295 -> 0.34 ms per pass) and keep the unshifted walk bitwise
-    static constexpr bool SHIFT = D >= 4;
+    static constexpr bool SHIFT = D >= GRAPE_WALK_SHIFT_MIN_D;
 };
 
 // The chunk's phase: sum of the steps' diagonal shifts (sm_regime), TwoSum-compensated; the chunk

@@ -9,6 +9,12 @@ struct DevBatch;
 constexpr int kWalkMaxD = 4;  // sector classes of at most this many levels take the walks
 constexpr int kWalkMaxNpA = 2;  // ... with at most this many controls per step and x_add entries
 constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBlock)
+// walk classes of at least this many levels hand the forward walk's propagators to the gradient walk
+// (B.Ew) instead of recomputing them (the engine's P.walk_store_e and the launchers agree on it)
+#ifndef GRAPE_WALK_STORE_MIN_D
+#define GRAPE_WALK_STORE_MIN_D 4
+#endif
+constexpr int kWalkStoreMinD = GRAPE_WALK_STORE_MIN_D;
 }  // namespace grape
 
 namespace grape_walk {
@@ -18,8 +24,9 @@ namespace grape_walk {
 // to B.Zl), stage 1 = k_img_fdx (per-sector F_dx terms to B.sec_part, [nb][Nt][nvg])
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
-// Latency-bound calls of the Rydberg layout -- class 0: one 4-level sector with stored propagators,
-// class 1: two 2-level sectors, no error sources, one gradient parameter -- run both classes' walks
+// Latency-bound calls of the Rydberg layout -- class 0: one 4-level sector (permutation sectors) or
+// one 3-level sector (symmetry-adapted), class 1: two 2-level sectors, no error sources, one gradient
+// parameter -- run both classes' walks
 // of a stage in ONE launch (k_walk_fwd_pair / k_walk_grad_pair).  pair_ok tells whether the layout
 // fits; launch_pair(stage, ...) then replaces launch<4>(stage, class 0) + launch<2>(stage, class 1).
 bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1);

@@ -20,8 +20,8 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
         }
         return;
     }
-    // stored propagators: the 4-level class only (engine: P.walk_store_e)
-    constexpr bool CAN_STORE = D >= 4;
+    // stored propagators: classes of >= kWalkStoreMinD levels (engine: P.walk_store_e)
+    constexpr bool CAN_STORE = D >= grape::kWalkStoreMinD;
     const bool store = CAN_STORE && P.walk_store_e;
     if (stage == 0) {
         if (store) hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, CAN_STORE>), grid, blk, 0, st, P, B);
@@ -57,9 +57,12 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
     return hipGetLastError();
 }
 
+// class 0: one sector of 4 levels with stored propagators (permutation sectors of the Rydberg model)
+// or of 3 levels (its symmetry-adapted sectors, grape_symmetry.hpp); class 1: two 2-level sectors
 bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1) {
-    return P0.walk && P1.walk && P0.ne == 0 && P0.nvg == 1 && P0.D == 4 && P0.nsec == 1 && P0.walk_store_e &&
-           P1.D == 2 && P1.nsec == 2 && P1.nvg == 1 && !P1.walk_store_e;
+    const bool c0 = (P0.D == 4 || P0.D == 3) && (P0.walk_store_e != 0) == (P0.D >= grape::kWalkStoreMinD);
+    return P0.walk && P1.walk && P0.ne == 0 && P0.nvg == 1 && c0 && P0.nsec == 1 && P1.D == 2 && P1.nsec == 2 &&
+           P1.nvg == 1 && !P1.walk_store_e;
 }
 hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevBatch &B0, const grape::DevProblem &P1,
                        const grape::DevBatch &B1, hipStream_t st) {
@@ -71,10 +74,21 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
     };
     const int gx0 = gx(P0, B0), gy0 = 1, gx1 = gx(P1, B1);  // class 0: one sector per lane; class 1: both per lane
     const dim3 grid((unsigned)(gx0 * gy0 + gx1)), blk(grape::kWalkBlock);
-    if (stage == 0)
-        hipLaunchKernelGGL((grape::k_walk_fwd_pair<4, 1, true, 2, 2>), grid, blk, 0, st, P0, B0, P1, B1, gx0, gy0, gx1);
-    else
-        hipLaunchKernelGGL((grape::k_walk_grad_pair<4, 1, true, 2, 2>), grid, blk, 0, st, P0, B0, P1, B1, gx0, gy0, gx1);
+    if (P0.D == 4) {
+        if (stage == 0)
+            hipLaunchKernelGGL((grape::k_walk_fwd_pair<4, 1, (4 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0, B0,
+                               P1, B1, gx0, gy0, gx1);
+        else
+            hipLaunchKernelGGL((grape::k_walk_grad_pair<4, 1, (4 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0,
+                               B0, P1, B1, gx0, gy0, gx1);
+    } else {
+        if (stage == 0)
+            hipLaunchKernelGGL((grape::k_walk_fwd_pair<3, 1, (3 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0, B0,
+                               P1, B1, gx0, gy0, gx1);
+        else
+            hipLaunchKernelGGL((grape::k_walk_grad_pair<3, 1, (3 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0,
+                               B0, P1, B1, gx0, gy0, gx1);
+    }
     return hipGetLastError();
 }
 

@@ -167,6 +167,7 @@ OPT_GENERAL_H0 = 64  # non-Hermitian H0: LU-inverted chain, fidelity from the ma
 OPT_NO_FORK = 128  # every call on the plan's one stream (no auxiliary stream for the second sector class)
 OPT_GENERAL_HEAD = 256  # the general sector head even for a diagonal projector and target
 OPT_NO_PAIR = 512  # latency-bound calls: one launch per sector class (not both classes per launch)
+OPT_NO_SYMMETRY = 1024  # permutation sectors only (no symmetry-adapted basis, grape_symmetry.hpp)
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):

@@ -57,6 +57,14 @@ def fullblk_problem(ntimes, t0=T0_TO, errors=(), device=True):
     return FidelityRobustGRAPEProblem(up, W_FULLBLK, target)
 
 
+# sector layouts of the d = 9 Rydberg model (GrapePlan.sectors()): with equal Rabi frequencies and
+# detunings the atom-swap symmetry splits the 4-level block (include/grape.h GRAPE_OPT_NO_SYMMETRY,
+# csrc/grape_symmetry.hpp) -- one 3-level sector + two 2-level ones; single-atom error sources
+# (C3) break the symmetry and keep the permutation sectors.
+FULL9_SYM = ((3, 1), (2, 2))
+FULL9_PERM = ((4, 1), (2, 2))
+
+
 def full9_problem(ntimes=512, t0=T0_TO, nerr=0, device=True, B=10.0):
     """SURVEY.md 8d C2 (nerr=0) / C3 (nerr=4): d=9 rydberg_hamiltonian_full, Omega=1, B=10."""
     kinds = [("rabi", 1), ("rabi", 2), ("det", 1), ("det", 2)][:nerr]

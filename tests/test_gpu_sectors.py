@@ -34,8 +34,8 @@ def _plan(fp, max_batch, monkeypatch, whole=False, nparam=1, options=0):
                      options=options | (OPT_NO_SECTORS if whole else 0))
 
 
-def _both(fp, X, monkeypatch):
-    ps, pw = _plan(fp, len(X), monkeypatch), _plan(fp, len(X), monkeypatch, whole=True)
+def _both(fp, X, monkeypatch, options=0):
+    ps, pw = _plan(fp, len(X), monkeypatch, options=options), _plan(fp, len(X), monkeypatch, whole=True)
     try:
         return ps.sectors(), pw.sectors(), ps.fidelity_grad(X), pw.fidelity_grad(X)
     finally:
@@ -58,16 +58,19 @@ def _close(a, b, tight=True):
 
 
 @pytest.mark.parametrize("name,fp,layout", [
-    ("full9", lambda: P.full9_problem(40), ((4, 1), (2, 2))),
+    ("full9", lambda: P.full9_problem(40), P.FULL9_SYM),
+    ("full9-perm", lambda: P.full9_problem(40), P.FULL9_PERM),
     ("sym5", lambda: P.sym_problem(24), ((2, 2),)),
     ("fullblk7", lambda: P.fullblk_problem(24), ((2, 3),)),
 ])
 def test_sectors_match_whole_matrices_and_oracle(name, fp, layout, monkeypatch):
+    """-perm: the permutation sectors (GRAPE_OPT_NO_SYMMETRY); full9: the symmetry-adapted ones."""
     from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_SYMMETRY
     f = fp()
     nt, d = f.unitary_problem.ntimes, f.unitary_problem.ndim
     X = np.stack([P.random_x(nt, 40 + s) for s in range(6)])
-    sec, whole, out, ref = _both(f, X, monkeypatch)
+    sec, whole, out, ref = _both(f, X, monkeypatch, OPT_NO_SYMMETRY if name.endswith("-perm") else 0)
     assert sec == layout and whole == ((d, 1),)
     tight = P.fd_tier(f, X)
     _close(out, ref, tight)
@@ -96,7 +99,7 @@ def _close_err(a, b, label, fac=1.0):
 
 @pytest.mark.parametrize("name,fp,fo,layout", [
     ("full9-C3", lambda: P.full9_problem(24, nerr=4), lambda: P.full9_problem(24, nerr=4, device=False),
-     ((4, 1), (2, 2))),
+     P.FULL9_PERM),
     ("sym5-amp-freq", lambda: P.sym_problem(20, errors=("amp", "freq")),
      lambda: P.sym_problem(20, errors=("amp", "freq"), device=False), ((2, 2),)),
     ("fullblk7-amp", lambda: P.fullblk_problem(16, errors=("amp",)),
@@ -150,18 +153,21 @@ def test_sectors_with_xadd_dependent_h0(d, monkeypatch):
     _close((out[0][2], out[1][2]), (F0, g0), P.fd_tier(fp, X))
 
 
-def test_general_projector_mixing_sectors(monkeypatch):
+@pytest.mark.parametrize("sym", [True, False])
+def test_general_projector_mixing_sectors(sym, monkeypatch):
     """A projector coupling levels of different sectors: only the head sees it (the sector
-    blocks of M feed the contractions)."""
+    blocks of M feed the contractions).  sym: the symmetry-adapted sectors, whose head takes the
+    rotated P0' = V^dag P0 V with the rotated pattern P' = V^dag (P0 .!= 0) V (general form)."""
     from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_SYMMETRY
     nt = 20
     rng = np.random.default_rng(9)
     Qm, _ = np.linalg.qr(rng.standard_normal((9, 3)))
     P0 = Qm @ Qm.T
     fp = P.full9_problem(nt).replace(projector=P0)
     X = np.stack([P.random_x(nt, 90 + s) for s in range(3)])
-    sec, _, out, ref = _both(fp, X, monkeypatch)
-    assert sec == ((4, 1), (2, 2))
+    sec, _, out, ref = _both(fp, X, monkeypatch, 0 if sym else OPT_NO_SYMMETRY)
+    assert sec == (P.FULL9_SYM if sym else P.FULL9_PERM)
     _close(out, ref, P.fd_tier(fp, X))
     fo = P.full9_problem(nt, device=False).replace(projector=P0)
     F0, g0 = O.calculate_fidelity_and_derivatives(fo, X[1])[:2]
@@ -204,7 +210,7 @@ def test_sectors_tiny_step_counts(nt, monkeypatch):
         f = P.full9_problem(nt, nerr=nerr)
         X = np.stack([P.random_x(nt, 500 + s) for s in range(3)])
         sec, _, out, ref = _both(f, X, monkeypatch)
-        assert sec == ((4, 1), (2, 2))
+        assert sec == (P.FULL9_SYM if nerr == 0 else P.FULL9_PERM)
         fac = max(1.0, P.max_step_norm(f, X))
         _close_err(out, ref, f"nt={nt} ne={nerr} vs whole", fac)
         o = O.calculate_fidelity_and_derivatives(P.full9_problem(nt, nerr=nerr, device=False), X[2])
@@ -232,7 +238,9 @@ def test_sectors_two_controls(monkeypatch):
     ps = GrapePlan(fp, nparam=2, device=0, max_batch=3)
     pw = GrapePlan(fp, nparam=2, device=0, max_batch=3, options=OPT_NO_SECTORS)
     try:
-        assert ps.sectors() == ((4, 1), (2, 2)) and pw.sectors() == ((9, 1),)
+        # the detuning control keeps the swap symmetry; the dark level (1r - r1)/sqrt2 now has a
+        # diagonal (Nr = 1 there): a 1-level sector in the 2-level class
+        assert ps.sectors() == ((3, 1), (2, 3)) and pw.sectors() == ((9, 1),)
         out, ref = ps.fidelity_grad(X), pw.fidelity_grad(X)
     finally:
         ps.close()

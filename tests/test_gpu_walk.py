@@ -62,22 +62,27 @@ def _check(test, F, Fdx, F0, g0, tight):
 
 
 @pytest.mark.parametrize("name,fp,layout", [
-    ("full9", lambda: P.full9_problem(40), ((4, 1), (2, 2))),
-    ("full9-one-step", lambda: P.full9_problem(1), ((4, 1), (2, 2))),
-    ("full9-chunk-starts", lambda: P.full9_problem(3), ((4, 1), (2, 2))),
+    ("full9", lambda: P.full9_problem(40), P.FULL9_SYM),
+    ("full9-one-step", lambda: P.full9_problem(1), P.FULL9_SYM),
+    ("full9-chunk-starts", lambda: P.full9_problem(3), P.FULL9_SYM),
+    ("full9-perm", lambda: P.full9_problem(40), P.FULL9_PERM),
+    ("full9-one-step-perm", lambda: P.full9_problem(1), P.FULL9_PERM),
+    ("full9-chunk-starts-perm", lambda: P.full9_problem(3), P.FULL9_PERM),
     ("sym5", lambda: P.sym_problem(24), ((2, 2),)),
     ("fullblk7", lambda: P.fullblk_problem(24), ((2, 3),)),
     ("c1-evered", lambda: P.sym_problem(1000), ((2, 2),)),
 ])
 def test_walk_matches_oracle_and_stored_path(name, fp, layout):
-    """Walks vs the oracle and vs the stored-intermediate sector kernels (GRAPE_OPT_NO_WALK)."""
+    """Walks vs the oracle and vs the stored-intermediate sector kernels (GRAPE_OPT_NO_WALK); -perm:
+    the permutation sectors (GRAPE_OPT_NO_SYMMETRY: the 4-level walk), else the symmetry-adapted ones."""
     from oracle import grape_oracle as O
-    from robustgrape_amd.operators import OPT_NO_WALK
+    from robustgrape_amd.operators import OPT_NO_SYMMETRY, OPT_NO_WALK
     f = fp()
     nt = f.unitary_problem.ntimes
     X = np.stack([P.evered_pulse(nt) if name == "c1-evered" and s == 0 else P.random_x(nt, 700 + s)
                   for s in range(5)])
-    pw, ps = _plan(f, len(X)), _plan(f, len(X), OPT_NO_WALK)
+    so = OPT_NO_SYMMETRY if name.endswith("-perm") else 0
+    pw, ps = _plan(f, len(X), so), _plan(f, len(X), OPT_NO_WALK | so)
     try:
         assert pw.sectors() == layout
         out, ref = pw.fidelity_grad(X), ps.fidelity_grad(X)
@@ -97,11 +102,12 @@ def test_walk_matches_oracle_and_stored_path(name, fp, layout):
         assert out[0][0] > 0.9999 and abs(out[0][0] - 0.999996184760959) < 1e-12
 
 
-@pytest.mark.parametrize("walk", [True, False])
-def test_bench_size_plan_matches_goldens(walk):
+@pytest.mark.parametrize("walk,sym", [(True, True), (True, False), (False, True)])
+def test_bench_size_plan_matches_goldens(walk, sym):
     """C2 and C4 goldens inside one 2 048-evaluation launch (the bench's kernel configuration),
-    at scattered batch positions, with the walks and with the round-2 stored-intermediate path."""
-    from robustgrape_amd.operators import OPT_NO_WALK
+    at scattered batch positions, with the walks (symmetry-adapted sectors, the bench's default,
+    and the permutation sectors) and with the round-2 stored-intermediate path."""
+    from robustgrape_amd.operators import OPT_NO_SYMMETRY, OPT_NO_WALK
     g2, g4 = _golden("c2"), _golden("c4")
     rng = np.random.default_rng(5)
     X = np.stack([P.random_x(512, 3000 + s, small=True) for s in range(BIG)])
@@ -111,13 +117,14 @@ def test_bench_size_plan_matches_goldens(walk):
         X[p] = g2["x"]
     for j, p in enumerate(pos4):
         X[p] = g4["x"][j]
-    pl = _plan(P.full9_problem(512), BIG, 0 if walk else OPT_NO_WALK)
+    opts = (0 if walk else OPT_NO_WALK) | (0 if sym else OPT_NO_SYMMETRY)
+    pl = _plan(P.full9_problem(512), BIG, opts)
     try:
-        assert pl.sectors() == ((4, 1), (2, 2))
+        assert pl.sectors() == (P.FULL9_SYM if sym else P.FULL9_PERM)
         F, Fdx, _, _ = pl.fidelity_grad(X)
     finally:
         pl.close()
-    tag = "walk" if walk else "stored"
+    tag = ("walk" if walk else "stored") + ("" if sym else "_perm")
     for p in pos2:
         _check(f"big_{tag}_c2_at{p}", F[p], Fdx[p], g2["F"], g2["F_dx"], tight=True)
     for j, p in enumerate(pos4):
@@ -125,7 +132,7 @@ def test_bench_size_plan_matches_goldens(walk):
     # the rest of the batch: rows are independent and deterministic -> a re-run of a slice in a
     # small plan (other kernel widths) agrees at the T2s tier
     idx = rng.choice(BIG, size=6, replace=False)
-    small = _plan(P.full9_problem(512), 8, 0 if walk else OPT_NO_WALK)
+    small = _plan(P.full9_problem(512), 8, opts)
     try:
         Fs, gs, _, _ = small.fidelity_grad(X[idx])
     finally:
@@ -233,8 +240,9 @@ def test_walk_single_calls_are_the_batch():
 def test_walk_propagator_modes_bitwise(name, fp):
     """The gradient walk reading the forward walk's stored propagators (default for the 4-level class)
     and recomputing them (GRAPE_OPT_WALK_RECOMPUTE) run the same exponential code on the same inputs:
-    F and F_dx agree bit for bit."""
-    from robustgrape_amd.operators import OPT_WALK_RECOMPUTE
+    F and F_dx agree bit for bit.  (Permutation sectors: the stored propagators serve the 4-level
+    class, which the symmetry-adapted C2 layout does not have.)"""
+    from robustgrape_amd.operators import OPT_NO_SYMMETRY, OPT_WALK_RECOMPUTE
     f = fp()
     nparam = 2 if name == "full9-hot" else 1
     nt = f.unitary_problem.ntimes
@@ -244,7 +252,7 @@ def test_walk_propagator_modes_bitwise(name, fp):
         X[::7, 1::2][:, 5] = 700.0  # one high-norm step in every 7th row (the squaring path)
     outs = []
     for opts in (0, OPT_WALK_RECOMPUTE):
-        pl = _plan(f, 300, opts, nparam=nparam)
+        pl = _plan(f, 300, opts | OPT_NO_SYMMETRY, nparam=nparam)
         try:
             outs.append(pl.fidelity_grad(X)[:2])
         finally:
@@ -281,15 +289,16 @@ def test_diagonal_head_matches_general_head(name, fp):
             assert float(np.max(np.abs(a - b))) <= 1e-12 * scale + 1e-15, (name, float(np.max(np.abs(a - b))), scale)
 
 
+@pytest.mark.parametrize("sym", [True, False])
 @pytest.mark.parametrize("name,fp,nparam", [("full9", lambda: P.full9_problem(512), 1),
                                             ("full9-hot", lambda: _high_norm_problem(64)[0], 2)])
-def test_pair_launches_bitwise(name, fp, nparam):
+def test_pair_launches_bitwise(name, fp, nparam, sym):
     """Latency-bound calls (16-wave scans) of the Rydberg layout run both sector classes' walks and
     scans in one launch per stage (k_walk_fwd_pair, k_scan_pair, k_walk_grad_pair): the same
     arithmetic as one launch per class (GRAPE_OPT_NO_PAIR), so F and F_dx agree bit for bit --
     batched (stream path) and single (graph path) calls; the C2-size problem also against the
     oracle at the T2s tier."""
-    from robustgrape_amd.operators import OPT_NO_PAIR
+    from robustgrape_amd.operators import OPT_NO_PAIR, OPT_NO_SYMMETRY
     f = fp()
     nt = f.unitary_problem.ntimes
     rng = np.random.default_rng(11)
@@ -300,7 +309,7 @@ def test_pair_launches_bitwise(name, fp, nparam):
         X[::2, 1::2][:, 5] = 700.0  # a high-norm step (squaring path) in every other row
     outs = []
     for opts in (0, OPT_NO_PAIR):
-        pl = _plan(f, 8, opts, nparam=nparam)
+        pl = _plan(f, 8, opts | (0 if sym else OPT_NO_SYMMETRY), nparam=nparam)
         try:
             batch = pl.fidelity_grad(X)[:2]
             single = pl.fidelity_grad(X[3:4])[:2]
