@@ -78,7 +78,7 @@ def flops_expm(d, m=5, s=0):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
-WALK_STORE_LEVELS = 4  # csrc/grape_walk_api.hpp kWalkMaxD: the sector class whose walk stores E
+WALK_STORE_LEVELS = 4  # csrc/grape_walk_api.hpp kWalkStoreMinD: walk classes of >= this many levels store E
 PMC_SUMMARY_C5 = os.path.join(ROOT, "profiles", "pmc_c5_latest.json")
 PMC_SUMMARY_C3 = os.path.join(ROOT, "profiles", "pmc_c3_latest.json")
 
@@ -278,14 +278,18 @@ def _kernel_fracs(flop_model, ktimes):
     return out
 
 
-def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=None):
+def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=None, info=None):
     """C2 bench line.  `sectors`: GrapePlan.sectors() -- ((S, nsec), ...) per sector class, or
     ((D, 1),) for whole matrices; `passes`: device passes in the timed region (per-pass kernel
     times = total / passes: the sector classes launch each kernel once per class)."""
     nvg = 1  # np = 1 control; H0 does not read x_add, so no x_add variants
     classes = tuple(sectors) if sectors else ((D, 1),)
     sec = classes[0][0] < D
+    twins = tuple((info or {}).get("twin", ())) + (False,) * len(classes)
     per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
+    # executed work: a twin class (grape_walk.hpp TWIN) runs ONE exponential per step for its two
+    # sectors (the products and contractions stay per sector)
+    per_step_exp = lambda f: sum((1 if twins[c] else ns) * f(S) for c, (S, ns) in enumerate(classes))  # noqa: E731
     walk = ktimes.get("k_walk_grad", (0.0, 0))[1] > 0
     xbytes = L * 8 * (NT + 1)  # the x rows every per-step kernel streams
     if walk:
@@ -295,9 +299,11 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
         # contraction Re tr(Y dE).  The 2-level classes recompute E in the gradient walk
         # (executed, not credited); the 4-level class stores E once (walk_store_e) and the
         # gradient walk reads it back -- the only per-step HBM intermediate left
-        store = lambda S: S == WALK_STORE_LEVELS  # noqa: E731
-        flop_model = {"k_walk_fwd": L * NT * per_step(lambda S: flops_expm(S) + 8 * S ** 3),
-                      "k_walk_grad": L * NT * nvg * per_step(lambda S: flops_expm(S) + 2 * 8 * S ** 3 + 8 * S ** 2)}
+        store = lambda S: S >= WALK_STORE_LEVELS  # noqa: E731
+        flop_model = {"k_walk_fwd": L * NT * (per_step_exp(flops_expm)
+                                              + sum((1 if twins[c] else ns) * 8 * S ** 3 for c, (S, ns) in enumerate(classes))),
+                      "k_walk_grad": L * NT * nvg * (per_step_exp(flops_expm)
+                                                     + per_step(lambda S: 2 * 8 * S ** 3 + 8 * S ** 2))}
         byte_model = {"k_walk_fwd": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0),
                       "k_walk_grad": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0)}
     else:
@@ -347,8 +353,10 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                                "np=1, na=1, ne=0; restart sweep",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
                    "pipeline": "chunk walks" if walk else ("sector kernels" if sec else "whole matrices"),
-                   "sectors": [{"levels": S, "sectors": ns, "stored_propagators": bool(walk and store(S))}
-                               for S, ns in classes] if sec else None},
+                   "sectors": [{"levels": S, "sectors": ns, "stored_propagators": bool(walk and store(S)),
+                                "twin": bool(twins[c])}
+                               for c, (S, ns) in enumerate(classes)] if sec else None,
+                   "symmetry_adapted": bool((info or {}).get("symmetric", False))},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
         "kernels_ms_per_pass": per_pass,
@@ -357,7 +365,8 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     # (nominal + one eps-variant exp per step per sector, chain + contraction products; with
     # sectors also the head's d x d products), and the survey's canonical whole-matrix C2 figure
     # (which also counts the x_add-variant exps, zero differences, this engine skips)
-    exe = NT * per_step(lambda S: (1 + nvg) * flops_expm(S) + 3 * 8 * S ** 3 + nvg * 8 * S ** 2)
+    exe = NT * (per_step_exp(lambda S: (1 + nvg) * flops_expm(S) + 8 * S ** 3)
+                + per_step(lambda S: 2 * 8 * S ** 3 + nvg * 8 * S ** 2))
     if sec:
         exe += 16 * 8 * D ** 3
     canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
@@ -818,6 +827,7 @@ def main():
     value = evals / elapsed
     ktimes = plan.kernel_times()
     sectors = plan.sectors()
+    info = plan.sector_info()
     if rank == 0:
         L = min(count, chunk)
         if c5err:
@@ -829,7 +839,7 @@ def main():
                             args.steps * ((count + L - 1) // L))
         else:
             out = c2_report(args, B, L, world, value, elapsed, ktimes, sectors,
-                            args.steps * ((count + L - 1) // L))
+                            args.steps * ((count + L - 1) // L), info)
         if best is not None:
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         out["config"]["evals_per_device_pass"] = min(count, chunk)

@@ -184,6 +184,10 @@ typedef struct grape_desc {
  * and projector rotated (V^dag X V), the outputs (traces) unchanged.  This option keeps the
  * permutation sectors. */
 #define GRAPE_OPT_NO_SYMMETRY 1024
+/* Twin sectors (ABI 8): two sectors of a chunk-walk class whose blocks of every H0 operator are
+ * identical (the Rydberg sectors {01, 0r} and {10, r0} at equal Rabi frequencies and detunings)
+ * share one exponential per step; this option computes each sector's own. */
+#define GRAPE_OPT_NO_TWIN 2048
 
 typedef struct grape_plan grape_plan;
 
@@ -431,6 +435,10 @@ int grape_plan_kernel_times(grape_plan *plan, double *total_ms, long long *launc
  * number of classes; a plan that runs whole matrices reports one class (ndim, 1).
  */
 int grape_plan_sectors(grape_plan *plan, int *sector_dims, int *nsectors, int max_classes);
+/* (ABI 8) Per sector class of grape_plan_sectors: twin[c] = 1 when its two sectors share one
+ * exponential per step (GRAPE_OPT_NO_TWIN), symmetric (optional) = 1 when the sectors are the
+ * symmetry-adapted ones (GRAPE_OPT_NO_SYMMETRY).  Returns the number of classes. */
+int grape_plan_sector_info(grape_plan *plan, int *twin, int *symmetric, int max_classes);
 
 /*
  * Symmetry-adapted basis (ABI 8, host only: no device needed).  The unitary V (ndim x ndim,

@@ -1222,6 +1222,20 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                 return bail(fail(GRAPE_ERR_HIP, "upload failed (sectors)"));
             Ps.ops = b.ops;
             Ps.opsT = b.opsT;
+            // twin sectors (grape_walk.hpp TWIN): two walk sectors whose blocks of every operator H0
+            // and the error sources use are identical, with the same padding -- one exponential
+            // per step serves both (the 2-level Rydberg sectors at equal Rabi frequencies)
+            Ps.twin = 0;
+            if (Ps.walk && P.ne == 0 && sc.nsec == 2 && S <= 3 && !Ps.walk_store_e && !(P.opts & GRAPE_OPT_NO_TWIN)) {
+                bool same = true;
+                for (int a = 0; a < S; ++a) same = same && ((sc.sidx[a] < 0) == (sc.sidx[S + a] < 0));
+                std::vector<char> used(n_ops, 0);
+                for (int t = 0; t < desc->n_h0_terms; ++t) used[desc->h0_terms[t].op] = 1;
+                for (int o = 0; same && o < n_ops; ++o)
+                    if (used[o])
+                        same = std::memcmp(&sops[(size_t)o * TS], &sops[((size_t)n_ops + o) * TS], TS * sizeof(cd)) == 0;
+                Ps.twin = same ? 1 : 0;
+            }
             H.S[cl] = S;
             H.nsec[cl] = sc.nsec;
             H.sidx[cl] = b.sidx;
@@ -1247,6 +1261,15 @@ int grape_plan_sectors(grape_plan *p, int *sector_dims, int *nsectors, int max_c
         if (sector_dims) sector_dims[c] = p->ncls ? p->Ps[c].D : (p->dense ? p->DP.P.D : p->P.D);
         if (nsectors) nsectors[c] = p->ncls ? p->Ps[c].nsec : 1;
     }
+    return n;
+}
+
+int grape_plan_sector_info(grape_plan *p, int *twin, int *symmetric, int max_classes) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    const int n = p->ncls > 0 ? p->ncls : 1;
+    for (int c = 0; c < n && c < max_classes; ++c)
+        if (twin) twin[c] = p->ncls ? p->Ps[c].twin : 0;
+    if (symmetric) *symmetric = p->symmetry ? 1 : 0;
     return n;
 }
 

@@ -92,6 +92,8 @@ struct DevProblem {
     int walk;            // sector class served by the chunk walks (grape_walk.hpp: k_walk_fwd / k_walk_grad)
     int walk_store_e;    // ... k_walk_fwd stores the nominal propagators for k_walk_grad (B.Ew) instead of
                          //     k_walk_grad recomputing them
+    int twin;            // ... two sectors with identical operator blocks (grape_walk.hpp TWIN): one
+                         //     exponential per step serves both
     int opts;            // grape_desc.reserved[1]: GRAPE_OPT_* (fixed at plan creation)
 };
 

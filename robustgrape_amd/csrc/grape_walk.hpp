@@ -682,9 +682,14 @@ template <int D>
 constexpr int kEwStride = D * D + 1;
 
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
-template <int D, int NS, bool STORE>
+// TWIN (P.twin, NS = 2): the lane's two sectors have identical operator blocks (e.g. the Rydberg
+// sectors {01, 0r} and {10, r0} at equal Rabi frequencies and detunings): their propagators, chains
+// and chunk totals are identical, so one exponential and one chain per step serve both.
+template <int D, int NS, bool STORE, bool TWIN = false>
 __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
     using C = WalkCfg<D, NS>;
+    static_assert(!TWIN || (NS == 2 && !STORE), "twin sectors: two per lane, recomputed propagators");
+    constexpr int NE = TWIN ? 1 : NS;  // distinct propagators / chains per lane
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1;
@@ -705,10 +710,10 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));  // x_add
     const int k0 = L.c * P.L;
     X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
-    cd Q[NS][D][D];
-    WalkPhase ph[NS];
+    cd Q[NE][D][D];
+    WalkPhase ph[NE];
 #pragma unroll
-    for (int w = 0; w < NS; ++w) {
+    for (int w = 0; w < NE; ++w) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
 #pragma unroll
@@ -721,10 +726,10 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         const bool act = k0 + jj < P.Nt;
         walk_set_xk(X, xn);
         xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
-        SM<D> A[NS];
-        walk_build<D, NS>(P, ops, X, k + 1, none, A);
+        SM<D> A[NE];
+        walk_build<D, NE>(P, ops, X, k + 1, none, A);
 #pragma unroll
-        for (int w = 0; w < NS; ++w) {
+        for (int w = 0; w < NE; ++w) {
             double mu;
             walk_expm<D, C::FENCE_FWD, true, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu, true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
@@ -759,22 +764,26 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         }
     }
     if (L.ok) {
+        if constexpr (C::SHIFT) {
+#pragma unroll
+            for (int w = 0; w < NE; ++w) walk_phase<D>(ph[w], Q[w]);
+        }
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
-            if constexpr (C::SHIFT) walk_phase<D>(ph[w], Q[w]);
+            const int we = TWIN ? 0 : w;
             cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
 #pragma unroll
             for (int j = 0; j < D; ++j) {
 #pragma unroll
-                for (int i = 0; i < D; ++i) dst[j * D + i] = Q[w][j][i];
+                for (int i = 0; i < D; ++i) dst[j * D + i] = Q[we][j][i];
             }
         }
     }
 }
 
-template <int D, int NS, bool STORE>
+template <int D, int NS, bool STORE, bool TWIN = false>
 __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_walk_fwd(DevProblem P, DevBatch B) {
-    walk_fwd_body<D, NS, STORE>(P, B, hw_block());
+    walk_fwd_body<D, NS, STORE, TWIN>(P, B, hw_block());
 }
 
 // STORED: the nominal propagators come from the forward walk's copy (B.Ew, prefetched one step
@@ -782,9 +791,14 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
 // HBM traffic per step and sector.
 // NVG: the number of gradient parameters when known at compile time (1: C1 / C2 / C4), else 0
 // (a runtime loop) -- a static count of the F_dx stores per step keeps the prefetch waits exact.
-template <int D, int NS, bool STORED, int NVG>
+// TWIN: one nominal and one eps-variant exponential per step serve both sectors of the lane (their
+// X, Y and contractions stay per sector: M differs between them in general)
+template <int D, int NS, bool STORED, int NVG, bool TWIN = false>
 __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
     using C = WalkCfg<D, NS>;
+    static_assert(!TWIN || (NS == 2 && !STORED), "twin sectors: two per lane, recomputed propagators");
+    constexpr int NE = TWIN ? 1 : NS;     // distinct propagators per lane
+    constexpr int NSH = TWIN ? NS : 1;    // sectors sharing each of them
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1;
@@ -798,7 +812,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     // X_{k-1} = C_{k-1} M C_{k-1}^dag of every sector (M'_c at the chunk start); Y_k in place
     constexpr bool XL = C::X_LDS && !STORED, EL = C::E_LDS_GRAD && !STORED;
     MStore<D, XL> X[NS];
-    MStore<D, EL> E[NS];
+    MStore<D, EL> E[NE];
     if constexpr (XL || EL) {
         static_assert(NS == 1 && !(XL && EL), "one LDS slot per lane");
         __shared__ cd lds[kWalkBlock * MStore<D, true>::kStride];
@@ -808,7 +822,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
     auto ew = [&](int jj, int w) { return B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * kEwStride<D>) * lanes + lane; };
     cd En[STORED ? NS : 1][D][D];  // the next step's stored propagators (STORED)
-    double mun[NS], mu[NS];        // ... and their shifts; this step's shifts
+    double mun[NS], mu[NE];        // ... and their shifts; this step's shifts
     if constexpr (STORED) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
@@ -879,10 +893,10 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
                 mun[w] = src[(size_t)TS * lanes].re;
             }
         } else {
-            SM<D> A[NS];
-            walk_build<D, NS>(P, ops, XV, k + 1, none, A);
+            SM<D> A[NE];
+            walk_build<D, NE>(P, ops, XV, k + 1, none, A);
 #pragma unroll
-            for (int w = 0; w < NS; ++w)
+            for (int w = 0; w < NE; ++w)
                 walk_expm<D, C::FENCE, C::KEEP_A2_NOM, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu[w], true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
                     for (int j = 0; j < D; ++j) E[w].set(j, i, x[j]);
@@ -891,6 +905,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
         // Y = X E^dag, in place row by row (row r of Y reads row r of X only)
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
+            const int we = TWIN ? 0 : w;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
                 cd xr[D], y[D];
@@ -900,7 +915,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
                 for (int cc = 0; cc < D; ++cc) {
                     cd s = czero();
 #pragma unroll
-                    for (int j = 0; j < D; ++j) cmac(s, xr[j], cconj(E[w].at(cc, j)));
+                    for (int j = 0; j < D; ++j) cmac(s, xr[j], cconj(E[we].at(cc, j)));
                     y[cc] = s;
                 }
 #pragma unroll
@@ -910,31 +925,55 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
         // eps-variants: F_dx[u, k] = Re tr(Y (E' - E)) / eps, column j of E' against row j of Y
 #pragma unroll 1
         for (int u = 0; u < (NVG > 0 ? NVG : P.nvg); ++u) {
-            SM<D> Ap[NS];
-            walk_build<D, NS>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
+            SM<D> Ap[NE];
+            walk_build<D, NE>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
 #pragma unroll
-            for (int w = 0; w < NS; ++w) {
-                double s = 0.0;
-                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD, C::SHIFT>(Ap[w], scr + (size_t)w * 2 * TS, mu[w], false, [&](int j, const cd (&x)[D]) {
-                    const auto &Yj = X[w].opaque();  // row j of Y and column j of E read here, after
-                    const auto &Ej = E[w].opaque();  // column j of E'
+            for (int we = 0; we < NE; ++we) {
+                double s[NSH];
 #pragma unroll
-                    for (int r = 0; r < D; ++r) {
-                        const cd de = cscale(P.inv_eps, csub(x[r], Ej.at(r, j)));  // (1/eps) (E' - E)
-                        const cd y = Yj.at(j, r);
-                        s = fma(y.re, de.re, s);
-                        s = fma(-y.im, de.im, s);
+                for (int t = 0; t < NSH; ++t) s[t] = 0.0;
+                walk_expm<D, C::FENCE, C::KEEP_A2_GRAD, C::SHIFT>(Ap[we], scr + (size_t)we * 2 * TS, mu[we], false, [&](int j, const cd (&x)[D]) {
+                    if constexpr (NSH == 1) {
+                        const auto &Yj = X[we].opaque();  // row j of Y and column j of E read here, after
+                        const auto &Ej = E[we].opaque();  // column j of E'
+#pragma unroll
+                        for (int r = 0; r < D; ++r) {
+                            const cd de = cscale(P.inv_eps, csub(x[r], Ej.at(r, j)));  // (1/eps) (E' - E)
+                            const cd y = Yj.at(j, r);
+                            s[0] = fma(y.re, de.re, s[0]);
+                            s[0] = fma(-y.im, de.im, s[0]);
+                        }
+                    } else {  // twins: one difference column, contracted with each sector's row j of Y
+                        const auto &Ej = E[we].opaque();
+                        cd de[D];
+#pragma unroll
+                        for (int r = 0; r < D; ++r) de[r] = cscale(P.inv_eps, csub(x[r], Ej.at(r, j)));
+#pragma unroll
+                        for (int t = 0; t < NSH; ++t) {
+                            const auto &Yj = X[we * NSH + t].opaque();
+#pragma unroll
+                            for (int r = 0; r < D; ++r) {
+                                const cd y = Yj.at(j, r);
+                                s[t] = fma(y.re, de[r].re, s[t]);
+                                s[t] = fma(-y.im, de[r].im, s[t]);
+                            }
+                        }
                     }
                 });
-                // unconditional store (inactive lanes write the sink): exact vmcnt accounting
-                double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
-                                  : reinterpret_cast<double *>(B.sink);
-                *dst = s;
+#pragma unroll
+                for (int t = 0; t < NSH; ++t) {
+                    const int w = we * NSH + t;
+                    // unconditional store (inactive lanes write the sink): exact vmcnt accounting
+                    double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
+                                      : reinterpret_cast<double *>(B.sink);
+                    *dst = s[t];
+                }
             }
         }
         // X <- E Y, in place column by column
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
+            const int we = TWIN ? 0 : w;
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 cd y[D], t[D];
@@ -944,7 +983,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
                 for (int j = 0; j < D; ++j) {
                     cd c = czero();
 #pragma unroll
-                    for (int m = 0; m < D; ++m) cmac(c, E[w].at(j, m), y[m]);
+                    for (int m = 0; m < D; ++m) cmac(c, E[we].at(j, m), y[m]);
                     t[j] = c;
                 }
 #pragma unroll
@@ -954,10 +993,10 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     }
 }
 
-template <int D, int NS, bool STORED, int NVG>
+template <int D, int NS, bool STORED, int NVG, bool TWIN = false>
 __global__ __launch_bounds__(kWalkBlock, (STORED ? WalkCfg<D, NS>::WAVES_GRAD_STORED : WalkCfg<D, NS>::WAVES_GRAD))
 void k_walk_grad(DevProblem P, DevBatch B) {
-    walk_grad_body<D, NS, STORED, NVG>(P, B, hw_block());
+    walk_grad_body<D, NS, STORED, NVG, TWIN>(P, B, hw_block());
 }
 
 // Pair kernels (latency-bound calls): two sector classes' walks in ONE launch -- the first
@@ -965,19 +1004,19 @@ void k_walk_grad(DevProblem P, DevBatch B) {
 // -- so a single evaluation's classes run side by side instead of one launch after the other
 // (graph branches do not run concurrently on this runtime: scripts/probes/graph_branch_probe.hip).
 // The registers are the larger class's; at these sizes the grid is a few workgroups.
-template <int D0, int NS0, bool ST0, int D1, int NS1>
+template <int D0, int NS0, bool ST0, int D1, int NS1, bool TW1 = false>
 __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_fwd_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1,
                                                                  int gx0, int gy0, int gx1) {
     const int id = blockIdx.x, n0 = gx0 * gy0;
     if (id < n0) walk_fwd_body<D0, NS0, ST0>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
-    else walk_fwd_body<D1, NS1, false>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+    else walk_fwd_body<D1, NS1, false, TW1>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
 }
-template <int D0, int NS0, bool ST0, int D1, int NS1>
+template <int D0, int NS0, bool ST0, int D1, int NS1, bool TW1 = false>
 __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1,
                                                                   int gx0, int gy0, int gx1) {
     const int id = blockIdx.x, n0 = gx0 * gy0;
     if (id < n0) walk_grad_body<D0, NS0, ST0, 1>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
-    else walk_grad_body<D1, NS1, false, 1>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+    else walk_grad_body<D1, NS1, false, 1, TW1>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
 }
 
 // ---------------------------------------------------------------------------

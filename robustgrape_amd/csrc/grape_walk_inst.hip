@@ -1,5 +1,7 @@
 // grape_walk_inst.hip -- the chunk-walk kernels (grape_walk.hpp) for D = 2 .. kWalkMaxD and their
 // launchers; built with -mllvm -disable-machine-licm (robustgrape_amd/build.py).
+#include <type_traits>
+
 #include "grape_walk.hpp"
 #include "grape_walk_api.hpp"
 
@@ -19,6 +21,14 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
             hipLaunchKernelGGL(grape::k_img_fdx<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, B);
         }
         return;
+    }
+    if constexpr (NS == 2) {  // twin sectors (P.twin): one exponential per step for both
+        if (P.twin) {
+            if (stage == 0) hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, false, true>), grid, blk, 0, st, P, B);
+            else if (P.nvg == 1) hipLaunchKernelGGL((grape::k_walk_grad<D, NS, false, 1, true>), grid, blk, 0, st, P, B);
+            else hipLaunchKernelGGL((grape::k_walk_grad<D, NS, false, 0, true>), grid, blk, 0, st, P, B);
+            return;
+        }
     }
     // stored propagators: classes of >= kWalkStoreMinD levels (engine: P.walk_store_e)
     constexpr bool CAN_STORE = D >= grape::kWalkStoreMinD;
@@ -74,21 +84,22 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
     };
     const int gx0 = gx(P0, B0), gy0 = 1, gx1 = gx(P1, B1);  // class 0: one sector per lane; class 1: both per lane
     const dim3 grid((unsigned)(gx0 * gy0 + gx1)), blk(grape::kWalkBlock);
-    if (P0.D == 4) {
+    auto go = [&](auto d0, auto tw) {
+        constexpr int D0 = decltype(d0)::value;
+        constexpr bool TW = decltype(tw)::value;
         if (stage == 0)
-            hipLaunchKernelGGL((grape::k_walk_fwd_pair<4, 1, (4 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0, B0,
-                               P1, B1, gx0, gy0, gx1);
+            hipLaunchKernelGGL((grape::k_walk_fwd_pair<D0, 1, (D0 >= grape::kWalkStoreMinD), 2, 2, TW>), grid, blk, 0, st,
+                               P0, B0, P1, B1, gx0, gy0, gx1);
         else
-            hipLaunchKernelGGL((grape::k_walk_grad_pair<4, 1, (4 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0,
-                               B0, P1, B1, gx0, gy0, gx1);
-    } else {
-        if (stage == 0)
-            hipLaunchKernelGGL((grape::k_walk_fwd_pair<3, 1, (3 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0, B0,
-                               P1, B1, gx0, gy0, gx1);
-        else
-            hipLaunchKernelGGL((grape::k_walk_grad_pair<3, 1, (3 >= grape::kWalkStoreMinD), 2, 2>), grid, blk, 0, st, P0,
-                               B0, P1, B1, gx0, gy0, gx1);
-    }
+            hipLaunchKernelGGL((grape::k_walk_grad_pair<D0, 1, (D0 >= grape::kWalkStoreMinD), 2, 2, TW>), grid, blk, 0, st,
+                               P0, B0, P1, B1, gx0, gy0, gx1);
+    };
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using T = std::true_type;
+    using F = std::false_type;
+    if (P0.D == 4) P1.twin ? go(I4{}, T{}) : go(I4{}, F{});
+    else P1.twin ? go(I3{}, T{}) : go(I3{}, F{});
     return hipGetLastError();
 }
 

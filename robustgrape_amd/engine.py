@@ -237,6 +237,14 @@ class GrapePlan:
         _capi.check(min(k, 0))
         return tuple((S[c], n[c]) for c in range(k))
 
+    def sector_info(self) -> dict:
+        """{"twin": (per class: its two sectors share one exponential per step), "symmetric":
+        the sectors are the symmetry-adapted ones} (include/grape.h grape_plan_sector_info)."""
+        t, sym = (ctypes.c_int * 2)(), ctypes.c_int(0)
+        k = _capi.lib().grape_plan_sector_info(self.handle, t, ctypes.byref(sym), 2)
+        _capi.check(min(k, 0))
+        return {"twin": tuple(bool(t[c]) for c in range(k)), "symmetric": bool(sym.value)}
+
 
 # Plan cache of the reference-shaped entry points (one plan per problem object, nparam and
 # device).  A plan owns HBM workspace for `max_batch` evaluations; larger batches are

@@ -168,6 +168,7 @@ OPT_NO_FORK = 128  # every call on the plan's one stream (no auxiliary stream fo
 OPT_GENERAL_HEAD = 256  # the general sector head even for a diagonal projector and target
 OPT_NO_PAIR = 512  # latency-bound calls: one launch per sector class (not both classes per launch)
 OPT_NO_SYMMETRY = 1024  # permutation sectors only (no symmetry-adapted basis, grape_symmetry.hpp)
+OPT_NO_TWIN = 2048  # every walk sector computes its own exponentials (no twin sharing, grape_walk.hpp)
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):

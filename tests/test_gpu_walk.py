@@ -324,3 +324,26 @@ def test_pair_launches_bitwise(name, fp, nparam, sym):
         from oracle import grape_oracle as O
         F0, g0 = O.calculate_fidelity_and_derivatives(f, X[0])[:2]
         _check("pair_full9", b0[0][0], b0[1][0], F0, g0, True)
+
+
+@pytest.mark.parametrize("nb,max_batch", [(300, 300), (3, 8)])
+def test_twin_sectors_bitwise(nb, max_batch):
+    """Twin sectors (grape_walk.hpp TWIN: the 2-level Rydberg sectors {01, 0r} and {10, r0} have
+    identical operator blocks at equal Rabi frequencies): one exponential per step serves both.
+    The shared propagators are the ones each sector would compute from the same inputs, so F and
+    F_dx equal those of GRAPE_OPT_NO_TWIN bit for bit -- a throughput-size batch and a latency-bound
+    one (16-wave scans, pair kernels), plus a single call."""
+    from robustgrape_amd.operators import OPT_NO_TWIN
+    f = P.full9_problem(128)
+    rng = np.random.default_rng(21)
+    X = rng.uniform(0, 2 * np.pi, size=(nb, 129))
+    outs = []
+    for opts in (0, OPT_NO_TWIN):
+        pl = _plan(f, max_batch, opts)
+        try:
+            outs.append((pl.fidelity_grad(X)[:2], pl.fidelity_grad(X[:1])[:2]))
+        finally:
+            pl.close()
+    (b0, s0), (b1, s1) = outs
+    assert np.array_equal(b0[0], b1[0]) and np.array_equal(b0[1], b1[1])
+    assert np.array_equal(s0[0], s1[0]) and np.array_equal(s0[1], s1[1])
