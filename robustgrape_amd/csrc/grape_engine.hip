@@ -175,7 +175,7 @@ struct grape_plan {
         int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr;
         double *part = nullptr;
         // error sources: local-frame images, per-chunk triples, Tot / M_e blocks, F_d2err_dx terms
-        cd *Zl = nullptr, *Me = nullptr, *TotS = nullptr, *MsecE = nullptr;
+        cd *Zl = nullptr, *Me = nullptr, *TotS = nullptr, *MsecE = nullptr, *Wc = nullptr;
         double *part_err = nullptr;
     };
     int ncls = 0;
@@ -266,7 +266,7 @@ static void free_plan(grape_plan *p) {
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
         void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part,
-                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr, c.Ew};
+                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr, c.Ew, c.Wc};
         for (void *b : sbufs)
             if (b) (void)hipFree(b);
     }
@@ -1159,10 +1159,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             if (scan_override == kScanTiny || scan_override == kScanNarrow || scan_override == kScanWide)
                 Ps.scan_waves = scan_override;
             // chunk walks (grape_walk.hpp): classes of <= kWalkMaxD levels; with error sources the
-            // image walk (k_walk_img), which keeps the eps2 propagators of one gradient parameter
+            // image walk (k_walk_img), for any number of gradient parameters per step
             // (its exponential keeps A skew-Hermitian in compressed form: Hermitian error generators only;
             // a decay-rate error, -i e/2 |r><r|, keeps the stored-variant kernels)
-            Ps.walk = (S <= grape::kWalkMaxD && (P.ne == 0 || (P.nvg == 1 && err_herm)) && P.np <= grape::kWalkMaxNpA &&
+            Ps.walk = (S <= grape::kWalkMaxD && (P.ne == 0 || err_herm) && P.np <= grape::kWalkMaxNpA &&
                        P.na <= grape::kWalkMaxNpA && !(P.opts & GRAPE_OPT_NO_WALK)) ? 1 : 0;
             // the forward walk hands its propagators to the gradient walk (HBM, lane-minor) where the
             // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
@@ -1197,7 +1197,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                 dalloc(&b.ovf2, R2 * P.Nt * nvg) != hipSuccess || dalloc(&b.part, R * P.Nt * nvg) != hipSuccess ||
                 dalloc(&b.sidx, sc.sidx.size()) != hipSuccess || dalloc(&b.ops, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
                 dalloc(&b.opsT, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
-                dalloc(&b.Zl, R * P.Nt * (ne ? P.nz : 0) * TS) != hipSuccess ||
+                // (the image walk's images are lane-minor over its padded launch width: grape_walk.hpp img_index)
+                dalloc(&b.Zl, (Ps.walk ? (size_t)sc.nsec * Ps.L * lanes_pad : R * P.Nt) * (ne ? P.nz : 0) * TS) != hipSuccess ||
+                dalloc(&b.Wc, (Ps.walk ? R * ne * Ps.nchunks : 0) * TS) != hipSuccess ||
                 dalloc(&b.Me, R * ne * Ps.nchunks * 3 * TS) != hipSuccess || dalloc(&b.TotS, R * ne * TS) != hipSuccess ||
                 dalloc(&b.MsecE, R * ne * TS) != hipSuccess || dalloc(&b.part_err, R * ne * P.Nt * nvg) != hipSuccess)
                 return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (sectors)"));
@@ -1374,6 +1376,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.part_err_add = p->d_part_err;
             if (p->P.ne > 0) {
                 B.Zl = sb.Zl;
+                B.Wc = p->Ps[cl].walk ? sb.Wc : nullptr;
                 B.Me = sb.Me;
                 B.TotS = sb.TotS;
                 B.MsecE = sb.MsecE;
@@ -1389,8 +1392,9 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.xT = nb == 1 ? d_x : p->d_xT;  // one evaluation: x[q] is already [nx][1]
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].nsec;
-            sp.lane_major[cl] = p->Ps[cl].walk && p->P.ne == 0;  // k_walk_grad's layout (k_img_fdx: row layout)
+            sp.lane_major[cl] = p->Ps[cl].walk;  // k_walk_grad's / k_walk_img_sum's layout
             sp.part_err[cl] = sb.part_err;
+            sp.lane_major_err[cl] = p->Ps[cl].walk;  // k_walk_err_grad's layout
         }
         bool parks = false;  // the chunk walks never park a step for k_expm_high: no counters to clear
         for (int cl = 0; cl < p->ncls; ++cl) parks = parks || !p->Ps[cl].walk;

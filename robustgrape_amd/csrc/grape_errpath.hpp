@@ -51,12 +51,20 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
 #pragma unroll
     for (int j = 0; j < D; ++j) acc[j] = czero();
     const int w_slot = P.nvg + e;
-    for (int j = 0; j < P.L; ++j) {
-        const int k = c * P.L + j;
-        if (gvalid && k < P.Nt) {
-            const cd *Wk = B.Zl + ((size_t)(b * P.Nt + k) * P.nz + w_slot) * TILE + i * D;
+    if (B.Wc) {  // the walk path's chunk sums (k_walk_img_sum, same summation order)
+        if (gvalid) {
+            const cd *Ws = B.Wc + (((size_t)b * P.ne + e) * P.nchunks + c) * TILE + i * D;
 #pragma unroll
-            for (int jj = 0; jj < D; ++jj) acc[jj] = cadd(acc[jj], Wk[jj]);
+            for (int jj = 0; jj < D; ++jj) acc[jj] = Ws[jj];
+        }
+    } else {
+        for (int j = 0; j < P.L; ++j) {
+            const int k = c * P.L + j;
+            if (gvalid && k < P.Nt) {
+                const cd *Wk = B.Zl + ((size_t)(b * P.Nt + k) * P.nz + w_slot) * TILE + i * D;
+#pragma unroll
+                for (int jj = 0; jj < D; ++jj) acc[jj] = cadd(acc[jj], Wk[jj]);
+            }
         }
     }
     // Phase A': Vc_c = Carry_c^dag (sum W) Carry_c  -> own tile

@@ -110,6 +110,7 @@ struct DevBatch {
     cd *Carry;              // [nb][nchunks][D][D]  C_{cL-1} (identity for c = 0)
     cd *Ub;                 // [nb][D][D]           U = C_Nt
     cd *Me;                 // [nb][ne][nchunks][3][D][D]  M'_{c,e}, T_c, Ttot_c (error path)
+    cd *Wc;                 // walk path with error sources: [nb][ne][nchunks][D][D] chunk sums of W (k_walk_img_sum)
     cd *Zl;                 // [nb][Nt][nz][D][D]  local-frame differences (error path, k_err_local):
                             //   Z1_u (nvg) | W_e (ne) | Z2_{e,u} (ne x nvg), row-major
     double *Fd2;            // [nb][ne]
@@ -1004,9 +1005,10 @@ __global__ void k_sec_mc_err(DevProblem P, DevBatch B) {
 // the walk layout's reads and the F_dx rows' writes are coalesced.
 struct SecParts {
     const double *part[2];      // per sector class, layout by lane_major
-    const double *part_err[2];  // [nb][nsec_c][ne][Nt][nvg] (error sources)
+    const double *part_err[2];  // per sector class (error sources), layout by lane_major_err
     int nsec[2];                // 0 for an absent class
-    int lane_major[2];          // 1: [nsec][Nt][nvg][nb] (chunk walks)
+    int lane_major[2];          // 1: [nsec][Nt][nvg][nb] (chunk walks), else [nb][nsec][Nt][nvg]
+    int lane_major_err[2];      // 1: [nsec][ne][Nt][nvg][nb] (k_walk_err_grad), else [nb][nsec][ne][Nt][nvg]
 };
 constexpr int kRedTile = 32;
 template <int D>
@@ -1039,22 +1041,43 @@ __global__ __launch_bounds__(256) void k_sec_reduce(DevProblem P, double *Fdx, d
     }
 }
 
-// The same for F_d2err_dx (or its per-step x_add term), one thread per (b, e, k, u).
+// The same for F_d2err_dx (or its per-step x_add term): rows q = e * Nt * nvg + (k * nvg + u) of every
+// evaluation, through the same LDS transpose (reads evaluation-fastest, writes q-fastest).
 template <int D>
-__global__ void k_sec_reduce_err(DevProblem P, double *Fd2dx, double *part_err_add, SecParts S, int nb) {
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long per = (long)P.Nt * P.nvg;
-    if (t >= (long)nb * P.ne * per) return;
-    const long be = t / per;  // b * ne + e
-    const int b = (int)(be / P.ne), e = (int)(be - (long)b * P.ne);
-    const long r = t - be * per;
-    const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
-    double s = 0.0;
-    for (int c = 0; c < 2; ++c)
-        for (int w = 0; w < S.nsec[c]; ++w)
-            s += S.part_err[c][(((size_t)b * S.nsec[c] + w) * P.ne + e) * per + r];
-    if (u < P.np) Fd2dx[(size_t)be * P.nx + (size_t)k * P.np + u] = s;
-    else part_err_add[((size_t)be * P.Nt + k) * P.na + (u - P.np)] = s;
+__global__ __launch_bounds__(256) void k_sec_reduce_err(DevProblem P, double *Fd2dx, double *part_err_add, SecParts S,
+                                                        int nb) {
+    __shared__ double tile[kRedTile][kRedTile + 1];
+    const long per = (long)P.Nt * P.nvg, rows = per * P.ne;
+    const int b0 = blockIdx.x * kRedTile;
+    const long q0 = (long)blockIdx.y * kRedTile;
+    const int tx = threadIdx.x % kRedTile, ty = threadIdx.x / kRedTile;
+    for (int i = ty; i < kRedTile; i += 256 / kRedTile) {
+        const int b = b0 + tx;
+        const long q = q0 + i;
+        double s = 0.0;
+        if (b < nb && q < rows) {
+            const int e = (int)(q / per);
+            const long r = q - (long)e * per;
+            for (int c = 0; c < 2; ++c)
+                for (int w = 0; w < S.nsec[c]; ++w)
+                    s += S.lane_major_err[c] ? S.part_err[c][(((size_t)w * P.ne + e) * per + r) * nb + b]
+                                             : S.part_err[c][(((size_t)b * S.nsec[c] + w) * P.ne + e) * per + r];
+        }
+        tile[i][tx] = s;
+    }
+    __syncthreads();
+    for (int i = ty; i < kRedTile; i += 256 / kRedTile) {
+        const int b = b0 + i;
+        const long q = q0 + tx;
+        if (b >= nb || q >= rows) continue;
+        const int e = (int)(q / per);
+        const long r = q - (long)e * per;
+        const int k = (int)(r / P.nvg), u = (int)(r - (long)k * P.nvg);
+        const size_t be = (size_t)b * P.ne + e;
+        const double s = tile[tx][i];
+        if (u < P.np) Fd2dx[be * P.nx + (size_t)k * P.np + u] = s;
+        else part_err_add[(be * P.Nt + k) * P.na + (u - P.np)] = s;
+    }
 }
 
 }  // namespace grape

@@ -244,18 +244,18 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                 return hipGetLastError();
             }
             if (stage == 1) {
-                if (P.ne > 0) {  // k_img_fdx reads M'_c (k_walk_grad forms it in the lane)
+                if (P.ne > 0) {  // k_walk_img_sum reads M'_c (k_walk_grad forms it in the lane)
                     mark(GRAPE_KERNEL_REDUCE, 0);
                     const long nmc = (long)B.nb * P.nchunks * D * D;
                     hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
                     mark(GRAPE_KERNEL_REDUCE, 1);
                 }
-                const int kid = P.ne > 0 ? GRAPE_KERNEL_GRAD : GRAPE_KERNEL_WALK_GRAD;  // k_img_fdx / k_walk_grad
+                const int kid = P.ne > 0 ? GRAPE_KERNEL_GRAD : GRAPE_KERNEL_WALK_GRAD;  // k_walk_img_sum / k_walk_grad
                 mark(kid, 0);
                 const hipError_t e = grape_walk::launch<D>(1, P, B, st);
                 mark(kid, 1);
                 if (e != hipSuccess) return e;
-                if (P.ne > 0) {  // the error scans read the walk's images (B.Zl)
+                if (P.ne > 0) {  // the error scans start from the chunk sums of W (B.Wc)
                     mark(GRAPE_KERNEL_ERR_SCAN, 0);
                     launch_err_scan<D>(P, B, st);
                     mark(GRAPE_KERNEL_ERR_SCAN, 1);
@@ -263,7 +263,13 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                 return hipGetLastError();
             }
             if (P.ne == 0) return hipErrorInvalidValue;  // no stage 2 without error sources
-            // stage 2 with error sources: the common F_d2err_dx walks below
+            // stage 2 with error sources: M'_{c,e}, then the F_d2err_dx walks over the lane-minor images
+            mark(GRAPE_KERNEL_ERR_GRAD, 0);
+            const long nmce = (long)B.nb * P.ne * P.nchunks * D * D;
+            hipLaunchKernelGGL(grape::k_sec_mc_err<D>, dim3((unsigned)((nmce + 255) / 256)), dim3(256), 0, st, P, B);
+            const hipError_t e = grape_walk::launch<D>(2, P, B, st);
+            mark(GRAPE_KERNEL_ERR_GRAD, 1);
+            return e != hipSuccess ? e : hipGetLastError();
         }
     }
     if (stage == 0) {
@@ -351,14 +357,16 @@ template <int D>
 hipError_t launch_sector_reduce(const DevProblem &P, const DevBatch &B, const grape::SecParts &S, int nev,
                                 hipStream_t st, const KMark &mark) {
     mark(GRAPE_KERNEL_REDUCE, 0);
-    const long nred = (long)nev * P.Nt * P.nvg, per = (long)P.Nt * P.nvg;
+    const long per = (long)P.Nt * P.nvg;
     hipLaunchKernelGGL(grape::k_sec_reduce<D>,
                        dim3((unsigned)((nev + grape::kRedTile - 1) / grape::kRedTile),
                             (unsigned)((per + grape::kRedTile - 1) / grape::kRedTile)),
                        dim3(256), 0, st, P, B.Fdx, B.part_add, S, nev);
     if (P.ne > 0)
-        hipLaunchKernelGGL(grape::k_sec_reduce_err<D>, dim3((unsigned)((nred * P.ne + 255) / 256)), dim3(256), 0, st,
-                           P, B.Fd2dx, B.part_err_add, S, nev);
+        hipLaunchKernelGGL(grape::k_sec_reduce_err<D>,
+                           dim3((unsigned)((nev + grape::kRedTile - 1) / grape::kRedTile),
+                                (unsigned)((per * P.ne + grape::kRedTile - 1) / grape::kRedTile)),
+                           dim3(256), 0, st, P, B.Fd2dx, B.part_err_add, S, nev);
     if (P.xadd_dep && P.na > 0) {
         DevBatch Be = B;  // the x_add sums run over evaluations, not sub-evaluations
         Be.nb = nev;

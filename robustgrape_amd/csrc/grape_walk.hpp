@@ -28,9 +28,9 @@
 // by the |re|+|im| column bound of A shifted by the midpoint of its diagonal, sm_regime), column
 // by column: column i of exp(A) needs
 // only column i of A, A^2 and the running vector, so no full matrix is materialised for it.
-// Above the Taylor-12 range (exact 1-norm > 0.25) the lane scales A by 2^-s so that
-// |A / 2^s|_1 <= 0.25 and squares s times (Higham's scaling and squaring on the same Taylor
-// approximant) -- where the row-group path parks the item for Julia's Pade 7 / 9 / 13.  Both are
+// Above the Taylor-12 range (exact 1-norm > 0.25) the lane takes Taylor 30 of A / 2^s with
+// |A / 2^s|_1 <= 3.2 and squares s times (Higham's scaling and squaring; kWalkThetaHi) -- where
+// the row-group path parks the item for Julia's Pade 7 / 9 / 13, with the same measured accuracy.  Both are
 // exp(A) to a few ulps (T0); the FD differences keep the reference's (E' - E) / eps form,
 // element by element, before the contraction.
 //
@@ -156,6 +156,24 @@ __device__ __forceinline__ void sm_cube(const SM<D> &A, SM<D> &A2, SM<D> &A3) {
     }
 }
 
+// The high-norm regime (|A - i mu I|_1 > 0.25, where Julia's exp! takes Pade 7 / 9 / 13): Taylor 30
+// (Paterson-Stockmeyer in A^3, kWalkNstHi = 9 Horner steps) of A / 2^s with s = max(0,
+// ceil(log2(|A|_1 / kWalkThetaHi))) and s squarings.  The remainder at 3.2 is 3.2^31 / 31! = 6e-19;
+// the measured errors of E, (E' - E) / eps and the eps2 mixed stencil against an extended-precision
+// reference equal Julia's Pade 13 at every |A|_1 from 0.3 to 80 (scripts/probes/highnorm_study.py,
+// DESIGN.md 4.2), where the round-3 Taylor 12 at 0.25 (s = ceil(log2 4|A|_1): 4 more squarings) was up
+// to 10x worse.  Coefficients by index from constant memory (the Horner loop is not unrolled: a rare
+// path, kept out of the common path's registers and code).
+constexpr double kWalkThetaHi = 3.2;
+constexpr int kWalkNstHi = 9;
+__host__ __device__ constexpr double inv_fact_r(int k) { return k <= 1 ? 1.0 : inv_fact_r(k - 1) / k; }
+static __constant__ double kWalkInvFact[3 * kWalkNstHi + 4] = {
+    inv_fact_r(0),  inv_fact_r(1),  inv_fact_r(2),  inv_fact_r(3),  inv_fact_r(4),  inv_fact_r(5),  inv_fact_r(6),
+    inv_fact_r(7),  inv_fact_r(8),  inv_fact_r(9),  inv_fact_r(10), inv_fact_r(11), inv_fact_r(12), inv_fact_r(13),
+    inv_fact_r(14), inv_fact_r(15), inv_fact_r(16), inv_fact_r(17), inv_fact_r(18), inv_fact_r(19), inv_fact_r(20),
+    inv_fact_r(21), inv_fact_r(22), inv_fact_r(23), inv_fact_r(24), inv_fact_r(25), inv_fact_r(26), inv_fact_r(27),
+    inv_fact_r(28), inv_fact_r(29), inv_fact_r(30)};
+
 // The top coefficients of a Paterson-Stockmeyer evaluation in A^3 with nst Horner steps
 // (degree 3 nst + 3: nst = 1, 2, 3 -> Taylor 6, 9, 12)
 __device__ __forceinline__ double ps_top(int nst, int m) {
@@ -191,8 +209,47 @@ __device__ __forceinline__ void sm_taylor_col(int nst, int i, const SM<D> &A, co
     pin<D>(x);  // the column is final here: nothing of the next one is scheduled into it
 }
 
+// column i of the high-norm regime's Taylor 30 (a2: column i of A^2, from A2 or regenerated)
+template <int D, bool KEEP_A2>
+__device__ __forceinline__ void sm_taylor_col_hi(int i, const SM<D> &A, const SM<D> &A2, const SM<D> &A3, cd (&x)[D]) {
+    cd a2[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        if constexpr (KEEP_A2) {
+            a2[j] = sm_el<D, true>(A2, j, i);
+        } else {
+            cd c = czero();
+#pragma unroll
+            for (int k = 0; k < D; ++k) sm_mac<D, false>(c, A, j, k, sm_el<D, false>(A, k, i));
+            a2[j] = c;
+        }
+    }
+    constexpr int N = kWalkNstHi;
+    {
+        const double k0 = kWalkInvFact[3 * N], k1 = kWalkInvFact[3 * N + 1], k2 = kWalkInvFact[3 * N + 2],
+                     k3 = kWalkInvFact[3 * N + 3];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, a2[j], cscale(k3, sm_el<D, false>(A3, j, i))));
+            if (j == i) x[j].re += k0;
+        }
+    }
+#pragma unroll 1
+    for (int st = N - 1; st >= 0; --st) {
+        cd t[D];
+        sm_matvec<D, false>(A3, x, t);
+        const double k0 = kWalkInvFact[3 * st], k1 = kWalkInvFact[3 * st + 1], k2 = kWalkInvFact[3 * st + 2];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            x[j] = caxpy(k1, sm_el<D, false>(A, j, i), caxpy(k2, a2[j], t[j]));
+            if (j == i) x[j].re += k0;
+        }
+    }
+    pin<D>(x);
+}
+
 // Degree choice (grape_device.hpp expm_prologue_fast, per lane): 0 = diagonal (isdiag), 3 =
-// Taylor 6, 4 = Taylor 9, 5 = Taylor 12, 13 = Taylor 12 of A / 2^s (A scaled here) and s squarings.
+// Taylor 6, 4 = Taylor 9, 5 = Taylor 12, 13 = Taylor 30 of A / 2^s (A scaled here) and s squarings.
 //
 // Diagonal shift (GRAPE_WALK_SHIFT): the walks exponentiate A - i mu I, i.e. they compute
 // E~ = e^{-i mu} exp(A), with mu (`choose`) the midpoint of the diagonal's imaginary parts, which
@@ -261,7 +318,7 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choo
     if (GRAPE_WALK_SHIFT && SHIFT && nA <= 0.1) return 4;
     if (nA <= 0.25) return 5;
     if (!(nA <= 1e300)) return 5;  // NaN / Inf: propagates through the polynomial
-    s = (int)ceil(log2(nA * 4.0));  // |A / 2^s|_1 <= 0.25
+    s = nA <= kWalkThetaHi ? 0 : (int)ceil(log2(nA / kWalkThetaHi));  // |A / 2^s|_1 <= 3.2 (Taylor 30)
     const double f = ldexp(1.0, -s);  // exact
 #pragma unroll
     for (int j = 0; j < D; ++j) A.d[j] *= f;
@@ -352,7 +409,7 @@ __device__ __forceinline__ void walk_expm(SM<D> &A, cd *scr, double &mu, bool ch
 #pragma unroll
     for (int i = 0; i < D; ++i) {  // (unrolled: register arrays are only ever indexed by constants)
         cd x[D];
-        col(3, i, x);
+        sm_taylor_col_hi<D, KEEP_A2>(i, A, A2, A3, x);
 #pragma unroll
         for (int j = 0; j < D; ++j) T[i * D + j] = x[j];
     }
@@ -627,6 +684,12 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #ifndef GRAPE_WALK_G3_WAVES  // k_walk_grad<3, 1> (recomputed propagators)
 #define GRAPE_WALK_G3_WAVES 2
 #endif
+#ifndef GRAPE_WALK_F22_WAVES  // k_walk_fwd<2, 2>: waves per SIMD
+#define GRAPE_WALK_F22_WAVES 3
+#endif
+#ifndef GRAPE_WALK_G22_WAVES  // k_walk_grad<2, 2>
+#define GRAPE_WALK_G22_WAVES 3
+#endif
 #ifndef GRAPE_WALK_G3S_WAVES  // k_walk_grad<3, 1> with stored propagators
 #define GRAPE_WALK_G3S_WAVES 1
 #endif
@@ -641,9 +704,10 @@ struct WalkCfg {
     static constexpr bool KEEP_A2_GRAD = D < 4 || GRAPE_WALK_G4_KEEP_A2_GRAD;
     static constexpr bool KEEP_A2_IMG = D < 4 || GRAPE_WALK_IMG4_KEEP_A2;
     static constexpr bool KEEP_A2_NOM = D < 4 || GRAPE_WALK_G4_KEEP_A2_NOM;
-    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : 3) : D == 3 ? GRAPE_WALK_F3_WAVES : GRAPE_WALK_F4_WAVES;
+    static constexpr int WAVES_FWD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? GRAPE_WALK_F22_WAVES : 3)
+                                   : D == 3 ? GRAPE_WALK_F3_WAVES : GRAPE_WALK_F4_WAVES;
     static constexpr bool FENCE_FWD = D >= 4 && GRAPE_WALK_F4_FENCE;
-    static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? 3 : 2)
+    static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? GRAPE_WALK_G22_WAVES : 2)
                                     : D == 3 ? (NS == 1 ? GRAPE_WALK_G3_WAVES : 1) : GRAPE_WALK_G4_WAVES;
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? GRAPE_WALK_G3S_WAVES : GRAPE_WALK_G4S_WAVES;
     static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? 3 : 2) : 1;  // k_walk_img (error sources)
@@ -1035,8 +1099,8 @@ __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0,
 // column by column into its Zl slot, and finally Q <- E_k Q.  Only the images (9 tiles per step
 // at C3) and the chunk totals T_c (k_scan's input, as k_walk_fwd) reach HBM.  The eps2
 // propagators E(x_u + eps2) and E(err_e eps2) that the mixed stencil needs stay in registers:
-// the walk serves nvg == 1 (one gradient parameter per step: np = 1 without x_add-dependent
-// H0 -- C3); other problems keep the round-2 kernels.
+// the walk serves any number nvg of gradient parameters per step (controls, and x_add when H0 or
+// Herror read it); round 3 served nvg == 1 only.
 struct VArg {
     Pert p;
     int err;
@@ -1052,6 +1116,20 @@ __device__ __forceinline__ VArg vload(cptr<VSpec> p, int i) {
     return a;
 }
 
+// The images of the walk path (B.Zl), lane-minor like the stored propagators (B.Ew): element el of
+// image slot of sector w (of the lane's NS) at step jj of the lane's chunk, lanes = the image walk's
+// launch width (gx * kWalkBlock lanes: one per (chunk, evaluation), evaluation fastest).  A wave's
+// store or load of one element is 64 consecutive complex values (1 KB).
+template <int D, int NS>
+__device__ __forceinline__ size_t img_index(const DevProblem &P, int vy, int jj, int w, int slot, int el, size_t lanes,
+                                            size_t lane) {
+    return (((((size_t)vy * P.L + jj) * NS + w) * P.nz + slot) * (D * D) + el) * lanes + lane;
+}
+// the image walk's launch width for nbe evaluations (walk_lane: per = nbe * nchunks lanes, padded)
+__device__ __forceinline__ size_t img_lanes(const DevProblem &P, int nbe) {
+    return ((size_t)nbe * P.nchunks + kWalkBlock - 1) / kWalkBlock * kWalkBlock;
+}
+
 enum { IMG_DIFF = 0, IMG_MIX = 1, IMG_KEEP_D2 = 2, IMG_KEEP_E2 = 3 };
 template <int K>
 struct ImgKind {
@@ -1062,7 +1140,9 @@ template <int D, int NS>
 __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_walk_img(DevProblem P, DevBatch B) {
     using C = WalkCfg<D, NS>;
     constexpr int TS = D * D;
-    const WalkLane L = walk_lane<NS>(P, B, hw_block());
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<NS>(P, B, vb);
+    const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
     const int ns = P.nsec > 1 ? P.nsec : 1;
     const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
@@ -1151,8 +1231,9 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
                             Z[j][i] = c;
                         }
                     });
-                    // Y = Q^dag Z Q column by column: t = Z q_c, y = Q^dag t; row-major slot tile
-                    cd *dst = act ? B.Zl + ((((size_t)L.be * ns + L.w0 + w) * P.Nt + k) * P.nz + slot) * TS : B.sink;
+                    // Y = Q^dag Z Q column by column: t = Z q_c, y = Q^dag t, lane-minor (img_index): each
+                    // store one coalesced 1-KB row per wave (steps past N_t fill the padding rows)
+                    cd *dst = B.Zl + img_index<D, NS>(P, vb.y, jj, w, slot, 0, lanes, lane);
 #pragma unroll
                     for (int cc = 0; cc < D; ++cc) {
                         cd t[D];
@@ -1168,21 +1249,28 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
                             cd c = czero();
 #pragma unroll
                             for (int m = 0; m < D; ++m) cmac(c, cconj(Q[w][m][r]), t[m]);
-                            dst[r * D + cc] = c;
+                            dst[(size_t)(r * D + cc) * lanes] = c;
                         }
                     }
                 }
             }
         };
-        // the variant table of grape_plan_create (nvg == 1: u = 0)
-        variant(ImgKind<IMG_DIFF>{}, P.off_dx, 0);          // Z1
-        variant(ImgKind<IMG_KEEP_D2>{}, P.off_dx2, 0);      // E(x + eps2)
+        // the variant table of grape_plan_create, for nvg gradient parameters u (controls, then x_add
+        // when H0 / Herror read it).  The mixed stencil of (u, e) needs E(x_u + eps2) and E(err_e eps2)
+        // at once: one of each is kept, so E(err_e eps2) is recomputed for every u > 0 (nvg = 1, C3:
+        // exactly round 3's sequence, each exponential once)
 #pragma unroll 1
-        for (int e = 0; e < P.ne; ++e) {
-            const int ve = P.off_err + e * P.err_stride;
-            variant(ImgKind<IMG_DIFF>{}, ve, P.nvg + e);                   // W_e
-            variant(ImgKind<IMG_KEEP_E2>{}, ve + 1, 0);                    // E(err_e eps2)
-            variant(ImgKind<IMG_MIX>{}, ve + 2, P.nvg + P.ne + e * P.nvg);  // Z2_{e,0}
+        for (int u = 0; u < P.nvg; ++u) variant(ImgKind<IMG_DIFF>{}, P.off_dx + u, u);  // Z1_u
+#pragma unroll 1
+        for (int u = 0; u < P.nvg; ++u) {
+            variant(ImgKind<IMG_KEEP_D2>{}, P.off_dx2 + u, 0);  // E(x_u + eps2)
+#pragma unroll 1
+            for (int e = 0; e < P.ne; ++e) {
+                const int ve = P.off_err + e * P.err_stride;
+                if (u == 0) variant(ImgKind<IMG_DIFF>{}, ve, P.nvg + e);                 // W_e
+                variant(ImgKind<IMG_KEEP_E2>{}, ve + 1, 0);                              // E(err_e eps2)
+                variant(ImgKind<IMG_MIX>{}, ve + 2 + u, P.nvg + P.ne + e * P.nvg + u);  // Z2_{e,u}
+            }
         }
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
@@ -1218,30 +1306,175 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     }
 }
 
-// F_dx terms of the image walk, one thread per (sub-evaluation, step, parameter):
-// F_dx[u, k] (sector part) = Re tr(M'_c Z1_u)   (k_err_local's trace; FidelityCalculations.jl:56-76)
-template <int D>
-__global__ __launch_bounds__(256) void k_img_fdx(DevProblem P, DevBatch B) {
+// ---------------------------------------------------------------------------
+// The image walk's back end (error sources, walk path): walks over the lane-minor images
+// ---------------------------------------------------------------------------
+// Stage 1, k_walk_img_sum: one lane per (chunk c, evaluation) as the image walk, its NS sectors:
+//   F_dx[u, k] (sector part) = Re tr(M'_c Z1_u)          (FidelityCalculations.jl:56-76)
+// written lane-major (B.sec_part, [nsec][Nt][nvg][nbe], as k_walk_grad), and the chunk sums of the
+// error images sum_{k in c} W_{e,k} to B.Wc ([sub-evaluation][ne][nchunks][D][D], row-major tiles:
+// Phase A of k_err_scan, UnitaryCalculations.jl:112).  One read of Z1 and of every W per step.
+template <int D, int NS>
+__global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, DevBatch B) {
     constexpr int TS = D * D;
-    const long n = (long)B.nb * P.Nt * P.nvg;
-    const long g = (long)blockIdx.x * 256 + threadIdx.x;
-    if (g >= n) return;
-    const int u = (int)(g % P.nvg);
-    const long bk = g / P.nvg;
-    const int k = (int)(bk % P.Nt);
-    const long b = bk / P.Nt;
-    const cd *Z = B.Zl + ((size_t)bk * P.nz + u) * TS;
-    const cd *Mc = B.Mc + ((size_t)b * P.nchunks + k / P.L) * TS;
-    double s = 0.0;
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<NS>(P, B, vb);
+    const int ns = P.nsec > 1 ? P.nsec : 1;
+    const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
+    const int k0 = L.c * P.L;
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+        const size_t sub = (size_t)L.be * ns + L.w0 + w;
+        cd Mt[TS];  // M'_c, row-major
+        const cd *Mc = B.Mc + (sub * P.nchunks + L.c) * TS;
+#pragma unroll
+        for (int t = 0; t < TS; ++t) Mt[t] = Mc[t];
+#pragma unroll 1
+        for (int u = 0; u < P.nvg; ++u) {
+#pragma unroll 1
+            for (int jj = 0; jj < P.L; ++jj) {
+                const int k = k0 + jj;
+                const cd *Z = B.Zl + img_index<D, NS>(P, vb.y, jj, w, u, 0, lanes, lane);
+                double s = 0.0;  // sum_ij Re(Z1[i][j] M'[j][i]) in k_img_fdx's (round 3) order
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const cd z = Z[(size_t)(i * D + j) * lanes], m = Mt[j * D + i];
+                        s += z.re * m.re - z.im * m.im;
+                    }
+                }
+                double *dst = (L.ok && k < P.Nt)
+                                  ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
+                                  : reinterpret_cast<double *>(B.sink);
+                *dst = s;
+            }
+        }
+#pragma unroll 1
+        for (int e = 0; e < P.ne; ++e) {
+            cd acc[TS];
+#pragma unroll
+            for (int t = 0; t < TS; ++t) acc[t] = czero();
+#pragma unroll 1
+            for (int jj = 0; jj < P.L; ++jj) {
+                const bool act = k0 + jj < P.Nt;  // (uniform within a chunk's lanes)
+                const cd *Wk = B.Zl + img_index<D, NS>(P, vb.y, jj, w, P.nvg + e, 0, lanes, lane);
+#pragma unroll
+                for (int t = 0; t < TS; ++t) {
+                    const cd v = Wk[(size_t)t * lanes];
+                    acc[t] = act ? cadd(acc[t], v) : acc[t];
+                }
+            }
+            if (L.ok) {
+                cd *dst = B.Wc + ((sub * P.ne + e) * P.nchunks + L.c) * TS;
+#pragma unroll
+                for (int t = 0; t < TS; ++t) dst[t] = acc[t];
+            }
+        }
+    }
+}
+
+// Stage 2, k_walk_err_grad: one lane per (chunk c, evaluation, error e), e fastest (the ne lanes of
+// an evaluation share one wave, so its Z1 rows are fetched once), its NS sectors.  The B_k
+// recurrence of k_err_grad (grape_errpath.hpp) in the lane's registers:
+//   B = T_c M' - M' T_c + M' Ttot at the chunk start, then per step
+//   Lambda = B - M' W_k,  F_d2err_dx[u, k] (sector part) = Re tr(Lambda Z1_{k,u}) + Re tr(M' Z2_{k,e,u}),
+//   B <- Lambda + W_k M'                                 (UnitaryCalculations.jl:112-139,
+//                                                         FidelityCalculations.jl:85-113)
+// with M' = M'_{c,e}, T_c, Ttot from k_err_scan / k_sec_mc_err (B.Me), the images lane-minor.  The
+// terms go lane-major to B.sec_part_err ([nsec][ne][Nt][nvg][nbe]).
+template <int D>
+__device__ __forceinline__ void walk_mm(const cd (&A)[D * D], const cd (&Bm)[D * D], cd (&C)[D * D]) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const cd z = Z[i * D + j], m = Mc[j * D + i];
-            s += z.re * m.re - z.im * m.im;
+            cd c = czero();
+#pragma unroll
+            for (int m = 0; m < D; ++m) cmac(c, A[i * D + m], Bm[m * D + j]);
+            C[i * D + j] = c;
         }
     }
-    B.sec_part[g] = s;  // [(b Nt + k) nvg + u]
+}
+template <int D, int NS>
+__global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    const int ns = P.nsec > 1 ? P.nsec : 1;
+    const int nbe = B.nb / ns;
+    const long per = (long)nbe * P.nchunks;
+    const long gtot = (long)blockIdx.x * kWalkBlock + threadIdx.x;
+    const int e = (int)(gtot % P.ne);
+    const long g = gtot / P.ne;  // the image walk's lane
+    const bool ok = g < per;
+    const long gg = ok ? g : 0;
+    const int c = (int)(gg / nbe), be = (int)(gg - (long)c * nbe);
+    const size_t lanes = img_lanes(P, nbe), lane = (size_t)gg;
+    const int vy = blockIdx.y, w0 = vy * NS;
+    const int k0 = c * P.L;
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+        const size_t sub = (size_t)be * ns + w0 + w;
+        const cd *Mo = B.Me + ((sub * P.ne + e) * P.nchunks + c) * 3 * TS;  // M', T_c, Ttot
+        cd Mp[TS], Bk[TS], T1[TS], T2[TS];
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            Mp[t] = Mo[t];
+            T1[t] = Mo[TS + t];
+        }
+        walk_mm<D>(T1, Mp, Bk);  // T_c M'
+        walk_mm<D>(Mp, T1, T2);  // M' T_c
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            Bk[t] = csub(Bk[t], T2[t]);
+            T1[t] = Mo[2 * TS + t];
+        }
+        walk_mm<D>(Mp, T1, T2);  // M' Ttot
+#pragma unroll
+        for (int t = 0; t < TS; ++t) Bk[t] = cadd(Bk[t], T2[t]);
+        const int w_slot = P.nvg + e, z2_slot = P.nvg + P.ne + e * P.nvg;
+#pragma unroll 1
+        for (int jj = 0; jj < P.L; ++jj) {
+            const int k = k0 + jj;
+            const bool act = ok && k < P.Nt;
+            cd Wk[TS];
+            const cd *Wp = B.Zl + img_index<D, NS>(P, vy, jj, w, w_slot, 0, lanes, lane);
+#pragma unroll
+            for (int t = 0; t < TS; ++t) Wk[t] = Wp[(size_t)t * lanes];
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {  // Lambda_k = B - M' W, in place (no product temporary)
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, Mp[(t / D) * D + m], Wk[m * D + t % D]);
+                Bk[t] = csub(Bk[t], c);
+            }
+#pragma unroll 1
+            for (int u = 0; u < P.nvg; ++u) {
+                const cd *z1 = B.Zl + img_index<D, NS>(P, vy, jj, w, u, 0, lanes, lane);
+                const cd *z2 = B.Zl + img_index<D, NS>(P, vy, jj, w, z2_slot + u, 0, lanes, lane);
+                double s = 0.0;  // sum_i sum_j Lambda[i][j] Z1[j][i] + M'[i][j] Z2[j][i]
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const cd a = z1[(size_t)(j * D + i) * lanes], bz = z2[(size_t)(j * D + i) * lanes];
+                        s += Bk[i * D + j].re * a.re - Bk[i * D + j].im * a.im;
+                        s += Mp[i * D + j].re * bz.re - Mp[i * D + j].im * bz.im;
+                    }
+                }
+                double *dst = act ? B.sec_part_err +
+                                        (((((size_t)(w0 + w) * P.ne + e) * P.Nt + k) * P.nvg + u) * nbe + be)
+                                  : reinterpret_cast<double *>(B.sink);
+                *dst = s;
+            }
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {  // B_{k+1} = Lambda_k + W_k M', in place
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, Wk[(t / D) * D + m], Mp[m * D + t % D]);
+                Bk[t] = cadd(Bk[t], c);
+            }
+        }
+    }
 }
 
 }  // namespace grape

@@ -20,8 +20,10 @@ constexpr int kWalkStoreMinD = GRAPE_WALK_STORE_MIN_D;
 namespace grape_walk {
 // one lane per (sector, evaluation, chunk) of the class: stage 0 = k_walk_fwd (chunk totals to
 // B.Tc), stage 1 = k_walk_grad (per-sector F_dx terms to B.sec_part, evaluation-fastest).  With
-// error sources (P.ne > 0, nvg == 1): stage 0 = k_walk_img (chunk totals and the local-frame images
-// to B.Zl), stage 1 = k_img_fdx (per-sector F_dx terms to B.sec_part, [nb][Nt][nvg])
+// error sources (P.ne > 0, nvg == 1): stage 0 = k_walk_img (chunk totals and the lane-minor
+// local-frame images to B.Zl), stage 1 = k_walk_img_sum (per-sector F_dx terms to B.sec_part,
+// lane-major, and the chunk sums of W to B.Wc), stage 2 = k_walk_err_grad (per-sector F_d2err_dx
+// terms to B.sec_part_err, lane-major)
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
 // Latency-bound calls of the Rydberg layout -- class 0: one 4-level sector (permutation sectors) or

@@ -13,12 +13,14 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
     const long lanes = (long)(B.nb / ns) * P.nchunks;
     const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
     const dim3 blk(grape::kWalkBlock);
-    if (P.ne > 0) {  // error sources: the image walk, then (stage 1) the F_dx traces of its Z1 images
+    if (P.ne > 0) {  // error sources: the image walk, then its back end (grape_walk.hpp)
         if (stage == 0) {
             hipLaunchKernelGGL((grape::k_walk_img<D, NS>), grid, blk, 0, st, P, B);
-        } else {
-            const long n = (long)B.nb * P.Nt * P.nvg;
-            hipLaunchKernelGGL(grape::k_img_fdx<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, B);
+        } else if (stage == 1) {  // F_dx traces of Z1 and the chunk sums of W (k_err_scan's Phase A)
+            hipLaunchKernelGGL((grape::k_walk_img_sum<D, NS>), grid, blk, 0, st, P, B);
+        } else {  // the F_d2err_dx walks, one lane per (chunk, evaluation, error)
+            const dim3 grid_e((unsigned)((lanes * P.ne + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
+            hipLaunchKernelGGL((grape::k_walk_err_grad<D, NS>), grid_e, blk, 0, st, P, B);
         }
         return;
     }

@@ -65,6 +65,7 @@ def _check(test, F, Fdx, F0, g0, tight):
     ("full9", lambda: P.full9_problem(40), P.FULL9_SYM),
     ("full9-one-step", lambda: P.full9_problem(1), P.FULL9_SYM),
     ("full9-chunk-starts", lambda: P.full9_problem(3), P.FULL9_SYM),
+    ("full9-c1-label", lambda: P.full9_problem(256), P.FULL9_SYM),  # |dt H|_1 = 0.327: Taylor 30, no squaring
     ("full9-perm", lambda: P.full9_problem(40), P.FULL9_PERM),
     ("full9-one-step-perm", lambda: P.full9_problem(1), P.FULL9_PERM),
     ("full9-chunk-starts-perm", lambda: P.full9_problem(3), P.FULL9_PERM),

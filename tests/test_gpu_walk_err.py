@@ -83,6 +83,7 @@ def _check_all(test, out, b, ref, tier2, nmain):
 CASES = [
     ("c3", lambda d: P.full9_problem(40, nerr=4, device=d), ((4, 1), (2, 2))),
     ("c3-one-step", lambda d: P.full9_problem(1, nerr=4, device=d), ((4, 1), (2, 2))),
+    ("c3-nt256", lambda d: P.full9_problem(256, nerr=4, device=d), ((4, 1), (2, 2))),  # 0.327: unscaled T2 / T3
     ("c3-chunk-starts", lambda d: P.full9_problem(3, nerr=4, device=d), ((4, 1), (2, 2))),
     ("full9-2err", lambda d: P.full9_problem(33, nerr=2, device=d), ((4, 1), (2, 2))),
     ("sym5-amp-freq", lambda d: P.sym_problem(24, errors=("amp", "freq"), device=d), ((2, 2),)),
@@ -150,12 +151,31 @@ def test_image_walk_single_calls_are_the_batch():
         pl.close()
 
 
-def test_image_walk_not_for_two_gradient_parameters():
-    """An x_add-dependent H0 (nvg = 2 gradient parameters per step) keeps the stored-intermediate
-    kernels: the image walk holds one parameter's eps2 propagators."""
-    fp = P.xadd_err_problem(9, 16)
-    X = np.stack([P.xadd_x(16, s) for s in range(3)])
-    _run(fp, X, expect_walk=False)
+def test_image_walk_several_gradient_parameters():
+    """An x_add-dependent H0 and error generator (tests/problems.py xadd_err_problem: nvg = 3 gradient
+    parameters per step -- the control and both x_add entries) now runs the image walk (round 3 kept
+    the stored-intermediate kernels for nvg > 1): against the committed golden (d = 5, N_t = 40,
+    tests/golden/xadd_err.npz), and against the stored-variant path (GRAPE_OPT_NO_WALK) and the live
+    oracle at d = 9 (sectors of 4 and 2 levels), with test_gpu_xadd_err.py's tiers."""
+    import os
+    from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_WALK
+    from tests.test_gpu_xadd_err import _check
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "xadd_err.npz"),
+                     allow_pickle=False))
+    fp = P.xadd_err_problem(int(g["d"]), int(g["ntimes"]))
+    out, _ = _run(fp, g["x"][None, :], expect_walk=True)
+    _check(tuple(o[0] for o in out), (float(g["F"]), g["F_dx"], g["F_d2err"], g["F_d2err_dx"]), "imgwalk xadd golden")
+    nt = 24
+    f9 = P.xadd_err_problem(9, nt)
+    X = np.stack([P.xadd_x(nt, 70 + s) for s in range(3)])
+    out, sec = _run(f9, X, expect_walk=True)
+    ref, _ = _run(f9, X, OPT_NO_WALK, expect_walk=False)
+    assert sec == ((4, 1), (2, 2))
+    for b in range(len(X)):
+        _check(tuple(o[b] for o in out), tuple(r[b] for r in ref), f"imgwalk xadd d=9 vs stored {b}")
+    _check(tuple(o[1] for o in out), O.calculate_fidelity_and_derivatives(P.xadd_err_problem(9, nt, device=False), X[1]),
+           "imgwalk xadd d=9 vs oracle")
 
 
 def test_image_walk_not_for_non_hermitian_error_generator():
