@@ -251,11 +251,27 @@ def single_eval(fp, nparam, x, seconds=3.0):
         t = time.perf_counter()
         plan.fidelity_grad(X)
         lat.append(time.perf_counter() - t)
+    # the same C entry called as a Julia ccall would: preallocated buffers, no Python wrapper
+    from robustgrape_amd import _capi
+    L, h = _capi.lib(), plan.handle
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    F, Fdx = np.empty(1), np.empty((1, plan.nx))
+    Fd2 = np.empty((1, plan.nerr)) if plan.nerr else None
+    Fd2dx = np.empty((1, plan.nerr, plan.nx)) if plan.nerr else None
+    args = (h, 1, _capi.dptr(X), _capi.dptr(F), _capi.dptr(Fdx), _capi.dptr(Fd2), _capi.dptr(Fd2dx))
+    raw = []
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < min(1.0, seconds):
+        t = time.perf_counter()
+        L.grape_fidelity_grad(*args)
+        raw.append(time.perf_counter() - t)
     plan.close()
-    lat = np.array(lat)
+    lat, raw = np.array(lat), np.array(raw)
     return {"value": len(lat) / lat.sum(), "unit": "gradient-evals/s", "calls": len(lat),
             "latency_ms_median": float(np.median(lat) * 1e3), "latency_ms_p90": float(np.percentile(lat, 90) * 1e3),
-            "note": "nbatch = 1, host arrays in and out (grape_fidelity_grad), one synchronous call per evaluation"}
+            "c_entry_latency_ms_median": float(np.median(raw) * 1e3),
+            "note": "nbatch = 1, host arrays in and out (grape_fidelity_grad), one synchronous call per evaluation; "
+                    "c_entry_*: the same entry through a bare ctypes call with preallocated buffers (a ccall's view)"}
 
 
 def _roofline(kname, flop_launch, ktimes, batch, pmc_path=PMC_SUMMARY):

@@ -191,6 +191,7 @@ struct grape_plan {
     // first (fork / join events; the classes are independent until the sector heads)
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_done = nullptr;  // graph path: completion polled by the host (spin_sync)
     bool capturing = false;  // graph_capture in progress: no fork (one-stream graphs; events captured in a
                              // graph and recorded outside it crashed the runtime, round 3)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
@@ -281,6 +282,7 @@ static void free_plan(grape_plan *p) {
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_done) (void)hipEventDestroy(p->ev_done);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
@@ -1662,6 +1664,16 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     return GRAPE_OK;
 }
 
+// Latency experiment (single evaluations): GRAPE_SPIN_SYNC=1 busy-polls an event after the graph
+// replay instead of hipStreamSynchronize's wait.
+static bool spin_sync() {
+    static const bool on = [] {
+        const char *e = std::getenv("GRAPE_SPIN_SYNC");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 static bool graph_path(const grape_plan *p, int nbatch) {
     const bool disabled = (p->P.opts & GRAPE_OPT_NO_GRAPH) != 0;
     return !disabled && !p->profiling && !p->tables && !p->general_h0 && nbatch > 0 && nbatch <= kGraphBatch &&
@@ -1689,6 +1701,14 @@ static int fidelity_grad_graph(grape_plan *p, int nb, const double *x, double *F
         if (int rc = graph_capture(p, nb, &ex)) return rc;
     std::memcpy(p->h_x, x, (size_t)nb * nx * sizeof(double));
     HIPCHECK(hipGraphLaunch(ex, p->stream));
+    if (spin_sync()) {  // poll the completion instead of a blocking stream synchronize (A/B: GRAPE_SPIN_SYNC)
+        if (!p->ev_done) HIPCHECK(hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(p->ev_done, p->stream));
+        hipError_t q;
+        while ((q = hipEventQuery(p->ev_done)) == hipErrorNotReady) {
+        }
+        if (q != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph replay: ") + hipGetErrorString(q));
+    }
     if (int rc = grape_plan_synchronize(p)) return rc;
     std::memcpy(F, p->h_F, (size_t)nb * sizeof(double));
     std::memcpy(F_dx, p->h_F + B, (size_t)nb * nx * sizeof(double));

@@ -260,7 +260,8 @@ __device__ __forceinline__ void sm_taylor_col_hi(int i, const SM<D> &A, const SM
 // phase cancels in every sandwich the walks form (Y = X E^dag, X E^dag (E' - E), E X E^dag,
 // E^dag dX); only the chunk totals take e^{i sum mu} (walk_phase).  The thresholds bound the
 // Taylor remainder sum_{k > m} |A|^k / k! by ~3e-17 (0.015 at m = 6, 0.1 at m = 9; 2.4e-18 at
-// 0.25, m = 12).  A diagonal A (kind 0) keeps mu = 0 when choosing.
+// 0.25, m = 12).  A diagonal A (kind 0) keeps mu = 0 when choosing, and so does an A whose shifted
+// norm still exceeds 0.25 (the high-norm regime: no Horner step to save, more FD noise).
 #ifndef GRAPE_WALK_SHIFT
 #define GRAPE_WALK_SHIFT 1
 #endif
@@ -281,6 +282,24 @@ __device__ __forceinline__ int sm_regime(SM<D> &A, int &s, double &mu, bool choo
                 hi = fmax(hi, A.d[j]);
             }
             mu = 0.5 * (lo + hi);
+            // Only where the shifted A stays in the Taylor 6 / 9 / 12 regime: above that the shift
+            // saves no Horner step and its rounding raises the eps / eps2 stencils' noise (the
+            // shifted Taylor 30 at |A|_1 = 2.6 ... 84 measured 3-10x Julia's error on F_dx and
+            // F_d2err_dx against an extended-precision exponential, unshifted ~1x:
+            // scripts/probes/shift_noise_study.py).
+            double nsh = 0.0;
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+                double ub = fabs(A.d[c] - mu);
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    if (j == c) continue;
+                    const cd a = sm_el<D, false>(A, j, c);
+                    ub += fabs(a.re) + fabs(a.im);
+                }
+                nsh = fmax(nsh, ub);
+            }
+            if (!(nsh <= 0.25)) mu = 0.0;
         }
 #endif
     }
@@ -672,6 +691,15 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #ifndef GRAPE_WALK_G4_XLDS  // k_walk_grad<4>: 1 = X / Y in the LDS slot and E in registers, 0 = the reverse
 #define GRAPE_WALK_G4_XLDS 1
 #endif
+#ifndef GRAPE_WALK_I21_WAVES  // k_walk_img occupancy: one 2-level sector per lane ...
+#define GRAPE_WALK_I21_WAVES 3
+#endif
+#ifndef GRAPE_WALK_I22_WAVES  // ... or two
+#define GRAPE_WALK_I22_WAVES 2
+#endif
+#ifndef GRAPE_WALK_IMG2_NS1  // the 2-level image walks (error sources) with one sector per lane
+#define GRAPE_WALK_IMG2_NS1 0
+#endif
 #ifndef GRAPE_WALK_IMG_LDS
 #define GRAPE_WALK_IMG_LDS 1
 #endif
@@ -710,7 +738,7 @@ struct WalkCfg {
     static constexpr int WAVES_GRAD = D <= 2 ? (NS == 1 ? 4 : NS == 2 ? GRAPE_WALK_G22_WAVES : 2)
                                     : D == 3 ? (NS == 1 ? GRAPE_WALK_G3_WAVES : 1) : GRAPE_WALK_G4_WAVES;
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? GRAPE_WALK_G3S_WAVES : GRAPE_WALK_G4S_WAVES;
-    static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? 3 : 2) : 1;  // k_walk_img (error sources)
+    static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? GRAPE_WALK_I21_WAVES : GRAPE_WALK_I22_WAVES) : 1;  // k_walk_img
     static constexpr bool IMG_LDS = D >= 4 && GRAPE_WALK_IMG_LDS;      // k_walk_img: eps2 propagators in LDS
     // the diagonal shift + Taylor 9 (sm_regime) for the 4-level class only: it pays where the
     // Taylor-12 columns dominate; the smaller classes (Taylor 6 at C2) measured slower with its

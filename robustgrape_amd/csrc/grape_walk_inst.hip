@@ -56,6 +56,10 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
     const int ns = P.nsec > 1 ? P.nsec : 1;
     if ((long)(B.nb / ns) * P.nchunks <= 0) return hipSuccess;
     if constexpr (D == 2) {  // (the Rydberg two-level classes; a three-level class takes one sector per lane)
+        if (GRAPE_WALK_IMG2_NS1 && P.ne > 0) {
+            launch_ns<D, 1>(stage, P, B, st);
+            return hipGetLastError();
+        }
         if (ns == 2) {
             launch_ns<D, 2>(stage, P, B, st);
             return hipGetLastError();
