@@ -60,6 +60,14 @@ constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScan
 #define GRAPE_FORK_MAX_BATCH 4096
 #endif
 constexpr int kForkMaxBatch = GRAPE_FORK_MAX_BATCH;
+// GRAPE_GRAPH_FORK=1: small calls captured into HIP graphs fork too (off by default, see capturing)
+static bool graph_fork() {
+    static const bool on = [] {
+        const char *e = std::getenv("GRAPE_GRAPH_FORK");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
@@ -191,9 +199,10 @@ struct grape_plan {
     // first (fork / join events; the classes are independent until the sector heads)
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    hipEvent_t ev_done = nullptr;  // graph path: completion polled by the host (spin_sync)
     bool capturing = false;  // graph_capture in progress: no fork (one-stream graphs; events captured in a
-                             // graph and recorded outside it crashed the runtime, round 3)
+                             // graph and recorded outside it crashed the runtime in round 3; round 4's
+                             // probes could not reproduce it: GRAPE_GRAPH_FORK=1 re-enables the fork,
+                             // scripts/probes/graph_fork_stress.py)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -282,7 +291,6 @@ static void free_plan(grape_plan *p) {
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
-    if (p->ev_done) (void)hipEventDestroy(p->ev_done);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->h_status) (void)hipHostFree(p->h_status);
     delete p;
@@ -1409,7 +1417,8 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         // Small calls (latency-bound: the optimiser's line-search rounds, single evaluations) run
         // the second sector class on the auxiliary stream beside the first; large ones keep one
         // stream (no gain there, DESIGN 4.1, and per-kernel event times stay per kernel).
-        const bool fork = p->aux_stream && !p->capturing && nb <= kForkMaxBatch && !(p->P.opts & GRAPE_OPT_NO_FORK);
+        const bool fork = p->aux_stream && (!p->capturing || graph_fork()) && nb <= kForkMaxBatch &&
+                          !(p->P.opts & GRAPE_OPT_NO_FORK);
         // Latency-bound calls of the Rydberg layout: both classes' walks (and scans) in ONE launch per
         // stage (grape_walk_api.hpp launch_pair) -- neither a graph branch nor a second stream overlaps
         // them inside a captured graph on this runtime.  pa: the 4- (or 3-) level class, pb: the 2-level one.
@@ -1664,16 +1673,6 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     return GRAPE_OK;
 }
 
-// Latency experiment (single evaluations): GRAPE_SPIN_SYNC=1 busy-polls an event after the graph
-// replay instead of hipStreamSynchronize's wait.
-static bool spin_sync() {
-    static const bool on = [] {
-        const char *e = std::getenv("GRAPE_SPIN_SYNC");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 static bool graph_path(const grape_plan *p, int nbatch) {
     const bool disabled = (p->P.opts & GRAPE_OPT_NO_GRAPH) != 0;
     return !disabled && !p->profiling && !p->tables && !p->general_h0 && nbatch > 0 && nbatch <= kGraphBatch &&
@@ -1701,14 +1700,6 @@ static int fidelity_grad_graph(grape_plan *p, int nb, const double *x, double *F
         if (int rc = graph_capture(p, nb, &ex)) return rc;
     std::memcpy(p->h_x, x, (size_t)nb * nx * sizeof(double));
     HIPCHECK(hipGraphLaunch(ex, p->stream));
-    if (spin_sync()) {  // poll the completion instead of a blocking stream synchronize (A/B: GRAPE_SPIN_SYNC)
-        if (!p->ev_done) HIPCHECK(hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming));
-        HIPCHECK(hipEventRecord(p->ev_done, p->stream));
-        hipError_t q;
-        while ((q = hipEventQuery(p->ev_done)) == hipErrorNotReady) {
-        }
-        if (q != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph replay: ") + hipGetErrorString(q));
-    }
     if (int rc = grape_plan_synchronize(p)) return rc;
     std::memcpy(F, p->h_F, (size_t)nb * sizeof(double));
     std::memcpy(F_dx, p->h_F + B, (size_t)nb * nx * sizeof(double));

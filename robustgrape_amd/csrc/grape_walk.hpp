@@ -1342,6 +1342,11 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 // written lane-major (B.sec_part, [nsec][Nt][nvg][nbe], as k_walk_grad), and the chunk sums of the
 // error images sum_{k in c} W_{e,k} to B.Wc ([sub-evaluation][ne][nchunks][D][D], row-major tiles:
 // Phase A of k_err_scan, UnitaryCalculations.jl:112).  One read of Z1 and of every W per step.
+// GRAPE_WALK_FDX_IN_ERR (default): the F_dx traces are taken by k_walk_err_grad's e = 0 lanes, which
+// read Z1 anyway, so this kernel reads only the W images (C3: 5 -> 4 of the 9 tiles per step).
+#ifndef GRAPE_WALK_FDX_IN_ERR
+#define GRAPE_WALK_FDX_IN_ERR 1
+#endif
 template <int D, int NS>
 __global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, DevBatch B) {
     constexpr int TS = D * D;
@@ -1353,6 +1358,7 @@ __global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, De
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
         const size_t sub = (size_t)L.be * ns + L.w0 + w;
+#if !GRAPE_WALK_FDX_IN_ERR
         cd Mt[TS];  // M'_c, row-major
         const cd *Mc = B.Mc + (sub * P.nchunks + L.c) * TS;
 #pragma unroll
@@ -1378,6 +1384,7 @@ __global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, De
                 *dst = s;
             }
         }
+#endif
 #pragma unroll 1
         for (int e = 0; e < P.ne; ++e) {
             cd acc[TS];
@@ -1460,10 +1467,33 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
 #pragma unroll
         for (int t = 0; t < TS; ++t) Bk[t] = cadd(Bk[t], T2[t]);
         const int w_slot = P.nvg + e, z2_slot = P.nvg + P.ne + e * P.nvg;
+#if GRAPE_WALK_FDX_IN_ERR
+        const cd *Mc = B.Mc + (sub * P.nchunks + c) * TS;  // M'_c (the e = 0 lanes: F_dx)
+#endif
 #pragma unroll 1
         for (int jj = 0; jj < P.L; ++jj) {
             const int k = k0 + jj;
             const bool act = ok && k < P.Nt;
+#if GRAPE_WALK_FDX_IN_ERR
+            if (e == 0) {  // F_dx[u, k] (sector part) = Re tr(M'_c Z1_u), k_walk_img_sum's order
+#pragma unroll 1
+                for (int u = 0; u < P.nvg; ++u) {
+                    const cd *Z = B.Zl + img_index<D, NS>(P, vy, jj, w, u, 0, lanes, lane);
+                    double s = 0.0;
+#pragma unroll
+                    for (int i = 0; i < D; ++i) {
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            const cd z = Z[(size_t)(i * D + j) * lanes], m = Mc[j * D + i];
+                            s += z.re * m.re - z.im * m.im;
+                        }
+                    }
+                    double *dst = act ? B.sec_part + ((((size_t)(w0 + w) * P.Nt) + k) * P.nvg + u) * nbe + be
+                                      : reinterpret_cast<double *>(B.sink);
+                    *dst = s;
+                }
+            }
+#endif
             cd Wk[TS];
             const cd *Wp = B.Zl + img_index<D, NS>(P, vy, jj, w, w_slot, 0, lanes, lane);
 #pragma unroll
