@@ -1468,32 +1468,17 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
         for (int t = 0; t < TS; ++t) Bk[t] = cadd(Bk[t], T2[t]);
         const int w_slot = P.nvg + e, z2_slot = P.nvg + P.ne + e * P.nvg;
 #if GRAPE_WALK_FDX_IN_ERR
-        const cd *Mc = B.Mc + (sub * P.nchunks + c) * TS;  // M'_c (the e = 0 lanes: F_dx)
+        cd Mc[TS];  // M'_c (F_dx; every e-lane of an evaluation loads the same rows, the e = 0 lane stores)
+        {
+            const cd *Mcp = B.Mc + (sub * P.nchunks + c) * TS;
+#pragma unroll
+            for (int t = 0; t < TS; ++t) Mc[t] = Mcp[t];
+        }
 #endif
 #pragma unroll 1
         for (int jj = 0; jj < P.L; ++jj) {
             const int k = k0 + jj;
             const bool act = ok && k < P.Nt;
-#if GRAPE_WALK_FDX_IN_ERR
-            if (e == 0) {  // F_dx[u, k] (sector part) = Re tr(M'_c Z1_u), k_walk_img_sum's order
-#pragma unroll 1
-                for (int u = 0; u < P.nvg; ++u) {
-                    const cd *Z = B.Zl + img_index<D, NS>(P, vy, jj, w, u, 0, lanes, lane);
-                    double s = 0.0;
-#pragma unroll
-                    for (int i = 0; i < D; ++i) {
-#pragma unroll
-                        for (int j = 0; j < D; ++j) {
-                            const cd z = Z[(size_t)(i * D + j) * lanes], m = Mc[j * D + i];
-                            s += z.re * m.re - z.im * m.im;
-                        }
-                    }
-                    double *dst = act ? B.sec_part + ((((size_t)(w0 + w) * P.Nt) + k) * P.nvg + u) * nbe + be
-                                      : reinterpret_cast<double *>(B.sink);
-                    *dst = s;
-                }
-            }
-#endif
             cd Wk[TS];
             const cd *Wp = B.Zl + img_index<D, NS>(P, vy, jj, w, w_slot, 0, lanes, lane);
 #pragma unroll
@@ -1510,6 +1495,7 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
                 const cd *z1 = B.Zl + img_index<D, NS>(P, vy, jj, w, u, 0, lanes, lane);
                 const cd *z2 = B.Zl + img_index<D, NS>(P, vy, jj, w, z2_slot + u, 0, lanes, lane);
                 double s = 0.0;  // sum_i sum_j Lambda[i][j] Z1[j][i] + M'[i][j] Z2[j][i]
+                double sdx = 0.0;  // F_dx: sum_i sum_j M'_c[i][j] Z1[j][i] (from the same Z1 loads)
 #pragma unroll
                 for (int i = 0; i < D; ++i) {
 #pragma unroll
@@ -1517,8 +1503,20 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
                         const cd a = z1[(size_t)(j * D + i) * lanes], bz = z2[(size_t)(j * D + i) * lanes];
                         s += Bk[i * D + j].re * a.re - Bk[i * D + j].im * a.im;
                         s += Mp[i * D + j].re * bz.re - Mp[i * D + j].im * bz.im;
+#if GRAPE_WALK_FDX_IN_ERR
+                        sdx += Mc[i * D + j].re * a.re - Mc[i * D + j].im * a.im;
+#endif
                     }
                 }
+#if GRAPE_WALK_FDX_IN_ERR
+                if (e == 0) {  // F_dx[u, k] (sector part) = Re tr(M'_c Z1_u)
+                    double *dx = act ? B.sec_part + ((((size_t)(w0 + w) * P.Nt) + k) * P.nvg + u) * nbe + be
+                                     : reinterpret_cast<double *>(B.sink);
+                    *dx = sdx;
+                }
+#else
+                (void)sdx;
+#endif
                 double *dst = act ? B.sec_part_err +
                                         (((((size_t)(w0 + w) * P.ne + e) * P.Nt + k) * P.nvg + u) * nbe + be)
                                   : reinterpret_cast<double *>(B.sink);

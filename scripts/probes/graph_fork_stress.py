@@ -1,11 +1,11 @@
 """Stress of the captured fork/join: small calls whose HIP graphs fork the second
-sector class onto the auxiliary stream (GRAPE_GRAPH_FORK=1, set before the library loads), mixed
+sector class onto the auxiliary stream (the default since round 4; GRAPE_GRAPH_FORK=0 turns it off), mixed
 with eager fork/join calls that record and wait on the same plan events, through the graph cache's
 eviction (10 batch sizes, 8 cached graphs).  Every output is compared bitwise with a plan that
 neither forks nor captures (GRAPE_OPT_NO_FORK | GRAPE_OPT_NO_GRAPH): the fork changes only which
 stream a kernel runs on, never its arithmetic.
 
-    GRAPE_GRAPH_FORK=1 python scripts/probes/graph_fork_stress.py c3|c2 ITERATIONS
+    python scripts/probes/graph_fork_stress.py c3|c2 ITERATIONS
 
 c3: C3 (two walk classes with error sources); c2: C2 with GRAPE_OPT_NO_PAIR (the two classes as
 separate launches, so they fork).  Prints a progress line every 500 iterations and "OK" at the end;
