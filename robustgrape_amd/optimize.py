@@ -497,7 +497,9 @@ class RobustCost:
             from . import regularization as REG
             kinds = [2 if fn is REG.regularization_cost_phase else 1 if fn is REG.regularization_cost else -1
                      for fn in self.regs]
-            if not self.plan.tables and all(k > 0 for k in kinds) and 4 <= self.ntimes <= 4096:
+            # (grape_robust_cost reads one regulariser kind per control parameter)
+            if (not self.plan.tables and len(kinds) == nparam and all(k > 0 for k in kinds)
+                    and 4 <= self.ntimes <= 4096):
                 dev = self.device
                 self._fused = {"kind": torch.tensor(kinds, dtype=torch.int32, device=dev),
                                "c1": torch.tensor(self.c1, dtype=torch.float64, device=dev),

@@ -70,10 +70,10 @@ def _check_all(test, out, b, ref, tier2, nmain):
     told = max(T3, t2) * sd + max(T3_ABS, t2a)
     record(test, "F_d2err_dx", ed, sd, told)
     assert ed <= told, (test, "F_d2err_dx", ed, sd)
-    # x_add part: absolute, scaled by the step-norm factor of the long-step tier like the rest
-    # (tests/problems.py fd_tier: 1 for short steps, max_k |dt H_k|_1 where the walks square)
+    # x_add part: absolute and unscaled (round 3 scaled it with the step-norm tier; with Taylor 30 and
+    # the shift confined to low norms the high-norm cases measure 6.8e-7, the bench-size ones 5e-6)
     ea = float(np.max(np.abs(d2dx[nmain:] - r2dx[nmain:])))
-    tola = T3_XADD_ABS * max(1.0, t2 / 1e-6)
+    tola = T3_XADD_ABS
     record(test, "F_d2err_dx_add", ea, 0.0, tola)
     assert ea <= tola, (test, "F_d2err_dx_add", ea)
     print(f"{test}: |dF| {ef:.1e} F_dx {err / sc:.1e} F_d2err {e0 / max(s0, 1e-300):.1e} "
