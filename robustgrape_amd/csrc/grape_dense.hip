@@ -315,7 +315,9 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dmc(DenseProblem DP, DenseBatch
     img_store(B.Mc + ((size_t)b * DP.Nc + c) * IMG, X, ln);
 }
 
-// F_dx[p, k] for every control p of step k
+// F_dx[p, k] for every control p of step k, and (H0 reading x_add, DP.nva > 0) step k's term of
+// F_dx_add[q] = Re tr(M'_c Y((E(x_add + eps e_q) - E) / eps)) to B.Fadd (UnitaryCalculations.jl:57-64:
+// the x_add variant of every step, FidelityCalculations.jl:67-76: summed with the target's part)
 __global__ __launch_bounds__(NTHREADS, 1) void k_dgrad(DenseProblem DP, DenseBatch B) {
     extern __shared__ double lds[];
     const Lane ln = make_lane();
@@ -347,10 +349,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dgrad(DenseProblem DP, DenseBat
     double *zimg = B.Z + (size_t)item * IMG;
     img_store(zimg, Z, ln);
     const double *xb = B.x + (size_t)b * P.nx;
-    for (int p = 0; p < P.np; ++p) {
+    for (int p = 0; p < P.np + DP.nva; ++p) {
         grape::Pert pp;
-        pp.var = grape::VAR_X;
-        pp.index = p;
+        pp.var = p < P.np ? grape::VAR_X : grape::VAR_XADD;
+        pp.index = p < P.np ? p : p - P.np;
         pp.delta = P.eps;
         HM A, X;
         bool singular = false;
@@ -368,8 +370,28 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dgrad(DenseProblem DP, DenseBat
                 acc += Z.re[i][r] * dr - Z.im[i][r] * di;
             }
         const double s = wg_sum(acc, lds, ln);
-        if (threadIdx.x == 0) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + p] = s;
+        if (threadIdx.x == 0) {
+            if (p < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + p] = s;
+            else B.Fadd[(size_t)item * DP.nva + (p - P.np)] = s;
+        }
     }
+}
+
+// F_dx_add[q] += sum_k Fadd[k][q] (after k_dcarry wrote the target's part), one workgroup per (b, q),
+// fixed summation order
+__global__ __launch_bounds__(256) void k_dadd(DenseProblem DP, DenseBatch B) {
+    const grape::DevProblem &P = DP.P;
+    const int b = blockIdx.x / DP.nva, q = blockIdx.x % DP.nva;
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int k = threadIdx.x; k < P.Nt; k += 256) s += B.Fadd[((size_t)b * P.Nt + k) * DP.nva + q];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) B.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] += red[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -751,6 +773,7 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     if (P.P.ne == 0) {
         mark(GRAPE_KERNEL_DGRAD, 0);
         hipLaunchKernelGGL(k_dgrad, dim3(nsteps), dim3(NTHREADS), kLds, st, P, B);
+        if (P.nva > 0) hipLaunchKernelGGL(k_dadd, dim3((unsigned)(B.nb * P.nva)), dim3(256), 0, st, P, B);
         mark(GRAPE_KERNEL_DGRAD, 1);
         return hipGetLastError();
     }

@@ -16,6 +16,7 @@ struct DenseProblem {
     const double *W;      // [64] projector diagonal, zero-padded
     int Lc, Nc;           // chunk length / count of the prefix-product scan
     int nz;               // error path: local-frame slots per step, np (Z1) + ne (W) + ne np (Z2)
+    int nva;              // x_add gradient variants per step: na when H0 reads x_add (no error sources), else 0
 };
 
 struct DenseBatch {
@@ -29,6 +30,7 @@ struct DenseBatch {
     double *Z;        // [nb][Nt][IMG]   k_dgrad's Z_k, parked in HBM across the eps-variant exps
     double *F;        // [nb]
     double *Fdx;      // [nb][nx]
+    double *Fadd;     // [nb][Nt][nva]   H0 reads x_add: step k's term of F_dx_add[q] (k_dgrad; k_dadd sums)
     int *status;      // bit 0: singular Pade denominator
     int *mstats;      // optional [5]: Pade degree histogram (m = 3, 5, 7, 9, 13)
     // error path (P.ne > 0; the algebra of grape_errpath.hpp on 64 x 64 images):

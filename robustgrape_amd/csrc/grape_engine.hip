@@ -145,34 +145,6 @@ hipError_t dalloc(T **p, size_t n) {
     return hipMalloc(reinterpret_cast<void **>(p), n * sizeof(T));
 }
 
-// device graph path: staging copies (grape_fidelity_grad_device_async, small calls)
-__global__ void k_dg_in(const double *src, double *dst, int nb, int nbB, int nx) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long)nbB * nx) return;
-    const long r = i / nx, q = i - r * nx;
-    dst[i] = src[(r < nb ? r : nb - 1) * nx + q];  // bucket rows past nb repeat the last row
-}
-struct DgOut {
-    double *F, *Fdx, *Fd2, *Fd2dx;
-};
-// g: F [nbB] | F_dx [nbB][nx] | F_d2err [nbB][ne] | F_d2err_dx [nbB][ne][nx]; the first nb rows out
-__global__ void k_dg_out(const double *g, DgOut o, int nb, int nbB, int nx, int ne) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long n0 = nbB, n1 = (long)nbB * nx, n2 = (long)nbB * ne, n3 = (long)nbB * ne * nx;
-    if (i < n0) {
-        if (i < nb) o.F[i] = g[i];
-    } else if (i < n0 + n1) {
-        const long j = i - n0;
-        if (j < (long)nb * nx) o.Fdx[j] = g[i];
-    } else if (i < n0 + n1 + n2) {
-        const long j = i - n0 - n1;
-        if (j < (long)nb * ne) o.Fd2[j] = g[i];
-    } else if (i < n0 + n1 + n2 + n3) {
-        const long j = i - n0 - n1 - n2;
-        if (j < (long)nb * ne * nx) o.Fd2dx[j] = g[i];
-    }
-}
-
 }  // namespace
 
 struct grape_plan {
@@ -238,7 +210,8 @@ struct grape_plan {
     grape_dense::DenseProblem DP{};
     double *dn_opimg = nullptr, *dn_W = nullptr, *dn_E = nullptr, *dn_Q = nullptr, *dn_Carry = nullptr,
            *dn_M = nullptr, *dn_Mc = nullptr, *dn_Z = nullptr, *dn_Ub = nullptr, *dn_Zl = nullptr, *dn_Vc = nullptr,
-           *dn_Sx = nullptr, *dn_Tot = nullptr, *dn_Me = nullptr, *dn_Mp = nullptr, *dn_B0 = nullptr;
+           *dn_Sx = nullptr, *dn_Tot = nullptr, *dn_Me = nullptr, *dn_Mp = nullptr, *dn_B0 = nullptr,
+           *dn_Fadd = nullptr;
     // grape_unitary_derivs workspace (allocated on first use)
     grape::VSpec *ud_vs = nullptr;
     cd *ud_E = nullptr, *ud_C = nullptr, *ud_V = nullptr, *ud_S = nullptr, *ud_out = nullptr;
@@ -264,20 +237,6 @@ struct grape_plan {
     // graph path: F ([kGraphBatch]) and F_dx ([nb][nx]) of a call side by side in one device block
     // (h_F is its pinned image), so one D2H copy returns both
     double *d_gout = nullptr;
-    // small DEVICE-pointer calls (the optimiser's few-row line-search rounds, grape_fidelity_grad_
-    // device_async): one captured graph per batch bucket (powers of two up to kGraphBatch) over
-    // plan-owned staging rows; the copy-in / copy-out kernels' arguments (the caller's pointers and
-    // row count) are set per replay
-    struct DevGraphEntry {
-        int nb;  // bucket
-        hipGraph_t graph;
-        hipGraphExec_t exec;
-        hipGraphNode_t in_node, out_node;
-        dim3 in_grid, out_grid;
-    };
-    std::vector<DevGraphEntry> dgraphs;
-    bool dgraph_broken = false;  // node lookup failed once: device calls stay on the stream path
-    double *d_dgx = nullptr, *d_dgout = nullptr;  // staging: x rows; F | F_dx | F_d2err | F_d2err_dx
     // time-sharded evaluations (grape_slice_*): column-major U_slice / M' staging (2 d x d)
     cd *d_slice = nullptr;
     bool uses_tstep = false;  // some H0 term reads the step index (slices would need its offset)
@@ -310,12 +269,12 @@ static void free_plan(grape_plan *p) {
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_Zl, p->d_ovf2, p->d_ovf2_slots,
                     p->dn_opimg, p->dn_W, p->dn_E, p->dn_Q, p->dn_Carry, p->dn_M, p->dn_Mc, p->dn_Z,
-                    p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0,
+                    p->dn_Ub, p->dn_Zl, p->dn_Vc, p->dn_Sx, p->dn_Tot, p->dn_Me, p->dn_Mp, p->dn_B0, p->dn_Fadd,
                     p->ud_vs, p->ud_E, p->ud_C, p->ud_V, p->ud_S, p->ud_out, p->ud_ovf, p->ud_gscr, p->ud_Eimg,
                     p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
                     p->d_fixed, p->d_gout, p->d_slice, p->d_ops_sym, p->d_opsT_sym, p->d_PA_sym, p->d_PB_sym,
-                    p->d_W_sym, p->d_dgx, p->d_dgout};
+                    p->d_W_sym};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
@@ -330,10 +289,6 @@ static void free_plan(grape_plan *p) {
         (void)hipEventDestroy(pe.b);
     }
     for (auto &g : p->graphs) (void)hipGraphExecDestroy(g.exec);
-    for (auto &g : p->dgraphs) {
-        (void)hipGraphExecDestroy(g.exec);
-        (void)hipGraphDestroy(g.graph);
-    }
     for (double *h : {p->h_x, p->h_F, p->h_Fd2, p->h_Fd2dx})
         if (h) (void)hipHostFree(h);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
@@ -740,7 +695,10 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
                         int n_err_terms) {
     const double trP = ps.trP;
     const int D = desc->ndim, ne = desc->nerr;
-    if (xadd_dep) return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 / Herror must not depend on x_add");
+    // H0 reading x_add: k_dgrad adds each step's x_add variant (DP.nva); with error sources the
+    // dense error path has no x_add variants
+    if (xadd_dep && ne > 0)
+        return fail(GRAPE_ERR_UNSUPPORTED, "dense engine: H0 / Herror must not depend on x_add with error sources");
     // Hermitian H0: checked for every engine in grape_plan_create (the dense no-interchange
     // solve relies on it too, grape_dense.hpp).  The error variants exponentiate
     // H0 + err Herror (err <= eps2): Hermitian error terms keep them inside that proof.
@@ -795,6 +753,7 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
     P.nvg = P.np;
     DP.nz = P.np * (1 + ne) + ne;
     P.nz = DP.nz;
+    DP.nva = xadd_dep ? P.na : 0;
     // scan chunking: ~sqrt(N_t) chunks balances the chunk chains against the carry chain
     int nc = (int)std::ceil(std::sqrt((double)P.Nt));
     DP.Lc = (P.Nt + nc - 1) / nc;
@@ -813,6 +772,7 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
               dalloc(&p->d_x, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_F, MB) == hipSuccess && dalloc(&p->d_Fdx, MB * P.nx) == hipSuccess &&
               dalloc(&p->d_ctrl, kCtrlInts) == hipSuccess;
+    if (ok && DP.nva > 0) ok = dalloc(&p->dn_Fadd, MB * P.Nt * DP.nva) == hipSuccess;
     if (ok && ne > 0)
         ok = dalloc(&p->dn_Ub, MB * IMG) == hipSuccess && dalloc(&p->dn_Zl, MB * P.Nt * DP.nz * IMG) == hipSuccess &&
              dalloc(&p->dn_Vc, MB * NE * DP.Nc * IMG) == hipSuccess &&
@@ -1374,6 +1334,7 @@ static grape_dense::DenseBatch dense_batch(grape_plan *p, int nb, const double *
     DB.Fd2dx = d_Fd2dx;
     DB.F = d_F;
     DB.Fdx = d_Fdx;
+    DB.Fadd = p->dn_Fadd;
     DB.status = p->d_ctrl + 2;
     DB.mstats = nullptr;
     DB.gp_scr = p->d_gpscr;
@@ -1644,109 +1605,6 @@ static void resolve_events(grape_plan *p) {
     p->pending.clear();
 }
 
-// ---- device graph path (small device-pointer calls) ----
-constexpr int kDevGraphBatch = 64;  // = kGraphBatch of the host path
-
-static bool dgraph_path(const grape_plan *p, int nbatch) {
-    const bool disabled = (p->P.opts & GRAPE_OPT_NO_GRAPH) != 0 || p->dgraph_broken;
-    return !disabled && !p->profiling && !p->tables && !p->general_h0 && nbatch > 0 && nbatch <= kDevGraphBatch &&
-           nbatch <= p->max_batch;
-}
-
-static int dgraph_bucket(const grape_plan *p, int nb) {
-    int b = 1;
-    while (b < nb) b <<= 1;
-    return std::min(b, std::min(kDevGraphBatch, p->max_batch));
-}
-
-static int dgraph_set_args(grape_plan::DevGraphEntry &g, hipGraphExec_t ex, const double *x, DgOut o, int nb, int nx,
-                           int ne, double *dgx, const double *dgout) {
-    int nbB = g.nb;
-    hipKernelNodeParams kin{};
-    void *ain[] = {(void *)&x, (void *)&dgx, (void *)&nb, (void *)&nbB, (void *)&nx};
-    kin.func = reinterpret_cast<void *>(&k_dg_in);
-    kin.gridDim = g.in_grid;
-    kin.blockDim = dim3(256);
-    kin.sharedMemBytes = 0;
-    kin.kernelParams = ain;
-    kin.extra = nullptr;
-    HIPCHECK(hipGraphExecKernelNodeSetParams(ex, g.in_node, &kin));
-    hipKernelNodeParams kout{};
-    void *aout[] = {(void *)&dgout, (void *)&o, (void *)&nb, (void *)&nbB, (void *)&nx, (void *)&ne};
-    kout.func = reinterpret_cast<void *>(&k_dg_out);
-    kout.gridDim = g.out_grid;
-    kout.blockDim = dim3(256);
-    kout.sharedMemBytes = 0;
-    kout.kernelParams = aout;
-    kout.extra = nullptr;
-    HIPCHECK(hipGraphExecKernelNodeSetParams(ex, g.out_node, &kout));
-    return GRAPE_OK;
-}
-
-static int fidelity_grad_dgraph(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_F_dx, double *d_Fd2,
-                                double *d_Fd2dx) {
-    const int nx = p->P.nx, ne = p->P.ne, B = std::min(kDevGraphBatch, p->max_batch);
-    if (!p->d_dgx) {
-        if (dalloc(&p->d_dgx, (size_t)B * nx) != hipSuccess ||
-            dalloc(&p->d_dgout, (size_t)B * (1 + nx + ne + (size_t)ne * nx)) != hipSuccess)
-            return fail(GRAPE_ERR_ALLOC, "device allocation failed (device graph path)");
-    }
-    const int nbB = dgraph_bucket(p, nb);
-    const DgOut o{d_F, d_F_dx, ne ? d_Fd2 : nullptr, ne ? d_Fd2dx : nullptr};
-    grape_plan::DevGraphEntry *g = nullptr;
-    for (auto &e : p->dgraphs)
-        if (e.nb == nbB) g = &e;
-    hipStream_t st = p->stream;
-    if (!g) {  // capture: copy-in, the pipeline on the staging rows, copy-out
-        grape_plan::DevGraphEntry e{};
-        e.nb = nbB;
-        e.in_grid = dim3((unsigned)(((long)nbB * nx + 255) / 256));
-        e.out_grid = dim3((unsigned)(((long)nbB * (1 + nx + ne + (long)ne * nx) + 255) / 256));
-        double *F0 = p->d_dgout, *Fdx0 = F0 + nbB, *Fd20 = Fdx0 + (size_t)nbB * nx, *Fd2dx0 = Fd20 + (size_t)nbB * ne;
-        HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        hipLaunchKernelGGL(k_dg_in, e.in_grid, dim3(256), 0, st, d_x, p->d_dgx, nb, nbB, nx);
-        p->capturing = true;
-        int rc = enqueue_call(p, nbB, p->d_dgx, F0, Fdx0, ne ? Fd20 : nullptr, ne ? Fd2dx0 : nullptr);
-        p->capturing = false;
-        hipLaunchKernelGGL(k_dg_out, e.out_grid, dim3(256), 0, st, (const double *)p->d_dgout, o, nb, nbB, nx, ne);
-        hipGraph_t gr = nullptr;
-        const hipError_t ec = hipStreamEndCapture(st, &gr);
-        if (rc) {
-            if (gr) (void)hipGraphDestroy(gr);
-            return rc;
-        }
-        if (ec != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("device graph capture: ") + hipGetErrorString(ec));
-        size_t n = 0;
-        HIPCHECK(hipGraphGetNodes(gr, nullptr, &n));
-        std::vector<hipGraphNode_t> nodes(n);
-        HIPCHECK(hipGraphGetNodes(gr, nodes.data(), &n));
-        for (hipGraphNode_t nd : nodes) {
-            hipGraphNodeType t;
-            if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
-            hipKernelNodeParams kp{};
-            if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess) continue;
-            if (kp.func == reinterpret_cast<void *>(&k_dg_in)) e.in_node = nd;
-            if (kp.func == reinterpret_cast<void *>(&k_dg_out)) e.out_node = nd;
-        }
-        if (!e.in_node || !e.out_node) {  // (not expected): this call and every later one on the stream path
-            (void)hipGraphDestroy(gr);
-            p->dgraph_broken = true;
-            return enqueue_call(p, nb, d_x, d_F, d_F_dx, ne ? d_Fd2 : nullptr, ne ? d_Fd2dx : nullptr);
-        }
-        const hipError_t ei = hipGraphInstantiate(&e.exec, gr, nullptr, nullptr, 0);
-        if (ei != hipSuccess) {
-            (void)hipGraphDestroy(gr);
-            return fail(GRAPE_ERR_HIP, std::string("device graph instantiate: ") + hipGetErrorString(ei));
-        }
-        e.graph = gr;
-        p->dgraphs.push_back(e);
-        g = &p->dgraphs.back();
-    }
-    if (int rc = dgraph_set_args(*g, g->exec, d_x, o, nb, nx, ne, p->d_dgx, p->d_dgout)) return rc;
-    HIPCHECK(hipGraphLaunch(g->exec, st));
-    return GRAPE_OK;
-}
-
 int grape_fidelity_grad_device_async(grape_plan *p, int nbatch, const double *d_x, double *d_F, double *d_F_dx,
                                      double *d_F_d2err, double *d_F_d2err_dx) {
     if (!p || nbatch < 0 || (nbatch > 0 && (!d_x || !d_F || !d_F_dx))) return fail(GRAPE_ERR_INVALID, "bad argument");
@@ -1754,7 +1612,6 @@ int grape_fidelity_grad_device_async(grape_plan *p, int nbatch, const double *d_
     if (p->P.ne > 0 && nbatch > 0 && (!d_F_d2err || !d_F_d2err_dx))
         return fail(GRAPE_ERR_INVALID, "error sources need F_d2err and F_d2err_dx outputs");
     HIPCHECK(hipSetDevice(p->device));
-    if (dgraph_path(p, nbatch)) return fidelity_grad_dgraph(p, nbatch, d_x, d_F, d_F_dx, d_F_d2err, d_F_d2err_dx);
     for (int b0 = 0; b0 < nbatch; b0 += p->max_batch) {
         const int nb = std::min(p->max_batch, nbatch - b0);
         int rc = enqueue_call(p, nb, d_x + (size_t)b0 * p->P.nx, d_F + b0, d_F_dx + (size_t)b0 * p->P.nx,

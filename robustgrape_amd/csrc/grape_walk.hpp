@@ -692,14 +692,21 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #define GRAPE_WALK_G4_XLDS 1
 #endif
 #ifndef GRAPE_WALK_I21_WAVES  // k_walk_img occupancy: one 2-level sector per lane ...
-#define GRAPE_WALK_I21_WAVES 3
+#define GRAPE_WALK_I21_WAVES 2
 #endif
 #ifndef GRAPE_WALK_I22_WAVES  // ... or two
 #define GRAPE_WALK_I22_WAVES 2
 #endif
 #ifndef GRAPE_WALK_IMG2_NS1  // the 2-level image walks (error sources) with one sector per lane
-#define GRAPE_WALK_IMG2_NS1 0
+#define GRAPE_WALK_IMG2_NS1 1
 #endif
+#ifndef GRAPE_WALK_FDX_IN_ERR  // F_dx traces in k_walk_err_grad (k_walk_img_sum: W chunk sums only)
+#define GRAPE_WALK_FDX_IN_ERR 1
+#endif
+#ifndef GRAPE_WALK_IMG_WSUM  // ... and those sums in the 2-level image walk itself (LDS accumulators)
+#define GRAPE_WALK_IMG_WSUM 1
+#endif
+constexpr int kWsumMaxE = 4;  // error sources whose W chunk sums the 2-level image walk accumulates
 #ifndef GRAPE_WALK_IMG_LDS
 #define GRAPE_WALK_IMG_LDS 1
 #endif
@@ -740,6 +747,9 @@ struct WalkCfg {
     static constexpr int WAVES_GRAD_STORED = D <= 2 ? (NS == 1 ? 3 : 2) : D == 3 ? GRAPE_WALK_G3S_WAVES : GRAPE_WALK_G4S_WAVES;
     static constexpr int WAVES_IMG = D <= 2 ? (NS == 1 ? GRAPE_WALK_I21_WAVES : GRAPE_WALK_I22_WAVES) : 1;  // k_walk_img
     static constexpr bool IMG_LDS = D >= 4 && GRAPE_WALK_IMG_LDS;      // k_walk_img: eps2 propagators in LDS
+    // k_walk_img sums W_e over the chunk in LDS (kWalkBlock x kWsumMaxE x D^2 entries: 64 KB at D = 2)
+    // and k_walk_img_sum is not launched (ne <= kWsumMaxE)
+    static constexpr bool IMG_WSUM = D == 2 && NS == 1 && GRAPE_WALK_IMG_WSUM && GRAPE_WALK_FDX_IN_ERR;
     // the diagonal shift + Taylor 9 (sm_regime) for the 4-level class only: it pays where the
     // Taylor-12 columns dominate; the smaller classes (Taylor 6 at C2) measured slower with its
     // bookkeeping (k_walk_fwd<2,2> 0.295 -> 0.34 ms per pass) and keep the unshifted walk bitwise
@@ -1191,6 +1201,15 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     double mu[NS];  // this step's diagonal shifts (every variant takes the nominal's)
     constexpr bool EL = C::IMG_LDS;
     MStore<D, EL> Ed2[NS], Ee2[NS];
+    // W chunk sums in LDS (IMG_WSUM): entry (e, t) of this lane at wacc[(e * TS + t) * kWalkBlock]
+    const bool ws = C::IMG_WSUM && P.ne <= kWsumMaxE;
+    cd *wacc = nullptr;
+    if constexpr (C::IMG_WSUM) {
+        __shared__ cd lds_w[kWalkBlock * kWsumMaxE * TS];
+        wacc = lds_w + threadIdx.x;
+#pragma unroll
+        for (int t = 0; t < kWsumMaxE * TS; ++t) wacc[t * kWalkBlock] = czero();
+    }
     if constexpr (EL) {
         static_assert(NS == 1, "one pair of LDS slots per lane");
         __shared__ cd lds_d2[kWalkBlock * MStore<D, true>::kStride], lds_e2[kWalkBlock * MStore<D, true>::kStride];
@@ -1278,6 +1297,12 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 #pragma unroll
                             for (int m = 0; m < D; ++m) cmac(c, cconj(Q[w][m][r]), t[m]);
                             dst[(size_t)(r * D + cc) * lanes] = c;
+                            if constexpr (C::IMG_WSUM && KIND == IMG_DIFF) {  // W_e: the chunk sum, in step order
+                                if (ws && act && slot >= P.nvg) {
+                                    cd &a = wacc[((slot - P.nvg) * TS + r * D + cc) * kWalkBlock];
+                                    a = cadd(a, c);
+                                }
+                            }
                         }
                     }
                 }
@@ -1320,6 +1345,17 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
             }
         }
     }
+    if constexpr (C::IMG_WSUM) {
+        if (ws && L.ok) {  // B.Wc [sub-evaluation][ne][nchunks][D][D] (k_walk_img_sum's layout and sums)
+            const size_t sub = (size_t)L.be * ns + L.w0;
+#pragma unroll 1
+            for (int e = 0; e < P.ne; ++e) {
+                cd *dst = B.Wc + ((sub * P.ne + e) * P.nchunks + L.c) * TS;
+#pragma unroll
+                for (int t = 0; t < TS; ++t) dst[t] = wacc[(e * TS + t) * kWalkBlock];
+            }
+        }
+    }
     if (L.ok) {
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
@@ -1343,10 +1379,8 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 // error images sum_{k in c} W_{e,k} to B.Wc ([sub-evaluation][ne][nchunks][D][D], row-major tiles:
 // Phase A of k_err_scan, UnitaryCalculations.jl:112).  One read of Z1 and of every W per step.
 // GRAPE_WALK_FDX_IN_ERR (default): the F_dx traces are taken by k_walk_err_grad's e = 0 lanes, which
-// read Z1 anyway, so this kernel reads only the W images (C3: 5 -> 4 of the 9 tiles per step).
-#ifndef GRAPE_WALK_FDX_IN_ERR
-#define GRAPE_WALK_FDX_IN_ERR 1
-#endif
+// read Z1 anyway, so this kernel reads only the W images (C3: 5 -> 4 of the 9 tiles per step), and
+// not at all for the 2-level classes whose image walk sums W itself (WalkCfg::IMG_WSUM).
 template <int D, int NS>
 __global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, DevBatch B) {
     constexpr int TS = D * D;

@@ -17,7 +17,9 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
         if (stage == 0) {
             hipLaunchKernelGGL((grape::k_walk_img<D, NS>), grid, blk, 0, st, P, B);
         } else if (stage == 1) {  // F_dx traces of Z1 and the chunk sums of W (k_err_scan's Phase A)
-            hipLaunchKernelGGL((grape::k_walk_img_sum<D, NS>), grid, blk, 0, st, P, B);
+            // (the 2-level image walk summed W itself: WalkCfg::IMG_WSUM)
+            if (!(grape::WalkCfg<D, NS>::IMG_WSUM && P.ne <= grape::kWsumMaxE))
+                hipLaunchKernelGGL((grape::k_walk_img_sum<D, NS>), grid, blk, 0, st, P, B);
         } else {  // the F_d2err_dx walks, one lane per (chunk, evaluation, error)
             const dim3 grid_e((unsigned)((lanes * P.ne + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
             hipLaunchKernelGGL((grape::k_walk_err_grad<D, NS>), grid_e, blk, 0, st, P, B);

@@ -136,6 +136,47 @@ def test_dense_rejects_what_it_does_not_serve():
         GrapePlan(fp.replace(unitary_problem=bad), nparam=2)
 
 
+def _xadd_h0_problem(d, ntimes):
+    """The C5 family with two additional parameters: x_add[0] a phase on the target's first column
+    (as dense_error_problem(phase=True)), x_add[1] a global detuning of H0 (a Hermitian Ginibre
+    operator times x_add[1]) and x_add[0] also modulating it (cos), so that every step's exponential
+    depends on x_add (UnitaryCalculations.jl:57-64)."""
+    from robustgrape_amd.operators import FN_COS, FN_LINEAR, VAR_XADD, OperatorBasisHamiltonian, Term
+    base = S.dense_error_problem(d, ntimes, nerr=0, phase=True)
+    up = base.unitary_problem
+    Hx = S._hermitian(d, 70)
+    H0 = OperatorBasisHamiltonian(list(up.H0.terms) + [Term(Hx, var=VAR_XADD, index=1, func=FN_LINEAR, scale=0.4),
+                                                        Term(Hx, var=VAR_XADD, index=0, func=FN_COS, scale=0.2)])
+    return base.replace(unitary_problem=up.replace(H0=H0, nb_additional_param=2))
+
+
+@pytest.mark.parametrize("d,ntimes", [(13, 1), (16, 7), (40, 9), (64, 5)])
+def test_dense_xadd_dependent_h0_matches_live_oracle(d, ntimes):
+    """H0 reading x_add above 12 levels (round 4): k_dgrad adds each step's x_add variant and k_dadd
+    sums them onto the target's part of F_dx_add, against the oracle (FidelityCalculations.jl:67-76)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = _xadd_h0_problem(d, ntimes)
+    x = np.concatenate([S.dense_x(ntimes, seed=500 + ntimes), [0.7, -0.3]])
+    ref = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, _, _ = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, ref[0], ref[1])
+    assert g.shape == (len(x),) and abs(g[-1]) > 1e-6  # the H0 part of F_dx_add is not empty
+
+
+def test_dense_xadd_h0_batch_equals_single():
+    from robustgrape_amd.engine import GrapePlan
+    fp = _xadd_h0_problem(24, 6)
+    X = np.stack([np.concatenate([S.dense_x(6, seed=s), [0.3 * s, -0.1 * s]]) for s in range(4)])
+    plan = GrapePlan(fp, nparam=2, max_batch=4)
+    F, Fdx, _, _ = plan.fidelity_grad(X)
+    plan.close()
+    one = GrapePlan(fp, nparam=2, max_batch=1)
+    F1, Fdx1, _, _ = one.fidelity_grad(X)
+    one.close()
+    assert np.array_equal(F, F1) and np.array_equal(Fdx, Fdx1)
+
+
 # ---------------------------------------------------------------- error sources (d > 12)
 T3, T3_ABS = 1e-5, 1e-7
 

@@ -1,13 +1,12 @@
-"""Small device-pointer calls through captured graphs (grape_fidelity_grad_device_async, the
-optimiser's line-search rounds; csrc/grape_engine.hip fidelity_grad_dgraph).
+"""Device-pointer calls (grape_fidelity_grad_device_async, the optimiser's line-search rounds) against
+the host-array entry on the same plan (grape_fidelity_grad: captured graphs for <= 64 evaluations,
+the stream path above), bitwise: fresh output tensors per call, row counts through and past the
+graph limit, error sources (F_d2err, F_d2err_dx).  And the optimiser's cost (RobustCost) on a few
+rows equals the same rows inside a large call, bitwise, through the fused cost and the torch cost.
 
-Calls of <= 64 evaluations are replayed from one graph per batch bucket (powers of two): a copy-in
-kernel stages the caller's rows (the bucket's extra rows repeat the last one), the pipeline runs on
-the staging rows, a copy-out kernel writes the caller's outputs, and the two copy kernels' pointer
-arguments are set per replay.  Every output must be bitwise the stream path's (GRAPE_OPT_NO_GRAPH):
-rows are independent and the chunking is the plan's, so neither the bucket padding nor the graph
-changes any arithmetic.  Also: fresh output tensors per call (the pointer update), buckets reused
-with other row counts, large (stream-path) calls in between, error sources (F_d2err, F_d2err_dx)."""
+(Round 4 also replayed small device-pointer calls from captured graphs; it measured no faster than
+the stream path -- 0.104 vs 0.100 ms for one row, scripts/probes/cost_call_latency.py -- and was
+removed.)"""
 import numpy as np
 import pytest
 
@@ -51,24 +50,23 @@ CASES = [
 
 
 @pytest.mark.parametrize("name,mk,ne,sizes", CASES)
-def test_device_graph_calls_are_the_stream_path(name, mk, ne, sizes):
+def test_device_calls_are_the_host_calls(name, mk, ne, sizes):
     from robustgrape_amd.engine import GrapePlan
-    from robustgrape_amd.operators import OPT_NO_GRAPH
     fp = mk()
     nt = fp.unitary_problem.ntimes
     X = np.stack([P.random_x(nt, 300 + s) for s in range(128)])
     plan = GrapePlan(fp, nparam=1, device=0, max_batch=128)
-    ref = GrapePlan(fp, nparam=1, device=0, max_batch=128, options=OPT_NO_GRAPH)
     try:
         for i, nb in enumerate(sizes):
             rows = X[(5 * i) % 20:(5 * i) % 20 + nb]
-            got, want = _call(plan, rows, ne), _call(ref, rows, ne)
+            got = _call(plan, rows, ne)
+            F, Fdx, Fd2, Fd2dx = plan.fidelity_grad(rows)
+            want = [F, Fdx] + ([Fd2, np.ascontiguousarray(Fd2dx.transpose(0, 2, 1))] if ne else [])
             for g, w in zip(got, want):
                 assert np.all(np.isfinite(g)), (name, nb)
                 assert np.array_equal(g, w), (name, nb, float(np.max(np.abs(g - w))))
     finally:
         plan.close()
-        ref.close()
 
 
 @pytest.mark.parametrize("fused", [True, False])
