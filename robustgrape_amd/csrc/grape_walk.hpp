@@ -692,19 +692,22 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #define GRAPE_WALK_G4_XLDS 1
 #endif
 #ifndef GRAPE_WALK_I21_WAVES  // k_walk_img occupancy: one 2-level sector per lane ...
-#define GRAPE_WALK_I21_WAVES 2
+#define GRAPE_WALK_I21_WAVES 3
 #endif
 #ifndef GRAPE_WALK_I22_WAVES  // ... or two
 #define GRAPE_WALK_I22_WAVES 2
 #endif
 #ifndef GRAPE_WALK_IMG2_NS1  // the 2-level image walks (error sources) with one sector per lane
-#define GRAPE_WALK_IMG2_NS1 1
+#define GRAPE_WALK_IMG2_NS1 0
 #endif
 #ifndef GRAPE_WALK_FDX_IN_ERR  // F_dx traces in k_walk_err_grad (k_walk_img_sum: W chunk sums only)
 #define GRAPE_WALK_FDX_IN_ERR 1
 #endif
-#ifndef GRAPE_WALK_IMG_WSUM  // ... and those sums in the 2-level image walk itself (LDS accumulators)
-#define GRAPE_WALK_IMG_WSUM 1
+// ... and those sums in the 2-level image walk itself (LDS accumulators; needs GRAPE_WALK_IMG2_NS1).
+// Off: measured slower, C3 580 k -> 569-570 k evals/s (k_walk_img +1.55 ms, k_walk_img_sum -1.0 ms
+// per bench step, A/B in one GPU call)
+#ifndef GRAPE_WALK_IMG_WSUM
+#define GRAPE_WALK_IMG_WSUM 0
 #endif
 constexpr int kWsumMaxE = 4;  // error sources whose W chunk sums the 2-level image walk accumulates
 #ifndef GRAPE_WALK_IMG_LDS

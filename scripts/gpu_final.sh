@@ -17,9 +17,11 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/${TAG}_smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/${TAG}_smoke.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python bench.py > $OUT/${TAG}_bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; faulted $OUT/${TAG}_bench.log && { echo FAULT; exit 99; }; [ $rc -ne 0 ] && exit $rc
-grep '^{' $OUT/${TAG}_bench.log | tail -1 | cut -c1-300
+if [ -z "${SKIP_BENCH:-}" ]; then
+  timeout -k 10 600 python bench.py > $OUT/${TAG}_bench.log 2>&1
+  rc=$?; echo "bench rc=$rc"; faulted $OUT/${TAG}_bench.log && { echo FAULT; exit 99; }; [ $rc -ne 0 ] && exit $rc
+  grep '^{' $OUT/${TAG}_bench.log | tail -1 | cut -c1-300
+fi
 if [ -z "${SKIP_PROFILE:-}" ]; then
   BATCH=32768 bash scripts/gpu_profile.sh ${TAG}_c2 || exit $?
 fi
