@@ -726,7 +726,7 @@ def c2_closure(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
                     help="restarts per GPU per step; default 262144 (c2), 16384 (c3), 16 (c5)")
@@ -789,10 +789,10 @@ def main():
     else:
         fp, nparam, d, nt, inputs = problem(), 1, D, NT, restart_inputs
     ne = len(fp.unitary_problem.error_sources)
-    # One step = B restarts per GPU, evaluated in device passes of `chunk` (measured C2 passes on
-    # sectors: 8 192 -> 2.64M, 16 384 -> 2.65M, 32 768 -> 2.70M, 65 536 -> 2.71M evals/s;
-    # DESIGN.md 9).  B is sized so that 20 steps last about 2 s (the driver's GPU-busy sampler
-    # must see them).
+    # One step = B restarts per GPU, evaluated in device passes of `chunk` (C2 passes of 16 384 /
+    # 32 768 / 65 536 / 131 072 measured 8.12 / 8.11 / 7.76 / 7.98 M evals/s in round 3, DESIGN.md
+    # 10).  B is sized so that the default steps last long enough for the driver's GPU-busy
+    # sampler to see them.
     B = args.batch or (16 if c5 else 16384 if c3 else 262144)
     chunk = args.chunk or (16 if c5 else 8192 if c3 else 32768)
     first, count = shard(B * world, world, rank)  # weak scaling: B restarts per GPU
