@@ -60,16 +60,6 @@ constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScan
 #define GRAPE_FORK_MAX_BATCH 4096
 #endif
 constexpr int kForkMaxBatch = GRAPE_FORK_MAX_BATCH;
-// Small calls captured into HIP graphs fork too (the fork becomes a graph branch): C3 single
-// evaluation 0.631 -> 0.548 ms; C2 single calls take the pair kernels (no fork) and are unchanged.
-// GRAPE_GRAPH_FORK=0 captures one stream (round 3's workaround, see capturing).
-static bool graph_fork() {
-    static const bool on = [] {
-        const char *e = std::getenv("GRAPE_GRAPH_FORK");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
@@ -204,7 +194,7 @@ struct grape_plan {
     bool capturing = false;  // graph_capture in progress (round 3 disabled the fork while capturing after
                              // intermittent runtime crashes on replays; round 4's probes and a 10 000-call
                              // bitwise stress could not reproduce them, so the fork is captured again
-                             // unless GRAPE_GRAPH_FORK=0: scripts/probes/graph_fork_stress.py)
+                             // unless GRAPE_OPT_NO_GRAPH_FORK: scripts/probes/graph_fork_stress.py)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -261,6 +251,11 @@ struct grape_plan {
         return e;
     }
 };
+
+// Small calls captured into HIP graphs fork too (the fork becomes a graph branch): C3 single
+// evaluation 0.631 -> 0.548 ms; C2 single calls take the pair kernels (no fork) and are unchanged.
+// GRAPE_OPT_NO_GRAPH_FORK captures one stream (round 3's workaround, see grape_plan::capturing).
+static bool graph_fork(const grape_plan *p) { return !(p->P.opts & GRAPE_OPT_NO_GRAPH_FORK); }
 
 static void free_plan(grape_plan *p) {
     if (!p) return;
@@ -1426,7 +1421,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         // Small calls (latency-bound: the optimiser's line-search rounds, single evaluations) run
         // the second sector class on the auxiliary stream beside the first; large ones keep one
         // stream (no gain there, DESIGN 4.1, and per-kernel event times stay per kernel).
-        const bool fork = p->aux_stream && (!p->capturing || graph_fork()) && nb <= kForkMaxBatch &&
+        const bool fork = p->aux_stream && (!p->capturing || graph_fork(p)) && nb <= kForkMaxBatch &&
                           !(p->P.opts & GRAPE_OPT_NO_FORK);
         // Latency-bound calls of the Rydberg layout: both classes' walks (and scans) in ONE launch per
         // stage (grape_walk_api.hpp launch_pair) -- neither a graph branch nor a second stream overlaps

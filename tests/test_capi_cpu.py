@@ -210,3 +210,16 @@ def test_closure_tables_detect_non_hermitian_h0():
     ok = fp.replace(unitary_problem=up.replace(error_sources=[ErrorSource(lambda t, p, xa, e: -0.5j * e * decay)]))
     H, _ = host_tables(ok, x[None, :], 1)
     assert np.isfinite(H).all() and is_hermitian_h0(H[:, :, 0])
+
+
+def test_plan_option_constants_match_the_header():
+    """Every GRAPE_OPT_* of include/grape.h has its operators.OPT_* twin with the same value."""
+    import os
+    import re
+
+    from robustgrape_amd import operators as OPS
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "grape.h")).read()
+    defs = dict((m.group(1), int(m.group(2))) for m in re.finditer(r"#define GRAPE_OPT_(\w+) (\d+)", hdr))
+    assert len(defs) >= 12
+    for name, val in defs.items():
+        assert getattr(OPS, "OPT_" + name) == val, name
