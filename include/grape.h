@@ -188,9 +188,9 @@ typedef struct grape_desc {
  * identical (the Rydberg sectors {01, 0r} and {10, r0} at equal Rabi frequencies and detunings)
  * share one exponential per step; this option computes each sector's own. */
 #define GRAPE_OPT_NO_TWIN 2048
-/* Small calls captured into HIP graphs run both sector classes on one stream (no fork/join branch;
-   round 3's workaround for runtime crashes that round 4 could not reproduce). */
-#define GRAPE_OPT_NO_GRAPH_FORK 4096
+/* Small calls captured into HIP graphs also fork the second sector class onto the auxiliary stream
+   (a graph branch).  Experimental, off by default: it crashed the host process. */
+#define GRAPE_OPT_GRAPH_FORK 4096
 
 typedef struct grape_plan grape_plan;
 

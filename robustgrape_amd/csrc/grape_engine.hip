@@ -191,10 +191,8 @@ struct grape_plan {
     // first (fork / join events; the classes are independent until the sector heads)
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool capturing = false;  // graph_capture in progress (round 3 disabled the fork while capturing after
-                             // intermittent runtime crashes on replays; round 4's probes and a 10 000-call
-                             // bitwise stress could not reproduce them, so the fork is captured again
-                             // unless GRAPE_OPT_NO_GRAPH_FORK: scripts/probes/graph_fork_stress.py)
+    bool capturing = false;  // graph_capture in progress: no fork unless GRAPE_OPT_GRAPH_FORK (captured
+                             // forks crashed the host process in rounds 3 and 4)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -252,10 +250,11 @@ struct grape_plan {
     }
 };
 
-// Small calls captured into HIP graphs fork too (the fork becomes a graph branch): C3 single
-// evaluation 0.631 -> 0.548 ms; C2 single calls take the pair kernels (no fork) and are unchanged.
-// GRAPE_OPT_NO_GRAPH_FORK captures one stream (round 3's workaround, see grape_plan::capturing).
-static bool graph_fork(const grape_plan *p) { return !(p->P.opts & GRAPE_OPT_NO_GRAPH_FORK); }
+// GRAPE_OPT_GRAPH_FORK: small calls captured into HIP graphs fork too (the fork becomes a graph
+// branch; C3 single evaluation 0.631 -> 0.548 ms).  Off by default: with it, the host process
+// segfaulted inside grape_fidelity_grad on tests/test_gpu_xadd_err.py
+// test_xadd_with_errors_batch_is_bitwise_the_single_calls (round 4).
+static bool graph_fork(const grape_plan *p) { return (p->P.opts & GRAPE_OPT_GRAPH_FORK) != 0; }
 
 static void free_plan(grape_plan *p) {
     if (!p) return;
@@ -1405,7 +1404,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.Ew = sb.Ew;
             B.xT = nb == 1 ? d_x : p->d_xT;  // one evaluation: x[q] is already [nx][1]
             sp.part[cl] = sb.part;
-            sp.nsec[cl] = p->Ps[cl].nsec;
+            sp.nsec[cl] = p->Ps[cl].walk ? grape_walk::grad_parts(p->Ps[cl]) : p->Ps[cl].nsec;
             sp.lane_major[cl] = p->Ps[cl].walk;  // k_walk_grad's / k_walk_img_sum's layout
             sp.part_err[cl] = sb.part_err;
             sp.lane_major_err[cl] = p->Ps[cl].walk;  // k_walk_err_grad's layout

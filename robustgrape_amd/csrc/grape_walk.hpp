@@ -709,7 +709,14 @@ __device__ __forceinline__ WalkLane walk_lane(const DevProblem &P, const DevBatc
 #ifndef GRAPE_WALK_IMG_WSUM
 #define GRAPE_WALK_IMG_WSUM 0
 #endif
-constexpr int kWsumMaxE = 4;  // error sources whose W chunk sums the 2-level image walk accumulates
+constexpr int kWsumMaxE = 4;
+// k_walk_grad with several sectors per lane (the 2-level classes without error sources) writes ONE
+// F_dx part per lane row -- its sectors' terms summed in sector order -- so k_sec_reduce reads
+// nsec / NS parts for that class (grape_walk_api.hpp walk_parts)
+#ifndef GRAPE_WALK_PRESUM
+#define GRAPE_WALK_PRESUM 1
+#endif
+constexpr bool kWalkPresum = GRAPE_WALK_PRESUM;  // error sources whose W chunk sums the 2-level image walk accumulates
 #ifndef GRAPE_WALK_IMG_LDS
 #define GRAPE_WALK_IMG_LDS 1
 #endif
@@ -1032,6 +1039,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
         for (int u = 0; u < (NVG > 0 ? NVG : P.nvg); ++u) {
             SM<D> Ap[NE];
             walk_build<D, NE>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
+            double tot = 0.0;  // (kWalkPresum: the lane's sectors summed, in sector order)
 #pragma unroll
             for (int we = 0; we < NE; ++we) {
                 double s[NSH];
@@ -1068,11 +1076,20 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
                 for (int t = 0; t < NSH; ++t) {
                     const int w = we * NSH + t;
-                    // unconditional store (inactive lanes write the sink): exact vmcnt accounting
-                    double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
-                                      : reinterpret_cast<double *>(B.sink);
-                    *dst = s[t];
+                    if constexpr (kWalkPresum && NS > 1) {
+                        tot += s[t];
+                    } else {
+                        // unconditional store (inactive lanes write the sink): exact vmcnt accounting
+                        double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
+                                          : reinterpret_cast<double *>(B.sink);
+                        *dst = s[t];
+                    }
                 }
+            }
+            if constexpr (kWalkPresum && NS > 1) {  // one part per lane row: index w0 / NS
+                double *dst = act ? B.sec_part + ((((size_t)(L.w0 / NS) * P.Nt) + k) * P.nvg + u) * L.nbe + L.be
+                                  : reinterpret_cast<double *>(B.sink);
+                *dst = tot;
             }
         }
         // X <- E Y, in place column by column

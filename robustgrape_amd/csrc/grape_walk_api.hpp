@@ -34,6 +34,9 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
 bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1);
 hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevBatch &B0, const grape::DevProblem &P1,
                        const grape::DevBatch &B1, hipStream_t st);
+// F_dx parts the class's gradient stage writes per evaluation: its sectors, or (k_walk_grad with several
+// sectors per lane, no error sources) one pre-summed part per lane row (grape_walk.hpp kWalkPresum)
+int grad_parts(const grape::DevProblem &P);
 // the walks' controls: x [nb][nx] -> xT [nx][nb] (B.xT), once per launch for every walk class
 hipError_t transpose_x(const double *x, double *xT, int nb, int nx, hipStream_t st);
 }  // namespace grape_walk

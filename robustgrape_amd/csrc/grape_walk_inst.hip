@@ -75,6 +75,13 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
     return hipGetLastError();
 }
 
+int grad_parts(const grape::DevProblem &P) {
+    const int ns = P.nsec > 1 ? P.nsec : 1;
+    if (!grape::kWalkPresum || P.ne > 0 || P.D != 2) return ns;
+    if (ns == 2 || ns == 3) return 1;  // launch<2>: both (all three) sectors in one lane
+    return ns;
+}
+
 // class 0: one sector of 4 levels with stored propagators (permutation sectors of the Rydberg model)
 // or of 3 levels (its symmetry-adapted sectors, grape_symmetry.hpp); class 1: two 2-level sectors
 bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1) {
