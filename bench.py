@@ -111,6 +111,32 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY, dims=None):
     return sum(rows) if rows else None
 
 
+PMC_MIX = os.path.join(ROOT, "profiles", "pmc_mix_latest.json")
+
+
+def pmc_executed_flop(kernel, batch, dims, path=PMC_MIX):
+    """Executed FP64 FLOP per device pass of `kernel` (all its instantiations of the sector
+    dimensions `dims`) from the committed instruction-mix summary recorded at this pass size, or None."""
+    try:
+        with open(path) as fh:
+            js = json.load(fh)
+        ks = js["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    if js.get("batch") != batch:
+        return None
+    tot = 0.0
+    for name, row in ks.items():
+        base = name.split("<")[0].split("::")[-1]
+        try:
+            dim = int(name.split("<")[1].split(",")[0].split(">")[0])
+        except (IndexError, ValueError):
+            dim = None
+        if base == kernel and dim in dims and "fp64_flop_per_dispatch" in row:
+            tot += row["fp64_flop_per_dispatch"]
+    return tot or None
+
+
 def pmc_pipeline(batch, per_pass_kernel, dims, path=PMC_SUMMARY):
     """PMC HBM bytes of one whole device pass: every kernel's mean bytes per dispatch times its
     dispatches per pass (dispatch count over that of `per_pass_kernel`, which runs once per pass
@@ -353,6 +379,14 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                  "fp64": {"achieved_TFLOPs": fp, "frac": fp_frac},
                  "hbm": {"achieved_GBs": hb, "frac": hb_frac,
                          "traffic_GBs": (traffic / (ms * 1e-3) / 1e9) if traffic else None}})
+    ex = pmc_executed_flop(kname, L, dims)
+    if ex is not None:  # what the VALU actually issued (PMC), beside the algorithmic credit above
+        roof["fp64_executed"] = {"TFLOPs": ex / (ms * 1e-3) / 1e12, "frac": ex / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                                 "flop_per_launch": ex,
+                                 "note": "64 x (2 FMA + MUL + ADD) F64 VALU instructions per dispatch "
+                                         "(profiles/pmc_mix_latest.json, scripts/pmc_mix.py) over this run's "
+                                         "kernel time; the walks' Taylor polynomials issue more FLOP than "
+                                         "SURVEY 8d's Pade-5 credit"}
     pipe = pmc_pipeline(L, grad_name, dims)
     if pipe is not None:
         total_ms = sum(per_pass.values())
