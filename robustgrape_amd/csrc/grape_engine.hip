@@ -1402,7 +1402,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.Tc = sb.Tc;  // chunk walks (null otherwise)
             B.wscr = sb.wscr;
             B.Ew = sb.Ew;
-            B.xT = nb == 1 ? d_x : p->d_xT;  // one evaluation: x[q] is already [nx][1]
+            B.xT = (nb == 1 || grape::kWalkXRow) ? d_x : p->d_xT;  // one evaluation: x[q] is already [nx][1]
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].walk ? grape_walk::grad_parts(p->Ps[cl]) : p->Ps[cl].nsec;
             sp.lane_major[cl] = p->Ps[cl].walk;  // k_walk_grad's / k_walk_img_sum's layout
@@ -1412,7 +1412,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         bool parks = false;  // the chunk walks never park a step for k_expm_high: no counters to clear
         for (int cl = 0; cl < p->ncls; ++cl) parks = parks || !p->Ps[cl].walk;
         if (parks) HIPCHECK(hipMemsetAsync(p->d_ctrl + 4, 0, 4 * sizeof(int), st));
-        if (p->d_xT && nb > 1) {  // the walks read the controls transposed (one coalesced row per step)
+        if (p->d_xT && nb > 1 && !grape::kWalkXRow) {  // the walks read the controls transposed (one coalesced row per step)
             mk(GRAPE_KERNEL_WALK_FWD, 0);
             HIPCHECK(grape_walk::transpose_x(d_x, p->d_xT, nb, p->P.nx, st));
             mk(GRAPE_KERNEL_WALK_FWD, 1);

@@ -716,7 +716,8 @@ constexpr int kWsumMaxE = 4;
 #ifndef GRAPE_WALK_PRESUM
 #define GRAPE_WALK_PRESUM 1
 #endif
-constexpr bool kWalkPresum = GRAPE_WALK_PRESUM;  // error sources whose W chunk sums the 2-level image walk accumulates
+constexpr bool kWalkPresum = GRAPE_WALK_PRESUM;
+  // error sources whose W chunk sums the 2-level image walk accumulates
 #ifndef GRAPE_WALK_IMG_LDS
 #define GRAPE_WALK_IMG_LDS 1
 #endif
@@ -805,7 +806,8 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
+    const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);  // x[q] of this evaluation at xt[q * xs]
+    const int xs = kWalkXRow ? 1 : L.nbe;
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
     cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
     Pert none;
@@ -819,9 +821,9 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         E.p = MStore<D, true>::slot(lds);
     }
     WalkX X;
-    walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));  // x_add
+    walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * xs, xs));  // x_add
     const int k0 = L.c * P.L;
-    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
+    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * xs, xs);
     cd Q[NE][D][D];
     WalkPhase ph[NE];
 #pragma unroll
@@ -837,7 +839,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = k0 + jj < P.Nt;
         walk_set_xk(X, xn);
-        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
+        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * xs, xs);  // next step's controls
         SM<D> A[NE];
         walk_build<D, NE>(P, ops, X, k + 1, none, A);
 #pragma unroll
@@ -914,7 +916,8 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
+    const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);  // x[q] of this evaluation at xt[q * xs]
+    const int xs = kWalkXRow ? 1 : L.nbe;
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
     cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
     Pert none;
@@ -973,16 +976,16 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
         }
     }
     WalkX XV;
-    walk_set_xa(XV, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));
+    walk_set_xa(XV, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * xs, xs));
     const int k0 = L.c * P.L;
-    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
+    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * xs, xs);
     const cptr<VSpec> vs = as_constant(P.vs);
 #pragma unroll 1
     for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store nothing
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = L.ok && k0 + jj < P.Nt;
         walk_set_xk(XV, xn);
-        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
+        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * xs, xs);  // next step's controls
         if constexpr (STORED) {  // this step's propagators; the next step's loads go out now
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
@@ -1202,7 +1205,8 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     const WalkLane L = walk_lane<NS>(P, B, vb);
     const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
     const int ns = P.nsec > 1 ? P.nsec : 1;
-    const double *xt = B.xT + L.be;  // x[q] of this evaluation at xt[q * nbe]
+    const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);  // x[q] of this evaluation at xt[q * xs]
+    const int xs = kWalkXRow ? 1 : L.nbe;
     const cptr<cd> ops = as_constant(P.ops) + (size_t)L.w0 * P.sec_ops;
     const cptr<VSpec> vs = as_constant(P.vs);
     cd *scr = B.wscr + (size_t)L.slot * NS * 2 * TS;
@@ -1211,9 +1215,9 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
     none.index = 0;
     none.delta = 0.0;
     WalkX X;
-    walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * L.nbe, L.nbe));  // x_add
+    walk_set_xa(X, walk_load_x(P.na, xt + (size_t)P.np * P.Nt * xs, xs));  // x_add
     const int k0 = L.c * P.L;
-    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * L.nbe, L.nbe);
+    X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * xs, xs);
     // Q_{k-1} (chunk-local), E_k, and the step's eps2 propagators E(x + eps2), E(err_e eps2) (the
     // latter two in the lane's LDS slots at D = 4, where the registers run out)
     cd Q[NS][D][D], E[NS][D][D];
@@ -1249,7 +1253,7 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = L.ok && k0 + jj < P.Nt;
         walk_set_xk(X, xn);
-        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * L.nbe, L.nbe);  // next step's controls
+        xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * xs, xs);  // next step's controls
         {
             SM<D> A[NS];
             walk_build<D, NS>(P, ops, X, k + 1, none, A);

@@ -15,6 +15,12 @@ constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBl
 #define GRAPE_WALK_STORE_MIN_D 4
 #endif
 constexpr int kWalkStoreMinD = GRAPE_WALK_STORE_MIN_D;
+// GRAPE_WALK_XROW (A/B): the walks read the controls row-major from x itself (B.xT = x, stride 1 per
+// value, nx per evaluation) instead of the transposed copy, and the engine skips k_transpose_x
+#ifndef GRAPE_WALK_XROW
+#define GRAPE_WALK_XROW 0
+#endif
+constexpr bool kWalkXRow = GRAPE_WALK_XROW;
 }  // namespace grape
 
 namespace grape_walk {
