@@ -60,6 +60,12 @@ constexpr int kScanWide = grape_host::kScanWide, kScanNarrow = grape_host::kScan
 #define GRAPE_FORK_MAX_BATCH 4096
 #endif
 constexpr int kForkMaxBatch = GRAPE_FORK_MAX_BATCH;
+// throughput passes of the Rydberg layout: both walk classes' one-wave scans in one launch
+// (grape_launch.hpp launch_scan_pair; GRAPE_SCAN_PAIR_ALL=0 keeps one launch per class for A/B)
+#ifndef GRAPE_SCAN_PAIR_ALL
+#define GRAPE_SCAN_PAIR_ALL 1
+#endif
+constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
@@ -1443,6 +1449,23 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
                     mk(GRAPE_KERNEL_SCAN, 1);
                 }
                 return e;
+            }
+            if (s == 0 && !fork && !pair && kScanPairAll) {  // both walk classes' one-wave scans in one launch
+                const int ca = p->Ps[0].D == 2 ? 1 : 0, cb = 1 - ca;
+                const DevProblem &Pa = p->Ps[ca], &Pb = p->Ps[cb];
+                if (p->ncls == 2 && Pa.walk && Pb.walk && (Pa.D == 3 || Pa.D == 4) && Pb.D == 2 &&
+                    Pa.scan_waves == kScanTiny && Pb.scan_waves == kScanTiny) {
+                    mk(GRAPE_KERNEL_WALK_FWD, 0);
+                    hipError_t e = Pa.D == 4 ? grape_walk::launch<4>(0, Pa, Bc[ca], st) : grape_walk::launch<3>(0, Pa, Bc[ca], st);
+                    if (e == hipSuccess) e = grape_walk::launch<2>(0, Pb, Bc[cb], st);
+                    mk(GRAPE_KERNEL_WALK_FWD, 1);
+                    if (e != hipSuccess) return e;
+                    mk(GRAPE_KERNEL_SCAN, 0);
+                    e = Pa.D == 4 ? grape_host::launch_scan_pair<4, 2, kScanTiny>(Pa, Bc[ca], Pb, Bc[cb], st)
+                                  : grape_host::launch_scan_pair<3, 2, kScanTiny>(Pa, Bc[ca], Pb, Bc[cb], st);
+                    mk(GRAPE_KERNEL_SCAN, 1);
+                    return e;
+                }
             }
             if (!fork || pair) {
                 for (int cl = 0; cl < p->ncls; ++cl) {

@@ -99,22 +99,24 @@ void launch_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
         hipLaunchKernelGGL((grape::k_scan<D, kScanWide>), dim3(B.nb), dim3(64 * kScanWide), scan_lds<D>(kScanWide), st,
                            P, B);
 }
-// the latency scans of two walk classes in one launch (D0 = 4, D1 = 2: the Rydberg layout)
-template <int D0, int D1>
+// the scans of two walk classes in one launch (D0 = 4 or 3, D1 = 2: the Rydberg layout), both at
+// width W: the latency scans (16 waves), and the throughput passes' one-wave scans, where the two
+// classes' short, under-filled scans then run side by side instead of one after the other
+template <int D0, int D1, int W = kScanLatency>
 hipError_t launch_scan_pair(const DevProblem &P0, const DevBatch &B0, const DevProblem &P1, const DevBatch &B1,
                             hipStream_t st) {
-    const size_t lds = std::max(scan_lds<D0>(kScanLatency), scan_lds<D1>(kScanLatency));
+    const size_t lds = std::max(scan_lds<D0>(W), scan_lds<D1>(W));
     static unsigned long long limit_set = 0;  // per device (idempotent: a race only repeats the call)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev >= 64) return hipErrorInvalidDevice;
     if (!((limit_set >> dev) & 1ull)) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan_pair<D0, D1, kScanLatency>),
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan_pair<D0, D1, W>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         limit_set |= 1ull << dev;
     }
-    hipLaunchKernelGGL((grape::k_scan_pair<D0, D1, kScanLatency>), dim3((unsigned)(B0.nb + B1.nb)),
-                       dim3(64 * kScanLatency), lds, st, P0, B0, P1, B1);
+    hipLaunchKernelGGL((grape::k_scan_pair<D0, D1, W>), dim3((unsigned)(B0.nb + B1.nb)), dim3(64 * W), lds, st, P0,
+                       B0, P1, B1);
     return hipGetLastError();
 }
 template <int D>
