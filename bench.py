@@ -684,6 +684,7 @@ def c4opt(args):
     dev = torch.device("cuda", 0)
     opts = OPT._solver_options(params)
     opts.update(g_tol=0.0)  # no early stop: every restart iterates through the timed region
+    opts["asynchronous"] = not args.sync_rows
     res = OPT.lbfgs_batched(cost, torch.as_tensor(X0, device=dev), **dict(opts, iterations=args.warmup))
     torch.cuda.synchronize()
     calls0 = int(res.f_calls.sum())
@@ -777,6 +778,8 @@ def main():
                     help="c4opt: the plan's scan width (chunking); 0 = by batch size, default: RobustCost's choice")
     ap.add_argument("--plan-options", type=int, default=0,
                     help="GRAPE_OPT_* flags of the timed plan (A/B runs; c2/c3/c5 device legs and c4opt)")
+    ap.add_argument("--sync-rows", action="store_true",
+                    help="c4opt: the synchronous optimiser loop (rows wait for each other every iteration)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-paths", action="store_true",
                     help="skip the host-array (PCIe-inclusive) and nbatch = 1 legs")

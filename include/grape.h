@@ -321,6 +321,15 @@ int grape_lbfgs_ls_init(const grape_lbfgs_state *state, void *stream);
 int grape_lbfgs_ls_begin(const grape_lbfgs_state *state, void *stream);
 int grape_lbfgs_ls_end(const grape_lbfgs_state *state, int count, const double *ft, const double *gt, void *stream);
 int grape_lbfgs_step(const grape_lbfgs_state *state, void *stream);
+/* Asynchronous rows (round 4): instead of the per-iteration sequence above, call this at the start
+ * of every round, then grape_lbfgs_ls_begin / evaluate / grape_lbfgs_ls_end.  Every row advances on
+ * its own: a row whose line search ended (accepted, or max_rounds trial evaluations spent) takes its
+ * step (grape_lbfgs_step), then its direction and line-search start (grape_lbfgs_direction,
+ * grape_lbfgs_ls_init), so each round evaluates every searching row whatever its iteration; each
+ * row's arithmetic and order are those of the per-iteration sequence (bitwise the same trajectory).
+ * Rows start with phase = 3; rounds: int32 [R] device scratch; steepest != 0 clears the history after
+ * every step (gradient descent).  Done when ls_begin's count is 0. */
+int grape_lbfgs_async_advance(const grape_lbfgs_state *state, int steepest, int max_rounds, int *rounds, void *stream);
 
 /*
  * The optimiser's cost of R restarts in one launch (calculate_common!, FidelityCalculations.jl:

@@ -35,17 +35,13 @@ __device__ __forceinline__ double block_sum(double v, double *red) {
 }
 
 // D[r] = -H_r g[r]: H_r the L-BFGS inverse-Hessian estimate of restart r from its
-// newest hist[r] pairs (ring buffer, newest at head[r] - 1), scaled by gamma[r].
-__global__ __launch_bounds__(kThreads) void k_lbfgs_dir(int R, int n, int m, const double *__restrict__ S,
-                                                        const double *__restrict__ Y,
-                                                        const double *__restrict__ rho,
-                                                        const int64_t *__restrict__ head,
-                                                        const int64_t *__restrict__ hist,
-                                                        const double *__restrict__ gamma,
-                                                        const double *__restrict__ g, double *__restrict__ D) {
+// newest hist[r] pairs (ring buffer, newest at head[r] - 1), scaled by gamma[r].  One workgroup.
+__device__ void dir_row(int r, int R, int n, int m, const double *__restrict__ S, const double *__restrict__ Y,
+                        const double *__restrict__ rho, const int64_t *__restrict__ head,
+                        const int64_t *__restrict__ hist, const double *__restrict__ gamma,
+                        const double *__restrict__ g, double *__restrict__ D) {
     __shared__ double red[kThreads / 64];
     __shared__ double alpha[kMaxHistory];
-    const int r = blockIdx.x;  // grid == R
     const size_t row = (size_t)r * n;
     double *q = D + row;
     for (int i = threadIdx.x; i < n; i += kThreads) q[i] = -g[row + i];
@@ -70,6 +66,15 @@ __global__ __launch_bounds__(kThreads) void k_lbfgs_dir(int R, int n, int m, con
         const double c = alpha[j] - rho[(size_t)slot * R + r] * block_sum(part, red);
         for (int i = threadIdx.x; i < n; i += kThreads) q[i] += c * s[i];
     }
+}
+__global__ __launch_bounds__(kThreads) void k_lbfgs_dir(int R, int n, int m, const double *__restrict__ S,
+                                                        const double *__restrict__ Y,
+                                                        const double *__restrict__ rho,
+                                                        const int64_t *__restrict__ head,
+                                                        const int64_t *__restrict__ hist,
+                                                        const double *__restrict__ gamma,
+                                                        const double *__restrict__ g, double *__restrict__ D) {
+    dir_row(blockIdx.x, R, n, m, S, Y, rho, head, hist, gamma, g, D);  // grid == R
 }
 
 // ---------------------------------------------------------------------------
@@ -121,9 +126,8 @@ __device__ double cubic_min(double a0, double f0, double g0, double a1, double f
 
 // per row: which rows still search, the descent check (-g where D is not a descent direction)
 // and the line-search state at a = 1
-__global__ __launch_bounds__(kThreads) void k_ls_init(grape_lbfgs_state s) {
+__device__ void ls_init_row(const grape_lbfgs_state &s, int r) {
     __shared__ double red[kThreads / 64];
-    const int r = blockIdx.x;
     const size_t row = (size_t)r * s.n;
     const bool active = !(s.gconv[r] | s.fconv[r] | s.xconv[r] | s.lsfail[r]) && s.iters[r] < s.iterations &&
                         (s.f_calls_limit <= 0 || s.f_calls[r] < s.f_calls_limit);
@@ -158,6 +162,7 @@ __global__ __launch_bounds__(kThreads) void k_ls_init(grape_lbfgs_state s) {
         s.first[r] = 1;
     }
 }
+__global__ __launch_bounds__(kThreads) void k_ls_init(grape_lbfgs_state s) { ls_init_row(s, blockIdx.x); }
 
 // the rows still searching, in row order (one workgroup: an exclusive scan of per-thread counts)
 __global__ __launch_bounds__(kCompactThreads) void k_ls_compact(grape_lbfgs_state s) {
@@ -268,9 +273,8 @@ __global__ __launch_bounds__(kThreads) void k_ls_end(grape_lbfgs_state s, const 
 
 // per row after the line search: the accepted point, the ring-buffer update and Optim's
 // stopping rules (optimize.py lbfgs_batched)
-__global__ __launch_bounds__(kThreads) void k_lbfgs_step(grape_lbfgs_state s) {
+__device__ void step_row(const grape_lbfgs_state &s, int r) {
     __shared__ double red[kThreads / 64];
-    const int r = blockIdx.x;
     const size_t row = (size_t)r * s.n;
     const bool active = s.active[r] != 0;
     const bool moved = active && s.fn[r] < s.f0[r];
@@ -318,6 +322,47 @@ __global__ __launch_bounds__(kThreads) void k_lbfgs_step(grape_lbfgs_state s) {
             if (dx <= s.x_abstol || dx <= s.x_reltol * xmax) s.xconv[r] = 1;
         }
     }
+}
+__global__ __launch_bounds__(kThreads) void k_lbfgs_step(grape_lbfgs_state s) { step_row(s, blockIdx.x); }
+
+// Asynchronous rows (optimize.py _lbfgs_device, asynchronous=True): at the start of every round each
+// row advances on its own -- a row whose line search ended (accepted, or its round budget spent)
+// takes its step, its next direction and its line-search start at a = 1, so the round evaluates
+// every searching row whatever its iteration.  Rows are independent, so every row runs exactly the
+// per-row arithmetic of the synchronous loop (direction -> ls_init -> rounds -> step) in the same
+// order: bitwise the same trajectory.  phase 3 = a row that has not started its first iteration;
+// rounds[r] = trial evaluations of the current line search (the synchronous loop's round cap).
+__global__ __launch_bounds__(kThreads) void k_async_advance(grape_lbfgs_state s, int steepest, int max_rounds,
+                                                            int *rounds) {
+    __shared__ int ph_s;
+    const int r = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int ph = s.phase[r];
+        if (ph < 2 && rounds[r] >= max_rounds) ph = 2;  // the synchronous loop's MAX_LS_ROUNDS: the search ends
+        ph_s = ph;
+    }
+    __syncthreads();
+    const int ph = ph_s;
+    if (ph < 2) {  // still searching: one more trial this round
+        if (threadIdx.x == 0) rounds[r] += 1;
+        return;
+    }
+    if (ph == 2) {
+        if (!s.active[r]) return;  // finished for good
+        step_row(s, r);
+        __syncthreads();
+        if (steepest && threadIdx.x == 0) {  // GradientDescent: drop the pair just stored
+            s.hist[r] = 0;
+            s.gamma[r] = 1.0;
+        }
+        __syncthreads();
+    }
+    // phase 3 (first iteration) or after the step: direction, line-search start
+    dir_row(r, s.R, s.n, s.m, s.S, s.Y, s.rho, s.head, s.hist, s.gamma, s.g, s.D);
+    __syncthreads();
+    ls_init_row(s, r);
+    __syncthreads();
+    if (threadIdx.x == 0) rounds[r] = s.phase[r] < 2 ? 1 : 0;  // (an inactive row ends in phase 2)
 }
 
 // ---------------------------------------------------------------------------
@@ -442,6 +487,16 @@ extern "C" int grape_lbfgs_step(const grape_lbfgs_state *st, void *stream) {
     if (!st || st->R < 0 || st->n < 1 || st->m < 1) return GRAPE_ERR_INVALID;
     if (st->R == 0) return GRAPE_OK;
     hipLaunchKernelGGL(k_lbfgs_step, dim3(st->R), dim3(kThreads), 0, static_cast<hipStream_t>(stream), *st);
+    return hipGetLastError() == hipSuccess ? GRAPE_OK : GRAPE_ERR_HIP;
+}
+
+extern "C" int grape_lbfgs_async_advance(const grape_lbfgs_state *st, int steepest, int max_rounds, int *rounds,
+                                         void *stream) {
+    if (!st || st->R < 0 || st->n < 1 || st->m < 1 || st->m > kMaxHistory || !rounds || max_rounds < 1)
+        return GRAPE_ERR_INVALID;
+    if (st->R == 0) return GRAPE_OK;
+    hipLaunchKernelGGL(k_async_advance, dim3(st->R), dim3(kThreads), 0, static_cast<hipStream_t>(stream), *st,
+                       steepest, max_rounds, rounds);
     return hipGetLastError() == hipSuccess ? GRAPE_OK : GRAPE_ERR_HIP;
 }
 

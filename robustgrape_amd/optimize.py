@@ -40,6 +40,7 @@ from .types import FidelityRobustGRAPEParameters, FidelityRobustGRAPEProblem
 
 C1, C2 = 1e-4, 0.9
 MAX_LS_ROUNDS = 30
+_ASYNC_ROWS_DEFAULT = False  # device optimiser: rows advance asynchronously unless a callback is given
 MAX_PLAN_BATCH = 4096
 
 
@@ -190,10 +191,16 @@ _LS_I32 = ("phase", "first", "accepted", "gconv", "fconv", "xconv", "lsfail", "a
 
 
 def _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, time_limit, x_reltol, g_reltol,
-                  f_calls_limit, callback, steepest=False) -> BatchResult:
+                  f_calls_limit, callback, steepest=False, asynchronous=None) -> BatchResult:
     """lbfgs_batched on the GPU: the same algorithm with its per-round state machine, the descent
     check and the L-BFGS update as HIP kernels (csrc/grape_lbfgs.hip, include/grape.h
-    grape_lbfgs_state), one host sync per line-search round (the count of searching rows)."""
+    grape_lbfgs_state), one host sync per line-search round (the count of searching rows).
+
+    asynchronous (default when there is no callback): rows do not wait for each other at iteration
+    boundaries -- every round evaluates every searching row whatever its iteration
+    (grape_lbfgs_async_advance), so the few-row tail rounds of each iteration disappear; each row's
+    trajectory is bitwise the synchronous one.  The callback (Optim's, per iteration of all rows)
+    needs the synchronous loop."""
     import ctypes
 
     from . import _capi
@@ -234,6 +241,28 @@ def _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, t
     stream = lambda: ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
     timed_out = False
     stopped = callback is not None and bool(callback(t["X"], t["f"], t["g"], t["iters"]))
+    if asynchronous is None:
+        asynchronous = _ASYNC_ROWS_DEFAULT and callback is None
+    if asynchronous and not stopped:
+        rounds = torch.zeros(max(R, 1), dtype=torch.int32, device=dev)
+        t["phase"].fill_(3)  # no row has started its first iteration
+        while True:
+            if not math.isnan(time_limit) and time.perf_counter() - t_start > time_limit:
+                timed_out = True  # (one more advance: rows whose search ended take their step)
+                _capi.check(L.grape_lbfgs_async_advance(sp, int(bool(steepest)), MAX_LS_ROUNDS,
+                                                        ctypes.c_void_p(rounds.data_ptr()), stream()))
+                break
+            _capi.check(L.grape_lbfgs_async_advance(sp, int(bool(steepest)), MAX_LS_ROUNDS,
+                                                    ctypes.c_void_p(rounds.data_ptr()), stream()))
+            _capi.check(L.grape_lbfgs_ls_begin(sp, stream()))
+            cnt = int(t["count"][0].item())  # the round's one host sync
+            if cnt == 0:
+                break
+            ft, gt = fun(t["Xt"][:cnt], t["rows"][:cnt])
+            ft, gt = ft.to(dt).contiguous(), gt.to(dt).contiguous()
+            _capi.check(L.grape_lbfgs_ls_end(sp, cnt, ctypes.c_void_p(ft.data_ptr()), ctypes.c_void_p(gt.data_ptr()),
+                                             stream()))
+        stopped = True
     while not stopped:
         if not math.isnan(time_limit) and time.perf_counter() - t_start > time_limit:
             timed_out = True
@@ -271,7 +300,8 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
                   iterations: int = 1000, g_tol: float = 1e-8, f_abstol: float = 0.0, f_reltol: float = 0.0,
                   x_abstol: float = 0.0, time_limit: float = float("nan"), x_reltol: float = 0.0,
                   g_reltol: float = 0.0, f_calls_limit: int = 0,
-                  callback: Optional[Callable] = None, steepest: bool = False) -> BatchResult:
+                  callback: Optional[Callable] = None, steepest: bool = False,
+                  asynchronous: Optional[bool] = None) -> BatchResult:
     """Minimise fun row-wise from every row of X0.
 
     fun(X, rows) -> (f (r,), g (r, n)) evaluates the rows `rows` (int64 indices into the
@@ -280,10 +310,12 @@ def lbfgs_batched(fun: Callable[[torch.Tensor, torch.Tensor], tuple], X0: torch.
     x_reltol |x|_inf, f_calls_limit (0: none)).  callback(X, f, g, iters) runs after the initial
     evaluation and after every iteration; a True return stops every row (Optim's callback).
     steepest: gradient descent (GradientDescent): the history is cleared after every step, so the
-    two-loop recursion returns D = -g (gamma = 1) and the same line search runs along it."""
+    two-loop recursion returns D = -g (gamma = 1) and the same line search runs along it.
+    asynchronous (device path): rows advance without waiting for each other (default without a
+    callback; same per-row trajectories, _lbfgs_device)."""
     if X0.is_cuda and not _TORCH_LS and not _TORCH_TWO_LOOP and X0.dtype == torch.float64 and m <= 64:
         return _lbfgs_device(fun, X0, m, iterations, g_tol, f_abstol, f_reltol, x_abstol, time_limit, x_reltol,
-                             g_reltol, f_calls_limit, callback, steepest)
+                             g_reltol, f_calls_limit, callback, steepest, asynchronous)
     t_start = time.perf_counter()
     X = X0.clone()
     R, n = X.shape

@@ -211,3 +211,37 @@ def test_fused_cost_matches_torch_cost(case):
         cost.close()
     assert torch.allclose(c_f, c_t, rtol=1e-13, atol=1e-15), float((c_f - c_t).abs().max())
     assert torch.allclose(g_f, g_t, rtol=1e-12, atol=1e-14), float((g_f - g_t).abs().max())
+
+
+@pytest.mark.parametrize("steepest", [False, True])
+def test_asynchronous_rows_are_the_synchronous_trajectories(steepest):
+    """grape_lbfgs_async_advance: rows advance without waiting for each other at iteration
+    boundaries; each row's arithmetic is the synchronous loop's, so iterations, call counts, flags
+    and minimisers are bitwise equal (Rosenbrock rows that need very different numbers of line-search
+    rounds, and the GRAPE cost of a Rydberg batch)."""
+    rng = np.random.default_rng(11)
+    X0 = torch.as_tensor(rng.uniform(-2, 2, size=(13, 4)), device="cuda")
+    res = {}
+    for asy in (False, True):
+        res[asy] = OPT.lbfgs_batched(_rosen, X0, iterations=60 if steepest else 300, g_tol=1e-9,
+                                     steepest=steepest, asynchronous=asy)
+    a, b = res[False], res[True]
+    assert torch.equal(a.iterations, b.iterations) and torch.equal(a.f_calls, b.f_calls)
+    assert torch.equal(a.minimizer, b.minimizer) and torch.equal(a.minimum, b.minimum)
+    for k in ("g_converged", "f_converged", "x_converged", "ls_failed"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    if steepest:
+        return
+    fp = P.sym_problem(60, t0=P.T0_TO)
+    Xg = torch.as_tensor(np.stack([P.random_x(60, 2000 + r, small=True) for r in range(7)]), device="cuda")
+    params = _params(Xg[0].cpu().numpy(), iterations=15)
+    out = {}
+    for asy in (False, True):
+        cost = OPT.RobustCost(fp, params, nparam=1, max_batch=7)
+        try:
+            out[asy] = OPT.lbfgs_batched(cost, Xg, iterations=15, g_tol=1e-12, asynchronous=asy)
+        finally:
+            cost.close()
+    a, b = out[False], out[True]
+    assert torch.equal(a.iterations, b.iterations) and torch.equal(a.f_calls, b.f_calls)
+    assert torch.equal(a.minimizer, b.minimizer)
