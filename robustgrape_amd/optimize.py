@@ -40,7 +40,7 @@ from .types import FidelityRobustGRAPEParameters, FidelityRobustGRAPEProblem
 
 C1, C2 = 1e-4, 0.9
 MAX_LS_ROUNDS = 30
-_ASYNC_ROWS_DEFAULT = False  # device optimiser: rows advance asynchronously unless a callback is given
+_ASYNC_ROWS_DEFAULT = True  # device optimiser: rows advance asynchronously unless a callback is given
 MAX_PLAN_BATCH = 4096
 
 
