@@ -1405,6 +1405,9 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
 // GRAPE_WALK_FDX_IN_ERR (default): the F_dx traces are taken by k_walk_err_grad's e = 0 lanes, which
 // read Z1 anyway, so this kernel reads only the W images (C3: 5 -> 4 of the 9 tiles per step), and
 // not at all for the 2-level classes whose image walk sums W itself (WalkCfg::IMG_WSUM).
+#ifndef GRAPE_WALK_IMGSUM_UNROLL
+#define GRAPE_WALK_IMGSUM_UNROLL 1
+#endif
 template <int D, int NS>
 __global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, DevBatch B) {
     constexpr int TS = D * D;
@@ -1448,14 +1451,24 @@ __global__ __launch_bounds__(kWalkBlock, 2) void k_walk_img_sum(DevProblem P, De
             cd acc[TS];
 #pragma unroll
             for (int t = 0; t < TS; ++t) acc[t] = czero();
+            // GRAPE_WALK_IMGSUM_UNROLL steps per iteration, loads unconditional (the step index
+            // clamped), so their reads are in flight together; the sums stay in step order
+            constexpr int UN = GRAPE_WALK_IMGSUM_UNROLL;
 #pragma unroll 1
-            for (int jj = 0; jj < P.L; ++jj) {
-                const bool act = k0 + jj < P.Nt;  // (uniform within a chunk's lanes)
-                const cd *Wk = B.Zl + img_index<D, NS>(P, vb.y, jj, w, P.nvg + e, 0, lanes, lane);
+            for (int j0 = 0; j0 < P.L; j0 += UN) {
+                cd v[UN][TS];
 #pragma unroll
-                for (int t = 0; t < TS; ++t) {
-                    const cd v = Wk[(size_t)t * lanes];
-                    acc[t] = act ? cadd(acc[t], v) : acc[t];
+                for (int du = 0; du < UN; ++du) {
+                    const int jj = min(j0 + du, P.L - 1);
+                    const cd *Wk = B.Zl + img_index<D, NS>(P, vb.y, jj, w, P.nvg + e, 0, lanes, lane);
+#pragma unroll
+                    for (int t = 0; t < TS; ++t) v[du][t] = Wk[(size_t)t * lanes];
+                }
+#pragma unroll
+                for (int du = 0; du < UN; ++du) {
+                    const bool act = j0 + du < P.L && k0 + j0 + du < P.Nt;  // (uniform within a chunk's lanes)
+#pragma unroll
+                    for (int t = 0; t < TS; ++t) acc[t] = act ? cadd(acc[t], v[du][t]) : acc[t];
                 }
             }
             if (L.ok) {
