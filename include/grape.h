@@ -257,6 +257,11 @@ int grape_fidelity_grad_device_async(grape_plan *plan, int nbatch, const double 
  *   propagators of the last grape_slice_forward on this plan.  Both synchronous. */
 int grape_slice_forward(grape_plan *plan, const double *x, double *U_slice);
 int grape_slice_gradient(grape_plan *plan, const double *M_prime, double *F_dx);
+/* The same with DEVICE buffers (round 4), enqueued on the plan's stream without a synchronize
+ * (grape_plan_synchronize reports a singular Pade denominator): the time-sharded evaluation then
+ * exchanges slice totals and F_dx slices device to device (robustgrape_amd/timeshard.py). */
+int grape_slice_forward_device(grape_plan *plan, const double *x, double *U_slice);
+int grape_slice_gradient_device(grape_plan *plan, const double *M_prime, double *F_dx);
 
 /*
  * Closure fallback (plans created with GRAPE_DESC_HOST_TABLES): the outputs of

@@ -26,7 +26,8 @@ EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grap
             "grape_lbfgs_direction", "grape_unitary_derivs_tables", "grape_interaction_error_operators_tables",
             "grape_expectation_values_tables", "grape_plan_sectors", "grape_lbfgs_ls_init", "grape_lbfgs_ls_begin",
             "grape_lbfgs_ls_end", "grape_lbfgs_step", "grape_robust_cost", "grape_slice_forward",
-            "grape_slice_gradient", "grape_symmetry_basis", "grape_plan_sector_info", "grape_lbfgs_async_advance"]
+            "grape_slice_gradient", "grape_symmetry_basis", "grape_plan_sector_info", "grape_lbfgs_async_advance",
+            "grape_slice_forward_device", "grape_slice_gradient_device"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad/k_err_local", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad",
                 "k_walk_fwd", "k_walk_grad"]
@@ -77,6 +78,9 @@ def lib():
         L.grape_lbfgs_ls_end.restype = ctypes.c_int
         L.grape_lbfgs_async_advance.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
         L.grape_lbfgs_async_advance.restype = ctypes.c_int
+        for name in ("grape_slice_forward_device", "grape_slice_gradient_device"):
+            getattr(L, name).argtypes = [vp, vp, vp]
+            getattr(L, name).restype = ctypes.c_int
         L.grape_robust_cost.argtypes = [ctypes.c_int] * 5 + [vp] * 12
         L.grape_robust_cost.restype = ctypes.c_int
         L.grape_slice_forward.argtypes = [vp, dp, dp]

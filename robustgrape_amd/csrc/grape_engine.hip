@@ -1809,6 +1809,27 @@ int grape_slice_gradient(grape_plan *p, const double *M_prime, double *F_dx) {
     return grape_plan_synchronize(p);
 }
 
+int grape_slice_forward_device(grape_plan *p, const double *d_x, double *d_U_slice) {
+    if (!p || !d_x || !d_U_slice) return fail(GRAPE_ERR_INVALID, "bad argument");
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = slice_check(p)) return rc;
+    hipStream_t st = p->stream;
+    // the slice's controls stay in the plan for grape_slice_gradient_device (as the host entry)
+    HIPCHECK(hipMemcpyAsync(p->d_x, d_x, (size_t)p->P.nx * sizeof(double), hipMemcpyDeviceToDevice, st));
+    const grape_dense::DenseBatch DB = dense_batch(p, 1, p->d_x, p->d_F, p->d_Fdx, nullptr, nullptr);
+    HIPCHECK(grape_dense::launch_slice_forward(p->DP, DB, reinterpret_cast<cd *>(d_U_slice), st));
+    return GRAPE_OK;
+}
+
+int grape_slice_gradient_device(grape_plan *p, const double *d_M_prime, double *d_F_dx) {
+    if (!p || !d_M_prime || !d_F_dx) return fail(GRAPE_ERR_INVALID, "bad argument");
+    HIPCHECK(hipSetDevice(p->device));
+    if (int rc = slice_check(p)) return rc;
+    const grape_dense::DenseBatch DB = dense_batch(p, 1, p->d_x, p->d_F, d_F_dx, nullptr, nullptr);
+    HIPCHECK(grape_dense::launch_slice_gradient(p->DP, DB, reinterpret_cast<const cd *>(d_M_prime), p->stream));
+    return GRAPE_OK;
+}
+
 int grape_fidelity_grad_tables(grape_plan *p, int nbatch, const double *x, const double *H, const double *U0,
                                double *F, double *F_dx, double *F_d2err, double *F_d2err_dx) {
     if (!p || nbatch < 0 || (nbatch > 0 && (!x || !H || !U0 || !F || !F_dx)))

@@ -86,6 +86,40 @@ class SlicePlan:
                                                      _capi.dptr(g)))
         return g
 
+    # device buffers (grape_slice_*_device).  The plan runs on a side stream ordered after the
+    # caller's current torch stream and joined back into it (a null current stream cannot be handed
+    # to grape_plan_set_stream, which takes 0 for the plan's own, non-blocking stream).
+    def _enqueue(self, dev, call):
+        import torch
+        cur = torch.cuda.current_stream(dev)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=dev)
+        self._side.wait_stream(cur)
+        self.plan.set_stream(self._side.cuda_stream)
+        call()
+        cur.wait_stream(self._side)
+
+    def forward_device(self, x_t):
+        """forward() on a device tensor; returns the total as a (d, d) complex128 device tensor."""
+        import torch
+        if tuple(x_t.shape) != (self.nparam * (self.k1 - self.k0),) or x_t.dtype != torch.float64:
+            raise AssertionError("slice controls: nparam * steps float64 values")
+        x_t = x_t.contiguous()
+        Ut = torch.empty(self.d, self.d, dtype=torch.complex128, device=x_t.device)  # column-major U = Ut^T
+        self._enqueue(x_t.device, lambda: _capi.check(_capi.lib().grape_slice_forward_device(
+            self.plan.handle, ctypes.c_void_p(x_t.data_ptr()), ctypes.c_void_p(Ut.data_ptr()))))
+        return Ut.transpose(0, 1)
+
+    def gradient_device(self, M_prime_t):
+        """gradient() for a (d, d) complex128 device tensor M'; returns a float64 device tensor
+        (synchronise with plan.synchronize() before trusting it: it reports a singular Pade)."""
+        import torch
+        Mc = M_prime_t.transpose(0, 1).contiguous()  # column-major storage of M'
+        g = torch.empty(self.nparam * (self.k1 - self.k0), dtype=torch.float64, device=Mc.device)
+        self._enqueue(Mc.device, lambda: _capi.check(_capi.lib().grape_slice_gradient_device(
+            self.plan.handle, ctypes.c_void_p(Mc.data_ptr()), ctypes.c_void_p(g.data_ptr()))))
+        return g
+
     def close(self):
         self.plan.close()
 
@@ -107,6 +141,31 @@ def fidelity_head(fp: FidelityRobustGRAPEProblem, U: np.ndarray, x_add=()):
     F = (np.trace(A @ K @ B @ K.conj().T).real + abs(tau) ** 2) / DD
     M = ((B @ K.conj().T @ A + B.T @ K.conj().T @ A.conj().T) @ K + 2.0 * np.conj(tau) * (A @ K)) / DD
     return float(F), M
+
+
+def fidelity_head_torch(fp: FidelityRobustGRAPEProblem, U):
+    """fidelity_head on a device tensor U (the same expressions in torch): (F as a 0-d tensor, M)."""
+    import torch
+    dev = U.device
+    P0 = torch.as_tensor(np.asarray(fp.projector, dtype=np.float64), device=dev).to(torch.complex128)
+    P = (P0 != 0).to(torch.complex128)
+    D = float(np.trace(np.asarray(fp.projector, dtype=np.float64)))
+    DD = D * (D + 1.0)
+    U0 = torch.as_tensor(np.asarray(fp.target_unitary(np.zeros(0)), dtype=np.complex128), device=dev)
+    K = U0.conj().T @ U
+    A, B = P0 @ P, P
+    tau = torch.trace(A @ K)
+    F = (torch.trace(A @ K @ B @ K.conj().T).real + torch.abs(tau) ** 2) / DD
+    M = ((B @ K.conj().T @ A + B.T @ K.conj().T @ A.conj().T) @ K + 2.0 * torch.conj(tau) * (A @ K)) / DD
+    return F, M
+
+
+def _chain_torch(mats, d, dev):
+    import torch
+    out = torch.eye(d, dtype=torch.complex128, device=dev)
+    for S in mats:
+        out = S @ out
+    return out
 
 
 _plans: "OrderedDict[tuple, SlicePlan]" = OrderedDict()
@@ -146,13 +205,15 @@ def _chain(mats, d):
 
 
 def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, nslices: int | None = None,
-                               group=None, device: int = 0):
+                               group=None, device: int = 0, device_exchange: bool | None = None):
     """(F, F_dx) of ONE evaluation with its time steps split into slices.
 
     group: a torch.distributed process group (or the default group when torch.distributed is
     initialised and group is None and nslices is None): one slice per rank, two all_gathers.
     Otherwise `nslices` slices run one after another on `device`.  Every rank returns the full
-    (F, F_dx)."""
+    (F, F_dx).  device_exchange (default: with the nccl backend; optional for the in-order slices):
+    slice totals, the chain, the head, M' and the F_dx slices stay device tensors
+    (grape_slice_*_device, RCCL all_gathers of device buffers); only F and F_dx come back."""
     up = fp.unitary_problem
     x = np.ascontiguousarray(x, dtype=np.float64)
     if x.shape != (nparam * up.ntimes,):
@@ -165,6 +226,21 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
         nslices = dist.get_world_size(group)
         rank = dist.get_rank(group)
     bounds = slice_bounds(up.ntimes, nslices)
+    if dist is None and device_exchange:  # virtual ranks, device buffers throughout
+        import torch
+        dev = torch.device("cuda", device)
+        xt = torch.as_tensor(x, device=dev)
+        plans = [_slice_plan(fp, nparam, a, b, device, keep=nslices) for a, b in bounds]
+        totals = [sp.forward_device(xt[a * nparam:b * nparam]) for sp, (a, b) in zip(plans, bounds)]
+        F, M = fidelity_head_torch(fp, _chain_torch(totals, up.ndim, dev))
+        grads = []
+        for r, sp in enumerate(plans):
+            B = _chain_torch(totals[:r], up.ndim, dev)
+            grads.append(sp.gradient_device(B @ M @ B.conj().T))
+        Fdx = torch.cat(grads)
+        for sp in plans:
+            sp.plan.synchronize()
+        return float(F.item()), Fdx.cpu().numpy()
     if dist is None:  # virtual ranks: every slice here, in order
         plans = [_slice_plan(fp, nparam, a, b, device, keep=nslices) for a, b in bounds]
         totals = [sp.forward(x[a * nparam:b * nparam]) for sp, (a, b) in zip(plans, bounds)]
@@ -177,8 +253,28 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
     import torch
     a, b = bounds[rank]
     sp = _slice_plan(fp, nparam, a, b, device)
-    S = sp.forward(x[a * nparam:b * nparam])
     backend = dist.get_backend(group)
+    if device_exchange is None:
+        device_exchange = backend == "nccl"
+    if device_exchange:  # device buffers throughout: two RCCL all_gathers, no host staging
+        dev = torch.device("cuda", torch.cuda.current_device())
+        d = up.ndim
+        S = torch.view_as_real(sp.forward_device(torch.as_tensor(x[a * nparam:b * nparam], device=dev)).contiguous())
+        got = [torch.empty_like(S) for _ in range(nslices)]
+        dist.all_gather(got, S, group=group)  # the one exchange of slice totals (as real pairs)
+        got = [torch.view_as_complex(t) for t in got]
+        F, M = fidelity_head_torch(fp, _chain_torch(got, d, dev))
+        B = _chain_torch(got[:rank], d, dev)
+        g = sp.gradient_device(B @ M @ B.conj().T)
+        width = max(nb - na for na, nb in bounds) * nparam
+        pad = torch.zeros(width, dtype=torch.float64, device=dev)
+        pad[:g.numel()] = g
+        parts = [torch.empty_like(pad) for _ in range(nslices)]
+        dist.all_gather(parts, pad, group=group)  # the F_dx slices
+        Fdx = torch.cat([parts[r][:(nb - na) * nparam] for r, (na, nb) in enumerate(bounds)])
+        sp.plan.synchronize()
+        return float(F.item()), Fdx.cpu().numpy()
+    S = sp.forward(x[a * nparam:b * nparam])
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     d = up.ndim
     mine = torch.from_numpy(np.ascontiguousarray(S).view(np.float64).reshape(d, d, 2)).to(dev)

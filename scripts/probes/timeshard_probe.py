@@ -55,4 +55,19 @@ for R in (2, 4, 8):
     grad = best(lambda: sp.gradient(M))
     print(f"  {R} slices: sequential on one GPU {seq:.2f} ms; one slice forward {fwd:.2f} ms + gradient "
           f"{grad:.2f} ms (the {R}-GPU critical path without the exchange: {fwd + grad:.2f} ms)")
+    # device exchange: totals, head, M' and F_dx stay device tensors (grape_slice_*_device)
+    import torch
+    TS.time_sharded_fidelity_grad(fp, x, nparam=2, nslices=R, device_exchange=True)
+    seqd = best(lambda: TS.time_sharded_fidelity_grad(fp, x, nparam=2, nslices=R, device_exchange=True))
+    xt = torch.as_tensor(x[2 * a:2 * b], device="cuda:0")
+    Mt = torch.eye(fp.unitary_problem.ndim, dtype=torch.complex128, device="cuda:0")
+
+    def one_slice():
+        sp.forward_device(xt)
+        sp.gradient_device(Mt)
+        torch.cuda.synchronize()
+    one_slice()
+    fg = best(one_slice)
+    print(f"  {R} slices, device exchange: sequential on one GPU {seqd:.2f} ms; one slice forward + "
+          f"gradient on device buffers {fg:.2f} ms")
 pl.close()

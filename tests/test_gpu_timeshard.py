@@ -83,3 +83,66 @@ def test_slices_refuse_unsupported_plans():
             sp.forward(np.zeros(16))
     finally:
         sp.close()
+
+
+@pytest.mark.parametrize("nslices", [1, 3, 8])
+def test_device_exchange_matches_host_exchange(nslices):
+    """grape_slice_forward_device / grape_slice_gradient_device with the chain, head and M' as
+    device tensors (the nccl path of time_sharded_fidelity_grad, here with the slices in order):
+    the same F and F_dx as the host-staged exchange (rocBLAS products instead of numpy's: 1e-14)
+    and as the oracle."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd.synthetic import dense_problem, dense_x
+    from robustgrape_amd.timeshard import time_sharded_fidelity_grad
+    fp = dense_problem(d=24, ntimes=40, dt=0.3, rank=8)
+    x = dense_x(ntimes=40, seed=9)
+    Fh, gh = time_sharded_fidelity_grad(fp, x, nparam=2, nslices=nslices)
+    Fd, gd = time_sharded_fidelity_grad(fp, x, nparam=2, nslices=nslices, device_exchange=True)
+    assert abs(Fd - Fh) <= 1e-14
+    assert np.max(np.abs(gd - gh)) <= 1e-14 * max(1.0, float(np.max(np.abs(gh))))
+    F0, g0 = O.calculate_fidelity_and_derivatives(fp, x)[:2]
+    _check(f"timeshard_device_s{nslices}_oracle", Fd, gd, F0, np.asarray(g0))
+
+
+def _device_exchange_worker(rank, world, port, q):
+    import os
+    import torch
+    import torch.distributed as dist
+    from robustgrape_amd.synthetic import dense_problem, dense_x
+    from robustgrape_amd.timeshard import time_sharded_fidelity_grad
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fp = dense_problem(d=24, ntimes=40, dt=0.3, rank=8)
+        F, Fdx = time_sharded_fidelity_grad(fp, dense_x(ntimes=40, seed=9), nparam=2, device_exchange=True)
+        q.put((rank, F, Fdx.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ranks_exchange_device_buffers():
+    """The rank path of the device exchange (all_gathers of device tensors; gloo's CUDA all_gather
+    here, RCCL on a multi-GPU node), two ranks sharing this GPU: every rank returns the oracle's
+    F and F_dx."""
+    import socket
+    import torch.multiprocessing as mp
+    from oracle import grape_oracle as O
+    from robustgrape_amd.synthetic import dense_problem, dense_x
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_device_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=100) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    fp = dense_problem(d=24, ntimes=40, dt=0.3, rank=8)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fp, dense_x(ntimes=40, seed=9))[:2]
+    for r, F, Fdx in out:
+        _check(f"timeshard_device_rank{r}_oracle", F, np.asarray(Fdx), F0, np.asarray(g0))
