@@ -1818,6 +1818,8 @@ int grape_slice_forward_device(grape_plan *p, const double *d_x, double *d_U_sli
     HIPCHECK(hipMemcpyAsync(p->d_x, d_x, (size_t)p->P.nx * sizeof(double), hipMemcpyDeviceToDevice, st));
     const grape_dense::DenseBatch DB = dense_batch(p, 1, p->d_x, p->d_F, p->d_Fdx, nullptr, nullptr);
     HIPCHECK(grape_dense::launch_slice_forward(p->DP, DB, reinterpret_cast<cd *>(d_U_slice), st));
+    // the Pade status for the caller's grape_plan_synchronize (as the host entries report it)
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, st));
     return GRAPE_OK;
 }
 
@@ -1827,6 +1829,7 @@ int grape_slice_gradient_device(grape_plan *p, const double *d_M_prime, double *
     if (int rc = slice_check(p)) return rc;
     const grape_dense::DenseBatch DB = dense_batch(p, 1, p->d_x, p->d_F, d_F_dx, nullptr, nullptr);
     HIPCHECK(grape_dense::launch_slice_gradient(p->DP, DB, reinterpret_cast<const cd *>(d_M_prime), p->stream));
+    HIPCHECK(hipMemcpyAsync(p->h_status, p->d_ctrl + 2, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     return GRAPE_OK;
 }
 
