@@ -197,6 +197,10 @@ struct grape_plan {
     // first (fork / join events; the classes are independent until the sector heads)
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // GRAPE_OPT_GRAPH_FORK: the fork/join events of ONE capture (one pair per stage), created at
+    // capture start and destroyed once the graph is instantiated, so no event recorded inside a
+    // capture is ever recorded again outside it or in a later capture.
+    hipEvent_t cap_fork[3] = {}, cap_join[3] = {};
     bool capturing = false;  // graph_capture in progress: no fork unless GRAPE_OPT_GRAPH_FORK (captured
                              // forks crashed the host process in rounds 3 and 4)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
@@ -260,7 +264,14 @@ struct grape_plan {
 // branch; C3 single evaluation 0.631 -> 0.548 ms).  Off by default: with it, the host process
 // segfaulted inside grape_fidelity_grad on tests/test_gpu_xadd_err.py
 // test_xadd_with_errors_batch_is_bitwise_the_single_calls (round 4).
-static bool graph_fork(const grape_plan *p) { return (p->P.opts & GRAPE_OPT_GRAPH_FORK) != 0; }
+// GRAPE_GRAPH_FORK=1 in the environment turns it on for every plan (test runs of the whole suite).
+static bool graph_fork(const grape_plan *p) {
+    static const bool forced = [] {
+        const char *v = std::getenv("GRAPE_GRAPH_FORK");
+        return v && v[0] == '1';
+    }();
+    return forced || (p->P.opts & GRAPE_OPT_GRAPH_FORK) != 0;
+}
 
 static void free_plan(grape_plan *p) {
     if (!p) return;
@@ -1474,14 +1485,16 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
                 }
                 return hipSuccess;
             }
-            hipError_t e = hipEventRecord(p->ev_fork, st);
-            if (e == hipSuccess) e = hipStreamWaitEvent(p->aux_stream, p->ev_fork, 0);
+            hipEvent_t evf = p->capturing ? p->cap_fork[s] : p->ev_fork;
+            hipEvent_t evj = p->capturing ? p->cap_join[s] : p->ev_join;
+            hipError_t e = hipEventRecord(evf, st);
+            if (e == hipSuccess) e = hipStreamWaitEvent(p->aux_stream, evf, 0);
             if (e == hipSuccess) e = dispatch_sector_stage(p->Ps[0].D, s, p->Ps[0], Bc[0], st, mk);
             p->cur_stream = p->aux_stream;
             if (e == hipSuccess) e = dispatch_sector_stage(p->Ps[1].D, s, p->Ps[1], Bc[1], p->aux_stream, mk);
             p->cur_stream = st;
-            if (e == hipSuccess) e = hipEventRecord(p->ev_join, p->aux_stream);
-            if (e == hipSuccess) e = hipStreamWaitEvent(st, p->ev_join, 0);
+            if (e == hipSuccess) e = hipEventRecord(evj, p->aux_stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(st, evj, 0);
             return e;
         };
         HIPCHECK(stage(0));
@@ -1663,6 +1676,20 @@ constexpr int kGraphBatch = 64, kGraphCache = 8;
 static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     const int nx = p->P.nx, ne = p->P.ne;
     hipStream_t st = p->stream;
+    auto drop_cap_events = [p]() {
+        for (int i = 0; i < 3; ++i) {
+            if (p->cap_fork[i]) (void)hipEventDestroy(p->cap_fork[i]);
+            if (p->cap_join[i]) (void)hipEventDestroy(p->cap_join[i]);
+            p->cap_fork[i] = p->cap_join[i] = nullptr;
+        }
+    };
+    if (p->aux_stream && graph_fork(p))
+        for (int i = 0; i < 3; ++i)
+            if (hipEventCreateWithFlags(&p->cap_fork[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->cap_join[i], hipEventDisableTiming) != hipSuccess) {
+                drop_cap_events();
+                return fail(GRAPE_ERR_HIP, "event creation failed (graph capture)");
+            }
     HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     auto body = [&]() -> int {
         HIPCHECK(hipMemcpyAsync(p->d_x, p->h_x, (size_t)nb * nx * sizeof(double), hipMemcpyHostToDevice, st));
@@ -1683,12 +1710,17 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     const hipError_t e = hipStreamEndCapture(st, &g);
     if (rc) {
         if (g) (void)hipGraphDestroy(g);
+        drop_cap_events();
         return rc;
     }
-    if (e != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    if (e != hipSuccess) {
+        drop_cap_events();
+        return fail(GRAPE_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    }
     hipGraphExec_t ex = nullptr;
     const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
+    drop_cap_events();
     if (ei != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
     if ((int)p->graphs.size() >= kGraphCache) {
         (void)hipGraphExecDestroy(p->graphs.front().exec);
