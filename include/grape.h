@@ -189,7 +189,8 @@ typedef struct grape_desc {
  * share one exponential per step; this option computes each sector's own. */
 #define GRAPE_OPT_NO_TWIN 2048
 /* Small calls captured into HIP graphs also fork the second sector class onto the auxiliary stream
-   (a graph branch).  Experimental, off by default: it crashed the host process. */
+   (a graph branch).  Experimental, off by default: it crashed the host process once in round 4
+   (DESIGN.md 10).  GRAPE_GRAPH_FORK=1 in the environment turns it on for every plan. */
 #define GRAPE_OPT_GRAPH_FORK 4096
 
 typedef struct grape_plan grape_plan;
