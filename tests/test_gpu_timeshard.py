@@ -115,8 +115,8 @@ def _device_exchange_worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        fp = dense_problem(d=24, ntimes=40, dt=0.3, rank=8)
-        F, Fdx = time_sharded_fidelity_grad(fp, dense_x(ntimes=40, seed=9), nparam=2, device_exchange=True)
+        fp = dense_problem(d=24, ntimes=41, dt=0.3, rank=8)
+        F, Fdx = time_sharded_fidelity_grad(fp, dense_x(ntimes=41, seed=9), nparam=2, device_exchange=True)
         q.put((rank, F, Fdx.tolist()))
     finally:
         dist.destroy_process_group()
@@ -124,8 +124,8 @@ def _device_exchange_worker(rank, world, port, q):
 
 def test_ranks_exchange_device_buffers():
     """The rank path of the device exchange (all_gathers of device tensors; gloo's CUDA all_gather
-    here, RCCL on a multi-GPU node), two ranks sharing this GPU: every rank returns the oracle's
-    F and F_dx."""
+    here, RCCL on a multi-GPU node), two ranks sharing this GPU, ragged slices (21 + 20 steps: the
+    padded F_dx all_gather): every rank returns the oracle's F and F_dx."""
     import socket
     import torch.multiprocessing as mp
     from oracle import grape_oracle as O
@@ -142,7 +142,7 @@ def test_ranks_exchange_device_buffers():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    fp = dense_problem(d=24, ntimes=40, dt=0.3, rank=8)
-    F0, g0 = O.calculate_fidelity_and_derivatives(fp, dense_x(ntimes=40, seed=9))[:2]
+    fp = dense_problem(d=24, ntimes=41, dt=0.3, rank=8)
+    F0, g0 = O.calculate_fidelity_and_derivatives(fp, dense_x(ntimes=41, seed=9))[:2]
     for r, F, Fdx in out:
         _check(f"timeshard_device_rank{r}_oracle", F, np.asarray(Fdx), F0, np.asarray(g0))
