@@ -220,6 +220,35 @@ def cpu_baseline(seconds=15.0, fp=None, label="C2"):
             "sample": f"{n} sequential C2 evaluations by the numpy restatement oracle/grape_oracle.py, 1 thread"}
 
 
+def cpu_baseline_c5(seconds, fp, x, label="C5"):
+    """SURVEY.md 8d C5 CPU baseline: the reference-faithful C++ port (oracle/cref, 1 thread) on
+    whole C5 evaluations (d = 64, N_t = 1 024: 5 120 Pade exponentials of 64 x 64 plus the LU
+    inverses and trace products per evaluation, UnitaryCalculations.jl:44-100).  Warm-up: one
+    evaluation of the same problem cut to 16 steps; then whole evaluations until `seconds` have
+    passed (at least one; about 18-30 s each)."""
+    from oracle.cref import cref
+    from robustgrape_amd import synthetic as S
+    if not cref.available():
+        return None
+    up = fp.unitary_problem
+    ne = len(up.error_sources)
+    nparam = (len(x) - up.nb_additional_param) // up.ntimes
+    warm = (S.dense_error_problem(ntimes=16, nerr=ne) if ne else S.dense_problem(ntimes=16))
+    cref.fidelity_grad(warm, S.dense_x(ntimes=16, nparam=nparam))
+    t = time.perf_counter()
+    n = 0
+    while True:
+        cref.fidelity_grad(fp, x)
+        n += 1
+        if time.perf_counter() - t > seconds:
+            break
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "gradient-evals/s", "cores": 1, "kind": "port",
+            "sample": f"{n} whole {label} evaluation(s) (d=64, N_t=1024) by the reference-faithful C++ restatement "
+                      f"oracle/cref after a 16-step warm-up, 1 thread", "seconds_per_eval": dt / n,
+            "host_cpu": _host_cpu()}
+
+
 def cpu_baseline_allcores(seconds=10.0, fp=None, label="C4"):
     """SURVEY.md 8d C4 CPU baseline: the C++ port over restarts on every host core this job may
     use (OpenMP; OMP_NUM_THREADS, the GPU box grants 16 CPUs per GPU), timed on a bounded sample."""
@@ -501,6 +530,10 @@ def c4_points(fp, nparam, inputs, dev, batches=(256, 32), seconds=1.5):
         plan.close()
         out[f"batch_{b}"] = {"value": n * b / dt, "unit": "gradient-evals/s", "ms_per_step": dt / n * 1e3,
                              "steps": n}
+    if "batch_256" in out and "batch_32" in out:
+        # 1 -> 8 GPU strong scaling of the 256-restart sweep implied by the two single-GPU points,
+        # before the (microsecond-scale) all_gather: 8 GPUs at 32 each against one GPU at 256
+        out["projected_8gpu_strong_ratio"] = 8 * out["batch_32"]["value"] / out["batch_256"]["value"]
     out["note"] = ("C4 as BASELINE names it: 256 restarts / 8 GPUs = 32 per GPU; per-GPU rate at that batch "
                    "(x resident in HBM, steps queued back to back on the plan's stream)")
     return out
@@ -758,9 +791,116 @@ def c2_closure(args):
     print(json.dumps(out), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`--gpus N` without a launcher (WORLD_SIZE unset): start N rank processes of this script,
+    one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would,
+    and wait for them.  The parent makes no GPU call (it never initialises HIP), so the children
+    own the devices; rank 0 prints the JSON line.  If one rank fails the others are stopped (their
+    exact PIDs) and the failing status is returned."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for i in sorted(pending):
+            c = procs[i].poll()
+            if c is None:
+                continue
+            pending.discard(i)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {i} exited with status {c}; stopping the other ranks", file=sys.stderr)
+                for j in pending:
+                    procs[j].terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def c4_strong(make_step, world, rank, use_dist, sync, total=256, evals_per_restart=100):
+    """BASELINE C4 as a strong-scaling sweep: `total` restarts sharded over the ranks (contiguous
+    blocks, robustgrape_amd/sweep.py), `evals_per_restart` fidelity+gradient evaluations of every
+    restart (examples/time_optimal_cz.jl:32 initialises them; the optimiser's evaluations are the
+    unit), then the sweep's exchange -- one all_gather of (best F, id) and the winner's broadcast --
+    INSIDE the timed region, bracketed by barrier + synchronize and maxed over ranks.
+    make_step(first, count) -> (step, F, X, ids, close)."""
+    import torch
+    import torch.distributed as dist
+    from robustgrape_amd.sweep import gather_best, gather_best_local, shard
+    first, count = shard(total, world, rank)
+    step, F, X, ids, close = make_step(first, count)
+    for _ in range(3):
+        step()
+    sync()
+    if use_dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(evals_per_restart):
+        step()
+    if use_dist:
+        fb, rid, owner, _ = gather_best(F, ids, X)
+        dist.barrier()
+    else:
+        fb, rid, owner, _ = gather_best_local(F, ids, X)
+    sync()
+    elapsed = time.perf_counter() - t0
+    close()
+    if use_dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=F.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return {"value": total * evals_per_restart / elapsed, "unit": "gradient-evals/s", "n_gpus": world,
+            "restarts_total": total, "restarts_per_rank": count, "evals_per_restart": evals_per_restart,
+            "ms_per_eval_round": elapsed / evals_per_restart * 1e3, "scaling": "strong",
+            "sweep": {"best_F": fb, "restart": rid, "owner_rank": owner},
+            "note": "256 restarts sharded over the ranks, 100 evaluations each, all_gather + broadcast of the "
+                    "best inside the timed region (max over ranks)"}
+
+
+def dry_run(args, world, rank, use_dist):
+    """Plumbing check of the multi-rank bench (no GPU, gloo): the launcher, the world-size check,
+    the barrier / max-over-ranks timing and the sweep exchange, with a placeholder score in place
+    of the evaluation.  Its line says "dry_run" and carries no throughput claim."""
+    import torch
+    from robustgrape_amd.sweep import gather_best, gather_best_local, shard
+    B = args.batch or 16
+    first, count = shard(B * world, world, rank)
+    X = torch.from_numpy(restart_inputs(first, count))
+    ids = torch.arange(first, first + count)
+    F = torch.empty(count, dtype=torch.float64)
+
+    def make_step(f, c):
+        Xs = torch.from_numpy(restart_inputs(f, c))
+        Fs = torch.empty(c, dtype=torch.float64)
+        return (lambda: torch.sum(torch.cos(Xs), dim=1, out=Fs)), Fs, Xs, torch.arange(f, f + c), (lambda: None)
+
+    torch.sum(torch.cos(X), dim=1, out=F)
+    best = gather_best(F, ids, X) if use_dist else gather_best_local(F, ids, X)
+    strong = c4_strong(make_step, world, rank, use_dist, lambda: None, total=args.c4_total,
+                       evals_per_restart=2)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher and exchange only)", "value": None, "dry_run": True,
+                          "n_gpus": world, "restarts_per_gpu": B,
+                          "sweep": {"best_F": best[0], "restart": best[1], "owner_rank": best[2]},
+                          "c4_strong": strong}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a launcher bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
@@ -786,21 +926,34 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-whole-matrix", action="store_true",
                     help="skip the C2 whole-matrix comparison leg (PMC passes: one pipeline per run)")
+    ap.add_argument("--no-c4-strong", action="store_true",
+                    help="skip the C4 strong-scaling leg (256 restarts over the ranks)")
+    ap.add_argument("--c4-total", type=int, default=256, help="restarts of the C4 strong-scaling leg")
     ap.add_argument("--dist", action="store_true",
                     help="run the multi-rank path (RCCL process group, the sweep's all_gather + "
                          "broadcast, max-over-ranks timing) even with one rank")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU plumbing check: gloo ranks, no GPU, placeholder scores (tests/test_bench_launch.py)")
     args = ap.parse_args()
+
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks (WORLD_SIZE); refusing "
+              "to print a mislabelled line", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.workload in ("c4opt", "c2-closure"):
+        print(f"bench.py: --workload {args.workload} is a single-GPU leg", file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
 
-    if args.workload == "c4opt":
-        return c4opt(args)
-    if args.workload == "c2-closure":
-        return c2_closure(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     use_dist = world > 1 or args.dist
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -808,6 +961,18 @@ def main():
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
         os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout (one JSON line)
+    if args.dry_run:
+        if use_dist:
+            dist.init_process_group("gloo")
+        dry_run(args, world, rank, use_dist)
+        if use_dist:
+            dist.destroy_process_group()
+        return
+    if args.workload == "c4opt":
+        return c4opt(args)
+    if args.workload == "c2-closure":
+        return c2_closure(args)
+    if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -897,6 +1062,19 @@ def main():
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         out["config"]["evals_per_device_pass"] = min(count, chunk)
     plan.close()
+
+    if not (c3 or c5) and not args.no_c4_strong:
+        def make_step(f, c):
+            p = GrapePlan(fp, nparam=nparam, device=local, max_batch=max(1, c))
+            p.set_stream(stream.cuda_stream)
+            Xs = torch.from_numpy(inputs(f, c)).to(dev)
+            Fs = torch.empty(c, dtype=torch.float64, device=dev)
+            Gs = torch.empty(c, Xs.shape[1], dtype=torch.float64, device=dev)
+            return ((lambda: p.fidelity_grad_device_async(Xs.data_ptr(), Fs.data_ptr(), Gs.data_ptr(), c, 0, 0)),
+                    Fs, Xs, torch.arange(f, f + c, device=dev), p.close)
+        strong = c4_strong(make_step, world, rank, use_dist, torch.cuda.synchronize, total=args.c4_total)
+        if rank == 0:
+            out["c4_strong"] = strong
     if rank == 0 and world == 1 and not (c3 or c5) and sectors[0][0] < d and not args.no_whole_matrix:
         out["whole_matrix_path"] = whole_matrix_leg(fp, nparam, X, F, Fdx, min(count, chunk), stream, args)
     if rank == 0:
@@ -908,9 +1086,13 @@ def main():
             out["single_eval"] = single_eval(fp, nparam, Xh[0])
             if not (c3 or c5):
                 out["c4_points"] = c4_points(fp, nparam, inputs, dev)
-        if world == 1 and not args.no_cpu_baseline and not c5:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, fp if c3 else None, "C3" if c3 else "C2")
-            if not c3:
+        if world == 1 and not args.no_cpu_baseline:
+            if c5:
+                out["cpu_baseline"] = cpu_baseline_c5(args.cpu_seconds, fp, c5_inputs(0, 1)[0],
+                                                      "C5 + 2 error sources" if c5err else "C5")
+            else:
+                out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, fp if c3 else None, "C3" if c3 else "C2")
+            if not (c3 or c5):
                 allc = cpu_baseline_allcores(args.cpu_seconds * 2 / 3, fp, "C4")
                 if allc is not None:
                     out["cpu_baseline_allcores"] = allc
