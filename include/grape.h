@@ -188,15 +188,18 @@ typedef struct grape_desc {
  * identical (the Rydberg sectors {01, 0r} and {10, r0} at equal Rabi frequencies and detunings)
  * share one exponential per step; this option computes each sector's own. */
 #define GRAPE_OPT_NO_TWIN 2048
-/* Small calls captured into HIP graphs also fork the second sector class onto the auxiliary stream
-   (a graph branch).  Experimental, off by default: it crashed the host process once in round 4
-   (DESIGN.md 10).  GRAPE_GRAPH_FORK=1 in the environment turns it on for every plan. */
+/* Accepted and ignored since round 5: captured small calls no longer fork the second sector class
+   (the experimental captured fork was removed).  Kept so that old callers still build. */
 #define GRAPE_OPT_GRAPH_FORK 4096
 
 typedef struct grape_plan grape_plan;
 
 /* Library / ABI identification. */
 int grape_abi_version(void);
+/* Content hash of the sources and flags the library was built from (robustgrape_amd/build.py
+ * source_id; round 5).  The Python binding refuses a library whose id differs from the sources
+ * next to it. */
+const char *grape_build_id(void);
 const char *grape_last_error(void);
 
 /* Number of visible HIP devices (0 when none); does not create a context. */

@@ -120,8 +120,33 @@ function cz_full_target(; index::Integer=1, rydberg_dimension::Integer=5)
                           OperatorTerm(e((4,)); var=VAR_XADD, index=index, func=FN_CIS, a=2.0, b=Float64(π))])
 end
 
+const GRAPE_ERR_UNSUPPORTED = Cint(-2)  # include/grape.h
+
+"A problem libgrape does not serve (GRAPE_ERR_UNSUPPORTED): the caller takes the reference's CPU method."
+struct GrapeUnsupported <: Exception
+    msg::String
+end
+
 function _check(rc)
-    rc == 0 || error("libgrape: " * unsafe_string(ccall((:grape_last_error, libgrape), Cstring, ())))
+    rc == 0 && return nothing
+    msg = unsafe_string(ccall((:grape_last_error, libgrape), Cstring, ()))
+    rc == GRAPE_ERR_UNSUPPORTED && throw(GrapeUnsupported(msg))
+    error("libgrape: " * msg)
+end
+
+# The graceful edge of the drop-in: a problem libgrape refuses (d > 64, non-Hermitian closure tables
+# above 12 levels, the dense engine's limits -- INTEGRATION.md section 5) is evaluated by the
+# reference's own method, reached with `invoke` past this shim's more specific Vector{Float64}
+# method (RobustGRAPE's signatures: FidelityCalculations.jl:19,368, UnitaryCalculations.jl:20,180).
+# Any other libgrape error still raises.
+function _or_reference(device_call, f, sig, args...)
+    try
+        return device_call()
+    catch e
+        e isa GrapeUnsupported || rethrow()
+        @debug "libgrape does not serve this problem ($(e.msg)); using RobustGRAPE's CPU method"
+        return invoke(f, sig, args...)
+    end
 end
 
 mutable struct DevicePlan
@@ -220,8 +245,8 @@ end
 # interchange-free solve, which needs them Hermitian, so anything else is refused.
 function _closure_general(up, H0s::AbstractArray, Hall::AbstractArray)
     if up.ndim > 12
-        _is_hermitian(Hall) || error("closure problems above 12 levels need Hermitian H0 / H0 + Herror tables " *
-                                     "(the dense engine's exponential); non-Hermitian generators are served up to 12 levels")
+        _is_hermitian(Hall) || throw(GrapeUnsupported("closure problems above 12 levels need Hermitian H0 / H0 + " *
+                                                      "Herror tables (the dense engine's exponential)"))
         return false
     end
     return !_is_hermitian(H0s)
@@ -302,8 +327,29 @@ function fidelity_wrapper(problem::UnitaryRobustGRAPEProblem)
 end
 
 "Drop-in for src/FidelityCalculations.jl:19-119: (F, F_dx_tot, F_d2err, F_d2err_dx_tot)."
-function calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::Vector{Float64})
+calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::Vector{Float64}) =
+    _or_reference(() -> _device_fidelity(fp, x), calculate_fidelity_and_derivatives,
+                  Tuple{FidelityRobustGRAPEProblem,Vector{<:Real}}, fp, x)
+
+"Drop-in for src/UnitaryCalculations.jl:20-155: (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add)."
+calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64}) =
+    _or_reference(() -> _device_unitary(problem, x), calculate_unitary_and_derivatives,
+                  Tuple{UnitaryRobustGRAPEProblem,Vector{<:Real}}, problem, x)
+
+"Drop-in for src/UnitaryCalculations.jl:180-204: (ndim, ndim, ntimes, nerr)."
+calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64}) =
+    _or_reference(() -> _device_interaction(problem, x), calculate_interaction_error_operators,
+                  Tuple{UnitaryRobustGRAPEProblem,Vector{<:Real}}, problem, x)
+
+"Drop-in for src/FidelityCalculations.jl:368-390: (ntimes, nerr)."
+calculate_expectation_values(fp::FidelityRobustGRAPEProblem, x::Vector{Float64}) =
+    _or_reference(() -> _device_expectation(fp, x), calculate_expectation_values,
+                  Tuple{FidelityRobustGRAPEProblem,Vector{<:Real}}, fp, x)
+
+# device bodies of the four entry points (GrapeUnsupported escapes to _or_reference)
+function _device_fidelity(fp::FidelityRobustGRAPEProblem, x::Vector{Float64})
     up = fp.unitary_problem
+    up.ndim > 64 && throw(GrapeUnsupported("ndim > GRAPE_MAX_DENSE_DIM (64)"))
     xm = length(x) - up.nb_additional_param
     @assert mod(xm, up.ntimes) == 0 "Control parameter size must be a multiple of time steps"
     if !is_operator_basis(fp)          # closure fallback
@@ -331,8 +377,8 @@ function calculate_fidelity_and_derivatives(fp::FidelityRobustGRAPEProblem, x::V
     return (F[], F_dx, F_d2err, F_d2err_dx)
 end
 
-"Drop-in for src/UnitaryCalculations.jl:20-155: (U, U_dx, U_dx_add, U_derr, U_derr_dx, U_derr_dx_add)."
-function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64})
+function _device_unitary(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64})
+    problem.ndim > 64 && throw(GrapeUnsupported("ndim > GRAPE_MAX_DENSE_DIM (64)"))
     fp = fidelity_wrapper(problem)
     up = problem
     d, nt, na, ne = up.ndim, up.ntimes, up.nb_additional_param, length(up.error_sources)
@@ -362,8 +408,8 @@ function calculate_unitary_and_derivatives(problem::UnitaryRobustGRAPEProblem, x
     return outs
 end
 
-"Drop-in for src/UnitaryCalculations.jl:180-204: (ndim, ndim, ntimes, nerr)."
-function calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64})
+function _device_interaction(problem::UnitaryRobustGRAPEProblem, x::Vector{Float64})
+    problem.ndim > 64 && throw(GrapeUnsupported("ndim > GRAPE_MAX_DENSE_DIM (64)"))
     fp = fidelity_wrapper(problem)
     up = problem
     np = (length(x) - up.nb_additional_param) ÷ up.ntimes
@@ -387,9 +433,9 @@ function calculate_interaction_error_operators(problem::UnitaryRobustGRAPEProble
     return O
 end
 
-"Drop-in for src/FidelityCalculations.jl:368-390: (ntimes, nerr)."
-function calculate_expectation_values(fp::FidelityRobustGRAPEProblem, x::Vector{Float64})
+function _device_expectation(fp::FidelityRobustGRAPEProblem, x::Vector{Float64})
     up = fp.unitary_problem
+    up.ndim > 64 && throw(GrapeUnsupported("ndim > GRAPE_MAX_DENSE_DIM (64)"))
     np = (length(x) - up.nb_additional_param) ÷ up.ntimes
     xv = Vector{Float64}(x)
     ev = zeros(Float64, up.ntimes, length(up.error_sources))

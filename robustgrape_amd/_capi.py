@@ -17,7 +17,7 @@ STATUS_NAMES = {-1: "GRAPE_ERR_INVALID", -2: "GRAPE_ERR_UNSUPPORTED", -3: "GRAPE
                 -4: "GRAPE_ERR_HIP", -5: "GRAPE_ERR_SINGULAR", -6: "GRAPE_ERR_NO_DEVICE"}
 
 # every symbol include/grape.h declares
-EXPORTED = ["grape_abi_version", "grape_last_error", "grape_device_count", "grape_plan_create",
+EXPORTED = ["grape_abi_version", "grape_build_id", "grape_last_error", "grape_device_count", "grape_plan_create",
             "grape_plan_destroy", "grape_plan_stream", "grape_plan_set_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times",
@@ -53,6 +53,7 @@ def lib():
         dp = ctypes.POINTER(ctypes.c_double)
         vp = ctypes.c_void_p
         L.grape_abi_version.restype = ctypes.c_int
+        L.grape_build_id.restype = ctypes.c_char_p
         L.grape_last_error.restype = ctypes.c_char_p
         L.grape_device_count.restype = ctypes.c_int
         L.grape_plan_create.argtypes = [ctypes.POINTER(CDesc), ctypes.c_int, ctypes.POINTER(vp)]
@@ -118,8 +119,19 @@ def lib():
         L.grape_symmetry_basis.restype = ctypes.c_int
         if L.grape_abi_version() != ABI_VERSION:
             raise ImportError("libgrape.so ABI version mismatch")
+        # provenance: the library must have been built from the csrc/ next to it (content hash)
+        from .build import source_id
+        got, want = L.grape_build_id().decode(), source_id()
+        if got != want:
+            raise ImportError(f"{LIB_PATH} was built from other sources (build id {got}, csrc/ hashes to {want}): "
+                              "rebuild with `python -m robustgrape_amd.build`")
         _lib = L
     return _lib
+
+
+def build_id() -> str:
+    """Source hash the loaded library was built from (robustgrape_amd/build.py source_id)."""
+    return lib().grape_build_id().decode()
 
 
 def check(code):

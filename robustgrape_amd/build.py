@@ -7,6 +7,7 @@ the GPU box (built .so files are git-ignored but not gpurun-ignored).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -41,11 +42,28 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
          "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 
+def source_id() -> str:
+    """Content hash of every source the library is built from (DEPS) and the compiler flags: the
+    library embeds it (grape_build_id()) and _capi.lib() refuses a library whose id differs from
+    the sources next to it, so a test or bench run names the sources it ran."""
+    h = hashlib.sha256()
+    for d in sorted(DEPS):
+        h.update(os.path.relpath(d, ROOT).encode() + b"\0")
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join(FLAGS[:5]).encode())
+    return h.hexdigest()[:16]
+
+
+ID_FILE = LIB + ".id"  # the id the in-tree library was linked with (read without loading it)
+
+
 def needs_build() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(ID_FILE):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+    with open(ID_FILE) as fh:
+        return fh.read().strip() != source_id()
 
 
 def _units(defines):
@@ -73,6 +91,7 @@ def build_library(force: bool = False, verbose: bool = True, out: str = LIB, def
     if verbose:
         print("[robustgrape_amd] building", os.path.relpath(out, ROOT), *defines,
               f"({len(units)} translation units)", flush=True)
+    sid = source_id()
     dflags = [f"-D{d}" for d in defines]
     jobs = max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
     pending = list(units)
@@ -82,6 +101,8 @@ def build_library(force: bool = False, verbose: bool = True, out: str = LIB, def
         while pending and len(running) < jobs:
             src, extra, obj = pending.pop(0)
             cmd = [HIPCC] + FLAGS + dflags + extra + ["-c", src, "-o", obj]
+            if src == ENGINE:
+                cmd.insert(1, f'-DGRAPE_BUILD_ID="{sid}"')
             running.append((subprocess.Popen(cmd), obj))
         proc, obj = running.pop(0)
         if proc.wait() != 0:
@@ -92,6 +113,9 @@ def build_library(force: bool = False, verbose: bool = True, out: str = LIB, def
     subprocess.run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + [u[2] for u in units] + ["-o", tmp],
                    check=True)
     os.replace(tmp, out)
+    if out == LIB:
+        with open(ID_FILE, "w") as fh:
+            fh.write(sid + "\n")
     return out
 
 

@@ -14,6 +14,9 @@
 #include <cstring>
 #include <string>
 #include <cstdlib>
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
 #include <vector>
 
 #include "grape.h"
@@ -197,12 +200,8 @@ struct grape_plan {
     // first (fork / join events; the classes are independent until the sector heads)
     hipStream_t aux_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // GRAPE_OPT_GRAPH_FORK: the fork/join events of ONE capture (one pair per stage), created at
-    // capture start and destroyed once the graph is instantiated, so no event recorded inside a
-    // capture is ever recorded again outside it or in a later capture.
-    hipEvent_t cap_fork[3] = {}, cap_join[3] = {};
-    bool capturing = false;  // graph_capture in progress: no fork unless GRAPE_OPT_GRAPH_FORK (captured
-                             // forks crashed the host process in rounds 3 and 4)
+    bool capturing = false;  // graph_capture in progress: calls captured into graphs never fork (the
+                             // captured fork was removed in round 5)
     // dense engine (GRAPE_MAX_SMALL_DIM < d <= GRAPE_MAX_DENSE_DIM)
     bool dense = false;
     grape_dense::DenseProblem DP{};
@@ -259,19 +258,6 @@ struct grape_plan {
         return e;
     }
 };
-
-// GRAPE_OPT_GRAPH_FORK: small calls captured into HIP graphs fork too (the fork becomes a graph
-// branch; C3 single evaluation 0.631 -> 0.548 ms).  Off by default: with it, the host process
-// segfaulted inside grape_fidelity_grad on tests/test_gpu_xadd_err.py
-// test_xadd_with_errors_batch_is_bitwise_the_single_calls (round 4).
-// GRAPE_GRAPH_FORK=1 in the environment turns it on for every plan (test runs of the whole suite).
-static bool graph_fork(const grape_plan *p) {
-    static const bool forced = [] {
-        const char *v = std::getenv("GRAPE_GRAPH_FORK");
-        return v && v[0] == '1';
-    }();
-    return forced || (p->P.opts & GRAPE_OPT_GRAPH_FORK) != 0;
-}
 
 static void free_plan(grape_plan *p) {
     if (!p) return;
@@ -832,9 +818,48 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
     return GRAPE_OK;
 }
 
+// A fatal signal inside the library names its native frames on stderr before the previous
+// handler (Python's faulthandler, or the default action) runs: the handler prints the
+// backtrace, reinstalls the handler it displaced and returns, so the faulting instruction
+// faults again into that one.  backtrace() is called once at load so that the unwinder is
+// resolved before any signal (it is not async-signal-safe on its first call).
+// GRAPE_NO_SIGNAL_HANDLER=1 leaves the process's handlers alone.
+namespace {
+struct sigaction g_prev_sig[2];
+const int kFatalSigs[2] = {SIGSEGV, SIGBUS};
+
+void grape_fatal_signal(int sig, siginfo_t *, void *) {
+    static const char head[] = "\n[libgrape] fatal signal; native frames (innermost first):\n";
+    (void)!write(2, head, sizeof head - 1);
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    backtrace_symbols_fd(frames, n, 2);
+    for (int i = 0; i < 2; ++i)
+        if (kFatalSigs[i] == sig) sigaction(sig, &g_prev_sig[i], nullptr);
+}
+
+__attribute__((constructor)) void grape_install_signal_handler() {
+    const char *off = std::getenv("GRAPE_NO_SIGNAL_HANDLER");
+    if (off && off[0] == '1') return;
+    void *warm[2];
+    (void)backtrace(warm, 2);
+    struct sigaction sa {};
+    sa.sa_sigaction = grape_fatal_signal;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    for (int i = 0; i < 2; ++i) sigaction(kFatalSigs[i], &sa, &g_prev_sig[i]);
+}
+}  // namespace
+
+#ifndef GRAPE_BUILD_ID
+#define GRAPE_BUILD_ID "unversioned"
+#endif
+
 extern "C" {
 
 int grape_abi_version(void) { return GRAPE_ABI_VERSION; }
+
+const char *grape_build_id(void) { return GRAPE_BUILD_ID; }
 
 const char *grape_last_error(void) { return g_err.c_str(); }
 
@@ -1437,7 +1462,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
         // Small calls (latency-bound: the optimiser's line-search rounds, single evaluations) run
         // the second sector class on the auxiliary stream beside the first; large ones keep one
         // stream (no gain there, DESIGN 4.1, and per-kernel event times stay per kernel).
-        const bool fork = p->aux_stream && (!p->capturing || graph_fork(p)) && nb <= kForkMaxBatch &&
+        const bool fork = p->aux_stream && !p->capturing && nb <= kForkMaxBatch &&
                           !(p->P.opts & GRAPE_OPT_NO_FORK);
         // Latency-bound calls of the Rydberg layout: both classes' walks (and scans) in ONE launch per
         // stage (grape_walk_api.hpp launch_pair) -- neither a graph branch nor a second stream overlaps
@@ -1485,8 +1510,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
                 }
                 return hipSuccess;
             }
-            hipEvent_t evf = p->capturing ? p->cap_fork[s] : p->ev_fork;
-            hipEvent_t evj = p->capturing ? p->cap_join[s] : p->ev_join;
+            hipEvent_t evf = p->ev_fork, evj = p->ev_join;
             hipError_t e = hipEventRecord(evf, st);
             if (e == hipSuccess) e = hipStreamWaitEvent(p->aux_stream, evf, 0);
             if (e == hipSuccess) e = dispatch_sector_stage(p->Ps[0].D, s, p->Ps[0], Bc[0], st, mk);
@@ -1676,20 +1700,6 @@ constexpr int kGraphBatch = 64, kGraphCache = 8;
 static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     const int nx = p->P.nx, ne = p->P.ne;
     hipStream_t st = p->stream;
-    auto drop_cap_events = [p]() {
-        for (int i = 0; i < 3; ++i) {
-            if (p->cap_fork[i]) (void)hipEventDestroy(p->cap_fork[i]);
-            if (p->cap_join[i]) (void)hipEventDestroy(p->cap_join[i]);
-            p->cap_fork[i] = p->cap_join[i] = nullptr;
-        }
-    };
-    if (p->aux_stream && graph_fork(p))
-        for (int i = 0; i < 3; ++i)
-            if (hipEventCreateWithFlags(&p->cap_fork[i], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&p->cap_join[i], hipEventDisableTiming) != hipSuccess) {
-                drop_cap_events();
-                return fail(GRAPE_ERR_HIP, "event creation failed (graph capture)");
-            }
     HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     auto body = [&]() -> int {
         HIPCHECK(hipMemcpyAsync(p->d_x, p->h_x, (size_t)nb * nx * sizeof(double), hipMemcpyHostToDevice, st));
@@ -1710,17 +1720,12 @@ static int graph_capture(grape_plan *p, int nb, hipGraphExec_t *out) {
     const hipError_t e = hipStreamEndCapture(st, &g);
     if (rc) {
         if (g) (void)hipGraphDestroy(g);
-        drop_cap_events();
         return rc;
     }
-    if (e != hipSuccess) {
-        drop_cap_events();
-        return fail(GRAPE_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
-    }
+    if (e != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
     hipGraphExec_t ex = nullptr;
     const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
-    drop_cap_events();
     if (ei != hipSuccess) return fail(GRAPE_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
     if ((int)p->graphs.size() >= kGraphCache) {
         (void)hipGraphExecDestroy(p->graphs.front().exec);

@@ -32,6 +32,27 @@ def test_library_exports_every_declared_symbol():
     assert len(_capi.KERNEL_NAMES) == int(re.search(r"GRAPE_NUM_KERNELS = (\d+)", src).group(1))
 
 
+def test_library_build_id_is_the_source_hash(tmp_path):
+    """Provenance: the loaded library embeds the content hash of the sources it
+    was built from, equal to the hash of csrc/ + include/ as they are now; a changed source gives
+    a different hash (so _capi.lib() would refuse the stale library)."""
+    from robustgrape_amd import _capi, build
+    build.build_library(verbose=False)
+    assert _capi.build_id() == build.source_id()
+    with open(build.ID_FILE) as fh:
+        assert fh.read().strip() == build.source_id()
+    src = build.DEPS[-1]
+    orig = open(src, "rb").read()
+    try:
+        with open(src, "ab") as fh:
+            fh.write(b"\n")
+        assert build.source_id() != _capi.build_id() and build.needs_build()
+    finally:
+        with open(src, "wb") as fh:
+            fh.write(orig)
+    assert build.source_id() == _capi.build_id() and not build.needs_build()
+
+
 def test_descriptor_packing_roundtrip():
     """The ctypes descriptor reproduces the operator basis (column-major, interleaved)."""
     from robustgrape_amd.operators import DescriptorBuffers

@@ -49,7 +49,9 @@ def _src():
 
 def _signatures(src):
     sigs = {}
-    for name, args in re.findall(r"^function (\w+)\((.*?)\)\s*$", src, re.M):
+    found = re.findall(r"^function (\w+)\((.*?)\)\s*$", src, re.M)
+    found += re.findall(r"^(\w+)\((.*?)\) =\s*$", src, re.M)  # one-expression methods
+    for name, args in found:
         types = [a.split("::", 1)[1].strip() if "::" in a else None
                  for a in re.split(r",\s*(?![^{]*\})", args.split(";")[0]) if a.strip()]
         sigs.setdefault(name, []).append(types)
@@ -128,3 +130,26 @@ def test_shim_checks_the_abi_version():
     src = _src()
     m = re.search(r"const GRAPE_ABI_VERSION = (\d+)", src)
     assert m and int(m.group(1)) == _capi.ABI_VERSION
+
+
+def test_every_entry_point_falls_back_to_the_reference_method():
+    """a problem libgrape refuses (GRAPE_ERR_UNSUPPORTED: d > 64, non-Hermitian
+    closure tables above 12 levels, the dense engine's limits) is evaluated by the reference's own
+    CPU method through `invoke` with the reference's signature -- never an error where the
+    reference worked.  Other libgrape errors still raise."""
+    src = _src()
+    assert re.search(r"const GRAPE_ERR_UNSUPPORTED = Cint\(-2\)", src)
+    from robustgrape_amd import _capi
+    assert _capi.STATUS_NAMES[-2] == "GRAPE_ERR_UNSUPPORTED"
+    # _check turns exactly that code into GrapeUnsupported, everything else into error(...)
+    chk = re.search(r"^function _check\(rc\)\n(.*?)^end", src, re.M | re.S).group(1)
+    assert "rc == GRAPE_ERR_UNSUPPORTED && throw(GrapeUnsupported(msg))" in chk and 'error("libgrape: "' in chk
+    fb = re.search(r"^function _or_reference\(device_call, f, sig, args\.\.\.\)\n(.*?)^end", src, re.M | re.S).group(1)
+    assert "e isa GrapeUnsupported || rethrow()" in fb and "return invoke(f, sig, args...)" in fb
+    for name, t0 in REFERENCE_SIGNATURES.items():
+        m = re.search(r"^%s\((\w+)::%s, x::Vector\{Float64\}\) =\n\s*_or_reference\(\(\) -> _device_\w+\(\1, x\), "
+                      r"%s,\n\s*Tuple\{%s,Vector\{<:Real\}\}, \1, x\)" % (name, t0, name, t0), src, re.M)
+        assert m, name
+    # refusals found on the host side take the same path instead of error(...)
+    assert "error(\"closure problems above 12 levels" not in src
+    assert src.count('throw(GrapeUnsupported("ndim > GRAPE_MAX_DENSE_DIM (64)"))') == 4
