@@ -357,24 +357,37 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     classes = tuple(sectors) if sectors else ((D, 1),)
     sec = classes[0][0] < D
     twins = tuple((info or {}).get("twin", ())) + (False,) * len(classes)
+    gauges = tuple((info or {}).get("gauge", ())) + (False,) * len(classes)
     per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
     # executed work: a twin class (grape_walk.hpp TWIN) runs ONE exponential per step for its two
     # sectors (the products and contractions stay per sector)
     per_step_exp = lambda f: sum((1 if twins[c] else ns) * f(S) for c, (S, ns) in enumerate(classes))  # noqa: E731
+    # the step propagator of a class: an S x S exponential (Pade-5 credit), or for a
+    # phase-covariant class (grape_walk.hpp GAUGE) E_k = D_k E~ D_k^dag formed from the lane's one
+    # exponential: two complex products per off-diagonal entry (12 FLOP each; the lane's own E~ is one
+    # exponential per chunk of L steps and not counted)
+    gform = lambda S: 12 * (S * S - S)  # noqa: E731
+    prop = lambda c, S: gform(S) if gauges[c] else flops_expm(S)  # noqa: E731
+    # the eps-variant's contraction: Re tr(Y dE) (8 S^2), or from the level phases (22 FLOP per
+    # off-diagonal entry: f = rho_r + conj(rho_j) + rho_r conj(rho_j), E f, 2 FMA)
+    contr = lambda c, S: 22 * (S * S - S) if gauges[c] else 8 * S ** 2  # noqa: E731
     walk = ktimes.get("k_walk_grad", (0.0, 0))[1] > 0
     xbytes = L * 8 * (NT + 1)  # the x rows every per-step kernel streams
     if walk:
         # chunk walks (grape_walk.hpp), algorithmic work per device pass:
-        # k_walk_fwd: one nominal S x S exp per (step, sector) + the chain product Q <- E Q;
-        # k_walk_grad: one eps-variant exp per (step, sector), Y = X E^dagger, X <- E Y and the
+        # k_walk_fwd: one nominal S x S propagator per (step, sector) + the chain product Q <- E Q;
+        # k_walk_grad: one eps-variant propagator per (step, sector), Y = X E^dagger, X <- E Y and the
         # contraction Re tr(Y dE).  The 2-level classes recompute E in the gradient walk
         # (executed, not credited); the 4-level class stores E once (walk_store_e) and the
-        # gradient walk reads it back -- the only per-step HBM intermediate left
-        store = lambda S: S >= WALK_STORE_LEVELS  # noqa: E731
-        flop_model = {"k_walk_fwd": L * NT * (per_step_exp(flops_expm)
-                                              + sum((1 if twins[c] else ns) * 8 * S ** 3 for c, (S, ns) in enumerate(classes))),
-                      "k_walk_grad": L * NT * nvg * (per_step_exp(flops_expm)
-                                                     + per_step(lambda S: 2 * 8 * S ** 3 + 8 * S ** 2))}
+        # gradient walk reads it back -- the only per-step HBM intermediate left.  Phase-covariant
+        # classes form the nominal propagator in both walks and the eps-variant's difference from
+        # the level phases: no exponential per step (counted as executed)
+        store = lambda S: S >= WALK_STORE_LEVELS and not any(gauges)  # noqa: E731
+        nE = lambda c, ns: 1 if twins[c] else ns  # noqa: E731
+        flop_model = {"k_walk_fwd": L * NT * sum(nE(c, ns) * (prop(c, S) + 8 * S ** 3)
+                                                 for c, (S, ns) in enumerate(classes)),
+                      "k_walk_grad": L * NT * nvg * sum(nE(c, ns) * prop(c, S) + ns * (2 * 8 * S ** 3 + contr(c, S))
+                                                        for c, (S, ns) in enumerate(classes))}
         byte_model = {"k_walk_fwd": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0),
                       "k_walk_grad": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0)}
     else:
@@ -435,7 +448,8 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                    "sectors": [{"levels": S, "sectors": ns, "stored_propagators": bool(walk and store(S)),
                                 "twin": bool(twins[c])}
                                for c, (S, ns) in enumerate(classes)] if sec else None,
-                   "symmetry_adapted": bool((info or {}).get("symmetric", False))},
+                   "symmetry_adapted": bool((info or {}).get("symmetric", False)),
+                   "phase_covariant": [bool(g) for g in gauges[:len(classes)]]},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
         "kernels_ms_per_pass": per_pass,
@@ -444,8 +458,8 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     # (nominal + one eps-variant exp per step per sector, chain + contraction products; with
     # sectors also the head's d x d products), and the survey's canonical whole-matrix C2 figure
     # (which also counts the x_add-variant exps, zero differences, this engine skips)
-    exe = NT * (per_step_exp(lambda S: (1 + nvg) * flops_expm(S) + 8 * S ** 3)
-                + per_step(lambda S: 2 * 8 * S ** 3 + nvg * 8 * S ** 2))
+    exe = NT * sum((1 if twins[c] else ns) * ((1 + nvg) * prop(c, S) + 8 * S ** 3)
+                   + ns * (2 * 8 * S ** 3 + nvg * contr(c, S)) for c, (S, ns) in enumerate(classes))
     if sec:
         exe += 16 * 8 * D ** 3
     canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)

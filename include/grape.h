@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 8
+#define GRAPE_ABI_VERSION 9
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -191,6 +191,12 @@ typedef struct grape_desc {
 /* Accepted and ignored since round 5: captured small calls no longer fork the second sector class
    (the experimental captured fork was removed).  Kept so that old callers still build. */
 #define GRAPE_OPT_GRAPH_FORK 4096
+/* Phase-covariant walk classes (ABI 9): when the one control enters every sector block as a phase,
+ * H(x) = D(a x) H(0) D(a x)^dag with D(t) = diag(e^{i t N_j}) -- the laser phase of the Rydberg models
+ * (RydbergTools.jl:31-130) -- the chunk walks form E_k = D_k exp(-i dt H(0)) D_k^dag and the
+ * eps-variant's difference from the level phases: one exponential per walk lane instead of one per
+ * step and variant.  This option keeps the per-step exponentials. */
+#define GRAPE_OPT_NO_GAUGE 8192
 
 typedef struct grape_plan grape_plan;
 
@@ -460,6 +466,9 @@ int grape_plan_sectors(grape_plan *plan, int *sector_dims, int *nsectors, int ma
  * exponential per step (GRAPE_OPT_NO_TWIN), symmetric (optional) = 1 when the sectors are the
  * symmetry-adapted ones (GRAPE_OPT_NO_SYMMETRY).  Returns the number of classes. */
 int grape_plan_sector_info(grape_plan *plan, int *twin, int *symmetric, int max_classes);
+/* Which sector classes run the phase-covariant walks (ABI 9; GRAPE_OPT_NO_GAUGE): gauge[c] = 1 per
+ * class; returns the number of classes (1 for whole matrices, gauge[0] = 0). */
+int grape_plan_gauge_info(grape_plan *plan, int *gauge, int max_classes);
 
 /*
  * Symmetry-adapted basis (ABI 8, host only: no device needed).  The unitary V (ndim x ndim,

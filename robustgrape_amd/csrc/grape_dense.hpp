@@ -255,8 +255,42 @@ __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &
 // of 4; rounding-level differences only (the dense parity tests hold at T0).  Measured at C5:
 // 940 -> 1 064 evals/s, k_dgrad 0.52 -> 0.58 of the FP64 peak credited with the algorithmic
 // 8 d^3 per complex product (executed: 6 d^3).
+#ifndef GRAPE_DENSE_4M
+#define GRAPE_DENSE_4M 0
+#endif
 template <bool LT, bool LC, bool RT, bool RC>
 __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
+    if constexpr (GRAPE_DENSE_4M) {
+        // the conventional four real products: re += Lr Rr - Li Ri, im += Lr Ri + Li Rr
+        Frag fc, fn;
+        v4d tr[2], ti[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) tr[i] = ti[i] = v4d{0.0, 0.0, 0.0, 0.0};
+        mm_load<LT, RT, RC>(L, R, 0, fc, ln);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            if (s < 15) mm_load<LT, RT, RC>(L, R, s + 1, fn, ln);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double ai = LC ? -fc.aI[i] : fc.aI[i];
+                tr[i] = mfma(fc.aR[i], fc.bR, tr[i]);
+                tr[i] = mfma(-ai, fc.bI, tr[i]);
+                ti[i] = mfma(fc.aR[i], fc.bI, ti[i]);
+                ti[i] = mfma(ai, fc.bR, ti[i]);
+            }
+            if (s < 15) {
+                fc = fn;
+                asm volatile("" : "+v"(fc.aR[0]), "+v"(fc.aR[1]), "+v"(fc.aI[0]), "+v"(fc.aI[1]), "+v"(fc.bR),
+                             "+v"(fc.bI)::"memory");
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            P.re[i] += tr[i];
+            P.im[i] += ti[i];
+        }
+        return;
+    }
     // Gauss's three-multiplication complex product: T1 = Lr Rr, T2 = Li Ri, T3 = (Lr + Li)(Rr + Ri),
     // P += (T1 - T2) + i (T3 - T1 - T2): 3 MFMAs per tile and k-step instead of 4.
     Frag fc, fn;

@@ -181,7 +181,7 @@ struct grape_plan {
     struct SecBuf {
         cd *E = nullptr, *Q = nullptr, *Mc = nullptr, *Carry = nullptr, *Ub = nullptr, *slots = nullptr,
            *ops = nullptr, *opsT = nullptr, *Msec = nullptr, *Tc = nullptr, *wscr = nullptr, *Ew = nullptr;
-        int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr;
+        int *ovf = nullptr, *ovf2 = nullptr, *sidx = nullptr, *gauge_n = nullptr;
         double *part = nullptr;
         // error sources: local-frame images, per-chunk triples, Tot / M_e blocks, F_d2err_dx terms
         cd *Zl = nullptr, *Me = nullptr, *TotS = nullptr, *MsecE = nullptr, *Wc = nullptr;
@@ -276,7 +276,7 @@ static void free_plan(grape_plan *p) {
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
         void *sbufs[] = {c.E, c.Q, c.Mc, c.Carry, c.Ub, c.slots, c.ops, c.opsT, c.Msec, c.ovf, c.ovf2, c.sidx, c.part,
-                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr, c.Ew, c.Wc};
+                         c.Zl, c.Me, c.TotS, c.MsecE, c.part_err, c.Tc, c.wscr, c.Ew, c.Wc, c.gauge_n};
         for (void *b : sbufs)
             if (b) (void)hipFree(b);
     }
@@ -557,6 +557,122 @@ static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
     ss.cls = best;
     ss.fixed = fixed;
     return ss;
+}
+
+// Phase covariance of a sector class (grape_walk.hpp GAUGE): does every sector block obey
+// H_w(x) = D(a x) H_w(0) D(a x)^dag, D(t) = diag(e^{i t N_j}), for the one control x?  Needs np = 1,
+// no error sources, H0 free of x_add and of the step index, and every term that reads x a
+// cos / sin / cis of a x + b with one common a.  The charges come from the ratios of the blocks'
+// entries at a small x to their values at x = 0 (N_j - N_k = n_jk, integer), propagated over each
+// sector's coupling graph; the identity is then checked entry by entry at seven x values (a
+// rotated basis -- the symmetry-adapted sectors -- is covered: the blocks are the rotated ones).
+// On success N holds [nsec][S] charges >= 0 (0 on padding slots) and a the common factor.
+static std::complex<double> host_coef(const grape_term &t, double x) {
+    const double v = t.var == 1 ? x : 1.0;
+    const double arg = t.a * v + t.b;
+    std::complex<double> f(1.0, 0.0);
+    if (t.func == 1) f = arg;
+    else if (t.func == 2) f = std::cos(arg);
+    else if (t.func == 3) f = std::sin(arg);
+    else if (t.func == 4) f = std::complex<double>(std::cos(arg), std::sin(arg));
+    return std::complex<double>(t.scale_re, t.scale_im) * f;
+}
+static bool find_gauge(const grape_desc *desc, const grape_desc &sdesc, const SectorClass &sc, double &a,
+                       std::vector<int> &N) {
+    constexpr int kMaxCharge = 8;
+    const int D = desc->ndim, S = sc.S;
+    const size_t T = (size_t)D * D;
+    if (desc->nparam != 1 || desc->nerr != 0) return false;
+    bool have_a = false;
+    a = 1.0;
+    for (int t = 0; t < desc->n_h0_terms; ++t) {
+        const grape_term &tm = desc->h0_terms[t];
+        if (tm.var == 2 || tm.var == 3) return false;  // x_add or the step index
+        if (tm.var != 1) continue;
+        if (tm.func != 2 && tm.func != 3 && tm.func != 4) return false;  // x must enter as a phase
+        if (!(tm.a != 0.0) || (have_a && tm.a != a)) return false;
+        a = tm.a;
+        have_a = true;
+    }
+    auto block = [&](int w, double x, std::vector<std::complex<double>> &H) {
+        H.assign((size_t)S * S, 0.0);
+        for (int t = 0; t < desc->n_h0_terms; ++t) {
+            const grape_term &tm = desc->h0_terms[t];
+            const std::complex<double> c = host_coef(tm, x);
+            for (int r = 0; r < S; ++r)
+                for (int q = 0; q < S; ++q) {
+                    const int gi = sc.sidx[(size_t)w * S + r], gj = sc.sidx[(size_t)w * S + q];
+                    if (gi < 0 || gj < 0) continue;
+                    const double *v = sdesc.ops + 2 * ((size_t)tm.op * T + gi + (size_t)gj * D);
+                    H[(size_t)r * S + q] += c * std::complex<double>(v[0], v[1]);
+                }
+        }
+    };
+    N.assign((size_t)sc.nsec * S, 0);
+    const double xs = 0.01 / std::fabs(a);
+    const double probe[7] = {0.37, -1.3, 2.9, 7.77, -31.4, 0.001, 123.456};
+    std::vector<std::complex<double>> H0, Hs, Hx;
+    for (int w = 0; w < sc.nsec; ++w) {
+        block(w, 0.0, H0);
+        block(w, xs, Hs);
+        double hmax = 0.0;
+        for (const auto &h : H0) hmax = std::max(hmax, std::abs(h));
+        for (const auto &h : Hs) hmax = std::max(hmax, std::abs(h));
+        const double tol = 1e-13 * std::max(hmax, 1e-300);
+        std::vector<int> n((size_t)S * S, 0);
+        for (int r = 0; r < S; ++r)
+            for (int q = 0; q < S; ++q) {
+                const std::complex<double> h0 = H0[(size_t)r * S + q], h1 = Hs[(size_t)r * S + q];
+                if (std::abs(h0) <= tol) {
+                    if (std::abs(h1) > tol) return false;  // vanishes at x = 0 only: not a phase
+                    continue;
+                }
+                const double m = std::arg(h1 / h0) / (a * xs);
+                const int nn = (int)std::lround(m);
+                if (std::fabs(m - nn) > 1e-6 || std::abs(nn) > kMaxCharge || (r == q && nn != 0)) return false;
+                n[(size_t)r * S + q] = nn;
+            }
+        std::vector<int> Nw(S, 0);  // charges by breadth-first search over the couplings
+        std::vector<char> seen(S, 0);
+        for (int s0 = 0; s0 < S; ++s0) {
+            if (seen[s0]) continue;
+            seen[s0] = 1;
+            std::vector<int> stack{s0};
+            while (!stack.empty()) {
+                const int r = stack.back();
+                stack.pop_back();
+                for (int q = 0; q < S; ++q) {
+                    if (std::abs(H0[(size_t)r * S + q]) <= tol) continue;
+                    const int want = Nw[r] - n[(size_t)r * S + q];  // n_rq = N_r - N_q
+                    if (!seen[q]) {
+                        seen[q] = 1;
+                        Nw[q] = want;
+                        stack.push_back(q);
+                    } else if (Nw[q] != want) {
+                        return false;
+                    }
+                }
+            }
+        }
+        const int lo = *std::min_element(Nw.begin(), Nw.end());
+        for (int r = 0; r < S; ++r) {
+            Nw[r] -= lo;
+            if (Nw[r] > kMaxCharge) return false;
+            N[(size_t)w * S + r] = Nw[r];
+        }
+        for (double x : probe) {  // the identity itself, entry by entry
+            block(w, x, Hx);
+            double hm = hmax;
+            for (const auto &h : Hx) hm = std::max(hm, std::abs(h));
+            for (int r = 0; r < S; ++r)
+                for (int q = 0; q < S; ++q) {
+                    const std::complex<double> ph = std::polar(1.0, a * x * (Nw[r] - Nw[q]));
+                    if (std::abs(Hx[(size_t)r * S + q] - ph * H0[(size_t)r * S + q]) > 1e-12 * std::max(hm, 1e-300))
+                        return false;
+                }
+        }
+    }
+    return true;
 }
 
 // Symmetry-adapted sectors (grape_symmetry.hpp): the sector path's view of the problem in the basis
@@ -1221,8 +1337,23 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // the forward walk hands its propagators to the gradient walk (HBM, lane-minor) where the
             // exponential is the expensive part: the 4-level class (grape_walk.hpp; measured C2 6.04 ->
             // 6.52 M evals/s; for the 2-level class it lost, 0.72 -> 1.01 ms per pass)
-            Ps.walk_store_e =
-                Ps.walk && P.ne == 0 && S >= grape::kWalkStoreMinD && !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
+            // phase-covariant classes (grape_walk.hpp GAUGE): one exponential per walk lane
+            std::vector<int> gauge_n;
+            double gauge_a = 1.0;
+            Ps.gauge = (Ps.walk && P.ne == 0 && !(P.opts & GRAPE_OPT_NO_GAUGE) &&
+                        find_gauge(desc, sdesc, sc, gauge_a, gauge_n)) ? 1 : 0;
+            Ps.gauge_a = gauge_a;
+            Ps.gauge_n = nullptr;
+            if (Ps.gauge) {
+                int *gn = nullptr;
+                if (dalloc(&gn, gauge_n.size()) != hipSuccess) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (gauge)"));
+                p->sb[cl].gauge_n = gn;
+                if (hipMemcpy(gn, gauge_n.data(), gauge_n.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+                    return bail(fail(GRAPE_ERR_HIP, "upload failed (gauge)"));
+                Ps.gauge_n = gn;
+            }
+            Ps.walk_store_e = Ps.walk && !Ps.gauge && P.ne == 0 && S >= grape::kWalkStoreMinD &&
+                              !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
             // latency-bound walk classes (fewer sub-evaluations than CUs, or the option): 16-wave scans,
             // half-length walks (grape_launch.hpp kScanLatency)
             if (Ps.walk && P.ne == 0 &&
@@ -1326,6 +1457,14 @@ int grape_plan_sector_info(grape_plan *p, int *twin, int *symmetric, int max_cla
     for (int c = 0; c < n && c < max_classes; ++c)
         if (twin) twin[c] = p->ncls ? p->Ps[c].twin : 0;
     if (symmetric) *symmetric = p->symmetry ? 1 : 0;
+    return n;
+}
+
+int grape_plan_gauge_info(grape_plan *p, int *gauge, int max_classes) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    const int n = p->ncls > 0 ? p->ncls : 1;
+    for (int c = 0; c < n && c < max_classes; ++c)
+        if (gauge) gauge[c] = p->ncls ? p->Ps[c].gauge : 0;
     return n;
 }
 

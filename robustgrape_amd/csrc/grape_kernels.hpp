@@ -95,6 +95,14 @@ struct DevProblem {
     int twin;            // ... two sectors with identical operator blocks (grape_walk.hpp TWIN): one
                          //     exponential per step serves both
     int opts;            // grape_desc.reserved[1]: GRAPE_OPT_* (fixed at plan creation)
+    // Phase-covariant walk class (grape_walk.hpp GAUGE, round 5): every sector w of the class obeys
+    // H_w(x) = D(a x) H_w(0) D(a x)^dag with D(t) = diag(e^{i t N_j}) for the one control x (np = 1,
+    // H0 free of x_add and of the step index), so E_k = D_k E~ D_k^dag with E~ = exp(-i dt H_w(0))
+    // and the eps-variant is E' = D'_k E~ D'_k^dag: one exponential per lane instead of one per step
+    // and variant.  gauge_n: [nsec][D] the integer charges N_j >= 0 (engine: find_gauge).
+    int gauge;
+    double gauge_a;
+    const int *gauge_n;
 };
 
 struct DevBatch {

@@ -739,6 +739,15 @@ constexpr bool kWalkPresum = GRAPE_WALK_PRESUM;
 #ifndef GRAPE_WALK_G3S_WAVES  // k_walk_grad<3, 1> with stored propagators
 #define GRAPE_WALK_G3S_WAVES 1
 #endif
+#ifndef GRAPE_WALK_GAUGE2_WAVES
+#define GRAPE_WALK_GAUGE2_WAVES 4
+#endif
+#ifndef GRAPE_WALK_GAUGE3_WAVES
+#define GRAPE_WALK_GAUGE3_WAVES 3
+#endif
+#ifndef GRAPE_WALK_GAUGE4_WAVES
+#define GRAPE_WALK_GAUGE4_WAVES 2
+#endif
 template <int D, int NS>
 struct WalkCfg {
     static constexpr bool FENCE = D >= 4;        // per-column scheduling fences (register discipline)
@@ -765,6 +774,9 @@ struct WalkCfg {
     // Taylor-12 columns dominate; the smaller classes (Taylor 6 at C2) measured slower with its
     // bookkeeping (k_walk_fwd<2,2> 0.295 -> 0.34 ms per pass) and keep the unshifted walk bitwise
     static constexpr bool SHIFT = D >= GRAPE_WALK_SHIFT_MIN_D;
+    // phase-covariant classes (GAUGE): E~, E and the walk state only -- no exponential per step
+    static constexpr int WAVES_GAUGE = D <= 2 ? GRAPE_WALK_GAUGE2_WAVES : D == 3 ? GRAPE_WALK_GAUGE3_WAVES
+                                                                         : GRAPE_WALK_GAUGE4_WAVES;
 };
 
 // The chunk's phase: sum of the steps' diagonal shifts (sm_regime), TwoSum-compensated; the chunk
@@ -794,14 +806,109 @@ __device__ __forceinline__ void walk_phase(const WalkPhase &ph, cd (&Q)[D][D]) {
 template <int D>
 constexpr int kEwStride = D * D + 1;
 
+// ---------------------------------------------------------------------------
+// Phase-covariant classes (P.gauge, round 5): E_k = D_k E~ D_k^dag
+// ---------------------------------------------------------------------------
+// A control that enters H only as a phase -- the laser phase phi of the Rydberg models
+// (RydbergTools.jl:31-130: e^{-i phi} Omega / 2 on every |1> -> |r> coupling) -- obeys
+// H(x) = D(a x) H(0) D(a x)^dag, D(t) = diag(e^{i t N_j}) with integer charges N_j (the Rydberg
+// excitation number).  The engine checks this per sector at plan creation (find_gauge: every entry
+// of every sector block is e^{i a x (N_j - N_k)} times its value at x = 0).  Then
+//   E_k = exp(-i dt H(x_k)) = D_k E~ D_k^dag,   E~ = exp(-i dt H(0))    (exactly, for any x_k)
+// and the eps-variant of the step is E'_k = D'_k E~ D'_k^dag with D'_k = D_k diag(e^{i phi N_j}),
+// phi = a ((x_k + eps) - x_k).  So a lane computes ONE exponential (E~, at its start) instead of
+// one per step and variant; per step it forms E_k from E~ and the D phases of its levels, and
+//   (E'_k - E_k)_rj = E_rj (rho_r + conj(rho_j) + rho_r conj(rho_j)),   1 + rho_j = e^{i phi N_j},
+// with rho computed without cancellation (gauge_rho), so the reference's forward difference
+// (UnitaryCalculations.jl:48-56) is formed from the exact perturbed propagator: same quantity, less
+// rounding noise than two separate exponentials.  The charges are wave-uniform (one sector per
+// workgroup row: scalar loads), so the per-level powers below are scalar-uniform loops.
+template <int D>
+struct GaugeN {
+    int n[D];
+};
+template <int D>
+__device__ __forceinline__ GaugeN<D> gauge_charges(const DevProblem &P, int w) {
+    const cptr<int> g = as_constant(P.gauge_n) + (size_t)w * D;
+    GaugeN<D> r;
+#pragma unroll
+    for (int j = 0; j < D; ++j) r.n[j] = g[j];
+    return r;
+}
+// z^n for a small wave-uniform n >= 0 (n - 1 complex products; exact 1 for n = 0)
+__device__ __forceinline__ cd gauge_pow(cd z, int n) {
+    cd r = cmake(1.0, 0.0);
+    if (n > 0) r = z;
+#pragma unroll 1
+    for (int m = 1; m < n; ++m) r = cmul(r, z);
+    return r;
+}
+// e^{i phi} - 1 without cancellation: (-2 sin^2(phi / 2), sin phi); Taylor for the FD-sized
+// phases (|phi| <= 0.05: truncation below 1e-22 relative), the library otherwise
+__device__ __forceinline__ cd cis_m1(double phi) {
+    if (fabs(phi) <= 0.05) {
+        const double p2 = phi * phi, h = 0.5 * phi, h2 = h * h;
+        const double s = phi * (1.0 - p2 / 6.0 * (1.0 - p2 / 20.0 * (1.0 - p2 / 42.0 * (1.0 - p2 / 72.0))));
+        const double sh = h * (1.0 - h2 / 6.0 * (1.0 - h2 / 20.0 * (1.0 - h2 / 42.0 * (1.0 - h2 / 72.0))));
+        return cmake(-2.0 * sh * sh, s);
+    }
+    const double sh = sin(0.5 * phi);
+    return cmake(-2.0 * sh * sh, sin(phi));
+}
+// rho = (1 + q)^n - 1 by rho <- rho + q + q rho (no cancellation), n wave-uniform
+__device__ __forceinline__ cd gauge_rho(cd q, int n) {
+    cd r = czero();
+#pragma unroll 1
+    for (int m = 0; m < n; ++m) r = cadd(cadd(r, q), cmul(q, r));
+    return r;
+}
+// E~ = exp(-i dt H_w(0)) of the lane's NE sectors (the nominal build at x = 0; no diagonal shift, so
+// E~ carries its own phase), into Et -- the same bits in the forward and the gradient walk
+template <int D, int NE, bool FENCE>
+__device__ __forceinline__ void gauge_base(const DevProblem &P, cptr<cd> ops, cd *scr, cd (&Et)[NE][D][D]) {
+    WalkX X0;
+    X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
+    Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    SM<D> A[NE];
+    walk_build<D, NE>(P, ops, X0, 1, none, A);
+#pragma unroll
+    for (int w = 0; w < NE; ++w) {
+        double mu0 = 0.0;
+        walk_expm<D, FENCE, true, false>(A[w], scr + (size_t)w * 2 * D * D, mu0, true, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) Et[w][j][i] = x[j];
+        });
+    }
+}
+// the level phases d_j = e^{i theta N_j} of one sector from p = e^{i theta}
+template <int D>
+__device__ __forceinline__ void gauge_phases(cd p, const GaugeN<D> &g, cd (&d)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) d[j] = gauge_pow(p, g.n[j]);
+}
+// E_jk = d_j E~_jk conj(d_k); the diagonal is E~'s own (d_j conj(d_j) = 1 exactly)
+template <int D, class Store>
+__device__ __forceinline__ void gauge_prop(const cd (&Et)[D][D], const cd (&d)[D], Store &E) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) E.set(j, k, j == k ? Et[j][k] : cmul(cmul(d[j], Et[j][k]), cconj(d[k])));
+    }
+}
+
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
 // TWIN (P.twin, NS = 2): the lane's two sectors have identical operator blocks (e.g. the Rydberg
 // sectors {01, 0r} and {10, r0} at equal Rabi frequencies and detunings): their propagators, chains
 // and chunk totals are identical, so one exponential and one chain per step serve both.
-template <int D, int NS, bool STORE, bool TWIN = false>
+// GAUGE: a phase-covariant class (P.gauge): E_k = D_k E~ D_k^dag from the lane's one exponential E~
+template <int D, int NS, bool STORE, bool TWIN = false, bool GAUGE = false>
 __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
     using C = WalkCfg<D, NS>;
     static_assert(!TWIN || (NS == 2 && !STORE), "twin sectors: two per lane, recomputed propagators");
+    static_assert(!(GAUGE && STORE), "gauge classes form E_k from E~: nothing to store");
     constexpr int NE = TWIN ? 1 : NS;  // distinct propagators / chains per lane
     constexpr int TS = D * D;
     const WalkLane L = walk_lane<NS>(P, B, vb);
@@ -834,22 +941,43 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
             for (int i = 0; i < D; ++i) Q[w][j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
         }
     }
+    cd Et[GAUGE ? NE : 1][D][D];  // GAUGE: E~ of the lane's sectors
+    GaugeN<D> gn[GAUGE ? NE : 1];
+    if constexpr (GAUGE) {
+        gauge_base<D, NE, C::FENCE_FWD>(P, ops, scr, Et);
+#pragma unroll
+        for (int w = 0; w < NE; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
+    }
+    constexpr bool SHIFT = C::SHIFT && !GAUGE;
 #pragma unroll 1
     for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t leave Q alone
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = k0 + jj < P.Nt;
         walk_set_xk(X, xn);
         xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * xs, xs);  // next step's controls
-        SM<D> A[NE];
-        walk_build<D, NE>(P, ops, X, k + 1, none, A);
+        SM<D> A[GAUGE ? 1 : NE];
+        cd p1 = czero();
+        if constexpr (GAUGE) {
+            double sn, cn;
+            sincos(P.gauge_a * X.k0, &sn, &cn);  // e^{i a x_k}
+            p1 = cmake(cn, sn);
+        } else {
+            walk_build<D, NE>(P, ops, X, k + 1, none, A);
+        }
 #pragma unroll
         for (int w = 0; w < NE; ++w) {
-            double mu;
-            walk_expm<D, C::FENCE_FWD, true, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu, true, [&](int i, const cd (&x)[D]) {
+            double mu = 0.0;
+            if constexpr (GAUGE) {
+                cd dph[D];
+                gauge_phases<D>(p1, gn[w], dph);
+                gauge_prop<D>(Et[w], dph, E);
+            } else {
+                walk_expm<D, C::FENCE_FWD, true, C::SHIFT>(A[w], scr + (size_t)w * 2 * TS, mu, true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
-                for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
-            });
-            if constexpr (C::SHIFT) ph[w].add(act ? mu : 0.0);
+                    for (int j = 0; j < D; ++j) E.set(j, i, x[j]);
+                });
+            }
+            if constexpr (SHIFT) ph[w].add(act ? mu : 0.0);
             if constexpr (STORE) {  // the gradient walk's copy: lane-minor, one coalesced 1-KB store per element
                 cd *ew = B.Ew + ((((size_t)vb.y * P.L + jj) * NS + w) * kEwStride<D>) * lanes + lane;
 #pragma unroll
@@ -878,7 +1006,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         }
     }
     if (L.ok) {
-        if constexpr (C::SHIFT) {
+        if constexpr (SHIFT) {
 #pragma unroll
             for (int w = 0; w < NE; ++w) walk_phase<D>(ph[w], Q[w]);
         }
@@ -895,9 +1023,10 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     }
 }
 
-template <int D, int NS, bool STORE, bool TWIN = false>
-__global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_walk_fwd(DevProblem P, DevBatch B) {
-    walk_fwd_body<D, NS, STORE, TWIN>(P, B, hw_block());
+template <int D, int NS, bool STORE, bool TWIN = false, bool GAUGE = false>
+__global__ __launch_bounds__(kWalkBlock, (GAUGE ? WalkCfg<D, NS>::WAVES_GAUGE : WalkCfg<D, NS>::WAVES_FWD))
+void k_walk_fwd(DevProblem P, DevBatch B) {
+    walk_fwd_body<D, NS, STORE, TWIN, GAUGE>(P, B, hw_block());
 }
 
 // STORED: the nominal propagators come from the forward walk's copy (B.Ew, prefetched one step
@@ -907,10 +1036,13 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_FWD)) void k_wal
 // (a runtime loop) -- a static count of the F_dx stores per step keeps the prefetch waits exact.
 // TWIN: one nominal and one eps-variant exponential per step serve both sectors of the lane (their
 // X, Y and contractions stay per sector: M differs between them in general)
-template <int D, int NS, bool STORED, int NVG, bool TWIN = false>
+// GAUGE: a phase-covariant class (P.gauge; NVG == 1): E_k from E~ and the level phases, and the
+// eps-variant's difference E' - E = E o f with f_rj = rho_r + conj(rho_j) + rho_r conj(rho_j)
+template <int D, int NS, bool STORED, int NVG, bool TWIN = false, bool GAUGE = false>
 __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBatch &B, const VBlock vb) {
     using C = WalkCfg<D, NS>;
     static_assert(!TWIN || (NS == 2 && !STORED), "twin sectors: two per lane, recomputed propagators");
+    static_assert(!GAUGE || (!STORED && NVG == 1), "gauge classes: recomputed propagators, one control");
     constexpr int NE = TWIN ? 1 : NS;     // distinct propagators per lane
     constexpr int NSH = TWIN ? NS : 1;    // sectors sharing each of them
     constexpr int TS = D * D;
@@ -980,13 +1112,35 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     const int k0 = L.c * P.L;
     X2 xn = walk_load_x(P.np, xt + (size_t)min(k0, P.Nt - 1) * P.np * xs, xs);
     const cptr<VSpec> vs = as_constant(P.vs);
+    cd Et[GAUGE ? NE : 1][D][D];  // GAUGE: E~ of the lane's sectors (the forward walk's bits)
+    GaugeN<D> gn[GAUGE ? NE : 1];
+    cd rho[GAUGE ? NE : 1][D];    // GAUGE: e^{i phi N_j} - 1 of this step
+    if constexpr (GAUGE) {
+        gauge_base<D, NE, C::FENCE>(P, ops, scr, Et);
+#pragma unroll
+        for (int w = 0; w < NE; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
+    }
 #pragma unroll 1
     for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store nothing
         const int k = min(k0 + jj, P.Nt - 1);
         const bool act = L.ok && k0 + jj < P.Nt;
         walk_set_xk(XV, xn);
         xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * xs, xs);  // next step's controls
-        if constexpr (STORED) {  // this step's propagators; the next step's loads go out now
+        if constexpr (GAUGE) {
+            const double xk = XV.k0, xe = xk + P.eps;  // the reference's perturbed control (Pert delta = eps)
+            double sn, cn;
+            sincos(P.gauge_a * xk, &sn, &cn);
+            const cd p1 = cmake(cn, sn), q = cis_m1(P.gauge_a * (xe - xk));  // (xe - xk: exact)
+#pragma unroll
+            for (int w = 0; w < NE; ++w) {
+                cd dph[D];
+                gauge_phases<D>(p1, gn[w], dph);
+                gauge_prop<D>(Et[w], dph, E[w]);
+                mu[w] = 0.0;
+#pragma unroll
+                for (int j = 0; j < D; ++j) rho[w][j] = gauge_rho(q, gn[w].n[j]);
+            }
+        } else if constexpr (STORED) {  // this step's propagators; the next step's loads go out now
 #pragma unroll
             for (int w = 0; w < NS; ++w) {
 #pragma unroll
@@ -1037,9 +1191,51 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
                 for (int cc = 0; cc < D; ++cc) X[w].set(r, cc, y[cc]);
             }
         }
+        if constexpr (GAUGE) {  // F_dx[k] = Re tr(Y (E' - E)) / eps with (E' - E)_rj = E_rj f_rj (f_jj = 0)
+            double tot = 0.0;
+#pragma unroll
+            for (int we = 0; we < NE; ++we) {
+                double s[NSH];
+#pragma unroll
+                for (int t = 0; t < NSH; ++t) s[t] = 0.0;
+                const auto &Ej = E[we].opaque();
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        if (r == j) continue;
+                        const cd rj = cconj(rho[we][j]);
+                        const cd f = cadd(cadd(rho[we][r], rj), cmul(rho[we][r], rj));
+                        const cd de = cscale(P.inv_eps, cmul(Ej.at(r, j), f));
+#pragma unroll
+                        for (int t = 0; t < NSH; ++t) {
+                            const cd y = X[we * NSH + t].opaque().at(j, r);
+                            s[t] = fma(y.re, de.re, s[t]);
+                            s[t] = fma(-y.im, de.im, s[t]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < NSH; ++t) {
+                    const int w = we * NSH + t;
+                    if constexpr (kWalkPresum && NS > 1) {
+                        tot += s[t];
+                    } else {
+                        double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg) * L.nbe + L.be
+                                          : reinterpret_cast<double *>(B.sink);
+                        *dst = s[t];
+                    }
+                }
+            }
+            if constexpr (kWalkPresum && NS > 1) {
+                double *dst = act ? B.sec_part + ((((size_t)(L.w0 / NS) * P.Nt) + k) * P.nvg) * L.nbe + L.be
+                                  : reinterpret_cast<double *>(B.sink);
+                *dst = tot;
+            }
+        }
         // eps-variants: F_dx[u, k] = Re tr(Y (E' - E)) / eps, column j of E' against row j of Y
 #pragma unroll 1
-        for (int u = 0; u < (NVG > 0 ? NVG : P.nvg); ++u) {
+        for (int u = 0; u < (GAUGE ? 0 : NVG > 0 ? NVG : P.nvg); ++u) {
             SM<D> Ap[NE];
             walk_build<D, NE>(P, ops, XV, k + 1, pload(vs, P.off_dx + u), Ap);
             double tot = 0.0;  // (kWalkPresum: the lane's sectors summed, in sector order)
@@ -1118,10 +1314,11 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     }
 }
 
-template <int D, int NS, bool STORED, int NVG, bool TWIN = false>
-__global__ __launch_bounds__(kWalkBlock, (STORED ? WalkCfg<D, NS>::WAVES_GRAD_STORED : WalkCfg<D, NS>::WAVES_GRAD))
+template <int D, int NS, bool STORED, int NVG, bool TWIN = false, bool GAUGE = false>
+__global__ __launch_bounds__(kWalkBlock, (GAUGE ? WalkCfg<D, NS>::WAVES_GAUGE
+                                                : STORED ? WalkCfg<D, NS>::WAVES_GRAD_STORED : WalkCfg<D, NS>::WAVES_GRAD))
 void k_walk_grad(DevProblem P, DevBatch B) {
-    walk_grad_body<D, NS, STORED, NVG, TWIN>(P, B, hw_block());
+    walk_grad_body<D, NS, STORED, NVG, TWIN, GAUGE>(P, B, hw_block());
 }
 
 // Pair kernels (latency-bound calls): two sector classes' walks in ONE launch -- the first
@@ -1129,19 +1326,20 @@ void k_walk_grad(DevProblem P, DevBatch B) {
 // -- so a single evaluation's classes run side by side instead of one launch after the other
 // (graph branches do not run concurrently on this runtime: scripts/probes/graph_branch_probe.hip).
 // The registers are the larger class's; at these sizes the grid is a few workgroups.
-template <int D0, int NS0, bool ST0, int D1, int NS1, bool TW1 = false>
+// GA: both classes phase-covariant (P.gauge; then class 0 stores nothing)
+template <int D0, int NS0, bool ST0, int D1, int NS1, bool TW1 = false, bool GA = false>
 __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_fwd_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1,
                                                                  int gx0, int gy0, int gx1) {
     const int id = blockIdx.x, n0 = gx0 * gy0;
-    if (id < n0) walk_fwd_body<D0, NS0, ST0>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
-    else walk_fwd_body<D1, NS1, false, TW1>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+    if (id < n0) walk_fwd_body<D0, NS0, ST0 && !GA, false, GA>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
+    else walk_fwd_body<D1, NS1, false, TW1, GA>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
 }
-template <int D0, int NS0, bool ST0, int D1, int NS1, bool TW1 = false>
+template <int D0, int NS0, bool ST0, int D1, int NS1, bool TW1 = false, bool GA = false>
 __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0, DevBatch B0, DevProblem P1, DevBatch B1,
                                                                   int gx0, int gy0, int gx1) {
     const int id = blockIdx.x, n0 = gx0 * gy0;
-    if (id < n0) walk_grad_body<D0, NS0, ST0, 1>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
-    else walk_grad_body<D1, NS1, false, 1, TW1>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+    if (id < n0) walk_grad_body<D0, NS0, ST0 && !GA, 1, false, GA>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
+    else walk_grad_body<D1, NS1, false, 1, TW1, GA>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
 }
 
 // ---------------------------------------------------------------------------

@@ -26,6 +26,18 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
         }
         return;
     }
+    if (P.gauge) {  // phase-covariant class: E_k = D_k E~ D_k^dag, one exponential per lane (grape_walk.hpp)
+        if constexpr (NS == 2) {
+            if (P.twin) {
+                if (stage == 0) hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, false, true, true>), grid, blk, 0, st, P, B);
+                else hipLaunchKernelGGL((grape::k_walk_grad<D, NS, false, 1, true, true>), grid, blk, 0, st, P, B);
+                return;
+            }
+        }
+        if (stage == 0) hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, false, false, true>), grid, blk, 0, st, P, B);
+        else hipLaunchKernelGGL((grape::k_walk_grad<D, NS, false, 1, false, true>), grid, blk, 0, st, P, B);
+        return;
+    }
     if constexpr (NS == 2) {  // twin sectors (P.twin): one exponential per step for both
         if (P.twin) {
             if (stage == 0) hipLaunchKernelGGL((grape::k_walk_fwd<D, NS, false, true>), grid, blk, 0, st, P, B);
@@ -84,10 +96,12 @@ int grad_parts(const grape::DevProblem &P) {
 
 // class 0: one sector of 4 levels with stored propagators (permutation sectors of the Rydberg model)
 // or of 3 levels (its symmetry-adapted sectors, grape_symmetry.hpp); class 1: two 2-level sectors
+// (phase-covariant: both classes gauge, class 0 storing nothing)
 bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1) {
-    const bool c0 = (P0.D == 4 || P0.D == 3) && (P0.walk_store_e != 0) == (P0.D >= grape::kWalkStoreMinD);
+    const bool c0 = (P0.D == 4 || P0.D == 3) &&
+                    (P0.walk_store_e != 0) == (!P0.gauge && P0.D >= grape::kWalkStoreMinD);
     return P0.walk && P1.walk && P0.ne == 0 && P0.nvg == 1 && c0 && P0.nsec == 1 && P1.D == 2 && P1.nsec == 2 &&
-           P1.nvg == 1 && !P1.walk_store_e;
+           P1.nvg == 1 && !P1.walk_store_e && (P0.gauge != 0) == (P1.gauge != 0);
 }
 hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevBatch &B0, const grape::DevProblem &P1,
                        const grape::DevBatch &B1, hipStream_t st) {
@@ -99,22 +113,26 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
     };
     const int gx0 = gx(P0, B0), gy0 = 1, gx1 = gx(P1, B1);  // class 0: one sector per lane; class 1: both per lane
     const dim3 grid((unsigned)(gx0 * gy0 + gx1)), blk(grape::kWalkBlock);
-    auto go = [&](auto d0, auto tw) {
+    auto go = [&](auto d0, auto tw, auto ga) {
         constexpr int D0 = decltype(d0)::value;
-        constexpr bool TW = decltype(tw)::value;
+        constexpr bool TW = decltype(tw)::value, GA = decltype(ga)::value;
         if (stage == 0)
-            hipLaunchKernelGGL((grape::k_walk_fwd_pair<D0, 1, (D0 >= grape::kWalkStoreMinD), 2, 2, TW>), grid, blk, 0, st,
-                               P0, B0, P1, B1, gx0, gy0, gx1);
+            hipLaunchKernelGGL((grape::k_walk_fwd_pair<D0, 1, (D0 >= grape::kWalkStoreMinD), 2, 2, TW, GA>), grid, blk, 0,
+                               st, P0, B0, P1, B1, gx0, gy0, gx1);
         else
-            hipLaunchKernelGGL((grape::k_walk_grad_pair<D0, 1, (D0 >= grape::kWalkStoreMinD), 2, 2, TW>), grid, blk, 0, st,
-                               P0, B0, P1, B1, gx0, gy0, gx1);
+            hipLaunchKernelGGL((grape::k_walk_grad_pair<D0, 1, (D0 >= grape::kWalkStoreMinD), 2, 2, TW, GA>), grid, blk, 0,
+                               st, P0, B0, P1, B1, gx0, gy0, gx1);
     };
     using I3 = std::integral_constant<int, 3>;
     using I4 = std::integral_constant<int, 4>;
     using T = std::true_type;
     using F = std::false_type;
-    if (P0.D == 4) P1.twin ? go(I4{}, T{}) : go(I4{}, F{});
-    else P1.twin ? go(I3{}, T{}) : go(I3{}, F{});
+    auto go2 = [&](auto ga) {
+        if (P0.D == 4) P1.twin ? go(I4{}, T{}, ga) : go(I4{}, F{}, ga);
+        else P1.twin ? go(I3{}, T{}, ga) : go(I3{}, F{}, ga);
+    };
+    if (P0.gauge) go2(T{});
+    else go2(F{});
     return hipGetLastError();
 }
 

@@ -243,7 +243,11 @@ class GrapePlan:
         t, sym = (ctypes.c_int * 2)(), ctypes.c_int(0)
         k = _capi.lib().grape_plan_sector_info(self.handle, t, ctypes.byref(sym), 2)
         _capi.check(min(k, 0))
-        return {"twin": tuple(bool(t[c]) for c in range(k)), "symmetric": bool(sym.value)}
+        g = (ctypes.c_int * 2)()
+        kg = _capi.lib().grape_plan_gauge_info(self.handle, g, 2)
+        _capi.check(min(kg, 0))
+        return {"twin": tuple(bool(t[c]) for c in range(k)), "symmetric": bool(sym.value),
+                "gauge": tuple(bool(g[c]) for c in range(kg))}
 
 
 # Plan cache of the reference-shaped entry points (one plan per problem object, nparam and

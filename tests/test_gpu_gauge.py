@@ -1,0 +1,135 @@
+"""Phase-covariant walk classes (csrc/grape_walk.hpp GAUGE, round 5).
+
+When the one control enters H only as a phase -- the laser phase of every Rydberg model of the
+reference (RydbergTools.jl:31-130) -- H(x) = D(a x) H(0) D(a x)^dag with D(t) = diag(e^{i t N_j}),
+so E_k = D_k exp(-i dt H(0)) D_k^dag exactly and the eps-variant E'_k = D'_k exp(-i dt H(0)) D'_k^dag.
+The walks then compute one exponential per lane instead of one per step and variant, and form the
+reference's forward difference (E' - E) / eps (UnitaryCalculations.jl:48-56) from the level phases.
+
+Checked here: which plans take it (grape_plan_gauge_info), and that its F / F_dx equal those of the
+per-step exponentials (GRAPE_OPT_NO_GAUGE) and the oracle -- F at T1; F_dx at the FD tier of the
+problem's step norms (tests/problems.py fd_tier): both sides are forward differences with eps = 1e-8,
+so they differ by the u / eps rounding noise of the per-step exponentials, the gauge side carrying
+almost none.  The golden C2 / C4 checks inside the bench-size plan (test_gpu_walk.py
+test_bench_size_plan_matches_goldens) run the gauge walks too: they are the default.
+"""
+import numpy as np
+import pytest
+
+from tests import problems as P
+
+pytestmark = pytest.mark.gpu
+T1 = 1e-12
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _plan(fp, max_batch, options=0, nparam=1):
+    from robustgrape_amd.engine import GrapePlan
+    return GrapePlan(fp, nparam=nparam, device=0, max_batch=max_batch, options=options)
+
+
+def _check(test, F, Fdx, F0, g0, tier):
+    from tests.parity_log import record
+    ef = float(np.max(np.abs(np.asarray(F) - np.asarray(F0))))
+    record(test, "F", ef, 1.0, T1)
+    assert ef <= T1, (test, ef)
+    err, scale = float(np.max(np.abs(Fdx - g0))), float(np.max(np.abs(g0)))
+    record(test, "F_dx", err, scale, tier[0] * scale + tier[1])
+    print(f"{test}: |dF| {ef:.2e} max|dF_dx| {err:.2e} (scale {scale:.2e}, rel {err / scale:.2e})")
+    assert err <= tier[0] * scale + tier[1], (test, err, scale)
+
+
+def test_which_plans_are_phase_covariant():
+    """Every Rydberg model with the phase as its control is; NO_GAUGE, two controls per step,
+    error sources and whole matrices are not."""
+    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_SECTORS, OPT_NO_SYMMETRY
+    cases = [(P.full9_problem(16), 0, 1, (True, True)), (P.full9_problem(16), OPT_NO_SYMMETRY, 1, (True, True)),
+             (P.sym_problem(16), 0, 1, (True,)), (P.fullblk_problem(16), 0, 1, (True,)),
+             (P.full9_problem(16), OPT_NO_GAUGE, 1, (False, False)),
+             (P.full9_problem(16, nerr=2), 0, 1, (False, False)),
+             (P.full9_problem(16), OPT_NO_SECTORS, 1, (False,))]
+    for fp, opts, nparam, want in cases:
+        pl = _plan(fp, 4, opts, nparam)
+        try:
+            assert pl.sector_info()["gauge"] == want, (opts, pl.sectors(), pl.sector_info())
+        finally:
+            pl.close()
+
+
+def test_two_controls_per_step_are_not_phase_covariant():
+    from tests.test_gpu_walk import _high_norm_problem
+    fp = _high_norm_problem(8)[0]  # phase and an amplitude control per step (np = 2)
+    pl = _plan(fp, 4, 0, 2)
+    try:
+        assert not any(pl.sector_info()["gauge"])
+    finally:
+        pl.close()
+
+
+@pytest.mark.parametrize("name,fp,opts", [
+    ("full9-sym", lambda: P.full9_problem(96), 0),
+    ("full9-perm", lambda: P.full9_problem(96), "perm"),
+    ("full9-one-step", lambda: P.full9_problem(1), 0),     # |dt H(0)|_1 ~ 76: E~ by Taylor 30 + squarings
+    ("full9-chunk-starts", lambda: P.full9_problem(3), 0),
+    ("full9-c1-label", lambda: P.full9_problem(256), 0),
+    ("sym5", lambda: P.sym_problem(40), 0),
+    ("fullblk7", lambda: P.fullblk_problem(40), 0),
+])
+@pytest.mark.parametrize("batch", [5, 300])
+def test_gauge_walks_match_per_step_exponentials_and_oracle(name, fp, opts, batch):
+    """Throughput (300: 8-wave scans) and latency-bound (5: 16-wave scans, pair kernels) plans,
+    and a single call (the graph path)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_SYMMETRY
+    f = fp()
+    nt = f.unitary_problem.ntimes
+    rng = np.random.default_rng(77 + nt)
+    X = np.stack([P.random_x(nt, 900 + s, small=(s % 2 == 0)) for s in range(batch)])
+    X[1, :nt] = rng.uniform(-40.0, 40.0, size=nt)  # large phases: argument reduction in the level phases
+    so = OPT_NO_SYMMETRY if opts == "perm" else 0
+    pg, pn = _plan(f, batch, so), _plan(f, batch, so | OPT_NO_GAUGE)
+    try:
+        assert all(pg.sector_info()["gauge"]) and not any(pn.sector_info()["gauge"])
+        out, ref = pg.fidelity_grad(X), pn.fidelity_grad(X)
+        one = pg.fidelity_grad(X[2:3])
+    finally:
+        pg.close()
+        pn.close()
+    assert one[0][0] == out[0][2] and np.array_equal(one[1][0], out[1][2])  # single call == batch row
+    for b in range(min(batch, 6)):
+        _check(f"gauge_vs_exp_{name}_{batch}_{b}", out[0][b], out[1][b], ref[0][b], ref[1][b], P.fd_tier(f, X[b]))
+    for b in (0, 1):
+        F0, g0 = O.calculate_fidelity_and_derivatives(f, X[b])[:2]
+        _check(f"gauge_vs_oracle_{name}_{batch}_{b}", out[0][b], out[1][b], F0, g0, P.fd_tier(f, X[b]))
+
+
+def test_gauge_bench_size_plan_against_c2_golden():
+    """The bench's configuration (32 768 per pass selects the same kernels as 2 048) with the C2
+    golden at scattered positions, and the whole batch against the per-step exponentials."""
+    import os
+    from robustgrape_amd.operators import OPT_NO_GAUGE
+    g2 = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2.npz"),
+                      allow_pickle=False))
+    n = 2048
+    X = np.stack([P.random_x(512, 5000 + s, small=True) for s in range(n)])
+    for p in (0, 777, n - 1):
+        X[p] = g2["x"]
+    pg, pn = _plan(P.full9_problem(512), n), _plan(P.full9_problem(512), n, OPT_NO_GAUGE)
+    try:
+        F, G, _, _ = pg.fidelity_grad(X)
+        Fn, Gn, _, _ = pn.fidelity_grad(X)
+    finally:
+        pg.close()
+        pn.close()
+    for p in (0, 777, n - 1):
+        _check(f"gauge_big_c2_at{p}", F[p], G[p], g2["F"], g2["F_dx"], (1e-7, 1e-9))
+    assert float(np.max(np.abs(F - Fn))) <= T1
+    err = np.max(np.abs(G - Gn), axis=1)
+    scale = np.max(np.abs(Gn), axis=1)
+    assert np.all(err <= 1e-7 * scale + 1e-9), float(np.max(err / scale))

@@ -243,7 +243,7 @@ def test_walk_propagator_modes_bitwise(name, fp):
     and recomputing them (GRAPE_OPT_WALK_RECOMPUTE) run the same exponential code on the same inputs:
     F and F_dx agree bit for bit.  (Permutation sectors: the stored propagators serve the 4-level
     class, which the symmetry-adapted C2 layout does not have.)"""
-    from robustgrape_amd.operators import OPT_NO_SYMMETRY, OPT_WALK_RECOMPUTE
+    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_SYMMETRY, OPT_WALK_RECOMPUTE
     f = fp()
     nparam = 2 if name == "full9-hot" else 1
     nt = f.unitary_problem.ntimes
@@ -252,8 +252,8 @@ def test_walk_propagator_modes_bitwise(name, fp):
     if name == "full9-hot":
         X[::7, 1::2][:, 5] = 700.0  # one high-norm step in every 7th row (the squaring path)
     outs = []
-    for opts in (0, OPT_WALK_RECOMPUTE):
-        pl = _plan(f, 300, opts | OPT_NO_SYMMETRY, nparam=nparam)
+    for opts in (0, OPT_WALK_RECOMPUTE):  # (per-step exponentials: the phase-covariant walks store nothing)
+        pl = _plan(f, 300, opts | OPT_NO_SYMMETRY | OPT_NO_GAUGE, nparam=nparam)
         try:
             outs.append(pl.fidelity_grad(X)[:2])
         finally:
@@ -290,16 +290,19 @@ def test_diagonal_head_matches_general_head(name, fp):
             assert float(np.max(np.abs(a - b))) <= 1e-12 * scale + 1e-15, (name, float(np.max(np.abs(a - b))), scale)
 
 
+@pytest.mark.parametrize("gauge", [True, False])
 @pytest.mark.parametrize("sym", [True, False])
 @pytest.mark.parametrize("name,fp,nparam", [("full9", lambda: P.full9_problem(512), 1),
                                             ("full9-hot", lambda: _high_norm_problem(64)[0], 2)])
-def test_pair_launches_bitwise(name, fp, nparam, sym):
+def test_pair_launches_bitwise(name, fp, nparam, sym, gauge):
     """Latency-bound calls (16-wave scans) of the Rydberg layout run both sector classes' walks and
     scans in one launch per stage (k_walk_fwd_pair, k_scan_pair, k_walk_grad_pair): the same
     arithmetic as one launch per class (GRAPE_OPT_NO_PAIR), so F and F_dx agree bit for bit --
     batched (stream path) and single (graph path) calls; the C2-size problem also against the
     oracle at the T2s tier."""
-    from robustgrape_amd.operators import OPT_NO_PAIR, OPT_NO_SYMMETRY
+    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_PAIR, OPT_NO_SYMMETRY
+    if not gauge and name == "full9-hot":
+        pytest.skip("two controls per step: never phase-covariant")
     f = fp()
     nt = f.unitary_problem.ntimes
     rng = np.random.default_rng(11)
@@ -310,7 +313,7 @@ def test_pair_launches_bitwise(name, fp, nparam, sym):
         X[::2, 1::2][:, 5] = 700.0  # a high-norm step (squaring path) in every other row
     outs = []
     for opts in (0, OPT_NO_PAIR):
-        pl = _plan(f, 8, opts | (0 if sym else OPT_NO_SYMMETRY), nparam=nparam)
+        pl = _plan(f, 8, opts | (0 if sym else OPT_NO_SYMMETRY) | (0 if gauge else OPT_NO_GAUGE), nparam=nparam)
         try:
             batch = pl.fidelity_grad(X)[:2]
             single = pl.fidelity_grad(X[3:4])[:2]
@@ -324,23 +327,24 @@ def test_pair_launches_bitwise(name, fp, nparam, sym):
     if name == "full9":
         from oracle import grape_oracle as O
         F0, g0 = O.calculate_fidelity_and_derivatives(f, X[0])[:2]
-        _check("pair_full9", b0[0][0], b0[1][0], F0, g0, True)
+        _check(f"pair_full9_{'gauge' if gauge else 'exp'}", b0[0][0], b0[1][0], F0, g0, True)
 
 
+@pytest.mark.parametrize("gauge", [True, False])
 @pytest.mark.parametrize("nb,max_batch", [(300, 300), (3, 8)])
-def test_twin_sectors_bitwise(nb, max_batch):
+def test_twin_sectors_bitwise(nb, max_batch, gauge):
     """Twin sectors (grape_walk.hpp TWIN: the 2-level Rydberg sectors {01, 0r} and {10, r0} have
     identical operator blocks at equal Rabi frequencies): one exponential per step serves both.
     The shared propagators are the ones each sector would compute from the same inputs, so F and
     F_dx equal those of GRAPE_OPT_NO_TWIN bit for bit -- a throughput-size batch and a latency-bound
     one (16-wave scans, pair kernels), plus a single call."""
-    from robustgrape_amd.operators import OPT_NO_TWIN
+    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_TWIN
     f = P.full9_problem(128)
     rng = np.random.default_rng(21)
     X = rng.uniform(0, 2 * np.pi, size=(nb, 129))
     outs = []
     for opts in (0, OPT_NO_TWIN):
-        pl = _plan(f, max_batch, opts)
+        pl = _plan(f, max_batch, opts | (0 if gauge else OPT_NO_GAUGE))
         try:
             outs.append((pl.fidelity_grad(X)[:2], pl.fidelity_grad(X[:1])[:2]))
         finally:
