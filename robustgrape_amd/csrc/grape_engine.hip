@@ -1413,7 +1413,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // and the error sources use are identical, with the same padding -- one exponential
             // per step serves both (the 2-level Rydberg sectors at equal Rabi frequencies)
             Ps.twin = 0;
-            if (Ps.walk && P.ne == 0 && sc.nsec == 2 && S <= 3 && !Ps.walk_store_e && !(P.opts & GRAPE_OPT_NO_TWIN)) {
+            // (S == 2 only: launch<2> is the one launcher that runs a class with two sectors per lane)
+            if (Ps.walk && P.ne == 0 && sc.nsec == 2 && S == 2 && !Ps.walk_store_e && !(P.opts & GRAPE_OPT_NO_TWIN)) {
                 bool same = true;
                 for (int a = 0; a < S; ++a) same = same && ((sc.sidx[a] < 0) == (sc.sidx[S + a] < 0));
                 std::vector<char> used(n_ops, 0);

@@ -21,6 +21,7 @@ from __future__ import annotations
 import atexit
 import contextlib
 import multiprocessing as mp
+import multiprocessing.pool
 import os
 import sys
 import threading
@@ -251,16 +252,33 @@ def _main_hidden():
         main.__dict__.update(saved)
 
 
+_SPAWN = mp.get_context("spawn")
+
+
+class _NoMainProcess(_SPAWN.Process):
+    """A spawned worker started with the parent's __main__ hidden (_main_hidden) -- every start,
+    including the replacements Pool._repopulate_pool makes when a worker dies.  The
+    hiding is a short process-wide change around the start; a thread of the parent that reads
+    __main__.__file__ at that instant would see it unset."""
+
+    def start(self):
+        with _main_hidden():
+            super().start()
+
+
+class _NoMainContext(type(_SPAWN)):
+    Process = _NoMainProcess
+
+
 class TableWorkers:
     """A process pool that fills closure tables in shared memory.  Spawned, not forked: the pool
     may first be needed after this process has initialised HIP, and a fork would copy that
     state into the workers (they never touch the GPU).  The workers start without the parent's
-    main module (_main_hidden)."""
+    main module (_NoMainProcess: also the pool's replacement workers)."""
 
     def __init__(self, nworkers: int):
         self.n = nworkers
-        with _main_hidden():
-            self.pool = mp.get_context("spawn").Pool(nworkers)
+        self.pool = multiprocessing.pool.Pool(nworkers, context=_NoMainContext())
         self.lock = threading.Lock()
 
     @staticmethod

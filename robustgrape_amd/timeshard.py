@@ -205,7 +205,7 @@ def _chain(mats, d):
 
 
 def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, nslices: int | None = None,
-                               group=None, device: int = 0, device_exchange: bool | None = None):
+                               group=None, device: int | None = None, device_exchange: bool | None = None):
     """(F, F_dx) of ONE evaluation with its time steps split into slices.
 
     group: a torch.distributed process group (or the default group when torch.distributed is
@@ -213,7 +213,11 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
     Otherwise `nslices` slices run one after another on `device`.  Every rank returns the full
     (F, F_dx).  device_exchange (default: with the nccl backend; optional for the in-order slices):
     slice totals, the chain, the head, M' and the F_dx slices stay device tensors
-    (grape_slice_*_device, RCCL all_gathers of device buffers); only F and F_dx come back."""
+    (grape_slice_*_device, RCCL all_gathers of device buffers); only F and F_dx come back.
+    device: the GPU of the slice plan(s); default: the current torch device on the rank path (under
+    torchrun with torch.cuda.set_device(local_rank): the rank's own GPU), 0 for the in-order slices.
+    On the rank path the plan, the slice tensors and the side stream are all on that device; a
+    `device` other than the current one with the device exchange is refused (ValueError)."""
     up = fp.unitary_problem
     x = np.ascontiguousarray(x, dtype=np.float64)
     if x.shape != (nparam * up.ntimes,):
@@ -226,6 +230,8 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
         nslices = dist.get_world_size(group)
         rank = dist.get_rank(group)
     bounds = slice_bounds(up.ntimes, nslices)
+    if dist is None and device is None:
+        device = 0
     if dist is None and device_exchange:  # virtual ranks, device buffers throughout
         import torch
         dev = torch.device("cuda", device)
@@ -252,12 +258,17 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
         return F, np.concatenate(grads)
     import torch
     a, b = bounds[rank]
-    sp = _slice_plan(fp, nparam, a, b, device)
     backend = dist.get_backend(group)
     if device_exchange is None:
         device_exchange = backend == "nccl"
+    if device is None:
+        device = torch.cuda.current_device() if (device_exchange or backend == "nccl") else 0
+    elif device_exchange and device != torch.cuda.current_device():
+        raise ValueError(f"device={device} but the current torch device is {torch.cuda.current_device()}: the "
+                         "device exchange keeps the slice tensors on the current device")
+    sp = _slice_plan(fp, nparam, a, b, device)
     if device_exchange:  # device buffers throughout: two RCCL all_gathers, no host staging
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cuda", device)
         d = up.ndim
         S = torch.view_as_real(sp.forward_device(torch.as_tensor(x[a * nparam:b * nparam], device=dev)).contiguous())
         got = [torch.empty_like(S) for _ in range(nslices)]
@@ -275,7 +286,7 @@ def time_sharded_fidelity_grad(fp: FidelityRobustGRAPEProblem, x, nparam: int, n
         sp.plan.synchronize()
         return float(F.item()), Fdx.cpu().numpy()
     S = sp.forward(x[a * nparam:b * nparam])
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
     d = up.ndim
     mine = torch.from_numpy(np.ascontiguousarray(S).view(np.float64).reshape(d, d, 2)).to(dev)
     got = [torch.empty_like(mine) for _ in range(nslices)]

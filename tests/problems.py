@@ -145,6 +145,14 @@ def fd_tier(fp, X, nparam=1):
     return 1e-6 * f, 1e-7 * f
 
 
+def fd_factor(fp, X, nparam=1):
+    """The step-norm factor of the FD tiers (fd_tier's rule): 1 up to Julia's Pade-13
+    threshold |dt H_k|_1 = 5.4, max_k |dt H_k|_1 / 5.4 beyond it (the reference squares there and its
+    u / eps noise grows like 2^s).  Used for the tiers fd_tier does not return (T2 of uncontracted
+    tensors and sensitivities, T3 of the mixed stencils)."""
+    return max(1.0, max_step_norm(fp, X, nparam) / JULIA_THETA13)
+
+
 def random_x(ntimes, seed, nparam=1, small=False):
     """x_main = 2pi*U (runtests.jl:335) or 2pi*0.001*U (examples/time_optimal_cz.jl:32); theta = 2pi*U."""
     rng = np.random.default_rng(seed)

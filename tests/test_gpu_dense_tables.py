@@ -49,7 +49,7 @@ def test_closures_above_12_levels_match_oracle(d, nt, nerr, phase):
     for b in range(len(X)):
         ref = O.calculate_fidelity_and_derivatives(fp, X[b])
         t2, t2a = P.fd_tier(fp, X[b], nparam=2)
-        fac = max(1.0, P.max_step_norm(fp, X[b], nparam=2))
+        fac = P.fd_factor(fp, X[b], nparam=2)
         assert abs(F[b] - ref[0]) <= T1, (F[b], ref[0])
         checks = [(Fdx[b], ref[1], t2, t2a)]
         if nerr:
@@ -67,7 +67,7 @@ def test_closure_unitary_derivatives_above_12_levels():
     x = _x(fp, 77)
     ref = O.calculate_unitary_and_derivatives(fp.unitary_problem, x)
     got = calculate_unitary_and_derivatives(fp.unitary_problem, x)
-    fac = max(1.0, P.max_step_norm(fp, x, nparam=2))
+    fac = P.fd_factor(fp, x, nparam=2)
     assert np.max(np.abs(got[0] - ref[0])) <= T1 * fac
     for n, (t, ta) in ((1, (T2, T2_ABS)), (3, (T2, T2_ABS)), (4, (T3, T3_ABS))):
         a, b = np.asarray(got[n]), np.asarray(ref[n])

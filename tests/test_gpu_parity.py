@@ -158,12 +158,9 @@ T3, T3_ABS, T3_XADD_ABS = 1e-5, 1e-7, 1e-5
 
 
 def _err_scale(fp, x):
-    """Step-norm factor of the FD tiers (tests/problems.py fd_tier): 1 while no step needs squaring,
-    else max(1, max_k |dt H_k|_1) -- with s squarings the u / eps (u / eps2^2) noise of the
-    differences grows like 2^s in any implementation, and the chunk walks (scaled Taylor 12) and
-    Julia (Pade 7 / 9 / 13) square differently."""
-    n = P.max_step_norm(fp, x)
-    return 1.0 if n <= 0.25 else max(1.0, n)
+    """Step-norm factor of the FD tiers: tests/problems.py fd_factor (1 up to |dt H_k|_1 = 5.4, where
+    Julia's exp! starts squaring; |dt H_k|_1 / 5.4 beyond)."""
+    return P.fd_factor(fp, x)
 
 
 def _assert_err(fp, d2, d2dx, ref_d2, ref_d2dx, test="", x=None):

@@ -146,3 +146,41 @@ def test_ranks_exchange_device_buffers():
     F0, g0 = O.calculate_fidelity_and_derivatives(fp, dense_x(ntimes=41, seed=9))[:2]
     for r, F, Fdx in out:
         _check(f"timeshard_device_rank{r}_oracle", F, np.asarray(Fdx), F0, np.asarray(g0))
+
+
+def test_rank_path_plan_follows_the_current_device():
+    """on the rank path the slice plan is built on the current torch device (the rank's
+    GPU under torchrun), where the slice tensors and the side stream live; an explicit `device`
+    other than the current one is refused with the device exchange."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    from robustgrape_amd import timeshard as TS
+    from robustgrape_amd.synthetic import dense_problem, dense_x
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        fp = dense_problem(d=16, ntimes=6, dt=0.3, rank=8)
+        x = dense_x(ntimes=6, seed=3)
+        seen = []
+        real = TS._slice_plan
+        TS._slice_plan = lambda fp_, nparam, k0, k1, device, keep=0: seen.append(device) or real(
+            fp_, nparam, k0, k1, device, keep)
+        try:
+            F, _ = TS.time_sharded_fidelity_grad(fp, x, nparam=2, device_exchange=True)
+        finally:
+            TS._slice_plan = real
+        assert seen == [torch.cuda.current_device()] and np.isfinite(F)
+        with pytest.raises(ValueError):
+            TS.time_sharded_fidelity_grad(fp, x, nparam=2, device_exchange=True,
+                                          device=torch.cuda.current_device() + 1)
+    finally:
+        if own:
+            dist.destroy_process_group()

@@ -190,3 +190,57 @@ def test_image_walk_not_for_non_hermitian_error_generator():
         error_sources=list(base.unitary_problem.error_sources) + [ErrorSource(OperatorBasisError([Term(decay, scale=-0.5j)]))]))
     X = np.stack([P.random_x(12, s) for s in range(2)])
     _run(fo, X, expect_walk=False)
+
+
+def _symmetric_error_problem(nt, device=True):
+    """C2's model with error sources that act on BOTH atoms alike -- a common Rabi-amplitude error
+    (Omega1 = Omega2 -> 1 + err) and a common detuning (delta1 = delta2 = err) -- so the atom-swap
+    symmetry survives and the plan keeps the symmetry-adapted sectors (the rotated error
+    operators, the rotated PA / PB of the sector error head and the 3-level image walk's
+    F_d2err / F_d2err_dx had no test; C3's single-atom errors break the symmetry)."""
+    from robustgrape_amd import rydberg as R
+    from robustgrape_amd.operators import OperatorBasisError, Term
+    from robustgrape_amd.types import ErrorSource, FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    B = 10.0
+    if device:
+        H0 = R.rydberg_full_operator_basis(1.0, 1.0, 0.0, 0.0, B)
+        rabi = OperatorBasisError(list(R.full_rabi_error(1).terms) + list(R.full_rabi_error(2).terms))
+        dd = np.zeros(9)
+        for i in (4, 6, 8):
+            dd[i] += 1.0
+        for i in (5, 7, 8):
+            dd[i] += 1.0
+        det = OperatorBasisError([Term(op=np.diag(dd).astype(np.complex128))])
+        errs, target = [ErrorSource(rabi), ErrorSource(det)], R.cz_full_target()
+    else:
+        H0 = lambda t, p, xa: R.rydberg_hamiltonian_full(p[0], 1, 1, 0, 0, B)  # noqa: E731
+        rabi = lambda t, p, xa, e: (R.rydberg_hamiltonian_full(p[0], 1 + e, 1 + e, 0, 0, B)  # noqa: E731
+                                    - R.rydberg_hamiltonian_full(p[0], 1, 1, 0, 0, B))
+        det = lambda t, p, xa, e: (R.rydberg_hamiltonian_full(p[0], 1, 1, e, e, B)  # noqa: E731
+                                   - R.rydberg_hamiltonian_full(p[0], 1, 1, 0, 0, B))
+        errs, target = [ErrorSource(rabi), ErrorSource(det)], (lambda xa: R.cz_with_1q_phase_full(xa[0]))
+    up = UnitaryRobustGRAPEProblem(t0=P.T0_TO, ntimes=nt, ndim=9, H0=H0, nb_additional_param=1, error_sources=errs)
+    return FidelityRobustGRAPEProblem(up, P.W_FULL9, target)
+
+
+@pytest.mark.parametrize("nt", [1, 40, 160])
+def test_symmetric_error_sources_keep_the_rotated_sectors(nt):
+    """Errors that keep the atom-swap symmetry: the symmetry-adapted sectors (3 + 2 + 2) with the
+    image walk, against the permutation sectors (GRAPE_OPT_NO_SYMMETRY) and the oracle: F, F_dx,
+    F_d2err, F_d2err_dx (FidelityCalculations.jl:78-117 in the rotated frame)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_SYMMETRY
+    fp, fo = _symmetric_error_problem(nt), _symmetric_error_problem(nt, device=False)
+    X = np.stack([P.random_x(nt, 4100 + s, small=(s == 1)) for s in range(3)])
+    out, sec = _run(fp, X, expect_walk=True)
+    assert sec == P.FULL9_SYM, sec
+    perm, sec_p = _run(fp, X, OPT_NO_SYMMETRY, expect_walk=True)
+    assert sec_p == P.FULL9_PERM, sec_p
+    nmain = nt
+    for b in range(len(X)):
+        tier = P.fd_tier(fp, X[b])
+        ref_perm = tuple(o[b] for o in perm)
+        _check_all(f"symerr_vs_perm_nt{nt}_{b}", out, b, ref_perm, tier, nmain)
+    for b in (0, 1):
+        ref = O.calculate_fidelity_and_derivatives(fo, X[b])
+        _check_all(f"symerr_vs_oracle_nt{nt}_{b}", out, b, ref, P.fd_tier(fp, X[b]), nmain)

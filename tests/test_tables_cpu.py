@@ -111,6 +111,18 @@ for r in W.submit(W.prepare(fp2), 1, tabs, X, range(len(X))):
     r.get(timeout=120)
 H, U0 = TB.host_tables(fp2, X, 1)
 assert np.array_equal(tabs.H, H) and np.array_equal(tabs.U0, U0)
+# a worker dies: the pool's replacement starts through the same hidden-main context
+import os as _os, signal as _signal, time as _time
+victim = W.pool._pool[0].pid
+_os.kill(victim, _signal.SIGKILL)
+for _ in range(200):
+    if all(p.pid != victim and p.is_alive() for p in W.pool._pool):
+        break
+    _time.sleep(0.05)
+assert all(p.pid != victim for p in W.pool._pool)
+for r in W.submit(W.prepare(fp2), 1, tabs, X, range(len(X))):
+    r.get(timeout=120)
+assert np.array_equal(tabs.H, H)
 W.release(tabs)
 tabs.close()
 W.close()
