@@ -580,24 +580,31 @@ static std::complex<double> host_coef(const grape_term &t, double x) {
 static bool find_gauge(const grape_desc *desc, const grape_desc &sdesc, const SectorClass &sc, double &a,
                        std::vector<int> &N) {
     constexpr int kMaxCharge = 8;
-    const int D = desc->ndim, S = sc.S;
+    const int D = desc->ndim, S = sc.S, NE = desc->nerr;
     const size_t T = (size_t)D * D;
-    if (desc->nparam != 1 || desc->nerr != 0) return false;
+    if (desc->nparam != 1) return false;
+    // the term lists: H0's, then every error source's (UnitaryCalculations.jl:67-97 adds
+    // errval * Herror_e to H0: both must be covariant with the same charges)
+    std::vector<std::pair<const grape_term *, int>> lists{{desc->h0_terms, desc->n_h0_terms}};
+    for (int e = 0; e < NE; ++e)
+        lists.push_back({desc->err_terms + desc->err_term_offsets[e],
+                         desc->err_term_offsets[e + 1] - desc->err_term_offsets[e]});
     bool have_a = false;
     a = 1.0;
-    for (int t = 0; t < desc->n_h0_terms; ++t) {
-        const grape_term &tm = desc->h0_terms[t];
-        if (tm.var == 2 || tm.var == 3) return false;  // x_add or the step index
-        if (tm.var != 1) continue;
-        if (tm.func != 2 && tm.func != 3 && tm.func != 4) return false;  // x must enter as a phase
-        if (!(tm.a != 0.0) || (have_a && tm.a != a)) return false;
-        a = tm.a;
-        have_a = true;
-    }
-    auto block = [&](int w, double x, std::vector<std::complex<double>> &H) {
+    for (const auto &l : lists)
+        for (int t = 0; t < l.second; ++t) {
+            const grape_term &tm = l.first[t];
+            if (tm.var == 2 || tm.var == 3) return false;  // x_add or the step index
+            if (tm.var != 1) continue;
+            if (tm.func != 2 && tm.func != 3 && tm.func != 4) return false;  // x must enter as a phase
+            if (!(tm.a != 0.0) || (have_a && tm.a != a)) return false;
+            a = tm.a;
+            have_a = true;
+        }
+    auto block = [&](int w, int li, double x, std::vector<std::complex<double>> &H) {
         H.assign((size_t)S * S, 0.0);
-        for (int t = 0; t < desc->n_h0_terms; ++t) {
-            const grape_term &tm = desc->h0_terms[t];
+        for (int t = 0; t < lists[li].second; ++t) {
+            const grape_term &tm = lists[li].first[t];
             const std::complex<double> c = host_coef(tm, x);
             for (int r = 0; r < S; ++r)
                 for (int q = 0; q < S; ++q) {
@@ -611,27 +618,36 @@ static bool find_gauge(const grape_desc *desc, const grape_desc &sdesc, const Se
     N.assign((size_t)sc.nsec * S, 0);
     const double xs = 0.01 / std::fabs(a);
     const double probe[7] = {0.37, -1.3, 2.9, 7.77, -31.4, 0.001, 123.456};
-    std::vector<std::complex<double>> H0, Hs, Hx;
+    const int NL = (int)lists.size();
+    std::vector<std::vector<std::complex<double>>> H0(NL), Hs(NL);
+    std::vector<std::complex<double>> Hx;
+    std::vector<double> tol(NL);
     for (int w = 0; w < sc.nsec; ++w) {
-        block(w, 0.0, H0);
-        block(w, xs, Hs);
-        double hmax = 0.0;
-        for (const auto &h : H0) hmax = std::max(hmax, std::abs(h));
-        for (const auto &h : Hs) hmax = std::max(hmax, std::abs(h));
-        const double tol = 1e-13 * std::max(hmax, 1e-300);
+        // charge differences n_rq = N_r - N_q from every block's entries (H0's and the errors')
         std::vector<int> n((size_t)S * S, 0);
-        for (int r = 0; r < S; ++r)
-            for (int q = 0; q < S; ++q) {
-                const std::complex<double> h0 = H0[(size_t)r * S + q], h1 = Hs[(size_t)r * S + q];
-                if (std::abs(h0) <= tol) {
-                    if (std::abs(h1) > tol) return false;  // vanishes at x = 0 only: not a phase
-                    continue;
+        std::vector<char> cpl((size_t)S * S, 0);
+        for (int li = 0; li < NL; ++li) {
+            block(w, li, 0.0, H0[li]);
+            block(w, li, xs, Hs[li]);
+            double hmax = 0.0;
+            for (const auto &h : H0[li]) hmax = std::max(hmax, std::abs(h));
+            for (const auto &h : Hs[li]) hmax = std::max(hmax, std::abs(h));
+            tol[li] = 1e-13 * std::max(hmax, 1e-300);
+            for (int r = 0; r < S; ++r)
+                for (int q = 0; q < S; ++q) {
+                    const std::complex<double> h0 = H0[li][(size_t)r * S + q], h1 = Hs[li][(size_t)r * S + q];
+                    if (std::abs(h0) <= tol[li]) {
+                        if (std::abs(h1) > tol[li]) return false;  // vanishes at x = 0 only: not a phase
+                        continue;
+                    }
+                    const double m = std::arg(h1 / h0) / (a * xs);
+                    const int nn = (int)std::lround(m);
+                    if (std::fabs(m - nn) > 1e-6 || std::abs(nn) > kMaxCharge || (r == q && nn != 0)) return false;
+                    if (cpl[(size_t)r * S + q] && n[(size_t)r * S + q] != nn) return false;
+                    cpl[(size_t)r * S + q] = 1;
+                    n[(size_t)r * S + q] = nn;
                 }
-                const double m = std::arg(h1 / h0) / (a * xs);
-                const int nn = (int)std::lround(m);
-                if (std::fabs(m - nn) > 1e-6 || std::abs(nn) > kMaxCharge || (r == q && nn != 0)) return false;
-                n[(size_t)r * S + q] = nn;
-            }
+        }
         std::vector<int> Nw(S, 0);  // charges by breadth-first search over the couplings
         std::vector<char> seen(S, 0);
         for (int s0 = 0; s0 < S; ++s0) {
@@ -642,7 +658,7 @@ static bool find_gauge(const grape_desc *desc, const grape_desc &sdesc, const Se
                 const int r = stack.back();
                 stack.pop_back();
                 for (int q = 0; q < S; ++q) {
-                    if (std::abs(H0[(size_t)r * S + q]) <= tol) continue;
+                    if (!cpl[(size_t)r * S + q]) continue;
                     const int want = Nw[r] - n[(size_t)r * S + q];  // n_rq = N_r - N_q
                     if (!seen[q]) {
                         seen[q] = 1;
@@ -660,17 +676,18 @@ static bool find_gauge(const grape_desc *desc, const grape_desc &sdesc, const Se
             if (Nw[r] > kMaxCharge) return false;
             N[(size_t)w * S + r] = Nw[r];
         }
-        for (double x : probe) {  // the identity itself, entry by entry
-            block(w, x, Hx);
-            double hm = hmax;
-            for (const auto &h : Hx) hm = std::max(hm, std::abs(h));
-            for (int r = 0; r < S; ++r)
-                for (int q = 0; q < S; ++q) {
-                    const std::complex<double> ph = std::polar(1.0, a * x * (Nw[r] - Nw[q]));
-                    if (std::abs(Hx[(size_t)r * S + q] - ph * H0[(size_t)r * S + q]) > 1e-12 * std::max(hm, 1e-300))
-                        return false;
-                }
-        }
+        for (int li = 0; li < NL; ++li)
+            for (double x : probe) {  // the identity itself, entry by entry, every block
+                block(w, li, x, Hx);
+                double hm = tol[li] * 1e13;
+                for (const auto &h : Hx) hm = std::max(hm, std::abs(h));
+                for (int r = 0; r < S; ++r)
+                    for (int q = 0; q < S; ++q) {
+                        const std::complex<double> ph = std::polar(1.0, a * x * (Nw[r] - Nw[q]));
+                        if (std::abs(Hx[(size_t)r * S + q] - ph * H0[li][(size_t)r * S + q]) > 1e-12 * std::max(hm, 1e-300))
+                            return false;
+                    }
+            }
     }
     return true;
 }
@@ -1340,8 +1357,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // phase-covariant classes (grape_walk.hpp GAUGE): one exponential per walk lane
             std::vector<int> gauge_n;
             double gauge_a = 1.0;
-            Ps.gauge = (Ps.walk && P.ne == 0 && !(P.opts & GRAPE_OPT_NO_GAUGE) &&
-                        find_gauge(desc, sdesc, sc, gauge_a, gauge_n)) ? 1 : 0;
+            // (with error sources: the phase-covariant image walk, one gradient parameter per step)
+            Ps.gauge = (Ps.walk && (P.ne == 0 || (P.nvg == 1 && P.ne <= grape::kGaugeMaxE)) &&
+                        !(P.opts & GRAPE_OPT_NO_GAUGE) && find_gauge(desc, sdesc, sc, gauge_a, gauge_n)) ? 1 : 0;
             Ps.gauge_a = gauge_a;
             Ps.gauge_n = nullptr;
             if (Ps.gauge) {

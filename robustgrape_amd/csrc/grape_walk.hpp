@@ -775,8 +775,8 @@ struct WalkCfg {
     // bookkeeping (k_walk_fwd<2,2> 0.295 -> 0.34 ms per pass) and keep the unshifted walk bitwise
     static constexpr bool SHIFT = D >= GRAPE_WALK_SHIFT_MIN_D;
     // phase-covariant classes (GAUGE): E~, E and the walk state only -- no exponential per step
-    static constexpr int WAVES_GAUGE = D <= 2 ? GRAPE_WALK_GAUGE2_WAVES : D == 3 ? GRAPE_WALK_GAUGE3_WAVES
-                                                                         : GRAPE_WALK_GAUGE4_WAVES;
+    static constexpr int WAVES_GAUGE = D <= 2 ? (NS >= 3 ? 2 : GRAPE_WALK_GAUGE2_WAVES)
+                                              : D == 3 ? GRAPE_WALK_GAUGE3_WAVES : GRAPE_WALK_GAUGE4_WAVES;
 };
 
 // The chunk's phase: sum of the steps' diagonal shifts (sm_regime), TwoSum-compensated; the chunk
@@ -1583,6 +1583,240 @@ __global__ __launch_bounds__(kWalkBlock, (WalkCfg<D, NS>::WAVES_IMG)) void k_wal
         for (int w = 0; w < NS; ++w) {
             if constexpr (C::SHIFT) walk_phase<D>(ph[w], Q[w]);
             cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;  // row-major chunk total
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int i = 0; i < D; ++i) dst[j * D + i] = Q[w][j][i];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The image walk of a phase-covariant class (P.gauge with error sources, nvg = 1; round 5)
+// ---------------------------------------------------------------------------
+// With H0 and every Herror_e covariant under the same D(a x) (find_gauge: the C3 Rabi and detuning
+// errors of the Rydberg models are), every variant propagator of a step is a phase sandwich of an
+// x-independent matrix: E_k = D E0 D^dag, E(err_e eps) = D E_e1 D^dag, E(x + eps2, err_e eps2) =
+// D'' E_e2 D''^dag ... with E0 = exp(A0), E_e1 = exp(A0 + eps A_e0), E_e2 = exp(A0 + eps2 A_e0) (A at
+// x = 0).  So the images' kernels Z = E_k^dag dX (UnitaryCalculations.jl:48-95) are
+//   Z1   = D (E0^dag (E0 o f1)) D^dag / eps                           f1 from (x + eps) - x
+//   W_e  = D (E0^dag (E_e1 - E0) / eps) D^dag = D K_e D^dag           x-independent K_e
+//   Z2_e = D (E0^dag ((E_e2 - E0) o f2)) D^dag / eps2^2                f2 from (x + eps2) - x
+// with (M o f)_rj = M_rj (rho_r + conj(rho_j) + rho_r conj(rho_j)) as in the gradient walk: the
+// mixed stencil's four-term difference becomes one product without cancellation.  The workgroup
+// (all lanes one sector group: blockIdx.y) computes E0, K_e and E_e2 - E0 once into LDS (1 + 2 ne
+// exponentials per sector, the first lanes in parallel); per step a lane forms D from its control's
+// phase, Z1 and Z2_e with one product each, and every image Y = Q^dag Z Q with two, instead of
+// 3 + 3 ne exponentials per step.  Images, chunk totals and their layouts are k_walk_img's.
+
+template <int D, int NS>
+__device__ __forceinline__ cd *img_gauge_base(cd *g, int w, int b) {  // matrix b of sector w, row-major
+    return g + ((size_t)w * (1 + 2 * kGaugeMaxE) + b) * D * D;
+}
+template <int D, int NS>
+constexpr int img_gauge_waves() { return D >= 4 ? 1 : D == 3 ? 2 : NS == 1 ? 3 : 2; }
+template <int D, int NS>
+__global__ __launch_bounds__(kWalkBlock, (img_gauge_waves<D, NS>())) void k_walk_img_gauge(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    constexpr int NBM = 1 + 2 * kGaugeMaxE;
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<NS>(P, B, vb);
+    const size_t lanes = (size_t)vb.gx * kWalkBlock, lane = (size_t)vb.x * kWalkBlock + threadIdx.x;
+    const int ns = P.nsec > 1 ? P.nsec : 1, NE = P.ne;
+    const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);
+    const int xs = kWalkXRow ? 1 : L.nbe;
+    __shared__ cd gbase[NS * NBM * TS];
+    // --- the workgroup's x-independent bases: lane t < NS (1 + 2 NE) computes matrix (w, b) ---
+    {
+        const int t = threadIdx.x, nb = 1 + 2 * NE;
+        if (t < NS * nb) {
+            const int w = t / nb, b = t % nb;
+            const int e = b == 0 ? -1 : b <= NE ? b - 1 : b - 1 - NE;
+            const double ev = b == 0 ? 0.0 : b <= NE ? P.eps : P.eps2;
+            WalkX X0;
+            X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
+            Pert none;
+            none.var = -1;
+            none.index = 0;
+            none.delta = 0.0;
+            SM<D> A[1];
+            walk_build<D, 1>(P, as_constant(P.ops) + (size_t)(L.w0 + w) * P.sec_ops, X0, 1, none, A, e, ev);
+            double mu0 = 0.0;
+            cd *dst = img_gauge_base<D, NS>(gbase, w, b);
+            walk_expm<D, false, true, false>(A[0], B.wscr + (size_t)L.slot * NS * 2 * TS, mu0, true,
+                                             [&](int i, const cd (&x)[D]) {
+#pragma unroll
+                                                 for (int j = 0; j < D; ++j) dst[j * D + i] = x[j];
+                                             });
+        }
+        __syncthreads();
+        // K_e = E0^dag (E_e1 - E0) / eps and M_e = E_e2 - E0, in place (lane (w, e) owns both)
+        cd K[TS], Mm[TS];
+        const bool own = t < NS * NE;
+        const int w = own ? t / NE : 0, e = own ? t % NE : 0;
+        if (own) {
+            const cd *E0 = img_gauge_base<D, NS>(gbase, w, 0), *E1 = img_gauge_base<D, NS>(gbase, w, 1 + e),
+                     *E2 = img_gauge_base<D, NS>(gbase, w, 1 + NE + e);
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+#pragma unroll
+                for (int c = 0; c < D; ++c) {
+                    cd acc = czero();
+#pragma unroll
+                    for (int m = 0; m < D; ++m) cmac(acc, cconj(E0[m * D + r]), csub(E1[m * D + c], E0[m * D + c]));
+                    K[r * D + c] = cscale(P.inv_eps, acc);
+                    Mm[r * D + c] = csub(E2[r * D + c], E0[r * D + c]);
+                }
+            }
+        }
+        __syncthreads();
+        if (own) {
+            cd *K1 = img_gauge_base<D, NS>(gbase, w, 1 + e), *M2 = img_gauge_base<D, NS>(gbase, w, 1 + NE + e);
+#pragma unroll
+            for (int q = 0; q < TS; ++q) {
+                K1[q] = K[q];
+                M2[q] = Mm[q];
+            }
+        }
+        __syncthreads();
+    }
+    GaugeN<D> gn[NS];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
+    const int k0 = L.c * P.L;
+    X2 xn = walk_load_x(1, xt + (size_t)min(k0, P.Nt - 1) * xs, xs);
+    cd Q[NS][D][D];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) Q[w][j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+        }
+    }
+#pragma unroll 1
+    for (int jj = 0; jj < P.L; ++jj) {  // uniform trip count; steps past N_t store into the padding rows
+        const int k = min(k0 + jj, P.Nt - 1);
+        const bool act = L.ok && k0 + jj < P.Nt;
+        const double xk = xn.v0;
+        xn = walk_load_x(1, xt + (size_t)min(k + 1, P.Nt - 1) * xs, xs);  // next step's control
+        double sn, cn;
+        sincos(P.gauge_a * xk, &sn, &cn);
+        const cd p1 = cmake(cn, sn);
+        const cd q1 = cis_m1(P.gauge_a * ((xk + P.eps) - xk)), q2 = cis_m1(P.gauge_a * ((xk + P.eps2) - xk));
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            cd d[D], r1[D], r2[D];
+            gauge_phases<D>(p1, gn[w], d);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                r1[j] = gauge_rho(q1, gn[w].n[j]);
+                r2[j] = gauge_rho(q2, gn[w].n[j]);
+            }
+            const cd *E0 = img_gauge_base<D, NS>(gbase, w, 0);
+            // image of slot: Y = Q^dag (D Zt D^dag) Q, Zt given row-major (scaled by `sc`)
+            auto emit = [&](const cd (&Zt)[D][D], int slot, double sc) {
+                cd Z[D][D];
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+#pragma unroll
+                    for (int c = 0; c < D; ++c)
+                        Z[r][c] = cscale(sc, r == c ? Zt[r][c] : cmul(cmul(d[r], Zt[r][c]), cconj(d[c])));
+                }
+                cd *dst = B.Zl + img_index<D, NS>(P, vb.y, jj, w, slot, 0, lanes, lane);
+#pragma unroll
+                for (int cc = 0; cc < D; ++cc) {
+                    cd tt[D];
+#pragma unroll
+                    for (int m = 0; m < D; ++m) {
+                        cd c = czero();
+#pragma unroll
+                        for (int n = 0; n < D; ++n) cmac(c, Z[m][n], Q[w][n][cc]);
+                        tt[m] = c;
+                    }
+#pragma unroll
+                    for (int r = 0; r < D; ++r) {
+                        cd c = czero();
+#pragma unroll
+                        for (int m = 0; m < D; ++m) cmac(c, cconj(Q[w][m][r]), tt[m]);
+                        dst[(size_t)(r * D + cc) * lanes] = c;
+                    }
+                }
+            };
+            // E0^dag (M o f) for M = E0 (Z1) or E_e2 - E0 (Z2_e)
+            auto kernel_f = [&](const cd *M, const cd (&rho)[D], cd (&Zt)[D][D]) {
+                cd Mf[D][D];
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+#pragma unroll
+                    for (int c = 0; c < D; ++c) {
+                        if (r == c) {
+                            Mf[r][c] = czero();
+                        } else {
+                            const cd rc = cconj(rho[c]);
+                            Mf[r][c] = cmul(M[r * D + c], cadd(cadd(rho[r], rc), cmul(rho[r], rc)));
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+#pragma unroll
+                    for (int c = 0; c < D; ++c) {
+                        cd acc = czero();
+#pragma unroll
+                        for (int m = 0; m < D; ++m) cmac(acc, cconj(E0[m * D + r]), Mf[m][c]);
+                        Zt[r][c] = acc;
+                    }
+                }
+            };
+            {  // Z1 (slot 0)
+                cd Zt[D][D];
+                kernel_f(E0, r1, Zt);
+                emit(Zt, 0, P.inv_eps);
+            }
+#pragma unroll 1
+            for (int e = 0; e < NE; ++e) {  // W_e (slot 1 + e) and Z2_e (slot 1 + NE + e)
+                cd Zt[D][D];
+                const cd *Ke = img_gauge_base<D, NS>(gbase, w, 1 + e);
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+#pragma unroll
+                    for (int c = 0; c < D; ++c) Zt[r][c] = Ke[r * D + c];
+                }
+                emit(Zt, 1 + e, 1.0);
+                kernel_f(img_gauge_base<D, NS>(gbase, w, 1 + NE + e), r2, Zt);
+                emit(Zt, 1 + NE + e, P.inv_eps2sq);
+            }
+            // Q <- E_k Q with E_k = D E0 D^dag (column by column, in place)
+            cd E[D][D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int m = 0; m < D; ++m) E[j][m] = j == m ? E0[j * D + m] : cmul(cmul(d[j], E0[j * D + m]), cconj(d[m]));
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                cd qq[D], t[D];
+#pragma unroll
+                for (int m = 0; m < D; ++m) qq[m] = Q[w][m][i];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    cd c = czero();
+#pragma unroll
+                    for (int m = 0; m < D; ++m) cmac(c, qq[m], E[j][m]);
+                    t[j] = c;
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    Q[w][j][i] = cmake(act ? t[j].re : Q[w][j][i].re, act ? t[j].im : Q[w][j][i].im);
+            }
+        }
+    }
+    if (L.ok) {
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            cd *dst = B.Tc + (((size_t)L.be * ns + L.w0 + w) * P.nchunks + L.c) * TS;
 #pragma unroll
             for (int j = 0; j < D; ++j) {
 #pragma unroll

@@ -8,6 +8,7 @@ struct DevProblem;
 struct DevBatch;
 constexpr int kWalkMaxD = 4;  // sector classes of at most this many levels take the walks
 constexpr int kWalkMaxNpA = 2;  // ... with at most this many controls per step and x_add entries
+constexpr int kGaugeMaxE = 8;  // error sources of a phase-covariant image walk (grape_walk.hpp k_walk_img_gauge)
 constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBlock)
 // walk classes of at least this many levels hand the forward walk's propagators to the gradient walk
 // (B.Ew) instead of recomputing them (the engine's P.walk_store_e and the launchers agree on it)

@@ -15,7 +15,8 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
     const dim3 blk(grape::kWalkBlock);
     if (P.ne > 0) {  // error sources: the image walk, then its back end (grape_walk.hpp)
         if (stage == 0) {
-            hipLaunchKernelGGL((grape::k_walk_img<D, NS>), grid, blk, 0, st, P, B);
+            if (P.gauge) hipLaunchKernelGGL((grape::k_walk_img_gauge<D, NS>), grid, blk, 0, st, P, B);
+            else hipLaunchKernelGGL((grape::k_walk_img<D, NS>), grid, blk, 0, st, P, B);
         } else if (stage == 1) {  // F_dx traces of Z1 and the chunk sums of W (k_err_scan's Phase A)
             // (the 2-level image walk summed W itself: WalkCfg::IMG_WSUM)
             if (!(grape::WalkCfg<D, NS>::IMG_WSUM && P.ne <= grape::kWsumMaxE))

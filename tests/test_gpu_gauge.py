@@ -46,13 +46,14 @@ def _check(test, F, Fdx, F0, g0, tier):
 
 
 def test_which_plans_are_phase_covariant():
-    """Every Rydberg model with the phase as its control is; NO_GAUGE, two controls per step,
-    error sources and whole matrices are not."""
+    """Every Rydberg model with the phase as its control is, with or without its Rabi / detuning
+    error sources; NO_GAUGE, two controls per step and whole matrices are not."""
     from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_SECTORS, OPT_NO_SYMMETRY
     cases = [(P.full9_problem(16), 0, 1, (True, True)), (P.full9_problem(16), OPT_NO_SYMMETRY, 1, (True, True)),
              (P.sym_problem(16), 0, 1, (True,)), (P.fullblk_problem(16), 0, 1, (True,)),
              (P.full9_problem(16), OPT_NO_GAUGE, 1, (False, False)),
-             (P.full9_problem(16, nerr=2), 0, 1, (False, False)),
+             (P.full9_problem(16, nerr=2), 0, 1, (True, True)),   # Rabi / detuning errors: covariant too
+             (P.full9_problem(16, nerr=2), OPT_NO_GAUGE, 1, (False, False)),
              (P.full9_problem(16), OPT_NO_SECTORS, 1, (False,))]
     for fp, opts, nparam, want in cases:
         pl = _plan(fp, 4, opts, nparam)
@@ -133,3 +134,43 @@ def test_gauge_bench_size_plan_against_c2_golden():
     err = np.max(np.abs(G - Gn), axis=1)
     scale = np.max(np.abs(Gn), axis=1)
     assert np.all(err <= 1e-7 * scale + 1e-9), float(np.max(err / scale))
+
+
+def _check_err(test, out, b, ref, tier):
+    from tests.test_gpu_walk_err import _check_all
+    _check_all(test, out, b, ref, tier, len(ref[1]) - 1)
+
+
+@pytest.mark.parametrize("name,fp", [
+    ("c3", lambda: P.full9_problem(64, nerr=4)),
+    ("c3-one-step", lambda: P.full9_problem(1, nerr=4)),
+    ("full9-2err", lambda: P.full9_problem(40, nerr=2)),
+    ("sym5-amp-freq", lambda: P.sym_problem(24, errors=("amp", "freq"))),
+    ("fullblk7-amp-freq", lambda: P.fullblk_problem(24, errors=("amp", "freq"))),
+])
+@pytest.mark.parametrize("batch", [3, 300])
+def test_gauge_image_walk_matches_per_step_exponentials_and_oracle(name, fp, batch):
+    """Error sources (k_walk_img_gauge): F, F_dx, F_d2err, F_d2err_dx against the per-step image walk
+    (GRAPE_OPT_NO_GAUGE) and the oracle (UnitaryCalculations.jl:66-151, FidelityCalculations.jl:78-117);
+    the mixed stencil is formed without its four-term cancellation, so the comparison carries the
+    per-step side's eps2 noise (T3 tier)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd.operators import OPT_NO_GAUGE
+    f = fp()
+    nt = f.unitary_problem.ntimes
+    X = np.stack([P.random_x(nt, 1300 + s, small=(s % 2 == 1)) for s in range(batch)])
+    pg, pn = _plan(f, batch), _plan(f, batch, OPT_NO_GAUGE)
+    try:
+        assert all(pg.sector_info()["gauge"]) and not any(pn.sector_info()["gauge"])
+        out, ref = pg.fidelity_grad(X), pn.fidelity_grad(X)
+        one = pg.fidelity_grad(X[1:2])
+    finally:
+        pg.close()
+        pn.close()
+    assert one[0][0] == out[0][1] and np.array_equal(one[1][0], out[1][1])
+    assert np.array_equal(one[3][0], out[3][1])
+    for b in range(min(batch, 4)):
+        _check_err(f"gauge_img_vs_exp_{name}_{batch}_{b}", out, b, tuple(o[b] for o in ref), P.fd_tier(f, X[b]))
+    for b in (0, 1):
+        ro = O.calculate_fidelity_and_derivatives(f, X[b])
+        _check_err(f"gauge_img_vs_oracle_{name}_{batch}_{b}", out, b, ro, P.fd_tier(f, X[b]))
