@@ -553,7 +553,7 @@ def c4_points(fp, nparam, inputs, dev, batches=(256, 32), seconds=1.5):
     return out
 
 
-def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passes=None):
+def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passes=None, info=None):
     # k_expm exponentiates every stored variant of every step: nominal, x + eps, x + eps2,
     # and per error source err(eps), err(eps2), (x + eps2, err eps2) -> 3 + 3 ne (Pade 5);
     # the x_add variants are skipped (H0 does not read x_add: their differences are exactly 0)
@@ -568,12 +568,18 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     prod = lambda S: 8 * S ** 3  # noqa: E731
     tile = lambda S: 16 * S * S  # noqa: E731
     walk = ktimes.get("k_walk_fwd", (0.0, 0))[1] > 0
+    gauges = tuple((info or {}).get("gauge", ())) + (False,) * len(classes)
+    # the phase-covariant image walk (grape_walk.hpp k_walk_img_gauge) per (step, sector): no
+    # exponential; E_k from E0 and the level phases, one product each for Z1 and Z2_e (E0^dag (M o f)),
+    # two per image (Q^dag Z Q), the chain product, and the phase sandwiches / stencil weights
+    img_gauge = lambda S: 8 * S ** 3 * (1 + 3 * (1 + ne) + 2 * ne) + (S * S - S) * (12 + 34 * (1 + ne) + 12 * ne)  # noqa: E731
+    img_step = lambda c, S: img_gauge(S) if gauges[c] else nv * flops_expm(S) + prod(S) * (1 + 3 * nz)  # noqa: E731
     if walk:
         # image walk (grape_walk.hpp k_walk_img) per (step, sector): the nv variant
         # exponentials, the chain product Q <- E Q and per image Z = E^dag dX, Y = Q^dag Z Q (3
         # products); HBM: the x row and the nz images written.  k_img_fdx (reported under
         # "k_grad/k_err_local") reads Z1 and M'_c; k_err_grad reads W, Z1, Z2 per (step, error).
-        flop_model = {"k_walk_fwd": L * NT * per_step(lambda S: nv * flops_expm(S) + prod(S) * (1 + 3 * nz)),
+        flop_model = {"k_walk_fwd": L * NT * sum(ns * img_step(c, S) for c, (S, ns) in enumerate(classes)),
                       "k_err_grad": L * NT * ne * 2 * per_step(prod)}
         byte_model = {"k_walk_fwd": L * 8 * (NT + 1) + L * NT * nz * per_step(tile),
                       "k_grad/k_err_local": L * NT * per_step(tile),
@@ -614,7 +620,8 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
         "config": {"workload": "C3: Rydberg CZ d=9 + 4 error operators (Omega1, Omega2, delta1, delta2), N_t=512, "
                                "np=1, na=1; F, F_dx, F_d2err, F_d2err_dx",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
-                   "sectors": [{"levels": S, "sectors": ns} for S, ns in classes] if sec else None},
+                   "sectors": [{"levels": S, "sectors": ns} for S, ns in classes] if sec else None,
+                   "phase_covariant": [bool(g) for g in gauges[:len(classes)]]},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
@@ -625,8 +632,8 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     # the local-frame images (3 products each in the image walk: E^dag dX, Q^dag . Q), the B_k
     # recurrence and the contractions (+ the sector heads)
     nimg = 3 if walk else 2
-    exe = NT * per_step(lambda S: nv * flops_expm(S) + prod(S) + nz * nimg * prod(S) + ne * 2 * prod(S)
-                        + 8 * S ** 2 * (1 + ne))
+    exe = NT * sum(ns * ((img_step(c, S) if walk else nv * flops_expm(S) + prod(S) + nz * nimg * prod(S))
+                         + ne * 2 * prod(S) + 8 * S ** 2 * (1 + ne)) for c, (S, ns) in enumerate(classes))
     if sec:
         exe += (16 + 24 * ne) * 8 * D ** 3
     out["roofline"]["whole_eval"] = {"flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
@@ -1068,7 +1075,7 @@ def main():
             out = c5_report(args, B, L, world, value, elapsed, ktimes, d, nt, nparam)
         elif c3:
             out = c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors,
-                            args.steps * ((count + L - 1) // L))
+                            args.steps * ((count + L - 1) // L), info)
         else:
             out = c2_report(args, B, L, world, value, elapsed, ktimes, sectors,
                             args.steps * ((count + L - 1) // L), info)

@@ -862,25 +862,39 @@ __device__ __forceinline__ cd gauge_rho(cd q, int n) {
     for (int m = 0; m < n; ++m) r = cadd(cadd(r, q), cmul(q, r));
     return r;
 }
-// E~ = exp(-i dt H_w(0)) of the lane's NE sectors (the nominal build at x = 0; no diagonal shift, so
-// E~ carries its own phase), into Et -- the same bits in the forward and the gradient walk
-template <int D, int NE, bool FENCE>
+// E~ = exp(-i dt H_w(0)) of the workgroup's NE sectors (the nominal build at x = 0; no diagonal shift,
+// so E~ carries its own phase), into every lane's Et.  Every lane of a workgroup walks the same
+// sectors (walk_lane: w0 = NS * blockIdx.y), so lane w < NE computes sector w's exponential into LDS
+// once for the whole workgroup -- the same code, hence the same bits, in the forward and the
+// gradient walk.  (Every lane of the workgroup reaches the barrier: the pair kernels give each
+// workgroup to one class.)
+template <int D, int NE>
 __device__ __forceinline__ void gauge_base(const DevProblem &P, cptr<cd> ops, cd *scr, cd (&Et)[NE][D][D]) {
-    WalkX X0;
-    X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
-    Pert none;
-    none.var = -1;
-    none.index = 0;
-    none.delta = 0.0;
-    SM<D> A[NE];
-    walk_build<D, NE>(P, ops, X0, 1, none, A);
+    __shared__ cd gE[NE * D * D];
+    if ((int)threadIdx.x < NE) {
+        const int w = threadIdx.x;
+        WalkX X0;
+        X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
+        Pert none;
+        none.var = -1;
+        none.index = 0;
+        none.delta = 0.0;
+        SM<D> A[1];
+        walk_build<D, 1>(P, ops + (size_t)w * P.sec_ops, X0, 1, none, A);
+        double mu0 = 0.0;
+        walk_expm<D, false, true, false>(A[0], scr, mu0, true, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) gE[(w * D + j) * D + i] = x[j];
+        });
+    }
+    __syncthreads();
 #pragma unroll
     for (int w = 0; w < NE; ++w) {
-        double mu0 = 0.0;
-        walk_expm<D, FENCE, true, false>(A[w], scr + (size_t)w * 2 * D * D, mu0, true, [&](int i, const cd (&x)[D]) {
 #pragma unroll
-            for (int j = 0; j < D; ++j) Et[w][j][i] = x[j];
-        });
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) Et[w][j][i] = gE[(w * D + j) * D + i];
+        }
     }
 }
 // the level phases d_j = e^{i theta N_j} of one sector from p = e^{i theta}
@@ -944,7 +958,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
     cd Et[GAUGE ? NE : 1][D][D];  // GAUGE: E~ of the lane's sectors
     GaugeN<D> gn[GAUGE ? NE : 1];
     if constexpr (GAUGE) {
-        gauge_base<D, NE, C::FENCE_FWD>(P, ops, scr, Et);
+        gauge_base<D, NE>(P, ops, scr, Et);
 #pragma unroll
         for (int w = 0; w < NE; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
     }
@@ -1116,7 +1130,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
     GaugeN<D> gn[GAUGE ? NE : 1];
     cd rho[GAUGE ? NE : 1][D];    // GAUGE: e^{i phi N_j} - 1 of this step
     if constexpr (GAUGE) {
-        gauge_base<D, NE, C::FENCE>(P, ops, scr, Et);
+        gauge_base<D, NE>(P, ops, scr, Et);
 #pragma unroll
         for (int w = 0; w < NE; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
     }
