@@ -1,0 +1,128 @@
+"""Extended-precision restatement of the reference's fidelity gradient: the value the reference's
+forward differences would return without rounding in the exponentials, the chain and the traces.
+
+TEST INFRASTRUCTURE ONLY (like grape_oracle.py): used by tests/ and scripts/probes/ as a second
+checker, never by robustgrape_amd/.
+
+The reference (FidelityCalculations.jl:19-119 over UnitaryCalculations.jl:20-155) computes, with
+eps = 1e-8 (Types.jl:38) and the controls and Hamiltonians in double precision,
+  E_k = exp(-i dt H0(k, x_k, x_add)),  C_k = E_k C_{k-1}                     (UnitaryCalculations.jl:45-47)
+  U_dx[p, k] = U C_k^-1 (exp(-i dt H0(k, x_k + eps e_p, x_add)) - E_k) / eps C_{k-1}   (:48-56, :114-118)
+  U0_dx_add[q] = (U0(x_add + eps e_q) - U0(x_add)) / eps                       (FidelityCalculations.jl:32-40)
+  F, F_dx, F_dx_add                                                          (:47-76)
+in double arithmetic, so every implementation's F_dx carries its own u / eps rounding noise (its
+exponential's rounding and the rounding of the Hamiltonian's trig, amplified by 1 / eps).  Here the
+SAME inputs -- the controls and the perturbed control fl(x + eps) as the reference forms it, the
+operators and the target in double -- go through the Hamiltonian's coefficients (operator bases;
+closures stay double), exponentials (Taylor 30 with scaling and squaring), products and traces in
+numpy longdouble (64-bit mantissa: the result's own noise is ~1e-19 / 1e-8 = 1e-11 of |F_dx|); an
+operator-basis target likewise.  What is left is the forward difference itself, O(eps) truncation
+included: the quantity
+the reference means to return, against which the noise of the oracle, the C++ port and the device
+paths can each be read off (scripts/probes/fd_exact_probe.py, tests/test_gpu_gauge.py).
+
+Scope: no error sources (F, F_dx, F_dx_add), H0 free of x_add (the target part of F_dx_add only).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+LD = np.clongdouble
+
+
+def exp_ld(A):
+    """exp of a longdouble complex matrix: Taylor 30 of A / 2^s with |A / 2^s|_1 <= 0.05, s squarings."""
+    n = float(np.max(np.sum(np.abs(A), axis=0)))
+    s = max(0, int(math.ceil(math.log2(n / 0.05)))) if n > 0.05 else 0
+    X = A / LD(2 ** s)
+    E = np.eye(A.shape[0], dtype=LD)
+    T = E.copy()
+    for k in range(1, 30):
+        T = T @ X / LD(k)
+        E = E + T
+    for _ in range(s):
+        E = E @ E
+    return E
+
+
+def _h0_ld(H0, k, xk, xa):
+    """H0(k, x_k, x_add) in longdouble: an operator basis (objects with .terms: op, var, index, func,
+    a, b, scale -- the grape_term fields) has its coefficients evaluated in longdouble from the double
+    controls, so the two propagators of a forward difference differ only through the exact change of
+    the control; any other closure is evaluated in double as the reference does."""
+    terms = getattr(H0, "terms", None)
+    if terms is None:
+        return np.asarray(H0(k, xk.copy(), xa.copy()), dtype=np.complex128).astype(LD)
+    H = np.zeros(terms[0].op.shape, dtype=LD)
+    for t in terms:  # var: 0 one, 1 x, 2 x_add, 3 step; func: 0 one, 1 linear, 2 cos, 3 sin, 4 cis
+        v = {0: np.longdouble(1), 1: np.longdouble(xk[t.index]) if t.var == 1 else 0,
+             2: np.longdouble(xa[t.index]) if t.var == 2 else 0, 3: np.longdouble(k)}[t.var]
+        arg = np.longdouble(t.a) * v + np.longdouble(t.b)
+        f = {0: LD(1), 1: LD(arg), 2: LD(np.cos(arg)), 3: LD(np.sin(arg)),
+             4: LD(np.cos(arg)) + LD(1j) * LD(np.sin(arg))}[t.func]
+        H = H + LD(complex(t.scale)) * f * np.asarray(t.op, dtype=np.complex128).astype(LD)
+    return H
+
+
+def _target_ld(target, xa):
+    """target_unitary(x_add) in longdouble for an operator basis (as _h0_ld), else in double."""
+    terms = getattr(target, "terms", None)
+    if terms is None:
+        return np.asarray(target(xa.copy()), dtype=np.complex128).astype(LD)
+    return _h0_ld(target, 1, np.zeros(0), xa)
+
+
+def fidelity_and_gradient(fp, x, nparam=1):
+    """(F, F_dx_tot) of calculate_fidelity_and_derivatives(fp, x), evaluated in longdouble."""
+    up = fp.unitary_problem
+    if len(up.error_sources):
+        raise ValueError("grape_exact covers problems without error sources")
+    nt, d, na = up.ntimes, up.ndim, up.nb_additional_param
+    eps = up.eps
+    dt = up.t0 / nt
+    x = np.asarray(x, dtype=np.float64)
+    xm = x[:len(x) - na].reshape(nt, nparam)
+    xa = x[len(x) - na:].copy()
+    Es, dEs = [], []
+    for k in range(nt):
+        E = exp_ld(LD(-1j * dt) * _h0_ld(up.H0, k + 1, xm[k], xa))
+        Es.append(E)
+        row = []
+        for p in range(nparam):
+            xp = xm[k].copy()
+            xp[p] = xp[p] + eps  # fl(x + eps): the perturbed control the reference forms
+            row.append((exp_ld(LD(-1j * dt) * _h0_ld(up.H0, k + 1, xp, xa)) - E) / LD(eps))
+        dEs.append(row)
+    C = [np.eye(d, dtype=LD)]
+    for E in Es:
+        C.append(E @ C[-1])
+    U = C[-1]
+    P0 = np.asarray(fp.projector, dtype=np.complex128)
+    P = P0.copy()
+    P[P != 0] = 1
+    Dn = float(np.real(np.trace(P0)))
+    P0, P = P0.astype(LD), P.astype(LD)
+    DD = Dn * (Dn + 1)
+    ct = lambda A: A.conj().T  # noqa: E731
+    tr_mod = lambda A: np.trace(P0 @ A)  # noqa: E731
+    U0 = _target_ld(fp.target_unitary, xa)
+    F = (np.real(tr_mod(P @ ct(U0) @ U @ P @ ct(U) @ U0)) + abs(tr_mod(P @ ct(U0) @ U)) ** 2) / DD
+    tau_c = np.conj(tr_mod(P @ ct(U0) @ U))
+    Fdx = np.zeros(len(x))
+    for k in range(nt):
+        for p in range(nparam):
+            Ud = U @ ct(C[k + 1]) @ dEs[k][p] @ C[k]  # C_k^-1 = C_k^dag (exact to 1e-19 here)
+            Fdx[k * nparam + p] = float(np.real(tr_mod(P @ ct(U0) @ Ud @ P @ ct(U) @ U0
+                                                       + P @ ct(U0) @ U @ P @ ct(Ud) @ U0))
+                                        + 2 * np.real(tau_c * tr_mod(P @ ct(U0) @ Ud))) / DD
+    for q in range(na):  # FidelityCalculations.jl:32-40, 67-76 with U_dx_add = 0 (H0 free of x_add)
+        xq = xa.copy()
+        xq[q] = xq[q] + eps
+        U0q = _target_ld(fp.target_unitary, xq)
+        U0d = (U0q - U0) / LD(eps)
+        Fdx[nt * nparam + q] = float(np.real(tr_mod(P @ ct(U0d) @ U @ P @ ct(U) @ U0
+                                                    + P @ ct(U0) @ U @ P @ ct(U) @ U0d))
+                                     + 2 * np.real(tau_c * tr_mod(P @ ct(U0d) @ U))) / DD
+    return float(F), Fdx

@@ -6,6 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
 TAG=${1:-r5}
 SKIP_PROFILE=1 SKIP_BENCH=${SKIP_BENCH:-} bash scripts/gpu_final.sh $TAG || exit $?
+timeout -k 10 600 python -u scripts/probes/fd_exact_probe.py --gpu > $OUT/${TAG}_fd_exact.log 2>&1 || { tail -5 $OUT/${TAG}_fd_exact.log; exit 1; }
+tail -5 $OUT/${TAG}_fd_exact.log | cut -c1-400
 timeout -k 10 300 python -u scripts/probes/dense_fd_noise.py 3m > $OUT/${TAG}_noise_3m.log 2>&1 || { tail -5 $OUT/${TAG}_noise_3m.log; exit 1; }
 tail -1 $OUT/${TAG}_noise_3m.log
 if [ -f robustgrape_amd/libgrape_4m.so ]; then

@@ -20,6 +20,8 @@ from tests import problems as P
 
 pytestmark = pytest.mark.gpu
 T1 = 1e-12
+# gauge walks against the exact (longdouble) forward difference: F_dx relative to max|F_dx| + absolute
+T_EXACT = (1e-9, 1e-12)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -86,6 +88,7 @@ def test_two_controls_per_step_are_not_phase_covariant():
 def test_gauge_walks_match_per_step_exponentials_and_oracle(name, fp, opts, batch):
     """Throughput (300: 8-wave scans) and latency-bound (5: 16-wave scans, pair kernels) plans,
     and a single call (the graph path)."""
+    from oracle import grape_exact as E
     from oracle import grape_oracle as O
     from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_SYMMETRY
     f = fp()
@@ -107,7 +110,19 @@ def test_gauge_walks_match_per_step_exponentials_and_oracle(name, fp, opts, batc
         _check(f"gauge_vs_exp_{name}_{batch}_{b}", out[0][b], out[1][b], ref[0][b], ref[1][b], P.fd_tier(f, X[b]))
     for b in (0, 1):
         F0, g0 = O.calculate_fidelity_and_derivatives(f, X[b])[:2]
-        _check(f"gauge_vs_oracle_{name}_{batch}_{b}", out[0][b], out[1][b], F0, g0, P.fd_tier(f, X[b]))
+        Fe, ge = E.fidelity_and_gradient(f, X[b])
+        # against the reference's forward difference evaluated without rounding (oracle/grape_exact.py):
+        # the phase sandwiches carry no exponential per step, hence none of its u / eps noise
+        # (the controls' entries; the x_add entry is the target's forward difference, which the head
+        # forms in double like the reference: the FD tier)
+        _check(f"gauge_vs_exact_{name}_{batch}_{b}", out[0][b], out[1][b][:nt], Fe, ge[:nt], T_EXACT)
+        _check(f"gauge_vs_exact_add_{name}_{batch}_{b}", out[0][b], out[1][b], Fe, ge, P.fd_tier(f, X[b]))
+        # against the oracle: the FD tier plus the oracle's own measured distance from the exact value
+        # (the reference's algorithm carries up to 2.3e-7 of max|F_dx| of u / eps noise on small
+        # gradients: scripts/probes/fd_exact_probe.py)
+        t2, t2a = P.fd_tier(f, X[b])
+        _check(f"gauge_vs_oracle_{name}_{batch}_{b}", out[0][b], out[1][b], F0, g0,
+               (t2, t2a + float(np.max(np.abs(np.asarray(g0) - ge)))))
 
 
 def test_gauge_bench_size_plan_against_c2_golden():
