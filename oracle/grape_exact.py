@@ -14,8 +14,9 @@ in double arithmetic, so every implementation's F_dx carries its own u / eps rou
 exponential's rounding and the rounding of the Hamiltonian's trig, amplified by 1 / eps).  Here the
 SAME inputs -- the controls and the perturbed control fl(x + eps) as the reference forms it, the
 operators and the target in double -- go through the Hamiltonian's coefficients (operator bases;
-closures stay double), exponentials (Taylor 30 with scaling and squaring), products and traces in
-numpy longdouble (64-bit mantissa: the result's own noise is ~1e-19 / 1e-8 = 1e-11 of |F_dx|); an
+closures stay double), exponentials (Taylor 40 with scaling and squaring), products and traces in
+numpy longdouble (64-bit mantissa: the result's own noise is ~1e-19 2^s / 1e-8 = 1e-11 2^s of |F_dx|
+with s the squarings of the largest step); an
 operator-basis target likewise.  What is left is the forward difference itself, O(eps) truncation
 included: the quantity
 the reference means to return, against which the noise of the oracle, the C++ port and the device
@@ -32,14 +33,20 @@ import numpy as np
 LD = np.clongdouble
 
 
+def squarings(norm1):
+    """Squarings exp_ld takes at |A|_1 = norm1 (its noise grows like 2^s: about 1e-19 * 2^s relative)."""
+    return max(0, int(math.ceil(math.log2(norm1)))) if norm1 > 1.0 else 0
+
+
 def exp_ld(A):
-    """exp of a longdouble complex matrix: Taylor 30 of A / 2^s with |A / 2^s|_1 <= 0.05, s squarings."""
+    """exp of a longdouble complex matrix: Taylor 40 of A / 2^s with |A / 2^s|_1 <= 1 (remainder below
+    1 / 41! = 3e-50), s squarings."""
     n = float(np.max(np.sum(np.abs(A), axis=0)))
-    s = max(0, int(math.ceil(math.log2(n / 0.05)))) if n > 0.05 else 0
+    s = squarings(n)
     X = A / LD(2 ** s)
     E = np.eye(A.shape[0], dtype=LD)
     T = E.copy()
-    for k in range(1, 30):
+    for k in range(1, 41):
         T = T @ X / LD(k)
         E = E + T
     for _ in range(s):
