@@ -115,6 +115,26 @@ def make_c5():
     print("wrote c5", F, hist.tolist())
 
 
+def make_c5_exact(precomputed=None):
+    """Add the exact (longdouble) forward difference of the C5 golden input to c5.npz (F_exact,
+    F_dx_exact; oracle/grape_exact.py, ~15 min of CPU): the tests read the oracle's own distance
+    from it as the checker's noise.  precomputed: an npz of scripts/probes/dense_exact_probe.py for
+    the same x."""
+    from oracle import grape_exact as E
+    from robustgrape_amd import synthetic as S
+    path = os.path.join(HERE, "c5.npz")
+    g = dict(np.load(path, allow_pickle=False))
+    if precomputed:
+        pre = dict(np.load(precomputed, allow_pickle=False))
+        assert np.array_equal(pre["x"], g["x"])
+        F, Fdx = float(pre["F"]), pre["F_dx"]
+    else:
+        F, Fdx = E.fidelity_and_gradient(S.dense_problem(), g["x"], nparam=2)
+    g["F_exact"], g["F_dx_exact"] = np.float64(F), np.asarray(Fdx)
+    np.savez_compressed(path, **g)
+    print("c5 exact: oracle - exact", float(np.max(np.abs(g["F_dx"] - Fdx))), "of", float(np.max(np.abs(Fdx))))
+
+
 def make_xadd_err():
     """Error sources with an H0 and an error generator that read x_add (tests/problems.py
     xadd_err_problem: d = 5, N_t = 40, na = 2, 2 errors), closures through the oracle."""
@@ -139,6 +159,8 @@ def make_c5err():
 if __name__ == "__main__":
     if sys.argv[1:] == ["c5"]:
         make_c5()
+    elif sys.argv[1:2] == ["c5_exact"]:
+        make_c5_exact(sys.argv[2] if len(sys.argv) > 2 else None)
     elif sys.argv[1:] == ["c5err"]:
         make_c5err()
     elif sys.argv[1:] == ["xadd_err"]:

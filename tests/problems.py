@@ -153,6 +153,16 @@ def fd_factor(fp, X, nparam=1):
     return max(1.0, max_step_norm(fp, X, nparam) / JULIA_THETA13)
 
 
+def tensor_factor(fp, X, nparam=1):
+    """The step-norm factor for UNCONTRACTED finite-difference tensors (U_dx, U_derr, U_derr_dx of
+    calculate_unitary_and_derivatives): max(1, max_k |dt H_k|_1) beyond the no-squaring range, like
+    T0.  An entry of (E' - E) / eps carries the exponential's own rounding, ~u |A|_1 per entry, over
+    eps; the traces of the fidelity path average it (fd_factor's 5.4 rule), a single tensor entry
+    does not."""
+    n = max_step_norm(fp, X, nparam)
+    return 1.0 if n <= 0.25 else max(1.0, n)
+
+
 def random_x(ntimes, seed, nparam=1, small=False):
     """x_main = 2pi*U (runtests.jl:335) or 2pi*0.001*U (examples/time_optimal_cz.jl:32); theta = 2pi*U."""
     rng = np.random.default_rng(seed)

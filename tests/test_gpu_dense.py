@@ -2,11 +2,17 @@
 through the C ABI, against the CPU oracle (live, small sizes) and the committed
 C5 golden fixture (d = 64, N_t = 1024).
 
-Tolerances (SURVEY.md 8c tiers; DESIGN.md 2):
+Tolerances (SURVEY.md 8c tiers; DESIGN.md 2, 7):
   T0  exp(A)          <= 1e-13 relative x max(1, |A|_1); Pade 13 (where this engine
                        takes extra squarings to keep its pivot-free solve safe) 1e-12
   T1  F               <= 1e-12 absolute
-  T2  F_dx            <= 1e-6 max|ref| + 1e-7
+  T2  F_dx            <= 1e-6 max|ref| + 1e-9 + |ref - exact|
+      where exact is the reference's forward difference evaluated in longdouble
+      (oracle/grape_exact.py) and |ref - exact| the checker's own u / eps noise: at d = 16 the
+      oracle (Julia's exp! restated) already sits 5.8e-7 of max|F_dx| from it and the C++ port
+      1.1e-6 (scripts/probes/dense_exact_probe.py), so two correct double implementations differ
+      by up to their two noises.  The device result is also checked against exact directly:
+      <= 1e-6 max|exact| + 1e-9.  (Round 4 used a blanket + 1e-7, 350x the tier at C5.)
 """
 import os
 
@@ -18,7 +24,8 @@ from robustgrape_amd import synthetic as S
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 T1 = 1e-12
-T2, T2_ABS = 1e-6, 1e-7
+T2, T2_FLOOR = 1e-6, 1e-9
+T2_ABS = 1e-7  # the error-path tiers below (F_d2err: eps-FD of the error images, T3: eps2 stencils)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -28,10 +35,43 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def _assert_fid(F, Fdx, ref_F, ref_Fdx):
-    assert abs(F - ref_F) <= T1, (F, ref_F)
-    err = np.max(np.abs(Fdx - ref_Fdx))
-    assert err <= T2 * np.max(np.abs(ref_Fdx)) + T2_ABS, (err, np.max(np.abs(ref_Fdx)))
+def _assert_fid(F, Fdx, ref_F, ref_Fdx, test="dense", exact=None, spread=0.0):
+    """F at T1; F_dx against the checker at T2 with the checker's own distance from the exact
+    forward difference added (exact: (F, F_dx) of oracle/grape_exact.py, when evaluated), and
+    against exact itself at T2 + 1e-9."""
+    from tests.parity_log import record
+    ef = abs(F - ref_F)
+    record(test, "F", ef, 1.0, T1)
+    assert ef <= T1, (F, ref_F)
+    noise = spread
+    if exact is not None:
+        noise = float(np.max(np.abs(np.asarray(ref_Fdx) - exact[1])))
+        ee = float(np.max(np.abs(Fdx - exact[1])))
+        se = float(np.max(np.abs(exact[1])))
+        record(test + "_vs_exact", "F_dx", ee, se, T2 * se + T2_FLOOR)
+        assert ee <= T2 * se + T2_FLOOR, ("vs exact", ee, se)
+    err, scale = float(np.max(np.abs(Fdx - ref_Fdx))), float(np.max(np.abs(ref_Fdx)))
+    tol = T2 * scale + T2_FLOOR + noise
+    record(test, "F_dx", err, scale, tol)
+    print(f"{test}: F_dx err {err:.3e} (rel {err / scale:.2e}), checker noise {noise:.2e}, tol {tol:.2e}")
+    assert err <= tol, (err, scale, noise)
+
+
+def _cpu_spread(fp, x, ref_Fdx):
+    """Where no exact evaluation exists (x_add-dependent H0, error sources): the checker's noise
+    estimated by the spread of two correct CPU implementations of the reference's algorithm
+    (the oracle and the C++ port, oracle/cref) -- (None-like) 0 when the port is not built."""
+    try:
+        from oracle.cref import cref
+        if not cref.available():
+            return 0.0
+        return float(np.max(np.abs(np.asarray(cref.fidelity_grad(fp, x)[1]) - np.asarray(ref_Fdx))))
+    except Exception:
+        return 0.0
+
+
+def _assert_fid_spread(F, Fdx, ref_F, ref_Fdx, test, fp, x):
+    _assert_fid(F, Fdx, ref_F, ref_Fdx, test, spread=_cpu_spread(fp, x, ref_Fdx))
 
 
 def _skew_hermitian(d, norm, rng):
@@ -76,11 +116,12 @@ def test_dense_fidelity_gradient_matches_live_oracle(d, ntimes, scale):
     """Edge sizes: one step, chunk remainders, padded d, Pade 3..9 (scale moves |A|_1)."""
     from oracle import grape_oracle as O
     from robustgrape_amd import calculate_fidelity_and_derivatives
+    from oracle import grape_exact as E
     fp = S.dense_problem(d, ntimes, rank=min(16, d - 3), scale=scale)
     x = S.dense_x(ntimes, seed=300 + ntimes)
     F0, g0, _, _ = O.calculate_fidelity_and_derivatives(fp, x)
     F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
-    _assert_fid(F, g, F0, g0)
+    _assert_fid(F, g, F0, g0, f"dense_live_d{d}_nt{ntimes}_s{scale}", E.fidelity_and_gradient(fp, x, nparam=2))
     assert d2.shape == (0,) and d2dx.shape == (len(x), 0)
 
 
@@ -89,7 +130,8 @@ def test_c5_matches_golden():
     from robustgrape_amd import calculate_fidelity_and_derivatives
     g = dict(np.load(os.path.join(GOLDEN, "c5.npz"), allow_pickle=False))
     F, Fdx, _, _ = calculate_fidelity_and_derivatives(S.dense_problem(), g["x"])
-    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    exact = (float(g["F_exact"]), g["F_dx_exact"]) if "F_dx_exact" in g else None
+    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"], "c5_golden", exact)
 
 
 def test_dense_batch_equals_single():
@@ -160,7 +202,7 @@ def test_dense_xadd_dependent_h0_matches_live_oracle(d, ntimes):
     x = np.concatenate([S.dense_x(ntimes, seed=500 + ntimes), [0.7, -0.3]])
     ref = O.calculate_fidelity_and_derivatives(fp, x)
     F, g, _, _ = calculate_fidelity_and_derivatives(fp, x)
-    _assert_fid(F, g, ref[0], ref[1])
+    _assert_fid_spread(F, g, ref[0], ref[1], f"dense_xadd_d{d}_nt{ntimes}", fp, x)
     assert g.shape == (len(x),) and abs(g[-1]) > 1e-6  # the H0 part of F_dx_add is not empty
 
 
@@ -202,7 +244,7 @@ def test_dense_error_sources_match_live_oracle(d, ntimes, nerr, phase, scale):
         x = np.concatenate([x, [0.7]])
     ref = O.calculate_fidelity_and_derivatives(fp, x)
     F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
-    _assert_fid(F, g, ref[0], ref[1])
+    _assert_fid_spread(F, g, ref[0], ref[1], f"dense_err_d{d}_nt{ntimes}", fp, x)
     _assert_err(d2, d2dx, ref[2], ref[3])
     assert d2.shape == (nerr,) and d2dx.shape == (len(x), nerr)
 
@@ -213,7 +255,7 @@ def test_c5err_matches_golden():
     g = dict(np.load(os.path.join(GOLDEN, "c5err.npz"), allow_pickle=False))
     fp = S.dense_error_problem(64, int(g["ntimes"]))
     F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(fp, g["x"])
-    _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
+    _assert_fid_spread(F, Fdx, float(g["F"]), g["F_dx"], "c5err_golden", fp, g["x"])
     _assert_err(d2, d2dx, g["F_d2err"], g["F_d2err_dx"])
 
 

@@ -67,7 +67,7 @@ def test_closure_unitary_derivatives_above_12_levels():
     x = _x(fp, 77)
     ref = O.calculate_unitary_and_derivatives(fp.unitary_problem, x)
     got = calculate_unitary_and_derivatives(fp.unitary_problem, x)
-    fac = P.fd_factor(fp, x, nparam=2)
+    fac = P.tensor_factor(fp, x, nparam=2)  # uncontracted tensors (tests/problems.py)
     assert np.max(np.abs(got[0] - ref[0])) <= T1 * fac
     for n, (t, ta) in ((1, (T2, T2_ABS)), (3, (T2, T2_ABS)), (4, (T3, T3_ABS))):
         a, b = np.asarray(got[n]), np.asarray(ref[n])

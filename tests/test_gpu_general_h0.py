@@ -136,9 +136,9 @@ def test_decay_unitary_derivatives_and_interaction_operators(kind, nt, errs):
     got = calculate_unitary_and_derivatives(upd, x)
     assert np.max(np.abs(got[0] - ref[0])) <= T1
     assert abs(abs(np.linalg.det(ref[0])) - 1.0) > 1e-3  # not unitary
-    # the FD tiers scaled by max(1, max_k |dt H_k|_1), as tests/test_gpu_parity.py _assert_unitary: an
-    # uncontracted (E' - E) / eps carries the exponential's rounding (squarings) over eps
-    fac = P.fd_factor(_mk(kind, nt, errs, False), x)
+    # uncontracted FD tensors: tests/problems.py tensor_factor (as tests/test_gpu_parity.py
+    # _assert_unitary): an entry of (E' - E) / eps carries the exponential's rounding over eps
+    fac = P.tensor_factor(_mk(kind, nt, errs, False), x)
     for n, (tol, atol) in ((1, (T2 * fac, T2_ABS)), (2, (T2 * fac, T2_ABS)), (3, (T2 * fac, T2_ABS)),
                            (4, (T3 * fac, T3_ABS)), (5, (T3 * fac, T3_ABS))):
         a, b = np.asarray(got[n]), np.asarray(ref[n])

@@ -280,7 +280,7 @@ def test_large_batch_plan_matches_single():
 # ---------------------------------------------------------------- materialised derivatives
 def _assert_unitary(got, ref, fac=1.0):
     """T1 for U; T2 for eps quantities (U_dx, U_dx_add, U_derr); T3 for the eps2 mixed ones.
-    fac = max(1, max_k |dt H_k|_1) scales the FD tiers: an uncontracted (E' - E)/eps carries
+    fac = tests/problems.py tensor_factor scales the FD tiers: an uncontracted (E' - E)/eps carries
     the exponential's rounding (T0: 1e-13 x max(1, |A|_1), squarings for Pade 13) over eps."""
     names = ("U", "U_dx", "U_dx_add", "U_derr", "U_derr_dx", "U_derr_dx_add")
     for name, g, r in zip(names, got, ref):
@@ -322,9 +322,7 @@ def test_unitary_derivatives_match_live_oracle(d, ntimes, nerr):
     up = mk(False).unitary_problem
     ref = O.calculate_unitary_and_derivatives(up, x)
     got = calculate_unitary_and_derivatives(mk(True).unitary_problem, x)
-    dt = up.t0 / ntimes
-    fac = max(1.0, max(np.abs(dt * up.H0(k + 1, x[k:k + 1], x[-1:])).sum(axis=0).max() for k in range(ntimes)))
-    _assert_unitary(got, ref, fac)
+    _assert_unitary(got, ref, P.tensor_factor(mk(False), x))
 
 
 def test_unitary_derivatives_consistent_with_fidelity_gradient():
