@@ -133,3 +133,110 @@ def fidelity_and_gradient(fp, x, nparam=1):
                                                     + P @ ct(U0) @ U @ P @ ct(U) @ U0d))
                                      + 2 * np.real(tau_c * tr_mod(P @ ct(U0d) @ U))) / DD
     return float(F), Fdx
+
+
+def _herr_ld(src, k, xk, xa, err):
+    """Herror_e(k, x_k, x_add, err) in longdouble (an operator-basis error is err * sum of terms)."""
+    H = src.Herror
+    if getattr(H, "terms", None) is None:
+        return np.asarray(H(k, xk.copy(), xa.copy(), err), dtype=np.complex128).astype(LD)
+    return LD(err) * _h0_ld(H, k, xk, xa)
+
+
+def fidelity_and_derivatives(fp, x, nparam=1):
+    """(F, F_dx_tot, F_d2err, F_d2err_dx_tot) of calculate_fidelity_and_derivatives(fp, x) with error
+    sources (UnitaryCalculations.jl:44-151, FidelityCalculations.jl:19-119), evaluated in longdouble:
+    the eps differences of the error propagators (:66-73) and the eps2 mixed stencils (:75-97, left to
+    right as the reference writes them), the cumulative sums (:112-113) and the assembly (:114-151).
+    Scope: H0 and Herror free of x_add (then U_dx_add and U_derr_dx_add are exactly zero in the
+    reference too; the target's difference remains in F_dx_add and F_d2err_dx_add)."""
+    up = fp.unitary_problem
+    nt, d, na, ne = up.ntimes, up.ndim, up.nb_additional_param, len(up.error_sources)
+    eps, eps2 = up.eps, up.eps2
+    dt = up.t0 / nt
+    x = np.asarray(x, dtype=np.float64)
+    xm = x[:len(x) - na].reshape(nt, nparam)
+    xa = x[len(x) - na:].copy()
+    cdt = LD(-1j * dt)
+    ct = lambda A: A.conj().T  # noqa: E731
+    C = np.eye(d, dtype=LD)
+    Vdx = np.zeros((nparam, nt, d, d), dtype=LD)
+    Verr = np.zeros((ne, nt, d, d), dtype=LD)
+    Vmix = np.zeros((nparam, ne, nt, d, d), dtype=LD)
+    for k in range(nt):
+        xk = xm[k].copy()
+        H0k = _h0_ld(up.H0, k + 1, xk, xa)
+        E = exp_ld(cdt * H0k)
+        Cold, C = C, E @ C
+        Ci = ct(C)  # the unitary chain's inverse (exact here to 1e-19)
+        Edx2 = []
+        for p in range(nparam):
+            xp = xk.copy()
+            xp[p] = xp[p] + eps
+            Vdx[p, k] = Ci @ ((exp_ld(cdt * _h0_ld(up.H0, k + 1, xp, xa)) - E) / LD(eps)) @ Cold
+            xp[p] = xk[p] + eps2
+            Edx2.append(exp_ld(cdt * _h0_ld(up.H0, k + 1, xp, xa)))
+        for e, src in enumerate(up.error_sources):
+            E1 = exp_ld(cdt * (_herr_ld(src, k + 1, xk, xa, eps) + H0k))
+            Verr[e, k] = Ci @ ((E1 - E) / LD(eps)) @ Cold
+            E2 = exp_ld(cdt * (_herr_ld(src, k + 1, xk, xa, eps2) + H0k))
+            for p in range(nparam):
+                xp = xk.copy()
+                xp[p] = xp[p] + eps2
+                Em = exp_ld(cdt * (_herr_ld(src, k + 1, xp, xa, eps2) + _h0_ld(up.H0, k + 1, xp, xa)))
+                Vmix[p, e, k] = Ci @ (((Em + E) - E2 - Edx2[p]) / LD(eps2 * eps2)) @ Cold
+    U = C
+    P0 = np.asarray(fp.projector, dtype=np.complex128)
+    P = P0.copy()
+    P[P != 0] = 1
+    Dn = float(np.real(np.trace(P0)))
+    P0, P = P0.astype(LD), P.astype(LD)
+    DD = Dn * (Dn + 1)
+    tr_mod = lambda A: np.trace(P0 @ A)  # noqa: E731
+    U0 = _target_ld(fp.target_unitary, xa)
+    U0d = []
+    for q in range(na):
+        xq = xa.copy()
+        xq[q] = xq[q] + eps
+        U0d.append((_target_ld(fp.target_unitary, xq) - U0) / LD(eps))
+    F = (np.real(tr_mod(P @ ct(U0) @ U @ P @ ct(U) @ U0)) + abs(tr_mod(P @ ct(U0) @ U)) ** 2) / DD
+    tau_c = np.conj(tr_mod(P @ ct(U0) @ U))
+    Fdx = np.zeros(nt * nparam + na)
+    for k in range(nt):
+        for p in range(nparam):
+            Ud = U @ Vdx[p, k]
+            Fdx[k * nparam + p] = float((np.real(tr_mod(P @ ct(U0) @ Ud @ P @ ct(U) @ U0
+                                                         + P @ ct(U0) @ U @ P @ ct(Ud) @ U0))
+                                         + 2 * np.real(tau_c * tr_mod(P @ ct(U0) @ Ud))) / DD)
+    for q in range(na):
+        Fdx[nt * nparam + q] = float((np.real(tr_mod(P @ ct(U0d[q]) @ U @ P @ ct(U) @ U0
+                                                     + P @ ct(U0) @ U @ P @ ct(U) @ U0d[q]))
+                                      + 2 * np.real(tau_c * tr_mod(P @ ct(U0d[q]) @ U))) / DD)
+    Fd2 = np.zeros(ne)
+    Fd2dx = np.zeros((nt * nparam + na, ne))
+    for e in range(ne):
+        S = np.cumsum(Verr[e], axis=0)                      # S[k] = sum_{j <= k}
+        R = np.flip(np.cumsum(np.flip(Verr[e], 0), axis=0), 0)  # R[k] = sum_{j >= k}
+        Ue = U @ S[-1]
+        Fd2[e] = float(2 * (np.real(tr_mod(P @ ct(U0) @ Ue @ P @ ct(Ue) @ U0 - P @ ct(Ue) @ Ue))
+                            + abs(tr_mod(P @ ct(U0) @ Ue)) ** 2
+                            - Dn * np.real(tr_mod(P @ ct(Ue) @ Ue))) / DD)
+        te_c = np.conj(tr_mod(P @ ct(U0) @ Ue))
+        for k in range(nt):
+            for p in range(nparam):
+                acc = Vmix[p, e, k].copy()
+                if k >= 1:
+                    acc = acc + Vdx[p, k] @ S[k - 1]
+                if k <= nt - 2:
+                    acc = acc + R[k + 1] @ Vdx[p, k]
+                Y = U @ acc
+                Fd2dx[k * nparam + p, e] = float(2 * (
+                    np.real(tr_mod(P @ ct(U0) @ Y @ P @ ct(Ue) @ U0 + P @ ct(U0) @ Ue @ P @ ct(Y) @ U0
+                                   - P @ ct(Y) @ Ue - P @ ct(Ue) @ Y))
+                    + 2 * np.real(te_c * tr_mod(P @ ct(U0) @ Y))
+                    - Dn * np.real(tr_mod(P @ ct(Y) @ Ue + P @ ct(Ue) @ Y))) / DD)
+        for q in range(na):  # U_derr_dx_add = 0 (H0, Herror free of x_add): the target's part only
+            Fd2dx[nt * nparam + q, e] = float(2 * (
+                np.real(tr_mod(P @ ct(U0d[q]) @ Ue @ P @ ct(Ue) @ U0 + P @ ct(U0) @ Ue @ P @ ct(Ue) @ U0d[q]))
+                + 2 * np.real(te_c * tr_mod(P @ ct(U0d[q]) @ Ue))) / DD)
+    return float(F), Fdx, Fd2, Fd2dx

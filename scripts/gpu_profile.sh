@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$PWD; OUT=$ROOT/gpurun_out; mkdir -p $OUT
 TAG=${1:-prof}; shift || true
-ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-host-paths --no-whole-matrix $*"
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline --no-host-paths --no-whole-matrix --no-c4-strong $*"
 faulted() { grep -qE "HSA_STATUS_ERROR|illegal memory access|Memory access fault|core dumped" "$1"; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_stats -o run -- \

@@ -163,17 +163,31 @@ def _err_scale(fp, x):
     return P.fd_factor(fp, x)
 
 
-def _assert_err(fp, d2, d2dx, ref_d2, ref_d2dx, test="", x=None):
+def _assert_err(fp, d2, d2dx, ref_d2, ref_d2dx, test="", x=None, exact=None):
+    """F_d2err / F_d2err_dx at T3 (scaled by fd_factor).  exact: (F, F_dx, F_d2err, F_d2err_dx) of
+    oracle/grape_exact.py for these inputs -- then the device must be no farther from the exact
+    forward differences than the checker (the reference's own algorithm) is, plus the tier, and
+    within the tier plus twice that distance of the checker (its noise and the device's own)."""
     from tests.parity_log import record
     f = 1.0 if x is None else _err_scale(fp, x)
     t3, t3a = T3 * f, T3_ABS * f
     nmain = d2dx.shape[0] - fp.unitary_problem.nb_additional_param
+    n0 = n1 = 0.0
+    if exact is not None:
+        n0 = float(np.max(np.abs(ref_d2 - exact[2])))
+        n1 = float(np.max(np.abs(ref_d2dx[:nmain] - exact[3][:nmain])))
+        x0, s0x = float(np.max(np.abs(d2 - exact[2]))), float(np.max(np.abs(exact[2])))
+        record(test + "_vs_exact", "F_d2err", x0, s0x, t3 * s0x + t3a + n0)
+        assert x0 <= t3 * s0x + t3a + n0, ("F_d2err vs exact", x0, n0)
+        x1, s1x = float(np.max(np.abs(d2dx[:nmain] - exact[3][:nmain]))), float(np.max(np.abs(exact[3][:nmain])))
+        record(test + "_vs_exact", "F_d2err_dx", x1, s1x, t3 * s1x + t3a + n1)
+        assert x1 <= t3 * s1x + t3a + n1, ("F_d2err_dx vs exact", x1, n1)
     e0, s0 = np.max(np.abs(d2 - ref_d2)), np.max(np.abs(ref_d2))
-    record(test, "F_d2err", e0, s0, t3 * s0 + t3a)
-    assert e0 <= t3 * s0 + t3a, (d2, ref_d2)
+    record(test, "F_d2err", e0, s0, t3 * s0 + t3a + 2 * n0)
+    assert e0 <= t3 * s0 + t3a + 2 * n0, (d2, ref_d2)
     err, scale = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain])), np.max(np.abs(ref_d2dx[:nmain]))
-    record(test, "F_d2err_dx", err, scale, t3 * scale + t3a)
-    assert err <= t3 * scale + t3a, err
+    record(test, "F_d2err_dx", err, scale, t3 * scale + t3a + 2 * n1)
+    assert err <= t3 * scale + t3a + 2 * n1, err
     ea = np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) if d2dx.shape[0] > nmain else 0.0
     record(test, "F_d2err_dx_add", ea, np.max(np.abs(ref_d2dx[nmain:])) if d2dx.shape[0] > nmain else 0.0,
            T3_XADD_ABS)
@@ -210,11 +224,13 @@ def test_error_path_small_problems_match_live_oracle(d, ntimes, errors):
     else:
         mk = lambda dev: P.full9_problem(ntimes, nerr=errors, device=dev)
     x = P.random_x(ntimes, 200 + ntimes)
+    from oracle import grape_exact as E
     F0, g0, d20, d2dx0 = O.calculate_fidelity_and_derivatives(mk(False), x)
     fp = mk(True)
     F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
     _assert_fid(F, g, F0, g0)
-    _assert_err(fp, d2, d2dx, d20, d2dx0, x=x)
+    _assert_err(fp, d2, d2dx, d20, d2dx0, test=f"live_err_d{d}_nt{ntimes}", x=x,
+                exact=E.fidelity_and_derivatives(fp, x))
 
 
 def test_error_sensitivity_gradient_identity_on_gpu():
