@@ -111,8 +111,12 @@ def test_device_exchange_matches_host_exchange(nslices):
     Fd, gd = time_sharded_fidelity_grad(fp, x, nparam=2, nslices=nslices, device_exchange=True)
     assert abs(Fd - Fh) <= 1e-14
     assert np.max(np.abs(gd - gh)) <= 1e-14 * max(1.0, float(np.max(np.abs(gh))))
+    from oracle import grape_exact as E
     F0, g0 = O.calculate_fidelity_and_derivatives(fp, x)[:2]
-    _check(f"timeshard_device_s{nslices}_oracle", Fd, gd, F0, np.asarray(g0))
+    Fe, ge = E.fidelity_and_gradient(fp, x, nparam=2)
+    _check(f"timeshard_device_s{nslices}_exact", Fd, gd, Fe, ge)
+    _check(f"timeshard_device_s{nslices}_oracle", Fd, gd, F0, np.asarray(g0),
+           t2a=T2_ABS + float(np.max(np.abs(np.asarray(g0) - ge))))
 
 
 def _device_exchange_worker(rank, world, port, q):
@@ -153,10 +157,14 @@ def test_ranks_exchange_device_buffers():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
+    from oracle import grape_exact as E
     fp = dense_problem(d=24, ntimes=41, dt=0.3, rank=8)
     F0, g0 = O.calculate_fidelity_and_derivatives(fp, dense_x(ntimes=41, seed=9))[:2]
+    Fe, ge = E.fidelity_and_gradient(fp, dense_x(ntimes=41, seed=9), nparam=2)
     for r, F, Fdx in out:
-        _check(f"timeshard_device_rank{r}_oracle", F, np.asarray(Fdx), F0, np.asarray(g0))
+        _check(f"timeshard_device_rank{r}_exact", F, np.asarray(Fdx), Fe, ge)
+        _check(f"timeshard_device_rank{r}_oracle", F, np.asarray(Fdx), F0, np.asarray(g0),
+               t2a=T2_ABS + float(np.max(np.abs(np.asarray(g0) - ge))))
 
 
 def test_rank_path_plan_follows_the_current_device():
