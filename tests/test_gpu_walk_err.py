@@ -204,7 +204,9 @@ def _symmetric_error_problem(nt, device=True):
     B = 10.0
     if device:
         H0 = R.rydberg_full_operator_basis(1.0, 1.0, 0.0, 0.0, B)
-        rabi = OperatorBasisError(list(R.full_rabi_error(1).terms) + list(R.full_rabi_error(2).terms))
+        # one operator pair for both atoms (each basis operator must keep the symmetry: the commutant
+        # is taken over the operators, grape_symmetry.hpp)
+        rabi = OperatorBasisError(R._drive_terms(*R._phase_pair(9, R._FULL_COUPLINGS, lambda w: 1.0)))
         dd = np.zeros(9)
         for i in (4, 6, 8):
             dd[i] += 1.0
