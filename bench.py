@@ -861,7 +861,9 @@ def c4_strong(make_step, world, rank, use_dist, sync, total=256, evals_per_resta
     from robustgrape_amd.sweep import gather_best, gather_best_local, shard
     first, count = shard(total, world, rank)
     step, F, X, ids, close = make_step(first, count)
-    for _ in range(3):
+    # warm-up: one whole sweep's worth of steps, so that the clocks have left the idle state the
+    # previous leg's teardown left them in (a 100-step sweep of 32 restarts lasts ~10 ms)
+    for _ in range(max(3, evals_per_restart)):
         step()
     sync()
     if use_dist:
