@@ -69,6 +69,11 @@ constexpr int kForkMaxBatch = GRAPE_FORK_MAX_BATCH;
 #define GRAPE_SCAN_PAIR_ALL 1
 #endif
 constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
+// chunks of a phase-covariant throughput walk class: (64 / S) / this per scan wave.  2: C2
+// 26.4 -> 29.0 M evals/s (4: 27.7 M; one GPU call, gpurun_out A/B r5chunk)
+#ifndef GRAPE_GAUGE_CHUNK_DIV
+#define GRAPE_GAUGE_CHUNK_DIV 2
+#endif
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
@@ -1377,7 +1382,10 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             if (Ps.walk && P.ne == 0 &&
                 (scan_override == kScanLatency || (scan_override == 0 && (long)R < (long)ncu)))
                 Ps.scan_waves = kScanLatency;
-            const int ncs = std::min(Ps.scan_waves * (64 / S), P.Nt);
+            // phase-covariant throughput classes: a step costs a few products instead of an
+            // exponential, so longer chunks (fewer per-lane prologues and a shorter scan) can pay
+            const int cdiv = (Ps.gauge && Ps.scan_waves == kScanTiny) ? GRAPE_GAUGE_CHUNK_DIV : 1;
+            const int ncs = std::max(1, std::min(Ps.scan_waves * (64 / S) / cdiv, P.Nt));
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
             grape_plan::SecBuf &b = p->sb[cl];
