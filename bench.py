@@ -531,9 +531,11 @@ def c4_points(fp, nparam, inputs, dev, batches=(256, 32), seconds=1.5):
         F = torch.empty(b, dtype=torch.float64, device=dev)
         G = torch.empty(b, X.shape[1], dtype=torch.float64, device=dev)
         step = lambda: plan.fidelity_grad_device_async(X.data_ptr(), F.data_ptr(), G.data_ptr(), b, 0, 0)  # noqa: E731
-        for _ in range(3):
-            step()
-        plan.synchronize()
+        tw = time.perf_counter()  # warm-up by the clock (the GPU leaves its idle state: see c4_strong)
+        while time.perf_counter() - tw < 0.3:
+            for _ in range(10):
+                step()
+            plan.synchronize()
         n, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds:
             for _ in range(10):
@@ -861,17 +863,27 @@ def c4_strong(make_step, world, rank, use_dist, sync, total=256, evals_per_resta
     from robustgrape_amd.sweep import gather_best, gather_best_local, shard
     first, count = shard(total, world, rank)
     step, F, X, ids, close = make_step(first, count)
-    # warm-up: one whole sweep's worth of steps, so that the clocks have left the idle state the
-    # previous leg's teardown left them in (a 100-step sweep of 32 restarts lasts ~10 ms)
-    for _ in range(max(3, evals_per_restart)):
-        step()
-    sync()
+    # warm-up by the clock, not by a step count: a whole sweep lasts 2-10 ms, less than the GPU
+    # needs to leave an idle state (scripts/probes/c4_strong_probe.py); 0.3 s of back-to-back sweeps
+    tw = time.perf_counter()
+    while True:
+        for _ in range(max(3, evals_per_restart)):
+            step()
+        sync()
+        if time.perf_counter() - tw >= 0.3:
+            break
+    # ... and the exchange once: the first use of its torch ops (and collectives) loads their code,
+    # ~0.4 s that a cold first sweep would count (measured 4.06 -> 0.025 ms per round)
     if use_dist:
+        gather_best(F, ids, X)
         dist.barrier()
+    else:
+        gather_best_local(F, ids, X)
     sync()
     t0 = time.perf_counter()
     for _ in range(evals_per_restart):
         step()
+    sync()  # the steps run on the plan's stream; the exchange below reads F on torch's
     if use_dist:
         fb, rid, owner, _ = gather_best(F, ids, X)
         dist.barrier()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 9
+#define GRAPE_ABI_VERSION 10
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -197,6 +197,12 @@ typedef struct grape_desc {
  * eps-variant's difference from the level phases: one exponential per walk lane instead of one per
  * step and variant.  This option keeps the per-step exponentials. */
 #define GRAPE_OPT_NO_GAUGE 8192
+/* One workgroup per evaluation (ABI 10): calls of at most 256 evaluations of a plan with the Rydberg
+ * sector layout (one 3-level and two 2-level phase-covariant classes, one control per step, no error
+ * sources) run each evaluation -- propagators, chain scan, head, gradient -- inside one workgroup,
+ * every intermediate in LDS; host-array calls read x from and write F, F_dx to
+ * mapped pinned memory.  This option keeps the pair-kernel pipeline. */
+#define GRAPE_OPT_NO_EVAL1 16384
 
 typedef struct grape_plan grape_plan;
 
@@ -443,7 +449,8 @@ typedef enum grape_kernel {
     GRAPE_KERNEL_DGRAD = 13,    /* dense engine: eps-variant propagators contracted in place */
     GRAPE_KERNEL_WALK_FWD = 14, /* sector chunk walks: propagators + chunk totals (grape_walk.hpp) */
     GRAPE_KERNEL_WALK_GRAD = 15,/* sector chunk walks: eps-variants contracted along the chunk */
-    GRAPE_NUM_KERNELS = 16
+    GRAPE_KERNEL_EVAL1 = 16,    /* one workgroup per evaluation (latency-bound calls, ABI 10) */
+    GRAPE_NUM_KERNELS = 17
 } grape_kernel;
 
 int grape_plan_set_profiling(grape_plan *plan, int enable);
@@ -469,6 +476,9 @@ int grape_plan_sector_info(grape_plan *plan, int *twin, int *symmetric, int max_
 /* Which sector classes run the phase-covariant walks (ABI 9; GRAPE_OPT_NO_GAUGE): gauge[c] = 1 per
  * class; returns the number of classes (1 for whole matrices, gauge[0] = 0). */
 int grape_plan_gauge_info(grape_plan *plan, int *gauge, int max_classes);
+/* 1 when every call of the plan runs one workgroup per evaluation (ABI 10; GRAPE_OPT_NO_EVAL1 above:
+ * an eligible layout and max_batch <= 256), 0 otherwise, or a negative grape_status. */
+int grape_plan_eval1(grape_plan *plan);
 
 /*
  * Symmetry-adapted basis (ABI 8, host only: no device needed).  The unitary V (ndim x ndim,

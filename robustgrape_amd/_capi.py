@@ -27,11 +27,11 @@ EXPORTED = ["grape_abi_version", "grape_build_id", "grape_last_error", "grape_de
             "grape_expectation_values_tables", "grape_plan_sectors", "grape_lbfgs_ls_init", "grape_lbfgs_ls_begin",
             "grape_lbfgs_ls_end", "grape_lbfgs_step", "grape_robust_cost", "grape_slice_forward",
             "grape_slice_gradient", "grape_symmetry_basis", "grape_plan_sector_info", "grape_lbfgs_async_advance",
-            "grape_slice_forward_device", "grape_slice_gradient_device", "grape_plan_gauge_info"]
+            "grape_slice_forward_device", "grape_slice_gradient_device", "grape_plan_gauge_info", "grape_plan_eval1"]
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad/k_err_local", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad",
-                "k_walk_fwd", "k_walk_grad"]
-ABI_VERSION = 9  # GRAPE_ABI_VERSION in include/grape.h
+                "k_walk_fwd", "k_walk_grad", "k_eval1"]
+ABI_VERSION = 10  # GRAPE_ABI_VERSION in include/grape.h
 
 
 class GrapeError(RuntimeError):
@@ -117,6 +117,8 @@ def lib():
         L.grape_plan_sector_info.restype = ctypes.c_int
         L.grape_plan_gauge_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.grape_plan_gauge_info.restype = ctypes.c_int
+        L.grape_plan_eval1.argtypes = [vp]
+        L.grape_plan_eval1.restype = ctypes.c_int
         L.grape_symmetry_basis.argtypes = [ctypes.POINTER(CDesc), dp, ctypes.POINTER(ctypes.c_int)]
         L.grape_symmetry_basis.restype = ctypes.c_int
         if L.grape_abi_version() != ABI_VERSION:

@@ -24,11 +24,12 @@ UNITARY = os.path.join(CSRC, "grape_unitary.hip")
 LBFGS = os.path.join(CSRC, "grape_lbfgs.hip")
 PROJ = os.path.join(CSRC, "grape_projector.hip")
 WALK = os.path.join(CSRC, "grape_walk_inst.hip")
+EVAL1 = os.path.join(CSRC, "grape_eval1.hip")
 DIMS = list(range(2, 13))  # GRAPE_DIMS in grape_launch.hpp; GRAPE_MAX_SMALL_DIM = 12
-SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS, PROJ, WALK]
+SOURCES = [ENGINE, INST, DENSE, UNITARY, LBFGS, PROJ, WALK, EVAL1]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in
                   ("grape_device.hpp", "grape_kernels.hpp", "grape_errpath.hpp", "grape_launch.hpp", "grape_lane.hpp",
-                   "grape_walk.hpp", "grape_walk_api.hpp",
+                   "grape_walk.hpp", "grape_walk_api.hpp", "grape_eval1_api.hpp",
                    "grape_dense.hpp", "grape_dense_api.hpp", "grape_unitary_api.hpp",
                    "grape_projector_api.hpp")] + \
     [os.path.join(ROOT, "include", "grape.h")]
@@ -74,7 +75,9 @@ def _units(defines):
              (UNITARY, [], os.path.join(sub, "grape_unitary.o")), (LBFGS, [], os.path.join(sub, "grape_lbfgs.o")),
              (PROJ, [], os.path.join(sub, "grape_projector.o")),
              # the chunk walks: no MachineLICM (grape_walk.hpp explains the register budget)
-             (WALK, ["-mllvm", "-disable-machine-licm"], os.path.join(sub, "grape_walk.o"))]
+             (WALK, ["-mllvm", "-disable-machine-licm"], os.path.join(sub, "grape_walk.o")),
+             # the one-workgroup-per-evaluation kernel (latency-bound calls): the walks' arithmetic
+             (EVAL1, ["-mllvm", "-disable-machine-licm"], os.path.join(sub, "grape_eval1.o"))]
     units += [(INST, [f"-DGRAPE_INST_DIM={d}"], os.path.join(sub, f"grape_inst_d{d}.o")) for d in DIMS]
     return sub, units
 

@@ -24,6 +24,7 @@
 #include "grape_dense_api.hpp"
 #include "grape_unitary_api.hpp"
 #include "grape_symmetry.hpp"
+#include "grape_eval1_api.hpp"
 
 // instantiated in grape_inst.hip (one translation unit per dimension)
 namespace grape_host {
@@ -77,6 +78,14 @@ constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
+// One workgroup per evaluation (grape_eval1.hip) for every call of an eligible plan (the Rydberg
+// layout with phase-covariant classes) whose max_batch is at most this: a plan-level choice, so that a
+// single evaluation and the same evaluation inside a batch stay bit-identical on every plan
+// (GRAPE_OPT_NO_EVAL1 turns it off)
+#ifndef GRAPE_EVAL1_MAX_BATCH
+#define GRAPE_EVAL1_MAX_BATCH 256
+#endif
+constexpr int kEval1MaxBatch = GRAPE_EVAL1_MAX_BATCH;
 constexpr int kCtrlInts = 8;  // [0..1] single-eval counters, [2] status, [4..5] pipeline overflow counters
 using grape_host::KMark;
 using grape_host::launch_pipeline;
@@ -197,6 +206,15 @@ struct grape_plan {
     SecBuf sb[2];
     int *d_fixed = nullptr;
     grape_proj::SectorHead SH{};
+    // one workgroup per evaluation (grape_eval1.hip): eligible plan, its E~ tables, class A's index
+    bool e1 = false;
+    cd *d_e1_Et = nullptr, *d_e1_scr = nullptr;
+    int e1_pa = 0;
+    // GRAPE_EVAL1_TRACE=1: workgroup 0's phase clocks of every host-array call, averaged and printed
+    // to stderr when the plan is destroyed (mapped pinned buffer; a tuning aid)
+    long long *e1_trace = nullptr, *e1_trace_d = nullptr;
+    double e1_phase[16] = {0};
+    long e1_calls = 0;
     // symmetry-adapted sectors (grape_symmetry.hpp): the head's rotated operators, projector, weights
     bool symmetry = false;
     cd *d_ops_sym = nullptr, *d_opsT_sym = nullptr, *d_PA_sym = nullptr, *d_PB_sym = nullptr;
@@ -236,6 +254,7 @@ struct grape_plan {
     };
     std::vector<GraphEntry> graphs;
     double *h_x = nullptr, *h_F = nullptr, *h_Fd2 = nullptr, *h_Fd2dx = nullptr;  // pinned
+    double *hd_x = nullptr, *hd_F = nullptr;  // ... h_x and h_F as the device sees them (eval1 calls)
     // graph path: F ([kGraphBatch]) and F_dx ([nb][nx]) of a call side by side in one device block
     // (h_F is its pinned image), so one D2H copy returns both
     double *d_gout = nullptr;
@@ -267,6 +286,19 @@ struct grape_plan {
 static void free_plan(grape_plan *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
+    if (p->e1_trace) {
+        if (p->e1_calls > 0) {
+            std::fprintf(stderr, "[grape eval1 trace] %ld calls, mean clocks per phase:", p->e1_calls);
+            for (int i = 0; i < 9; ++i) std::fprintf(stderr, " %.0f", p->e1_phase[i] / p->e1_calls);
+            std::fprintf(stderr, " (x+tables, totals, wave scan, sync, carry, head, grad, sync, store);"
+                                 " clocks per us %.1f; head wave: sums %.0f, reduce+F %.0f, M blocks %.0f,"
+                                 " x_add %.0f; phase A: head wave %.0f, class B %.0f\n", p->e1_phase[9] / p->e1_calls,
+                                 p->e1_phase[10] / p->e1_calls, p->e1_phase[11] / p->e1_calls,
+                                 p->e1_phase[12] / p->e1_calls, p->e1_phase[13] / p->e1_calls,
+                                 p->e1_phase[14] / p->e1_calls, p->e1_phase[15] / p->e1_calls);
+        }
+        (void)hipHostFree(p->e1_trace);
+    }
     void *bufs[] = {p->d_ops, p->d_opsT, p->d_h0, p->d_tgt, p->d_err, p->d_err_off, p->d_W, p->d_E, p->d_Q, p->d_Mc,
                     p->d_x, p->d_F, p->d_Fdx, p->d_part, p->d_tgt_part, p->d_ovf, p->d_ctrl, p->d_sink,
                     p->d_Carry, p->d_Ub, p->d_Me, p->d_vs, p->d_Fd2, p->d_Fd2dx, p->d_part_err, p->d_Zl, p->d_ovf2, p->d_ovf2_slots,
@@ -276,7 +308,7 @@ static void free_plan(grape_plan *p) {
                     p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
                     p->d_fixed, p->d_gout, p->d_slice, p->d_ops_sym, p->d_opsT_sym, p->d_PA_sym, p->d_PB_sym,
-                    p->d_W_sym};
+                    p->d_W_sym, p->d_e1_Et, p->d_e1_scr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
@@ -1459,6 +1491,29 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             H.MsecE[cl] = b.MsecE;
         }
         p->ncls = (int)ss.cls.size();
+        // latency-bound calls of the Rydberg layout with phase-covariant classes: one workgroup per
+        // evaluation (grape_eval1.hip), with E~ of each class computed here once
+        if (p->ncls == 2 && (long)MB <= kEval1MaxBatch && !(P.opts & GRAPE_OPT_NO_EVAL1)) {
+            int pa = 0, pb = 1;
+            if (grape_walk::pair_ok(p->Ps[1], p->Ps[0])) std::swap(pa, pb);
+            if (grape_walk::pair_ok(p->Ps[pa], p->Ps[pb]) && grape_eval1::eligible(p->Ps[pa], p->Ps[pb], H)) {
+                if (dalloc(&p->d_e1_Et, (size_t)p->Ps[pa].D * p->Ps[pa].D + 8) != hipSuccess ||
+                    dalloc(&p->d_e1_scr, (size_t)2 * 2 * 16) != hipSuccess)
+                    return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (eval1)"));
+                const hipError_t e = grape_eval1::prepare(p->Ps[pa], p->Ps[pb], p->d_e1_Et,
+                                                          p->d_e1_Et + (size_t)p->Ps[pa].D * p->Ps[pa].D, p->d_e1_scr,
+                                                          p->stream);
+                if (e != hipSuccess || hipStreamSynchronize(p->stream) != hipSuccess)
+                    return bail(fail(GRAPE_ERR_HIP, "eval1 preparation failed"));
+                p->e1 = true;
+                p->e1_pa = pa;
+                const char *tr = std::getenv("GRAPE_EVAL1_TRACE");
+                if (tr && tr[0] == '1' &&
+                    (hipHostMalloc(reinterpret_cast<void **>(&p->e1_trace), 32 * sizeof(long long), hipHostMallocDefault) != hipSuccess ||
+                     hipHostGetDevicePointer(reinterpret_cast<void **>(&p->e1_trace_d), p->e1_trace, 0) != hipSuccess))
+                    return bail(fail(GRAPE_ERR_ALLOC, "eval1 trace buffer"));
+            }
+        }
         if (p->ncls == 2 && (hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess ||
                              hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
                              hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess))
@@ -1493,6 +1548,11 @@ int grape_plan_gauge_info(grape_plan *p, int *gauge, int max_classes) {
     for (int c = 0; c < n && c < max_classes; ++c)
         if (gauge) gauge[c] = p->ncls ? p->Ps[c].gauge : 0;
     return n;
+}
+
+int grape_plan_eval1(grape_plan *p) {
+    if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
+    return p->e1 ? 1 : 0;
 }
 
 void grape_plan_destroy(grape_plan *plan) { free_plan(plan); }
@@ -1543,6 +1603,21 @@ static grape_dense::DenseBatch dense_batch(grape_plan *p, int nb, const double *
     return DB;
 }
 
+static grape_eval1::Args eval1_args(const grape_plan *p, const double *x, double *F, double *Fdx) {
+    grape_eval1::Args A{};
+    A.PA = p->Ps[p->e1_pa];
+    A.PB = p->Ps[1 - p->e1_pa];
+    A.H = p->SH;
+    A.EtA = p->d_e1_Et;
+    A.EtB = p->d_e1_Et + (size_t)A.PA.D * A.PA.D;
+    A.x = x;
+    A.F = F;
+    A.Fdx = Fdx;
+    A.a_first = p->e1_pa == 0 ? 1 : 0;
+    A.trace = p->e1_trace_d;
+    return A;
+}
+
 // One launch sequence of `nb` evaluations on the plan's stream over workspace rows
 // [0, nb).  The caller copies the status word afterwards.
 static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double *d_Fdx, double *d_Fd2,
@@ -1568,6 +1643,12 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
     if (p->dense) {
         const grape_dense::DenseBatch DB = dense_batch(p, nb, d_x, d_F, d_Fdx, d_Fd2, d_Fd2dx);
         HIPCHECK(grape_dense::launch_pipeline(p->DP, DB, st, mk));
+        return GRAPE_OK;
+    }
+    if (p->e1) {  // one workgroup per evaluation (grape_eval1.hip)
+        mk(GRAPE_KERNEL_EVAL1, 0);
+        HIPCHECK(grape_eval1::launch(eval1_args(p, d_x, d_F, d_Fdx), nb, st));
+        mk(GRAPE_KERNEL_EVAL1, 1);
         return GRAPE_OK;
     }
     if (p->ncls) {  // sectors: stage 0 of every class, the head, stage 1 of every class, the sum
@@ -1921,6 +2002,29 @@ static int fidelity_grad_graph(grape_plan *p, int nb, const double *x, double *F
             return fail(GRAPE_ERR_ALLOC, "pinned allocation failed (graph path)");
         if (dalloc(&p->d_gout, B * (1 + nx)) != hipSuccess)
             return fail(GRAPE_ERR_ALLOC, "device allocation failed (graph path)");
+    }
+    if (p->e1) {
+        // one workgroup per evaluation: a single launch that reads x from and writes F, F_dx to the
+        // mapped pinned buffers -- no staging copies, no graph
+        if (!p->hd_x && (hipHostGetDevicePointer(reinterpret_cast<void **>(&p->hd_x), p->h_x, 0) != hipSuccess ||
+                         hipHostGetDevicePointer(reinterpret_cast<void **>(&p->hd_F), p->h_F, 0) != hipSuccess))
+            return fail(GRAPE_ERR_HIP, "pinned buffers are not mapped (eval1)");
+        std::memcpy(p->h_x, x, (size_t)nb * nx * sizeof(double));
+        if (int rc = enqueue_call(p, nb, p->hd_x, p->hd_F, p->hd_F + B, nullptr, nullptr)) return rc;
+        if (int rc = grape_plan_synchronize(p)) return rc;
+        std::memcpy(F, p->h_F, (size_t)nb * sizeof(double));
+        std::memcpy(F_dx, p->h_F + B, (size_t)nb * nx * sizeof(double));
+        if (p->e1_trace) {
+            const long long *tr = p->e1_trace;
+            for (int i = 0; i < 9; ++i) p->e1_phase[i] += (double)(tr[i + 1] - tr[i]);
+            const double us = (double)(tr[15] - tr[14]) / 100.0;  // (wall clock: 100 MHz)
+            if (us > 0) p->e1_phase[9] += (double)(tr[9] - tr[0]) / us;
+            for (int i = 0; i < 4; ++i) p->e1_phase[10 + i] += (double)(tr[17 + i] - tr[16 + i]);
+            p->e1_phase[14] += (double)(tr[21] - tr[1]);
+            p->e1_phase[15] += (double)(tr[22] - tr[1]);
+            p->e1_calls += 1;
+        }
+        return GRAPE_OK;
     }
     hipGraphExec_t ex = nullptr;
     for (auto &g : p->graphs)

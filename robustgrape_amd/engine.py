@@ -246,8 +246,10 @@ class GrapePlan:
         g = (ctypes.c_int * 2)()
         kg = _capi.lib().grape_plan_gauge_info(self.handle, g, 2)
         _capi.check(min(kg, 0))
+        e1 = _capi.lib().grape_plan_eval1(self.handle)
+        _capi.check(min(e1, 0))
         return {"twin": tuple(bool(t[c]) for c in range(k)), "symmetric": bool(sym.value),
-                "gauge": tuple(bool(g[c]) for c in range(kg))}
+                "gauge": tuple(bool(g[c]) for c in range(kg)), "eval1": bool(e1)}
 
 
 # Plan cache of the reference-shaped entry points (one plan per problem object, nparam and

@@ -300,7 +300,7 @@ def test_pair_launches_bitwise(name, fp, nparam, sym, gauge):
     arithmetic as one launch per class (GRAPE_OPT_NO_PAIR), so F and F_dx agree bit for bit --
     batched (stream path) and single (graph path) calls; the C2-size problem also against the
     oracle at the T2s tier."""
-    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_PAIR, OPT_NO_SYMMETRY
+    from robustgrape_amd.operators import OPT_NO_EVAL1, OPT_NO_GAUGE, OPT_NO_PAIR, OPT_NO_SYMMETRY
     if not gauge and name == "full9-hot":
         pytest.skip("two controls per step: never phase-covariant")
     f = fp()
@@ -313,7 +313,9 @@ def test_pair_launches_bitwise(name, fp, nparam, sym, gauge):
         X[::2, 1::2][:, 5] = 700.0  # a high-norm step (squaring path) in every other row
     outs = []
     for opts in (0, OPT_NO_PAIR):
-        pl = _plan(f, 8, opts | (0 if sym else OPT_NO_SYMMETRY) | (0 if gauge else OPT_NO_GAUGE), nparam=nparam)
+        # (OPT_NO_EVAL1: the pair kernels themselves, not one workgroup per evaluation)
+        pl = _plan(f, 8, opts | OPT_NO_EVAL1 | (0 if sym else OPT_NO_SYMMETRY) | (0 if gauge else OPT_NO_GAUGE),
+                   nparam=nparam)
         try:
             batch = pl.fidelity_grad(X)[:2]
             single = pl.fidelity_grad(X[3:4])[:2]
