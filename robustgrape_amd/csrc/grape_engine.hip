@@ -209,6 +209,7 @@ struct grape_plan {
     // one workgroup per evaluation (grape_eval1.hip): eligible plan, its E~ tables, class A's index
     bool e1 = false;
     cd *d_e1_Et = nullptr, *d_e1_scr = nullptr;
+    unsigned char *d_e1_tab = nullptr;  // the kernel's table blob (grape_eval1 tab_build)
     int e1_pa = 0;
     // GRAPE_EVAL1_TRACE=1: workgroup 0's phase clocks of every host-array call, averaged and printed
     // to stderr when the plan is destroyed (mapped pinned buffer; a tuning aid)
@@ -283,6 +284,8 @@ struct grape_plan {
     }
 };
 
+static grape_eval1::Args eval1_args(const grape_plan *p, const double *x, double *F, double *Fdx);
+
 static void free_plan(grape_plan *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
@@ -308,7 +311,7 @@ static void free_plan(grape_plan *p) {
                     p->ud_Ci, p->d_G, p->d_xT, p->d_fscr, p->ud_Aimg,
                     p->d_Htab, p->d_U0tab, p->d_PA, p->d_PB, p->d_P0g, p->d_gpscr,
                     p->d_fixed, p->d_gout, p->d_slice, p->d_ops_sym, p->d_opsT_sym, p->d_PA_sym, p->d_PB_sym,
-                    p->d_W_sym, p->d_e1_Et, p->d_e1_scr};
+                    p->d_W_sym, p->d_e1_Et, p->d_e1_scr, p->d_e1_tab};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &c : p->sb) {
@@ -1507,6 +1510,12 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                     return bail(fail(GRAPE_ERR_HIP, "eval1 preparation failed"));
                 p->e1 = true;
                 p->e1_pa = pa;
+                const size_t tb = grape_eval1::tab_bytes(p->Ps[pa], p->Ps[pb], H);
+                if (hipMalloc(reinterpret_cast<void **>(&p->d_e1_tab), std::max<size_t>(tb, 16)) != hipSuccess)
+                    return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (eval1)"));
+                if (grape_eval1::tab_build(eval1_args(p, nullptr, nullptr, nullptr), p->d_e1_tab, p->stream) != hipSuccess ||
+                    hipStreamSynchronize(p->stream) != hipSuccess)
+                    return bail(fail(GRAPE_ERR_HIP, "eval1 table build failed"));
                 const char *tr = std::getenv("GRAPE_EVAL1_TRACE");
                 if (tr && tr[0] == '1' &&
                     (hipHostMalloc(reinterpret_cast<void **>(&p->e1_trace), 32 * sizeof(long long), hipHostMallocDefault) != hipSuccess ||
@@ -1615,6 +1624,7 @@ static grape_eval1::Args eval1_args(const grape_plan *p, const double *x, double
     A.Fdx = Fdx;
     A.a_first = p->e1_pa == 0 ? 1 : 0;
     A.trace = p->e1_trace_d;
+    A.tab = p->d_e1_tab;
     return A;
 }
 

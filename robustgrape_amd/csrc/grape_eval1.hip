@@ -49,7 +49,8 @@ __global__ __launch_bounds__(64) void k_gauge_tilde(DevProblem P, cd *out, cd *s
 }
 
 struct Lay {
-    size_t SA, SB, Wt, MA, MB, u0, dq, xs, pA, pB, Et, gn, sidx, W, fixed, out, terms, tdiag, cq, total;
+    size_t SA, SB, Wt, MA, MB, u0, dq, xs, ph, pA, pB, out, cq, tab, Et, gn, sidx, W, fixed, terms, tdiag, tab_bytes,
+        total;
 };
 __host__ __device__ inline Lay layout(int DA, int neB, int nch, int Nt, int nx, int D, int na, int nfixed, int ntgt) {
     Lay L{};
@@ -67,17 +68,22 @@ __host__ __device__ inline Lay layout(int DA, int neB, int nch, int Nt, int nx, 
     L.u0 = take((size_t)D * sizeof(cd));
     L.dq = take((size_t)na * D * sizeof(cd));
     L.xs = take((size_t)nx * sizeof(double));
+    L.ph = take((size_t)Nt * sizeof(cd));  // e^{i a x_k} of every step (phase 0b)
     L.pA = take((size_t)Nt * sizeof(double));
     L.pB = take((size_t)Nt * sizeof(double));
+    L.out = take((size_t)(1 + na) * sizeof(double));  // F and the x_add entries of F_dx (stored in phase E)
+    // the target terms' coefficients at x_add, x_add + eps e_q; then the head's K blocks and weights
+    L.cq = take((size_t)(1 + na) * ntgt * sizeof(cd) + 27 * sizeof(cd) + 9 * sizeof(double));
+    // the plan's tables, one contiguous region: a byte copy of the plan's table blob (tab_build)
+    L.tab = o;
     L.Et = take((size_t)(DA * DA + neB * 4) * sizeof(cd));  // E~ of class A, then class B
     L.gn = take((size_t)(DA + 2 * 2) * sizeof(int));        // charges: class A's sector, B's two
     L.sidx = take((size_t)(DA + 2 * 2) * sizeof(int));      // sector slots: plan class 0, then 1
     L.W = take((size_t)D * sizeof(double));
     L.fixed = take((size_t)(nfixed > 0 ? nfixed : 1) * sizeof(int));
-    L.out = take((size_t)(1 + na) * sizeof(double));  // F and the x_add entries of F_dx (stored in phase E)
     L.terms = take((size_t)ntgt * sizeof(Term));       // the target's terms ...
     L.tdiag = take((size_t)ntgt * D * sizeof(cd));     // ... and the diagonals of their operators
-    L.cq = take((size_t)(1 + na) * ntgt * sizeof(cd));  // their coefficients at x_add, x_add + eps e_q
+    L.tab_bytes = o - L.tab;
     L.total = o;
     return L;
 }
@@ -161,8 +167,8 @@ __device__ __forceinline__ GaugeN<D> charges(const int *g) {
 
 // phase A: the chunk total T_c of each of the lane's NE chains (E~ and the charges from LDS)
 template <int D, int NE>
-__device__ __forceinline__ void lane_total(const DevProblem &Pc, const cd *EtL, const int *gnL, const double *xs, int c,
-                                           int L, int Nt, cd (&R)[NE][D][D]) {
+__device__ __forceinline__ void lane_total(const cd *EtL, const int *gnL, const cd *ph, int c, int L, int Nt,
+                                           cd (&R)[NE][D][D]) {
     cd Et[NE][D][D];
     GaugeN<D> gn[NE];
 #pragma unroll
@@ -174,12 +180,11 @@ __device__ __forceinline__ void lane_total(const DevProblem &Pc, const cd *EtL, 
     const int k0 = c * L, k1 = min(k0 + L, Nt);
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
-        double sn, cn;
-        sincos(Pc.gauge_a * xs[k], &sn, &cn);
+        const cd p1 = ph[k];  // e^{i a x_k} (phase 0b)
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             cd E[D][D];
-            step_prop<D>(Et[e], gn[e], cmake(cn, sn), E);
+            step_prop<D>(Et[e], gn[e], p1, E);
             if (k == k0) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
@@ -238,7 +243,7 @@ __device__ __forceinline__ void wave_carry(cd (&R)[NE][D][D], const cd *Wt, int 
 // then the chunk's steps (walk_grad_body's GAUGE step, presummed over the lane's sectors)
 template <int D, int NE, int NSEC>
 __device__ __forceinline__ void lane_grad(const DevProblem &Pc, const cd *EtL, const int *gnL, const cd *S, const cd *Mb,
-                                          const double *xs, int c, int L, int Nt, int nch, double *part) {
+                                          const double *xs, const cd *ph, int c, int L, int Nt, int nch, double *part) {
     constexpr int NSH = NSEC / NE;  // sectors per chain (twins: 2)
     cd Et[NE][D][D];
     GaugeN<D> gn[NE];
@@ -278,13 +283,12 @@ __device__ __forceinline__ void lane_grad(const DevProblem &Pc, const cd *EtL, c
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
         const double xk = xs[k], xe = xk + Pc.eps;  // the reference's perturbed control
-        double sn, cn;
-        sincos(Pc.gauge_a * xk, &sn, &cn);
         const cd q = cis_m1(Pc.gauge_a * (xe - xk));
+        const cd p1 = ph[k];
         cd E[NE][D][D], rho[NE][D];
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
-            step_prop<D>(Et[e], gn[e], cmake(cn, sn), E[e]);
+            step_prop<D>(Et[e], gn[e], p1, E[e]);
 #pragma unroll
             for (int j = 0; j < D; ++j) rho[e][j] = gauge_rho(q, gn[e].n[j]);
         }
@@ -355,105 +359,6 @@ __device__ __forceinline__ void lane_grad(const DevProblem &Pc, const cd *EtL, c
     }
 }
 
-// ---- the head (phase C): grape_projector.hip's diagonal head, one lane per sector row ----
-// Every LDS value a row needs is read into registers first (no load waits behind the M stores).
-struct HeadCtx {
-    const double *W;         // [D] projector weights (LDS)
-    const int *sidx0, *sidx1;  // sector slots of plan class 0 / 1 (LDS)
-    const cd *U0, *U1;       // U blocks of plan class 0 / 1 (LDS, row-major) ...
-    int us0, us1;            // ... sector w's at U + w * us (twins: 0, one chain)
-    cd *M0, *M1;             // M_ww blocks out (LDS, [w][S][S])
-    int S0, S1, na, D;
-    const cd *u0, *dq;       // target diagonal; its x_add forward differences [na][D] (LDS)
-    double sc;               // 2 / DD
-};
-struct HeadSums {            // one row's partial sums: F's, tau's, and per x_add entry sa's and trd's
-    double fsum;
-    cd tau;
-    double sa[kMaxNa];
-    cd trd[kMaxNa];
-};
-// One lane per sector block, every block as 3 slots (the 2-level sectors padded with an empty
-// slot, g = -1): one code path for all lanes (no divergence between the classes), every row index
-// a compile-time constant (nothing lands in scratch), and the block's K kept in registers from the
-// sums to the M block.
-constexpr int kHS = 3;
-struct HeadBlock {
-    int g[kHS];
-    cd U[kHS][kHS], K[kHS][kHS];  // U block; K_kc = conj(u0_{g_k}) U_kc (zero on padding slots)
-    double w[kHS];                // W at the slots (0 on padding)
-};
-__device__ __forceinline__ void head_load(const HeadCtx &h, int cl, int wsec, HeadBlock &B) {
-    const int S = cl == 0 ? h.S0 : h.S1;
-    const int *sx = (cl == 0 ? h.sidx0 : h.sidx1) + wsec * S;
-    const cd *Ub = (cl == 0 ? h.U0 : h.U1) + (size_t)wsec * (cl == 0 ? h.us0 : h.us1);
-    cd u0g[kHS];
-#pragma unroll
-    for (int k = 0; k < kHS; ++k) B.g[k] = k < S ? sx[k] : -1;
-#pragma unroll
-    for (int k = 0; k < kHS; ++k) {
-#pragma unroll
-        for (int c = 0; c < kHS; ++c) B.U[k][c] = (k < S && c < S) ? Ub[k * S + c] : czero();
-        u0g[k] = h.u0[B.g[k] >= 0 ? B.g[k] : 0];
-        B.w[k] = B.g[k] >= 0 ? h.W[B.g[k]] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < kHS; ++k) {
-#pragma unroll
-        for (int c = 0; c < kHS; ++c)
-            B.K[k][c] = (B.g[k] >= 0 && B.g[c] >= 0) ? cmul(cconj(u0g[k]), B.U[k][c]) : czero();
-    }
-}
-// passes 0 and 2 of diag_row over the block's rows: F's and tau's terms, the F_dx_add terms per d_q
-__device__ __forceinline__ void head_sums(const HeadCtx &h, const HeadBlock &B, HeadSums &o) {
-#pragma unroll
-    for (int r = 0; r < kHS; ++r) {
-        if (B.g[r] < 0) continue;
-#pragma unroll
-        for (int c = 0; c < kHS; ++c) {
-            if (B.g[c] < 0) continue;
-            o.fsum += B.w[r] * (B.w[c] != 0.0 ? 1.0 : 0.0) * (B.K[r][c].re * B.K[r][c].re + B.K[r][c].im * B.K[r][c].im);
-        }
-        o.tau = cadd(o.tau, cscale(B.w[r], B.K[r][r]));
-    }
-#pragma unroll
-    for (int q = 0; q < kMaxNa; ++q) {  // (unrolled: the sums stay in registers)
-        if (q >= h.na) break;
-#pragma unroll
-        for (int r = 0; r < kHS; ++r) {
-            if (B.g[r] < 0) continue;
-            const cd dr = cconj(h.dq[(size_t)q * h.D + B.g[r]]);
-#pragma unroll
-            for (int c = 0; c < kHS; ++c) {
-                if (B.g[c] < 0) continue;
-                const cd kd = cmul(dr, B.U[r][c]);
-                o.sa[q] += B.w[r] * (B.w[c] != 0.0 ? 1.0 : 0.0) * (kd.re * B.K[r][c].re + kd.im * B.K[r][c].im);
-            }
-            o.trd[q] = cadd(o.trd[q], cscale(B.w[r], cmul(dr, B.U[r][r])));
-        }
-    }
-}
-// pass 1: M_ww = (2/DD) [p_r (K^dag W K)_rc + W_r conj(tau) K_rc]
-__device__ __forceinline__ void head_mblock(const HeadCtx &h, int cl, int wsec, const HeadBlock &B, cd tau) {
-    const int S = cl == 0 ? h.S0 : h.S1;
-    cd *dst = (cl == 0 ? h.M0 : h.M1) + (size_t)wsec * S * S;
-#pragma unroll
-    for (int r = 0; r < kHS; ++r) {
-#pragma unroll
-        for (int c = 0; c < kHS; ++c) {
-            cd m = czero();
-            if (B.g[r] >= 0 && B.g[c] >= 0) {
-                cd sm = czero();
-#pragma unroll
-                for (int k = 0; k < kHS; ++k)
-                    if (B.g[k] >= 0) sm = cadd(sm, cscale(B.w[k], cmul(cconj(B.K[k][r]), B.K[k][c])));
-                const double pr = B.w[r] != 0.0 ? 1.0 : 0.0;
-                m = cscale(h.sc, cadd(cscale(pr, sm), cscale(B.w[r], cmul(cconj(tau), B.K[r][c]))));
-            }
-            if (r < S && c < S) dst[r * S + c] = m;
-        }
-    }
-}
 __device__ __forceinline__ double gadd(double v, int G) {
     for (int o = G >> 1; o >= 1; o >>= 1) v += __shfl_xor(v, o, G);
     return v;
@@ -471,6 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     cd *MA = reinterpret_cast<cd *>(e1_smem + Lo.MA), *MB = reinterpret_cast<cd *>(e1_smem + Lo.MB);
     cd *u0 = reinterpret_cast<cd *>(e1_smem + Lo.u0), *dq = reinterpret_cast<cd *>(e1_smem + Lo.dq);
     double *xs = reinterpret_cast<double *>(e1_smem + Lo.xs);
+    cd *ph = reinterpret_cast<cd *>(e1_smem + Lo.ph);
     double *pA = reinterpret_cast<double *>(e1_smem + Lo.pA), *pB = reinterpret_cast<double *>(e1_smem + Lo.pB);
     cd *EtL = reinterpret_cast<cd *>(e1_smem + Lo.Et);
     int *gnL = reinterpret_cast<int *>(e1_smem + Lo.gn), *sxL = reinterpret_cast<int *>(e1_smem + Lo.sidx);
@@ -490,22 +396,21 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     }
     const int role = t / kLanes;  // 0: class A lanes, 1: class B lanes, 2: the head wave (wave-uniform)
     const int c = t - role * kLanes;
-    // phase 0: the controls, and (head wave) the tables every phase reads, into LDS
+    // phase 0: the controls and the plan's table blob (one coalesced 16-B copy) into LDS
     const double *xb = A.x + (size_t)b * P.nx;
     for (int i = t; i < P.nx; i += kBlock) xs[i] = xb[i];
-    if (role == 2) {
-        const int nEA = DA * DA, nE = nEA + NEB * 4;
-        for (int i = c; i < nE; i += 64) EtL[i] = i < nEA ? A.EtA[i] : A.EtB[i - nEA];
-        for (int i = c; i < DA + 4; i += 64) gnL[i] = i < DA ? A.PA.gauge_n[i] : A.PB.gauge_n[i - DA];
-        const int n0 = H.S[0] * H.nsec[0];
-        for (int i = c; i < n0 + H.S[1] * H.nsec[1]; i += 64) sxL[i] = i < n0 ? H.sidx[0][i] : H.sidx[1][i - n0];
-        for (int i = c; i < P.D; i += 64) WL[i] = P.W[i];
-        for (int i = c; i < H.nfixed; i += 64) fxL[i] = H.fixed[i];
-        for (int i = c; i < P.n_tgt; i += 64) tmL[i] = P.tgt[i];
-        for (int i = c; i < P.n_tgt * P.D; i += 64) {
-            const int q = i / P.D, j = i - q * P.D;
-            tdL[i] = P.ops[((size_t)P.tgt[q].op * P.D + j) * P.D + j];
-        }
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(A.tab);
+        uint4 *dst = reinterpret_cast<uint4 *>(e1_smem + Lo.tab);
+        for (int i = t; i < (int)(Lo.tab_bytes / 16); i += kBlock) dst[i] = src[i];
+    }
+    __syncthreads();
+    // phase 0b: the level phases' base e^{i a x_k} of every step, once (both classes share a), in
+    // parallel over the workgroup instead of twice per step on each class's critical path
+    for (int k = t; k < P.Nt; k += kBlock) {
+        double sn, cn;
+        sincos(A.PA.gauge_a * xs[k], &sn, &cn);
+        ph[k] = cmake(cn, sn);
     }
     __syncthreads();
     if (tr) tc[1] = clock64();
@@ -518,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     cd RA[1][DA][DA], RB[NEB][2][2];
     if (role == 0) {
         if (wact) {
-            lane_total<DA, 1>(A.PA, EtL, gnL, xs, c, A.L, P.Nt, RA);
+            lane_total<DA, 1>(EtL, gnL, ph, c, A.L, P.Nt, RA);
             if (tr) tc[2] = clock64();
             wave_scan<DA, 1>(RA, lane);
             if (tr) tc[3] = clock64();
@@ -526,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
         }
     } else if (role == 1) {
         if (wact) {
-            lane_total<2, NEB>(A.PB, EtL + DA * DA, gnL + DA, xs, c, A.L, P.Nt, RB);
+            lane_total<2, NEB>(EtL + DA * DA, gnL + DA, ph, c, A.L, P.Nt, RB);
             wave_scan<2, NEB>(RB, lane);
             if (A.trace && b == 0 && c == 0) A.trace[22] = clock64();  // (class B's phase A + scan done)
             if (lane == 63) {
@@ -578,50 +483,52 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     }
     __syncthreads();
     if (tr) tc[5] = clock64();
-    // phase C: the head wave
+    // phase C: the head wave, one lane per element (r, c) of each sector block (blocks padded to 3 x 3:
+    // 27 lanes) -- K_rc = conj(u0_{g_r}) U_rc and its terms of F, tau and the F_dx_add sums, a
+    // shuffle reduction over the wave, then M_rc from the K columns in LDS (diag_row's quantities,
+    // FidelityCalculations.jl:47-76)
     if (role == 2) {
         const bool trh = A.trace && b == 0 && c == 0;  // (trace: the head wave's own steps, [16..20])
         long long th[5];
         if (trh) th[0] = clock64();
-        HeadCtx h;
-        h.W = WL;
-        h.sidx0 = sxL;
-        h.sidx1 = sxL + H.S[0] * H.nsec[0];
-        h.S0 = H.S[0];
-        h.S1 = H.S[1];
-        h.na = P.na;
-        h.D = P.D;
-        // U = S_last of each class (the 2-level twins share one chain: sector stride 0)
-        const cd *UA = SA + (size_t)(A.nch - 1) * DA * DA, *UB = SB + (size_t)(A.nch - 1) * 4;
-        const int usB = TW ? 0 : A.nch * 4;
-        h.u0 = u0;
-        h.dq = dq;
-        h.sc = 2.0 / P.DD;
-        h.U0 = A.a_first ? UA : UB;
-        h.U1 = A.a_first ? UB : UA;
-        h.us0 = A.a_first ? DA * DA : usB;
-        h.us1 = A.a_first ? usB : DA * DA;
-        h.M0 = A.a_first ? MA : MB;
-        h.M1 = A.a_first ? MB : MA;
-        // lane l: sector block l (plan class 0's sectors first)
-        const int n0 = h.S0 == 2 ? 2 : 1, nsec = n0 + (h.S1 == 2 ? 2 : 1);
-        constexpr int G = 4;
-        const bool ok = c < nsec;
-        const int cl = c < n0 ? 0 : 1, w = c < n0 ? c : c - n0;
-        HeadSums hs;
-        hs.fsum = 0.0;
-        hs.tau = czero();
+        const int S0 = H.S[0], S1 = H.S[1];
+        const int n0 = S0 == 2 ? 2 : 1, nsec = n0 + (S1 == 2 ? 2 : 1);
+        const int l = c / 9, e = c - 9 * l, r = e / 3, col = e - 3 * (e / 3);
+        const int cl = l < n0 ? 0 : 1, w = l < n0 ? l : l - n0, S = cl == 0 ? S0 : S1;
+        const bool isA = (cl == 0) == (A.a_first != 0);
+        const bool valid = l < nsec && r < S && col < S;
+        const int *sx = (cl == 0 ? sxL : sxL + S0 * H.nsec[0]) + w * S;
+        // U = S_last of each class (the 2-level twins share one chain)
+        const cd *Ub = isA ? SA + (size_t)(A.nch - 1) * DA * DA
+                           : SB + ((size_t)(TW ? 0 : w) * A.nch + A.nch - 1) * 4;
+        const int gr = valid ? sx[r] : -1, gc = valid ? sx[col] : -1;
+        const bool live = gr >= 0 && gc >= 0;
+        const cd U = live ? Ub[r * S + col] : czero();
+        const cd u0r = u0[gr >= 0 ? gr : 0];
+        const double wr = gr >= 0 ? WL[gr] : 0.0, pc = (gc >= 0 && WL[gc] != 0.0) ? 1.0 : 0.0;
+        const cd K = live ? cmul(cconj(u0r), U) : czero();
+        cd *kb = cqL + (size_t)(1 + P.na) * P.n_tgt;  // K of every block, [l][r][c] (LDS)
+        double *wb = reinterpret_cast<double *>(kb + 27);  // W at each block's slots, [l][r]
+        if (c < 27) kb[c] = K;
+        if (c < 27 && col == 0) wb[l * 3 + r] = wr;
+        double fsum = wr * pc * (K.re * K.re + K.im * K.im);
+        cd tau = (r == col) ? cscale(wr, K) : czero();
+        double sa[kMaxNa];
+        cd trd[kMaxNa];
 #pragma unroll
         for (int q = 0; q < kMaxNa; ++q) {
-            hs.sa[q] = 0.0;
-            hs.trd[q] = czero();
+            sa[q] = 0.0;
+            trd[q] = czero();
+            if (q < P.na && gr >= 0) {
+                const cd dr = cconj(dq[(size_t)q * P.D + gr]);
+                const cd kd = cmul(dr, U);
+                sa[q] = wr * pc * (kd.re * K.re + kd.im * K.im);
+                if (r == col) trd[q] = cscale(wr, kd);
+            }
         }
-        HeadBlock hb;
-        head_load(h, ok ? cl : 0, ok ? w : 0, hb);
-        if (ok) head_sums(h, hb, hs);
         if (trh) th[1] = clock64();
-        double fsum = gadd(hs.fsum, G);
-        cd tau = cmake(gadd(hs.tau.re, G), gadd(hs.tau.im, G));
+        fsum = gadd(fsum, 32);
+        tau = cmake(gadd(tau.re, 32), gadd(tau.im, 32));
         for (int q = 0; q < H.nfixed; ++q) {  // U_gg = 1: K_gg = conj(u0_g)
             const int g = fxL[q];
             const cd k = cconj(u0[g]);
@@ -630,21 +537,33 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
         }
         if (c == 0) outL[0] = (fsum + tau.re * tau.re + tau.im * tau.im) / P.DD;
         if (trh) th[2] = clock64();
-        if (ok) head_mblock(h, cl, w, hb, tau);
+        // (LDS is in order within a wave: the fences keep the compiler from hoisting the reads)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid) {  // M_rc = (2/DD) [p_r sum_k W_k conj(K_kr) K_kc + W_r conj(tau) K_rc]
+            const cd *kl = kb + l * 9;
+            cd sm = czero();
+#pragma unroll
+            for (int k = 0; k < 3; ++k) sm = cadd(sm, cscale(wb[l * 3 + k], cmul(cconj(kl[k * 3 + r]), kl[k * 3 + col])));
+            const double pr = wr != 0.0 ? 1.0 : 0.0;
+            const cd m = live ? cscale(2.0 / P.DD, cadd(cscale(pr, sm), cscale(wr, cmul(cconj(tau), K)))) : czero();
+            (isA ? MA : MB + (size_t)w * 4)[r * S + col] = m;
+        }
         if (trh) th[3] = clock64();
 #pragma unroll
         for (int q = 0; q < kMaxNa; ++q) {
             if (q >= P.na) break;
-            double sa = gadd(hs.sa[q], G);
-            cd trd = cmake(gadd(hs.trd[q].re, G), gadd(hs.trd[q].im, G));
+            double s_ = gadd(sa[q], 32);
+            cd t_ = cmake(gadd(trd[q].re, 32), gadd(trd[q].im, 32));
             const cd *d = dq + (size_t)q * P.D;
             for (int rr = 0; rr < H.nfixed; ++rr) {
                 const int g = fxL[rr];
                 const cd kd = cconj(d[g]), k = cconj(u0[g]);
-                sa += WL[g] * (WL[g] != 0.0 ? 1.0 : 0.0) * (kd.re * k.re + kd.im * k.im);
-                trd = cadd(trd, cscale(WL[g], kd));
+                s_ += WL[g] * (WL[g] != 0.0 ? 1.0 : 0.0) * (kd.re * k.re + kd.im * k.im);
+                t_ = cadd(t_, cscale(WL[g], kd));
             }
-            if (c == 0) outL[1 + q] = (2.0 * sa + 2.0 * (tau.re * trd.re + tau.im * trd.im)) / P.DD;
+            if (c == 0) outL[1 + q] = (2.0 * s_ + 2.0 * (tau.re * t_.re + tau.im * t_.im)) / P.DD;
         }
         if (trh) {
             th[4] = clock64();
@@ -655,10 +574,10 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     if (tr) tc[6] = clock64();
     // phase D
     if (role == 0) {
-        if (act) lane_grad<DA, 1, 1>(A.PA, EtL, gnL, SA, MA, xs, c, A.L, P.Nt, A.nch, pA);
+        if (act) lane_grad<DA, 1, 1>(A.PA, EtL, gnL, SA, MA, xs, ph, c, A.L, P.Nt, A.nch, pA);
         if (tr) tc[7] = clock64();
     } else if (role == 1) {
-        if (act) lane_grad<2, NEB, 2>(A.PB, EtL + DA * DA, gnL + DA, SB, MB, xs, c, A.L, P.Nt, A.nch, pB);
+        if (act) lane_grad<2, NEB, 2>(A.PB, EtL + DA * DA, gnL + DA, SB, MB, xs, ph, c, A.L, P.Nt, A.nch, pB);
     }
     __syncthreads();
     if (tr) tc[8] = clock64();
@@ -683,13 +602,55 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     }
 }
 
+// The plan's table blob (once per plan): k_eval1's LDS tables region, byte for byte -- E~ of both
+// classes, their charges, the sector slots, W, the fixed levels, the target's terms and the
+// diagonals of their operators -- gathered from wherever the plan keeps them.
+template <int DA, bool TW>
+__global__ __launch_bounds__(64) void k_tab_build(Args A, unsigned char *blob) {
+    constexpr int NEB = TW ? 1 : 2;
+    const DevProblem &P = A.H.P;
+    const grape_proj::SectorHead &H = A.H;
+    const Lay Lo = layout(DA, NEB, 1, P.Nt, P.nx, P.D, P.na, H.nfixed, P.n_tgt);
+    auto at = [&](size_t off) { return blob + (off - Lo.tab); };
+    cd *EtL = reinterpret_cast<cd *>(at(Lo.Et));
+    int *gnL = reinterpret_cast<int *>(at(Lo.gn)), *sxL = reinterpret_cast<int *>(at(Lo.sidx));
+    double *WL = reinterpret_cast<double *>(at(Lo.W));
+    int *fxL = reinterpret_cast<int *>(at(Lo.fixed));
+    Term *tmL = reinterpret_cast<Term *>(at(Lo.terms));
+    cd *tdL = reinterpret_cast<cd *>(at(Lo.tdiag));
+    const int c = threadIdx.x;
+    const int nEA = DA * DA, nE = nEA + NEB * 4;
+    for (int i = c; i < nE; i += 64) EtL[i] = i < nEA ? A.EtA[i] : A.EtB[i - nEA];
+    for (int i = c; i < DA + 4; i += 64) gnL[i] = i < DA ? A.PA.gauge_n[i] : A.PB.gauge_n[i - DA];
+    const int n0 = H.S[0] * H.nsec[0];
+    for (int i = c; i < n0 + H.S[1] * H.nsec[1]; i += 64) sxL[i] = i < n0 ? H.sidx[0][i] : H.sidx[1][i - n0];
+    for (int i = c; i < P.D; i += 64) WL[i] = P.W[i];
+    for (int i = c; i < H.nfixed; i += 64) fxL[i] = H.fixed[i];
+    for (int i = c; i < P.n_tgt; i += 64) tmL[i] = P.tgt[i];
+    for (int i = c; i < P.n_tgt * P.D; i += 64) {
+        const int q = i / P.D, j = i - q * P.D;
+        tdL[i] = P.ops[((size_t)P.tgt[q].op * P.D + j) * P.D + j];
+    }
+}
+
+size_t tab_bytes(const DevProblem &PA, const DevProblem &PB, const grape_proj::SectorHead &H) {
+    const DevProblem &P = H.P;
+    return layout(PA.D, PB.twin ? 1 : 2, 1, P.Nt, P.nx, P.D, P.na, H.nfixed, P.n_tgt).tab_bytes;
+}
+hipError_t tab_build(const Args &A, unsigned char *blob, hipStream_t st) {
+    if (A.PA.D != 3) return hipErrorInvalidValue;
+    if (A.PB.twin) hipLaunchKernelGGL((k_tab_build<3, true>), dim3(1), dim3(64), 0, st, A, blob);
+    else hipLaunchKernelGGL((k_tab_build<3, false>), dim3(1), dim3(64), 0, st, A, blob);
+    return hipGetLastError();
+}
+
 bool eligible(const DevProblem &PA, const DevProblem &PB, const grape_proj::SectorHead &H) {
     const DevProblem &P = H.P;
     const int neB = PB.twin ? 1 : 2;
     // (class A of 3 levels: the symmetry-adapted sectors.  The 4-level permutation sectors spill at
     // this workgroup's 168-VGPR budget and keep the pair kernels.)
     const bool shape = PA.D == 3 && PA.nsec == 1 && PB.D == 2 && PB.nsec == 2 && H.ncls == 2;
-    const bool gauge = PA.gauge && PB.gauge && PA.walk && PB.walk;
+    const bool gauge = PA.gauge && PB.gauge && PA.walk && PB.walk && PA.gauge_a == PB.gauge_a;
     const bool path = P.ne == 0 && P.np == 1 && P.nvg == 1 && !P.xadd_dep && P.na <= kMaxNa && H.diag &&
                       P.Nt >= 1 && P.Nt <= kMaxNt && P.gen_proj == 0;
     if (!(shape && gauge && path)) return false;

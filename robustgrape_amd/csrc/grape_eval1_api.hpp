@@ -21,6 +21,7 @@ struct Args {
     int L, nch;                   // steps per chunk, chunks (<= kLanes)
     int a_first;                  // 1: class A is the plan's class 0 (F_dx sums class 0, then class 1)
     long long *trace;             // optional: workgroup 0's phase clocks [0..9], wall clocks [14], [15]
+    const unsigned char *tab;     // the plan's table blob (tab_build), 16-B aligned
 };
 
 // Which plans it serves: both classes phase-covariant chunk walks of the pair layout
@@ -31,6 +32,10 @@ bool eligible(const grape::DevProblem &PA, const grape::DevProblem &PB, const gr
 // walks' own gauge_base arithmetic, hence their bits); scr: 2 * 4 * 16 complex of scratch
 hipError_t prepare(const grape::DevProblem &PA, const grape::DevProblem &PB, grape::cd *EtA, grape::cd *EtB,
                    grape::cd *scr, hipStream_t st);
+// the plan's table blob (E~, charges, sector slots, W, fixed levels, target terms and diagonals):
+// its size, and its one-time build from the plan's device tables (after prepare)
+size_t tab_bytes(const grape::DevProblem &PA, const grape::DevProblem &PB, const grape_proj::SectorHead &H);
+hipError_t tab_build(const Args &A, unsigned char *blob, hipStream_t st);
 // one workgroup per evaluation of the batch: F and F_dx (controls and x_add) of nb evaluations
 hipError_t launch(Args A, int nb, hipStream_t st);
 }  // namespace grape_eval1
