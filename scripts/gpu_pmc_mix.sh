@@ -12,7 +12,7 @@ for group in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES S
              "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d $OUT/${TAG}_p$i -o run -- \
-      python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-paths --no-whole-matrix --no-c4-strong > $OUT/${TAG}_p$i.log 2>&1
+      python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-paths --no-whole-matrix --no-c4-strong ${BENCH_EXTRA:-} > $OUT/${TAG}_p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   if grep -qE "HSA_STATUS_ERROR|illegal memory access|Memory access fault" $OUT/${TAG}_p$i.log; then echo FAULT; exit 99; fi
   [ $rc -ne 0 ] && { tail -5 $OUT/${TAG}_p$i.log; exit $rc; }
