@@ -75,6 +75,9 @@ constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
 #ifndef GRAPE_GAUGE_CHUNK_DIV
 #define GRAPE_GAUGE_CHUNK_DIV 2
 #endif
+#ifndef GRAPE_GAUGE_CHUNK_DIV2  // ... for the 2-level classes (A/B knob)
+#define GRAPE_GAUGE_CHUNK_DIV2 GRAPE_GAUGE_CHUNK_DIV
+#endif
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
@@ -1419,7 +1422,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                 Ps.scan_waves = kScanLatency;
             // phase-covariant throughput classes: a step costs a few products instead of an
             // exponential, so longer chunks (fewer per-lane prologues and a shorter scan) can pay
-            const int cdiv = (Ps.gauge && Ps.scan_waves == kScanTiny) ? GRAPE_GAUGE_CHUNK_DIV : 1;
+            const int cdiv = (Ps.gauge && Ps.scan_waves == kScanTiny) ? (S == 2 ? GRAPE_GAUGE_CHUNK_DIV2 : GRAPE_GAUGE_CHUNK_DIV) : 1;
             const int ncs = std::max(1, std::min(Ps.scan_waves * (64 / S) / cdiv, P.Nt));
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
