@@ -203,6 +203,10 @@ typedef struct grape_desc {
  * every intermediate in LDS; host-array calls read x from and write F, F_dx to
  * mapped pinned memory.  This option keeps the pair-kernel pipeline. */
 #define GRAPE_OPT_NO_EVAL1 16384
+/* Merged walks (ABI 10): throughput passes of the Rydberg layout with phase-covariant classes walk
+ * both sector classes of an (evaluation, chunk) in one lane; this option launches
+ * one walk kernel per class instead (the same chunking, the same results bit for bit). */
+#define GRAPE_OPT_NO_MERGE 32768
 
 typedef struct grape_plan grape_plan;
 

@@ -211,6 +211,10 @@ struct grape_plan {
     grape_proj::SectorHead SH{};
     // one workgroup per evaluation (grape_eval1.hip): eligible plan, its E~ tables, class A's index
     bool e1 = false;
+    // throughput passes: both walk classes in one lane (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m);
+    // merge_pa: the index of the class of 3 or 4 levels
+    bool merged = false;
+    int merge_pa = 0;
     cd *d_e1_Et = nullptr, *d_e1_scr = nullptr;
     unsigned char *d_e1_tab = nullptr;  // the kernel's table blob (grape_eval1 tab_build)
     int e1_pa = 0;
@@ -1497,6 +1501,23 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             H.MsecE[cl] = b.MsecE;
         }
         p->ncls = (int)ss.cls.size();
+        // throughput passes of the Rydberg layout with phase-covariant classes: class B (2 levels)
+        // takes class A's chunking (fewer, longer chunks: its buffers, sized for its own count,
+        // suffice) so that one lane can walk both (merged walks; GRAPE_OPT_NO_MERGE launches the
+        // same chunking per class)
+        if (p->ncls == 2) {
+            int pa = 0, pb = 1;
+            if (grape_walk::pair_ok(p->Ps[1], p->Ps[0])) std::swap(pa, pb);
+            DevProblem &A = p->Ps[pa], &Bq = p->Ps[pb];
+            if (grape_walk::pair_ok(A, Bq) && A.D == 3 && A.gauge && Bq.gauge && A.gauge_a == Bq.gauge_a &&
+                A.scan_waves == kScanTiny && Bq.scan_waves == kScanTiny && A.nchunks <= Bq.nchunks && P.np == 1 &&
+                P.na <= 1) {
+                Bq.L = A.L;
+                Bq.nchunks = A.nchunks;
+                p->merged = !(P.opts & GRAPE_OPT_NO_MERGE) && grape_walk::merged_ok(A, Bq);
+                p->merge_pa = pa;
+            }
+        }
         // latency-bound calls of the Rydberg layout with phase-covariant classes: one workgroup per
         // evaluation (grape_eval1.hip), with E~ of each class computed here once
         if (p->ncls == 2 && (long)MB <= kEval1MaxBatch && !(P.opts & GRAPE_OPT_NO_EVAL1)) {
@@ -1707,6 +1728,7 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             B.xT = (nb == 1 || grape::kWalkXRow) ? d_x : p->d_xT;  // one evaluation: x[q] is already [nx][1]
             sp.part[cl] = sb.part;
             sp.nsec[cl] = p->Ps[cl].walk ? grape_walk::grad_parts(p->Ps[cl]) : p->Ps[cl].nsec;
+            if (p->merged && cl != p->merge_pa) sp.nsec[cl] = 0;  // (the merged walk's one part is class A's)
             sp.lane_major[cl] = p->Ps[cl].walk;  // k_walk_grad's / k_walk_img_sum's layout
             sp.part_err[cl] = sb.part_err;
             sp.lane_major_err[cl] = p->Ps[cl].walk;  // k_walk_err_grad's layout
@@ -1734,6 +1756,19 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
                           p->Ps[0].scan_waves == kScanLatency &&
                           p->Ps[1].scan_waves == kScanLatency && grape_walk::pair_ok(p->Ps[pa], p->Ps[pb]);
         auto stage = [&](int s) -> hipError_t {  // stage s of every class (class 1 forked when `fork`)
+            if (p->merged && s < 2) {  // both classes in one lane (throughput passes)
+                const int ma = p->merge_pa, mb = 1 - ma;
+                mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 0);
+                hipError_t e = grape_walk::launch_merged(s, p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], ma == 0 ? 1 : 0, st);
+                mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 1);
+                if (e == hipSuccess && s == 0) {
+                    mk(GRAPE_KERNEL_SCAN, 0);
+                    e = p->Ps[ma].D == 4 ? grape_host::launch_scan_pair<4, 2, kScanTiny>(p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], st)
+                                         : grape_host::launch_scan_pair<3, 2, kScanTiny>(p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], st);
+                    mk(GRAPE_KERNEL_SCAN, 1);
+                }
+                return e;
+            }
             if (pair && s < 2) {
                 mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 0);
                 hipError_t e = grape_walk::launch_pair(s, p->Ps[pa], Bc[pa], p->Ps[pb], Bc[pb], st);

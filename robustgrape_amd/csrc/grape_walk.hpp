@@ -897,6 +897,30 @@ __device__ __forceinline__ void gauge_base(const DevProblem &P, cptr<cd> ops, cd
         }
     }
 }
+// gauge_base without the register copy: E~ of the workgroup's NE sectors stays in LDS, row-major
+// [w][D][D] (the merged walks read it at every step: 52 VGPRs fewer at DA = 3)
+template <int D, int NE>
+__device__ __forceinline__ const cd *gauge_base_lds(const DevProblem &P, cptr<cd> ops, cd *scr) {
+    __shared__ cd gE[NE * D * D];
+    if ((int)threadIdx.x < NE) {
+        const int w = threadIdx.x;
+        WalkX X0;
+        X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
+        Pert none;
+        none.var = -1;
+        none.index = 0;
+        none.delta = 0.0;
+        SM<D> A[1];
+        walk_build<D, 1>(P, ops + (size_t)w * P.sec_ops, X0, 1, none, A);
+        double mu0 = 0.0;
+        walk_expm<D, false, true, false>(A[0], scr, mu0, true, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) gE[(w * D + j) * D + i] = x[j];
+        });
+    }
+    __syncthreads();
+    return gE;
+}
 // the level phases d_j = e^{i theta N_j} of one sector from p = e^{i theta}
 template <int D>
 __device__ __forceinline__ void gauge_phases(cd p, const GaugeN<D> &g, cd (&d)[D]) {
@@ -1354,6 +1378,273 @@ __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0,
     const int id = blockIdx.x, n0 = gx0 * gy0;
     if (id < n0) walk_grad_body<D0, NS0, ST0 && !GA, 1, false, GA>(P0, B0, VBlock{id % gx0, id / gx0, gx0});
     else walk_grad_body<D1, NS1, false, 1, TW1, GA>(P1, B1, VBlock{(id - n0) % gx1, (id - n0) / gx1, gx1});
+}
+
+// ---------------------------------------------------------------------------
+// Merged phase-covariant walks (round 5): BOTH sector classes of the Rydberg layout in one lane
+// ---------------------------------------------------------------------------
+// The C2 walks are VALU-issue bound (≈ 84 % of SIMD cycles issue VALU instructions in every one of
+// the four walk kernels, profiles/r05/final_c2 instruction mix), and the two classes' lanes of one
+// (evaluation, chunk) repeat the same per-step work: the load of x_k, e^{i a x_k}, e^{i phi} - 1,
+// the loop.  A merged lane walks class A (one sector of DA levels) and class B (two 2-level
+// sectors, twins or not) over the same chunk, sharing that work, and its gradient walk writes ONE
+// F_dx part, (0 + part_A) + part_B in the plan's class order -- the value k_sec_reduce would have
+// formed from the two parts -- so the reduction reads one part.  Per class the operations are the
+// gauge walks' own (walk_fwd_body / walk_grad_body with GAUGE): at equal chunking the results are
+// those of the per-class kernels bit for bit.  Both classes take class A's chunking (the engine
+// sets class B's L and nchunks to class A's).
+#ifndef GRAPE_WALK_MERGED_WAVES
+#define GRAPE_WALK_MERGED_WAVES 2
+#endif
+template <int D>
+__device__ __forceinline__ void gauge_prop_lds(const cd *Et, const cd (&d)[D], MStore<D, false> &E) {  // gauge_prop, E~ in LDS
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const cd e = Et[j * D + k];
+            E.set(j, k, j == k ? e : cmul(cmul(d[j], e), cconj(d[k])));
+        }
+    }
+}
+template <int D, int NE>
+__device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, bool act,
+                                                cd (&Q)[NE][D][D]) {
+#pragma unroll
+    for (int w = 0; w < NE; ++w) {
+        cd dph[D];
+        gauge_phases<D>(p1, gn[w], dph);
+        MStore<D, false> E;
+        gauge_prop_lds<D>(Et + w * D * D, dph, E);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {  // column i of E_k Q (the forward walk's order)
+            cd q[D], t[D];
+#pragma unroll
+            for (int m = 0; m < D; ++m) q[m] = Q[w][m][i];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, q[m], E.at(j, m));
+                t[j] = c;
+            }
+#pragma unroll
+            for (int j = 0; j < D; ++j) Q[w][j][i] = cmake(act ? t[j].re : Q[w][j][i].re, act ? t[j].im : Q[w][j][i].im);
+        }
+    }
+}
+template <int DA, bool TWB>
+__global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fwd_m(DevProblem PA, DevBatch BA,
+                                                                                  DevProblem PB, DevBatch BB) {
+    constexpr int NEB = TWB ? 1 : 2;
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<1>(PA, BA, vb);  // (class A: one sector; its chunking is both classes')
+    const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
+    const int xs = kWalkXRow ? 1 : L.nbe;
+    const cd *EtA = gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
+    const cd *EtB = gauge_base_lds<2, NEB>(PB, as_constant(PB.ops), BB.wscr + (size_t)L.slot * 2 * 2 * 4);
+    GaugeN<DA> gA[1];
+    GaugeN<2> gB[NEB];
+    gA[0] = gauge_charges<DA>(PA, 0);
+#pragma unroll
+    for (int w = 0; w < NEB; ++w) gB[w] = gauge_charges<2>(PB, w);
+    cd QA[1][DA][DA], QB[NEB][2][2];
+#pragma unroll
+    for (int j = 0; j < DA; ++j) {
+#pragma unroll
+        for (int i = 0; i < DA; ++i) QA[0][j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+    }
+#pragma unroll
+    for (int w = 0; w < NEB; ++w) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) QB[w][j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+        }
+    }
+    const int k0 = L.c * PA.L;
+    X2 xn = walk_load_x(1, xt + (size_t)min(k0, PA.Nt - 1) * xs, xs);
+#pragma unroll 1
+    for (int jj = 0; jj < PA.L; ++jj) {  // uniform trip count; steps past N_t leave Q alone
+        const int k = min(k0 + jj, PA.Nt - 1);
+        const bool act = k0 + jj < PA.Nt;
+        const double xk = xn.v0;
+        xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs);  // next step's control
+        double sn, cn;
+        sincos(PA.gauge_a * xk, &sn, &cn);  // e^{i a x_k}, both classes (the engine checks one a)
+        const cd p1 = cmake(cn, sn);
+        merged_step_fwd<DA, 1>(EtA, gA, p1, act, QA);
+        merged_step_fwd<2, NEB>(EtB, gB, p1, act, QB);
+    }
+    if (L.ok) {
+        cd *da = BA.Tc + ((size_t)L.be * PA.nchunks + L.c) * DA * DA;  // row-major chunk totals
+#pragma unroll
+        for (int j = 0; j < DA; ++j) {
+#pragma unroll
+            for (int i = 0; i < DA; ++i) da[j * DA + i] = QA[0][j][i];
+        }
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            cd *db = BB.Tc + (((size_t)L.be * 2 + w) * PB.nchunks + L.c) * 4;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) db[j * 2 + i] = QB[TWB ? 0 : w][j][i];
+            }
+        }
+    }
+}
+// X = Carry_c M_ww Carry_c^dag of sector w (walk_grad_body's arithmetic)
+template <int D>
+__device__ __forceinline__ void merged_xinit(const cd *Cr, const cd *Mw, cd (&X)[D][D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        cd r[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            cd v = czero();
+#pragma unroll
+            for (int e = 0; e < D; ++e) v = cadd(v, cmul(Mw[a * D + e], cconj(Cr[j * D + e])));
+            r[a] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            cd acc = czero();
+#pragma unroll
+            for (int a = 0; a < D; ++a) acc = cadd(acc, cmul(Cr[i * D + a], r[a]));
+            X[i][j] = acc;
+        }
+    }
+}
+// one gradient step of NSEC sectors over NE propagators (NSH = NSEC / NE sectors share one):
+// Y = X E^dag, the contraction, X <- E Y; returns the sectors' terms summed in sector order
+// (kWalkPresum: (0 + s_0) + s_1 ...; one sector: s_0)
+template <int D, int NE, int NSEC>
+__device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, cd q,
+                                                   double inv_eps, cd (&X)[NSEC][D][D]) {
+    constexpr int NSH = NSEC / NE;
+    MStore<D, false> E[NE];
+    cd rho[NE][D];
+#pragma unroll
+    for (int w = 0; w < NE; ++w) {
+        cd dph[D];
+        gauge_phases<D>(p1, gn[w], dph);
+        gauge_prop_lds<D>(Et + w * D * D, dph, E[w]);
+#pragma unroll
+        for (int j = 0; j < D; ++j) rho[w][j] = gauge_rho(q, gn[w].n[j]);
+    }
+#pragma unroll
+    for (int w = 0; w < NSEC; ++w) {  // Y = X E^dag, row by row
+        const int we = w / NSH;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            cd xr[D], y[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) xr[j] = X[w][r][j];
+#pragma unroll
+            for (int cc = 0; cc < D; ++cc) {
+                cd s = czero();
+#pragma unroll
+                for (int j = 0; j < D; ++j) cmac(s, xr[j], cconj(E[we].at(cc, j)));
+                y[cc] = s;
+            }
+#pragma unroll
+            for (int cc = 0; cc < D; ++cc) X[w][r][cc] = y[cc];
+        }
+    }
+    double tot = 0.0, one = 0.0;
+#pragma unroll
+    for (int we = 0; we < NE; ++we) {
+        double s[NSH];
+#pragma unroll
+        for (int t = 0; t < NSH; ++t) s[t] = 0.0;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                if (r == j) continue;
+                const cd rj = cconj(rho[we][j]);
+                const cd f = cadd(cadd(rho[we][r], rj), cmul(rho[we][r], rj));
+                const cd de = cscale(inv_eps, cmul(E[we].at(r, j), f));
+#pragma unroll
+                for (int t = 0; t < NSH; ++t) {
+                    const cd y = X[we * NSH + t][j][r];
+                    s[t] = fma(y.re, de.re, s[t]);
+                    s[t] = fma(-y.im, de.im, s[t]);
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NSH; ++t) {
+            tot += s[t];
+            one = s[t];
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NSEC; ++w) {  // X <- E Y, column by column
+        const int we = w / NSH;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            cd y[D], t[D];
+#pragma unroll
+            for (int m = 0; m < D; ++m) y[m] = X[w][m][i];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                cd c = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(c, E[we].at(j, m), y[m]);
+                t[j] = c;
+            }
+#pragma unroll
+            for (int j = 0; j < D; ++j) X[w][j][i] = t[j];
+        }
+    }
+    return (kWalkPresum && NSEC > 1) ? tot : one;
+}
+template <int DA, bool TWB>
+__global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_grad_m(DevProblem PA, DevBatch BA,
+                                                                                   DevProblem PB, DevBatch BB, int a_first) {
+    constexpr int NEB = TWB ? 1 : 2;
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<1>(PA, BA, vb);
+    const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
+    const int xs = kWalkXRow ? 1 : L.nbe;
+    cd XA[1][DA][DA], XB[2][2][2];
+    {
+        const size_t bw = (size_t)L.be;
+        merged_xinit<DA>(BA.Carry + (bw * PA.nchunks + L.c) * DA * DA, BA.Msec + bw * DA * DA, XA[0]);
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            const size_t bb = (size_t)L.be * 2 + w;
+            merged_xinit<2>(BB.Carry + (bb * PB.nchunks + L.c) * 4, BB.Msec + bb * 4, XB[w]);
+        }
+    }
+    const cd *EtA = gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
+    const cd *EtB = gauge_base_lds<2, NEB>(PB, as_constant(PB.ops), BB.wscr + (size_t)L.slot * 2 * 2 * 4);
+    GaugeN<DA> gA[1];
+    GaugeN<2> gB[NEB];
+    gA[0] = gauge_charges<DA>(PA, 0);
+#pragma unroll
+    for (int w = 0; w < NEB; ++w) gB[w] = gauge_charges<2>(PB, w);
+    const int k0 = L.c * PA.L;
+    X2 xn = walk_load_x(1, xt + (size_t)min(k0, PA.Nt - 1) * xs, xs);
+#pragma unroll 1
+    for (int jj = 0; jj < PA.L; ++jj) {  // uniform trip count; steps past N_t store nothing
+        const int k = min(k0 + jj, PA.Nt - 1);
+        const bool act = L.ok && k0 + jj < PA.Nt;
+        const double xk = xn.v0, xe = xk + PA.eps;  // the reference's perturbed control
+        xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs);  // next step's control
+        double sn, cn;
+        sincos(PA.gauge_a * xk, &sn, &cn);
+        const cd p1 = cmake(cn, sn), q = cis_m1(PA.gauge_a * (xe - xk));  // (xe - xk: exact)
+        const double sa = merged_step_grad<DA, 1, 1>(EtA, gA, p1, q, PA.inv_eps, XA);
+        const double sb = merged_step_grad<2, NEB, 2>(EtB, gB, p1, q, PB.inv_eps, XB);
+        double v = 0.0;  // k_sec_reduce's sum of the classes' parts, in the plan's class order
+        v += a_first ? sa : sb;
+        v += a_first ? sb : sa;
+        double *dst = act ? BA.sec_part + (size_t)k * L.nbe + L.be : reinterpret_cast<double *>(BA.sink);
+        *dst = v;
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -41,6 +41,13 @@ hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &
 bool pair_ok(const grape::DevProblem &P0, const grape::DevProblem &P1);
 hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevBatch &B0, const grape::DevProblem &P1,
                        const grape::DevBatch &B1, hipStream_t st);
+// Throughput passes of the same layout with phase-covariant classes at equal chunking: ONE lane walks
+// both classes of an (evaluation, chunk) (k_walk_fwd_m / k_walk_grad_m); the gradient stage writes
+// one F_dx part, class 0's + class 1's (a_first: class A is the plan's class 0), into class A's
+// sec_part.  merged_ok tells whether the classes fit.
+bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB);
+hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
+                         const grape::DevBatch &BB, int a_first, hipStream_t st);
 // F_dx parts the class's gradient stage writes per evaluation: its sectors, or (k_walk_grad with several
 // sectors per lane, no error sources) one pre-summed part per lane row (grape_walk.hpp kWalkPresum)
 int grad_parts(const grape::DevProblem &P);

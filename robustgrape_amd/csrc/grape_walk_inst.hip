@@ -137,6 +137,27 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
     return hipGetLastError();
 }
 
+bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB) {
+    // (class A of 3 levels: at 4 levels the merged gradient lane spills at 2 waves per SIMD)
+    return pair_ok(PA, PB) && PA.D == 3 && PA.gauge && PB.gauge && PA.gauge_a == PB.gauge_a && PA.L == PB.L &&
+           PA.nchunks == PB.nchunks && PA.np == 1 && PA.na <= 1;
+}
+hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
+                         const grape::DevBatch &BB, int a_first, hipStream_t st) {
+    if (!merged_ok(PA, PB)) return hipErrorInvalidValue;
+    const long lanes = (long)BA.nb * PA.nchunks;  // (class A: one sector, BA.nb evaluations)
+    const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock)), blk(grape::kWalkBlock);
+    auto go = [&](auto da, auto tw) {
+        constexpr int DA = decltype(da)::value;
+        constexpr bool TW = decltype(tw)::value;
+        if (stage == 0) hipLaunchKernelGGL((grape::k_walk_fwd_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB);
+        else hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
+    };
+    using I3 = std::integral_constant<int, 3>;
+    PB.twin ? go(I3{}, std::true_type{}) : go(I3{}, std::false_type{});
+    return hipGetLastError();
+}
+
 // x [nb][nx] -> xT [nx][nb] through a 32 x 32 LDS tile (both sides coalesced)
 __global__ __launch_bounds__(256) void k_transpose_x(const double *x, double *xT, int nb, int nx) {
     __shared__ double t[32][33];

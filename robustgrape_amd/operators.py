@@ -172,6 +172,7 @@ OPT_NO_TWIN = 2048  # every walk sector computes its own exponentials (no twin s
 OPT_GRAPH_FORK = 4096  # accepted and ignored since round 5 (the captured fork was removed)
 OPT_NO_GAUGE = 8192  # per-step exponentials even for phase-covariant walk classes (grape_walk.hpp GAUGE)
 OPT_NO_EVAL1 = 16384  # latency-bound calls through the pair-kernel pipeline, not one workgroup per evaluation
+OPT_NO_MERGE = 32768  # throughput passes: one walk kernel per sector class instead of merged lanes
 
 
 def _reserved(flags: int = 0, options: int = 0, scan_waves: int = 0):

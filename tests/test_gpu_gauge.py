@@ -191,3 +191,34 @@ def test_gauge_image_walk_matches_per_step_exponentials_and_oracle(name, fp, bat
     for b in (0, 1):
         ro = O.calculate_fidelity_and_derivatives(f, X[b])
         _check_err(f"gauge_img_vs_oracle_{name}_{batch}_{b}", out, b, ro, P.fd_tier(f, X[b]))
+
+
+@pytest.mark.parametrize("n", [2048, 4100])
+def test_merged_walks_equal_per_class_walks_bitwise(n):
+    """Throughput passes walk both sector classes of an (evaluation, chunk) in one lane
+    (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m) at the per-class walks' chunking; with
+    GRAPE_OPT_NO_MERGE the same chunking runs one kernel per class: every output bit for bit
+    (4 100: a ragged last workgroup).  Against the per-step exponentials at the FD tier, and the
+    C2 golden inside the batch."""
+    import os
+    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_MERGE
+    g2 = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2.npz"),
+                      allow_pickle=False))
+    f = P.full9_problem(512)
+    X = np.stack([P.random_x(512, 7000 + s, small=(s % 3 != 0)) for s in range(n)])
+    X[5] = g2["x"]
+    pm, pu, pn = _plan(f, n), _plan(f, n, OPT_NO_MERGE), _plan(f, n, OPT_NO_GAUGE)
+    try:
+        F, G, _, _ = pm.fidelity_grad(X)
+        Fu, Gu, _, _ = pu.fidelity_grad(X)
+        Fn, Gn, _, _ = pn.fidelity_grad(X[:64])
+    finally:
+        pm.close()
+        pu.close()
+        pn.close()
+    assert np.array_equal(F, Fu) and np.array_equal(G, Gu)
+    _check(f"merged_c2_golden_{n}", F[5], G[5], g2["F"], g2["F_dx"], (1e-7, 1e-9))
+    assert float(np.max(np.abs(F[:64] - Fn))) <= T1
+    err = np.max(np.abs(G[:64] - Gn), axis=1)
+    scale = np.max(np.abs(Gn), axis=1)
+    assert np.all(err <= 1e-7 * scale + 1e-9), float(np.max(err / scale))
