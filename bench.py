@@ -449,7 +449,10 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                                 "twin": bool(twins[c])}
                                for c, (S, ns) in enumerate(classes)] if sec else None,
                    "symmetry_adapted": bool((info or {}).get("symmetric", False)),
-                   "phase_covariant": [bool(g) for g in gauges[:len(classes)]]},
+                   "phase_covariant": [bool(g) for g in gauges[:len(classes)]],
+                   # both classes in one lane (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m): one walk
+                   # launch per stage and pass instead of one per class
+                   "merged_walks": bool(walk and passes and ktimes.get("k_walk_grad", (0.0, 0))[1] == passes)},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
         "kernels_ms_per_pass": per_pass,

@@ -1761,10 +1761,9 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
                 mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 0);
                 hipError_t e = grape_walk::launch_merged(s, p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], ma == 0 ? 1 : 0, st);
                 mk(s == 0 ? GRAPE_KERNEL_WALK_FWD : GRAPE_KERNEL_WALK_GRAD, 1);
-                if (e == hipSuccess && s == 0) {
+                if (e == hipSuccess && s == 0) {  // the merged walks' sequential scan (lane-minor totals)
                     mk(GRAPE_KERNEL_SCAN, 0);
-                    e = p->Ps[ma].D == 4 ? grape_host::launch_scan_pair<4, 2, kScanTiny>(p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], st)
-                                         : grape_host::launch_scan_pair<3, 2, kScanTiny>(p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], st);
+                    e = grape_walk::launch_merged(2, p->Ps[ma], Bc[ma], p->Ps[mb], Bc[mb], ma == 0 ? 1 : 0, st);
                     mk(GRAPE_KERNEL_SCAN, 1);
                 }
                 return e;

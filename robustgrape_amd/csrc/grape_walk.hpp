@@ -1476,20 +1476,91 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fw
         merged_step_fwd<DA, 1>(EtA, gA, p1, act, QA);
         merged_step_fwd<2, NEB>(EtB, gB, p1, act, QB);
     }
-    if (L.ok) {
-        cd *da = BA.Tc + ((size_t)L.be * PA.nchunks + L.c) * DA * DA;  // row-major chunk totals
+    if (L.ok) {  // chunk totals lane-minor (k_scan_seq's coalesced reads): [c][element][evaluation]
+        const size_t nbe = (size_t)L.nbe;
+        cd *da = BA.Tc + (size_t)L.c * DA * DA * nbe + L.be;
 #pragma unroll
         for (int j = 0; j < DA; ++j) {
 #pragma unroll
-            for (int i = 0; i < DA; ++i) da[j * DA + i] = QA[0][j][i];
+            for (int i = 0; i < DA; ++i) da[(size_t)(j * DA + i) * nbe] = QA[0][j][i];
         }
 #pragma unroll
-        for (int w = 0; w < 2; ++w) {
-            cd *db = BB.Tc + (((size_t)L.be * 2 + w) * PB.nchunks + L.c) * 4;
+        for (int w = 0; w < NEB; ++w) {  // (twins: one chain)
+            cd *db = BB.Tc + ((size_t)w * PB.nchunks + L.c) * 4 * nbe + L.be;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i) db[j * 2 + i] = QB[TWB ? 0 : w][j][i];
+                for (int i = 0; i < 2; ++i) db[(size_t)(j * 2 + i) * nbe] = QB[w][j][i];
+            }
+        }
+    }
+}
+// The merged path's scan: one lane per evaluation walks its chunk totals in order,
+// Carry_0 = I, Carry_{c+1} = T_c Carry_c, U = T_{n-1} Carry_{n-1} -- 2 x (n - 1) small products per
+// lane where k_scan_pair spends a wave per sub-evaluation on a Hillis-Steele scan, and every read and
+// carry write coalesced (lane-minor [c][element][evaluation]); U row-major per sub-evaluation, as
+// the sector head reads it.  (The association of the chain differs from k_scan's: rounding only.)
+template <int D, int NE>
+__device__ __forceinline__ void scan_seq_chain(const cd *T, cd *Carry, int nch, size_t nbe, size_t be, cd (&P)[D][D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) P[j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+    }
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+        cd *dc = Carry + (size_t)c * D * D * nbe + be;
+        const cd *tc = T + (size_t)c * D * D * nbe + be;
+        cd t[D][D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                dc[(size_t)(j * D + i) * nbe] = P[j][i];
+                t[j][i] = tc[(size_t)(j * D + i) * nbe];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {  // P <- T_c P, column by column
+            cd q[D];
+#pragma unroll
+            for (int m = 0; m < D; ++m) q[m] = P[m][i];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                cd acc = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(acc, t[j][m], q[m]);
+                P[j][i] = acc;
+            }
+        }
+    }
+}
+template <int DA, bool TWB>
+__global__ __launch_bounds__(256) void k_scan_seq(DevProblem PA, DevBatch BA, DevProblem PB, DevBatch BB, int nb) {
+    constexpr int NEB = TWB ? 1 : 2;
+    const size_t be = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (be >= (size_t)nb) return;
+    const size_t nbe = (size_t)nb;
+    cd U[DA][DA];
+    scan_seq_chain<DA, 1>(BA.Tc, BA.Carry, PA.nchunks, nbe, be, U);
+    cd *ua = BA.Ub + be * DA * DA;
+#pragma unroll
+    for (int j = 0; j < DA; ++j) {
+#pragma unroll
+        for (int i = 0; i < DA; ++i) ua[j * DA + i] = U[j][i];
+    }
+#pragma unroll
+    for (int w = 0; w < NEB; ++w) {
+        cd V[2][2];
+        scan_seq_chain<2, 1>(BB.Tc + (size_t)w * PB.nchunks * 4 * nbe, BB.Carry + (size_t)w * PB.nchunks * 4 * nbe,
+                             PB.nchunks, nbe, be, V);
+#pragma unroll
+        for (int ws = 0; ws < (TWB ? 2 : 1); ++ws) {  // (twins: both sectors' U)
+            cd *ub = BB.Ub + (be * 2 + w + ws) * 4;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) ub[j * 2 + i] = V[j][i];
             }
         }
     }
@@ -1610,13 +1681,20 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
     const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
     const int xs = kWalkXRow ? 1 : L.nbe;
     cd XA[1][DA][DA], XB[2][2][2];
-    {
-        const size_t bw = (size_t)L.be;
-        merged_xinit<DA>(BA.Carry + (bw * PA.nchunks + L.c) * DA * DA, BA.Msec + bw * DA * DA, XA[0]);
+    {  // carries lane-minor (k_scan_seq), the head's M blocks row-major per sub-evaluation
+        const size_t nbe = (size_t)L.nbe, be = (size_t)L.be;
+        cd Cr[DA * DA];
+        const cd *ca = BA.Carry + (size_t)L.c * DA * DA * nbe + be;
+#pragma unroll
+        for (int e = 0; e < DA * DA; ++e) Cr[e] = ca[(size_t)e * nbe];
+        merged_xinit<DA>(Cr, BA.Msec + be * DA * DA, XA[0]);
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
-            const size_t bb = (size_t)L.be * 2 + w;
-            merged_xinit<2>(BB.Carry + (bb * PB.nchunks + L.c) * 4, BB.Msec + bb * 4, XB[w]);
+            cd Cb[4];
+            const cd *cb = BB.Carry + ((size_t)(TWB ? 0 : w) * PB.nchunks + L.c) * 4 * nbe + be;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Cb[e] = cb[(size_t)e * nbe];
+            merged_xinit<2>(Cb, BB.Msec + (be * 2 + w) * 4, XB[w]);
         }
     }
     const cd *EtA = gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);

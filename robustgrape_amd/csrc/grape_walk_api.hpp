@@ -44,7 +44,8 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
 // Throughput passes of the same layout with phase-covariant classes at equal chunking: ONE lane walks
 // both classes of an (evaluation, chunk) (k_walk_fwd_m / k_walk_grad_m); the gradient stage writes
 // one F_dx part, class 0's + class 1's (a_first: class A is the plan's class 0), into class A's
-// sec_part.  merged_ok tells whether the classes fit.
+// sec_part.  Stage 0: k_walk_fwd_m (chunk totals, lane-minor), stage 2: k_scan_seq (carries and U
+// from them), stage 1: k_walk_grad_m.  merged_ok tells whether the classes fit.
 bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB);
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
                          const grape::DevBatch &BB, int a_first, hipStream_t st);

@@ -150,8 +150,14 @@ hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::De
     auto go = [&](auto da, auto tw) {
         constexpr int DA = decltype(da)::value;
         constexpr bool TW = decltype(tw)::value;
-        if (stage == 0) hipLaunchKernelGGL((grape::k_walk_fwd_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB);
-        else hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
+        if (stage == 0) {
+            hipLaunchKernelGGL((grape::k_walk_fwd_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB);
+        } else if (stage == 2) {  // the chunk-total scan (one lane per evaluation)
+            hipLaunchKernelGGL((grape::k_scan_seq<DA, TW>), dim3((unsigned)((BA.nb + 255) / 256)), dim3(256), 0, st, PA,
+                               BA, PB, BB, BA.nb);
+        } else {
+            hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
+        }
     };
     using I3 = std::integral_constant<int, 3>;
     PB.twin ? go(I3{}, std::true_type{}) : go(I3{}, std::false_type{});

@@ -194,12 +194,14 @@ def test_gauge_image_walk_matches_per_step_exponentials_and_oracle(name, fp, bat
 
 
 @pytest.mark.parametrize("n", [2048, 4100])
-def test_merged_walks_equal_per_class_walks_bitwise(n):
+def test_merged_walks_match_per_class_walks(n):
     """Throughput passes walk both sector classes of an (evaluation, chunk) in one lane
-    (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m) at the per-class walks' chunking; with
-    GRAPE_OPT_NO_MERGE the same chunking runs one kernel per class: every output bit for bit
-    (4 100: a ragged last workgroup).  Against the per-step exponentials at the FD tier, and the
-    C2 golden inside the batch."""
+    (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m) at the per-class walks' chunking and scan the chunk
+    totals one lane per evaluation (k_scan_seq); with GRAPE_OPT_NO_MERGE the same chunking runs one
+    walk kernel per class and the Hillis-Steele scan: the same per-step arithmetic, the chain
+    associated differently, so F to T1 and F_dx to 1e-11 of max|F_dx| (4 100: a ragged last
+    workgroup).  Against the per-step exponentials at the FD tier, and the C2 golden inside the
+    batch."""
     import os
     from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_MERGE
     g2 = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2.npz"),
@@ -216,7 +218,9 @@ def test_merged_walks_equal_per_class_walks_bitwise(n):
         pm.close()
         pu.close()
         pn.close()
-    assert np.array_equal(F, Fu) and np.array_equal(G, Gu)
+    assert float(np.max(np.abs(F - Fu))) <= T1
+    err_u = np.max(np.abs(G - Gu), axis=1)
+    assert np.all(err_u <= 1e-11 * np.max(np.abs(Gu), axis=1) + 1e-13), float(np.max(err_u))
     _check(f"merged_c2_golden_{n}", F[5], G[5], g2["F"], g2["F_dx"], (1e-7, 1e-9))
     assert float(np.max(np.abs(F[:64] - Fn))) <= T1
     err = np.max(np.abs(G[:64] - Gn), axis=1)
