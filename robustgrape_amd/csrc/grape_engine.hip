@@ -1833,7 +1833,9 @@ static int enqueue(grape_plan *p, int nb, const double *d_x, double *d_F, double
             mk(GRAPE_KERNEL_ERR_SCAN, 1);
             HIPCHECK(stage(2));
         }
-        HIPCHECK(dispatch_sector_reduce(p->Ps[0].D, p->Ps[0], Bc[0], sp, nb, st, mk));
+        // (the merged gradient walk wrote F_dx itself; without x_add-dependent H0 nothing is left to sum)
+        if (!(p->merged && grape_walk::merged_writes_fdx() && !(p->P.xadd_dep && p->P.na > 0)))
+            HIPCHECK(dispatch_sector_reduce(p->Ps[0].D, p->Ps[0], Bc[0], sp, nb, st, mk));
         return GRAPE_OK;
     }
     const DevProblem &P = p->P;

@@ -1672,14 +1672,21 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
     }
     return (kWalkPresum && NSEC > 1) ? tot : one;
 }
+#ifndef GRAPE_WALK_MERGED_FDX  // the merged gradient walk writes F_dx itself (1) or a part for k_sec_reduce (0)
+#define GRAPE_WALK_MERGED_FDX 1
+#endif
+constexpr int kFdxTile = 16;  // steps per F_dx tile flush
 template <int DA, bool TWB>
 __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_grad_m(DevProblem PA, DevBatch BA,
                                                                                    DevProblem PB, DevBatch BB, int a_first) {
     constexpr int NEB = TWB ? 1 : 2;
+    __shared__ double ftile[kWalkBlock][kFdxTile + 1];  // (GRAPE_WALK_MERGED_FDX; +1: conflict-free rows)
+    __shared__ int2 frow[kWalkBlock];                   // each row's evaluation and first step
     const VBlock vb = hw_block();
     const WalkLane L = walk_lane<1>(PA, BA, vb);
     const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
     const int xs = kWalkXRow ? 1 : L.nbe;
+    if constexpr (GRAPE_WALK_MERGED_FDX) frow[threadIdx.x] = make_int2(L.ok ? L.be : -1, L.c * PA.L);
     cd XA[1][DA][DA], XB[2][2][2];
     {  // carries lane-minor (k_scan_seq), the head's M blocks row-major per sub-evaluation
         const size_t nbe = (size_t)L.nbe, be = (size_t)L.be;
@@ -1720,8 +1727,27 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
         double v = 0.0;  // k_sec_reduce's sum of the classes' parts, in the plan's class order
         v += a_first ? sa : sb;
         v += a_first ? sb : sa;
-        double *dst = act ? BA.sec_part + (size_t)k * L.nbe + L.be : reinterpret_cast<double *>(BA.sink);
-        *dst = v;
+        if constexpr (GRAPE_WALK_MERGED_FDX) {
+            // F_dx straight to its [evaluation][n_x] row through a workgroup tile of kFdxTile steps:
+            // the lanes of a workgroup hold consecutive evaluations, so a flush writes 16 lanes'
+            // kFdxTile-long row pieces per instruction (no part array, no k_sec_reduce)
+            const int jt = jj % kFdxTile;
+            ftile[threadIdx.x][jt] = v;
+            if (jt == kFdxTile - 1 || jj == PA.L - 1) {
+                __syncthreads();
+                const int j0 = jj - jt, nj = jt + 1;
+                const int j = threadIdx.x % kFdxTile;
+#pragma unroll 1
+                for (int row = threadIdx.x / kFdxTile; row < kWalkBlock; row += kWalkBlock / kFdxTile) {
+                    const int br = frow[row].x, kk = frow[row].y + j0 + j;  // (br < 0: past the last lane)
+                    if (j < nj && br >= 0 && kk < PA.Nt) BA.Fdx[(size_t)br * PA.nx + kk] = ftile[row][j];
+                }
+                __syncthreads();
+            }
+        } else {
+            double *dst = act ? BA.sec_part + (size_t)k * L.nbe + L.be : reinterpret_cast<double *>(BA.sink);
+            *dst = v;
+        }
     }
 }
 

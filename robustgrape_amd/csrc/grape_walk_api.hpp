@@ -16,10 +16,13 @@ constexpr int kWalkBlockA = 128;  // lanes per workgroup (grape_walk.hpp kWalkBl
 #define GRAPE_WALK_STORE_MIN_D 4
 #endif
 constexpr int kWalkStoreMinD = GRAPE_WALK_STORE_MIN_D;
-// GRAPE_WALK_XROW (A/B): the walks read the controls row-major from x itself (B.xT = x, stride 1 per
-// value, nx per evaluation) instead of the transposed copy, and the engine skips k_transpose_x
+// GRAPE_WALK_XROW: the walks read the controls row-major from x itself (B.xT = x, stride 1 per value,
+// nx per evaluation) instead of a transposed copy, and the engine skips k_transpose_x.  Each lane
+// streams its own row: 8 steps per 64-B line, reused from the vector cache.  Round 4 (per-class
+// walks) measured it neutral; with the merged walks it wins: C2 36.8 -> 38.4 M evals/s (fwd 0.269 ->
+// 0.222, grad 0.470 -> 0.481 ms per pass, no transpose; profiles/r05/ab_xrow)
 #ifndef GRAPE_WALK_XROW
-#define GRAPE_WALK_XROW 0
+#define GRAPE_WALK_XROW 1
 #endif
 constexpr bool kWalkXRow = GRAPE_WALK_XROW;
 }  // namespace grape
@@ -47,6 +50,8 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
 // sec_part.  Stage 0: k_walk_fwd_m (chunk totals, lane-minor), stage 2: k_scan_seq (carries and U
 // from them), stage 1: k_walk_grad_m.  merged_ok tells whether the classes fit.
 bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB);
+// 1: the merged gradient walk writes F_dx rows itself (no k_sec_reduce for such passes)
+bool merged_writes_fdx();
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
                          const grape::DevBatch &BB, int a_first, hipStream_t st);
 // F_dx parts the class's gradient stage writes per evaluation: its sectors, or (k_walk_grad with several

@@ -142,6 +142,7 @@ bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB) {
     return pair_ok(PA, PB) && PA.D == 3 && PA.gauge && PB.gauge && PA.gauge_a == PB.gauge_a && PA.L == PB.L &&
            PA.nchunks == PB.nchunks && PA.np == 1 && PA.na <= 1;
 }
+bool merged_writes_fdx() { return GRAPE_WALK_MERGED_FDX != 0; }
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
                          const grape::DevBatch &BB, int a_first, hipStream_t st) {
     if (!merged_ok(PA, PB)) return hipErrorInvalidValue;
