@@ -605,7 +605,8 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     fp = flop_model[kname] / (ms * 1e-3) / 1e12
     hb = byte_model[kname] / (ms * 1e-3) / 1e9
     img_kernel = "k_walk_img_gauge" if any(gauges[:len(classes)]) else "k_walk_img"
-    short = {"k_grad/k_err_local": "k_err_local", "k_walk_fwd": img_kernel}.get(kname, kname)
+    short = {"k_grad/k_err_local": "k_err_local", "k_walk_fwd": img_kernel,
+             "k_err_grad": "k_walk_err_grad" if walk else "k_err_grad"}.get(kname, kname)
     traffic = pmc_traffic(short, L, PMC_SUMMARY_C3, dims={S for S, _ in classes})
     if hb / HBM_PEAK_GBS > fp / FP64_PEAK_TFLOPS:
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -149,12 +149,12 @@ __device__ __forceinline__ void m_rmul(cd (&R)[D][D], const cd (&B)[D][D]) {
 // E_k = D_k E~ D_k^dag from p1 = e^{i a x_k} (gauge_prop's arithmetic)
 template <int D>
 __device__ __forceinline__ void step_prop(const cd (&Et)[D][D], const GaugeN<D> &gn, cd p1, cd (&E)[D][D]) {
-    cd dph[D];
+    cd dph[kGaugePairs<D>];
     gauge_phases<D>(p1, gn, dph);
 #pragma unroll
     for (int j = 0; j < D; ++j) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) E[j][k] = j == k ? Et[j][k] : cmul(cmul(dph[j], Et[j][k]), cconj(dph[k]));
+        for (int k = 0; k < D; ++k) E[j][k] = gauge_sandwich<D>(dph, j, k, Et[j][k]);
     }
 }
 template <int D>
@@ -316,14 +316,14 @@ __device__ __forceinline__ void lane_grad(const DevProblem &Pc, const cd *EtL, c
         for (int w = 0; w < NSEC; ++w) s[w] = 0.0;
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
+            cd fw[kGaugePairs<D>];
+            gauge_fd_weights<D>(rho[e], fw);
 #pragma unroll
             for (int r = 0; r < D; ++r) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
                     if (r == j) continue;
-                    const cd rj = cconj(rho[e][j]);
-                    const cd f = cadd(cadd(rho[e][r], rj), cmul(rho[e][r], rj));
-                    const cd de = cscale(Pc.inv_eps, cmul(E[e][r][j], f));
+                    const cd de = cscale(Pc.inv_eps, cmul(E[e][r][j], gauge_fd_weight<D>(fw, r, j)));
 #pragma unroll
                     for (int t = 0; t < NSH; ++t) {
                         const cd y = X[e * NSH + t][j][r];

@@ -828,6 +828,11 @@ struct GaugeN {
     int n[D];
 };
 template <int D>
+constexpr int kGaugePairs = D > 1 ? D * (D - 1) / 2 : 1;  // level pairs j < k of a sector
+__host__ __device__ constexpr int gauge_pair(int D, int j, int k) {  // j < k, row-major pair order
+    return j * D - j * (j + 1) / 2 + (k - j - 1);
+}
+template <int D>
 __device__ __forceinline__ GaugeN<D> gauge_charges(const DevProblem &P, int w) {
     const cptr<int> g = as_constant(P.gauge_n) + (size_t)w * D;
     GaugeN<D> r;
@@ -845,12 +850,16 @@ __device__ __forceinline__ cd gauge_pow(cd z, int n) {
 }
 // e^{i phi} - 1 without cancellation: (-2 sin^2(phi / 2), sin phi); Taylor for the FD-sized
 // phases (|phi| <= 0.05: truncation below 1e-22 relative), the library otherwise
+// (round 5: Horner in t^2 with the reciprocal factorials as constants -- the quotient form spent
+// 8 double divisions per step, ~7 % of the merged gradient walk's VALU instructions)
+__device__ __forceinline__ double sin_small(double t) {  // sin t, |t| <= 0.05: Taylor to t^9
+    const double t2 = t * t;
+    return t * fma(t2, fma(t2, fma(t2, fma(t2, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0), 1.0);
+}
 __device__ __forceinline__ cd cis_m1(double phi) {
     if (fabs(phi) <= 0.05) {
-        const double p2 = phi * phi, h = 0.5 * phi, h2 = h * h;
-        const double s = phi * (1.0 - p2 / 6.0 * (1.0 - p2 / 20.0 * (1.0 - p2 / 42.0 * (1.0 - p2 / 72.0))));
-        const double sh = h * (1.0 - h2 / 6.0 * (1.0 - h2 / 20.0 * (1.0 - h2 / 42.0 * (1.0 - h2 / 72.0))));
-        return cmake(-2.0 * sh * sh, s);
+        const double sh = sin_small(0.5 * phi);
+        return cmake(-2.0 * sh * sh, sin_small(phi));
     }
     const double sh = sin(0.5 * phi);
     return cmake(-2.0 * sh * sh, sin(phi));
@@ -861,6 +870,24 @@ __device__ __forceinline__ cd gauge_rho(cd q, int n) {
 #pragma unroll 1
     for (int m = 0; m < n; ++m) r = cadd(cadd(r, q), cmul(q, r));
     return r;
+}
+// the difference weights f_rj = (1 + rho_r)(1 + conj(rho_j)) - 1 = rho_r + conj(rho_j) + rho_r conj(rho_j)
+// (no cancellation) of (E' - E)_rj = E_rj f_rj, formed once per pair r < j: f_jr = conj(f_rj) bit for bit
+// (the same roundings, conjugated)
+template <int D>
+__device__ __forceinline__ void gauge_fd_weights(const cd (&rho)[D], cd (&f)[kGaugePairs<D>]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+#pragma unroll
+        for (int j = r + 1; j < D; ++j) {
+            const cd rj = cconj(rho[j]);
+            f[gauge_pair(D, r, j)] = cadd(cadd(rho[r], rj), cmul(rho[r], rj));
+        }
+    }
+}
+template <int D>
+__device__ __forceinline__ cd gauge_fd_weight(const cd (&f)[kGaugePairs<D>], int r, int j) {
+    return r < j ? f[gauge_pair(D, r, j)] : cconj(f[gauge_pair(D, j, r)]);
 }
 // E~ = exp(-i dt H_w(0)) of the workgroup's NE sectors (the nominal build at x = 0; no diagonal shift,
 // so E~ carries its own phase), into every lane's Et.  Every lane of a workgroup walks the same
@@ -921,19 +948,34 @@ __device__ __forceinline__ const cd *gauge_base_lds(const DevProblem &P, cptr<cd
     __syncthreads();
     return gE;
 }
-// the level phases d_j = e^{i theta N_j} of one sector from p = e^{i theta}
+// The pair phases e_jk = e^{i theta (N_j - N_k)}, j < k (gauge_pair order), of one
+// sector from p = e^{i theta}: p^|N_j - N_k| (|N_j - N_k| - 1 products, exactly 1 for equal charges),
+// conjugated when N_j < N_k.  Round 5: E_jk = E~_jk e_jk and e_kj = conj(e_jk) take one complex
+// product per off-diagonal element where d_j E~_jk conj(d_k) from the level phases took two.
 template <int D>
-__device__ __forceinline__ void gauge_phases(cd p, const GaugeN<D> &g, cd (&d)[D]) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) d[j] = gauge_pow(p, g.n[j]);
-}
-// E_jk = d_j E~_jk conj(d_k); the diagonal is E~'s own (d_j conj(d_j) = 1 exactly)
-template <int D, class Store>
-__device__ __forceinline__ void gauge_prop(const cd (&Et)[D][D], const cd (&d)[D], Store &E) {
+__device__ __forceinline__ void gauge_phases(cd p, const GaugeN<D> &g, cd (&e)[kGaugePairs<D>]) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) E.set(j, k, j == k ? Et[j][k] : cmul(cmul(d[j], Et[j][k]), cconj(d[k])));
+        for (int k = j + 1; k < D; ++k) {
+            const int dn = g.n[j] - g.n[k];
+            const cd z = gauge_pow(p, dn < 0 ? -dn : dn);
+            e[gauge_pair(D, j, k)] = cmake(z.re, dn < 0 ? -z.im : z.im);
+        }
+    }
+}
+// d_j M_jk conj(d_k) = M_jk e_jk (e_jj = 1: the diagonal unchanged)
+template <int D>
+__device__ __forceinline__ cd gauge_sandwich(const cd (&e)[kGaugePairs<D>], int j, int k, cd m) {
+    return j == k ? m : j < k ? cmul(m, e[gauge_pair(D, j, k)]) : cmul(m, cconj(e[gauge_pair(D, k, j)]));
+}
+// E_k = D_k E~ D_k^dag; the diagonal is E~'s own
+template <int D, class Store>
+__device__ __forceinline__ void gauge_prop(const cd (&Et)[D][D], const cd (&e)[kGaugePairs<D>], Store &E) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) E.set(j, k, gauge_sandwich<D>(e, j, k, Et[j][k]));
     }
 }
 
@@ -1006,7 +1048,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         for (int w = 0; w < NE; ++w) {
             double mu = 0.0;
             if constexpr (GAUGE) {
-                cd dph[D];
+                cd dph[kGaugePairs<D>];
                 gauge_phases<D>(p1, gn[w], dph);
                 gauge_prop<D>(Et[w], dph, E);
             } else {
@@ -1171,7 +1213,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
             const cd p1 = cmake(cn, sn), q = cis_m1(P.gauge_a * (xe - xk));  // (xe - xk: exact)
 #pragma unroll
             for (int w = 0; w < NE; ++w) {
-                cd dph[D];
+                cd dph[kGaugePairs<D>];
                 gauge_phases<D>(p1, gn[w], dph);
                 gauge_prop<D>(Et[w], dph, E[w]);
                 mu[w] = 0.0;
@@ -1237,14 +1279,14 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
 #pragma unroll
                 for (int t = 0; t < NSH; ++t) s[t] = 0.0;
                 const auto &Ej = E[we].opaque();
+                cd fw[kGaugePairs<D>];
+                gauge_fd_weights<D>(rho[we], fw);
 #pragma unroll
                 for (int r = 0; r < D; ++r) {
 #pragma unroll
                     for (int j = 0; j < D; ++j) {
                         if (r == j) continue;
-                        const cd rj = cconj(rho[we][j]);
-                        const cd f = cadd(cadd(rho[we][r], rj), cmul(rho[we][r], rj));
-                        const cd de = cscale(P.inv_eps, cmul(Ej.at(r, j), f));
+                        const cd de = cscale(P.inv_eps, cmul(Ej.at(r, j), gauge_fd_weight<D>(fw, r, j)));
 #pragma unroll
                         for (int t = 0; t < NSH; ++t) {
                             const cd y = X[we * NSH + t].opaque().at(j, r);
@@ -1397,22 +1439,19 @@ __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0,
 #define GRAPE_WALK_MERGED_WAVES 2
 #endif
 template <int D>
-__device__ __forceinline__ void gauge_prop_lds(const cd *Et, const cd (&d)[D], MStore<D, false> &E) {  // gauge_prop, E~ in LDS
+__device__ __forceinline__ void gauge_prop_lds(const cd *Et, const cd (&e)[kGaugePairs<D>],
+                                               MStore<D, false> &E) {  // gauge_prop, E~ in LDS
 #pragma unroll
     for (int j = 0; j < D; ++j) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            const cd e = Et[j * D + k];
-            E.set(j, k, j == k ? e : cmul(cmul(d[j], e), cconj(d[k])));
-        }
+        for (int k = 0; k < D; ++k) E.set(j, k, gauge_sandwich<D>(e, j, k, Et[j * D + k]));
     }
 }
 template <int D, int NE>
-__device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, bool act,
-                                                cd (&Q)[NE][D][D]) {
+__device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, cd (&Q)[NE][D][D]) {
 #pragma unroll
     for (int w = 0; w < NE; ++w) {
-        cd dph[D];
+        cd dph[kGaugePairs<D>];
         gauge_phases<D>(p1, gn[w], dph);
         MStore<D, false> E;
         gauge_prop_lds<D>(Et + w * D * D, dph, E);
@@ -1429,7 +1468,7 @@ __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&
                 t[j] = c;
             }
 #pragma unroll
-            for (int j = 0; j < D; ++j) Q[w][j][i] = cmake(act ? t[j].re : Q[w][j][i].re, act ? t[j].im : Q[w][j][i].im);
+            for (int j = 0; j < D; ++j) Q[w][j][i] = t[j];
         }
     }
 }
@@ -1467,14 +1506,15 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fw
 #pragma unroll 1
     for (int jj = 0; jj < PA.L; ++jj) {  // uniform trip count; steps past N_t leave Q alone
         const int k = min(k0 + jj, PA.Nt - 1);
-        const bool act = k0 + jj < PA.Nt;
         const double xk = xn.v0;
         xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs);  // next step's control
-        double sn, cn;
-        sincos(PA.gauge_a * xk, &sn, &cn);  // e^{i a x_k}, both classes (the engine checks one a)
-        const cd p1 = cmake(cn, sn);
-        merged_step_fwd<DA, 1>(EtA, gA, p1, act, QA);
-        merged_step_fwd<2, NEB>(EtB, gB, p1, act, QB);
+        if (k0 + jj < PA.Nt) {  // (a branch, not per-element selects: only the last chunk's lanes skip)
+            double sn, cn;
+            sincos(PA.gauge_a * xk, &sn, &cn);  // e^{i a x_k}, both classes (the engine checks one a)
+            const cd p1 = cmake(cn, sn);
+            merged_step_fwd<DA, 1>(EtA, gA, p1, QA);
+            merged_step_fwd<2, NEB>(EtB, gB, p1, QB);
+        }
     }
     if (L.ok) {  // chunk totals lane-minor (k_scan_seq's coalesced reads): [c][element][evaluation]
         const size_t nbe = (size_t)L.nbe;
@@ -1598,7 +1638,7 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
     cd rho[NE][D];
 #pragma unroll
     for (int w = 0; w < NE; ++w) {
-        cd dph[D];
+        cd dph[kGaugePairs<D>];
         gauge_phases<D>(p1, gn[w], dph);
         gauge_prop_lds<D>(Et + w * D * D, dph, E[w]);
 #pragma unroll
@@ -1629,14 +1669,14 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
         double s[NSH];
 #pragma unroll
         for (int t = 0; t < NSH; ++t) s[t] = 0.0;
+        cd fw[kGaugePairs<D>];
+        gauge_fd_weights<D>(rho[we], fw);
 #pragma unroll
         for (int r = 0; r < D; ++r) {
 #pragma unroll
             for (int j = 0; j < D; ++j) {
                 if (r == j) continue;
-                const cd rj = cconj(rho[we][j]);
-                const cd f = cadd(cadd(rho[we][r], rj), cmul(rho[we][r], rj));
-                const cd de = cscale(inv_eps, cmul(E[we].at(r, j), f));
+                const cd de = cscale(inv_eps, cmul(E[we].at(r, j), gauge_fd_weight<D>(fw, r, j)));
 #pragma unroll
                 for (int t = 0; t < NSH; ++t) {
                     const cd y = X[we * NSH + t][j][r];
@@ -2116,7 +2156,7 @@ __global__ __launch_bounds__(kWalkBlock, (img_gauge_waves<D, NS>())) void k_walk
         const cd q1 = cis_m1(P.gauge_a * ((xk + P.eps) - xk)), q2 = cis_m1(P.gauge_a * ((xk + P.eps2) - xk));
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
-            cd d[D], r1[D], r2[D];
+            cd d[kGaugePairs<D>], r1[D], r2[D];
             gauge_phases<D>(p1, gn[w], d);
 #pragma unroll
             for (int j = 0; j < D; ++j) {
@@ -2131,7 +2171,7 @@ __global__ __launch_bounds__(kWalkBlock, (img_gauge_waves<D, NS>())) void k_walk
                 for (int r = 0; r < D; ++r) {
 #pragma unroll
                     for (int c = 0; c < D; ++c)
-                        Z[r][c] = cscale(sc, r == c ? Zt[r][c] : cmul(cmul(d[r], Zt[r][c]), cconj(d[c])));
+                        Z[r][c] = cscale(sc, gauge_sandwich<D>(d, r, c, Zt[r][c]));
                 }
                 cd *dst = B.Zl + img_index<D, NS>(P, vb.y, jj, w, slot, 0, lanes, lane);
 #pragma unroll
@@ -2155,18 +2195,12 @@ __global__ __launch_bounds__(kWalkBlock, (img_gauge_waves<D, NS>())) void k_walk
             };
             // E0^dag (M o f) for M = E0 (Z1) or E_e2 - E0 (Z2_e)
             auto kernel_f = [&](const cd *M, const cd (&rho)[D], cd (&Zt)[D][D]) {
-                cd Mf[D][D];
+                cd Mf[D][D], fw[kGaugePairs<D>];
+                gauge_fd_weights<D>(rho, fw);
 #pragma unroll
                 for (int r = 0; r < D; ++r) {
 #pragma unroll
-                    for (int c = 0; c < D; ++c) {
-                        if (r == c) {
-                            Mf[r][c] = czero();
-                        } else {
-                            const cd rc = cconj(rho[c]);
-                            Mf[r][c] = cmul(M[r * D + c], cadd(cadd(rho[r], rc), cmul(rho[r], rc)));
-                        }
-                    }
+                    for (int c = 0; c < D; ++c) Mf[r][c] = r == c ? czero() : cmul(M[r * D + c], gauge_fd_weight<D>(fw, r, c));
                 }
 #pragma unroll
                 for (int r = 0; r < D; ++r) {
@@ -2202,7 +2236,7 @@ __global__ __launch_bounds__(kWalkBlock, (img_gauge_waves<D, NS>())) void k_walk
 #pragma unroll
             for (int j = 0; j < D; ++j) {
 #pragma unroll
-                for (int m = 0; m < D; ++m) E[j][m] = j == m ? E0[j * D + m] : cmul(cmul(d[j], E0[j * D + m]), cconj(d[m]));
+                for (int m = 0; m < D; ++m) E[j][m] = gauge_sandwich<D>(d, j, m, E0[j * D + m]);
             }
 #pragma unroll
             for (int i = 0; i < D; ++i) {
