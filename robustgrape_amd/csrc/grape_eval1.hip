@@ -285,12 +285,18 @@ __device__ __forceinline__ void lane_grad(const DevProblem &Pc, const cd *EtL, c
         const double xk = xs[k], xe = xk + Pc.eps;  // the reference's perturbed control
         const cd q = cis_m1(Pc.gauge_a * (xe - xk));
         const cd p1 = ph[k];
-        cd E[NE][D][D], rho[NE][D];
+        cd E[NE][D][D], fwp[NE][kGaugePairs<D>];
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             step_prop<D>(Et[e], gn[e], p1, E[e]);
+#if GRAPE_GAUGE_FD_DN
+            gauge_fd_weights_dn<D>(q, gn[e], fwp[e]);
+#else
+            cd rho[D];
 #pragma unroll
-            for (int j = 0; j < D; ++j) rho[e][j] = gauge_rho(q, gn[e].n[j]);
+            for (int j = 0; j < D; ++j) rho[j] = gauge_rho(q, gn[e].n[j]);
+            gauge_fd_weights<D>(rho, fwp[e]);
+#endif
         }
 #pragma unroll
         for (int w = 0; w < NSEC; ++w) {  // Y = X E^dag, row by row
@@ -316,8 +322,7 @@ __device__ __forceinline__ void lane_grad(const DevProblem &Pc, const cd *EtL, c
         for (int w = 0; w < NSEC; ++w) s[w] = 0.0;
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
-            cd fw[kGaugePairs<D>];
-            gauge_fd_weights<D>(rho[e], fw);
+            const auto &fw = fwp[e];
 #pragma unroll
             for (int r = 0; r < D; ++r) {
 #pragma unroll
