@@ -1571,24 +1571,36 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fw
 // lane where k_scan_pair spends a wave per sub-evaluation on a Hillis-Steele scan, and every read and
 // carry write coalesced (lane-minor [c][element][evaluation]); U row-major per sub-evaluation, as
 // the sector head reads it.  (The association of the chain differs from k_scan's: rounding only.)
-template <int D, int NE>
-__device__ __forceinline__ void scan_seq_chain(const cd *T, cd *Carry, int nch, size_t nbe, size_t be, cd (&P)[D][D]) {
+// Round 5: both classes' chains advance in one loop over the chunks (class B has class A's chunk
+// count on merged passes), each with its next chunk total in flight while the current product runs,
+// in one-wave workgroups (32 768 evaluations: 2 waves on every CU): 0.064 -> 0.057 ms per C2 pass.
+// The pass moves ~26 tiles per (evaluation, chunk) through HBM, so the scan runs near the HBM rate;
+// three column lanes per evaluation (more waves, same bytes) measured 0.059 ms.
+template <int D>
+struct SeqChain {
+    const cd *T;
+    cd *Carry;
+    cd P[D][D], tn[D][D];
+    __device__ __forceinline__ void init(const cd *T_, cd *Carry_, size_t nbe, size_t be) {
+        T = T_ + be;
+        Carry = Carry_ + be;
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) P[j][i] = cmake(i == j ? 1.0 : 0.0, 0.0);
+        for (int e = 0; e < D * D; ++e) {
+            P[e / D][e % D] = cmake(e / D == e % D ? 1.0 : 0.0, 0.0);
+            tn[e / D][e % D] = T[(size_t)e * nbe];
+        }
     }
-#pragma unroll 1
-    for (int c = 0; c < nch; ++c) {
-        cd *dc = Carry + (size_t)c * D * D * nbe + be;
-        const cd *tc = T + (size_t)c * D * D * nbe + be;
+    __device__ __forceinline__ void step(int c, int nch, size_t nbe) {
+        cd *dc = Carry + (size_t)c * D * D * nbe;
+        const cd *tc = T + (size_t)min(c + 1, nch - 1) * D * D * nbe;
         cd t[D][D];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 dc[(size_t)(j * D + i) * nbe] = P[j][i];
-                t[j][i] = tc[(size_t)(j * D + i) * nbe];
+                t[j][i] = tn[j][i];
+                tn[j][i] = tc[(size_t)(j * D + i) * nbe];
             }
         }
 #pragma unroll
@@ -1605,33 +1617,42 @@ __device__ __forceinline__ void scan_seq_chain(const cd *T, cd *Carry, int nch, 
             }
         }
     }
-}
+};
+constexpr int kSeqBlock = 64;
 template <int DA, bool TWB>
-__global__ __launch_bounds__(256) void k_scan_seq(DevProblem PA, DevBatch BA, DevProblem PB, DevBatch BB, int nb) {
+__global__ __launch_bounds__(kSeqBlock) void k_scan_seq(DevProblem PA, DevBatch BA, DevProblem PB, DevBatch BB, int nb) {
     constexpr int NEB = TWB ? 1 : 2;
-    const size_t be = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t be = (size_t)blockIdx.x * kSeqBlock + threadIdx.x;
     if (be >= (size_t)nb) return;
     const size_t nbe = (size_t)nb;
-    cd U[DA][DA];
-    scan_seq_chain<DA, 1>(BA.Tc, BA.Carry, PA.nchunks, nbe, be, U);
+    const int nch = PA.nchunks;  // (== PB.nchunks: the engine gives class B class A's chunking)
+    SeqChain<DA> ca;
+    SeqChain<2> cb[NEB];
+    ca.init(BA.Tc, BA.Carry, nbe, be);
+#pragma unroll
+    for (int w = 0; w < NEB; ++w)
+        cb[w].init(BB.Tc + (size_t)w * PB.nchunks * 4 * nbe, BB.Carry + (size_t)w * PB.nchunks * 4 * nbe, nbe, be);
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+        ca.step(c, nch, nbe);
+#pragma unroll
+        for (int w = 0; w < NEB; ++w) cb[w].step(c, nch, nbe);
+    }
     cd *ua = BA.Ub + be * DA * DA;
 #pragma unroll
     for (int j = 0; j < DA; ++j) {
 #pragma unroll
-        for (int i = 0; i < DA; ++i) ua[j * DA + i] = U[j][i];
+        for (int i = 0; i < DA; ++i) ua[j * DA + i] = ca.P[j][i];
     }
 #pragma unroll
     for (int w = 0; w < NEB; ++w) {
-        cd V[2][2];
-        scan_seq_chain<2, 1>(BB.Tc + (size_t)w * PB.nchunks * 4 * nbe, BB.Carry + (size_t)w * PB.nchunks * 4 * nbe,
-                             PB.nchunks, nbe, be, V);
 #pragma unroll
         for (int ws = 0; ws < (TWB ? 2 : 1); ++ws) {  // (twins: both sectors' U)
             cd *ub = BB.Ub + (be * 2 + w + ws) * 4;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i) ub[j * 2 + i] = V[j][i];
+                for (int i = 0; i < 2; ++i) ub[j * 2 + i] = cb[w].P[j][i];
             }
         }
     }

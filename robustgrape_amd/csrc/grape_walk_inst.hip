@@ -154,7 +154,7 @@ hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::De
         if (stage == 0) {
             hipLaunchKernelGGL((grape::k_walk_fwd_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB);
         } else if (stage == 2) {  // the chunk-total scan (one lane per evaluation)
-            hipLaunchKernelGGL((grape::k_scan_seq<DA, TW>), dim3((unsigned)((BA.nb + 255) / 256)), dim3(256), 0, st, PA,
+            hipLaunchKernelGGL((grape::k_scan_seq<DA, TW>), dim3((unsigned)((BA.nb + grape::kSeqBlock - 1) / grape::kSeqBlock)), dim3(grape::kSeqBlock), 0, st, PA,
                                BA, PB, BB, BA.nb);
         } else {
             hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
