@@ -1770,6 +1770,9 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
     }
     return (kWalkPresum && NSEC > 1) ? tot : one;
 }
+#ifndef GRAPE_WALK_TWIN_SUM  // merged gradient walk, twin class B: one summed state for both sectors
+#define GRAPE_WALK_TWIN_SUM 1
+#endif
 #ifndef GRAPE_WALK_MERGED_FDX  // the merged gradient walk writes F_dx itself (1) or a part for k_sec_reduce (0)
 #define GRAPE_WALK_MERGED_FDX 1
 #endif
@@ -1785,7 +1788,11 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
     const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
     const int xs = kWalkXRow ? 1 : L.nbe;
     if constexpr (GRAPE_WALK_MERGED_FDX) frow[threadIdx.x] = make_int2(L.ok ? L.be : -1, L.c * PA.L);
-    cd XA[1][DA][DA], XB[2][2][2];
+    // Twin class B (one propagator for both sectors): X_w <- E X_w E^dag is linear and the lane sums
+    // the sectors' terms, so ONE state X = Carry (M_00 + M_11) Carry^dag carries both (GRAPE_WALK_TWIN_SUM:
+    // half of class B's products; the sectors' sum formed once instead of per step -- rounding only)
+    constexpr int NXB = (TWB && GRAPE_WALK_TWIN_SUM) ? 1 : 2;
+    cd XA[1][DA][DA], XB[NXB][2][2];
     {  // carries lane-minor (k_scan_seq), the head's M blocks row-major per sub-evaluation
         const size_t nbe = (size_t)L.nbe, be = (size_t)L.be;
         cd Cr[DA * DA];
@@ -1794,12 +1801,16 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
         for (int e = 0; e < DA * DA; ++e) Cr[e] = ca[(size_t)e * nbe];
         merged_xinit<DA>(Cr, BA.Msec + be * DA * DA, XA[0]);
 #pragma unroll
-        for (int w = 0; w < 2; ++w) {
-            cd Cb[4];
+        for (int w = 0; w < NXB; ++w) {
+            cd Cb[4], Mb[4];
             const cd *cb = BB.Carry + ((size_t)(TWB ? 0 : w) * PB.nchunks + L.c) * 4 * nbe + be;
+            const cd *mb = BB.Msec + (be * 2 + w) * 4;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Cb[e] = cb[(size_t)e * nbe];
-            merged_xinit<2>(Cb, BB.Msec + (be * 2 + w) * 4, XB[w]);
+            for (int e = 0; e < 4; ++e) {
+                Cb[e] = cb[(size_t)e * nbe];
+                Mb[e] = NXB == 1 ? cadd(mb[e], mb[4 + e]) : mb[e];
+            }
+            merged_xinit<2>(Cb, Mb, XB[w]);
         }
     }
     const cd *EtA = gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
@@ -1821,7 +1832,7 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
         sincos(PA.gauge_a * xk, &sn, &cn);
         const cd p1 = cmake(cn, sn), q = cis_m1(PA.gauge_a * (xe - xk));  // (xe - xk: exact)
         const double sa = merged_step_grad<DA, 1, 1>(EtA, gA, p1, q, PA.inv_eps, XA);
-        const double sb = merged_step_grad<2, NEB, 2>(EtB, gB, p1, q, PB.inv_eps, XB);
+        const double sb = merged_step_grad<2, NEB, NXB>(EtB, gB, p1, q, PB.inv_eps, XB);
         double v = 0.0;  // k_sec_reduce's sum of the classes' parts, in the plan's class order
         v += a_first ? sa : sb;
         v += a_first ? sb : sa;
