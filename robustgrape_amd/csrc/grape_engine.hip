@@ -78,6 +78,34 @@ constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
 #ifndef GRAPE_GAUGE_CHUNK_DIV2  // ... for the 2-level classes (A/B knob)
 #define GRAPE_GAUGE_CHUNK_DIV2 GRAPE_GAUGE_CHUNK_DIV
 #endif
+// Chunk count of the 3-level phase-covariant class on throughput passes (the merged walks' chunking,
+// grape_walk.hpp k_walk_fwd_m / k_walk_grad_m).  A walk's time is (rounds of resident waves) x (steps
+// per lane): every lane of a pass walks L steps, so a chunk count that leaves the last round of waves
+// partly empty wastes that round's SIMD time -- C2's 10 chunks at 32 768 evaluations per pass were
+// 5 120 gradient waves, 2.5 rounds at 2 waves per SIMD.  The model, in microseconds per C2 unit from
+// the round-5 profile (profiles/r05/final_c2b): 2.72 x rounds(grad, 2 waves/SIMD) x L + 5.7 x chunks
+// (k_scan_seq), minimised over [nc/2, 2 nc]; the forward walk measured the same at 8, 10, 12 and 16
+// chunks (0.185-0.187 ms per pass), so it has no term.  C2: 8 chunks, 48.5-48.9 -> 50.7 M evals/s
+// (12: 49.7 M, 16: 48.9 M; profiles/r05/ab_nchunks).  GRAPE_GAUGE_NCHUNKS=n (environment) forces n.
+static int merged_chunk_count(long MB, int Nt, int nc, int ncu) {
+    if (const char *e = getenv("GRAPE_GAUGE_NCHUNKS")) {
+        const int n = atoi(e);
+        if (n > 0) return std::min(n, Nt);
+    }
+    const double simds = 4.0 * ncu;
+    double best = 1e300;
+    int pick = nc;
+    for (int n = std::max(1, nc / 2); n <= std::min(2 * nc, Nt); ++n) {
+        const int L = (Nt + n - 1) / n, nch = (Nt + L - 1) / L;
+        const double waves = std::ceil((double)MB * nch / 64.0);
+        const double cost = 2.72 * std::ceil(waves / (2.0 * simds)) * L + 5.7 * nch;
+        if (cost < best - 1e-9) {
+            best = cost;
+            pick = nch;
+        }
+    }
+    return pick;
+}
 // Pair kernels (both sector classes of a stage in one launch) for calls of at most this many evaluations
 // (fewer sub-evaluations than CUs: latency-bound; grape_walk_api.hpp launch_pair)
 constexpr int kPairMaxBatch = 64;
@@ -1427,7 +1455,9 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             // phase-covariant throughput classes: a step costs a few products instead of an
             // exponential, so longer chunks (fewer per-lane prologues and a shorter scan) can pay
             const int cdiv = (Ps.gauge && Ps.scan_waves == kScanTiny) ? (S == 2 ? GRAPE_GAUGE_CHUNK_DIV2 : GRAPE_GAUGE_CHUNK_DIV) : 1;
-            const int ncs = std::max(1, std::min(Ps.scan_waves * (64 / S) / cdiv, P.Nt));
+            int ncs = std::max(1, std::min(Ps.scan_waves * (64 / S) / cdiv, P.Nt));
+            if (Ps.gauge && Ps.scan_waves == kScanTiny && S == 3 && P.ne == 0)
+                ncs = merged_chunk_count((long)MB, P.Nt, ncs, ncu);
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
             grape_plan::SecBuf &b = p->sb[cl];
