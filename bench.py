@@ -105,7 +105,8 @@ def pmc_traffic(kernel, batch, path=PMC_SUMMARY, dims=None):
         except (IndexError, ValueError):
             return None
     rows = [row["hbm_bytes_per_launch"] for name, row in js.get("kernels", {}).items()
-            if name.split("<")[0].split("::")[-1] in (kernel, kernel + "_lane", kernel + "_chain_lane")  # lane variants
+            if name.split("<")[0].split("::")[-1] in (kernel, kernel + "_lane", kernel + "_chain_lane",  # lane variants
+                                                       kernel + "_m")  # merged walks (both sector classes)
             and "hbm_bytes_per_launch" in row
             and (dims is None or dim(name) in dims)]
     return sum(rows) if rows else None
@@ -132,7 +133,7 @@ def pmc_executed_flop(kernel, batch, dims, path=PMC_MIX):
             dim = int(name.split("<")[1].split(",")[0].split(">")[0])
         except (IndexError, ValueError):
             dim = None
-        if base == kernel and dim in dims and "fp64_flop_per_dispatch" in row:
+        if base in (kernel, kernel + "_m") and dim in dims and "fp64_flop_per_dispatch" in row:
             tot += row["fp64_flop_per_dispatch"]
     return tot or None
 
@@ -155,7 +156,7 @@ def pmc_pipeline(batch, per_pass_kernel, dims, path=PMC_SUMMARY):
         except (IndexError, ValueError):
             return None
     ref = [r.get("dispatches") for n, r in ks.items()
-           if n.split("<")[0].split("::")[-1] == per_pass_kernel and dim(n) in dims]
+           if n.split("<")[0].split("::")[-1] in (per_pass_kernel, per_pass_kernel + "_m") and dim(n) in dims]
     if not ref or not ref[0]:
         return None
     total = 0.0
@@ -427,8 +428,8 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                                  "flop_per_launch": ex,
                                  "note": "64 x (2 FMA + MUL + ADD) F64 VALU instructions per dispatch "
                                          "(profiles/pmc_mix_latest.json, scripts/pmc_mix.py) over this run's "
-                                         "kernel time; the walks' Taylor polynomials issue more FLOP than "
-                                         "SURVEY 8d's Pade-5 credit"}
+                                         "kernel time (the phase-covariant walks execute a few products per "
+                                         "step where SURVEY 8d's credit counts a Pade-5 exponential)"}
     pipe = pmc_pipeline(L, grad_name, dims)
     if pipe is not None:
         total_ms = sum(per_pass.values())
