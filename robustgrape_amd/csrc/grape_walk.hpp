@@ -1497,6 +1497,10 @@ __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&
         }
     }
 }
+#ifndef GRAPE_WALK_FWD_M_UNROLL  // the merged forward walk's main loop unrolled (loop-carried register moves)
+#define GRAPE_WALK_FWD_M_UNROLL 2  // (2: no loop-carried register moves, 2 waves/SIMD: fwd 0.183 -> 0.179 ms per C2 pass)
+#endif
+constexpr int kFwdMUnroll = GRAPE_WALK_FWD_M_UNROLL;
 template <int DA, bool TWB>
 __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fwd_m(DevProblem PA, DevBatch BA,
                                                                                   DevProblem PB, DevBatch BB) {
@@ -1541,7 +1545,7 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fw
     // steps past N_t leave Q alone: only the last chunk has them, so the first n_last steps of every
     // chunk run unpredicated and the rest only in the other chunks' lanes (a branch, not selects)
     const int nlast = PA.Nt - (PA.nchunks - 1) * PA.L;
-#pragma unroll 1
+#pragma unroll kFwdMUnroll
     for (int jj = 0; jj < nlast; ++jj) step(jj);
 #pragma unroll 1
     for (int jj = nlast; jj < PA.L; ++jj) {
