@@ -1826,10 +1826,8 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
     for (int w = 0; w < NEB; ++w) gB[w] = gauge_charges<2>(PB, w);
     const int k0 = L.c * PA.L;
     X2 xn = walk_load_x(1, xt + (size_t)min(k0, PA.Nt - 1) * xs, xs);
-#pragma unroll 1
-    for (int jj = 0; jj < PA.L; ++jj) {  // uniform trip count; steps past N_t store nothing
+    auto step = [&](int jj) {  // one step of both classes: the F_dx value, in the plan's class order
         const int k = min(k0 + jj, PA.Nt - 1);
-        const bool act = L.ok && k0 + jj < PA.Nt;
         const double xk = xn.v0, xe = xk + PA.eps;  // the reference's perturbed control
         xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs);  // next step's control
         double sn, cn;
@@ -1840,24 +1838,33 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
         double v = 0.0;  // k_sec_reduce's sum of the classes' parts, in the plan's class order
         v += a_first ? sa : sb;
         v += a_first ? sb : sa;
-        if constexpr (GRAPE_WALK_MERGED_FDX) {
-            // F_dx straight to its [evaluation][n_x] row through a workgroup tile of kFdxTile steps:
-            // the lanes of a workgroup hold consecutive evaluations, so a flush writes 16 lanes'
-            // kFdxTile-long row pieces per instruction (no part array, no k_sec_reduce)
-            const int jt = jj % kFdxTile;
-            ftile[threadIdx.x][jt] = v;
-            if (jt == kFdxTile - 1 || jj == PA.L - 1) {
-                __syncthreads();
-                const int j0 = jj - jt, nj = jt + 1;
-                const int j = threadIdx.x % kFdxTile;
+        return v;
+    };
+    if constexpr (GRAPE_WALK_MERGED_FDX) {
+        // F_dx straight to its [evaluation][n_x] row through a workgroup tile of kFdxTile steps: the
+        // lanes of a workgroup hold consecutive evaluations, so a flush writes 16 lanes' kFdxTile-long
+        // row pieces per instruction (no part array, no k_sec_reduce).  Uniform trip counts: every
+        // lane reaches the barriers; steps past N_t are walked and not stored.
 #pragma unroll 1
-                for (int row = threadIdx.x / kFdxTile; row < kWalkBlock; row += kWalkBlock / kFdxTile) {
-                    const int br = frow[row].x, kk = frow[row].y + j0 + j;  // (br < 0: past the last lane)
-                    if (j < nj && br >= 0 && kk < PA.Nt) BA.Fdx[(size_t)br * PA.nx + kk] = ftile[row][j];
-                }
-                __syncthreads();
+        for (int j0 = 0; j0 < PA.L; j0 += kFdxTile) {
+            const int nj = min(kFdxTile, PA.L - j0);
+#pragma unroll 1  // (unrolled by 2: the same instructions per step)
+            for (int t = 0; t < nj; ++t) ftile[threadIdx.x][t] = step(j0 + t);
+            __syncthreads();
+            const int j = threadIdx.x % kFdxTile;
+#pragma unroll 1
+            for (int row = threadIdx.x / kFdxTile; row < kWalkBlock; row += kWalkBlock / kFdxTile) {
+                const int br = frow[row].x, kk = frow[row].y + j0 + j;  // (br < 0: past the last lane)
+                if (j < nj && br >= 0 && kk < PA.Nt) BA.Fdx[(size_t)br * PA.nx + kk] = ftile[row][j];
             }
-        } else {
+            __syncthreads();
+        }
+    } else {
+#pragma unroll 1
+        for (int jj = 0; jj < PA.L; ++jj) {
+            const int k = min(k0 + jj, PA.Nt - 1);
+            const bool act = L.ok && k0 + jj < PA.Nt;
+            const double v = step(jj);
             double *dst = act ? BA.sec_part + (size_t)k * L.nbe + L.be : reinterpret_cast<double *>(BA.sink);
             *dst = v;
         }
