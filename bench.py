@@ -57,6 +57,29 @@ def problem_c3():
     return FidelityRobustGRAPEProblem(up, np.diag([1.0] * 4 + [0.0] * 5), R.cz_full_target())
 
 
+T0_AR, NT_AR = 14.32, 200  # examples/ar_cz.jl:14-15
+
+
+def problem_arcz():
+    """examples/ar_cz.jl:17-36: the d = 5 symmetric blockaded CZ (RydbergTools.jl:31-39) with one
+    amplitude error source, N_t = 200, t0 = 14.32 -- the reference's robust-optimisation call pattern
+    (optimize_fidelity_and_error_sources evaluates one x per call, FidelityCalculations.jl:174-207)."""
+    from robustgrape_amd import rydberg as R
+    from robustgrape_amd.types import ErrorSource, FidelityRobustGRAPEProblem, UnitaryRobustGRAPEProblem
+    up = UnitaryRobustGRAPEProblem(t0=T0_AR, ntimes=NT_AR, ndim=5, H0=R.rydberg_symmetric_blockaded_operator_basis(),
+                                   nb_additional_param=1, error_sources=[ErrorSource(R.symmetric_amplitude_error())])
+    return FidelityRobustGRAPEProblem(up, np.diag([1.0, 2.0, 1.0, 0.0, 0.0]), R.cz_symmetric_target())
+
+
+def arcz_inputs(first, count):
+    """x_initial of examples/ar_cz.jl:40: [2pi 0.001 U(N_t); 2pi U] (numpy seeds 43 + r)."""
+    xs = []
+    for r in range(first, first + count):
+        rng = np.random.default_rng(43 + r)
+        xs.append(np.concatenate([2 * math.pi * 0.001 * rng.uniform(size=NT_AR), [2 * math.pi * rng.uniform()]]))
+    return np.stack(xs)
+
+
 def restart_inputs(first, count):
     xs = []
     for r in range(first, first + count):
@@ -778,6 +801,37 @@ def c4opt(args):
     print(json.dumps(out), flush=True)
 
 
+def arcz(args):
+    """The ar_cz-shaped latency leg (examples/ar_cz.jl): one x per call through the host-array entry,
+    as optimize_fidelity_and_error_sources calls the reference (FidelityCalculations.jl:174-207):
+    F, F_dx, F_d2err, F_d2err_dx of the d = 5 problem with one amplitude error, N_t = 200.  Beside
+    it the 1-core C++ port on the same input."""
+    fp = problem_arcz()
+    x = arcz_inputs(0, 1)[0]
+    out = {"metric": "GRAPE single-evaluation latency (fidelity+sensitivity+gradients), ar_cz d=5 N_t=200, 1 error source",
+           "unit": "gradient-evals/s", "n_gpus": 1, "higher_is_better": True, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": "examples/ar_cz.jl: symmetric blockaded d=5, t0=14.32, N_t=200, np=1, na=1, "
+                                  "ne=1 (amplitude error); nbatch=1 per call"}}
+    se = single_eval(fp, 1, x, seconds=3.0)
+    out.update({"value": se["value"], "single_eval": se})
+    if not args.no_cpu_baseline:
+        try:
+            from oracle.cref import cref
+            if cref.available():
+                t, n = time.perf_counter(), 0
+                while time.perf_counter() - t < min(args.cpu_seconds, 5.0):
+                    cref.fidelity_grad(fp, x)
+                    n += 1
+                dt = time.perf_counter() - t
+                out["cpu_baseline"] = {"value": n / dt, "unit": "gradient-evals/s", "cores": 1, "kind": "port",
+                                       "sample": f"{n} sequential ar_cz evaluations by oracle/cref, 1 thread",
+                                       "host_cpu": _host_cpu()}
+                out["vs_cpu"] = se["value"] / (n / dt)
+        except Exception as exc:  # the baseline is a report, not the measurement
+            out["cpu_baseline_error"] = repr(exc)
+    print(json.dumps(out), flush=True)
+
+
 def c2_closure(args):
     """SURVEY.md 8b closure fallback on C2: the same physics as plain Python closures (the
     reference's idiom, src/Types.jl:10,50 -- tests/problems.full9_problem(device=False)), so
@@ -958,12 +1012,13 @@ def main():
     ap.add_argument("--chunk", type=int, default=None,
                     help="evaluations per device pass (the plan's workspace; larger steps are chunked "
                          "by the C side); default 32768 (c2), 8192 (c3), 16 (c5)")
-    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c5err", "c4opt", "c2-closure"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c5", "c5err", "c4opt", "c2-closure", "arcz"), default="c2",
                     help="c2: the BASELINE metric (d=9 Rydberg CZ); c3: C2 + 4 error sources "
                          "(sensitivities and their gradients); c5: synthetic d=64, N_t=1024 "
                          "(dense MFMA engine, SURVEY.md 8d C5); c4opt: the C4 restart sweep as "
                          "batched L-BFGS (one step = one iteration of every restart); c2-closure: C2 as "
-                         "plain Python closures through the host-table fallback")
+                         "plain Python closures through the host-table fallback; arcz: examples/ar_cz.jl's d=5 "
+                         "problem with one amplitude error, single-evaluation latency")
     ap.add_argument("--scan-waves", type=int, default=None, choices=(0, 1, 4, 8, 16),
                     help="c4opt: the plan's scan width (chunking); 0 = by batch size, default: RobustCost's choice")
     ap.add_argument("--plan-options", type=int, default=0,
@@ -997,7 +1052,7 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.workload in ("c4opt", "c2-closure"):
+    if world > 1 and args.workload in ("c4opt", "c2-closure", "arcz"):
         print(f"bench.py: --workload {args.workload} is a single-GPU leg", file=sys.stderr)
         sys.exit(2)
 
@@ -1022,6 +1077,8 @@ def main():
         return c4opt(args)
     if args.workload == "c2-closure":
         return c2_closure(args)
+    if args.workload == "arcz":
+        return arcz(args)
     if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -1111,6 +1168,10 @@ def main():
         if best is not None:
             out["sweep"] = {"best_F": best[0], "restart": best[1], "owner_rank": best[2]}
         out["config"]["evals_per_device_pass"] = min(count, chunk)
+        from robustgrape_amd import _capi
+        out["build_id"] = _capi.build_id()  # the library the timed region ran (robustgrape_amd/build.py)
+        if _capi.build_defines():
+            out["build_defines"] = list(_capi.build_defines())
     plan.close()
 
     if not (c3 or c5) and not args.no_c4_strong:
