@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GRAPE_ABI_VERSION 10
+#define GRAPE_ABI_VERSION 11
 
 typedef enum grape_status {
     GRAPE_OK = 0,
@@ -217,6 +217,12 @@ int grape_abi_version(void);
  * next to it. */
 const char *grape_build_id(void);
 const char *grape_last_error(void);
+/* ABI 11: opt-in SIGSEGV / SIGBUS handler that prints libgrape's native frames when the fault lies in
+ * the library's own host code and then hands the signal to the handler it displaced (every other
+ * fault goes there directly).  Nothing is installed at load time; the Python binding calls this
+ * (unless GRAPE_NO_SIGNAL_HANDLER=1); a Julia host should not (Julia uses SIGSEGV itself).
+ * Returns 1 when installed (or already installed), 0 when the library's text range is unknown. */
+int grape_install_fault_handler(void);
 
 /* Number of visible HIP devices (0 when none); does not create a context. */
 int grape_device_count(void);

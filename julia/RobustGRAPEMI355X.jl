@@ -35,7 +35,7 @@ export OperatorTerm, OperatorBasis, grape_expm_batch, plan_sectors, rydberg_full
        optimize_fidelity_and_error_sources
 
 const libgrape = normpath(joinpath(@__DIR__, "..", "robustgrape_amd", "libgrape.so"))
-const GRAPE_ABI_VERSION = 10  # include/grape.h
+const GRAPE_ABI_VERSION = 11  # include/grape.h
 
 function __init__()
     v = ccall((:grape_abi_version, libgrape), Cint, ())

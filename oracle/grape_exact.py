@@ -31,6 +31,9 @@ import math
 import numpy as np
 
 LD = np.clongdouble
+# the whole point is a wider mantissa than double's 52 bits: on a platform whose longdouble is double
+# the "exact" tiers would silently compare double with double
+assert np.finfo(np.longdouble).nmant >= 63, "grape_exact needs an x87 80-bit (or wider) np.longdouble"
 
 
 def squarings(norm1):
@@ -81,9 +84,39 @@ def _target_ld(target, xa):
     return _h0_ld(target, 1, np.zeros(0), xa)
 
 
+def _reads_xadd(H, na, err=False):
+    """True when the Hamiltonian (an operator basis: a term with var == 2; a closure: a probe at two
+    x_add values) depends on x_add -- outside this evaluator's scope (it takes U_dx_add = 0)."""
+    if na == 0:
+        return False
+    terms = getattr(H, "terms", None)
+    if terms is not None:
+        return any(t.var == 2 for t in terms)
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-1.0, 1.0, size=8)
+    xa = rng.uniform(-1.0, 1.0, size=na)
+    args = (lambda a: (1, x.copy(), a.copy(), 0.01)) if err else (lambda a: (1, x.copy(), a.copy()))
+    try:
+        h0 = np.asarray(H(*args(xa)))
+        h1 = np.asarray(H(*args(xa + 0.37)))
+    except (IndexError, TypeError, ValueError):
+        return False  # a closure that cannot be probed this way: left to the caller
+    return not np.array_equal(h0, h1)
+
+
+def _check_scope(up):
+    na = up.nb_additional_param
+    if _reads_xadd(up.H0, na):
+        raise ValueError("grape_exact covers H0 independent of x_add (it takes U_dx_add = 0)")
+    for src in up.error_sources:
+        if _reads_xadd(src.Herror, na, err=True):
+            raise ValueError("grape_exact covers Herror independent of x_add (it takes U_derr_dx_add = 0)")
+
+
 def fidelity_and_gradient(fp, x, nparam=1):
     """(F, F_dx_tot) of calculate_fidelity_and_derivatives(fp, x), evaluated in longdouble."""
     up = fp.unitary_problem
+    _check_scope(up)
     if len(up.error_sources):
         raise ValueError("grape_exact covers problems without error sources")
     nt, d, na = up.ntimes, up.ndim, up.nb_additional_param
@@ -151,6 +184,7 @@ def fidelity_and_derivatives(fp, x, nparam=1):
     Scope: H0 and Herror free of x_add (then U_dx_add and U_derr_dx_add are exactly zero in the
     reference too; the target's difference remains in F_dx_add and F_d2err_dx_add)."""
     up = fp.unitary_problem
+    _check_scope(up)
     nt, d, na, ne = up.ntimes, up.ndim, up.nb_additional_param, len(up.error_sources)
     eps, eps2 = up.eps, up.eps2
     dt = up.t0 / nt

@@ -17,7 +17,7 @@ STATUS_NAMES = {-1: "GRAPE_ERR_INVALID", -2: "GRAPE_ERR_UNSUPPORTED", -3: "GRAPE
                 -4: "GRAPE_ERR_HIP", -5: "GRAPE_ERR_SINGULAR", -6: "GRAPE_ERR_NO_DEVICE"}
 
 # every symbol include/grape.h declares
-EXPORTED = ["grape_abi_version", "grape_build_id", "grape_last_error", "grape_device_count", "grape_plan_create",
+EXPORTED = ["grape_abi_version", "grape_build_id", "grape_last_error", "grape_install_fault_handler", "grape_device_count", "grape_plan_create",
             "grape_plan_destroy", "grape_plan_stream", "grape_plan_set_stream", "grape_fidelity_grad",
             "grape_fidelity_grad_device_async", "grape_plan_synchronize", "grape_unitary_derivs",
             "grape_expm_batch", "grape_plan_set_profiling", "grape_plan_kernel_times",
@@ -31,7 +31,7 @@ EXPORTED = ["grape_abi_version", "grape_build_id", "grape_last_error", "grape_de
 KERNEL_NAMES = ["k_expm", "k_expm_high", "k_scan", "k_grad/k_err_local", "k_reduce_add", "k_err_scan", "k_err_grad",
                 "k_expm_grad", "k_grad_high", "k_dexp", "k_dscan", "k_dcarry", "k_dmc", "k_dgrad",
                 "k_walk_fwd", "k_walk_grad", "k_eval1"]
-ABI_VERSION = 10  # GRAPE_ABI_VERSION in include/grape.h
+ABI_VERSION = 11  # GRAPE_ABI_VERSION in include/grape.h
 
 
 class GrapeError(RuntimeError):
@@ -55,6 +55,7 @@ def lib():
         L.grape_abi_version.restype = ctypes.c_int
         L.grape_build_id.restype = ctypes.c_char_p
         L.grape_last_error.restype = ctypes.c_char_p
+        L.grape_install_fault_handler.restype = ctypes.c_int
         L.grape_device_count.restype = ctypes.c_int
         L.grape_plan_create.argtypes = [ctypes.POINTER(CDesc), ctypes.c_int, ctypes.POINTER(vp)]
         L.grape_plan_create.restype = ctypes.c_int
@@ -123,12 +124,16 @@ def lib():
         L.grape_symmetry_basis.restype = ctypes.c_int
         if L.grape_abi_version() != ABI_VERSION:
             raise ImportError("libgrape.so ABI version mismatch")
-        # provenance: the library must have been built from the csrc/ next to it (content hash)
-        from .build import source_id
-        got, want = L.grape_build_id().decode(), source_id()
+        # provenance: the library must have been built from the csrc/ next to it (content hash of the
+        # sources, flags and -- for an A/B variant loaded through GRAPE_LIB -- its recorded defines)
+        from .build import read_id_file, source_id
+        _, defines = read_id_file(LIB_PATH)
+        got, want = L.grape_build_id().decode(), source_id(defines)
         if got != want:
             raise ImportError(f"{LIB_PATH} was built from other sources (build id {got}, csrc/ hashes to {want}): "
                               "rebuild with `python -m robustgrape_amd.build`")
+        if os.environ.get("GRAPE_NO_SIGNAL_HANDLER", "0") != "1":
+            L.grape_install_fault_handler()  # native frames of a fault inside libgrape (opt-in, ABI 11)
         _lib = L
     return _lib
 
@@ -136,6 +141,12 @@ def lib():
 def build_id() -> str:
     """Source hash the loaded library was built from (robustgrape_amd/build.py source_id)."""
     return lib().grape_build_id().decode()
+
+
+def build_defines():
+    """The -D defines of the loaded library's variant (empty for the in-tree default build)."""
+    from .build import read_id_file
+    return read_id_file(LIB_PATH)[1]
 
 
 def check(code):

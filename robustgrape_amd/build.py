@@ -43,28 +43,45 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
          "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 
-def source_id() -> str:
-    """Content hash of every source the library is built from (DEPS) and the compiler flags: the
-    library embeds it (grape_build_id()) and _capi.lib() refuses a library whose id differs from
-    the sources next to it, so a test or bench run names the sources it ran."""
+def source_id(defines=()) -> str:
+    """Content hash of every source the library is built from (DEPS), the compiler flags (the common
+    ones and every unit's own) and the variant's -D defines: the library embeds it (grape_build_id())
+    and _capi.lib() refuses a library whose id differs from the sources next to it, so a test or bench
+    run names the sources -- and the A/B variant (scripts/build_variants.py) -- it ran."""
     h = hashlib.sha256()
     for d in sorted(DEPS):
         h.update(os.path.relpath(d, ROOT).encode() + b"\0")
         with open(d, "rb") as fh:
             h.update(fh.read())
         h.update(b"\0")
-    h.update(" ".join(FLAGS[:5]).encode())
+    h.update(" ".join(f for f in FLAGS if not f.startswith("-I")).encode() + b"\0")
+    for src, extra, _ in _units(())[1]:
+        h.update(os.path.basename(src).encode() + b":" + " ".join(extra).encode() + b"\0")
+    h.update(("defines:" + " ".join(sorted(defines))).encode())
     return h.hexdigest()[:16]
 
 
 ID_FILE = LIB + ".id"  # the id the in-tree library was linked with (read without loading it)
 
 
+def read_id_file(lib_path):
+    """(build id, defines) recorded next to a built library (`<lib>.id`: the id, then the variant's
+    -D defines on the second line), or (None, ()) when there is no record."""
+    try:
+        with open(lib_path + ".id") as fh:
+            lines = fh.read().splitlines()
+    except OSError:
+        return None, ()
+    sid = lines[0].strip() if lines else None
+    defines = tuple(lines[1].split()) if len(lines) > 1 else ()
+    return sid, defines
+
+
 def needs_build() -> bool:
-    if not os.path.exists(LIB) or not os.path.exists(ID_FILE):
+    if not os.path.exists(LIB):
         return True
-    with open(ID_FILE) as fh:
-        return fh.read().strip() != source_id()
+    sid, defines = read_id_file(LIB)
+    return defines != () or sid != source_id()
 
 
 def _units(defines):
@@ -94,7 +111,7 @@ def build_library(force: bool = False, verbose: bool = True, out: str = LIB, def
     if verbose:
         print("[robustgrape_amd] building", os.path.relpath(out, ROOT), *defines,
               f"({len(units)} translation units)", flush=True)
-    sid = source_id()
+    sid = source_id(defines)
     dflags = [f"-D{d}" for d in defines]
     jobs = max(1, min(len(units), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
     pending = list(units)
@@ -116,9 +133,8 @@ def build_library(force: bool = False, verbose: bool = True, out: str = LIB, def
     subprocess.run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + [u[2] for u in units] + ["-o", tmp],
                    check=True)
     os.replace(tmp, out)
-    if out == LIB:
-        with open(ID_FILE, "w") as fh:
-            fh.write(sid + "\n")
+    with open(out + ".id", "w") as fh:
+        fh.write(sid + "\n" + " ".join(defines) + "\n")
     return out
 
 

@@ -15,7 +15,11 @@
 #include <string>
 #include <cstdlib>
 #include <csignal>
+#include <cstdint>
+#include <dlfcn.h>
 #include <execinfo.h>
+#include <link.h>
+#include <ucontext.h>
 #include <unistd.h>
 #include <vector>
 
@@ -636,8 +640,9 @@ static SectorSetup find_sectors(const grape_desc *desc, bool tables) {
 
 // Phase covariance of a sector class (grape_walk.hpp GAUGE): does every sector block obey
 // H_w(x) = D(a x) H_w(0) D(a x)^dag, D(t) = diag(e^{i t N_j}), for the one control x?  Needs np = 1,
-// no error sources, H0 free of x_add and of the step index, and every term that reads x a
-// cos / sin / cis of a x + b with one common a.  The charges come from the ratios of the blocks'
+// H0 and every error source's terms free of x_add and of the step index (error sources are accepted:
+// their terms must be covariant with the same charges, k_walk_img_gauge), and every term that reads x
+// a cos / sin / cis of a x + b with one common a.  The charges come from the ratios of the blocks'
 // entries at a small x to their values at x = 0 (N_j - N_k = n_jk, integer), propagated over each
 // sector's coupling graph; the identity is then checked entry by entry at seven x values (a
 // rotated basis -- the symmetry-adapted sectors -- is covered: the blocks are the rotated ones).
@@ -1026,29 +1031,69 @@ static int create_dense(const grape_desc *desc, grape_plan *p, bool xadd_dep, co
     return GRAPE_OK;
 }
 
-// A fatal signal inside the library names its native frames on stderr before the previous
-// handler (Python's faulthandler, or the default action) runs: the handler prints the
-// backtrace, reinstalls the handler it displaced and returns, so the faulting instruction
-// faults again into that one.  backtrace() is called once at load so that the unwinder is
-// resolved before any signal (it is not async-signal-safe on its first call).
-// GRAPE_NO_SIGNAL_HANDLER=1 leaves the process's handlers alone.
+// A fatal signal raised by code inside the library names its native frames on stderr before the
+// previous handler (Python's faulthandler, or the default action) runs.  Opt-in: the Python binding
+// installs it (grape_install_fault_handler, _capi.lib(); GRAPE_NO_SIGNAL_HANDLER=1 skips that), never
+// a load-time constructor -- a host such as Julia uses SIGSEGV itself (GC safepoints, stack probes),
+// so the library leaves every process's handlers alone unless asked.  A signal whose faulting PC lies
+// outside libgrape's own text goes straight to the displaced handler (called in place, or, for the
+// default action, reinstated so that the instruction faults again into it); only a fault inside the
+// library prints the frames first.  backtrace() is called once at install time so that the unwinder
+// is resolved before any signal (it is not async-signal-safe on its first call).
 namespace {
 struct sigaction g_prev_sig[2];
 const int kFatalSigs[2] = {SIGSEGV, SIGBUS};
+uintptr_t g_text_lo = 0, g_text_hi = 0;  // libgrape's executable segments (host code)
+bool g_handler_installed = false;
 
-void grape_fatal_signal(int sig, siginfo_t *, void *) {
-    static const char head[] = "\n[libgrape] fatal signal; native frames (innermost first):\n";
-    (void)!write(2, head, sizeof head - 1);
-    void *frames[64];
-    const int n = backtrace(frames, 64);
-    backtrace_symbols_fd(frames, n, 2);
-    for (int i = 0; i < 2; ++i)
-        if (kFatalSigs[i] == sig) sigaction(sig, &g_prev_sig[i], nullptr);
+int find_text(struct dl_phdr_info *info, size_t, void *base) {
+    if (info->dlpi_addr != (uintptr_t)base) return 0;
+    for (int i = 0; i < info->dlpi_phnum; ++i) {
+        const ElfW(Phdr) &ph = info->dlpi_phdr[i];
+        if (ph.p_type != PT_LOAD || !(ph.p_flags & PF_X)) continue;
+        const uintptr_t lo = info->dlpi_addr + ph.p_vaddr, hi = lo + ph.p_memsz;
+        if (!g_text_lo || lo < g_text_lo) g_text_lo = lo;
+        if (hi > g_text_hi) g_text_hi = hi;
+    }
+    return 1;
 }
 
-__attribute__((constructor)) void grape_install_signal_handler() {
-    const char *off = std::getenv("GRAPE_NO_SIGNAL_HANDLER");
-    if (off && off[0] == '1') return;
+void chain_previous(int sig, siginfo_t *si, void *uc) {
+    for (int i = 0; i < 2; ++i) {
+        if (kFatalSigs[i] != sig) continue;
+        const struct sigaction &prev = g_prev_sig[i];
+        if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) {
+            prev.sa_sigaction(sig, si, uc);
+        } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN) {
+            prev.sa_handler(sig);
+        } else {
+            sigaction(sig, &prev, nullptr);  // returning re-raises the fault into the default action
+        }
+    }
+}
+
+void grape_fatal_signal(int sig, siginfo_t *si, void *uc) {
+    uintptr_t pc = 0;
+#if defined(__x86_64__)
+    if (uc) pc = (uintptr_t) static_cast<ucontext_t *>(uc)->uc_mcontext.gregs[REG_RIP];
+#endif
+    if (pc >= g_text_lo && pc < g_text_hi) {
+        static const char head[] = "\n[libgrape] fatal signal inside libgrape; native frames (innermost first):\n";
+        (void)!write(2, head, sizeof head - 1);
+        void *frames[64];
+        const int n = backtrace(frames, 64);
+        backtrace_symbols_fd(frames, n, 2);
+    }
+    chain_previous(sig, si, uc);
+}
+}  // namespace
+
+extern "C" int grape_install_fault_handler(void) {
+    if (g_handler_installed) return 1;
+    Dl_info di;
+    if (!dladdr(reinterpret_cast<void *>(&grape_install_fault_handler), &di) || !di.dli_fbase) return 0;
+    dl_iterate_phdr(find_text, di.dli_fbase);
+    if (!g_text_hi) return 0;
     void *warm[2];
     (void)backtrace(warm, 2);
     struct sigaction sa {};
@@ -1056,8 +1101,9 @@ __attribute__((constructor)) void grape_install_signal_handler() {
     sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
     sigemptyset(&sa.sa_mask);
     for (int i = 0; i < 2; ++i) sigaction(kFatalSigs[i], &sa, &g_prev_sig[i]);
+    g_handler_installed = true;
+    return 1;
 }
-}  // namespace
 
 #ifndef GRAPE_BUILD_ID
 #define GRAPE_BUILD_ID "unversioned"
@@ -1437,7 +1483,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                         !(P.opts & GRAPE_OPT_NO_GAUGE) && find_gauge(desc, sdesc, sc, gauge_a, gauge_n)) ? 1 : 0;
             Ps.gauge_a = gauge_a;
             Ps.gauge_n = nullptr;
+            Ps.gauge_ladder = 0;
             if (Ps.gauge) {
+                Ps.gauge_ladder = 1;
+                for (size_t i = 0; i < gauge_n.size(); ++i)
+                    if (gauge_n[i] != (int)(i % (size_t)S)) Ps.gauge_ladder = 0;
                 int *gn = nullptr;
                 if (dalloc(&gn, gauge_n.size()) != hipSuccess) return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (gauge)"));
                 p->sb[cl].gauge_n = gn;

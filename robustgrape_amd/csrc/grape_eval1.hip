@@ -22,6 +22,9 @@
 // Same quantities and the same per-step arithmetic as the chunk walks; the chain products are
 // associated differently (a scan over 256 chunks instead of the pair path's walk + scan
 // geometry), so results agree with the pair path to rounding, not bit for bit.
+#include <bitset>
+#include <mutex>
+
 #include "grape_eval1_api.hpp"
 #include "grape_walk.hpp"
 
@@ -674,12 +677,21 @@ hipError_t prepare(const DevProblem &PA, const DevProblem &PB, cd *EtA, cd *EtB,
 
 template <int DA, bool TW>
 static hipError_t go(const Args &A, int nb, size_t lds, hipStream_t st) {
-    static bool raised = false;  // (one attribute call per instantiation; idempotent)
-    if (!raised) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_eval1<DA, TW>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        raised = true;
+    // 160 KB of dynamic LDS: the attribute is per device, so it is raised once per (instantiation,
+    // device) -- under a lock, as plans may be created and called from several threads
+    static std::mutex mu;
+    static std::bitset<256> raised;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (dev < 0 || dev >= (int)raised.size() || !raised.test((size_t)dev)) {
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_eval1<DA, TW>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            if (dev >= 0 && dev < (int)raised.size()) raised.set((size_t)dev);
+        }
     }
     hipLaunchKernelGGL((k_eval1<DA, TW>), dim3((unsigned)nb), dim3(kBlock), lds, st, A);
     return hipGetLastError();

@@ -103,6 +103,10 @@ struct DevProblem {
     int gauge;
     double gauge_a;
     const int *gauge_n;
+    // (round 6) every sector of the class has the ladder charges N_j = j (the Rydberg sectors in the
+    // engine's level order: {11, S, rr} and {01, 0r}): the merged walks then take the pair phases and
+    // difference weights from compile-time charge differences (grape_walk.hpp kLadder), same values
+    int gauge_ladder;
 };
 
 struct DevBatch {

@@ -138,9 +138,13 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
 }
 
 bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB) {
-    // (class A of 3 levels: at 4 levels the merged gradient lane spills at 2 waves per SIMD)
+    // (class A of 3 levels: at 4 levels the merged gradient lane spills at 2 waves per SIMD).  The merged
+    // gradient walk writes F_dx itself and k_sec_reduce is skipped on merged passes, which is only right
+    // when there are no x_add variants (H0 free of x_add: one gradient parameter per step) -- required
+    // here, not left to pair_ok / gauge detection
     return pair_ok(PA, PB) && PA.D == 3 && PA.gauge && PB.gauge && PA.gauge_a == PB.gauge_a && PA.L == PB.L &&
-           PA.nchunks == PB.nchunks && PA.np == 1 && PA.na <= 1;
+           PA.nchunks == PB.nchunks && PA.np == 1 && PA.na <= 1 && !PA.xadd_dep && !PB.xadd_dep &&
+           PA.nvg == 1 && PB.nvg == 1 && PA.ne == 0 && PB.ne == 0;
 }
 bool merged_writes_fdx() { return GRAPE_WALK_MERGED_FDX != 0; }
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,

@@ -10,6 +10,8 @@
  *                      on the target) and prints F and F_dx; the GPU test compares them with
  *                      the CPU oracle
  */
+#define _POSIX_C_SOURCE 200809L
+#include <signal.h>
 #include <stddef.h>
 #include <stdio.h>
 #include <string.h>
@@ -139,7 +141,21 @@ static int gpu(void) {
     return 0;
 }
 
+/* the fault handler is opt-in (ABI 11): loading the library leaves SIGSEGV / SIGBUS alone */
+static int signals(void) {
+    struct sigaction sa;
+    sigaction(SIGSEGV, NULL, &sa);
+    printf("segv_default_at_load %d\n", sa.sa_handler == SIG_DFL);
+    sigaction(SIGBUS, NULL, &sa);
+    printf("bus_default_at_load %d\n", sa.sa_handler == SIG_DFL);
+    printf("installed %d\n", grape_install_fault_handler());
+    sigaction(SIGSEGV, NULL, &sa);
+    printf("segv_default_after %d\n", sa.sa_handler == SIG_DFL);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu();
+    if (argc > 1 && strcmp(argv[1], "signals") == 0) return signals();
     return layout();
 }

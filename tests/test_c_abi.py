@@ -98,3 +98,11 @@ def test_c_caller_fidelity_grad_matches_oracle():
     assert abs(vals["F"] - F0) <= 1e-12
     g = np.array([vals[f"F_dx {i}"] for i in range(5)])
     assert np.max(np.abs(g - g0)) <= 1e-6 * np.max(np.abs(g0)) + 1e-8
+
+
+def test_fault_handler_is_opt_in():
+    """loading libgrape installs no SIGSEGV / SIGBUS handler (a Julia host uses SIGSEGV
+    itself); grape_install_fault_handler (ABI 11, called by the Python binding) installs it."""
+    out = subprocess.run([_binary(), "signals"], check=True, capture_output=True, text=True).stdout
+    got = {k: int(v) for k, v in (line.split() for line in out.splitlines())}
+    assert got == {"segv_default_at_load": 1, "bus_default_at_load": 1, "installed": 1, "segv_default_after": 0}

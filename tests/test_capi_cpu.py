@@ -244,3 +244,14 @@ def test_plan_option_constants_match_the_header():
     assert len(defs) >= 12
     for name, val in defs.items():
         assert getattr(OPS, "OPT_" + name) == val, name
+
+
+def test_build_id_names_the_variant():
+    """an A/B variant (scripts/build_variants.py, -D defines) has its own build id, and the
+    id recorded next to a library carries the defines it was built with."""
+    from robustgrape_amd import build
+    base = build.source_id()
+    assert build.source_id(("GRAPE_WALK_TWIN_SUM=0",)) != base
+    assert build.source_id(("A=1", "B=2")) == build.source_id(("B=2", "A=1"))
+    sid, defines = build.read_id_file(build.LIB)
+    assert sid == base and defines == ()
