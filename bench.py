@@ -161,6 +161,33 @@ def pmc_executed_flop(kernel, batch, dims, path=PMC_MIX):
     return tot or None
 
 
+def pmc_mix(batch, path=PMC_MIX):
+    """The committed instruction-mix summary (scripts/pmc_mix.py) if it was recorded at this pass size."""
+    try:
+        with open(path) as fh:
+            js = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    return js if js.get("batch") == batch else None
+
+
+def pmc_pass_flop(mix, per_pass_kernel, batch):
+    """Executed FP64 FLOP per evaluation over every kernel of one device pass: sum over kernels of
+    FLOP per dispatch x dispatches per pass (dispatch count over that of `per_pass_kernel`, which runs
+    once per pass), divided by the pass's evaluations; None without dispatch counts."""
+    if not mix:
+        return None
+    ks = mix.get("kernels", {})
+    ref = [r.get("dispatches") for n, r in ks.items() if n.split("<")[0].split("::")[-1] in (per_pass_kernel, per_pass_kernel + "_m")]
+    if not ref or not ref[0]:
+        return None
+    tot = 0.0
+    for n, r in ks.items():
+        if "fp64_flop_per_dispatch" in r and r.get("dispatches"):
+            tot += r["fp64_flop_per_dispatch"] * r["dispatches"] / ref[0]
+    return tot / batch
+
+
 def pmc_pipeline(batch, per_pass_kernel, dims, path=PMC_SUMMARY):
     """PMC HBM bytes of one whole device pass: every kernel's mean bytes per dispatch times its
     dispatches per pass (dispatch count over that of `per_pass_kernel`, which runs once per pass
@@ -383,35 +410,51 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     twins = tuple((info or {}).get("twin", ())) + (False,) * len(classes)
     gauges = tuple((info or {}).get("gauge", ())) + (False,) * len(classes)
     per_step = lambda f: sum(ns * f(S) for S, ns in classes)  # noqa: E731
-    # executed work: a twin class (grape_walk.hpp TWIN) runs ONE exponential per step for its two
-    # sectors (the products and contractions stay per sector)
-    per_step_exp = lambda f: sum((1 if twins[c] else ns) * f(S) for c, (S, ns) in enumerate(classes))  # noqa: E731
-    # the step propagator of a class: an S x S exponential (Pade-5 credit), or for a
-    # phase-covariant class (grape_walk.hpp GAUGE) E_k = D_k E~ D_k^dag formed from the lane's one
-    # exponential: two complex products per off-diagonal entry (12 FLOP each; the lane's own E~ is one
-    # exponential per chunk of L steps and not counted)
-    gform = lambda S: 12 * (S * S - S)  # noqa: E731
-    prop = lambda c, S: gform(S) if gauges[c] else flops_expm(S)  # noqa: E731
-    # the eps-variant's contraction: Re tr(Y dE) (8 S^2), or from the level phases (22 FLOP per
-    # off-diagonal entry: f = rho_r + conj(rho_j) + rho_r conj(rho_j), E f, 2 FMA)
-    contr = lambda c, S: 22 * (S * S - S) if gauges[c] else 8 * S ** 2  # noqa: E731
+    ladders = tuple((info or {}).get("ladder", ())) + (False,) * len(classes)
     walk = ktimes.get("k_walk_grad", (0.0, 0))[1] > 0
+    # both classes walked by one lane (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m): one walk launch per
+    # stage and pass instead of one per class
+    merged = bool(walk and passes and ktimes.get("k_walk_grad", (0.0, 0))[1] == passes)
+    from robustgrape_amd import _capi
+    defines = set(_capi.build_defines())
+    # merged gradient walk, twin class: ONE summed state for both sectors (GRAPE_WALK_TWIN_SUM, on by
+    # default): its products and contraction run once per step, not once per sector
+    twin_sum = merged and "GRAPE_WALK_TWIN_SUM=0" not in defines
+    ladder_contr = merged and "GRAPE_WALK_LADDER_CONTR=0" not in defines
+    nX = lambda c, ns: 1 if (twins[c] and twin_sum) else ns  # noqa: E731  (gradient states of a class)
+    # Executed FP64 FLOP (FMA = 2, MUL / ADD = 1) per step of the phase-covariant walks
+    # (grape_walk.hpp), term by term:
+    #  E_k = D_k E~ D_k^dag: one complex product (6) per off-diagonal entry, plus the pair phases' powers
+    #    p^2 .. p^{S-1} (one product each);
+    #  a product of two S x S complex matrices: 8 S^3 (Y = X E^dag and X <- E Y in the gradient walk,
+    #    Q <- E Q in the forward walk);
+    #  the eps-difference contraction: ladder charges grouped by charge difference (merged walks,
+    #    GRAPE_WALK_LADDER_CONTR): 4 FMA per off-diagonal entry, 2 FMA per charge difference, the
+    #    weights rho(m) (10 each beyond m = 1) and 1/eps; otherwise per entry E_rj f_rj / eps (8) and a
+    #    real MAC pair (4), the weights per level pair;
+    #  per step and lane (shared by the classes of a merged lane): e^{i a x_k} (grape_cis.hpp: ~37) and,
+    #    in the gradient walk, e^{i phi} - 1 of the FD phase (~27).
+    # A non-phase-covariant class is credited SURVEY 8d's Pade-5 exponential instead of E_k's formation.
+    gform = lambda S: 6 * (S * S - S) + 6 * max(0, S - 2)  # noqa: E731
+    prop = lambda c, S: gform(S) if gauges[c] else flops_expm(S)  # noqa: E731
+    contr = lambda c, S: ((8 * (S * S - S) + 4 * (S - 1) + 1 + 10 * max(0, S - 2))  # noqa: E731
+                          if (gauges[c] and ladders[c] and ladder_contr) else
+                          (12 * (S * S - S) + 10 * max(0, S - 2)) if gauges[c] else 8 * S ** 2)
+    trig_f, trig_g = (37, 64) if any(gauges[:len(classes)]) else (0, 0)
+    lanes_per_step = 1 if merged else len(classes)  # the trig runs once per lane and step
     xbytes = L * 8 * (NT + 1)  # the x rows every per-step kernel streams
     if walk:
-        # chunk walks (grape_walk.hpp), algorithmic work per device pass:
-        # k_walk_fwd: one nominal S x S propagator per (step, sector) + the chain product Q <- E Q;
-        # k_walk_grad: one eps-variant propagator per (step, sector), Y = X E^dagger, X <- E Y and the
-        # contraction Re tr(Y dE).  The 2-level classes recompute E in the gradient walk
-        # (executed, not credited); the 4-level class stores E once (walk_store_e) and the
-        # gradient walk reads it back -- the only per-step HBM intermediate left.  Phase-covariant
-        # classes form the nominal propagator in both walks and the eps-variant's difference from
-        # the level phases: no exponential per step (counted as executed)
+        # chunk walks (grape_walk.hpp), executed work per device pass: the forward walk
+        # forms every state's E_k and its chain product; the gradient walk forms E_k again, Y = X E^dag,
+        # the contraction and X <- E Y per gradient state.  The 4-level class of a non-phase-covariant
+        # plan stores E once (walk_store_e) and the gradient walk reads it back -- the only per-step HBM
+        # intermediate left.
         store = lambda S: S >= WALK_STORE_LEVELS and not any(gauges)  # noqa: E731
         nE = lambda c, ns: 1 if twins[c] else ns  # noqa: E731
-        flop_model = {"k_walk_fwd": L * NT * sum(nE(c, ns) * (prop(c, S) + 8 * S ** 3)
-                                                 for c, (S, ns) in enumerate(classes)),
-                      "k_walk_grad": L * NT * nvg * sum(nE(c, ns) * prop(c, S) + ns * (2 * 8 * S ** 3 + contr(c, S))
-                                                        for c, (S, ns) in enumerate(classes))}
+        flop_model = {"k_walk_fwd": L * NT * (sum(nE(c, ns) * (prop(c, S) + 8 * S ** 3)
+                                                  for c, (S, ns) in enumerate(classes)) + lanes_per_step * trig_f),
+                      "k_walk_grad": L * NT * (nvg * sum(nE(c, ns) * prop(c, S) + nX(c, ns) * (2 * 8 * S ** 3 + contr(c, S))
+                                                         for c, (S, ns) in enumerate(classes)) + lanes_per_step * trig_g)}
         byte_model = {"k_walk_fwd": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0),
                       "k_walk_grad": xbytes + L * NT * per_step(lambda S: 16 * S * S if store(S) else 0)}
     else:
@@ -427,9 +470,18 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
     per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
     kname = max(flop_model, key=lambda k: per_pass.get(k, 0.0))
     ms = per_pass[kname]
-    fp = flop_model[kname] / (ms * 1e-3) / 1e12
-    hb = byte_model[kname] / (ms * 1e-3) / 1e9
     dims = {S for S, _ in classes}
+    # FLOP per launch: the FP64 the VALU issued, from the instruction-mix PMC pass recorded on THIS build
+    # at this pass size (profiles/pmc_mix_latest.json, scripts/gpu_pmc_mix.sh: 64 x (2 FMA + MUL + ADD)
+    # F64 instructions per dispatch) when there is one; else the term-by-term model above.  Both are in
+    # the line with their ratio, so the credited work can be checked against the counters.
+    mix = pmc_mix(L)
+    mix_build = (mix or {}).get("build_id")
+    this_build = _capi.build_id()
+    ex = pmc_executed_flop(kname, L, dims) if mix_build == this_build else None
+    flop = ex if ex is not None else flop_model[kname]
+    fp = flop / (ms * 1e-3) / 1e12
+    hb = byte_model[kname] / (ms * 1e-3) / 1e9
     traffic = pmc_traffic(kname, L, dims=dims)
     fp_frac, hb_frac = fp / FP64_PEAK_TFLOPS, hb / HBM_PEAK_GBS
     if hb_frac > fp_frac:
@@ -441,18 +493,16 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                 "pipe": "fp64 (VALU; gfx950 FP64 vector peak == matrix peak)"}
     roof.update({"traffic_unit": "HBM bytes per device pass (PMC)", "per_launch_ms": ms,
                  "per_launch_note": "per device pass of evals_per_device_pass evaluations (all sector classes)",
-                 "flop_per_launch": flop_model[kname], "algorithmic_bytes_per_launch": byte_model[kname],
+                 "flop_per_launch": flop,
+                 "flop_source": ("pmc: FP64 VALU instructions of this build (profiles/pmc_mix_latest.json)"
+                                 if ex is not None else "model (no instruction-mix PMC of this build)"),
+                 "flop_per_launch_model": flop_model[kname],
+                 "model_over_pmc": (flop_model[kname] / ex) if ex else None,
+                 "pmc_mix_build_id": mix_build, "build_id": this_build,
+                 "algorithmic_bytes_per_launch": byte_model[kname],
                  "fp64": {"achieved_TFLOPs": fp, "frac": fp_frac},
                  "hbm": {"achieved_GBs": hb, "frac": hb_frac,
                          "traffic_GBs": (traffic / (ms * 1e-3) / 1e9) if traffic else None}})
-    ex = pmc_executed_flop(kname, L, dims)
-    if ex is not None:  # what the VALU actually issued (PMC), beside the algorithmic credit above
-        roof["fp64_executed"] = {"TFLOPs": ex / (ms * 1e-3) / 1e12, "frac": ex / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                                 "flop_per_launch": ex,
-                                 "note": "64 x (2 FMA + MUL + ADD) F64 VALU instructions per dispatch "
-                                         "(profiles/pmc_mix_latest.json, scripts/pmc_mix.py) over this run's "
-                                         "kernel time (the phase-covariant walks execute a few products per "
-                                         "step where SURVEY 8d's credit counts a Pade-5 exponential)"}
     pipe = pmc_pipeline(L, grad_name, dims)
     if pipe is not None:
         total_ms = sum(per_pass.values())
@@ -476,24 +526,27 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
                    "phase_covariant": [bool(g) for g in gauges[:len(classes)]],
                    # both classes in one lane (grape_walk.hpp k_walk_fwd_m / k_walk_grad_m): one walk
                    # launch per stage and pass instead of one per class
-                   "merged_walks": bool(walk and passes and ktimes.get("k_walk_grad", (0.0, 0))[1] == passes)},
+                   "merged_walks": merged, "twin_sum": twin_sum,
+                   "ladder_charges": [bool(x) for x in ladders[:len(classes)]]},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
         "kernels_ms_per_pass": per_pass,
     }
-    # whole-evaluation view: FLOP of the work executed per evaluation
-    # (nominal + one eps-variant exp per step per sector, chain + contraction products; with
-    # sectors also the head's d x d products), and the survey's canonical whole-matrix C2 figure
-    # (which also counts the x_add-variant exps, zero differences, this engine skips)
-    exe = NT * sum((1 if twins[c] else ns) * ((1 + nvg) * prop(c, S) + 8 * S ** 3)
-                   + ns * (2 * 8 * S ** 3 + nvg * contr(c, S)) for c, (S, ns) in enumerate(classes))
-    if sec:
-        exe += 16 * 8 * D ** 3
+    # whole-evaluation view: FLOP executed per evaluation -- the PMC FP64 count of every
+    # kernel of one device pass of this build (dispatches per pass from the same profile) over the pass's
+    # evaluations when recorded, else the walks' model (the head and scan not modelled) -- and the
+    # survey's canonical whole-matrix C2 figure (not executed, not credited with sectors)
+    exe_model = NT * (sum((1 if twins[c] else ns) * ((1 + nvg) * prop(c, S) + 8 * S ** 3)
+                          + nX(c, ns) * (2 * 8 * S ** 3 + nvg * contr(c, S)) for c, (S, ns) in enumerate(classes))
+                      + lanes_per_step * (trig_f + trig_g)) if walk else None
+    exe_pmc = pmc_pass_flop(mix, kname, L) if mix_build == this_build else None
+    exe = exe_pmc if exe_pmc is not None else exe_model
     canon = NT * (3 * flops_expm(D) + 3 * 8 * D ** 3 + 2 * 8 * D ** 2)
     out["roofline"]["whole_eval"] = {
-        "flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
-        "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
-        "flop_per_eval_survey": canon}
+        "flop_per_eval_executed": exe, "achieved_executed": (exe * value / 1e12) if exe else None,
+        "frac_executed": (exe * value / 1e12 / FP64_PEAK_TFLOPS) if exe else None,
+        "source": "pmc (every kernel of a pass, this build)" if exe_pmc is not None else "model (walks only)",
+        "flop_per_eval_model_walks": exe_model, "flop_per_eval_survey": canon}
     if sec:
         out["roofline"]["whole_eval"]["note"] = (
             "sectors: the executed work is the block-diagonal work; SURVEY 8d's whole-matrix "

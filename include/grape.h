@@ -484,7 +484,8 @@ int grape_plan_sectors(grape_plan *plan, int *sector_dims, int *nsectors, int ma
  * symmetry-adapted ones (GRAPE_OPT_NO_SYMMETRY).  Returns the number of classes. */
 int grape_plan_sector_info(grape_plan *plan, int *twin, int *symmetric, int max_classes);
 /* Which sector classes run the phase-covariant walks (ABI 9; GRAPE_OPT_NO_GAUGE): gauge[c] = 1 per
- * class; returns the number of classes (1 for whole matrices, gauge[0] = 0). */
+ * class, 2 (ABI 11) when the class's charges are the ladder N_j = j (the merged walks then use
+ * compile-time charge differences); returns the number of classes (1 for whole matrices, gauge[0] = 0). */
 int grape_plan_gauge_info(grape_plan *plan, int *gauge, int max_classes);
 /* 1 when every call of the plan runs one workgroup per evaluation (ABI 10; GRAPE_OPT_NO_EVAL1 above:
  * an eligible layout and max_batch <= 256), 0 otherwise, or a negative grape_status. */

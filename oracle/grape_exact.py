@@ -274,3 +274,61 @@ def fidelity_and_derivatives(fp, x, nparam=1):
                 np.real(tr_mod(P @ ct(U0d[q]) @ Ue @ P @ ct(Ue) @ U0 + P @ ct(U0) @ Ue @ P @ ct(Ue) @ U0d[q]))
                 + 2 * np.real(te_c * tr_mod(P @ ct(U0d[q]) @ Ue))) / DD)
     return float(F), Fdx, Fd2, Fd2dx
+
+
+def sensitivities_and_xadd(fp, x, nparam=1):
+    """(F, F_d2err, F_d2err_dx[n_main:]) evaluated in longdouble -- the x_add rows of the mixed gradient
+    without the mixed stencils: with H0 and Herror free of x_add, U_derr_dx_add = 0 and those rows are
+    the target's difference against U_derr (FidelityCalculations.jl:96-113), so only the nominal and the
+    eps error propagators are needed (UnitaryCalculations.jl:45-47, 66-73; 1 + ne exponentials per step
+    instead of fidelity_and_derivatives' 1 + 2 np + ne (2 + np)).  The same expressions as
+    fidelity_and_derivatives, so the values are its own."""
+    up = fp.unitary_problem
+    _check_scope(up)
+    nt, d, na, ne = up.ntimes, up.ndim, up.nb_additional_param, len(up.error_sources)
+    eps = up.eps
+    dt = up.t0 / nt
+    x = np.asarray(x, dtype=np.float64)
+    xm = x[:len(x) - na].reshape(nt, nparam)
+    xa = x[len(x) - na:].copy()
+    cdt = LD(-1j * dt)
+    ct = lambda A: A.conj().T  # noqa: E731
+    C = np.eye(d, dtype=LD)
+    Ssum = np.zeros((ne, d, d), dtype=LD)
+    for k in range(nt):
+        xk = xm[k].copy()
+        H0k = _h0_ld(up.H0, k + 1, xk, xa)
+        E = exp_ld(cdt * H0k)
+        Cold, C = C, E @ C
+        Ci = ct(C)
+        for e, src in enumerate(up.error_sources):
+            E1 = exp_ld(cdt * (_herr_ld(src, k + 1, xk, xa, eps) + H0k))
+            Ssum[e] = Ssum[e] + Ci @ ((E1 - E) / LD(eps)) @ Cold
+    U = C
+    P0 = np.asarray(fp.projector, dtype=np.complex128)
+    P = P0.copy()
+    P[P != 0] = 1
+    Dn = float(np.real(np.trace(P0)))
+    P0, P = P0.astype(LD), P.astype(LD)
+    DD = Dn * (Dn + 1)
+    tr_mod = lambda A: np.trace(P0 @ A)  # noqa: E731
+    U0 = _target_ld(fp.target_unitary, xa)
+    U0d = []
+    for q in range(na):
+        xq = xa.copy()
+        xq[q] = xq[q] + eps
+        U0d.append((_target_ld(fp.target_unitary, xq) - U0) / LD(eps))
+    F = (np.real(tr_mod(P @ ct(U0) @ U @ P @ ct(U) @ U0)) + abs(tr_mod(P @ ct(U0) @ U)) ** 2) / DD
+    Fd2 = np.zeros(ne)
+    add = np.zeros((na, ne))
+    for e in range(ne):
+        Ue = U @ Ssum[e]
+        Fd2[e] = float(2 * (np.real(tr_mod(P @ ct(U0) @ Ue @ P @ ct(Ue) @ U0 - P @ ct(Ue) @ Ue))
+                            + abs(tr_mod(P @ ct(U0) @ Ue)) ** 2
+                            - Dn * np.real(tr_mod(P @ ct(Ue) @ Ue))) / DD)
+        te_c = np.conj(tr_mod(P @ ct(U0) @ Ue))
+        for q in range(na):
+            add[q, e] = float(2 * (
+                np.real(tr_mod(P @ ct(U0d[q]) @ Ue @ P @ ct(Ue) @ U0 + P @ ct(U0) @ Ue @ P @ ct(Ue) @ U0d[q]))
+                + 2 * np.real(te_c * tr_mod(P @ ct(U0d[q]) @ Ue))) / DD)
+    return float(F), Fd2, add

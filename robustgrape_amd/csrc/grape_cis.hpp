@@ -29,18 +29,28 @@ constexpr double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-
                  C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
 
-// sin and cos of t, |t| <= kCisFast
-__host__ __device__ __forceinline__ void cis_fast(double t, double &s, double &c) {
-    const double kf = rint(t * kTwoOverPi);
-    double r = fma(-kf, kPio2Hi, t);
-    r = fma(-kf, kPio2Mid, r);
-    r = fma(-kf, kPio2Lo, r);
+// The constants of cis_fast by index: reduction, then sin, then cos coefficients
+enum : int { kTwoPi_ = 0, kHi_, kMid_, kLo_, S1_, S2_, S3_, S4_, S5_, S6_, C1_, C2_, C3_, C4_, C5_, C6_, kCisN };
+constexpr double kCisCoef[kCisN] = {kTwoOverPi, kPio2Hi, kPio2Mid, kPio2Lo, S1, S2, S3, S4, S5, S6,
+                                    C1, C2, C3, C4, C5, C6};
+
+// sin and cos of t, |t| <= kCisFast.  k(i) returns constant i of kCisCoef: on the host the array itself
+// (tests/test_cis_cpu.py); on the device a scalar load from a __constant__ copy (grape_walk.hpp
+// gauge_cis), so that every Horner step is one v_fma_f64 with an SGPR operand instead of a
+// v_fmac_f64 behind two v_mov_b32 of a literal (the walks are built without MachineLICM, so literals
+// were re-materialised every step)
+template <class K>
+__host__ __device__ __forceinline__ void cis_fast(double t, double &s, double &c, K k) {
+    const double kf = rint(t * k(kTwoPi_));
+    double r = fma(-kf, k(kHi_), t);
+    r = fma(-kf, k(kMid_), r);
+    r = fma(-kf, k(kLo_), r);
     const double z = r * r;
     // sin r = r + r^3 (S1 + z (S2 + ... + z S6))
-    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, S6, S5), S4), S3), S2), S1);
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, k(S6_), k(S5_)), k(S4_)), k(S3_)), k(S2_)), k(S1_));
     const double sr = fma(z * r, ps, r);
     // cos r = w + ((1 - w) - z / 2 + z^2 (C1 + ... + z C6)), w = 1 - z / 2 (fdlibm's compensated form)
-    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, k(C6_), k(C5_)), k(C4_)), k(C3_)), k(C2_)), k(C1_));
     const double hz = 0.5 * z, w = 1.0 - hz;
     const double cr = w + (((1.0 - w) - hz) + (z * z) * pc);
     const int q = (int)kf & 3;  // quadrant (two's complement: & 3 is k mod 4 for negative k too)

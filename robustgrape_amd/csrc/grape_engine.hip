@@ -1659,7 +1659,7 @@ int grape_plan_gauge_info(grape_plan *p, int *gauge, int max_classes) {
     if (!p) return fail(GRAPE_ERR_INVALID, "null plan");
     const int n = p->ncls > 0 ? p->ncls : 1;
     for (int c = 0; c < n && c < max_classes; ++c)
-        if (gauge) gauge[c] = p->ncls ? p->Ps[c].gauge : 0;
+        if (gauge) gauge[c] = p->ncls ? (p->Ps[c].gauge ? (p->Ps[c].gauge_ladder ? 2 : 1) : 0) : 0;
     return n;
 }
 

@@ -416,9 +416,7 @@ __global__ __launch_bounds__(kBlock) void k_eval1(Args A) {
     // phase 0b: the level phases' base e^{i a x_k} of every step, once (both classes share a), in
     // parallel over the workgroup instead of twice per step on each class's critical path
     for (int k = t; k < P.Nt; k += kBlock) {
-        double sn, cn;
-        sincos(A.PA.gauge_a * xs[k], &sn, &cn);
-        ph[k] = cmake(cn, sn);
+        ph[k] = gauge_cis(A.PA.gauge_a * xs[k]);
     }
     __syncthreads();
     if (tr) tc[1] = clock64();

@@ -41,6 +41,7 @@
 // polynomial constants of the inlined ocml calls out of the step loop pinned ~50 VGPRs and
 // spilled the walk state (k_walk_grad<2>: 128 VGPRs + 18 spilled -> 98, none spilled).
 #pragma once
+#include "grape_cis.hpp"
 #include "grape_kernels.hpp"
 #include "grape_walk_api.hpp"
 
@@ -848,6 +849,33 @@ __device__ __forceinline__ cd gauge_pow(cd z, int n) {
     for (int m = 1; m < n; ++m) r = cmul(r, z);
     return r;
 }
+// p = e^{i t}: the per-step phase base of the phase-covariant walks (grape_cis.hpp: Cody-Waite reduction
+// and fdlibm kernels, <= 0.67 ulp; the library sincos above |t| = 1e5).  Every gauge kernel (forward,
+// gradient, image walk, eval1) takes its phases here, so the walks of one evaluation agree bit for bit.
+#ifndef GRAPE_GAUGE_FAST_CIS  // 0: the library sincos (A/B)
+#define GRAPE_GAUGE_FAST_CIS 1
+#endif
+// the constants of grape_cis::cis_fast as opaque SGPR pairs: an empty asm hides the literal from the
+// instruction selector, so each Horner step is one v_fma_f64 with a scalar operand (not a v_fmac_f64 on
+// a VGPR copy of the literal, two v_mov_b32 per constant and step: the walks are built without
+// MachineLICM, so nothing is hoisted).  Not volatile: the asm stays free to move and to merge.
+struct CisConst {
+    __device__ __forceinline__ double operator()(int i) const {
+        double v = grape_cis::kCisCoef[i];
+        asm("" : "+s"(v));
+        return v;
+    }
+};
+__device__ __forceinline__ cd gauge_cis(double t) {
+    double s, c;
+#if GRAPE_GAUGE_FAST_CIS
+    if (fabs(t) <= grape_cis::kCisFast) grape_cis::cis_fast(t, s, c, CisConst());
+    else sincos(t, &s, &c);
+#else
+    sincos(t, &s, &c);
+#endif
+    return cmake(c, s);
+}
 // e^{i phi} - 1 without cancellation: (-2 sin^2(phi / 2), sin phi); Taylor for the FD-sized
 // phases (|phi| <= 0.05: truncation below 1e-22 relative), the library otherwise
 // (round 5: Horner in t^2 with the reciprocal factorials as constants -- the quotient form spent
@@ -999,6 +1027,33 @@ __device__ __forceinline__ void gauge_prop(const cd (&Et)[D][D], const cd (&e)[k
     }
 }
 
+// Ladder charges N_j = j (DevProblem::gauge_ladder, round 6): the pair phases e_jk = conj(p^{k-j}) and the
+// difference weights f_rj = conj(rho(j - r)) (r < j) from compile-time charge differences -- the products
+// of gauge_phases / gauge_fd_weights_dn in the same order (same bits), without their scalar loops over
+// runtime charge differences
+template <int D>
+__device__ __forceinline__ void ladder_powers(cd z, cd (&pw)[D]) {  // pw[m] = z^m (gauge_pow's product order)
+    pw[0] = cmake(1.0, 0.0);
+#pragma unroll
+    for (int m = 1; m < D; ++m) pw[m] = m == 1 ? z : cmul(pw[m - 1], z);
+}
+template <int D>
+__device__ __forceinline__ void ladder_rho(cd q, cd (&rh)[D]) {  // rho(m) = (1 + q)^m - 1 (gauge_fd_weights_dn)
+    rh[0] = czero();
+#pragma unroll
+    for (int m = 1; m < D; ++m) rh[m] = m == 1 ? q : cadd(cadd(rh[m - 1], q), cmul(q, rh[m - 1]));
+}
+template <int D>
+__device__ __forceinline__ void gauge_phases_ladder(cd p, cd (&e)[kGaugePairs<D>]) {
+    cd pw[D];
+    ladder_powers<D>(p, pw);
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int k = j + 1; k < D; ++k) e[gauge_pair(D, j, k)] = cconj(pw[k - j]);
+    }
+}
+
 // STORE: also hand the propagators to the gradient walk (B.Ew; P.walk_store_e)
 // TWIN (P.twin, NS = 2): the lane's two sectors have identical operator blocks (e.g. the Rydberg
 // sectors {01, 0r} and {10, r0} at equal Rabi frequencies and detunings): their propagators, chains
@@ -1058,9 +1113,7 @@ __device__ __forceinline__ void walk_fwd_body(const DevProblem &P, const DevBatc
         SM<D> A[GAUGE ? 1 : NE];
         cd p1 = czero();
         if constexpr (GAUGE) {
-            double sn, cn;
-            sincos(P.gauge_a * X.k0, &sn, &cn);  // e^{i a x_k}
-            p1 = cmake(cn, sn);
+            p1 = gauge_cis(P.gauge_a * X.k0);  // e^{i a x_k}
         } else {
             walk_build<D, NE>(P, ops, X, k + 1, none, A);
         }
@@ -1228,9 +1281,7 @@ __device__ __forceinline__ void walk_grad_body(const DevProblem &P, const DevBat
         xn = walk_load_x(P.np, xt + (size_t)min(k + 1, P.Nt - 1) * P.np * xs, xs);  // next step's controls
         if constexpr (GAUGE) {
             const double xk = XV.k0, xe = xk + P.eps;  // the reference's perturbed control (Pert delta = eps)
-            double sn, cn;
-            sincos(P.gauge_a * xk, &sn, &cn);
-            const cd p1 = cmake(cn, sn), q = cis_m1(P.gauge_a * (xe - xk));  // (xe - xk: exact)
+            const cd p1 = gauge_cis(P.gauge_a * xk), q = cis_m1(P.gauge_a * (xe - xk));  // (xe - xk: exact)
 #pragma unroll
             for (int w = 0; w < NE; ++w) {
                 cd dph[kGaugePairs<D>];
@@ -1472,12 +1523,13 @@ __device__ __forceinline__ void gauge_prop_lds(const cd *Et, const cd (&e)[kGaug
         for (int k = 0; k < D; ++k) E.set(j, k, gauge_sandwich<D>(e, j, k, Et[j * D + k]));
     }
 }
-template <int D, int NE>
+template <int D, int NE, bool LAD>
 __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, cd (&Q)[NE][D][D]) {
 #pragma unroll
     for (int w = 0; w < NE; ++w) {
         cd dph[kGaugePairs<D>];
-        gauge_phases<D>(p1, gn[w], dph);
+        if constexpr (LAD) gauge_phases_ladder<D>(p1, dph);
+        else gauge_phases<D>(p1, gn[w], dph);
         MStore<D, false> E;
         gauge_prop_lds<D>(Et + w * D * D, dph, E);
 #pragma unroll
@@ -1501,7 +1553,7 @@ __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&
 #define GRAPE_WALK_FWD_M_UNROLL 2  // (2: no loop-carried register moves, 2 waves/SIMD: fwd 0.183 -> 0.179 ms per C2 pass)
 #endif
 constexpr int kFwdMUnroll = GRAPE_WALK_FWD_M_UNROLL;
-template <int DA, bool TWB>
+template <int DA, bool TWB, bool LAD>
 __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fwd_m(DevProblem PA, DevBatch BA,
                                                                                   DevProblem PB, DevBatch BB) {
     constexpr int NEB = TWB ? 1 : 2;
@@ -1536,17 +1588,26 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fw
         const int k = min(k0 + jj, PA.Nt - 1);
         const double xk = xn.v0;
         xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs);  // next step's control
-        double sn, cn;
-        sincos(PA.gauge_a * xk, &sn, &cn);  // e^{i a x_k}, both classes (the engine checks one a)
-        const cd p1 = cmake(cn, sn);
-        merged_step_fwd<DA, 1>(EtA, gA, p1, QA);
-        merged_step_fwd<2, NEB>(EtB, gB, p1, QB);
+        const cd p1 = gauge_cis(PA.gauge_a * xk);  // e^{i a x_k}, both classes (the engine checks one a)
+        merged_step_fwd<DA, 1, LAD>(EtA, gA, p1, QA);
+        merged_step_fwd<2, NEB, LAD>(EtB, gB, p1, QB);
     };
     // steps past N_t leave Q alone: only the last chunk has them, so the first n_last steps of every
     // chunk run unpredicated and the rest only in the other chunks' lanes (a branch, not selects)
     const int nlast = PA.Nt - (PA.nchunks - 1) * PA.L;
-#pragma unroll kFwdMUnroll
-    for (int jj = 0; jj < nlast; ++jj) step(jj);
+    // unrolled by hand (two steps per trip, then the odd one): the phases' constants pass through an
+    // inline asm (gauge_cis), which LLVM treats as convergent and will not runtime-unroll
+    static_assert(kFwdMUnroll == 1 || kFwdMUnroll == 2, "GRAPE_WALK_FWD_M_UNROLL: 1 or 2");
+    int j2 = 0;
+    if constexpr (kFwdMUnroll == 2) {
+#pragma unroll 1
+        for (; j2 + 1 < nlast; j2 += 2) {
+            step(j2);
+            step(j2 + 1);
+        }
+    }
+#pragma unroll 1
+    for (; j2 < nlast; ++j2) step(j2);
 #pragma unroll 1
     for (int jj = nlast; jj < PA.L; ++jj) {
         if (L.c != PA.nchunks - 1) step(jj);
@@ -1686,7 +1747,10 @@ __device__ __forceinline__ void merged_xinit(const cd *Cr, const cd *Mw, cd (&X)
 // one gradient step of NSEC sectors over NE propagators (NSH = NSEC / NE sectors share one):
 // Y = X E^dag, the contraction, X <- E Y; returns the sectors' terms summed in sector order
 // (kWalkPresum: (0 + s_0) + s_1 ...; one sector: s_0)
-template <int D, int NE, int NSEC>
+#ifndef GRAPE_WALK_LADDER_CONTR  // ladder classes: the contraction grouped by charge difference (below)
+#define GRAPE_WALK_LADDER_CONTR 1
+#endif
+template <int D, int NE, int NSEC, bool LAD>
 __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, cd q,
                                                    double inv_eps, cd (&X)[NSEC][D][D]) {
     constexpr int NSH = NSEC / NE;
@@ -1695,7 +1759,8 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
 #pragma unroll
     for (int w = 0; w < NE; ++w) {
         cd dph[kGaugePairs<D>];
-        gauge_phases<D>(p1, gn[w], dph);
+        if constexpr (LAD) gauge_phases_ladder<D>(p1, dph);
+        else gauge_phases<D>(p1, gn[w], dph);
         gauge_prop_lds<D>(Et + w * D * D, dph, E[w]);
 #if !GRAPE_GAUGE_FD_DN
 #pragma unroll
@@ -1722,6 +1787,52 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
         }
     }
     double tot = 0.0, one = 0.0;
+    if constexpr (LAD && GRAPE_WALK_LADDER_CONTR) {
+        // Ladder charges: f_rj = rho(r - j) for r > j and conj(rho(j - r)) for r < j, so with
+        // T_m = sum_{r - j = m} Y_jr E_rj + conj(sum_{r - j = -m} Y_jr E_rj) (m = 1 .. D-1)
+        //   sum_{r != j} Re(Y_jr E_rj f_rj) = sum_m Re(rho(m) T_m):
+        // one complex MAC per off-diagonal entry and one product per charge difference, where the
+        // per-entry form spends E_rj f_rj / eps and a real MAC pair on every entry (same quantity,
+        // other roundings)
+        cd rh[D];
+        ladder_rho<D>(q, rh);
+#pragma unroll
+        for (int we = 0; we < NE; ++we) {
+#pragma unroll
+            for (int t = 0; t < NSH; ++t) {
+                double tre[D], tim[D];
+#pragma unroll
+                for (int m = 0; m < D; ++m) tre[m] = tim[m] = 0.0;
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        if (r == j) continue;
+                        const int m = r > j ? r - j : j - r;
+                        const cd y = X[we * NSH + t][j][r], e = E[we].at(r, j);
+                        tre[m] = fma(y.re, e.re, tre[m]);
+                        tre[m] = fma(-y.im, e.im, tre[m]);
+                        if (r > j) {
+                            tim[m] = fma(y.re, e.im, tim[m]);
+                            tim[m] = fma(y.im, e.re, tim[m]);
+                        } else {
+                            tim[m] = fma(-y.re, e.im, tim[m]);
+                            tim[m] = fma(-y.im, e.re, tim[m]);
+                        }
+                    }
+                }
+                double c = 0.0;
+#pragma unroll
+                for (int m = 1; m < D; ++m) {
+                    c = fma(rh[m].re, tre[m], c);
+                    c = fma(-rh[m].im, tim[m], c);
+                }
+                const double sv = c * inv_eps;
+                tot += sv;
+                one = sv;
+            }
+        }
+    } else {
 #pragma unroll
     for (int we = 0; we < NE; ++we) {
         double s[NSH];
@@ -1753,6 +1864,7 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
             one = s[t];
         }
     }
+    }
 #pragma unroll
     for (int w = 0; w < NSEC; ++w) {  // X <- E Y, column by column
         const int we = w / NSH;
@@ -1781,7 +1893,7 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
 #define GRAPE_WALK_MERGED_FDX 1
 #endif
 constexpr int kFdxTile = 16;  // steps per F_dx tile flush
-template <int DA, bool TWB>
+template <int DA, bool TWB, bool LAD>
 __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_grad_m(DevProblem PA, DevBatch BA,
                                                                                    DevProblem PB, DevBatch BB, int a_first) {
     constexpr int NEB = TWB ? 1 : 2;
@@ -1830,11 +1942,9 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
         const int k = min(k0 + jj, PA.Nt - 1);
         const double xk = xn.v0, xe = xk + PA.eps;  // the reference's perturbed control
         xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs);  // next step's control
-        double sn, cn;
-        sincos(PA.gauge_a * xk, &sn, &cn);
-        const cd p1 = cmake(cn, sn), q = cis_m1(PA.gauge_a * (xe - xk));  // (xe - xk: exact)
-        const double sa = merged_step_grad<DA, 1, 1>(EtA, gA, p1, q, PA.inv_eps, XA);
-        const double sb = merged_step_grad<2, NEB, NXB>(EtB, gB, p1, q, PB.inv_eps, XB);
+        const cd p1 = gauge_cis(PA.gauge_a * xk), q = cis_m1(PA.gauge_a * (xe - xk));  // (xe - xk: exact)
+        const double sa = merged_step_grad<DA, 1, 1, LAD>(EtA, gA, p1, q, PA.inv_eps, XA);
+        const double sb = merged_step_grad<2, NEB, NXB, LAD>(EtB, gB, p1, q, PB.inv_eps, XB);
         double v = 0.0;  // k_sec_reduce's sum of the classes' parts, in the plan's class order
         v += a_first ? sa : sb;
         v += a_first ? sb : sa;
@@ -2230,9 +2340,7 @@ __global__ __launch_bounds__(kWalkBlock, (img_gauge_waves<D, NS>())) void k_walk
         const bool act = L.ok && k0 + jj < P.Nt;
         const double xk = xn.v0;
         xn = walk_load_x(1, xt + (size_t)min(k + 1, P.Nt - 1) * xs, xs);  // next step's control
-        double sn, cn;
-        sincos(P.gauge_a * xk, &sn, &cn);
-        const cd p1 = cmake(cn, sn);
+        const cd p1 = gauge_cis(P.gauge_a * xk);
         const cd q1 = cis_m1(P.gauge_a * ((xk + P.eps) - xk)), q2 = cis_m1(P.gauge_a * ((xk + P.eps2) - xk));
 #pragma unroll
         for (int w = 0; w < NS; ++w) {

@@ -152,20 +152,26 @@ hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::De
     if (!merged_ok(PA, PB)) return hipErrorInvalidValue;
     const long lanes = (long)BA.nb * PA.nchunks;  // (class A: one sector, BA.nb evaluations)
     const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock)), blk(grape::kWalkBlock);
-    auto go = [&](auto da, auto tw) {
+    auto go = [&](auto da, auto tw, auto lad) {
         constexpr int DA = decltype(da)::value;
         constexpr bool TW = decltype(tw)::value;
+        constexpr bool LAD = decltype(lad)::value;
         if (stage == 0) {
-            hipLaunchKernelGGL((grape::k_walk_fwd_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB);
+            hipLaunchKernelGGL((grape::k_walk_fwd_m<DA, TW, LAD>), grid, blk, 0, st, PA, BA, PB, BB);
         } else if (stage == 2) {  // the chunk-total scan (one lane per evaluation)
             hipLaunchKernelGGL((grape::k_scan_seq<DA, TW>), dim3((unsigned)((BA.nb + grape::kSeqBlock - 1) / grape::kSeqBlock)), dim3(grape::kSeqBlock), 0, st, PA,
                                BA, PB, BB, BA.nb);
         } else {
-            hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
+            hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW, LAD>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
         }
     };
     using I3 = std::integral_constant<int, 3>;
-    PB.twin ? go(I3{}, std::true_type{}) : go(I3{}, std::false_type{});
+    // ladder charges in both classes (DevProblem::gauge_ladder): compile-time charge differences
+    const bool lad = PA.gauge_ladder && PB.gauge_ladder;
+    if (PB.twin)
+        lad ? go(I3{}, std::true_type{}, std::true_type{}) : go(I3{}, std::true_type{}, std::false_type{});
+    else
+        lad ? go(I3{}, std::false_type{}, std::true_type{}) : go(I3{}, std::false_type{}, std::false_type{});
     return hipGetLastError();
 }
 

@@ -249,7 +249,8 @@ class GrapePlan:
         e1 = _capi.lib().grape_plan_eval1(self.handle)
         _capi.check(min(e1, 0))
         return {"twin": tuple(bool(t[c]) for c in range(k)), "symmetric": bool(sym.value),
-                "gauge": tuple(bool(g[c]) for c in range(kg)), "eval1": bool(e1)}
+                "gauge": tuple(bool(g[c]) for c in range(kg)), "ladder": tuple(g[c] == 2 for c in range(kg)),
+                "eval1": bool(e1)}
 
 
 # Plan cache of the reference-shaped entry points (one plan per problem object, nparam and

@@ -32,13 +32,18 @@ def kname(n):
 
 def main(prefix, out_json=None, batch=None):
     vals = defaultdict(lambda: defaultdict(list))
-    for f in sorted(glob.glob(prefix + "_p*/run_counter_collection.csv")):
+    disp = defaultdict(set)  # dispatches per kernel in the first pass (the bench's timed steps + warm-up)
+    files = sorted(glob.glob(prefix + "_p*/run_counter_collection.csv"))
+    for fi, f in enumerate(files):
         for r in csv.DictReader(open(f)):
             vals[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if fi == 0:
+                disp[kname(r["Kernel_Name"])].add(r["Dispatch_Id"])
     res = {}
     for k, cs in vals.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         row = dict(m)
+        row["dispatches"] = len(disp.get(k, ()))
         fma, mul, add = (m.get("SQ_INSTS_VALU_%s_F64" % t) for t in ("FMA", "MUL", "ADD"))
         if fma is not None and mul is not None and add is not None:
             row["fp64_flop_per_dispatch"] = 64.0 * (2.0 * fma + mul + add)
@@ -48,7 +53,13 @@ def main(prefix, out_json=None, batch=None):
         print(f"{k[:60]:60s} waves {r.get('SQ_WAVES', 0):10.0f} VALU {r.get('SQ_INSTS_VALU', 0):14.0f} "
               f"FP64 FLOP/dispatch {r.get('fp64_flop_per_dispatch', 0):.4g}")
     if out_json:
-        json.dump({"batch": batch, "kernels": res,
+        import os
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        try:  # the library the profiled bench ran (robustgrape_amd/build.py writes libgrape.so.id)
+            build_id = open(os.path.join(root, "robustgrape_amd", "libgrape.so.id")).read().split()[0]
+        except (OSError, IndexError):
+            build_id = None
+        json.dump({"batch": batch, "build_id": build_id, "kernels": res,
                    "note": "per-dispatch means of rocprofv3 --pmc counters (scripts/pmc_mix.py)"},
                   open(out_json, "w"), indent=1)
 

@@ -116,13 +116,20 @@ def test_closure_batch_equals_single_and_equals_operator_basis_path():
 T3, T3_ABS, T3_XADD_ABS = 1e-5, 1e-7, 1e-5
 
 
-def _assert_err(nx_add, d2, d2dx, ref_d2, ref_d2dx):
+def _assert_err(nx_add, d2, d2dx, ref_d2, ref_d2dx, fp=None, x=None, test="tables_err"):
     nmain = d2dx.shape[0] - nx_add
     assert np.max(np.abs(d2 - ref_d2)) <= T3 * np.max(np.abs(ref_d2)) + T3_ABS, (d2, ref_d2)
     err = np.max(np.abs(d2dx[:nmain] - ref_d2dx[:nmain]))
     assert err <= T3 * np.max(np.abs(ref_d2dx[:nmain])) + T3_ABS, err
     if nx_add:
-        assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
+        # the x_add rows against their exact value (tests/xadd_pin.py); the table path tabulates the
+        # reference's x_add stencil itself, so it carries a residue of the checker's kind
+        from tests.xadd_pin import check_xadd, exact_rows
+        ex = exact_rows(fp, x) if fp is not None else None
+        if ex is not None:
+            check_xadd(test, d2dx, ref_d2dx, nmain, ex, stencil=True)
+        else:
+            assert np.max(np.abs(d2dx[nmain:] - ref_d2dx[nmain:])) <= T3_XADD_ABS
 
 
 @pytest.mark.parametrize("name,builder", [
@@ -134,9 +141,10 @@ def test_closure_error_sources_match_golden(name, builder):
     """The reference's own idiom Herror = H(eps) - H(0) as closures (runtests.jl:57-75, 474-494)."""
     from robustgrape_amd import calculate_fidelity_and_derivatives
     g = dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
-    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(builder(), g["x"])
+    fp = builder()
+    F, Fdx, d2, d2dx = calculate_fidelity_and_derivatives(fp, g["x"])
     _assert_fid(F, Fdx, float(g["F"]), g["F_dx"])
-    _assert_err(1, d2, d2dx, g["F_d2err"], g["F_d2err_dx"])
+    _assert_err(1, d2, d2dx, g["F_d2err"], g["F_d2err_dx"], fp, g["x"], "tables_golden_" + name)
 
 
 @pytest.mark.parametrize("d,ntimes,errors", [(5, 1, ("amp",)), (5, 11, ("amp", "freq")), (7, 6, ("freq",))])
@@ -149,7 +157,7 @@ def test_closure_error_sources_match_live_oracle(d, ntimes, errors):
     F0, g0, e0, ed0 = O.calculate_fidelity_and_derivatives(fp, x)
     F, g, e, ed = calculate_fidelity_and_derivatives(fp, x)
     _assert_fid(F, g, F0, g0)
-    _assert_err(1, e, ed, e0, ed0)
+    _assert_err(1, e, ed, e0, ed0, fp, x, f"tables_live_d{d}_nt{ntimes}")
 
 
 def test_closure_error_sources_with_xadd_dependent_h0():

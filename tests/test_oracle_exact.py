@@ -41,3 +41,19 @@ def test_exact_reproduces_the_evered_known_answer():
     from oracle import grape_exact as E
     F, g = E.fidelity_and_gradient(P.sym_problem(1000), P.evered_pulse(1000))
     assert F > 0.9999 and abs(F - 0.999996184760959) < 1e-12
+
+
+def test_sensitivities_and_xadd_are_the_full_evaluators_rows():
+    """grape_exact.sensitivities_and_xadd (only the nominal and eps error propagators) returns
+    fidelity_and_derivatives' own F, F_d2err and x_add rows of F_d2err_dx (tests/xadd_pin.py uses it)."""
+    import numpy as np
+    from oracle import grape_exact as E
+    from tests import problems as P
+    for fp, x in ((P.sym_problem(7, errors=("amp", "freq")), P.random_x(7, 11)),
+                  (P.full9_problem(5, nerr=4), P.random_x(5, 12, small=True))):
+        F, _, d2, d2dx = E.fidelity_and_derivatives(fp, x)
+        F1, d21, add = E.sensitivities_and_xadd(fp, x)
+        assert F1 == F and np.array_equal(d21, d2) and np.array_equal(add, d2dx[len(x) - 1:])
+    import pytest
+    with pytest.raises(ValueError):
+        E.sensitivities_and_xadd(P.xadd_err_problem(5, 3), P.xadd_x(3, 1))
