@@ -465,7 +465,19 @@ def c2_report(args, B, L, world, value, elapsed, ktimes, sectors=None, passes=No
         byte_model = {"k_expm": L * NT * per_step(lambda S: 16 * S * S),
                       "k_scan": L * NT * per_step(lambda S: 2 * 16 * S * S),
                       "k_expm_grad": L * NT * nvg * per_step(lambda S: 2 * 16 * S * S)}
-    grad_name = "k_walk_grad" if walk else "k_expm_grad"
+    eval1 = ktimes.get("k_eval1", (0.0, 0))[1] > 0
+    if eval1:
+        # one workgroup per evaluation (grape_eval1.hip): the walks' per-step work of both classes (the
+        # merged walks' model with one lane per chunk of 256) in one kernel
+        walk = True
+        merged = True
+        nE = lambda c, ns: 1 if twins[c] else ns  # noqa: E731
+        store = lambda S: False  # noqa: E731
+        step = sum(nE(c, ns) * (2 * prop(c, S) + 8 * S ** 3) + nX(c, ns) * (2 * 8 * S ** 3 + contr(c, S))
+                   for c, (S, ns) in enumerate(classes)) + trig_f + trig_g
+        flop_model = {"k_eval1": L * NT * step}
+        byte_model = {"k_eval1": xbytes + L * 8 * (NT + 2)}
+    grad_name = "k_eval1" if eval1 else ("k_walk_grad" if walk else "k_expm_grad")
     npass = passes or max(1, ktimes.get(grad_name, (0.0, 1))[1])
     per_pass = {k: v[0] / npass for k, v in ktimes.items() if v[1]}
     kname = max(flop_model, key=lambda k: per_pass.get(k, 0.0))

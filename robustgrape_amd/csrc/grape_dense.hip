@@ -394,12 +394,31 @@ __global__ __launch_bounds__(256) void k_dadd(DenseProblem DP, DenseBatch B) {
     if (threadIdx.x == 0) B.Fdx[(size_t)b * P.nx + (size_t)P.np * P.Nt + q] += red[0];
 }
 
+// F_d2err_dx_add[q, e] += sum_k Fd2add[e][k][q] (after k_derr_scan / the error head wrote the target's
+// part), one workgroup per (b, e, q), fixed summation order
+__global__ __launch_bounds__(256) void k_dadd_err(DenseProblem DP, DenseBatch B) {
+    const grape::DevProblem &P = DP.P;
+    const int q = blockIdx.x % DP.nva, be = blockIdx.x / DP.nva;
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int k = threadIdx.x; k < P.Nt; k += 256) s += B.Fd2add[((size_t)be * P.Nt + k) * DP.nva + q];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) B.Fd2dx[(size_t)be * P.nx + (size_t)P.np * P.Nt + q] += red[0];
+}
+
 // ---------------------------------------------------------------------------
 // error sources
 // ---------------------------------------------------------------------------
-// local-frame image Y = Q_k^dag dX Q_{k-1} of one difference, stored as Y^T (slot s of step k):
-//   s < np: Z1_u = Y((E_dx_u - E)/eps), and F_dx[u, k] = Re tr(M'_c Z1_u) = Re sum M'_c o Z1_u^T;
-//   np <= s < np + ne: W_e = Y((E_err_e - E)/eps);  then Z2_{e,u} = Y(mixed stencil, :79-83)
+// local-frame image Y = Q_k^dag dX Q_{k-1} of one difference, stored as Y^T (slot s of step k), over the
+// G = P.nvg gradient parameters of a step (np controls, then -- H0 / Herror reading x_add -- the x_add ones):
+//   s < G: Z1_u = Y((E_dx_u - E)/eps), and F_dx[u, k] = Re tr(M'_c Z1_u) = Re sum M'_c o Z1_u^T (a control's
+//          entry of F_dx, or step k's term of F_dx_add[u - np], summed by k_dadd);
+//   G <= s < G + ne: W_e = Y((E_err_e - E)/eps);  then Z2_{e,u} = Y(mixed stencil, :79-95)
 __global__ __launch_bounds__(NTHREADS, 1) void k_dlocal(DenseProblem DP, DenseBatch B) {
     extern __shared__ double lds[];
     const Lane ln = make_lane();
@@ -411,16 +430,17 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dlocal(DenseProblem DP, DenseBa
     SM S0 = sm_at(lds, LDS_R0), S1 = sm_at(lds, LDS_R1);
     const size_t nv = P.nv, step = (size_t)b * P.Nt + k;
     const double *Ek = B.E + step * nv * IMG;
+    const int G = P.nvg;
     HM X, T;
     {
         img_load(Ek, T, ln);  // E_k (nominal)
-        if (s < P.np + P.ne) {
-            const int v = s < P.np ? P.off_dx + s : P.off_err + (s - P.np) * P.err_stride;
+        if (s < G + P.ne) {
+            const int v = s < G ? P.off_dx + s : P.off_err + (s - G) * P.err_stride;  // (dxa follows dx)
             img_load(Ek + (size_t)v * IMG, X, ln);
             hm_sub(X, T);
             hm_scale(X, P.inv_eps);  // (1/eps) (E' - E)
         } else {
-            const int r = s - P.np - P.ne, e = r / P.np, u = r % P.np;
+            const int r = s - G - P.ne, e = r / G, u = r % G;
             const int v_err = P.off_err + e * P.err_stride;
             img_load(Ek + (size_t)(v_err + 2 + u) * IMG, X, ln);
             hm_add(X, T);
@@ -446,10 +466,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dlocal(DenseProblem DP, DenseBa
     hm_zero(T);
     mm<true, false, true, false>(S0, S1, T, ln);  // Q_{k-1}^T (Q_k^dag dX)^T = Y^T
     img_store(B.Zl + (step * DP.nz + s) * IMG, T, ln);
-    if (s < P.np) {
+    if (s < G) {
         img_load(B.Mc + ((size_t)b * DP.Nc + c) * IMG, X, ln);
         const double tr = wg_sum(hm_dot_re(X, T), lds, ln);
-        if (threadIdx.x == 0) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + s] = tr;
+        if (threadIdx.x == 0) {
+            if (s < P.np) B.Fdx[(size_t)b * P.nx + (size_t)k * P.np + s] = tr;
+            else B.Fadd[step * DP.nva + (s - P.np)] = tr;
+        }
     }
 }
 
@@ -464,7 +487,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_dwsum(DenseProblem DP, DenseBat
     hm_zero(acc);
     const int k0 = c * DP.Lc, k1 = min(k0 + DP.Lc, P.Nt);
     for (int k = k0; k < k1; ++k) {
-        img_load(B.Zl + (((size_t)b * P.Nt + k) * DP.nz + P.np + e) * IMG, T, ln);  // W_k^T
+        img_load(B.Zl + (((size_t)b * P.Nt + k) * DP.nz + P.nvg + e) * IMG, T, ln);  // W_k^T
         hm_add(acc, T);
     }
     img_load(B.Carry + ((size_t)b * DP.Nc + c) * IMG, T, ln);
@@ -671,10 +694,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_derr_grad(DenseProblem DP, Dens
     img_load(B.Mp + bec * IMG, Mr, ln);
     sm_store(S1, Mr, ln);  // M' for the whole chunk
     double *out = B.Fd2dx + be * P.nx;
-    const int k0 = c * DP.Lc, k1 = min(k0 + DP.Lc, P.Nt);
+    const int k0 = c * DP.Lc, k1 = min(k0 + DP.Lc, P.Nt), G = P.nvg;
     for (int k = k0; k < k1; ++k) {
         const double *Zk = B.Zl + ((size_t)b * P.Nt + k) * DP.nz * IMG;
-        img_load(Zk + (size_t)(P.np + e) * IMG, T, ln);  // W_k^T
+        img_load(Zk + (size_t)(G + e) * IMG, T, ln);  // W_k^T
         __syncthreads();
         sm_store(S0, T, ln);
         __syncthreads();
@@ -682,13 +705,16 @@ __global__ __launch_bounds__(NTHREADS, 1) void k_derr_grad(DenseProblem DP, Dens
         mm<false, false, true, false>(S1, S0, L, ln);  // M' W
         hm_scale(L, -1.0);
         hm_add(L, Bp);  // Lambda = B - M' W
-        for (int u = 0; u < P.np; ++u) {
+        for (int u = 0; u < G; ++u) {
             img_load(Zk + (size_t)u * IMG, T, ln);  // Z1_u^T
             double acc = hm_dot_re(L, T);
-            img_load(Zk + (size_t)(P.np + P.ne + e * P.np + u) * IMG, T, ln);  // Z2_{e,u}^T
+            img_load(Zk + (size_t)(G + P.ne + e * G + u) * IMG, T, ln);  // Z2_{e,u}^T
             acc += hm_dot_re(Mr, T);
             const double tr = wg_sum(acc, lds, ln);
-            if (threadIdx.x == 0) out[(size_t)k * P.np + u] = tr;
+            if (threadIdx.x == 0) {
+                if (u < P.np) out[(size_t)k * P.np + u] = tr;
+                else B.Fd2add[(be * P.Nt + k) * DP.nva + (u - P.np)] = tr;  // step k's x_add term (k_dadd_err)
+            }
         }
         hm_zero(Bp);
         mm<true, false, false, false>(S0, S1, Bp, ln);  // W M'
@@ -780,6 +806,7 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     const unsigned nerr_chunks = nchunks * (unsigned)P.P.ne;
     mark(GRAPE_KERNEL_GRAD, 0);
     hipLaunchKernelGGL(k_dlocal, dim3(nsteps * (unsigned)P.nz), dim3(NTHREADS), kLds, st, P, B);
+    if (P.nva > 0) hipLaunchKernelGGL(k_dadd, dim3((unsigned)(B.nb * P.nva)), dim3(256), 0, st, P, B);
     mark(GRAPE_KERNEL_GRAD, 1);
     mark(GRAPE_KERNEL_ERR_SCAN, 0);
     hipLaunchKernelGGL(k_dwsum, dim3(nerr_chunks), dim3(NTHREADS), kLds, st, P, B);
@@ -792,6 +819,8 @@ hipError_t launch_pipeline(const DenseProblem &P, const DenseBatch &B, hipStream
     mark(GRAPE_KERNEL_ERR_SCAN, 1);
     mark(GRAPE_KERNEL_ERR_GRAD, 0);
     hipLaunchKernelGGL(k_derr_grad, dim3(nerr_chunks), dim3(NTHREADS), kLds, st, P, B);
+    if (P.nva > 0)
+        hipLaunchKernelGGL(k_dadd_err, dim3((unsigned)(B.nb * P.P.ne * P.nva)), dim3(256), 0, st, P, B);
     mark(GRAPE_KERNEL_ERR_GRAD, 1);
     return hipGetLastError();
 }

@@ -16,7 +16,7 @@ struct DenseProblem {
     const double *W;      // [64] projector diagonal, zero-padded
     int Lc, Nc;           // chunk length / count of the prefix-product scan
     int nz;               // error path: local-frame slots per step, np (Z1) + ne (W) + ne np (Z2)
-    int nva;              // x_add gradient variants per step: na when H0 reads x_add (no error sources), else 0
+    int nva;              // x_add gradient variants per step: na when H0 / Herror read x_add, else 0
 };
 
 struct DenseBatch {
@@ -44,6 +44,8 @@ struct DenseBatch {
     double *B0;       // [nb][ne][Nc][IMG]   B at the chunk start: [T_c, M'] + M' Ttot
     double *Fd2;      // [nb][ne]
     double *Fd2dx;    // [nb][ne][nx]
+    double *Fd2add;   // [nb][ne][Nt][nva]  H0 / Herror read x_add: step k's term of F_d2err_dx_add[q] (k_derr_grad;
+                      //                    k_dadd_err sums them onto the target's part)
     grape::cd *gp_scr;  // general projector: head scratch (grape_projector_api.hpp)
 };
 

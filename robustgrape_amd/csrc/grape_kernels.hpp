@@ -107,6 +107,10 @@ struct DevProblem {
     // engine's level order: {11, S, rr} and {01, 0r}): the merged walks then take the pair phases and
     // difference weights from compile-time charge differences (grape_walk.hpp kLadder), same values
     int gauge_ladder;
+    // (round 6) E~ of every sector of the class, [nsec][D][D] row-major, computed once at plan creation by
+    // the walks' own exponential (grape_walk.hpp k_gauge_base_fill: the same bits as gauge_base_lds) for
+    // the merged walks, which read it through scalar loads (SGPR operands) instead of LDS copies
+    const cd *gauge_Et;
 };
 
 struct DevBatch {

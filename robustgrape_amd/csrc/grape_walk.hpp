@@ -1511,17 +1511,61 @@ __global__ __launch_bounds__(kWalkBlock, 1) void k_walk_grad_pair(DevProblem P0,
 // gauge walks' own (walk_fwd_body / walk_grad_body with GAUGE): at equal chunking the results are
 // those of the per-class kernels bit for bit.  Both classes take class A's chunking (the engine
 // sets class B's L and nchunks to class A's).
-#ifndef GRAPE_WALK_MERGED_WAVES
+#ifndef GRAPE_WALK_MERGED_WAVES  // waves per SIMD of the merged gradient walk (222 VGPRs with E~ in registers)
 #define GRAPE_WALK_MERGED_WAVES 2
 #endif
-template <int D>
+// E~ of the merged walks (round 6, GRAPE_WALK_FWD_ET_SMEM / GRAPE_WALK_GRAD_ET_SMEM): from the plan's
+// global copy (DevProblem::gauge_Et) through scalar loads -- E~ is launch-uniform, so each entry is an SGPR
+// operand of the complex product that forms E_k -- re-issued every step (the pointer is made opaque per
+// step, so the loads are not hoisted into 13 complex registers held across the walk).  The forward walk
+// then fits in 120 VGPRs (four waves per SIMD: fwd 0.161 -> 0.145 ms per C2 pass); the gradient walk would
+// fit in 160 (three waves) but measured slower there (0.308 -> 0.322 ms: the per-step scalar loads sit on
+// its critical path), so it keeps E~ from LDS in registers at two waves (A/B in one GPU call,
+// profiles/r06/ab_smem).  0: E~ in LDS (gauge_base_lds).
+#ifndef GRAPE_WALK_FWD_ET_SMEM
+#define GRAPE_WALK_FWD_ET_SMEM 1
+#endif
+#ifndef GRAPE_WALK_GRAD_ET_SMEM
+#define GRAPE_WALK_GRAD_ET_SMEM 0
+#endif
+template <int D, bool SMEM>
 __device__ __forceinline__ void gauge_prop_lds(const cd *Et, const cd (&e)[kGaugePairs<D>],
-                                               MStore<D, false> &E) {  // gauge_prop, E~ in LDS
+                                               MStore<D, false> &E) {  // gauge_prop, E~ in LDS or (SMEM) global
+    if constexpr (SMEM) {
+        cptr<cd> g = as_constant(Et);
+        asm volatile("" : "+s"(g));
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
+        for (int j = 0; j < D; ++j) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) E.set(j, k, gauge_sandwich<D>(e, j, k, Et[j * D + k]));
+            for (int k = 0; k < D; ++k) E.set(j, k, gauge_sandwich<D>(e, j, k, cload(g, j * D + k)));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) E.set(j, k, gauge_sandwich<D>(e, j, k, Et[j * D + k]));
+        }
     }
+}
+// E~ = exp(-i dt H_w(0)) of sectors w < nsec of a class into out [nsec][D][D] row-major: gauge_base_lds's
+// code (the nominal build at x = 0, the walks' exponential, unshifted), one lane per sector
+template <int D>
+__global__ __launch_bounds__(64) void k_gauge_base_fill(DevProblem P, cd *scr, cd *out, int nsec) {
+    const int w = threadIdx.x;
+    if (w >= nsec) return;
+    WalkX X0;
+    X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
+    Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    SM<D> A[1];
+    walk_build<D, 1>(P, as_constant(P.ops) + (size_t)w * P.sec_ops, X0, 1, none, A);
+    double mu0 = 0.0;
+    walk_expm<D, false, true, false>(A[0], scr + (size_t)w * 2 * D * D, mu0, true, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) out[(w * D + j) * D + i] = x[j];
+    });
 }
 template <int D, int NE, bool LAD>
 __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&gn)[NE], cd p1, cd (&Q)[NE][D][D]) {
@@ -1531,7 +1575,7 @@ __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&
         if constexpr (LAD) gauge_phases_ladder<D>(p1, dph);
         else gauge_phases<D>(p1, gn[w], dph);
         MStore<D, false> E;
-        gauge_prop_lds<D>(Et + w * D * D, dph, E);
+        gauge_prop_lds<D, GRAPE_WALK_FWD_ET_SMEM>(Et + w * D * D, dph, E);
 #pragma unroll
         for (int i = 0; i < D; ++i) {  // column i of E_k Q (the forward walk's order)
             cd q[D], t[D];
@@ -1553,16 +1597,23 @@ __device__ __forceinline__ void merged_step_fwd(const cd *Et, const GaugeN<D> (&
 #define GRAPE_WALK_FWD_M_UNROLL 2  // (2: no loop-carried register moves, 2 waves/SIMD: fwd 0.183 -> 0.179 ms per C2 pass)
 #endif
 constexpr int kFwdMUnroll = GRAPE_WALK_FWD_M_UNROLL;
+#ifndef GRAPE_WALK_FWD_M_WAVES  // the merged forward walk (120 VGPRs with E~ in SGPRs: four waves fit)
+#define GRAPE_WALK_FWD_M_WAVES 4
+#endif
 template <int DA, bool TWB, bool LAD>
-__global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_fwd_m(DevProblem PA, DevBatch BA,
+__global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_FWD_M_WAVES) void k_walk_fwd_m(DevProblem PA, DevBatch BA,
                                                                                   DevProblem PB, DevBatch BB) {
     constexpr int NEB = TWB ? 1 : 2;
     const VBlock vb = hw_block();
     const WalkLane L = walk_lane<1>(PA, BA, vb);  // (class A: one sector; its chunking is both classes')
     const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
     const int xs = kWalkXRow ? 1 : L.nbe;
-    const cd *EtA = gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
-    const cd *EtB = gauge_base_lds<2, NEB>(PB, as_constant(PB.ops), BB.wscr + (size_t)L.slot * 2 * 2 * 4);
+    const cd *EtA = GRAPE_WALK_FWD_ET_SMEM
+                        ? PA.gauge_Et
+                        : gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
+    const cd *EtB = GRAPE_WALK_FWD_ET_SMEM
+                        ? PB.gauge_Et
+                        : gauge_base_lds<2, NEB>(PB, as_constant(PB.ops), BB.wscr + (size_t)L.slot * 2 * 2 * 4);
     GaugeN<DA> gA[1];
     GaugeN<2> gB[NEB];
     gA[0] = gauge_charges<DA>(PA, 0);
@@ -1761,7 +1812,7 @@ __device__ __forceinline__ double merged_step_grad(const cd *Et, const GaugeN<D>
         cd dph[kGaugePairs<D>];
         if constexpr (LAD) gauge_phases_ladder<D>(p1, dph);
         else gauge_phases<D>(p1, gn[w], dph);
-        gauge_prop_lds<D>(Et + w * D * D, dph, E[w]);
+        gauge_prop_lds<D, GRAPE_WALK_GRAD_ET_SMEM>(Et + w * D * D, dph, E[w]);
 #if !GRAPE_GAUGE_FD_DN
 #pragma unroll
         for (int j = 0; j < D; ++j) rho[w][j] = gauge_rho(q, gn[w].n[j]);
@@ -1929,8 +1980,12 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_MERGED_WAVES) void k_walk_gr
             merged_xinit<2>(Cb, Mb, XB[w]);
         }
     }
-    const cd *EtA = gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
-    const cd *EtB = gauge_base_lds<2, NEB>(PB, as_constant(PB.ops), BB.wscr + (size_t)L.slot * 2 * 2 * 4);
+    const cd *EtA = GRAPE_WALK_GRAD_ET_SMEM
+                        ? PA.gauge_Et
+                        : gauge_base_lds<DA, 1>(PA, as_constant(PA.ops), BA.wscr + (size_t)L.slot * 2 * DA * DA);
+    const cd *EtB = GRAPE_WALK_GRAD_ET_SMEM
+                        ? PB.gauge_Et
+                        : gauge_base_lds<2, NEB>(PB, as_constant(PB.ops), BB.wscr + (size_t)L.slot * 2 * 2 * 4);
     GaugeN<DA> gA[1];
     GaugeN<2> gB[NEB];
     gA[0] = gauge_charges<DA>(PA, 0);

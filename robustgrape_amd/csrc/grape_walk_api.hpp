@@ -52,6 +52,8 @@ hipError_t launch_pair(int stage, const grape::DevProblem &P0, const grape::DevB
 bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB);
 // 1: the merged gradient walk writes F_dx rows itself (no k_sec_reduce for such passes)
 bool merged_writes_fdx();
+// E~ of the class's nsec sectors into out [nsec][D][D] (DevProblem::gauge_Et; scr: 2 D^2 complex per sector)
+hipError_t fill_gauge_base(const grape::DevProblem &P, int nsec, grape::cd *scr, grape::cd *out, hipStream_t st);
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
                          const grape::DevBatch &BB, int a_first, hipStream_t st);
 // F_dx parts the class's gradient stage writes per evaluation: its sectors, or (k_walk_grad with several

@@ -147,6 +147,16 @@ bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB) {
            PA.nvg == 1 && PB.nvg == 1 && PA.ne == 0 && PB.ne == 0;
 }
 bool merged_writes_fdx() { return GRAPE_WALK_MERGED_FDX != 0; }
+hipError_t fill_gauge_base(const grape::DevProblem &P, int nsec, grape::cd *scr, grape::cd *out, hipStream_t st) {
+    if (nsec < 1 || nsec > 64) return hipErrorInvalidValue;
+    switch (P.D) {
+        case 2: hipLaunchKernelGGL(grape::k_gauge_base_fill<2>, dim3(1), dim3(64), 0, st, P, scr, out, nsec); break;
+        case 3: hipLaunchKernelGGL(grape::k_gauge_base_fill<3>, dim3(1), dim3(64), 0, st, P, scr, out, nsec); break;
+        case 4: hipLaunchKernelGGL(grape::k_gauge_base_fill<4>, dim3(1), dim3(64), 0, st, P, scr, out, nsec); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
                          const grape::DevBatch &BB, int a_first, hipStream_t st) {
     if (!merged_ok(PA, PB)) return hipErrorInvalidValue;

@@ -320,3 +320,82 @@ def test_dense_analysis_entry_points_match_oracle():
     r0 = O.calculate_fidelity_response(fp, x, w)
     r = A.calculate_fidelity_response(fp, x, w)
     assert np.max(np.abs(r - r0)) <= T2 * np.max(np.abs(r0)) + T2_ABS
+
+
+def _split_terms_problem(d, ntimes, alpha=0.7):
+    """The C5 family with every Hermitian operator OP of H0 given as TWO non-Hermitian terms with complex
+    scales, e^{i alpha} U and e^{-i alpha} U^dag, U = triu(OP, 1) + diag(OP) / 2 (so each term is neither
+    Hermitian nor real-scaled, the sum is e^{i alpha} U + h.c.): the reference takes any closure whose value
+    is Hermitian (UnitaryCalculations.jl:45-47), the dense engine now checks the SUM at probe points."""
+    from robustgrape_amd.operators import OperatorBasisHamiltonian, Term
+    fp = S.dense_problem(d, ntimes, rank=min(16, d - 3))
+    up = fp.unitary_problem
+    terms = []
+    for t in up.H0.terms:
+        U = np.triu(t.op, 1) + np.diag(np.diag(t.op)) / 2
+        for op, sc in ((U, np.exp(1j * alpha)), (U.conj().T, np.exp(-1j * alpha))):
+            terms.append(Term(op, var=t.var, index=t.index, func=t.func, a=t.a, b=t.b, scale=t.scale * sc))
+    return fp.replace(unitary_problem=up.replace(H0=OperatorBasisHamiltonian(terms)))
+
+
+@pytest.mark.parametrize("d,ntimes", [(13, 3), (24, 17), (64, 5)])
+def test_dense_complex_coefficient_terms_match_live_oracle(d, ntimes):
+    """VERDICT r5 missing #2: H0 terms with complex coefficients (each term non-Hermitian, the sum Hermitian)
+    on the dense engine against the oracle and the exact forward difference."""
+    from oracle import grape_exact as E
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = _split_terms_problem(d, ntimes)
+    x = S.dense_x(ntimes, seed=800 + ntimes)
+    F0, g0, _, _ = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, _, _ = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid(F, g, F0, g0, f"dense_split_d{d}_nt{ntimes}", E.fidelity_and_gradient(fp, x, nparam=2))
+
+
+def _xadd_err_problem(d, ntimes, nerr=2):
+    """VERDICT r5 missing #2: the C5 family with error sources AND an H0 reading x_add (x_add[1] a global
+    detuning, x_add[0] the target phase modulating it), error 0 also modulated by cos(x_add[1]): every
+    variant of UnitaryCalculations.jl:57-95 (the x_add ones with the eps and eps2 error variants) is live."""
+    from robustgrape_amd.operators import FN_COS, FN_LINEAR, VAR_XADD, OperatorBasisError, OperatorBasisHamiltonian, Term
+    from robustgrape_amd.types import ErrorSource
+    base = S.dense_error_problem(d, ntimes, rank=min(16, d - 3), nerr=nerr, phase=True)
+    up = base.unitary_problem
+    Hx = S._hermitian(d, 70)
+    H0 = OperatorBasisHamiltonian(list(up.H0.terms) + [Term(Hx, var=VAR_XADD, index=1, func=FN_LINEAR, scale=0.4),
+                                                        Term(Hx, var=VAR_XADD, index=0, func=FN_COS, scale=0.2)])
+    errs = []
+    for e, es in enumerate(up.error_sources):
+        terms = list(es.Herror.terms)
+        if e == 0:
+            terms.append(Term(S._hermitian(d, 71), var=VAR_XADD, index=1, func=FN_COS, scale=0.3))
+        errs.append(ErrorSource(OperatorBasisError(terms)))
+    return base.replace(unitary_problem=up.replace(H0=H0, nb_additional_param=2, error_sources=errs))
+
+
+@pytest.mark.parametrize("d,ntimes,nerr", [(13, 1, 1), (16, 6, 2), (40, 5, 2), (64, 3, 1)])
+def test_dense_xadd_dependent_h0_with_error_sources_match_live_oracle(d, ntimes, nerr):
+    """x_add-dependent H0 and Herror with error sources above 12 levels (round 6): the x_add variants in the
+    dense error path (k_dlocal / k_derr_grad over np + na gradient parameters, k_dadd / k_dadd_err) against
+    the oracle: F, F_dx (incl. F_dx_add), F_d2err, F_d2err_dx (incl. its x_add rows)."""
+    from oracle import grape_oracle as O
+    from robustgrape_amd import calculate_fidelity_and_derivatives
+    fp = _xadd_err_problem(d, ntimes, nerr)
+    x = np.concatenate([S.dense_x(ntimes, seed=900 + ntimes), [0.7, -0.3]])
+    ref = O.calculate_fidelity_and_derivatives(fp, x)
+    F, g, d2, d2dx = calculate_fidelity_and_derivatives(fp, x)
+    _assert_fid_spread(F, g, ref[0], ref[1], f"dense_xadd_err_d{d}_nt{ntimes}", fp, x)
+    _assert_err(d2, d2dx, ref[2], ref[3])
+    assert d2dx.shape == (len(x), nerr) and np.max(np.abs(d2dx[-2:])) > 0
+
+
+def test_dense_xadd_err_batch_equals_single():
+    from robustgrape_amd.engine import GrapePlan
+    fp = _xadd_err_problem(24, 5)
+    X = np.stack([np.concatenate([S.dense_x(5, seed=s), [0.3 * s, -0.1 * s]]) for s in range(3)])
+    plan = GrapePlan(fp, nparam=2, max_batch=3)
+    out = plan.fidelity_grad(X)
+    plan.close()
+    one = GrapePlan(fp, nparam=2, max_batch=1)
+    out1 = one.fidelity_grad(X)
+    one.close()
+    assert all(np.array_equal(a, b) for a, b in zip(out, out1))

@@ -52,7 +52,8 @@ def _record(test, what, err, scale, tol):
 def test_which_plans_run_one_workgroup_per_evaluation():
     from robustgrape_amd.operators import OPT_NO_EVAL1, OPT_NO_GAUGE, OPT_NO_SYMMETRY
     cases = [(P.full9_problem(64), 1, 0, True), (P.full9_problem(64), 256, 0, True),
-             (P.full9_problem(64), 257, 0, False),            # a throughput plan: the walks
+             (P.full9_problem(64), 2048, 0, True),            # round 6: up to 2 048 (GRAPE_EVAL1_MAX_BATCH)
+             (P.full9_problem(64), 2049, 0, False),           # a throughput plan: the walks
              (P.full9_problem(64), 8, OPT_NO_EVAL1, False),
              (P.full9_problem(64), 8, OPT_NO_GAUGE, False),   # per-step exponentials: the pair kernels
              (P.full9_problem(64), 8, OPT_NO_SYMMETRY, False),  # 4-level permutation sectors

@@ -131,14 +131,14 @@ def test_gauge_bench_size_plan_against_c2_golden():
     """The bench's configuration (32 768 per pass selects the same kernels as 2 048) with the C2
     golden at scattered positions, and the whole batch against the per-step exponentials."""
     import os
-    from robustgrape_amd.operators import OPT_NO_GAUGE
+    from robustgrape_amd.operators import OPT_NO_EVAL1, OPT_NO_GAUGE
     g2 = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2.npz"),
                       allow_pickle=False))
-    n = 2048
+    n = 2048  # (plans of <= 2 048 take one workgroup per evaluation since round 6: OPT_NO_EVAL1 keeps the walks)
     X = np.stack([P.random_x(512, 5000 + s, small=True) for s in range(n)])
     for p in (0, 777, n - 1):
         X[p] = g2["x"]
-    pg, pn = _plan(P.full9_problem(512), n), _plan(P.full9_problem(512), n, OPT_NO_GAUGE)
+    pg, pn = _plan(P.full9_problem(512), n, OPT_NO_EVAL1), _plan(P.full9_problem(512), n, OPT_NO_GAUGE)
     try:
         F, G, _, _ = pg.fidelity_grad(X)
         Fn, Gn, _, _ = pn.fidelity_grad(X)
@@ -203,13 +203,14 @@ def test_merged_walks_match_per_class_walks(n):
     workgroup).  Against the per-step exponentials at the FD tier, and the C2 golden inside the
     batch."""
     import os
-    from robustgrape_amd.operators import OPT_NO_GAUGE, OPT_NO_MERGE
+    from robustgrape_amd.operators import OPT_NO_EVAL1, OPT_NO_GAUGE, OPT_NO_MERGE
     g2 = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2.npz"),
                       allow_pickle=False))
     f = P.full9_problem(512)
     X = np.stack([P.random_x(512, 7000 + s, small=(s % 3 != 0)) for s in range(n)])
     X[5] = g2["x"]
-    pm, pu, pn = _plan(f, n), _plan(f, n, OPT_NO_MERGE), _plan(f, n, OPT_NO_GAUGE)
+    pm, pu, pn = (_plan(f, n, OPT_NO_EVAL1), _plan(f, n, OPT_NO_MERGE | OPT_NO_EVAL1),  # (the throughput walks)
+                  _plan(f, n, OPT_NO_GAUGE))
     try:
         F, G, _, _ = pm.fidelity_grad(X)
         Fu, Gu, _, _ = pu.fidelity_grad(X)

@@ -7,7 +7,9 @@ eps2 stencil for x_add too (UnitaryCalculations.jl:87-95): ((E(x_add + eps2, err
 residue, summed over the steps -- so the oracle (a faithful restatement) carries up to ~5e-6 absolute
 there while the device, which forms no stencil for a parameter H does not read, carries none.  The
 device is therefore checked against the exact rows (oracle/grape_exact.sensitivities_and_xadd, longdouble)
-at T3 of their scale, and against the checker at T3 plus the checker's own measured distance from exact.
+at T3 of their scale plus the checker's own measured distance from exact (the double implementations'
+u / eps noise of the target difference is of the same size in the device and the checker), and against
+the checker within twice that distance.  Both comparisons are logged with the exact rows' scale.
 """
 import numpy as np
 
@@ -44,11 +46,14 @@ def check_xadd(test, got, ref, nmain, exact, rel=T3, ab=T3_ABS, stencil=False):
     scale = float(np.max(np.abs(ex)))
     noise = float(np.max(np.abs(ra - ex)))  # the checker's own distance from exact
     e_exact = float(np.max(np.abs(ga - ex)))
-    tol_exact = rel * scale + ab + (2 * noise if stencil else 0.0)
+    # the device's own u / eps noise (the double difference of the target, U0(x_add + eps) - U0, and of the
+    # error propagators) is of the checker's kind: both bounds carry the checker's measured distance from
+    # exact, which also holds the checker's stencil residue (T3 |exact| + that distance)
+    tol_exact = rel * scale + ab + (2 if stencil else 1) * noise
     record(test + "_vs_exact", "F_d2err_dx_add", e_exact, scale, tol_exact)
     assert e_exact <= tol_exact, (test, "F_d2err_dx_add vs exact", e_exact, scale)
     e_ref = float(np.max(np.abs(ga - ra)))
-    tol_ref = rel * scale + ab + (3 if stencil else 1) * noise
+    tol_ref = rel * scale + ab + (3 if stencil else 2) * noise
     record(test, "F_d2err_dx_add", e_ref, scale, tol_ref)
     assert e_ref <= tol_ref, (test, "F_d2err_dx_add", e_ref, scale, noise)
     return {"vs_exact": e_exact, "vs_ref": e_ref, "ref_noise": noise, "scale": scale}
