@@ -668,7 +668,24 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     # two per image (Q^dag Z Q), the chain product, and the phase sandwiches / stencil weights
     img_gauge = lambda S: 8 * S ** 3 * (1 + 3 * (1 + ne) + 2 * ne) + (S * S - S) * (12 + 34 * (1 + ne) + 12 * ne)  # noqa: E731
     img_step = lambda c, S: img_gauge(S) if gauges[c] else nv * flops_expm(S) + prod(S) * (1 + 3 * nz)  # noqa: E731
-    if walk:
+    # the lab-frame error walks (grape_walk.hpp GRAPE_WALK_ERR_LAB, round 6: every class phase-covariant, no
+    # images).  Per (step, sector, error): k_walk_wsum_lab 3 products (E~ R~ + N_e, . E~^dag, E~ Q^), the
+    # pair-phase rotation of R~ and the row phases of Q^; k_walk_err_lab 6 products (Y~, Lambda, G~, E~ G~,
+    # N_e Y~, E~ Y~), two weighted traces (a complex product and 2 FMAs per off-diagonal entry) and two
+    # rotations, plus per (step, sector) its F_dx lanes: 2 products, a trace, a rotation.  HBM: the x rows
+    # (one 8-B read per lane and step), the per-(step, error) terms written, the chunk states.
+    from robustgrape_amd import _capi
+    lab = walk and all(gauges[:len(classes)]) and "GRAPE_WALK_ERR_LAB=0" not in set(_capi.build_defines())
+    off = lambda S: S * S - S  # noqa: E731
+    lab_fwd = lambda S: ne * (3 * prod(S) + 6 * off(S) + 6 * S * S + 2 * S * S)  # noqa: E731
+    lab_err = lambda S: ne * (6 * prod(S) + 2 * 10 * off(S) + 2 * 6 * off(S)) + (2 * prod(S) + 16 * off(S))  # noqa: E731
+    if lab:
+        flop_model = {"k_walk_fwd": L * NT * per_step(lab_fwd), "k_err_grad": L * NT * per_step(lab_err)}
+        nsub = sum(ns for _, ns in classes)
+        byte_model = {"k_walk_fwd": L * 8 * NT * ne * len(classes) + L * (ne + 1) * 16 * per_step(lambda S: S * S) * 8,
+                      "k_grad/k_err_local": 0,
+                      "k_err_grad": L * 8 * NT * (ne + 1) * len(classes) + L * NT * 8 * nsub * (ne + 1)}
+    elif walk:
         # image walk (grape_walk.hpp k_walk_img) per (step, sector): the nv variant
         # exponentials, the chain product Q <- E Q and per image Z = E^dag dX, Y = Q^dag Z Q (3
         # products); HBM: the x row and the nz images written.  k_img_fdx (reported under
@@ -693,9 +710,9 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     ms = per_pass[kname]
     fp = flop_model[kname] / (ms * 1e-3) / 1e12
     hb = byte_model[kname] / (ms * 1e-3) / 1e9
-    img_kernel = "k_walk_img_gauge" if any(gauges[:len(classes)]) else "k_walk_img"
+    img_kernel = "k_walk_wsum_lab" if lab else "k_walk_img_gauge" if any(gauges[:len(classes)]) else "k_walk_img"
     short = {"k_grad/k_err_local": "k_err_local", "k_walk_fwd": img_kernel,
-             "k_err_grad": "k_walk_err_grad" if walk else "k_err_grad"}.get(kname, kname)
+             "k_err_grad": "k_walk_err_lab" if lab else "k_walk_err_grad" if walk else "k_err_grad"}.get(kname, kname)
     traffic = pmc_traffic(short, L, PMC_SUMMARY_C3, dims={S for S, _ in classes})
     if hb / HBM_PEAK_GBS > fp / FP64_PEAK_TFLOPS:
         roof = {"bound": "hbm", "kernel": kname, "achieved": hb, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -717,7 +734,8 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
                                "np=1, na=1; F, F_dx, F_d2err, F_d2err_dx",
                    "restarts_per_gpu": B, "global_batch": B * world, "parallelism": f"restarts x{world}",
                    "sectors": [{"levels": S, "sectors": ns} for S, ns in classes] if sec else None,
-                   "phase_covariant": [bool(g) for g in gauges[:len(classes)]]},
+                   "phase_covariant": [bool(g) for g in gauges[:len(classes)]],
+                   "error_walks": "lab-frame (no images)" if lab else "image walk" if walk else "stored variants"},
         "roofline": roof,
         "kernels_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ktimes.items() if v[1]},
     }
@@ -730,12 +748,14 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     nimg = 3 if walk else 2
     exe = NT * sum(ns * ((img_step(c, S) if walk else nv * flops_expm(S) + prod(S) + nz * nimg * prod(S))
                          + ne * 2 * prod(S) + 8 * S ** 2 * (1 + ne)) for c, (S, ns) in enumerate(classes))
+    if lab:
+        exe = NT * per_step(lambda S: lab_fwd(S) + lab_err(S))
     if sec:
         exe += (16 + 24 * ne) * 8 * D ** 3
     out["roofline"]["whole_eval"] = {"flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
                                      "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
                                      "flop_per_eval_survey": canon}
-    if walk:  # PMC HBM bytes of one whole device pass (every kernel), against the pass time
+    if walk and not lab:  # PMC HBM bytes of one whole device pass (every kernel), against the pass time
         pipe = pmc_pipeline(L, img_kernel, {S for S, _ in classes}, PMC_SUMMARY_C3)
         if pipe:
             pass_ms = sum(per_pass.values())

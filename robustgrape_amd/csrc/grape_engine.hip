@@ -1562,6 +1562,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                     return bail(fail(GRAPE_ERR_HIP, "upload failed (gauge)"));
                 Ps.gauge_n = gn;
             }
+            // error sources on a phase-covariant class: the lab-frame walks (no images, grape_walk.hpp
+            // GRAPE_WALK_ERR_LAB) when the base table's lanes fit one workgroup
+            Ps.gauge_lab = (GRAPE_WALK_ERR_LAB && Ps.gauge && P.ne > 0 &&
+                            sc.nsec * (1 + 2 * P.ne) <= grape::kLabBaseMaxLanes) ? 1 : 0;
+            Ps.gauge_Et = nullptr;
             Ps.walk_store_e = Ps.walk && !Ps.gauge && P.ne == 0 && S >= grape::kWalkStoreMinD &&
                               !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
             // latency-bound walk classes (fewer sub-evaluations than CUs, or the option): 16-wave scans,
@@ -1598,7 +1603,7 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                 dalloc(&b.sidx, sc.sidx.size()) != hipSuccess || dalloc(&b.ops, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
                 dalloc(&b.opsT, (size_t)sc.nsec * n_ops * TS) != hipSuccess ||
                 // (the image walk's images are lane-minor over its padded launch width: grape_walk.hpp img_index)
-                dalloc(&b.Zl, (Ps.walk ? (size_t)sc.nsec * Ps.L * lanes_pad : R * P.Nt) * (ne ? P.nz : 0) * TS) != hipSuccess ||
+                dalloc(&b.Zl, (Ps.walk ? (size_t)sc.nsec * Ps.L * lanes_pad : R * P.Nt) * (ne && !Ps.gauge_lab ? P.nz : 0) * TS) != hipSuccess ||
                 dalloc(&b.Wc, (Ps.walk ? R * ne * Ps.nchunks : 0) * TS) != hipSuccess ||
                 dalloc(&b.Me, R * ne * Ps.nchunks * 3 * TS) != hipSuccess || dalloc(&b.TotS, R * ne * TS) != hipSuccess ||
                 dalloc(&b.MsecE, R * ne * TS) != hipSuccess || dalloc(&b.part_err, R * ne * P.Nt * nvg) != hipSuccess)
@@ -1624,6 +1629,19 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                 return bail(fail(GRAPE_ERR_HIP, "upload failed (sectors)"));
             Ps.ops = b.ops;
             Ps.opsT = b.opsT;
+            if (Ps.gauge_lab) {  // the lab-frame error walks' base table, once per plan
+                const size_t nbm = (size_t)sc.nsec * (1 + 2 * P.ne);
+                cd *scr = nullptr;
+                if (dalloc(&b.gEt, nbm * TS) != hipSuccess || dalloc(&scr, nbm * 2 * TS) != hipSuccess) {
+                    if (scr) (void)hipFree(scr);
+                    return bail(fail(GRAPE_ERR_ALLOC, "device allocation failed (gauge error base)"));
+                }
+                const hipError_t e = grape_walk::fill_gauge_err_base(Ps, sc.nsec, scr, b.gEt, p->stream);
+                const hipError_t es = hipStreamSynchronize(p->stream);
+                (void)hipFree(scr);
+                if (e != hipSuccess || es != hipSuccess) return bail(fail(GRAPE_ERR_HIP, "gauge error base fill failed"));
+                Ps.gauge_Et = b.gEt;
+            }
             // twin sectors (grape_walk.hpp TWIN): two walk sectors whose blocks of every operator H0
             // and the error sources use are identical, with the same padding -- one exponential
             // per step serves both (the 2-level Rydberg sectors at equal Rabi frequencies)

@@ -110,7 +110,11 @@ struct DevProblem {
     // (round 6) E~ of every sector of the class, [nsec][D][D] row-major, computed once at plan creation by
     // the walks' own exponential (grape_walk.hpp k_gauge_base_fill: the same bits as gauge_base_lds) for
     // the merged walks, which read it through scalar loads (SGPR operands) instead of LDS copies
+    // With error sources (gauge_lab, round 6): the lab-frame error walks (grape_walk.hpp k_walk_wsum_lab /
+    // k_walk_err_lab, no images) and gauge_Et = [nsec][1 + 2 ne][D][D]: E~, N_e = (E~_e1 - E~) / eps,
+    // M_e = E~_e2 - E~ (k_gauge_err_base_fill)
     const cd *gauge_Et;
+    int gauge_lab;
 };
 
 struct DevBatch {

@@ -2731,4 +2731,438 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Phase-covariant classes with error sources, without images (round 6, GRAPE_WALK_ERR_LAB)
+// ---------------------------------------------------------------------------
+// The image walk (k_walk_img_gauge) writes 1 + 2 ne local-frame images Y(Z) = Q_{k-1}^dag Z Q_{k-1} per
+// step and sector -- 9 tiles at C3's 4-level class, ~10 GB per pass of 8 192 evaluations -- for
+// k_walk_img_sum and k_walk_err_grad to read back.  But every use of an image is a trace against a
+// chunk-local matrix A, Re tr(A Y(Z)) = Re tr(Abar Z) with Abar = Q_{k-1} A Q_{k-1}^dag, and the chunk-local
+// states of the back end obey recurrences whose lab-frame forms close over E_k and the step's differences
+// alone.  So both ends carry transported states and no image is formed or stored:
+//
+// stage 0, k_walk_wsum_lab -- one lane per (chunk, evaluation, error e):
+//     R <- (E R + dW_e) E^dag,  Q <- E Q
+//   R = Q (sum_{j<k} W_j) Q^dag and dW_e = (E(err_e eps) - E) / eps = E w_e; at the chunk end
+//   W_c = Q^dag R Q -- k_err_scan's chunk sum of the W images (UnitaryCalculations.jl:111-112) -- and, for
+//   e = 0, the chunk total T_c = Q.
+// stage 2, k_walk_err_lab -- one lane per (chunk, evaluation, error e); the lanes of e = ne take F_dx:
+//   X = M'_{c,e}, L = B_c = T_c M' - M' T_c + M' Ttot (k_walk_err_grad's chunk start), then per step
+//     Y = X E^dag,  L <- L - Y dW  (= Lambda_k),  G = L E^dag,
+//     F_d2err_dx[k] (sector part) = Re tr(G dX1) + Re tr(Y dX2_e)
+//     L <- E G + dW Y  (B_{k+1} = Lambda_k + W_k M'),  X <- E Y
+//   with dX1 = (E' - E) / eps and dX2_e the mixed stencil's numerator over eps2^2 (UnitaryCalculations.jl
+//   :48-95): with z = E^dag dX, Re tr(Lambda z1) = Re tr(G dX1), Re tr(X z2) = Re tr(Y dX2), and
+//   E w E^dag = dW E^dag gives the L update.  F_dx lanes: X = M'_c, Re tr(Y dX1), X <- E Y
+//   (FidelityCalculations.jl:56-76, the gauge gradient walk's step).
+//
+// Gauge frame.  E_k = D_k E~ D_k^dag (D_k = diag(e^{i a x_k N_j})), dW_e = D_k N_e D_k^dag with
+// N_e = (E~_e1 - E~) / eps, dX1 = D_k (E~ o f1) D_k^dag / eps and dX2_e = D_k (M_e o f2) D_k^dag / eps2^2 with
+// M_e = E~_e2 - E~ (E~_e1 = exp(A0 + eps A_e0), E~_e2 = exp(A0 + eps2 A_e0), A at x = 0; f1, f2 the
+// difference weights of the image walk).  So the states are carried as S~ = D_k^dag S D_k: every product
+// then has an x-independent, workgroup-uniform factor (E~ or N_e: LDS broadcasts, no per-lane propagator),
+// the traces take E~ o f1 and M_e o f2, and moving to the next step's frame is an element-wise phase,
+// S~ <- Om S~ Om^dag with Om = D_{k+1}^dag D_k (pair phases of e^{i a (x_k - x_{k+1})}).  The forward lane
+// carries Q^ = D_{k+1}^dag Q (Q^ <- Om E~ Q^) and R~; the D factors cancel in W_c = Q^dag R Q = Q^^dag R~ Q^.
+// Six D x D products per step and error (k_walk_err_grad: two, plus 9 image reads; the image walk: two
+// per image), the live state three matrices (two waves per SIMD at D = 4).
+#ifndef GRAPE_WALK_WSUM_LAB_WAVES
+#define GRAPE_WALK_WSUM_LAB_WAVES 2
+#endif
+#ifndef GRAPE_WALK_ERR_LAB_WAVES
+#define GRAPE_WALK_ERR_LAB_WAVES 2
+#endif
+#ifndef GRAPE_WALK_ERR_LAB4_WAVES  // k_walk_err_lab<4>: four 4 x 4 complex matrices live (256 VGPRs) at the peak
+#define GRAPE_WALK_ERR_LAB4_WAVES 1
+#endif
+template <int D>
+constexpr int err_lab_waves() { return D >= 4 ? GRAPE_WALK_ERR_LAB4_WAVES : GRAPE_WALK_ERR_LAB_WAVES; }
+// the base table: lanes t < nsec (1 + 2 ne) compute exp(A0), exp(A0 + eps A_e0), exp(A0 + eps2 A_e0)
+// (k_walk_img_gauge's builds and exponential), then N_e and M_e in place
+template <int D>
+__global__ __launch_bounds__(kLabBaseMaxLanes) void k_gauge_err_base_fill(DevProblem P, cd *scr, cd *out, int nsec) {
+    constexpr int TS = D * D;
+    const int nb = 1 + 2 * P.ne, t = threadIdx.x;
+    if (t < nsec * nb) {
+        const int w = t / nb, b = t % nb;
+        const int e = b == 0 ? -1 : b <= P.ne ? b - 1 : b - 1 - P.ne;
+        const double ev = b == 0 ? 0.0 : b <= P.ne ? P.eps : P.eps2;
+        WalkX X0;
+        X0.k0 = X0.k1 = X0.a0 = X0.a1 = 0.0;
+        Pert none;
+        none.var = -1;
+        none.index = 0;
+        none.delta = 0.0;
+        SM<D> A[1];
+        walk_build<D, 1>(P, as_constant(P.ops) + (size_t)w * P.sec_ops, X0, 1, none, A, e, ev);
+        double mu0 = 0.0;
+        cd *dst = out + (size_t)t * TS;
+        walk_expm<D, false, true, false>(A[0], scr + (size_t)t * 2 * TS, mu0, true, [&](int i, const cd (&x)[D]) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) dst[j * D + i] = x[j];
+        });
+    }
+    __syncthreads();
+    for (int q = t; q < nsec * P.ne * TS; q += blockDim.x) {
+        const int w = q / (P.ne * TS), r = q % (P.ne * TS), e = r / TS, el = r % TS;
+        const cd e0 = out[(size_t)w * nb * TS + el];
+        cd *n = out + ((size_t)w * nb + 1 + e) * TS + el, *m = out + ((size_t)w * nb + 1 + P.ne + e) * TS + el;
+        *n = cscale(P.inv_eps, csub(*n, e0));
+        *m = csub(*m, e0);
+    }
+}
+// The base table through scalar loads: every operand is uniform over a workgroup (sector group blockIdx.y,
+// error e = blockIdx.z), so each entry is an SGPR operand of the FMAs -- no VGPRs, no LDS instructions.  A
+// matrix is read row by row, each row's pointer tied (an empty asm with a register input) to a result two
+// rows back, so at most two rows (32 SGPRs at D = 4) are in flight: unchained, the scheduler issues every
+// load of a step at its top (LDS copies measured 190+ VGPRs of preloaded operands at D = 4, scalar loads
+// 128-198 SGPRs, spilled).
+struct LabBase {
+    cptr<cd> g;  // the class's table
+    int nb, ne, e;
+    template <int D>
+    __device__ __forceinline__ cptr<cd> mat(int w, int m) const {  // sector w; m: 0 E~, 1 N_e, 2 M_e
+        const int b = m == 0 ? 0 : m == 1 ? 1 + e : 1 + ne + e;
+        return g + ((size_t)w * nb + b) * (D * D);
+    }
+};
+__device__ __forceinline__ LabBase lab_base(const DevProblem &P, int e) {
+    LabBase b;
+    b.nb = 1 + 2 * P.ne;
+    b.ne = P.ne;
+    b.e = e < P.ne ? e : 0;  // (F_dx lanes: E~ only)
+    b.g = as_constant(P.gauge_Et);
+    return b;
+}
+// the table pointer made opaque once per step: the row addresses are then formed in the step (a few scalar
+// adds) instead of being hoisted out of the loop as ~40 loop-invariant 64-bit SGPR values (spilled to VGPR lanes)
+__device__ __forceinline__ LabBase lab_step(LabBase b) {
+    asm volatile("" : "+s"(b.g));
+    return b;
+}
+template <int D>
+__device__ __forceinline__ cptr<cd> lab_row(cptr<cd> U, int r, double dep) {
+    cptr<cd> p = U + r * D;
+    asm volatile("" : "+s"(p) : "v"(dep));
+    return p;
+}
+// C (+)= A U^dag, U uniform: row c of U gives column c of C
+template <int D, bool ACC>
+__device__ __forceinline__ void lab_mul_udag(const cd (&A)[D][D], cptr<cd> U, cd (&C)[D][D]) {
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+        const cptr<cd> row = lab_row<D>(U, c, c >= 2 ? C[0][c - 2].re : A[0][0].re);
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            const cd u = cconj(cload(row, m));
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                if (!ACC && m == 0) C[r][c] = cmul(A[r][m], u);
+                else cmac(C[r][c], A[r][m], u);
+            }
+        }
+    }
+}
+// C (+)= U A, U uniform: row r of U gives row r of C
+template <int D, bool ACC>
+__device__ __forceinline__ void lab_umul(cptr<cd> U, const cd (&A)[D][D], cd (&C)[D][D]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const cptr<cd> row = lab_row<D>(U, r, r >= 2 ? C[r - 2][0].re : A[0][0].re);
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            const cd u = cload(row, m);
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+                if (!ACC && m == 0) C[r][c] = cmul(u, A[m][c]);
+                else cmac(C[r][c], u, A[m][c]);
+            }
+        }
+    }
+}
+// C -= A U, U uniform: row m of U updates every entry of C
+template <int D>
+__device__ __forceinline__ void lab_sub_mul_u(const cd (&A)[D][D], cptr<cd> U, cd (&C)[D][D]) {
+    double dep[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        const cptr<cd> row = lab_row<D>(U, m, m >= 2 ? dep[m - 2] : A[0][0].re);
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            const cd u = cload(row, c);
+#pragma unroll
+            for (int r = 0; r < D; ++r) cmac(C[r][c], cmake(-A[r][m].re, -A[r][m].im), u);
+        }
+        dep[m] = C[D - 1][D - 1].re;
+    }
+}
+// C += U element-wise, U uniform
+template <int D>
+__device__ __forceinline__ void lab_add_u(cptr<cd> U, cd (&C)[D][D]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const cptr<cd> row = lab_row<D>(U, r, r >= 2 ? C[r - 2][0].re : C[0][0].re);
+#pragma unroll
+        for (int c = 0; c < D; ++c) C[r][c] = cadd(C[r][c], cload(row, c));
+    }
+}
+// S <- Om S Om^dag: S_ij e_ij with the pair phases e of Om (e_ji = conj(e_ij), the diagonal unchanged)
+template <int D>
+__device__ __forceinline__ void lab_rotate(const cd (&e)[kGaugePairs<D>], cd (&S)[D][D]) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) S[i][j] = gauge_sandwich<D>(e, i, j, S[i][j]);
+    }
+}
+// sum_{r != j} Re(Y_jr (U o f)_rj): the trace of Y against a uniform matrix with the difference weights
+template <int D>
+__device__ __forceinline__ double lab_trace_f(const cd (&Y)[D][D], cptr<cd> U, const cd (&f)[kGaugePairs<D>]) {
+    double s = 0.0, dep[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const cptr<cd> row = lab_row<D>(U, r, r >= 2 ? dep[r - 2] : Y[0][0].re);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            if (r == j) continue;
+            const cd d = cmul(cload(row, j), gauge_fd_weight<D>(f, r, j));
+            s = fma(Y[j][r].re, d.re, s);
+            s = fma(-Y[j][r].im, d.im, s);
+        }
+        dep[r] = s;
+    }
+    return s;
+}
+
+template <int D, int NS>
+__global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_WSUM_LAB_WAVES) void k_walk_wsum_lab(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<NS>(P, B, vb);
+    const int ns = P.nsec > 1 ? P.nsec : 1, e = blockIdx.z;
+    const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);
+    const int xs = kWalkXRow ? 1 : L.nbe;
+    const LabBase lb = lab_base(P, e);
+    GaugeN<D> gn[NS];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
+    const int k0 = L.c * P.L;
+    double xk = walk_load_x(1, xt + (size_t)min(k0, P.Nt - 1) * xs, xs).v0;
+    // Q^ = D_{k0}^dag (Q = I at the chunk start), R~ = 0
+    cd Q[NS][D][D], R[NS][D][D];
+    {
+        const cd pc = cconj(gauge_cis(P.gauge_a * xk));
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const cd dj = gauge_pow(pc, gn[w].n[j]);
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    Q[w][j][i] = i == j ? dj : czero();
+                    R[w][j][i] = czero();
+                }
+            }
+        }
+    }
+    double xnext = xk;
+    auto step = [&](int jj) {
+        const int k = min(k0 + jj, P.Nt - 1);
+        xnext = walk_load_x(1, xt + (size_t)min(k + 1, P.Nt - 1) * xs, xs).v0;
+        const cd om = gauge_cis(P.gauge_a * xk - P.gauge_a * xnext);  // Om = D_{k+1}^dag D_k
+        xk = xnext;
+        const LabBase lbs = lab_step(lb);
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            cd T[D][D];
+            lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), R[w], T);  // T = E~ R~ + N_e
+            lab_add_u<D>(lbs.mat<D>(L.w0 + w, 1), T);
+            lab_mul_udag<D, false>(T, lbs.mat<D>(L.w0 + w, 0), R[w]);  // R~ = T E~^dag
+            lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), Q[w], T);      // T = E~ Q^
+            cd ep[kGaugePairs<D>];
+            gauge_phases<D>(om, gn[w], ep);
+            lab_rotate<D>(ep, R[w]);
+            cd dl[D];  // Om's level phases om^{N_j}: Q^ <- Om T (rows)
+#pragma unroll
+            for (int j = 0; j < D; ++j) dl[j] = gauge_pow(om, gn[w].n[j]);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+#pragma unroll
+                for (int i = 0; i < D; ++i) Q[w][j][i] = cmul(dl[j], T[j][i]);
+            }
+        }
+    };
+    // steps past N_t leave Q^ and R~ alone: only the last chunk has them
+    const int nlast = P.Nt - (P.nchunks - 1) * P.L;
+    int j = 0;
+#pragma unroll 1
+    for (; j < nlast; ++j) step(j);
+#pragma unroll 1
+    for (; j < P.L; ++j) {
+        if (L.c != P.nchunks - 1) step(j);
+    }
+    if (!L.ok) return;
+    const cd pn = gauge_cis(P.gauge_a * xnext);  // Q = D_next Q^ (the frame of the last rotation)
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+        const size_t sub = (size_t)L.be * ns + L.w0 + w;
+        cd T[D][D];
+#pragma unroll
+        for (int r = 0; r < D; ++r) {  // T = R~ Q^
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+                cd s = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(s, R[w][r][m], Q[w][m][c]);
+                T[r][c] = s;
+            }
+        }
+        cd *dw = B.Wc + ((sub * P.ne + e) * P.nchunks + L.c) * TS;  // W_c = Q^^dag T, row-major
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+#pragma unroll
+            for (int c = 0; c < D; ++c) {
+                cd s = czero();
+#pragma unroll
+                for (int m = 0; m < D; ++m) cmac(s, cconj(Q[w][m][r]), T[m][c]);
+                dw[r * D + c] = s;
+            }
+        }
+        if (e == 0) {  // the chunk total (k_walk_img_gauge's layout)
+            cd *dst = B.Tc + (sub * P.nchunks + L.c) * TS;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const cd dr = gauge_pow(pn, gn[w].n[r]);
+#pragma unroll
+                for (int c = 0; c < D; ++c) dst[r * D + c] = cmul(dr, Q[w][r][c]);
+            }
+        }
+    }
+}
+
+template <int D, int NS>
+__global__ __launch_bounds__(kWalkBlock, err_lab_waves<D>()) void k_walk_err_lab(DevProblem P, DevBatch B) {
+    constexpr int TS = D * D;
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<NS>(P, B, vb);
+    const int ns = P.nsec > 1 ? P.nsec : 1, e = blockIdx.z;
+    const bool fdx = e == P.ne;  // (workgroup-uniform)
+    const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);
+    const int xs = kWalkXRow ? 1 : L.nbe;
+    const LabBase lb = lab_base(P, e);
+    GaugeN<D> gn[NS];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) gn[w] = gauge_charges<D>(P, L.w0 + w);
+    const int k0 = L.c * P.L;
+    double xk = walk_load_x(1, xt + (size_t)min(k0, P.Nt - 1) * xs, xs).v0;
+    cd X[NS][D][D], Lm[NS][D][D];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) {
+        const size_t sub = (size_t)L.be * ns + L.w0 + w;
+        if (fdx) {  // F_dx[k] (sector part) = Re tr(M'_c Z1_k): X = M'_c
+            const cd *Mc = B.Mc + (sub * P.nchunks + L.c) * TS;
+#pragma unroll
+            for (int t = 0; t < TS; ++t) X[w][t / D][t % D] = Mc[t];
+        } else {  // X = M', L = T_c M' - M' T_c + M' Ttot (k_walk_err_grad's B)
+            const cd *Mo = B.Me + ((sub * P.ne + e) * P.nchunks + L.c) * 3 * TS;  // M', T_c, Ttot
+            cd Mp[TS], T1[TS], Bk[TS], T2[TS];
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                Mp[t] = Mo[t];
+                T1[t] = Mo[TS + t];
+            }
+            walk_mm<D>(T1, Mp, Bk);  // T_c M'
+            walk_mm<D>(Mp, T1, T2);  // M' T_c
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                Bk[t] = csub(Bk[t], T2[t]);
+                T1[t] = Mo[2 * TS + t];
+            }
+            walk_mm<D>(Mp, T1, T2);  // M' Ttot
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                Lm[w][t / D][t % D] = cadd(Bk[t], T2[t]);
+                X[w][t / D][t % D] = Mp[t];
+            }
+        }
+    }
+    {  // into the first step's frame: S~ = D_{k0}^dag S D_{k0}
+        const cd pc = cconj(gauge_cis(P.gauge_a * xk));
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            cd ep[kGaugePairs<D>];
+            gauge_phases<D>(pc, gn[w], ep);
+            lab_rotate<D>(ep, X[w]);
+            if (!fdx) lab_rotate<D>(ep, Lm[w]);
+        }
+    }
+    if (fdx) {
+#pragma unroll 1
+        for (int jj = 0; jj < P.L; ++jj) {
+            const int k = min(k0 + jj, P.Nt - 1);
+            const bool act = L.ok && k0 + jj < P.Nt;
+            const double xn = walk_load_x(1, xt + (size_t)min(k + 1, P.Nt - 1) * xs, xs).v0;
+            const cd q1 = cis_m1(P.gauge_a * ((xk + P.eps) - xk));
+            const cd om = gauge_cis(P.gauge_a * xk - P.gauge_a * xn);
+            xk = xn;
+            const LabBase lbs = lab_step(lb);
+#pragma unroll
+            for (int w = 0; w < NS; ++w) {
+                cd f1[kGaugePairs<D>], Y[D][D];
+                gauge_fd_weights_dn<D>(q1, gn[w], f1);
+                lab_mul_udag<D, false>(X[w], lbs.mat<D>(L.w0 + w, 0), Y);  // Y~ = X~ E~^dag
+                const double s = lab_trace_f<D>(Y, lbs.mat<D>(L.w0 + w, 0), f1);
+                lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), Y, X[w]);  // X~ = E~ Y~
+                cd ep[kGaugePairs<D>];
+                gauge_phases<D>(om, gn[w], ep);
+                lab_rotate<D>(ep, X[w]);
+                double *dst = act ? B.sec_part + ((((size_t)(L.w0 + w) * P.Nt) + k) * P.nvg) * L.nbe + L.be
+                                  : reinterpret_cast<double *>(B.sink);
+                *dst = s * P.inv_eps;
+            }
+        }
+        return;
+    }
+#pragma unroll 1
+    for (int jj = 0; jj < P.L; ++jj) {
+        const int k = min(k0 + jj, P.Nt - 1);
+        const bool act = L.ok && k0 + jj < P.Nt;
+        const double xn = walk_load_x(1, xt + (size_t)min(k + 1, P.Nt - 1) * xs, xs).v0;
+        const cd q1 = cis_m1(P.gauge_a * ((xk + P.eps) - xk)), q2 = cis_m1(P.gauge_a * ((xk + P.eps2) - xk));
+        const cd om = gauge_cis(P.gauge_a * xk - P.gauge_a * xn);
+        xk = xn;
+        const LabBase lbs = lab_step(lb);
+#pragma unroll
+        for (int w = 0; w < NS; ++w) {
+            cd Y[D][D], G[D][D];
+            lab_mul_udag<D, false>(X[w], lbs.mat<D>(L.w0 + w, 0), Y);  // Y~ = X~ E~^dag
+            double s2, s1;
+            {
+                cd f2[kGaugePairs<D>];
+                gauge_fd_weights_dn<D>(q2, gn[w], f2);
+                s2 = lab_trace_f<D>(Y, lbs.mat<D>(L.w0 + w, 2), f2);  // Re tr(Y~ (M_e o f2))
+            }
+            lab_sub_mul_u<D>(Y, lbs.mat<D>(L.w0 + w, 1), Lm[w]);        // L~ <- L~ - Y~ N_e (Lambda)
+            lab_mul_udag<D, false>(Lm[w], lbs.mat<D>(L.w0 + w, 0), G);  // G~ = L~ E~^dag
+            {
+                cd f1[kGaugePairs<D>];
+                gauge_fd_weights_dn<D>(q1, gn[w], f1);
+                s1 = lab_trace_f<D>(G, lbs.mat<D>(L.w0 + w, 0), f1);  // Re tr(G~ (E~ o f1))
+            }
+            lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), G, Lm[w]);  // L~ = E~ G~ + N_e Y~
+            lab_umul<D, true>(lbs.mat<D>(L.w0 + w, 1), Y, Lm[w]);
+            lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), Y, X[w]);  // X~ = E~ Y~
+            cd ep[kGaugePairs<D>];
+            gauge_phases<D>(om, gn[w], ep);  // into the next step's frame
+            lab_rotate<D>(ep, X[w]);
+            lab_rotate<D>(ep, Lm[w]);
+            double *dst = act ? B.sec_part_err +
+                                    (((((size_t)(L.w0 + w) * P.ne + e) * P.Nt + k) * P.nvg) * L.nbe + L.be)
+                              : reinterpret_cast<double *>(B.sink);
+            *dst = s1 * P.inv_eps + s2 * P.inv_eps2sq;
+        }
+    }
+}
+
 }  // namespace grape

@@ -25,6 +25,12 @@ constexpr int kWalkStoreMinD = GRAPE_WALK_STORE_MIN_D;
 #define GRAPE_WALK_XROW 1
 #endif
 constexpr bool kWalkXRow = GRAPE_WALK_XROW;
+// error sources on a phase-covariant class (round 6): the lab-frame walks k_walk_wsum_lab / k_walk_err_lab
+// (grape_walk.hpp; the engine's P.gauge_lab), no images.  0: the image walk and its back end (A/B)
+#ifndef GRAPE_WALK_ERR_LAB
+#define GRAPE_WALK_ERR_LAB 1
+#endif
+constexpr int kLabBaseMaxLanes = 256;  // k_gauge_err_base_fill: one lane per (sector, base matrix)
 }  // namespace grape
 
 namespace grape_walk {
@@ -33,7 +39,9 @@ namespace grape_walk {
 // error sources (P.ne > 0, nvg == 1): stage 0 = k_walk_img (chunk totals and the lane-minor
 // local-frame images to B.Zl), stage 1 = k_walk_img_sum (per-sector F_dx terms to B.sec_part,
 // lane-major, and the chunk sums of W to B.Wc), stage 2 = k_walk_err_grad (per-sector F_d2err_dx
-// terms to B.sec_part_err, lane-major)
+// terms to B.sec_part_err, lane-major).  Phase-covariant classes with error sources (P.gauge_lab): stage 0 =
+// k_walk_wsum_lab (chunk totals and the chunk sums of W to B.Wc), stage 1 = nothing, stage 2 =
+// k_walk_err_lab (F_dx and F_d2err_dx terms, lane-major), no images
 template <int D>
 hipError_t launch(int stage, const grape::DevProblem &P, const grape::DevBatch &B, hipStream_t st);
 // Latency-bound calls of the Rydberg layout -- class 0: one 4-level sector (permutation sectors) or
@@ -54,6 +62,9 @@ bool merged_ok(const grape::DevProblem &PA, const grape::DevProblem &PB);
 bool merged_writes_fdx();
 // E~ of the class's nsec sectors into out [nsec][D][D] (DevProblem::gauge_Et; scr: 2 D^2 complex per sector)
 hipError_t fill_gauge_base(const grape::DevProblem &P, int nsec, grape::cd *scr, grape::cd *out, hipStream_t st);
+// the lab-frame error walks' base table [nsec][1 + 2 ne][D][D] (DevProblem::gauge_Et with gauge_lab; scr: 2 D^2
+// complex per base matrix)
+hipError_t fill_gauge_err_base(const grape::DevProblem &P, int nsec, grape::cd *scr, grape::cd *out, hipStream_t st);
 hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::DevBatch &BA, const grape::DevProblem &PB,
                          const grape::DevBatch &BB, int a_first, hipStream_t st);
 // F_dx parts the class's gradient stage writes per evaluation: its sectors, or (k_walk_grad with several

@@ -13,6 +13,14 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
     const long lanes = (long)(B.nb / ns) * P.nchunks;
     const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
     const dim3 blk(grape::kWalkBlock);
+    if (P.ne > 0 && P.gauge_lab) {  // phase-covariant class with error sources: the lab-frame walks
+        if (stage == 0) {  // chunk totals and chunk sums of W, one lane per (chunk, evaluation, error)
+            hipLaunchKernelGGL((grape::k_walk_wsum_lab<D, NS>), dim3(grid.x, grid.y, (unsigned)P.ne), blk, 0, st, P, B);
+        } else if (stage == 2) {  // F_d2err_dx per error (blockIdx.z < ne) and F_dx (blockIdx.z = ne)
+            hipLaunchKernelGGL((grape::k_walk_err_lab<D, NS>), dim3(grid.x, grid.y, (unsigned)P.ne + 1), blk, 0, st, P, B);
+        }
+        return;
+    }
     if (P.ne > 0) {  // error sources: the image walk, then its back end (grape_walk.hpp)
         if (stage == 0) {
             if (P.gauge) hipLaunchKernelGGL((grape::k_walk_img_gauge<D, NS>), grid, blk, 0, st, P, B);
@@ -153,6 +161,17 @@ hipError_t fill_gauge_base(const grape::DevProblem &P, int nsec, grape::cd *scr,
         case 2: hipLaunchKernelGGL(grape::k_gauge_base_fill<2>, dim3(1), dim3(64), 0, st, P, scr, out, nsec); break;
         case 3: hipLaunchKernelGGL(grape::k_gauge_base_fill<3>, dim3(1), dim3(64), 0, st, P, scr, out, nsec); break;
         case 4: hipLaunchKernelGGL(grape::k_gauge_base_fill<4>, dim3(1), dim3(64), 0, st, P, scr, out, nsec); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+hipError_t fill_gauge_err_base(const grape::DevProblem &P, int nsec, grape::cd *scr, grape::cd *out, hipStream_t st) {
+    if (nsec < 1 || P.ne < 1 || nsec * (1 + 2 * P.ne) > grape::kLabBaseMaxLanes) return hipErrorInvalidValue;
+    const dim3 g(1), b(grape::kLabBaseMaxLanes);
+    switch (P.D) {
+        case 2: hipLaunchKernelGGL(grape::k_gauge_err_base_fill<2>, g, b, 0, st, P, scr, out, nsec); break;
+        case 3: hipLaunchKernelGGL(grape::k_gauge_err_base_fill<3>, g, b, 0, st, P, scr, out, nsec); break;
+        case 4: hipLaunchKernelGGL(grape::k_gauge_err_base_fill<4>, g, b, 0, st, P, scr, out, nsec); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
