@@ -2774,7 +2774,7 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
 #define GRAPE_WALK_ERR_LAB_WAVES 2
 #endif
 #ifndef GRAPE_WALK_ERR_LAB4_WAVES  // k_walk_err_lab<4>: four 4 x 4 complex matrices live (256 VGPRs) at the peak
-#define GRAPE_WALK_ERR_LAB4_WAVES 1
+#define GRAPE_WALK_ERR_LAB4_WAVES 2
 #endif
 template <int D>
 constexpr int err_lab_waves() { return D >= 4 ? GRAPE_WALK_ERR_LAB4_WAVES : GRAPE_WALK_ERR_LAB_WAVES; }
@@ -2814,10 +2814,14 @@ __global__ __launch_bounds__(kLabBaseMaxLanes) void k_gauge_err_base_fill(DevPro
 }
 // The base table through scalar loads: every operand is uniform over a workgroup (sector group blockIdx.y,
 // error e = blockIdx.z), so each entry is an SGPR operand of the FMAs -- no VGPRs, no LDS instructions.  A
-// matrix is read row by row, each row's pointer tied (an empty asm with a register input) to a result two
-// rows back, so at most two rows (32 SGPRs at D = 4) are in flight: unchained, the scheduler issues every
-// load of a step at its top (LDS copies measured 190+ VGPRs of preloaded operands at D = 4, scalar loads
-// 128-198 SGPRs, spilled).
+// uniform matrix is consumed one row at a time: row r + 1's loads are issued with row r's FMAs and a
+// scheduling barrier closes each row, so at most two rows (32 SGPRs at D = 4) are live.  Without the
+// barriers the scheduler interleaves the rows of a product and the loaded rows spill to VGPR lanes
+// (~700 v_writelane / v_readlane per step at D = 4: 39 % of the VALU instructions were not FP64); LDS
+// copies instead cost 190+ VGPRs of preloaded operands.
+#ifndef GRAPE_WALK_LAB_SEG
+#define GRAPE_WALK_LAB_SEG 1
+#endif
 struct LabBase {
     cptr<cd> g;  // the class's table
     int nb, ne, e;
@@ -2835,77 +2839,116 @@ __device__ __forceinline__ LabBase lab_base(const DevProblem &P, int e) {
     b.g = as_constant(P.gauge_Et);
     return b;
 }
-// the table pointer made opaque once per step: the row addresses are then formed in the step (a few scalar
-// adds) instead of being hoisted out of the loop as ~40 loop-invariant 64-bit SGPR values (spilled to VGPR lanes)
+// the table pointer made opaque once per step: the row addresses are formed in the step (a few scalar adds)
+// instead of being hoisted out of the loop as loop-invariant 64-bit SGPR values
 __device__ __forceinline__ LabBase lab_step(LabBase b) {
     asm volatile("" : "+s"(b.g));
     return b;
 }
+__device__ __forceinline__ void lab_seg() {
+#if GRAPE_WALK_LAB_SEG
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+// row r of U through an opaque pointer tied to `dep` (an empty asm with a register input): neither the asm nor
+// the loads can move above the instruction that produced dep
+// the row's results pinned where the row ends (an empty asm that reads and rewrites them): instruction
+// selection otherwise sinks a row's FMAs towards their later uses, past the barrier, and the row's SGPRs
+// stay live (spilled to VGPR lanes) until then
+__device__ __forceinline__ void lab_pin(cd &v) { asm volatile("" : "+v"(v.re), "+v"(v.im)); }
 template <int D>
-__device__ __forceinline__ cptr<cd> lab_row(cptr<cd> U, int r, double dep) {
-    cptr<cd> p = U + r * D;
+__device__ __forceinline__ void lab_row(cptr<cd> U, int r, double dep, cd (&v)[D]) {
+    cptr<cd> p = U;  // (the row offset is the loads' immediate: no per-row address to hoist out of the walk)
     asm volatile("" : "+s"(p) : "v"(dep));
-    return p;
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = cload(p, r * D + j);
+}
+// Row-wise consumption of a uniform matrix U: d_r = body(r, row r of U) (a result of the row), row r + 1 loaded
+// after row r - 1's result exists and consumed after a scheduling barrier: two rows live at most
+#ifndef GRAPE_WALK_LAB_PREFETCH  // row r + 1's loads issued with row r's FMAs
+#define GRAPE_WALK_LAB_PREFETCH 1
+#endif
+template <int D, class Body>
+__device__ __forceinline__ void lab_rows(cptr<cd> U, double dep0, Body &&body) {
+    cd cur[D], nxt[D];
+    lab_row<D>(U, 0, dep0, cur);
+    double dprev = dep0;
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        if (GRAPE_WALK_LAB_PREFETCH && r + 1 < D) lab_row<D>(U, r + 1, dprev, nxt);
+        const double d = body(r, cur);
+        lab_seg();
+        if (r + 1 < D) {
+            if (!GRAPE_WALK_LAB_PREFETCH) lab_row<D>(U, r + 1, d, nxt);
+#pragma unroll
+            for (int j = 0; j < D; ++j) cur[j] = nxt[j];
+        }
+        dprev = d;
+    }
 }
 // C (+)= A U^dag, U uniform: row c of U gives column c of C
 template <int D, bool ACC>
 __device__ __forceinline__ void lab_mul_udag(const cd (&A)[D][D], cptr<cd> U, cd (&C)[D][D]) {
-#pragma unroll
-    for (int c = 0; c < D; ++c) {
-        const cptr<cd> row = lab_row<D>(U, c, c >= 2 ? C[0][c - 2].re : A[0][0].re);
+    lab_rows<D>(U, A[0][0].re, [&](int c, const cd (&u)[D]) {
 #pragma unroll
         for (int m = 0; m < D; ++m) {
-            const cd u = cconj(cload(row, m));
+            const cd uc = cconj(u[m]);
 #pragma unroll
             for (int r = 0; r < D; ++r) {
-                if (!ACC && m == 0) C[r][c] = cmul(A[r][m], u);
-                else cmac(C[r][c], A[r][m], u);
+                if (!ACC && m == 0) C[r][c] = cmulf(A[r][m], uc);
+                else cmac(C[r][c], A[r][m], uc);
             }
         }
-    }
+#pragma unroll
+        for (int r = 0; r < D; ++r) lab_pin(C[r][c]);
+        return C[D - 1][c].re;
+    });
 }
 // C (+)= U A, U uniform: row r of U gives row r of C
 template <int D, bool ACC>
 __device__ __forceinline__ void lab_umul(cptr<cd> U, const cd (&A)[D][D], cd (&C)[D][D]) {
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-        const cptr<cd> row = lab_row<D>(U, r, r >= 2 ? C[r - 2][0].re : A[0][0].re);
+    lab_rows<D>(U, A[D - 1][D - 1].re, [&](int r, const cd (&u)[D]) {
 #pragma unroll
         for (int m = 0; m < D; ++m) {
-            const cd u = cload(row, m);
 #pragma unroll
             for (int c = 0; c < D; ++c) {
-                if (!ACC && m == 0) C[r][c] = cmul(u, A[m][c]);
-                else cmac(C[r][c], u, A[m][c]);
+                if (!ACC && m == 0) C[r][c] = cmulf(u[m], A[m][c]);
+                else cmac(C[r][c], u[m], A[m][c]);
             }
         }
-    }
+#pragma unroll
+        for (int c = 0; c < D; ++c) lab_pin(C[r][c]);
+        return C[r][D - 1].re;
+    });
 }
 // C -= A U, U uniform: row m of U updates every entry of C
 template <int D>
 __device__ __forceinline__ void lab_sub_mul_u(const cd (&A)[D][D], cptr<cd> U, cd (&C)[D][D]) {
-    double dep[D];
-#pragma unroll
-    for (int m = 0; m < D; ++m) {
-        const cptr<cd> row = lab_row<D>(U, m, m >= 2 ? dep[m - 2] : A[0][0].re);
+    lab_rows<D>(U, A[D - 1][D - 1].re, [&](int m, const cd (&u)[D]) {
 #pragma unroll
         for (int c = 0; c < D; ++c) {
-            const cd u = cload(row, c);
 #pragma unroll
-            for (int r = 0; r < D; ++r) cmac(C[r][c], cmake(-A[r][m].re, -A[r][m].im), u);
+            for (int r = 0; r < D; ++r) cmac(C[r][c], cmake(-A[r][m].re, -A[r][m].im), u[c]);
         }
-        dep[m] = C[D - 1][D - 1].re;
-    }
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+#pragma unroll
+            for (int r = 0; r < D; ++r) lab_pin(C[r][c]);
+        }
+        return C[D - 1][D - 1].re;
+    });
 }
 // C += U element-wise, U uniform
 template <int D>
 __device__ __forceinline__ void lab_add_u(cptr<cd> U, cd (&C)[D][D]) {
+    lab_rows<D>(U, C[D - 1][D - 1].re, [&](int r, const cd (&u)[D]) {
 #pragma unroll
-    for (int r = 0; r < D; ++r) {
-        const cptr<cd> row = lab_row<D>(U, r, r >= 2 ? C[r - 2][0].re : C[0][0].re);
-#pragma unroll
-        for (int c = 0; c < D; ++c) C[r][c] = cadd(C[r][c], cload(row, c));
-    }
+        for (int c = 0; c < D; ++c) {
+            C[r][c] = cadd(C[r][c], u[c]);
+            lab_pin(C[r][c]);
+        }
+        return C[r][D - 1].re;
+    });
 }
 // S <- Om S Om^dag: S_ij e_ij with the pair phases e of Om (e_ji = conj(e_ij), the diagonal unchanged)
 template <int D>
@@ -2913,25 +2956,26 @@ __device__ __forceinline__ void lab_rotate(const cd (&e)[kGaugePairs<D>], cd (&S
 #pragma unroll
     for (int i = 0; i < D; ++i) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) S[i][j] = gauge_sandwich<D>(e, i, j, S[i][j]);
+        for (int j = 0; j < D; ++j) {
+            if (i != j) S[i][j] = cmulf(S[i][j], i < j ? e[gauge_pair(D, i, j)] : cconj(e[gauge_pair(D, j, i)]));
+        }
     }
 }
 // sum_{r != j} Re(Y_jr (U o f)_rj): the trace of Y against a uniform matrix with the difference weights
 template <int D>
 __device__ __forceinline__ double lab_trace_f(const cd (&Y)[D][D], cptr<cd> U, const cd (&f)[kGaugePairs<D>]) {
-    double s = 0.0, dep[D];
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-        const cptr<cd> row = lab_row<D>(U, r, r >= 2 ? dep[r - 2] : Y[0][0].re);
+    double s = 0.0;
+    lab_rows<D>(U, Y[D - 1][D - 1].re, [&](int r, const cd (&u)[D]) {
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             if (r == j) continue;
-            const cd d = cmul(cload(row, j), gauge_fd_weight<D>(f, r, j));
+            const cd d = cmulf(u[j], gauge_fd_weight<D>(f, r, j));
             s = fma(Y[j][r].re, d.re, s);
             s = fma(-Y[j][r].im, d.im, s);
         }
-        dep[r] = s;
-    }
+        asm volatile("" : "+v"(s));
+        return s;
+    });
     return s;
 }
 
@@ -2989,7 +3033,7 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_WSUM_LAB_WAVES) void k_walk_
 #pragma unroll
             for (int j = 0; j < D; ++j) {
 #pragma unroll
-                for (int i = 0; i < D; ++i) Q[w][j][i] = cmul(dl[j], T[j][i]);
+                for (int i = 0; i < D; ++i) Q[w][j][i] = cmulf(dl[j], T[j][i]);
             }
         }
     };

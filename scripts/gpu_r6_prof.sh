@@ -18,6 +18,10 @@ for leg in ${LEGS:-mix arcz c4opt}; do
           -d $OUT/${TAG}_c2 -o run -- python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-paths \
           --no-whole-matrix --no-c4-strong > $OUT/${TAG}_c2.log 2>&1); rc=$?; echo "c2 stats rc=$rc"
           faulted $OUT/${TAG}_c2.log && exit 99; [ $rc -ne 0 ] && exit $rc; prune $OUT/${TAG}_c2 ;;
+    c3stats) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d $OUT/${TAG}_c3 -o run -- python3 $ROOT/bench.py --workload c3 --steps 6 --warmup 2 --no-cpu-baseline --no-host-paths > $OUT/${TAG}_c3.log 2>&1)
+          rc=$?; echo "c3 stats rc=$rc"; faulted $OUT/${TAG}_c3.log && exit 99; [ $rc -ne 0 ] && exit $rc; prune $OUT/${TAG}_c3 ;;
+    c3mix) BATCH=8192 BENCH_EXTRA="--workload c3" bash scripts/gpu_pmc_mix.sh ${TAG}_c3mix || exit $?; for d in $OUT/${TAG}_c3mix_p*; do prune $d; done ;;
     arcz) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d $OUT/${TAG}_arcz -o run -- python3 $ROOT/bench.py --workload arcz --no-cpu-baseline > $OUT/${TAG}_arcz.log 2>&1)
           rc=$?; echo "arcz rc=$rc"; faulted $OUT/${TAG}_arcz.log && exit 99; [ $rc -ne 0 ] && exit $rc; prune $OUT/${TAG}_arcz ;;
