@@ -23,11 +23,11 @@
 // computes its own two tiles of P.
 //
 // LDS matrices (SM) are two row-major 64 x 64 double planes with the column
-// swizzle  col ^ (((row & 15) << 1) ^ ((row & 1) << 4)):  C-tile stores
-// (16 contiguous columns of one row per 16 lanes), A-fragment reads of L and
-// of L^T, and B-fragment reads of R and R^T are all bank-conflict free
-// (gfx950 ds_read_b64: two 32-lane groups over 64 banks; ds_write_b64: four
-// 16-lane groups over 32 banks).
+// swizzle  col ^ swz64(row) (below):  C-tile stores (16 contiguous columns of
+// one row per 16 lanes), A-fragment reads of L and of L^T, and B-fragment reads
+// of R and R^T are all bank-conflict free, as ds_read_b64 (two 32-lane groups
+// over 64 banks) and as ds_read2st64_b64 / ds_write_b64 (four 16-lane groups
+// over 32 banks).
 //
 // HBM images: a complex matrix is stored as its register file, plane by plane
 // (re then im), index ((w*4 + t)*4 + r)*64 + lane: a wave loads or stores its
@@ -92,11 +92,26 @@ __device__ __forceinline__ SM sm_at(double *lds, int off) {
     return s;
 }
 
-__device__ __forceinline__ int sidx(int row, int col) {
-    return row * N + (col ^ (((row & 15) << 1) ^ ((row & 1) << 4)));
+// The swizzle f(row) = (row & 15) | (row & 1) << 4: its low four bits and its bits 4..1 are both
+// permutations of row & 15, and bit 4 alternates with the row parity.  So the fragment reads are
+// conflict free both as ds_read_b64 (two 32-lane groups over 64 banks: needs bits 4..1 distinct over 16 rows
+// and bit 4 split between rows 2k, 2k + 1) and as the ds_read2st64_b64 the compiler forms from the re / im
+// plane pair (four 16-lane groups over 32 banks: needs the low four bits distinct over 16 rows).  Round 6:
+// the round-2 swizzle ((row & 15) << 1) ^ ((row & 1) << 4) met only the first -- the A-fragment reads of L
+// and the B-fragment reads of R^T were 2-way conflicted as ds_read2st64_b64 (C5's LDS conflict
+// cycles above its LDS-active cycles).  Checked exhaustively for every access pattern below by
+// scripts/probes/lds_banks.py.
+#ifndef GRAPE_DENSE_SWZ_R2  // 1: the round-2 swizzles (A/B)
+#define GRAPE_DENSE_SWZ_R2 0
+#endif
+__device__ __forceinline__ int swz64(int row) {
+    if (GRAPE_DENSE_SWZ_R2) return ((row & 15) << 1) ^ ((row & 1) << 4);
+    return (row & 15) | ((row & 1) << 4);
 }
-// 64 x 16 / 16 x 16 buffers read as A fragments: conflict-free with this swizzle
-__device__ __forceinline__ int sidx16(int row, int col) { return row * 16 + (col ^ (row & 14)); }
+__device__ __forceinline__ int sidx(int row, int col) { return row * N + (col ^ swz64(row)); }
+// 64 x 16 / 16 x 16 buffers read as A fragments: conflict-free in both models with this swizzle (round 2:
+// row & 14, 2-way in the 16-lane one)
+__device__ __forceinline__ int sidx16(int row, int col) { return row * 16 + (col ^ (row & (GRAPE_DENSE_SWZ_R2 ? 14 : 15))); }
 
 __device__ __forceinline__ v4d mfma(double a, double b, v4d c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);

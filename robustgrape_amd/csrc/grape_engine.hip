@@ -79,6 +79,16 @@ constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
 #ifndef GRAPE_GAUGE_CHUNK_DIV
 #define GRAPE_GAUGE_CHUNK_DIV 2
 #endif
+// chunks per evaluation of the lab-frame error walks on throughput passes (0: the walks' formula, 8 and 16 at
+// C3).  C3 (A/B in one GPU call, profiles/r06/c3): 4-level class 8 -> 6 chunks 2.64 -> 2.68 M evals/s (12:
+// 2.49 M), 2-level class 16 -> 8 chunks 2.64 -> 2.69 M -- fewer lanes, whole waves per SIMD round, and
+// shorter error scans
+#ifndef GRAPE_LAB_CHUNKS4  // classes of 4 levels
+#define GRAPE_LAB_CHUNKS4 6
+#endif
+#ifndef GRAPE_LAB_CHUNKS2  // ... of fewer levels
+#define GRAPE_LAB_CHUNKS2 8
+#endif
 #ifndef GRAPE_GAUGE_CHUNK_DIV2  // ... for the 2-level classes (A/B knob)
 #define GRAPE_GAUGE_CHUNK_DIV2 GRAPE_GAUGE_CHUNK_DIV
 #endif
@@ -1580,6 +1590,11 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
             int ncs = std::max(1, std::min(Ps.scan_waves * (64 / S) / cdiv, P.Nt));
             if (Ps.gauge && Ps.scan_waves == kScanTiny && S == 3 && P.ne == 0)
                 ncs = merged_chunk_count((long)MB, P.Nt, ncs, ncu);
+            // the lab-frame error walks' throughput chunking (A/B knobs; 0: the formula above)
+            if (Ps.gauge_lab && Ps.scan_waves == kScanTiny) {
+                const int lc = S >= 4 ? GRAPE_LAB_CHUNKS4 : GRAPE_LAB_CHUNKS2;
+                if (lc > 0) ncs = std::max(1, std::min(lc, P.Nt));
+            }
             Ps.L = (P.Nt + ncs - 1) / ncs;
             Ps.nchunks = (P.Nt + Ps.L - 1) / Ps.L;
             grape_plan::SecBuf &b = p->sb[cl];

@@ -67,17 +67,21 @@ __global__ __launch_bounds__(64 * W) void k_err_scan(DevProblem P, DevBatch B) {
             }
         }
     }
-    // Phase A': Vc_c = Carry_c^dag (sum W) Carry_c  -> own tile
-    const cd *Cr = B.Carry + ((size_t)b * P.nchunks + (gvalid ? c : 0)) * TILE;
+    // Phase A': Vc_c = Carry_c^dag (sum W) Carry_c  -> own tile.  The lab-frame walks (P.gauge_lab,
+    // grape_walk.hpp k_walk_wsum_lab) hand over R = T_c (sum W) T_c^dag: Vc_c = Carry_{c+1}^dag R Carry_{c+1}
+    // (Carry_{c+1} = T_c Carry_c; past the last chunk, U)
+    const int cc = gvalid ? c : 0;
+    const cd *Cr = B.Carry + ((size_t)b * P.nchunks + cc) * TILE;
+    const cd *Ca = (P.gauge_lab && B.Wc) ? (cc + 1 < P.nchunks ? Cr + TILE : B.Ub + (size_t)b * TILE) : Cr;
     tile_store_row(G, acc, gvalid);
     gsync();
 #pragma unroll
-    for (int r = 0; r < D; ++r) x[r] = cconj(Cr[r * D + i]);
+    for (int r = 0; r < D; ++r) x[r] = cconj(Ca[r * D + i]);
     mm_tile<D>(x, G.tile, w);
     gsync();
     if (gvalid) {
 #pragma unroll
-        for (int jj = 0; jj < D; ++jj) G.tile[i * D + jj] = Cr[i * D + jj];
+        for (int jj = 0; jj < D; ++jj) G.tile[i * D + jj] = Ca[i * D + jj];
     }
     gsync();
     mm_tile<D>(w, G.tile, acc);

@@ -2743,10 +2743,10 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
 // alone.  So both ends carry transported states and no image is formed or stored:
 //
 // stage 0, k_walk_wsum_lab -- one lane per (chunk, evaluation, error e):
-//     R <- (E R + dW_e) E^dag,  Q <- E Q
-//   R = Q (sum_{j<k} W_j) Q^dag and dW_e = (E(err_e eps) - E) / eps = E w_e; at the chunk end
-//   W_c = Q^dag R Q -- k_err_scan's chunk sum of the W images (UnitaryCalculations.jl:111-112) -- and, for
-//   e = 0, the chunk total T_c = Q.
+//     R <- (E R + dW_e) E^dag
+//   R = Q (sum_{j<k} W_j) Q^dag and dW_e = (E(err_e eps) - E) / eps = E w_e; at the chunk end R = T_c W_c T_c^dag,
+//   the chunk sum of the W images (UnitaryCalculations.jl:111-112) in the lab frame, which k_err_scan maps
+//   with Carry_{c+1} = T_c Carry_c; lanes e = ne walk Q <- E Q for the chunk total T_c.
 // stage 2, k_walk_err_lab -- one lane per (chunk, evaluation, error e); the lanes of e = ne take F_dx:
 //   X = M'_{c,e}, L = B_c = T_c M' - M' T_c + M' Ttot (k_walk_err_grad's chunk start), then per step
 //     Y = X E^dag,  L <- L - Y dW  (= Lambda_k),  G = L E^dag,
@@ -2764,7 +2764,7 @@ __global__ __launch_bounds__(kWalkBlock, (D >= 4 ? 1 : 2)) void k_walk_err_grad(
 // then has an x-independent, workgroup-uniform factor (E~ or N_e: LDS broadcasts, no per-lane propagator),
 // the traces take E~ o f1 and M_e o f2, and moving to the next step's frame is an element-wise phase,
 // S~ <- Om S~ Om^dag with Om = D_{k+1}^dag D_k (pair phases of e^{i a (x_k - x_{k+1})}).  The forward lane
-// carries Q^ = D_{k+1}^dag Q (Q^ <- Om E~ Q^) and R~; the D factors cancel in W_c = Q^dag R Q = Q^^dag R~ Q^.
+// carries Q^ = D_{k+1}^dag Q (Q^ <- Om E~ Q^) or R~, and the chunk end maps back with D_next.
 // Six D x D products per step and error (k_walk_err_grad: two, plus 9 image reads; the image walk: two
 // per image), the live state three matrices (two waves per SIMD at D = 4).
 #ifndef GRAPE_WALK_WSUM_LAB_WAVES
@@ -2979,12 +2979,16 @@ __device__ __forceinline__ double lab_trace_f(const cd (&Y)[D][D], cptr<cd> U, c
     return s;
 }
 
+// stage 0: lanes of blockIdx.z = e < ne carry R~ only and write R at the chunk end in the lab frame,
+// R = T_c (sum_k W_k) T_c^dag (k_err_scan's Phase A' then takes Carry_{c+1} = T_c Carry_c in place of Carry_c:
+// Carry_{c+1}^dag R Carry_{c+1} = Carry_c^dag (sum W) Carry_c); the lanes of blockIdx.z = ne walk Q^ for T_c
 template <int D, int NS>
 __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_WSUM_LAB_WAVES) void k_walk_wsum_lab(DevProblem P, DevBatch B) {
     constexpr int TS = D * D;
     const VBlock vb = hw_block();
     const WalkLane L = walk_lane<NS>(P, B, vb);
     const int ns = P.nsec > 1 ? P.nsec : 1, e = blockIdx.z;
+    const bool tc = e == P.ne;  // (workgroup-uniform)
     const double *xt = B.xT + (size_t)L.be * (kWalkXRow ? P.nx : 1);
     const int xs = kWalkXRow ? 1 : L.nbe;
     const LabBase lb = lab_base(P, e);
@@ -2994,19 +2998,16 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_WSUM_LAB_WAVES) void k_walk_
     const int k0 = L.c * P.L;
     double xk = walk_load_x(1, xt + (size_t)min(k0, P.Nt - 1) * xs, xs).v0;
     // Q^ = D_{k0}^dag (Q = I at the chunk start), R~ = 0
-    cd Q[NS][D][D], R[NS][D][D];
+    cd S[NS][D][D];
     {
         const cd pc = cconj(gauge_cis(P.gauge_a * xk));
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
 #pragma unroll
             for (int j = 0; j < D; ++j) {
-                const cd dj = gauge_pow(pc, gn[w].n[j]);
+                const cd dj = tc ? gauge_pow(pc, gn[w].n[j]) : czero();
 #pragma unroll
-                for (int i = 0; i < D; ++i) {
-                    Q[w][j][i] = i == j ? dj : czero();
-                    R[w][j][i] = czero();
-                }
+                for (int i = 0; i < D; ++i) S[w][j][i] = i == j ? dj : czero();
             }
         }
     }
@@ -3020,24 +3021,25 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_WSUM_LAB_WAVES) void k_walk_
 #pragma unroll
         for (int w = 0; w < NS; ++w) {
             cd T[D][D];
-            lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), R[w], T);  // T = E~ R~ + N_e
-            lab_add_u<D>(lbs.mat<D>(L.w0 + w, 1), T);
-            lab_mul_udag<D, false>(T, lbs.mat<D>(L.w0 + w, 0), R[w]);  // R~ = T E~^dag
-            lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), Q[w], T);      // T = E~ Q^
-            cd ep[kGaugePairs<D>];
-            gauge_phases<D>(om, gn[w], ep);
-            lab_rotate<D>(ep, R[w]);
-            cd dl[D];  // Om's level phases om^{N_j}: Q^ <- Om T (rows)
+            if (tc) {
+                lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), S[w], T);  // T = E~ Q^, Q^ <- Om T (rows: om^{N_j})
 #pragma unroll
-            for (int j = 0; j < D; ++j) dl[j] = gauge_pow(om, gn[w].n[j]);
+                for (int j = 0; j < D; ++j) {
+                    const cd dl = gauge_pow(om, gn[w].n[j]);
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
-#pragma unroll
-                for (int i = 0; i < D; ++i) Q[w][j][i] = cmulf(dl[j], T[j][i]);
+                    for (int i = 0; i < D; ++i) S[w][j][i] = cmulf(dl, T[j][i]);
+                }
+            } else {
+                lab_umul<D, false>(lbs.mat<D>(L.w0 + w, 0), S[w], T);  // T = E~ R~ + N_e
+                lab_add_u<D>(lbs.mat<D>(L.w0 + w, 1), T);
+                lab_mul_udag<D, false>(T, lbs.mat<D>(L.w0 + w, 0), S[w]);  // R~ = T E~^dag
+                cd ep[kGaugePairs<D>];
+                gauge_phases<D>(om, gn[w], ep);
+                lab_rotate<D>(ep, S[w]);
             }
         }
     };
-    // steps past N_t leave Q^ and R~ alone: only the last chunk has them
+    // steps past N_t leave the state alone: only the last chunk has them
     const int nlast = P.Nt - (P.nchunks - 1) * P.L;
     int j = 0;
 #pragma unroll 1
@@ -3047,39 +3049,27 @@ __global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_WSUM_LAB_WAVES) void k_walk_
         if (L.c != P.nchunks - 1) step(j);
     }
     if (!L.ok) return;
-    const cd pn = gauge_cis(P.gauge_a * xnext);  // Q = D_next Q^ (the frame of the last rotation)
+    const cd pn = gauge_cis(P.gauge_a * xnext);  // D_next: the frame of the last rotation
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
         const size_t sub = (size_t)L.be * ns + L.w0 + w;
-        cd T[D][D];
-#pragma unroll
-        for (int r = 0; r < D; ++r) {  // T = R~ Q^
-#pragma unroll
-            for (int c = 0; c < D; ++c) {
-                cd s = czero();
-#pragma unroll
-                for (int m = 0; m < D; ++m) cmac(s, R[w][r][m], Q[w][m][c]);
-                T[r][c] = s;
-            }
-        }
-        cd *dw = B.Wc + ((sub * P.ne + e) * P.nchunks + L.c) * TS;  // W_c = Q^^dag T, row-major
-#pragma unroll
-        for (int r = 0; r < D; ++r) {
-#pragma unroll
-            for (int c = 0; c < D; ++c) {
-                cd s = czero();
-#pragma unroll
-                for (int m = 0; m < D; ++m) cmac(s, cconj(Q[w][m][r]), T[m][c]);
-                dw[r * D + c] = s;
-            }
-        }
-        if (e == 0) {  // the chunk total (k_walk_img_gauge's layout)
+        if (tc) {  // T_c = D_next Q^ (k_walk_img_gauge's layout)
             cd *dst = B.Tc + (sub * P.nchunks + L.c) * TS;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
                 const cd dr = gauge_pow(pn, gn[w].n[r]);
 #pragma unroll
-                for (int c = 0; c < D; ++c) dst[r * D + c] = cmul(dr, Q[w][r][c]);
+                for (int c = 0; c < D; ++c) dst[r * D + c] = cmul(dr, S[w][r][c]);
+            }
+        } else {  // R = D_next R~ D_next^dag, row-major
+            cd ep[kGaugePairs<D>];
+            gauge_phases<D>(pn, gn[w], ep);
+            lab_rotate<D>(ep, S[w]);
+            cd *dw = B.Wc + ((sub * P.ne + e) * P.nchunks + L.c) * TS;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+#pragma unroll
+                for (int c = 0; c < D; ++c) dw[r * D + c] = S[w][r][c];
             }
         }
     }

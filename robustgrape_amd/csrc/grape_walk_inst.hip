@@ -14,8 +14,8 @@ void launch_ns(int stage, const grape::DevProblem &P, const grape::DevBatch &B, 
     const dim3 grid((unsigned)((lanes + grape::kWalkBlock - 1) / grape::kWalkBlock), (unsigned)(ns / NS));
     const dim3 blk(grape::kWalkBlock);
     if (P.ne > 0 && P.gauge_lab) {  // phase-covariant class with error sources: the lab-frame walks
-        if (stage == 0) {  // chunk totals and chunk sums of W, one lane per (chunk, evaluation, error)
-            hipLaunchKernelGGL((grape::k_walk_wsum_lab<D, NS>), dim3(grid.x, grid.y, (unsigned)P.ne), blk, 0, st, P, B);
+        if (stage == 0) {  // chunk sums of W per error (blockIdx.z < ne) and chunk totals (blockIdx.z = ne)
+            hipLaunchKernelGGL((grape::k_walk_wsum_lab<D, NS>), dim3(grid.x, grid.y, (unsigned)P.ne + 1), blk, 0, st, P, B);
         } else if (stage == 2) {  // F_d2err_dx per error (blockIdx.z < ne) and F_dx (blockIdx.z = ne)
             hipLaunchKernelGGL((grape::k_walk_err_lab<D, NS>), dim3(grid.x, grid.y, (unsigned)P.ne + 1), blk, 0, st, P, B);
         }

@@ -31,6 +31,8 @@ for v in "$@"; do
       arcz) run $v arcz 200 --workload arcz --no-cpu-baseline ;;
       c3) run $v c3 300 --workload c3 --steps 10 --warmup 2 --no-cpu-baseline ;;
       c4opt) run $v c4opt 300 --workload c4opt --steps 20 --warmup 5 ;;
+      c5) run $v c5 300 --workload c5 --steps 30 --warmup 3 --no-cpu-baseline --no-host-paths ;;
+      c5err) run $v c5err 300 --workload c5err --steps 10 --warmup 2 --no-cpu-baseline --no-host-paths ;;
       c4optw0) run $v c4optw0 300 --workload c4opt --steps 20 --warmup 5 --scan-waves 0 ;;
       c2k2) run $v c2k2 300 --chunk 2048 --batch 65536 --steps 20 --warmup 3 --no-cpu-baseline --no-host-paths --no-whole-matrix --no-c4-strong ;;
       c2k1) run $v c2k1 300 --chunk 1024 --batch 65536 --steps 20 --warmup 3 --no-cpu-baseline --no-host-paths --no-whole-matrix --no-c4-strong ;;
