@@ -83,6 +83,12 @@ constexpr bool kScanPairAll = GRAPE_SCAN_PAIR_ALL;
 // C3).  C3 (A/B in one GPU call, profiles/r06/c3): 4-level class 8 -> 6 chunks 2.64 -> 2.68 M evals/s (12:
 // 2.49 M), 2-level class 16 -> 8 chunks 2.64 -> 2.69 M -- fewer lanes, whole waves per SIMD round, and
 // shorter error scans
+// latency-bound calls of the lab-frame error walks on the 16-wave scans (256 chunks of the 4-level class at
+// C3): measured slower, single C3 evaluation 0.169 -> 0.176 ms (A/B in one GPU call: the longer error scans
+// cost more than the shorter walks save), so off
+#ifndef GRAPE_LAB_LATENCY_SCAN
+#define GRAPE_LAB_LATENCY_SCAN 0
+#endif
 #ifndef GRAPE_LAB_CHUNKS4  // classes of 4 levels
 #define GRAPE_LAB_CHUNKS4 6
 #endif
@@ -1581,7 +1587,8 @@ int grape_plan_create(const grape_desc *desc, int device, grape_plan **out) {
                               !(P.opts & GRAPE_OPT_WALK_RECOMPUTE) ? 1 : 0;
             // latency-bound walk classes (fewer sub-evaluations than CUs, or the option): 16-wave scans,
             // half-length walks (grape_launch.hpp kScanLatency)
-            if (Ps.walk && P.ne == 0 &&
+            // (GRAPE_LAB_LATENCY_SCAN: the lab-frame error walks too)
+            if (Ps.walk && (P.ne == 0 || (Ps.gauge_lab && GRAPE_LAB_LATENCY_SCAN)) &&
                 (scan_override == kScanLatency || (scan_override == 0 && (long)R < (long)ncu)))
                 Ps.scan_waves = kScanLatency;
             // phase-covariant throughput classes: a step costs a few products instead of an

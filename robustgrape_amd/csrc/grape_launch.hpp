@@ -121,6 +121,13 @@ hipError_t launch_scan_pair(const DevProblem &P0, const DevBatch &B0, const DevP
 }
 template <int D>
 void launch_err_scan(const DevProblem &P, const DevBatch &B, hipStream_t st) {
+    if constexpr (D <= grape::kWalkMaxD) {
+        if (P.scan_waves == kScanLatency) {  // (the lab-frame error walks' latency-bound calls)
+            hipLaunchKernelGGL((grape::k_err_scan<D, kScanLatency>), dim3(B.nb * P.ne), dim3(64 * kScanLatency),
+                               errscan_lds<D>(kScanLatency), st, P, B);
+            return;
+        }
+    }
     if (P.scan_waves == kScanTiny)
         hipLaunchKernelGGL((grape::k_err_scan<D, kScanTiny>), dim3(B.nb * P.ne), dim3(64 * kScanTiny),
                            errscan_lds<D>(kScanTiny), st, P, B);
@@ -246,7 +253,7 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
                 return hipGetLastError();
             }
             if (stage == 1) {
-                if (P.ne > 0) {  // k_walk_img_sum reads M'_c (k_walk_grad forms it in the lane)
+                if (P.ne > 0 && !P.gauge_lab) {  // k_walk_img_sum reads M'_c (k_walk_grad / k_walk_err_lab form it in the lane)
                     mark(GRAPE_KERNEL_REDUCE, 0);
                     const long nmc = (long)B.nb * P.nchunks * D * D;
                     hipLaunchKernelGGL(grape::k_sec_mc<D>, dim3((unsigned)((nmc + 255) / 256)), dim3(256), 0, st, P, B);
@@ -268,7 +275,8 @@ hipError_t launch_sector_stage(int stage, const DevProblem &P, const DevBatch &B
             // stage 2 with error sources: M'_{c,e}, then the F_d2err_dx walks over the lane-minor images
             mark(GRAPE_KERNEL_ERR_GRAD, 0);
             const long nmce = (long)B.nb * P.ne * P.nchunks * D * D;
-            hipLaunchKernelGGL(grape::k_sec_mc_err<D>, dim3((unsigned)((nmce + 255) / 256)), dim3(256), 0, st, P, B);
+            if (!P.gauge_lab)  // (k_walk_err_lab forms M'_{c,e} in the lane)
+                hipLaunchKernelGGL(grape::k_sec_mc_err<D>, dim3((unsigned)((nmce + 255) / 256)), dim3(256), 0, st, P, B);
             const hipError_t e = grape_walk::launch<D>(2, P, B, st);
             mark(GRAPE_KERNEL_ERR_GRAD, 1);
             return e != hipSuccess ? e : hipGetLastError();
@@ -435,6 +443,9 @@ hipError_t set_lds_limits() {
         if (e == hipSuccess)
             e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_scan<D, kScanLatency>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds<D>(kScanLatency));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&grape::k_err_scan<D, kScanLatency>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)errscan_lds<D>(kScanLatency));
     }
     if (e == hipSuccess) e = set_lds_limits_w<D, kScanNarrow>();
     return e != hipSuccess ? e : set_lds_limits_w<D, kScanTiny>();

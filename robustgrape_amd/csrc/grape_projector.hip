@@ -885,8 +885,164 @@ __global__ __launch_bounds__(kDiagBlock) void k_sec_err_head_diag(SectorHead H, 
     }
 }
 
+// Row-parallel form of k_sec_err_head_diag (round 6, latency): one group of G lanes per (evaluation, error
+// source), lane = row r of one sector block, as k_sec_head_diag.  Pass 0 forms row r of Ue = U Tot and its
+// terms of te, t1, t2 (t2 regrouped by rows: sum_rc w_c |Ue_rc|^2), a shuffle tree sums them; row r of Ue
+// goes to LDS, and pass 1 writes row r of M_e from the block's columns; pass 2 the F_d2err_dx_add row terms.
+// Lane 0 of the group forms the target's diagonal (target_diag).  The per-element operations are
+// diag_err_blocks's; only the order of the sums over rows changed.  One C3 evaluation: 36.9 us in one lane.
+#ifndef GRAPE_ERR_HEAD_ROWS
+#define GRAPE_ERR_HEAD_ROWS 1
+#endif
+template <int S>
+__device__ void err_row(const SectorHead &H, int cl, int w, int r, size_t b, int e, int pass, const cd *u0, const cd *d,
+                        cd te, cd *ue, double &t1, double &t2, cd &acc) {
+    const grape::DevProblem &P = H.P;
+    const int ns = H.nsec[cl], ne = P.ne;
+    const double sc = 2.0 / P.DD;
+    const size_t bw = b * ns + w;
+    const cd *Ub = H.Ub[cl] + bw * S * S;
+    int g[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) g[k] = H.sidx[cl][w * S + k];
+    const int gr = g[r];
+    auto cu0 = [&](int k) { return p_conj(u0[g[k] >= 0 ? g[k] : 0]); };
+    if (pass == 0) {
+        const cd *Tb = H.TotS[cl] + (bw * ne + e) * S * S;
+        cd Ur[S];
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            cd v{0.0, 0.0};
+#pragma unroll
+            for (int m = 0; m < S; ++m) v = p_add(v, p_mul(Ub[r * S + m], Tb[m * S + c]));
+            Ur[c] = (gr >= 0 && g[c] >= 0) ? v : cd{0.0, 0.0};
+            ue[r * S + c] = Ur[c];
+        }
+        if (gr < 0) return;
+        const double wr = P.W[gr];
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            if (g[c] < 0) continue;
+            const cd ke = p_mul(cu0(r), Ur[c]);
+            t1 += wr * pdiag(P, g[c]) * (ke.re * ke.re + ke.im * ke.im);
+            t2 += P.W[g[c]] * (Ur[c].re * Ur[c].re + Ur[c].im * Ur[c].im);
+        }
+        acc = p_add(acc, p_scale(wr, p_mul(cu0(r), Ur[r])));
+    } else if (pass == 1) {
+        cd *dst = H.MsecE[cl] + (bw * ne + e) * S * S + (size_t)r * S;
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            cd m{0.0, 0.0};
+            if (gr >= 0 && g[c] >= 0) {
+                cd kwk{0.0, 0.0}, uu{0.0, 0.0};  // (Ke^dag W K)_rc, (Ue^dag U)_rc
+#pragma unroll
+                for (int k = 0; k < S; ++k) {
+                    if (g[k] < 0) continue;
+                    const cd kk = p_mul(cu0(k), Ub[k * S + c]), ke = p_mul(cu0(k), ue[k * S + r]);
+                    kwk = p_add(kwk, p_scale(P.W[g[k]], p_mul(p_conj(ke), kk)));
+                    uu = p_add(uu, p_mul(p_conj(ue[k * S + r]), Ub[k * S + c]));
+                }
+                const double wr = P.W[gr];
+                const cd krc = p_mul(cu0(r), Ub[r * S + c]);
+                m = p_add(p_scale(2.0 * pdiag(P, gr), kwk), p_scale(2.0 * wr, p_mul(cd{te.re, -te.im}, krc)));
+                m = p_scale(sc, p_sub(m, p_scale(2.0 * (1.0 + P.Dtr) * wr, uu)));
+            }
+            dst[c] = m;
+        }
+    } else {
+        if (gr < 0) return;
+        const double wr = P.W[gr];
+        const cd dr = p_conj(d[gr]);
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+            if (g[c] < 0) continue;
+            const cd kde = p_mul(dr, ue[r * S + c]), ke = p_mul(cu0(r), ue[r * S + c]);
+            t1 += wr * pdiag(P, g[c]) * (kde.re * ke.re + kde.im * ke.im);
+        }
+        acc = p_add(acc, p_scale(wr, p_mul(dr, ue[r * S + r])));
+    }
+}
+__device__ __forceinline__ void err_row_any(const SectorHead &H, int row, size_t b, int e, int pass, const cd *u0,
+                                            const cd *d, cd te, cd *ue_grp, double &t1, double &t2, cd &acc) {
+    int cl = 0;
+    cd *ue = ue_grp;
+    if (row >= H.nsec[0] * H.S[0]) {
+        row -= H.nsec[0] * H.S[0];
+        ue += (size_t)H.nsec[0] * H.S[0] * H.S[0];
+        cl = 1;
+        if (cl >= H.ncls || row >= H.nsec[1] * H.S[1]) return;  // padding lane of the group
+    }
+    const int S = H.S[cl], w = row / S, r = row - w * S;
+    ue += (size_t)w * S * S;
+    switch (S) {
+    case 2: err_row<2>(H, cl, w, r, b, e, pass, u0, d, te, ue, t1, t2, acc); break;
+    case 3: err_row<3>(H, cl, w, r, b, e, pass, u0, d, te, ue, t1, t2, acc); break;
+    default: err_row<4>(H, cl, w, r, b, e, pass, u0, d, te, ue, t1, t2, acc); break;
+    }
+}
+__host__ __device__ inline size_t err_rows_group_cd(const SectorHead &H) {  // per group: u0, d, the Ue blocks
+    size_t n = 2 * (size_t)H.P.D;
+    for (int cl = 0; cl < H.ncls; ++cl) n += (size_t)H.nsec[cl] * H.S[cl] * H.S[cl];
+    return n;
+}
+__global__ __launch_bounds__(kDiagBlock) void k_sec_err_head_rows(SectorHead H, int nb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char diag_smem[];
+    const grape::DevProblem &P = H.P;
+    const int G = diag_group(H), EB = kDiagBlock / G;
+    const int t = threadIdx.x, el = t / G, row = t - el * G;
+    const int be = blockIdx.x * EB + el;
+    const bool ok = be < nb * P.ne;  // (group-uniform; every lane reaches every barrier)
+    const int bb = ok ? be : 0, b = bb / P.ne, e = bb - b * P.ne;
+    cd *u0 = reinterpret_cast<cd *>(diag_smem) + (size_t)el * err_rows_group_cd(H), *d = u0 + P.D, *ue = d + P.D;
+    const double *xb = H.x + (size_t)b * P.nx;
+    grape::Pert none;
+    none.var = -1;
+    none.index = 0;
+    none.delta = 0.0;
+    if (ok && row == 0) target_diag(P, xb, none, u0);
+    __syncthreads();
+    double t1 = 0.0, t2 = 0.0;
+    cd te{0.0, 0.0};
+    if (ok) err_row_any(H, row, b, e, 0, u0, d, te, ue, t1, t2, te);
+    t1 = group_add(t1, G);
+    t2 = group_add(t2, G);
+    te.re = group_add(te.re, G);
+    te.im = group_add(te.im, G);
+    if (ok && row == 0) H.Fd2[be] = 2.0 * (t1 - (1.0 + P.Dtr) * t2 + te.re * te.re + te.im * te.im) / P.DD;
+    __syncthreads();  // the group's Ue rows
+    double u1 = 0.0, u2 = 0.0;
+    cd uc{0.0, 0.0};
+    if (ok) err_row_any(H, row, b, e, 1, u0, d, te, ue, u1, u2, uc);
+    for (int q = 0; q < P.na; ++q) {  // target part of F_d2err_dx_add
+        grape::Pert pq;
+        pq.var = grape::VAR_XADD;
+        pq.index = q;
+        pq.delta = P.eps;
+        __syncthreads();
+        if (ok && row == 0) {
+            target_diag(P, xb, pq, d);
+            for (int i = 0; i < P.D; ++i) d[i] = p_scale(P.inv_eps, p_sub(d[i], u0[i]));
+        }
+        __syncthreads();
+        double sa = 0.0, unused = 0.0;
+        cd trd{0.0, 0.0};
+        if (ok) err_row_any(H, row, b, e, 2, u0, d, te, ue, sa, unused, trd);
+        sa = group_add(sa, G);
+        trd.re = group_add(trd.re, G);
+        trd.im = group_add(trd.im, G);
+        if (ok && row == 0)
+            H.Fd2dx[(size_t)be * P.nx + (size_t)P.np * P.Nt + q] = 2.0 * (2.0 * sa + 2.0 * (te.re * trd.re + te.im * trd.im)) / P.DD;
+    }
+}
+
 hipError_t launch_sector_err_head(const SectorHead &H, int nb, hipStream_t st) {
     if (H.P.ne == 0) return hipSuccess;
+    if (H.diag && GRAPE_ERR_HEAD_ROWS && diag_group(H) <= kDiagBlock) {
+        const int G = diag_group(H), EB = kDiagBlock / G, n = nb * H.P.ne;
+        const size_t lds = (size_t)EB * err_rows_group_cd(H) * sizeof(cd);
+        hipLaunchKernelGGL(k_sec_err_head_rows, dim3((unsigned)((n + EB - 1) / EB)), dim3(kDiagBlock), lds, st, H, nb);
+        return hipGetLastError();
+    }
     if (H.diag) {
         const int n = nb * H.P.ne;
         const size_t lds = (size_t)kDiagBlock * 2 * H.P.D * sizeof(cd);

@@ -3094,18 +3094,22 @@ __global__ __launch_bounds__(kWalkBlock, err_lab_waves<D>()) void k_walk_err_lab
 #pragma unroll
     for (int w = 0; w < NS; ++w) {
         const size_t sub = (size_t)L.be * ns + L.w0 + w;
+        // M'_c = Carry_c M Carry_c^dag of the head's block, formed here (k_sec_mc / k_sec_mc_err's arithmetic:
+        // merged_xinit) instead of by two launches that store it for this kernel to read
+        const cd *Cr = B.Carry + (sub * P.nchunks + L.c) * TS;
         if (fdx) {  // F_dx[k] (sector part) = Re tr(M'_c Z1_k): X = M'_c
-            const cd *Mc = B.Mc + (sub * P.nchunks + L.c) * TS;
-#pragma unroll
-            for (int t = 0; t < TS; ++t) X[w][t / D][t % D] = Mc[t];
-        } else {  // X = M', L = T_c M' - M' T_c + M' Ttot (k_walk_err_grad's B)
-            const cd *Mo = B.Me + ((sub * P.ne + e) * P.nchunks + L.c) * 3 * TS;  // M', T_c, Ttot
+            merged_xinit<D>(Cr, B.Msec + sub * TS, X[w]);
+        } else {  // X = M'_{c,e}, L = T_c M' - M' T_c + M' Ttot (k_walk_err_grad's B)
+            const cd *Mo = B.Me + ((sub * P.ne + e) * P.nchunks + L.c) * 3 * TS;  // (M'), T_c, Ttot
             cd Mp[TS], T1[TS], Bk[TS], T2[TS];
+            {
+                cd Xm[D][D];
+                merged_xinit<D>(Cr, B.MsecE + (sub * P.ne + e) * TS, Xm);
 #pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                Mp[t] = Mo[t];
-                T1[t] = Mo[TS + t];
+                for (int t = 0; t < TS; ++t) Mp[t] = Xm[t / D][t % D];
             }
+#pragma unroll
+            for (int t = 0; t < TS; ++t) T1[t] = Mo[TS + t];
             walk_mm<D>(T1, Mp, Bk);  // T_c M'
             walk_mm<D>(Mp, T1, T2);  // M' T_c
 #pragma unroll
