@@ -30,6 +30,8 @@ for v in "$@"; do
     case $leg in
       arcz) run $v arcz 200 --workload arcz --no-cpu-baseline ;;
       c3) run $v c3 300 --workload c3 --steps 10 --warmup 2 --no-cpu-baseline ;;
+      c3p16) run $v c3p16 300 --workload c3 --steps 10 --warmup 2 --no-cpu-baseline --no-host-paths --chunk 16384 ;;
+      c3p4) run $v c3p4 300 --workload c3 --steps 10 --warmup 2 --no-cpu-baseline --no-host-paths --chunk 4096 ;;
       c4opt) run $v c4opt 300 --workload c4opt --steps 20 --warmup 5 ;;
       c5) run $v c5 300 --workload c5 --steps 30 --warmup 3 --no-cpu-baseline --no-host-paths ;;
       c5err) run $v c5err 300 --workload c5err --steps 10 --warmup 2 --no-cpu-baseline --no-host-paths ;;
