@@ -755,15 +755,17 @@ def c3_report(args, B, L, world, value, elapsed, ktimes, ne, sectors=None, passe
     out["roofline"]["whole_eval"] = {"flop_per_eval_executed": exe, "achieved_executed": exe * value / 1e12,
                                      "frac_executed": exe * value / 1e12 / FP64_PEAK_TFLOPS,
                                      "flop_per_eval_survey": canon}
-    if walk and not lab:  # PMC HBM bytes of one whole device pass (every kernel), against the pass time
+    if walk:  # PMC HBM bytes of one whole device pass (every kernel), against the pass time
         pipe = pmc_pipeline(L, img_kernel, {S for S, _ in classes}, PMC_SUMMARY_C3)
         if pipe:
             pass_ms = sum(per_pass.values())
             out["roofline"]["pipeline_traffic"] = {
                 "bytes_per_pass": pipe, "bytes_per_eval": pipe / L, "GBs_over_pass": pipe / (pass_ms * 1e-3) / 1e9,
                 "frac_hbm": pipe / (pass_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "note": "PMC HBM bytes of every kernel of one device pass (images written by the image walk and "
-                        "re-read by k_walk_img_sum and k_walk_err_grad dominate), over the summed kernel time"}
+                "note": ("PMC HBM bytes of every kernel of one device pass (lab-frame walks: x rows, chunk states, "
+                         "per-step terms; no images), over the summed kernel time" if lab else
+                         "PMC HBM bytes of every kernel of one device pass (images written by the image walk and "
+                         "re-read by k_walk_img_sum and k_walk_err_grad dominate), over the summed kernel time")}
     if not sec:
         out["roofline"]["whole_eval"].update({"achieved_survey": canon * value / 1e12,
                                               "frac_survey": canon * value / 1e12 / FP64_PEAK_TFLOPS})
