@@ -3203,4 +3203,153 @@ __global__ __launch_bounds__(kWalkBlock, err_lab_waves<D>()) void k_walk_err_lab
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// The merged gradient walk in the gauge frame (round 6, GRAPE_WALK_GRAD_TILDE)
+// ---------------------------------------------------------------------------
+// k_walk_grad_m carries X_k = C M C^dag per class and forms E_k = D_k E~ D_k^dag in registers each step.
+// Here the state is X~ = D_k^dag X D_k (k_walk_err_lab's frame): per step
+//   Y~ = X~ E~^dag,  F_dx part = Re tr(Y~ (E~ o f)) / eps,  X~ <- Om (E~ Y~) Om^dag   (Om = D_{k+1}^dag D_k)
+// -- the same quantities (traces are frame-invariant), E~ a workgroup-uniform SGPR operand read row by row
+// (lab_rows), so E_k's registers and its formation go and the lane fits three waves per SIMD; the rotation
+// costs what E_k's formation did.  Ladder classes only (the merged walks' classes); output as k_walk_grad_m.
+// Measured slower and off: 168 VGPRs, three waves per SIMD, no scratch, parity-green (the gauge / walk /
+// parity suites on it), but 0.343 against 0.309-0.316 ms per C2 pass (A/B twice in one GPU call): the
+// row-wise uniform operands cost the products their cross-row ILP, which the third wave does not win back
+#ifndef GRAPE_WALK_GRAD_TILDE
+#define GRAPE_WALK_GRAD_TILDE 0
+#endif
+#ifndef GRAPE_WALK_GRAD_TILDE_WAVES
+#define GRAPE_WALK_GRAD_TILDE_WAVES 3
+#endif
+// sum_{r != j} Re(Y_jr (U o f)_rj) for ladder charges: f_rj = rho(r - j) (conj for r < j), grouped by charge
+// difference (merged_step_grad's contraction) with U uniform
+template <int D>
+__device__ __forceinline__ double lab_trace_ladder(const cd (&Y)[D][D], cptr<cd> U, const cd (&rh)[D]) {
+    double tre[D], tim[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) tre[m] = tim[m] = 0.0;
+    lab_rows<D>(U, Y[D - 1][D - 1].re, [&](int r, const cd (&u)[D]) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            if (r == j) continue;
+            const int m = r > j ? r - j : j - r;
+            const cd y = Y[j][r], e = u[j];
+            tre[m] = fma(y.re, e.re, tre[m]);
+            tre[m] = fma(-y.im, e.im, tre[m]);
+            if (r > j) {
+                tim[m] = fma(y.re, e.im, tim[m]);
+                tim[m] = fma(y.im, e.re, tim[m]);
+            } else {
+                tim[m] = fma(-y.re, e.im, tim[m]);
+                tim[m] = fma(-y.im, e.re, tim[m]);
+            }
+        }
+#pragma unroll
+        for (int m = 1; m < D; ++m) asm volatile("" : "+v"(tre[m]), "+v"(tim[m]));
+        return tre[D - 1];
+    });
+    double c = 0.0;
+#pragma unroll
+    for (int m = 1; m < D; ++m) {
+        c = fma(rh[m].re, tre[m], c);
+        c = fma(-rh[m].im, tim[m], c);
+    }
+    return c;
+}
+template <int D>
+__device__ __forceinline__ double tilde_step(cptr<cd> Et, const cd (&om_e)[kGaugePairs<D>], const cd (&rh)[D],
+                                             cd (&X)[D][D]) {
+    cd Y[D][D];
+    lab_mul_udag<D, false>(X, Et, Y);            // Y~ = X~ E~^dag
+    const double s = lab_trace_ladder<D>(Y, Et, rh);
+    lab_umul<D, false>(Et, Y, X);                // X~ = E~ Y~
+    lab_rotate<D>(om_e, X);                      // into the next step's frame
+    return s;
+}
+template <int DA, bool TWB>
+__global__ __launch_bounds__(kWalkBlock, GRAPE_WALK_GRAD_TILDE_WAVES) void k_walk_grad_mt(DevProblem PA, DevBatch BA,
+                                                                                       DevProblem PB, DevBatch BB, int a_first) {
+    constexpr int NXB = (TWB && GRAPE_WALK_TWIN_SUM) ? 1 : 2;
+    __shared__ double ftile[kWalkBlock][kFdxTile + 1];
+    __shared__ int2 frow[kWalkBlock];
+    const VBlock vb = hw_block();
+    const WalkLane L = walk_lane<1>(PA, BA, vb);
+    const double *xt = BA.xT + (size_t)L.be * (kWalkXRow ? PA.nx : 1);
+    const int xs = kWalkXRow ? 1 : L.nbe;
+    frow[threadIdx.x] = make_int2(L.ok ? L.be : -1, L.c * PA.L);
+    cd XA[DA][DA], XB[NXB][2][2];
+    {
+        const size_t nbe = (size_t)L.nbe, be = (size_t)L.be;
+        cd Cr[DA * DA];
+        const cd *ca = BA.Carry + (size_t)L.c * DA * DA * nbe + be;
+#pragma unroll
+        for (int e = 0; e < DA * DA; ++e) Cr[e] = ca[(size_t)e * nbe];
+        merged_xinit<DA>(Cr, BA.Msec + be * DA * DA, XA);
+#pragma unroll
+        for (int w = 0; w < NXB; ++w) {
+            cd Cb[4], Mb[4];
+            const cd *cb = BB.Carry + ((size_t)(TWB ? 0 : w) * PB.nchunks + L.c) * 4 * nbe + be;
+            const cd *mb = BB.Msec + (be * 2 + w) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                Cb[e] = cb[(size_t)e * nbe];
+                Mb[e] = NXB == 1 ? cadd(mb[e], mb[4 + e]) : mb[e];
+            }
+            merged_xinit<2>(Cb, Mb, XB[w]);
+        }
+    }
+    const int k0 = L.c * PA.L;
+    double xk = walk_load_x(1, xt + (size_t)min(k0, PA.Nt - 1) * xs, xs).v0;
+    {  // into the first step's frame: X~ = D_{k0}^dag X D_{k0}
+        const cd pc = cconj(gauge_cis(PA.gauge_a * xk));
+        cd ea[kGaugePairs<DA>], eb[kGaugePairs<2>];
+        gauge_phases_ladder<DA>(pc, ea);
+        gauge_phases_ladder<2>(pc, eb);
+        lab_rotate<DA>(ea, XA);
+#pragma unroll
+        for (int w = 0; w < NXB; ++w) lab_rotate<2>(eb, XB[w]);
+    }
+    const cptr<cd> gA0 = as_constant(PA.gauge_Et), gB0 = as_constant(PB.gauge_Et);
+    auto step = [&](int jj) {
+        const int k = min(k0 + jj, PA.Nt - 1);
+        const double xn = walk_load_x(1, xt + (size_t)min(k + 1, PA.Nt - 1) * xs, xs).v0;
+        const double xe = xk + PA.eps;  // the reference's perturbed control
+        const cd q = cis_m1(PA.gauge_a * (xe - xk)), om = gauge_cis(PA.gauge_a * xk - PA.gauge_a * xn);
+        xk = xn;
+        cptr<cd> gA = gA0, gB = gB0;  // (opaque per step: the row addresses stay in the step)
+        asm volatile("" : "+s"(gA), "+s"(gB));
+        cd rh[DA];
+        ladder_rho<DA>(q, rh);
+        cd ea[kGaugePairs<DA>], eb[kGaugePairs<2>];
+        gauge_phases_ladder<DA>(om, ea);
+        gauge_phases_ladder<2>(om, eb);
+        cd rb[2];
+        rb[0] = rh[0];
+        rb[1] = rh[1];
+        const double sa = tilde_step<DA>(gA, ea, rh, XA) * PA.inv_eps;
+        double sb = 0.0;
+#pragma unroll
+        for (int w = 0; w < NXB; ++w) sb += tilde_step<2>(gB + (TWB ? 0 : w) * 4, eb, rb, XB[w]) * PB.inv_eps;
+        double v = 0.0;  // k_sec_reduce's sum of the classes' parts, in the plan's class order
+        v += a_first ? sa : sb;
+        v += a_first ? sb : sa;
+        return v;
+    };
+#pragma unroll 1
+    for (int j0 = 0; j0 < PA.L; j0 += kFdxTile) {
+        const int nj = min(kFdxTile, PA.L - j0);
+#pragma unroll 1
+        for (int t = 0; t < nj; ++t) ftile[threadIdx.x][t] = step(j0 + t);
+        __syncthreads();
+        const int j = threadIdx.x % kFdxTile;
+#pragma unroll 1
+        for (int row = threadIdx.x / kFdxTile; row < kWalkBlock; row += kWalkBlock / kFdxTile) {
+            const int br = frow[row].x, kk = frow[row].y + j0 + j;
+            if (j < nj && br >= 0 && kk < PA.Nt) BA.Fdx[(size_t)br * PA.nx + kk] = ftile[row][j];
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace grape

@@ -190,6 +190,8 @@ hipError_t launch_merged(int stage, const grape::DevProblem &PA, const grape::De
         } else if (stage == 2) {  // the chunk-total scan (one lane per evaluation)
             hipLaunchKernelGGL((grape::k_scan_seq<DA, TW>), dim3((unsigned)((BA.nb + grape::kSeqBlock - 1) / grape::kSeqBlock)), dim3(grape::kSeqBlock), 0, st, PA,
                                BA, PB, BB, BA.nb);
+        } else if (GRAPE_WALK_GRAD_TILDE && LAD) {  // the gauge-frame gradient walk (ladder classes)
+            hipLaunchKernelGGL((grape::k_walk_grad_mt<DA, TW>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
         } else {
             hipLaunchKernelGGL((grape::k_walk_grad_m<DA, TW, LAD>), grid, blk, 0, st, PA, BA, PB, BB, a_first);
         }

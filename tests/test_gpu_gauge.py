@@ -167,10 +167,13 @@ def _check_err(test, out, b, ref, tier):
 ])
 @pytest.mark.parametrize("batch", [3, 300])
 def test_gauge_image_walk_matches_per_step_exponentials_and_oracle(name, fp, batch):
-    """Error sources (k_walk_img_gauge): F, F_dx, F_d2err, F_d2err_dx against the per-step image walk
-    (GRAPE_OPT_NO_GAUGE) and the oracle (UnitaryCalculations.jl:66-151, FidelityCalculations.jl:78-117);
-    the mixed stencil is formed without its four-term cancellation, so the comparison carries the
-    per-step side's eps2 noise (T3 tier)."""
+    """Error sources on phase-covariant classes (round 6: the lab-frame walks k_walk_wsum_lab /
+    k_walk_err_lab; k_walk_img_gauge with GRAPE_WALK_ERR_LAB=0): F, F_dx, F_d2err,
+    F_d2err_dx against the per-step image walk (GRAPE_OPT_NO_GAUGE) and the oracle
+    (UnitaryCalculations.jl:66-151, FidelityCalculations.jl:78-117); the mixed stencil is formed without
+    its four-term cancellation, so the comparison carries the per-step side's eps2 noise (T3 tier).
+    Batches of 3 (latency scans, 128 / 256 chunks) and 300 (4-wave scans); the throughput chunking
+    (one-wave scans, 6 / 8 chunks) runs in test_gpu_walk.py test_bench_size_plan_c3_golden."""
     from oracle import grape_oracle as O
     from robustgrape_amd.operators import OPT_NO_GAUGE
     f = fp()
