@@ -243,6 +243,63 @@ struct Frag {
     double aR[2], aI[2], bR, bI;
 };
 
+// Round 6 (GRAPE_DENSE_FRAG_ADDR): the fragment addresses in closed form.  With the round-6 swizzle,
+// for k-step s (a compile-time constant in the unrolled loop) and byte offsets
+//   A of L:    a + ((32 s) ^ ac) (+ 8 192 for the second tile),   A of L^T: (a ^ (32 (s & 3) [+ 128])) + 2 048 s
+//   B of R^T:  b + ((32 s) ^ bc),                                  B of R:   (b ^ (32 (s & 3))) + 2 048 s
+// from four per-lane values formed once per product (frag_addr) -- one or two VALU instructions per address
+// and step, the rest the loads' immediate offsets, where recomputing sidx from the lane id cost ~15 per
+// step (checked for every lane, tile and step against sidx by scripts/probes/lds_banks.py).
+#ifndef GRAPE_DENSE_FRAG_ADDR
+#define GRAPE_DENSE_FRAG_ADDR 1
+#endif
+struct FragAddr {
+    int a, ac, b, bc;
+};
+template <bool LT, bool RT>
+__device__ __forceinline__ FragAddr frag_addr(const Lane &ln) {
+    const int l = ln.l, g = l >> 4, c = l & 15, gp = g | ((g & 1) << 4);
+    FragAddr f;
+    const int ir = 16 * ln.tile(0) + c, jc = 16 * ln.w + c;
+    if (LT) {
+        f.a = 8 * (64 * g + (ir ^ gp));
+        f.ac = 0;
+    } else {
+        const int sw = swz64(ir);
+        f.a = 8 * (ir * 64 + (g ^ (sw & 3)));
+        f.ac = 32 * (sw >> 2);
+    }
+    if (RT) {
+        const int sw = swz64(jc);
+        f.b = 8 * (jc * 64 + (g ^ (sw & 3)));
+        f.bc = 32 * (sw >> 2);
+    } else {
+        f.b = 8 * (64 * g + (jc ^ gp));
+        f.bc = 0;
+    }
+    return f;
+}
+__device__ __forceinline__ double lds_at(const double *base, int byte_off) {
+    return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + byte_off);
+}
+template <bool LT, bool RT, bool RC>
+__device__ __forceinline__ void mm_load_fa(SM L, SM R, int s, Frag &f, FragAddr &fa) {
+    // made opaque in place at every step (no copies): each step's addresses are formed here instead of being
+    // hoisted out of the product as 16 x 3 VGPRs; only the fields this product reads
+    if constexpr (LT) asm volatile("" : "+v"(fa.a));
+    else asm volatile("" : "+v"(fa.a), "+v"(fa.ac));
+    if constexpr (RT) asm volatile("" : "+v"(fa.b), "+v"(fa.bc));
+    else asm volatile("" : "+v"(fa.b));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int o = LT ? (fa.a ^ ((i ? 128 : 0) + 32 * (s & 3))) + 2048 * s : fa.a + ((32 * s) ^ fa.ac) + 8192 * i;
+        f.aR[i] = lds_at(L.re, o);
+        f.aI[i] = lds_at(L.im, o);
+    }
+    const int o = RT ? fa.b + ((32 * s) ^ fa.bc) : (fa.b ^ (32 * (s & 3))) + 2048 * s;
+    f.bR = lds_at(R.re, o);
+    f.bI = RC ? -lds_at(R.im, o) : lds_at(R.im, o);
+}
 template <bool LT, bool RT, bool RC>
 __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &ln) {
     // Indices are recomputed from a freshly pinned lane id every step: otherwise
@@ -312,10 +369,16 @@ __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
     v4d t1[2], t2[2], t3[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) t1[i] = t2[i] = t3[i] = v4d{0.0, 0.0, 0.0, 0.0};
-    mm_load<LT, RT, RC>(L, R, 0, fc, ln);
+    constexpr bool kFA = GRAPE_DENSE_FRAG_ADDR && !GRAPE_DENSE_SWZ_R2;
+    FragAddr fa = kFA ? frag_addr<LT, RT>(pinned(ln)) : FragAddr{0, 0, 0, 0};
+    auto load = [&](int s, Frag &f) {
+        if constexpr (kFA) mm_load_fa<LT, RT, RC>(L, R, s, f, fa);
+        else mm_load<LT, RT, RC>(L, R, s, f, ln);
+    };
+    load(0, fc);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-        if (s < 15) mm_load<LT, RT, RC>(L, R, s + 1, fn, ln);
+        if (s < 15) load(s + 1, fn);
         const double bs = fc.bR + fc.bI;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
