@@ -83,12 +83,14 @@ struct HM {
 
 struct SM {
     double *re, *im;
+    int boff;  // byte offset of re from the LDS start (mm's fragment addresses)
 };
 
 __device__ __forceinline__ SM sm_at(double *lds, int off) {
     SM s;
     s.re = lds + off;
     s.im = lds + off + PLANE;
+    s.boff = 8 * off;
     return s;
 }
 
@@ -282,6 +284,14 @@ __device__ __forceinline__ FragAddr frag_addr(const Lane &ln) {
 __device__ __forceinline__ double lds_at(const double *base, int byte_off) {
     return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + byte_off);
 }
+// GRAPE_DENSE_FA_BASE: both operands addressed from the LDS start, their regions' byte offsets folded
+// into fa.a / fa.b once per product.  Region 1 starts at 64 KB, beyond a ds_read_b64's 16-bit immediate:
+// addressed from its own base, every B (and, for L in region 1, A) fragment load of a step took two
+// v_add_u32 (base + re plane, base + im plane) and the re / im pair was not merged into one
+// ds_read2st64_b64.
+#ifndef GRAPE_DENSE_FA_BASE
+#define GRAPE_DENSE_FA_BASE 0
+#endif
 template <bool LT, bool RT, bool RC>
 __device__ __forceinline__ void mm_load_fa(SM L, SM R, int s, Frag &f, FragAddr &fa) {
     // made opaque in place at every step (no copies): each step's addresses are formed here instead of being
@@ -290,15 +300,17 @@ __device__ __forceinline__ void mm_load_fa(SM L, SM R, int s, Frag &f, FragAddr 
     else asm volatile("" : "+v"(fa.a), "+v"(fa.ac));
     if constexpr (RT) asm volatile("" : "+v"(fa.b), "+v"(fa.bc));
     else asm volatile("" : "+v"(fa.b));
+    const double *lre = GRAPE_DENSE_FA_BASE ? L.re - L.boff / 8 : L.re, *lim = lre + PLANE;
+    const double *rre = GRAPE_DENSE_FA_BASE ? R.re - R.boff / 8 : R.re, *rim = rre + PLANE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int o = LT ? (fa.a ^ ((i ? 128 : 0) + 32 * (s & 3))) + 2048 * s : fa.a + ((32 * s) ^ fa.ac) + 8192 * i;
-        f.aR[i] = lds_at(L.re, o);
-        f.aI[i] = lds_at(L.im, o);
+        f.aR[i] = lds_at(lre, o);
+        f.aI[i] = lds_at(lim, o);
     }
     const int o = RT ? fa.b + ((32 * s) ^ fa.bc) : (fa.b ^ (32 * (s & 3))) + 2048 * s;
-    f.bR = lds_at(R.re, o);
-    f.bI = RC ? -lds_at(R.im, o) : lds_at(R.im, o);
+    f.bR = lds_at(rre, o);
+    f.bI = RC ? -lds_at(rim, o) : lds_at(rim, o);
 }
 template <bool LT, bool RT, bool RC>
 __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &ln) {
@@ -329,6 +341,9 @@ __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &
 // 8 d^3 per complex product (executed: 6 d^3).
 #ifndef GRAPE_DENSE_4M
 #define GRAPE_DENSE_4M 0
+#endif
+#ifndef GRAPE_DENSE_CONJ_EPI
+#define GRAPE_DENSE_CONJ_EPI 0
 #endif
 template <bool LT, bool LC, bool RT, bool RC>
 __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
@@ -365,23 +380,38 @@ __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
     }
     // Gauss's three-multiplication complex product: T1 = Lr Rr, T2 = Li Ri, T3 = (Lr + Li)(Rr + Ri),
     // P += (T1 - T2) + i (T3 - T1 - T2): 3 MFMAs per tile and k-step instead of 4.
+    // GRAPE_DENSE_CONJ_EPI: a conjugated operand's sign goes to the sums (a - b: a free source modifier)
+    // and to T2's sign in the combination below, instead of a negated copy of the fragment per step (two
+    // VALU instructions each: sign flip and move)
+    constexpr bool kCE = GRAPE_DENSE_CONJ_EPI;
+    constexpr bool kT2Neg = kCE && (LC != RC);  // T2 accumulated as -(Li Ri)
     Frag fc, fn;
     v4d t1[2], t2[2], t3[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) t1[i] = t2[i] = t3[i] = v4d{0.0, 0.0, 0.0, 0.0};
     constexpr bool kFA = GRAPE_DENSE_FRAG_ADDR && !GRAPE_DENSE_SWZ_R2;
     FragAddr fa = kFA ? frag_addr<LT, RT>(pinned(ln)) : FragAddr{0, 0, 0, 0};
+    if constexpr (kFA && GRAPE_DENSE_FA_BASE) {
+        fa.a += L.boff;
+        fa.b += R.boff;
+    }
     auto load = [&](int s, Frag &f) {
-        if constexpr (kFA) mm_load_fa<LT, RT, RC>(L, R, s, f, fa);
-        else mm_load<LT, RT, RC>(L, R, s, f, ln);
+        if constexpr (kFA) mm_load_fa<LT, RT, RC && !kCE>(L, R, s, f, fa);
+        else mm_load<LT, RT, RC && !kCE>(L, R, s, f, ln);
     };
     load(0, fc);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
         if (s < 15) load(s + 1, fn);
-        const double bs = fc.bR + fc.bI;
+        const double bs = (kCE && RC) ? fc.bR - fc.bI : fc.bR + fc.bI;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
+            if constexpr (kCE) {
+                t1[i] = mfma(fc.aR[i], fc.bR, t1[i]);
+                t2[i] = mfma(fc.aI[i], fc.bI, t2[i]);
+                t3[i] = mfma(LC ? fc.aR[i] - fc.aI[i] : fc.aR[i] + fc.aI[i], bs, t3[i]);
+                continue;
+            }
             const double ai = LC ? -fc.aI[i] : fc.aI[i];
             t1[i] = mfma(fc.aR[i], fc.bR, t1[i]);
             t2[i] = mfma(ai, fc.bI, t2[i]);
@@ -395,8 +425,13 @@ __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        P.re[i] += t1[i] - t2[i];
-        P.im[i] += t3[i] - t1[i] - t2[i];
+        if constexpr (kT2Neg) {  // T2 = -t2: the same roundings as the negated-copy form
+            P.re[i] += t1[i] + t2[i];
+            P.im[i] += t3[i] - t1[i] + t2[i];
+        } else {
+            P.re[i] += t1[i] - t2[i];
+            P.im[i] += t3[i] - t1[i] - t2[i];
+        }
     }
 }
 
