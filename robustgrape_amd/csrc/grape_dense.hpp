@@ -750,6 +750,21 @@ __device__ __forceinline__ void taylor_block(HM &x, int b, int n, const HM &A, c
     if (n > 4 && A4) hm_axpy(x, kDInvFact[b + 4], *A4);
 }
 
+// The Taylor degree for |A|_1 <= 0.95: the lowest of 8 / 12 / 16 / 18 (4 / 5 / 6 / 7 products) whose
+// remainder bound |A|^(m+1) / (m+1)! stays at or below degree 18's at 0.95 (3.1e-18):
+//   m = 8: |A|_1 <= 0.047,  12: <= 0.25,  16: <= 0.668,  18: <= 0.95.
+// Round 6 (GRAPE_DENSE_TAYLOR16): degrees 8 and 16; before, 12 up to 0.25 and 18 above.  At C5
+// 63 % of the steps fall in 0.25 < |A|_1 <= 0.668 (|A|_1 in 0.49 .. 0.88): one product fewer each.
+#ifndef GRAPE_DENSE_TAYLOR16
+#define GRAPE_DENSE_TAYLOR16 1
+#endif
+__device__ __forceinline__ int taylor_degree(double nA) {
+    if (GRAPE_DENSE_TAYLOR16 && nA <= 0.047) return 8;
+    if (nA <= 0.25) return 12;
+    if (GRAPE_DENSE_TAYLOR16 && nA <= 0.668) return 16;
+    return 18;
+}
+
 // A is in S0 and in registers; returns X = T(A).  Uses both LDS regions.
 __device__ __forceinline__ void wg_expm_taylor(const HM &A, int degree, HM &X, double *lds, const Lane &ln) {
     SM S0 = sm_at(lds, LDS_R0), S1 = sm_at(lds, LDS_R1);
@@ -767,11 +782,11 @@ __device__ __forceinline__ void wg_expm_taylor(const HM &A, int degree, HM &X, d
         mm<false, false, false, false>(S1, S1, A4, ln);  // A^2 . A^2
         __syncthreads();
         sm_store(S0, A4, ln);  // the Horner left operand from here on
-        if (degree == 12) taylor_block(X, 8, 5, A, A2, A3, &A4, ln);  // c8..c12
-        else taylor_block(X, 16, 3, A, A2, A3, nullptr, ln);          // c16..c18
+        if (degree == 18) taylor_block(X, 16, 3, A, A2, A3, nullptr, ln);  // c16..c18
+        else taylor_block(X, degree - 4, 5, A, A2, A3, &A4, ln);           // c_{m-4}..c_m, m = 8, 12, 16
         hm_pin(X);
     }
-    const int top = degree == 12 ? 1 : 3;  // blocks B_top .. B_0 below the initial one
+    const int top = degree == 18 ? 3 : degree / 4 - 2;  // blocks B_top .. B_0 below the initial one
     for (int j = top; j >= 0; --j) {
         __syncthreads();  // S1's previous contents consumed
         sm_store(S1, X, ln);
@@ -805,7 +820,7 @@ __device__ __forceinline__ int wg_expm(const Build &build, HM &X, double *lds, c
         sm_store(S0, A, ln);
         __syncthreads();
         if (m <= 7) {  // Julia's Pade 3 / 5 / 7 regime: solve-free Taylor (above)
-            wg_expm_taylor(A, m == 7 ? 18 : 12, X, lds, ln);
+            wg_expm_taylor(A, taylor_degree(nA), X, lds, ln);
             return m;
         }
     }
