@@ -345,6 +345,9 @@ __device__ __forceinline__ void mm_load(SM L, SM R, int s, Frag &f, const Lane &
 #ifndef GRAPE_DENSE_CONJ_EPI
 #define GRAPE_DENSE_CONJ_EPI 0
 #endif
+#ifndef GRAPE_DENSE_PINGPONG  // 3M products: fragment buffers by step parity (mm, below)
+#define GRAPE_DENSE_PINGPONG 1
+#endif
 template <bool LT, bool LC, bool RT, bool RC>
 __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
     if constexpr (GRAPE_DENSE_4M) {
@@ -399,10 +402,7 @@ __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
         if constexpr (kFA) mm_load_fa<LT, RT, RC && !kCE>(L, R, s, f, fa);
         else mm_load<LT, RT, RC && !kCE>(L, R, s, f, ln);
     };
-    load(0, fc);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        if (s < 15) load(s + 1, fn);
+    auto step = [&](const Frag &fc) {
         const double bs = (kCE && RC) ? fc.bR - fc.bI : fc.bR + fc.bI;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -417,11 +417,32 @@ __device__ __forceinline__ void mm(SM L, SM R, HM &P, const Lane &ln) {
             t2[i] = mfma(ai, fc.bI, t2[i]);
             t3[i] = mfma(fc.aR[i] + ai, bs, t3[i]);
         }
+    };
+    if constexpr (GRAPE_DENSE_PINGPONG) {
+        // two fragment buffers alternating by step parity (the loop is unrolled): no copy fc = fn, and
+        // the barrier between steps is a bare compiler fence (it keeps later steps' loads from being
+        // hoisted) instead of a pin on the fresh fragment, which forced the wait for step s+1's loads
+        // into step s after its first two MFMAs
+        Frag fb[2];
+        load(0, fb[0]);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            if (s < 15) load(s + 1, fb[(s + 1) & 1]);
+            step(fb[s & 1]);
+            if (s < 15) asm volatile("" ::: "memory");
+        }
+    } else {
+    load(0, fc);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        if (s < 15) load(s + 1, fn);
+        step(fc);
         if (s < 15) {
             fc = fn;
             asm volatile("" : "+v"(fc.aR[0]), "+v"(fc.aR[1]), "+v"(fc.aI[0]), "+v"(fc.aI[1]), "+v"(fc.bR),
                          "+v"(fc.bI)::"memory");
         }
+    }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
