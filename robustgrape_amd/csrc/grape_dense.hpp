@@ -755,11 +755,12 @@ __device__ __forceinline__ void hm_pin(HM &M) {
 // no Gauss-Jordan solve, whose serial 16 x 16 block inversions left the MFMA pipe idle for
 // about as long as the Pade products took.  Agrees with exp! to a few u (inside T0).
 // ---------------------------------------------------------------------------
-__constant__ const double kDInvFact[19] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040,
+__constant__ const double kDInvFact[21] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040,
                                            1.0 / 40320, 1.0 / 362880, 1.0 / 3628800, 1.0 / 39916800,
                                            1.0 / 479001600, 1.0 / 6227020800.0, 1.0 / 87178291200.0,
                                            1.0 / 1307674368000.0, 1.0 / 20922789888000.0,
-                                           1.0 / 355687428096000.0, 1.0 / 6402373705728000.0};
+                                           1.0 / 355687428096000.0, 1.0 / 6402373705728000.0,
+                                           1.0 / 121645100408832000.0, 1.0 / 2432902008176640000.0};
 
 // x = c0 I + c1 A + c2 A2 + c3 A3 (+ c4 A4) for coefficients kDInvFact[b..]
 __device__ __forceinline__ void taylor_block(HM &x, int b, int n, const HM &A, const HM &A2, const HM &A3,
@@ -771,15 +772,27 @@ __device__ __forceinline__ void taylor_block(HM &x, int b, int n, const HM &A, c
     if (n > 4 && A4) hm_axpy(x, kDInvFact[b + 4], *A4);
 }
 
-// The Taylor degree for |A|_1 <= 0.95: the lowest of 8 / 12 / 16 / 18 (4 / 5 / 6 / 7 products) whose
-// remainder bound |A|^(m+1) / (m+1)! stays at or below degree 18's at 0.95 (3.1e-18):
-//   m = 8: |A|_1 <= 0.047,  12: <= 0.25,  16: <= 0.668,  18: <= 0.95.
-// Round 6 (GRAPE_DENSE_TAYLOR16): degrees 8 and 16; before, 12 up to 0.25 and 18 above.  At C5
-// 63 % of the steps fall in 0.25 < |A|_1 <= 0.668 (|A|_1 in 0.49 .. 0.88): one product fewer each.
+// The Taylor degree for |A|_1 <= 0.95.  Paterson-Stockmeyer in A^4 costs 4 / 5 / 6 / 7 products at
+// degree 8 / 12 / 16 / 20 (degree 18 costs 7 as well).  GRAPE_DENSE_TAYLOR_U (default): the lowest of
+// them whose remainder bound |A|^(m+1) / (m+1)! is at most u = 2^-53, the accuracy Julia's theta_m
+// give its Pade degrees:  m = 8: |A|_1 <= 0.069,  12: <= 0.335,  16: <= 0.826,  20: <= 0.95 (bound
+// 6e-5 u there).  At C5 (|A|_1 in 0.49 .. 0.88) 98 % of the steps take degree 16.
+// GRAPE_DENSE_TAYLOR_U 0, GRAPE_DENSE_TAYLOR16 1: the bound of degree 18 at 0.95 (3.1e-18) for every
+// degree -- 8 <= 0.047, 12 <= 0.25, 16 <= 0.668, 18 above (64 % of C5's steps at degree 16).  Both 0:
+// round 2's 12 up to 0.25 and 18 above.
 #ifndef GRAPE_DENSE_TAYLOR16
 #define GRAPE_DENSE_TAYLOR16 1
 #endif
+#ifndef GRAPE_DENSE_TAYLOR_U
+#define GRAPE_DENSE_TAYLOR_U 1
+#endif
 __device__ __forceinline__ int taylor_degree(double nA) {
+    if (GRAPE_DENSE_TAYLOR_U) {
+        if (nA <= 0.069) return 8;
+        if (nA <= 0.335) return 12;
+        if (nA <= 0.826) return 16;
+        return 20;
+    }
     if (GRAPE_DENSE_TAYLOR16 && nA <= 0.047) return 8;
     if (nA <= 0.25) return 12;
     if (GRAPE_DENSE_TAYLOR16 && nA <= 0.668) return 16;
@@ -804,7 +817,7 @@ __device__ __forceinline__ void wg_expm_taylor(const HM &A, int degree, HM &X, d
         __syncthreads();
         sm_store(S0, A4, ln);  // the Horner left operand from here on
         if (degree == 18) taylor_block(X, 16, 3, A, A2, A3, nullptr, ln);  // c16..c18
-        else taylor_block(X, degree - 4, 5, A, A2, A3, &A4, ln);           // c_{m-4}..c_m, m = 8, 12, 16
+        else taylor_block(X, degree - 4, 5, A, A2, A3, &A4, ln);           // c_{m-4}..c_m, m = 8 .. 20
         hm_pin(X);
     }
     const int top = degree == 18 ? 3 : degree / 4 - 2;  // blocks B_top .. B_0 below the initial one

@@ -85,7 +85,7 @@ def test_dense_expm_matches_oracle_every_pade_degree(d):
     from oracle import grape_oracle as O
     from robustgrape_amd import _capi
     rng = np.random.default_rng(1000 + d)
-    norms = (0.01, 0.04, 0.2, 0.6, 0.8, 1.5, 4.0, 30.0)  # Taylor 8 / 8 / 12 / 16 / 18, Pade 9, 13, 13
+    norms = (0.01, 0.04, 0.2, 0.6, 0.8, 0.9, 1.5, 4.0, 30.0)  # Taylor 8 / 8 / 12 / 16 / 16 / 20, Pade 9, 13, 13
     A = np.stack([_skew_hermitian(d, nm, rng) for nm in norms])
     refs, ms = [], []
     for a in A:
